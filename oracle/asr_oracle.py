@@ -1,0 +1,407 @@
+"""CPU restatement of the ESPnet2 ASR training step — the ORACLE.
+
+TEST INFRASTRUCTURE ONLY.  Only tests/, __graft_entry__.smoke() and bench.py's
+cpu_baseline leg may import this module, and only as the checker / CPU baseline.  The
+product package (espnet-1_amd/espnet_amd) never imports it.
+
+Pinned against golden vectors captured from the reference itself
+(oracle/make_goldens.py -> tests/golden/*.npz; tests/test_oracle_goldens.py).
+
+This is a functional restatement over a flat {state_dict name -> tensor} map (the same
+key layout as the reference), written in plain PyTorch-CPU fp32 so that
+autograd supplies the backward.  Each function cites the reference lines it restates.
+"""
+from __future__ import annotations
+
+import math
+from typing import Dict, Optional
+
+import torch
+import torch.nn.functional as F
+
+Tensor = torch.Tensor
+
+
+# ---------------------------------------------------------------------------- helpers
+def pad_mask(lens: Tensor, maxlen: Optional[int] = None) -> Tensor:
+    """True at padded positions — espnet/nets/pytorch_backend/nets_utils.py:64-181."""
+    maxlen = int(lens.max()) if maxlen is None else maxlen
+    return torch.arange(maxlen)[None, :] >= lens[:, None]
+
+
+def layer_norm(P, name, x):
+    """LayerNorm(eps=1e-12) — transformer/layer_norm.py:12-42."""
+    return F.layer_norm(x, (x.shape[-1],), P[name + ".weight"], P[name + ".bias"], 1e-12)
+
+
+def linear(P, name, x, bias=True):
+    return F.linear(x, P[name + ".weight"], P.get(name + ".bias") if bias else None)
+
+
+def drop(x, p, training):
+    return F.dropout(x, p, training) if (training and p > 0) else x
+
+
+def swish(x):
+    """conformer/swish.py:16-18"""
+    return x * torch.sigmoid(x)
+
+
+def sinusoid_table(n, d):
+    """PositionalEncoding.extend_pe, embedding.py:60-79 (non-reversed)."""
+    pe = torch.zeros(n, d)
+    pos = torch.arange(0, n, dtype=torch.float32).unsqueeze(1)
+    div = torch.exp(torch.arange(0, d, 2, dtype=torch.float32) * -(math.log(10000.0) / d))
+    pe[:, 0::2] = torch.sin(pos * div)
+    pe[:, 1::2] = torch.cos(pos * div)
+    return pe
+
+
+def rel_pos_table(n, d):
+    """RelPositionalEncoding.extend_pe, embedding.py:282-313: rows are relative positions
+    n-1 ... 0 ... -(n-1)."""
+    pos = torch.arange(0, n, dtype=torch.float32).unsqueeze(1)
+    div = torch.exp(torch.arange(0, d, 2, dtype=torch.float32) * -(math.log(10000.0) / d))
+    pp = torch.zeros(n, d)
+    pn = torch.zeros(n, d)
+    pp[:, 0::2] = torch.sin(pos * div)
+    pp[:, 1::2] = torch.cos(pos * div)
+    pn[:, 0::2] = torch.sin(-1 * pos * div)
+    pn[:, 1::2] = torch.cos(-1 * pos * div)
+    return torch.cat([torch.flip(pp, [0]), pn[1:]], 0)
+
+
+# ---------------------------------------------------------------------------- attention
+def mha_core(q, k, v, scores_extra, mask, p_drop, training, d_k):
+    """forward_attention, attention.py:63-93 (masked softmax, masked_fill 0, dropout, AV).
+    q,k,v: (B,h,T,dk); mask (B,1|T1,T2) True=keep."""
+    scores = torch.matmul(q, k.transpose(-2, -1))
+    if scores_extra is not None:
+        scores = scores + scores_extra
+    scores = scores / math.sqrt(d_k)
+    m = mask.unsqueeze(1).eq(0)
+    scores = scores.masked_fill(m, torch.finfo(scores.dtype).min)
+    attn = torch.softmax(scores, dim=-1).masked_fill(m, 0.0)
+    return torch.matmul(drop(attn, p_drop, training), v)
+
+
+def split_heads(x, h):
+    B, T, d = x.shape
+    return x.view(B, T, h, d // h).transpose(1, 2)
+
+
+def merge_heads(x):
+    B, h, T, dk = x.shape
+    return x.transpose(1, 2).contiguous().view(B, T, h * dk)
+
+
+def rel_mha(P, name, x, pos_emb, mask, h, p_drop, training):
+    """RelPositionMultiHeadedAttention.forward, attention.py:262-305.
+    The rel_shift (attention.py:237-260) is restated as the index law
+    BD[i, j] = BD_raw[i, T-1-i+j] (verified bit-exact in SURVEY.md §8)."""
+    B, T, d = x.shape
+    dk = d // h
+    q = linear(P, name + ".linear_q", x).view(B, T, h, dk)
+    k = split_heads(linear(P, name + ".linear_k", x), h)
+    v = split_heads(linear(P, name + ".linear_v", x), h)
+    p = linear(P, name + ".linear_pos", pos_emb, bias=False).view(1, -1, h, dk).transpose(1, 2)
+    qu = (q + P[name + ".pos_bias_u"]).transpose(1, 2)
+    qv = (q + P[name + ".pos_bias_v"]).transpose(1, 2)
+    bd_raw = torch.matmul(qv, p.transpose(-2, -1))  # (B,h,T,2T-1)
+    idx = (T - 1 - torch.arange(T)[:, None] + torch.arange(T)[None, :])  # (T,T)
+    bd = torch.gather(bd_raw, 3, idx.expand(B, h, T, T))
+    o = mha_core(qu, k, v, bd, mask, p_drop, training, dk)
+    return linear(P, name + ".linear_out", merge_heads(o))
+
+
+def std_mha(P, name, xq, xkv, mask, h, p_drop, training):
+    """MultiHeadedAttention.forward, attention.py:95-111."""
+    dk = xq.shape[-1] // h
+    q = split_heads(linear(P, name + ".linear_q", xq), h)
+    k = split_heads(linear(P, name + ".linear_k", xkv), h)
+    v = split_heads(linear(P, name + ".linear_v", xkv), h)
+    o = mha_core(q, k, v, None, mask, p_drop, training, dk)
+    return linear(P, name + ".linear_out", merge_heads(o))
+
+
+# ---------------------------------------------------------------------------- conformer
+def ffn(P, name, x, act, p_drop, training):
+    """PositionwiseFeedForward, positionwise_feed_forward.py:30-32."""
+    return linear(P, name + ".w_2", drop(act(linear(P, name + ".w_1", x)), p_drop, training))
+
+
+def conv_module(P, name, x, bufs, training, momentum=0.1):
+    """ConvolutionModule.forward, conformer/convolution.py:56-79.  BatchNorm1d in training
+    mode normalises with batch stats over ALL B*T positions (padding included) and
+    updates the running stats (unbiased var)."""
+    x = x.transpose(1, 2)
+    x = F.conv1d(x, P[name + ".pointwise_conv1.weight"], P[name + ".pointwise_conv1.bias"])
+    x = F.glu(x, dim=1)
+    K = P[name + ".depthwise_conv.weight"].shape[-1]
+    x = F.conv1d(x, P[name + ".depthwise_conv.weight"], P[name + ".depthwise_conv.bias"],
+                 padding=(K - 1) // 2, groups=x.shape[1])
+    nb = name + ".norm"
+    x = F.batch_norm(x, bufs[nb + ".running_mean"], bufs[nb + ".running_var"],
+                     P[nb + ".weight"], P[nb + ".bias"], training, momentum, 1e-5)
+    if training:
+        bufs[nb + ".num_batches_tracked"] += 1
+    x = swish(x)
+    x = F.conv1d(x, P[name + ".pointwise_conv2.weight"], P[name + ".pointwise_conv2.bias"])
+    return x.transpose(1, 2)
+
+
+def conformer_layer(P, name, x, pos_emb, mask, cfg, bufs, training):
+    """EncoderLayer.forward, conformer/encoder_layer.py:79-179 (normalize_before=True,
+    concat_after=False, stochastic_depth 0)."""
+    pd = cfg["dropout_rate"]
+    h = cfg["attention_heads"]
+    macaron = cfg.get("macaron_style", False)
+    ff_scale = 0.5 if macaron else 1.0
+    if macaron:
+        x = x + ff_scale * drop(ffn(P, name + ".feed_forward_macaron",
+                                    layer_norm(P, name + ".norm_ff_macaron", x), swish, pd,
+                                    training), pd, training)
+    xn = layer_norm(P, name + ".norm_mha", x)
+    if cfg.get("selfattention_layer_type", "rel_selfattn") == "rel_selfattn":
+        a = rel_mha(P, name + ".self_attn", xn, pos_emb, mask, h,
+                    cfg["attention_dropout_rate"], training)
+    else:
+        a = std_mha(P, name + ".self_attn", xn, xn, mask, h, cfg["attention_dropout_rate"], training)
+    x = x + drop(a, pd, training)
+    if cfg.get("use_cnn_module", True):
+        x = x + drop(conv_module(P, name + ".conv_module", layer_norm(P, name + ".norm_conv", x),
+                                 bufs, training), pd, training)
+    x = x + ff_scale * drop(ffn(P, name + ".feed_forward", layer_norm(P, name + ".norm_ff", x),
+                                swish, pd, training), pd, training)
+    if cfg.get("use_cnn_module", True):
+        x = layer_norm(P, name + ".norm_final", x)
+    return x
+
+
+def utterance_mvn(x, ilens):
+    """utterance_mvn(norm_means=True, norm_vars=False), layers/utterance_mvn.py:45-88."""
+    x = x.masked_fill(pad_mask(ilens, x.shape[1])[:, :, None], 0.0)
+    mean = x.sum(dim=1, keepdim=True) / ilens.to(x.dtype).view(-1, 1, 1)
+    return x - mean
+
+
+def conv2d_subsampling(P, name, x, cfg, training):
+    """Conv2dSubsampling.forward, transformer/subsampling.py:71-91 + RelPositionalEncoding
+    (embedding.py:315-331): returns (x*sqrt(d) dropped, pos_emb dropped)."""
+    d = cfg["output_size"]
+    x = x.unsqueeze(1)
+    x = F.relu(F.conv2d(x, P[name + ".conv.0.weight"], P[name + ".conv.0.bias"], stride=2))
+    x = F.relu(F.conv2d(x, P[name + ".conv.2.weight"], P[name + ".conv.2.bias"], stride=2))
+    b, c, t, f = x.shape
+    x = linear(P, name + ".out.0", x.transpose(1, 2).contiguous().view(b, t, c * f))
+    x = x * math.sqrt(d)
+    pdp = cfg["positional_dropout_rate"]
+    if cfg.get("pos_enc_layer_type", "rel_pos") == "rel_pos":
+        pe = rel_pos_table(max(5000, t), d)
+        c0 = pe.shape[0] // 2
+        pos = pe[c0 - t + 1: c0 + t].unsqueeze(0)
+        return drop(x, pdp, training), drop(pos, pdp, training)
+    x = x + sinusoid_table(t, d).unsqueeze(0)
+    return drop(x, pdp, training), None
+
+
+def subsample_lens(ilens, T):
+    """Output lengths of Conv2dSubsampling as the reference computes them: by slicing the
+    input mask twice, x_mask[:, :, :-2:2][:, :, :-2:2] (subsampling.py:91), then summing
+    (conformer_encoder.py:374).  NOT the conv formula: a short utterance in a long batch
+    keeps ceil(l/2) twice."""
+    m = ~pad_mask(ilens, T)
+    m = m[:, :-2:2][:, :-2:2]
+    return m.sum(1)
+
+
+def conformer_encoder(P, x, ilens, cfg, bufs, training):
+    """ConformerEncoder.forward, espnet2/asr/encoder/conformer_encoder.py:300-377."""
+    if x.shape[1] < 7:
+        raise ValueError("TooShortUttError: needs more than 7 frames")
+    T = x.shape[1]
+    x, pos = conv2d_subsampling(P, "encoder.embed", x, cfg, training)
+    Tp = x.shape[1]
+    olens = subsample_lens(ilens, T)
+    mask = (~pad_mask(olens, Tp))[:, None, :]
+    for i in range(cfg["num_blocks"]):
+        x = conformer_layer(P, f"encoder.encoders.{i}", x, pos, mask, cfg, bufs, training)
+    x = layer_norm(P, "encoder.after_norm", x)
+    return x, olens
+
+
+# ---------------------------------------------------------------------------- decoder
+def transformer_decoder(P, hs, hlens, ys_in, ys_in_lens, cfg, training):
+    """BaseTransformerDecoder.forward, espnet2/asr/decoder/transformer_decoder.py:92-145,
+    DecoderLayer.forward, transformer/decoder_layer.py:63-134."""
+    B, L = ys_in.shape
+    d = hs.shape[-1]
+    h = cfg["attention_heads"]
+    pd = cfg["dropout_rate"]
+    tgt_mask = (~pad_mask(ys_in_lens, L))[:, None, :] & torch.tril(torch.ones(L, L, dtype=torch.bool))[None]
+    mem_mask = (~pad_mask(hlens, hs.shape[1]))[:, None, :]
+    x = F.embedding(ys_in, P["decoder.embed.0.weight"])
+    x = x * math.sqrt(d) + sinusoid_table(L, d).unsqueeze(0)
+    x = drop(x, cfg["positional_dropout_rate"], training)
+    for i in range(cfg["num_blocks"]):
+        n = f"decoder.decoders.{i}"
+        y = layer_norm(P, n + ".norm1", x)
+        x = x + drop(std_mha(P, n + ".self_attn", y, y, tgt_mask, h,
+                             cfg["self_attention_dropout_rate"], training), pd, training)
+        y = layer_norm(P, n + ".norm2", x)
+        x = x + drop(std_mha(P, n + ".src_attn", y, hs, mem_mask, h,
+                             cfg["src_attention_dropout_rate"], training), pd, training)
+        y = layer_norm(P, n + ".norm3", x)
+        x = x + drop(ffn(P, n + ".feed_forward", y, F.relu, pd, training), pd, training)
+    x = layer_norm(P, "decoder.after_norm", x)
+    return linear(P, "decoder.output_layer", x)
+
+
+# ---------------------------------------------------------------------------- losses
+def ctc_loss(logits_btv, hlens, ys_pad, ys_lens):
+    """CTC.forward / loss_fn builtin, espnet2/asr/ctc.py:52-97:
+    log_softmax -> CTCLoss(reduction=none, zero_infinity=True, blank=0) -> sum / B."""
+    lp = logits_btv.transpose(0, 1).log_softmax(2)
+    tgt = torch.cat([ys_pad[i, :l] for i, l in enumerate(ys_lens.tolist())])
+    loss = F.ctc_loss(lp, tgt, hlens, ys_lens, blank=0, reduction="none", zero_infinity=True)
+    return loss.sum() / lp.shape[1]
+
+
+def label_smoothing_loss(x, target, smoothing, ignore_id=-1, normalize_length=False):
+    """LabelSmoothingLoss.forward, transformer/label_smoothing_loss.py:41-63."""
+    B = x.shape[0]
+    V = x.shape[-1]
+    x = x.reshape(-1, V)
+    t = target.reshape(-1)
+    ignore = t == ignore_id
+    total = len(t) - int(ignore.sum())
+    t0 = t.masked_fill(ignore, 0)
+    true = torch.full_like(x, smoothing / (V - 1)).detach()
+    true.scatter_(1, t0.unsqueeze(1), 1.0 - smoothing)
+    kl = F.kl_div(torch.log_softmax(x, 1), true, reduction="none")
+    return kl.masked_fill(ignore.unsqueeze(1), 0).sum() / (total if normalize_length else B)
+
+
+def accuracy(x, target, ignore_id=-1):
+    """th_accuracy, nets_utils.py:304-324."""
+    pred = x.argmax(-1)
+    m = target != ignore_id
+    return float((pred[m] == target[m]).sum()) / float(m.sum())
+
+
+def add_sos_eos(ys_pad, ys_lens, sos, eos, ignore_id=-1):
+    """add_sos_eos + pad_list, transformer/add_sos_eos.py:12-31."""
+    B, L = ys_pad.shape
+    ys_in = torch.full((B, L + 1), eos, dtype=torch.long)
+    ys_out = torch.full((B, L + 1), ignore_id, dtype=torch.long)
+    for b, l in enumerate(ys_lens.tolist()):
+        ys_in[b, 0] = sos
+        ys_in[b, 1:l + 1] = ys_pad[b, :l]
+        ys_out[b, :l] = ys_pad[b, :l]
+        ys_out[b, l] = eos
+    return ys_in, ys_out
+
+
+# ---------------------------------------------------------------------------- model
+class OracleASR:
+    """ESPnetASRModel.forward (espnet2/asr/espnet_model.py:188-338) with encoder=conformer,
+    decoder=transformer, normalize=utterance_mvn, frontend/specaug None."""
+
+    def __init__(self, cfg: dict, state: Dict[str, Tensor]):
+        self.cfg = cfg
+        self.V = cfg["vocab_size"]
+        self.ctc_weight = cfg["model_conf"].get("ctc_weight", 0.5)
+        self.lsm = cfg["model_conf"].get("lsm_weight", 0.0)
+        self.norm_len = cfg["model_conf"].get("length_normalized_loss", False)
+        self.sos = self.eos = self.V - 1
+        self.params = {}
+        self.bufs = {}
+        for k, v in state.items():
+            t = torch.as_tensor(v).clone()
+            if "running" in k or "num_batches" in k:
+                self.bufs[k] = t
+            elif self.ctc_weight == 1.0 and k.startswith("decoder."):
+                continue  # decoder dropped when ctc_weight == 1 (espnet_model.py:147-155)
+            else:
+                self.params[k] = t.float().requires_grad_(True)
+        self.training = True
+
+    def forward(self, speech, speech_lengths, text, text_lengths):
+        cfg = self.cfg
+        P = self.params
+        text = text.clone()
+        text = text[:, : int(text_lengths.max())]
+        speech = speech[:, : int(speech_lengths.max())]
+        feats = utterance_mvn(speech, speech_lengths)
+        enc, olens = conformer_encoder(P, feats, speech_lengths, cfg["encoder_conf"], self.bufs,
+                                       self.training)
+        stats = {}
+        loss_ctc = loss_att = acc = None
+        if self.ctc_weight != 0.0:
+            self.ctc_logits = linear(P, "ctc.ctc_lo", enc)
+            loss_ctc = ctc_loss(self.ctc_logits, olens, text, text_lengths)
+            stats["loss_ctc"] = loss_ctc.detach()
+        if self.ctc_weight != 1.0:
+            ys_in, ys_out = add_sos_eos(text, text_lengths, self.sos, self.eos)
+            dec = transformer_decoder(P, enc, olens, ys_in, text_lengths + 1, cfg["decoder_conf"],
+                                      self.training)
+            self.decoder_out = dec
+            loss_att = label_smoothing_loss(dec, ys_out, self.lsm, -1, self.norm_len)
+            acc = accuracy(dec.detach(), ys_out)
+            stats["loss_att"] = loss_att.detach()
+            stats["acc"] = torch.tensor(acc)
+        if self.ctc_weight == 0.0:
+            loss = loss_att
+        elif self.ctc_weight == 1.0:
+            loss = loss_ctc
+        else:
+            loss = self.ctc_weight * loss_ctc + (1 - self.ctc_weight) * loss_att
+        stats["loss"] = loss.detach()
+        self.encoder_out, self.encoder_out_lens = enc, olens
+        return loss, stats, torch.tensor([speech.shape[0]])
+
+    __call__ = forward
+
+    def parameters(self):
+        return list(self.params.values())
+
+
+# ---------------------------------------------------------------------------- trainer step
+def warmup_lr(base_lr, step_num, warmup_steps):
+    """WarmupLR.get_lr, espnet2/schedulers/warmup_lr.py:43-50 (step_num = last_epoch + 1)."""
+    return base_lr * warmup_steps ** 0.5 * min(step_num ** -0.5, step_num * warmup_steps ** -1.5)
+
+
+class OracleTrainer:
+    """Trainer.train_one_epoch step semantics (espnet2/train/trainer.py:604-701):
+    backward -> clip_grad_norm_(grad_clip, 2) -> skip if non-finite -> Adam.step ->
+    WarmupLR.step -> zero_grad."""
+
+    def __init__(self, model: OracleASR, lr, weight_decay, warmup_steps, grad_clip=5.0):
+        self.model = model
+        self.base_lr = lr
+        self.warmup = warmup_steps
+        self.grad_clip = grad_clip
+        self.step_num = 1
+        self.opt = torch.optim.Adam(model.parameters(), lr=warmup_lr(lr, 1, warmup_steps),
+                                    weight_decay=weight_decay)
+
+    def step(self, batch, world_size=1, all_reduce=None):
+        loss, stats, weight = self.model(**batch)
+        if all_reduce is not None:  # DDP weighting, trainer.py:604-619 + recursive_op.py
+            w = weight.to(loss.dtype)
+            loss = (loss * w).sum()
+            wsum = all_reduce(w.clone())
+            loss = loss / wsum * world_size
+        loss.backward()
+        if all_reduce is not None:
+            for p in self.model.parameters():
+                p.grad = all_reduce(p.grad) / world_size
+        gn = torch.nn.utils.clip_grad_norm_(self.model.parameters(), self.grad_clip, 2.0)
+        if torch.isfinite(gn):
+            self.opt.step()
+        self.step_num += 1
+        for g in self.opt.param_groups:
+            g["lr"] = warmup_lr(self.base_lr, self.step_num, self.warmup)
+        self.opt.zero_grad()
+        return loss.detach(), stats, gn

@@ -1,0 +1,418 @@
+"""Capture golden vectors by running the REFERENCE implementation (this container only).
+
+TEST INFRASTRUCTURE — never imported by the product package.
+
+The reference (DavidLBick/espnet-1 at /root/reference) is pure Python over PyTorch ATen
+(SURVEY.md §2, §8c).  It imports here with the import-only stubs in `oracle/shim/`
+(typeguard, humanfriendly, librosa, torch_complex, numba) and
+PYTHONDONTWRITEBYTECODE so nothing is written into the reference tree.  The ASRTask
+entry point itself does not import (hydra is absent), so models are built from the
+module classes exactly as `espnet2/tasks/asr.py:476-602` (build_model) does.
+
+Every fixture stores weights + inputs + outputs (+ grads) as float32/int64 arrays in a
+compressed .npz under tests/golden/.  The weights are stored, not regenerated, so the
+fixtures do not depend on torch's RNG stream.
+
+Run:  PYTHONDONTWRITEBYTECODE=1 python -B oracle/make_goldens.py
+"""
+from __future__ import annotations
+
+import json
+import os
+import sys
+
+sys.dont_write_bytecode = True
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(HERE)
+REF = os.environ.get("ESPNET_REFERENCE", "/root/reference")
+OUT = os.path.join(REPO, "tests", "golden")
+sys.path[:0] = [os.path.join(HERE, "shim"), REF]
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+torch.set_num_threads(4)
+
+
+# --------------------------------------------------------------------------------------
+# model builders (mirror espnet2/tasks/asr.py:476-602 for frontend=None, input_size=F)
+# --------------------------------------------------------------------------------------
+def token_list(V):
+    return ["<blank>", "<unk>"] + [f"t{i}" for i in range(V - 3)] + ["<sos/eos>"]
+
+
+def build_reference_model(cfg):
+    from espnet2.asr.ctc import CTC
+    from espnet2.asr.decoder.transformer_decoder import TransformerDecoder
+    from espnet2.asr.encoder.conformer_encoder import ConformerEncoder
+    from espnet2.asr.encoder.transformer_encoder import TransformerEncoder
+    from espnet2.asr.espnet_model import ESPnetASRModel
+    from espnet2.layers.utterance_mvn import UtteranceMVN
+
+    V = cfg["vocab_size"]
+    enc_cls = {"conformer": ConformerEncoder, "transformer": TransformerEncoder}[cfg["encoder"]]
+    encoder = enc_cls(input_size=cfg["input_size"], **cfg["encoder_conf"])
+    decoder = None
+    if cfg.get("decoder"):
+        decoder = TransformerDecoder(
+            vocab_size=V, encoder_output_size=encoder.output_size(), **cfg["decoder_conf"]
+        )
+    ctc = CTC(odim=V, encoder_output_size=encoder.output_size(), **cfg.get("ctc_conf", {}))
+    model = ESPnetASRModel(
+        vocab_size=V,
+        token_list=token_list(V),
+        frontend=None,
+        specaug=None,
+        normalize=UtteranceMVN(),
+        preencoder=None,
+        encoder=encoder,
+        postencoder=None,
+        decoder=decoder,
+        ctc=ctc,
+        joint_network=None,
+        **cfg["model_conf"],
+    )
+    return model
+
+
+def perturb_norms(model, gen):
+    """Make LayerNorm/BatchNorm affine params and BN running stats non-trivial so that
+    the goldens discriminate gamma/beta/statistics bugs (defaults are 1/0)."""
+    with torch.no_grad():
+        for name, p in model.named_parameters():
+            if "norm" in name:
+                p.add_(0.1 * torch.randn(p.shape, generator=gen))
+        for name, b in model.named_buffers():
+            if name.endswith("running_mean"):
+                b.copy_(0.1 * torch.randn(b.shape, generator=gen))
+            elif name.endswith("running_var"):
+                b.copy_(1.0 + 0.2 * torch.rand(b.shape, generator=gen))
+
+
+def make_batch(cfg, gen):
+    B = len(cfg["speech_lengths"])
+    T = max(cfg["speech_lengths"])
+    F = cfg["input_size"]
+    V = cfg["vocab_size"]
+    speech = torch.zeros(B, T, F)
+    for b, t in enumerate(cfg["speech_lengths"]):
+        speech[b, :t] = torch.randn(t, F, generator=gen)
+    L = max(cfg["text_lengths"])
+    text = torch.full((B, L), -1, dtype=torch.long)
+    for b, l in enumerate(cfg["text_lengths"]):
+        text[b, :l] = torch.randint(2, V - 1, (l,), generator=gen)
+    return dict(
+        speech=speech,
+        speech_lengths=torch.tensor(cfg["speech_lengths"], dtype=torch.long),
+        text=text,
+        text_lengths=torch.tensor(cfg["text_lengths"], dtype=torch.long),
+    )
+
+
+def np32(t):
+    t = t.detach().cpu()
+    if t.dtype in (torch.float64, torch.float16, torch.bfloat16):
+        t = t.float()
+    return t.numpy()
+
+
+# --------------------------------------------------------------------------------------
+# configs
+# --------------------------------------------------------------------------------------
+def conformer_conf(d, h, ff, nb, k=31, drop=0.0):
+    return dict(
+        output_size=d, attention_heads=h, linear_units=ff, num_blocks=nb,
+        dropout_rate=drop, positional_dropout_rate=drop, attention_dropout_rate=drop,
+        input_layer="conv2d", normalize_before=True, macaron_style=True,
+        rel_pos_type="latest", pos_enc_layer_type="rel_pos",
+        selfattention_layer_type="rel_selfattn", activation_type="swish",
+        use_cnn_module=True, cnn_module_kernel=k,
+    )
+
+
+def decoder_conf(h, ff, nb, drop=0.0):
+    return dict(
+        attention_heads=h, linear_units=ff, num_blocks=nb, dropout_rate=drop,
+        positional_dropout_rate=drop, self_attention_dropout_rate=drop,
+        src_attention_dropout_rate=drop,
+    )
+
+
+CONFIGS = {
+    # 2-block conformer + 2-block decoder, hybrid 0.3/0.7, lsm 0.1, ragged lengths
+    "tiny_hybrid": dict(
+        encoder="conformer", input_size=80, vocab_size=50,
+        encoder_conf=conformer_conf(64, 4, 128, 2, k=15),
+        decoder="transformer", decoder_conf=decoder_conf(4, 128, 2),
+        model_conf=dict(ctc_weight=0.3, lsm_weight=0.1, length_normalized_loss=False),
+        speech_lengths=[120, 97, 64, 33], text_lengths=[12, 9, 7, 3],
+    ),
+    # CTC-only (ctc_weight=1.0 -> decoder dropped), C2-style, kernel 31 > T'
+    "tiny_ctc": dict(
+        encoder="conformer", input_size=80, vocab_size=40,
+        encoder_conf=conformer_conf(64, 4, 256, 2, k=31),
+        decoder="transformer", decoder_conf=decoder_conf(4, 128, 1),
+        model_conf=dict(ctc_weight=1.0, lsm_weight=0.0, length_normalized_loss=False),
+        speech_lengths=[100, 100, 81], text_lengths=[10, 4, 8],
+    ),
+    # realistic widths (d=256, h=4, ff=1024, d_k=64), one block each, equal lengths
+    "medium_hybrid": dict(
+        encoder="conformer", input_size=80, vocab_size=300,
+        encoder_conf=conformer_conf(256, 4, 1024, 1, k=31),
+        decoder="transformer", decoder_conf=decoder_conf(4, 1024, 1),
+        model_conf=dict(ctc_weight=0.3, lsm_weight=0.1, length_normalized_loss=False),
+        speech_lengths=[200, 200], text_lengths=[15, 15],
+    ),
+}
+
+
+def capture_model(name, cfg, seed=0, light=False):
+    torch.manual_seed(seed)
+    model = build_reference_model(cfg)
+    gen = torch.Generator().manual_seed(1000 + seed)
+    perturb_norms(model, gen)
+    batch = make_batch(cfg, torch.Generator().manual_seed(1))
+    model.train()
+    sd0 = {k: v.clone() for k, v in model.state_dict().items()}
+
+    mids = {}
+    hooks = []
+
+    def keep(key):
+        def fn(mod, inp, out):
+            x = out
+            if isinstance(x, tuple):
+                x = x[0]
+            if isinstance(x, tuple):
+                mids[key + ".pos"] = np32(out[0][1])
+                x = x[0]
+            mids[key] = np32(x)
+
+        return fn
+
+    hooks.append(model.encoder.embed.register_forward_hook(keep("embed")))
+    for i, layer in enumerate(model.encoder.encoders):
+        hooks.append(layer.register_forward_hook(keep(f"enc{i}")))
+    enc_out = {}
+
+    def enc_hook(mod, inp, out):
+        enc_out["x"], enc_out["lens"] = out[0], out[1]
+
+    hooks.append(model.encoder.register_forward_hook(enc_hook))
+    dec_out = {}
+    if model.decoder is not None:
+        def dec_hook(mod, inp, out):
+            dec_out["x"] = out[0]
+
+        hooks.append(model.decoder.register_forward_hook(dec_hook))
+
+    inputs = {k: v.clone() for k, v in batch.items()}
+    loss, stats, weight = model(**batch)
+    loss.backward()
+    for h in hooks:
+        h.remove()
+
+    rec = {"cfg": np.array(json.dumps({k: v for k, v in cfg.items()}))}
+    for k, v in sd0.items():
+        rec["w." + k] = np32(v)
+    for k, v in inputs.items():
+        rec["in." + k] = v.numpy()
+    rec["out.loss"] = np32(loss)
+    for k, v in stats.items():
+        if v is not None:
+            rec["stat." + k] = np32(v)
+    rec["out.weight"] = weight.numpy()
+    rec["out.encoder_out"] = np32(enc_out["x"])
+    rec["out.encoder_out_lens"] = enc_out["lens"].numpy()
+    with torch.no_grad():
+        rec["out.ctc_argmax"] = model.ctc.argmax(enc_out["x"]).numpy()
+        rec["out.ctc_logits"] = np32(model.ctc.ctc_lo(enc_out["x"]))
+    if dec_out:
+        rec["out.decoder_out"] = np32(dec_out["x"])
+    for k, v in mids.items():
+        rec["mid." + k] = v
+    for k, p in model.named_parameters():
+        if p.grad is None:
+            continue
+        if light and p.numel() > 4096:
+            # keep the fixture small: norm, sum and a 256-element head of big grads
+            g = p.grad.detach().double()
+            rec["gn." + k] = np.array(g.norm().item())
+            rec["gs." + k] = np.array(g.sum().item())
+            rec["gh." + k] = np32(p.grad.reshape(-1)[:256])
+        else:
+            rec["g." + k] = np32(p.grad)
+    if light:
+        rec = {k: v for k, v in rec.items() if not k.startswith("mid.enc")}
+    for k, v in model.state_dict().items():
+        if "running" in k or "num_batches" in k:
+            rec["buf_after." + k] = np32(v)
+    path = os.path.join(OUT, f"{name}.npz")
+    np.savez_compressed(path, **rec)
+    print(f"{name}: loss={loss.item():.6f} stats={ {k: (float(v) if v is not None else None) for k, v in stats.items()} } -> {path} ({os.path.getsize(path)/1e6:.2f} MB)")
+
+
+def capture_train_steps(name="train2", cfg_name="tiny_hybrid", steps=2):
+    """Two Trainer steps (trainer.py:604-701 semantics, single process):
+    loss.backward -> clip_grad_norm_(5.0) -> Adam(lr, wd) step -> WarmupLR step -> zero_grad."""
+    from espnet2.schedulers.warmup_lr import WarmupLR
+
+    cfg = CONFIGS[cfg_name]
+    torch.manual_seed(0)
+    model = build_reference_model(cfg)
+    perturb_norms(model, torch.Generator().manual_seed(1000))
+    sd0 = {k: v.clone() for k, v in model.state_dict().items()}
+    opt = torch.optim.Adam(model.parameters(), lr=0.002, weight_decay=1e-6)
+    sched = WarmupLR(opt, warmup_steps=10)
+    model.train()
+    rec = {"cfg": np.array(json.dumps(dict(cfg_name=cfg_name, lr=0.002, weight_decay=1e-6,
+                                           warmup_steps=10, grad_clip=5.0, steps=steps)))}
+    for k, v in sd0.items():
+        rec["w." + k] = np32(v)
+    for s in range(steps):
+        batch = make_batch(cfg, torch.Generator().manual_seed(1 + s))
+        for k, v in batch.items():
+            rec[f"in{s}." + k] = v.clone().numpy()
+        loss, stats, weight = model(**batch)
+        loss.backward()
+        gn = torch.nn.utils.clip_grad_norm_(model.parameters(), max_norm=5.0, norm_type=2.0)
+        opt.step()
+        sched.step()
+        opt.zero_grad()
+        rec[f"out{s}.loss"] = np32(loss)
+        rec[f"out{s}.grad_norm"] = np32(gn)
+        rec[f"out{s}.lr_after"] = np.array(opt.param_groups[0]["lr"], dtype=np.float64)
+    for k, v in model.state_dict().items():
+        rec["w_after." + k] = np32(v)
+    path = os.path.join(OUT, f"{name}.npz")
+    np.savez_compressed(path, **rec)
+    print(f"{name}: -> {path} ({os.path.getsize(path)/1e6:.2f} MB)")
+
+
+def capture_ctc_op(name="ctc_op"):
+    """Raw CTC (espnet2/asr/ctc.py:52-63 builtin path) on random logits, incl. repeated
+    labels, a zero-length target and an infeasible target (zero_infinity=True -> 0)."""
+    g = torch.Generator().manual_seed(7)
+    T, B, V = 30, 5, 12
+    logits = torch.randn(T, B, V, generator=g) * 2.0
+    logits.requires_grad_(True)
+    ilens = torch.tensor([30, 25, 30, 8, 17])
+    olens = torch.tensor([6, 4, 0, 6, 9])  # utt3: 6 labels w/ repeats need >8 frames -> inf
+    ys = [
+        torch.tensor([3, 3, 5, 7, 7, 7]),
+        torch.tensor([1, 2, 3, 4]),
+        torch.tensor([], dtype=torch.long),
+        torch.tensor([2, 2, 2, 2, 2, 2]),
+        torch.tensor([4, 9, 4, 9, 4, 9, 11, 10, 1]),
+    ]
+    target = torch.cat(ys)
+    lp = logits.log_softmax(2)
+    ctc = torch.nn.CTCLoss(reduction="none", zero_infinity=True)
+    loss_utt = ctc(lp, target, ilens, olens)
+    loss = loss_utt.sum() / B
+    loss.backward()
+    rec = dict(logits=np32(logits), ilens=ilens.numpy(), olens=olens.numpy(),
+               target=target.numpy(), loss_utt=np32(loss_utt), loss=np32(loss),
+               grad_logits=np32(logits.grad))
+    path = os.path.join(OUT, f"{name}.npz")
+    np.savez_compressed(path, **rec)
+    print(f"{name}: loss_utt={loss_utt.tolist()} -> {path}")
+
+
+def capture_lsm_op(name="lsm_op"):
+    """LabelSmoothingLoss (transformer/label_smoothing_loss.py:41-63) + th_accuracy
+    (nets_utils.py:304-324) on random logits with ignore_id=-1 rows."""
+    from espnet.nets.pytorch_backend.nets_utils import th_accuracy
+    from espnet.nets.pytorch_backend.transformer.label_smoothing_loss import LabelSmoothingLoss
+
+    g = torch.Generator().manual_seed(11)
+    B, L, V = 3, 7, 23
+    x = torch.randn(B, L, V, generator=g) * 3.0
+    x.requires_grad_(True)
+    tgt = torch.randint(0, V, (B, L), generator=g)
+    tgt[0, 5:] = -1
+    tgt[2, 2:] = -1
+    rec = {}
+    for sm, norm in ((0.1, False), (0.0, False), (0.2, True)):
+        crit = LabelSmoothingLoss(V, -1, sm, normalize_length=norm)
+        if x.grad is not None:
+            x.grad = None
+        loss = crit(x, tgt)
+        loss.backward()
+        tag = f"s{sm}_n{int(norm)}"
+        rec[f"loss.{tag}"] = np32(loss)
+        rec[f"grad.{tag}"] = np32(x.grad)
+    rec["acc"] = np.array(th_accuracy(x.detach().view(-1, V), tgt, ignore_label=-1))
+    rec["x"] = np32(x)
+    rec["tgt"] = tgt.numpy()
+    path = os.path.join(OUT, f"{name}.npz")
+    np.savez_compressed(path, **rec)
+    print(f"{name}: -> {path}")
+
+
+def _ddp_worker(rank, world, init_file, cfg_name, out_path):
+    import torch.distributed as dist
+    from espnet2.torch_utils.recursive_op import recursive_average
+
+    dist.init_process_group("gloo", init_method=f"file://{init_file}", rank=rank, world_size=world)
+    cfg = CONFIGS[cfg_name]
+    torch.manual_seed(0)
+    model = build_reference_model(cfg)
+    perturb_norms(model, torch.Generator().manual_seed(1000))
+    ddp = torch.nn.parallel.DistributedDataParallel(model)
+    ddp.train()
+    full = make_batch(cfg, torch.Generator().manual_seed(1))
+    # abs_task.py:1566-1575: each rank takes batch[rank::world_size] of the global batch
+    batch = {k: v[rank::world] for k, v in full.items()}
+    # collate crops padding to the local max (collate_fn.py pads per minibatch)
+    tl = int(batch["speech_lengths"].max())
+    batch["speech"] = batch["speech"][:, :tl].contiguous()
+    loss, stats, weight = ddp(**batch)
+    stats = {k: v for k, v in stats.items() if v is not None}
+    # trainer.py:604-619
+    loss = (loss * weight.type(loss.dtype)).sum()
+    stats, weight = recursive_average(stats, weight, True)
+    loss /= weight
+    loss *= dist.get_world_size()
+    loss.backward()
+    if rank == 0:
+        rec = {"cfg": np.array(json.dumps(dict(cfg_name=cfg_name, world=world)))}
+        for k, v in full.items():
+            rec["in." + k] = v.numpy()
+        rec["out.loss_scaled"] = np32(loss)
+        rec["out.weight"] = weight.numpy()
+        for k, v in stats.items():
+            rec["stat." + k] = np32(v)
+        for k, p in model.named_parameters():
+            rec["g." + k] = np32(p.grad)
+        for k, v in model.state_dict().items():
+            if "running" in k or "num_batches" in k:
+                rec["buf_after." + k] = np32(v)
+        np.savez_compressed(out_path, **rec)
+    dist.destroy_process_group()
+
+
+def capture_ddp(name="ddp2", cfg_name="tiny_hybrid"):
+    import tempfile
+
+    import torch.multiprocessing as mp
+
+    init_file = tempfile.mktemp(prefix="ddp_init_")
+    out_path = os.path.join(OUT, f"{name}.npz")
+    mp.spawn(_ddp_worker, args=(2, init_file, cfg_name, out_path), nprocs=2, join=True)
+    print(f"{name}: -> {out_path}")
+
+
+if __name__ == "__main__":
+    os.makedirs(OUT, exist_ok=True)
+    which = sys.argv[1:] or ["models", "train", "ops", "ddp"]
+    if "models" in which:
+        for n, c in CONFIGS.items():
+            capture_model(n, c, light=n.startswith("medium"))
+    if "train" in which:
+        capture_train_steps()
+    if "ops" in which:
+        capture_ctc_op()
+        capture_lsm_op()
+    if "ddp" in which:
+        capture_ddp()
