@@ -1,0 +1,80 @@
+"""Build libespnet_amd.so (all HIP kernels, gfx950) in-tree.
+
+    python espnet-1_amd/build.py [-j N] [--force]
+
+Each csrc/*.hip is compiled to an object with hipcc --offload-arch=gfx950 (in parallel,
+skipped when up to date), then linked into espnet_amd/lib/libespnet_amd.so.  The .so is
+git-ignored but travels to the GPU box with the gpurun snapshot.
+"""
+from __future__ import annotations
+
+import argparse
+import concurrent.futures as cf
+import glob
+import os
+import subprocess
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+CSRC = os.path.join(HERE, "csrc")
+INCLUDE = os.path.join(os.path.dirname(HERE), "include")
+OBJ = os.path.join(HERE, "build", "obj")
+LIB = os.path.join(HERE, "espnet_amd", "lib", "libespnet_amd.so")
+ARCH = os.environ.get("ESPNET_AMD_ARCH", "gfx950")
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+CFLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-munsafe-fp-atomics",
+          "-Wno-pass-failed", f"-I{INCLUDE}"]
+
+
+def _deps(src):
+    return [src] + glob.glob(os.path.join(CSRC, "*.h")) + glob.glob(os.path.join(INCLUDE, "*.h"))
+
+
+def _stale(out, deps):
+    if not os.path.exists(out):
+        return True
+    t = os.path.getmtime(out)
+    return any(os.path.getmtime(d) > t for d in deps)
+
+
+def _compile(src, force):
+    obj = os.path.join(OBJ, os.path.basename(src) + ".o")
+    if not force and not _stale(obj, _deps(src)):
+        return obj, None
+    cmd = [HIPCC, *CFLAGS, "-c", src, "-o", obj]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        return obj, f"{' '.join(cmd)}\n{r.stdout}\n{r.stderr}"
+    return obj, None
+
+
+def build(jobs: int = 8, force: bool = False, verbose: bool = True) -> str:
+    os.makedirs(OBJ, exist_ok=True)
+    os.makedirs(os.path.dirname(LIB), exist_ok=True)
+    srcs = sorted(glob.glob(os.path.join(CSRC, "*.hip")))
+    with cf.ThreadPoolExecutor(max_workers=jobs) as ex:
+        results = list(ex.map(lambda s: _compile(s, force), srcs))
+    errs = [e for _, e in results if e]
+    if errs:
+        raise RuntimeError("HIP compile failed:\n" + "\n".join(errs))
+    objs = [o for o, _ in results]
+    if force or _stale(LIB, objs):
+        cmd = [HIPCC, "-shared", f"--offload-arch={ARCH}", "-o", LIB, *objs]
+        r = subprocess.run(cmd, capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError(f"link failed:\n{r.stdout}\n{r.stderr}")
+        if verbose:
+            print(f"[espnet_amd] linked {LIB} ({len(objs)} objects)")
+    return LIB
+
+
+if __name__ == "__main__":
+    ap = argparse.ArgumentParser()
+    ap.add_argument("-j", type=int, default=min(8, os.cpu_count() or 8))
+    ap.add_argument("--force", action="store_true")
+    a = ap.parse_args()
+    try:
+        build(a.j, a.force)
+    except RuntimeError as e:
+        print(e, file=sys.stderr)
+        sys.exit(1)

@@ -1,0 +1,379 @@
+// MFMA GEMM for gfx950 with fused epilogues (see include/espnet_amd.h: ea_gemm).
+//
+// Tile 128x128, 256 threads = 4 wave64s in 2x2, each wave owns a 64x64 sub-tile
+// (4x4 MFMA 16x16 blocks).  K-tiles of 64 (bf16) / 32 (f32) are staged
+// global -> registers -> LDS (double buffered, one barrier per K-tile); the next
+// tile's global loads are issued before the current tile's MFMAs so HBM latency
+// hides under the math.
+//
+// LDS images keep the operand's global orientation:
+//  * K-contiguous operand  -> [mn][K-tile] rows of 128 B, 16-B chunk XOR-swizzled by
+//    (row>>1)&7; bf16 fragments are one ds_read_b128 (conflict-free for the
+//    ds_read_b128 lane groups), f32 fragments one ds_read_b32.
+//  * MN-contiguous operand -> [k][128] rows; bf16 fragments come from two
+//    ds_read_b64_tr_b16 (hardware transpose), chunk swizzle 2*((k&3)|((k>>3)&1)<<2) so
+//    the 8 rows of a 32-lane half land on 8 distinct 32-B bank windows.
+// So Linear forward (A K-major, W K-major), dX = dY.W (B N-major) and
+// dW = dY^T.X (A M-major, B N-major) all run without explicit transposes.
+#include "common.h"
+
+namespace {
+
+constexpr int BM = 128, BN = 128, NT = 256;
+constexpr int TILE_BYTES = 16384;
+
+template <typename T> struct KCfg;
+template <> struct KCfg<bf16> { static constexpr int KT = 64, KS = 32, E = 8, NKS = 2; };
+template <> struct KCfg<float> { static constexpr int KT = 32, KS = 4, E = 4, NKS = 8; };
+
+struct GemmP {
+  int M, N, K;
+  const void* A; long lda, sAb, sAh;
+  const void* B; long ldb, sBb, sBh;
+  int nh, splitk, kchunk;
+  void* C; int c_dtype; long ldc, sCb, sCh;
+  ea_epilogue epi;
+  float* ws;  // split-K partial slabs [z][s][M][N]
+  int tiles_m, tiles_n;
+};
+
+EA_DEV int swz_k(int row) { return (row >> 1) & 7; }                         // K-major rows
+EA_DEV int swz_mn_bf16(int k) { return 2 * ((k & 3) | (((k >> 3) & 1) << 2)); }  // [k][128] bf16
+EA_DEV int swz_mn_f32(int k) { return (k & 1) * 4; }                         // [k][128] f32
+
+// ---------------------------------------------------------------- global -> registers
+template <typename T, bool KMAJ>
+EA_DEV void load_tile(const T* __restrict__ base, long ld, int mn0, int MN, int k0, int K,
+                      uint4 (&v)[4]) {
+  constexpr int E = KCfg<T>::E;
+  constexpr int CPR = KMAJ ? 8 : (128 * (int)sizeof(T)) / 16;  // 16-B chunks per LDS row
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int c = threadIdx.x + NT * i;
+    const int row = c / CPR, ch = c % CPR;
+    int mn, k;
+    if (KMAJ) { mn = mn0 + row; k = k0 + ch * E; }
+    else      { k = k0 + row; mn = mn0 + ch * E; }
+    const T* p = KMAJ ? base + (long)mn * ld + k : base + (long)k * ld + mn;
+    const bool full = KMAJ ? (mn < MN && k + E <= K) : (k < K && mn + E <= MN);
+    if (full) {
+      v[i] = *(const uint4*)p;
+    } else {
+      union { uint4 u; T e[E]; } t;
+#pragma unroll
+      for (int e = 0; e < E; ++e) {
+        const bool ok = KMAJ ? (mn < MN && k + e < K) : (k < K && mn + e < MN);
+        t.e[e] = ok ? p[e] : (T)0.f;
+      }
+      v[i] = t.u;
+    }
+  }
+}
+
+template <typename T, bool KMAJ>
+EA_DEV void store_tile(char* lds, const uint4 (&v)[4]) {
+  constexpr int CPR = KMAJ ? 8 : (128 * (int)sizeof(T)) / 16;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int c = threadIdx.x + NT * i;
+    const int row = c / CPR, ch = c % CPR;
+    int off;
+    if (KMAJ) off = row * 128 + ((ch ^ swz_k(row)) << 4);
+    else if (sizeof(T) == 2) off = row * 256 + ((ch ^ swz_mn_bf16(row)) << 4);
+    else off = row * 512 + ((ch ^ swz_mn_f32(row)) << 4);
+    *(uint4*)(lds + off) = v[i];
+  }
+}
+
+// ---------------------------------------------------------------- LDS -> fragments
+// bf16: fragment = 8 consecutive k of row/col (lane&15), k-block 8*(lane>>4)
+template <bool KMAJ>
+EA_DEV bf16x8 frag_bf16(const char* lds, int r0, int ks, int lane) {
+  if (KMAJ) {
+    const int row = r0 + (lane & 15);
+    const int ch = ks * 4 + (lane >> 4);
+    return *(const bf16x8*)(lds + row * 128 + ((ch ^ swz_k(row)) << 4));
+  } else {
+    const int i = lane & 15, q = i >> 2, p = i & 3;
+    const int col = r0 + 4 * p;
+    const int ch = col >> 3, within = (col & 7) * 2;
+    union { bf16x8 v; s16x4 h[2]; } out;
+#pragma unroll
+    for (int half = 0; half < 2; ++half) {
+      const int row = ks * 32 + 8 * (lane >> 4) + 4 * half + q;
+      const char* a = lds + row * 256 + ((ch ^ swz_mn_bf16(row)) << 4) + within;
+      out.h[half] = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+          (__attribute__((address_space(3))) s16x4*)(uintptr_t)(a));
+    }
+    return out.v;
+  }
+}
+// f32: fragment = element (row/col lane&15, k = ks*4 + lane>>4)
+template <bool KMAJ>
+EA_DEV float frag_f32(const char* lds, int r0, int ks, int lane) {
+  if (KMAJ) {
+    const int row = r0 + (lane & 15);
+    return *(const float*)(lds + row * 128 + ((ks ^ swz_k(row)) << 4) + (lane >> 4) * 4);
+  } else {
+    const int k = ks * 4 + (lane >> 4);
+    const int col = r0 + (lane & 15);
+    return *(const float*)(lds + k * 512 + (((col >> 2) ^ swz_mn_f32(k)) << 4) + (col & 3) * 4);
+  }
+}
+
+// ---------------------------------------------------------------- epilogue
+template <int KIND>
+EA_DEV void epi_one(const GemmP& p, int z, int zb, int zh, int row, int col, float acc) {
+  const ea_epilogue& e = p.epi;
+  const long cidx = zb * p.sCb + zh * p.sCh + (long)row * p.ldc + col;
+  const uint64_t didx = ((uint64_t)z * p.M + row) * (uint64_t)p.N + col;
+  float v = e.alpha * acc;
+  if constexpr (KIND == EA_EPI_STORE) {
+    if (e.bias) v += e.bias[col];
+    v *= e.post_scale;
+    if (e.drop_p > 0.f) v *= drop_scale(e.seed, didx, e.drop_p);
+    if (e.beta != 0.f) v += e.beta * load_as_f(p.C, cidx, p.c_dtype);
+    store_from_f(p.C, cidx, p.c_dtype, v);
+  } else if constexpr (KIND == EA_EPI_ACT) {
+    if (e.bias) v += e.bias[col];
+    store_from_f(e.aux, (long)row * e.ldaux + col, e.aux_dtype, v);
+    float a = act_fwd(e.act, v);
+    if (e.drop_p > 0.f) a *= drop_scale(e.seed, didx, e.drop_p);
+    store_from_f(p.C, cidx, p.c_dtype, a);
+  } else if constexpr (KIND == EA_EPI_RESID) {
+    if (e.bias) v += e.bias[col];
+    if (e.drop_p > 0.f) v *= drop_scale(e.seed, didx, e.drop_p);
+    const float r = e.resid ? e.resid[(long)row * e.ldr + col] : 0.f;
+    ((float*)p.C)[cidx] = r + e.rscale * v;
+  } else {  // EA_EPI_DACT
+    if (e.drop_p > 0.f) v *= drop_scale(e.seed, didx, e.drop_p);
+    v *= act_bwd(e.act, load_as_f(e.aux, (long)row * e.ldaux + col, e.aux_dtype));
+    store_from_f(p.C, cidx, p.c_dtype, v);
+  }
+}
+
+EA_DEV void epi_apply(const GemmP& p, int z, int zb, int zh, int row, int col, float acc) {
+  switch (p.epi.kind) {
+    case EA_EPI_STORE: epi_one<EA_EPI_STORE>(p, z, zb, zh, row, col, acc); break;
+    case EA_EPI_ACT: epi_one<EA_EPI_ACT>(p, z, zb, zh, row, col, acc); break;
+    case EA_EPI_RESID: epi_one<EA_EPI_RESID>(p, z, zb, zh, row, col, acc); break;
+    default: epi_one<EA_EPI_DACT>(p, z, zb, zh, row, col, acc); break;
+  }
+}
+
+template <int KIND>
+EA_DEV void epi_tile(const GemmP& p, int z, int zb, int zh, int r0, int c0, int lane,
+                     const f32x4 (&acc)[4][4]) {
+  const int rq = (lane >> 4) * 4, cc = lane & 15;
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr) {
+        const int row = r0 + i * 16 + rq + rr, col = c0 + j * 16 + cc;
+        if (row < p.M && col < p.N) epi_one<KIND>(p, z, zb, zh, row, col, acc[i][j][rr]);
+      }
+}
+
+// ---------------------------------------------------------------- kernel
+template <typename T, bool AK, bool BKM>
+__global__ __launch_bounds__(NT, 2) void gemm_kernel(GemmP p) {
+  constexpr int KT = KCfg<T>::KT, NKS = KCfg<T>::NKS;
+  __shared__ __attribute__((aligned(16))) char smem[2][2][TILE_BYTES];
+
+  // XCD-aware tile order: blocks b, b+8, ... share an XCD; give each XCD a contiguous
+  // run of tiles (bijective remap), then walk tiles in column-groups of 8 row-tiles
+  // so neighbouring tiles on one XCD share A rows / B columns in its L2.
+  const int nt = p.tiles_m * p.tiles_n;
+  const int b = blockIdx.x;
+  const int q = nt / 8, r = nt % 8, xcd = b % 8;
+  const int t = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + b / 8;
+  const int GM = 8;
+  const int grp = t / (GM * p.tiles_n);
+  const int gm0 = grp * GM;
+  const int gsz = min(GM, p.tiles_m - gm0);
+  const int tm = gm0 + (t % (GM * p.tiles_n)) % gsz;
+  const int tn = (t % (GM * p.tiles_n)) / gsz;
+  const int m0 = tm * BM, n0 = tn * BN;
+
+  const int z = blockIdx.z / p.splitk, s = blockIdx.z % p.splitk;
+  const int zb = z / p.nh, zh = z % p.nh;
+  const T* A = (const T*)p.A + zb * p.sAb + zh * p.sAh;
+  const T* B = (const T*)p.B + zb * p.sBb + zh * p.sBh;
+  const int kbeg = s * p.kchunk;
+  const int kend = min(p.K, kbeg + p.kchunk);
+  const int nkt = (kend - kbeg + KT - 1) / KT;
+
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int wm = (w >> 1) * 64, wn = (w & 1) * 64;
+
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+  uint4 ra[4], rb[4];
+  if (nkt > 0) {
+    load_tile<T, AK>(A, p.lda, m0, p.M, kbeg, kend, ra);
+    load_tile<T, BKM>(B, p.ldb, n0, p.N, kbeg, kend, rb);
+    store_tile<T, AK>(smem[0][0], ra);
+    store_tile<T, BKM>(smem[0][1], rb);
+  }
+  __syncthreads();
+
+  for (int kt = 0; kt < nkt; ++kt) {
+    const int cur = kt & 1;
+    const bool more = kt + 1 < nkt;
+    if (more) {
+      load_tile<T, AK>(A, p.lda, m0, p.M, kbeg + (kt + 1) * KT, kend, ra);
+      load_tile<T, BKM>(B, p.ldb, n0, p.N, kbeg + (kt + 1) * KT, kend, rb);
+    }
+    const char* la = smem[cur][0];
+    const char* lb = smem[cur][1];
+#pragma unroll
+    for (int ks = 0; ks < NKS; ++ks) {
+      if constexpr (sizeof(T) == 2) {
+        bf16x8 fa[4], fb[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) fa[i] = frag_bf16<AK>(la, wm + i * 16, ks, lane);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) fb[j] = frag_bf16<BKM>(lb, wn + j * 16, ks, lane);
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+      } else {
+        float fa[4], fb[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) fa[i] = frag_f32<AK>(la, wm + i * 16, ks, lane);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) fb[j] = frag_f32<BKM>(lb, wn + j * 16, ks, lane);
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(fa[i], fb[j], acc[i][j], 0, 0, 0);
+      }
+    }
+    if (more) {
+      store_tile<T, AK>(smem[cur ^ 1][0], ra);
+      store_tile<T, BKM>(smem[cur ^ 1][1], rb);
+    }
+    __syncthreads();
+  }
+
+  // epilogue: C/D map of 16x16 MFMA: col = lane&15, row = 4*(lane>>4) + reg
+  const int rq = (lane >> 4) * 4, cc = lane & 15;
+  if (p.splitk > 1) {
+    float* slab = p.ws + ((long)z * p.splitk + s) * (long)p.M * p.N;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int rr = 0; rr < 4; ++rr) {
+          const int row = m0 + wm + i * 16 + rq + rr, col = n0 + wn + j * 16 + cc;
+          if (row < p.M && col < p.N) slab[(long)row * p.N + col] = acc[i][j][rr];
+        }
+    return;
+  }
+  switch (p.epi.kind) {
+    case EA_EPI_STORE: epi_tile<EA_EPI_STORE>(p, z, zb, zh, m0 + wm, n0 + wn, lane, acc); break;
+    case EA_EPI_ACT: epi_tile<EA_EPI_ACT>(p, z, zb, zh, m0 + wm, n0 + wn, lane, acc); break;
+    case EA_EPI_RESID: epi_tile<EA_EPI_RESID>(p, z, zb, zh, m0 + wm, n0 + wn, lane, acc); break;
+    default: epi_tile<EA_EPI_DACT>(p, z, zb, zh, m0 + wm, n0 + wn, lane, acc); break;
+  }
+}
+
+// split-K combine: C = epi(sum_s slab[s]) for EA_EPI_STORE
+__global__ void splitk_reduce(GemmP p) {
+  const long MN = (long)p.M * p.N;
+  const int z = blockIdx.y;
+  const int zb = z / p.nh, zh = z % p.nh;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < MN; i += (long)gridDim.x * blockDim.x) {
+    const float* slab = p.ws + (long)z * p.splitk * MN + i;
+    float a = 0.f;
+    for (int s = 0; s < p.splitk; ++s) a += slab[s * MN];
+    const int row = (int)(i / p.N), col = (int)(i % p.N);
+    epi_apply(p, z, zb, zh, row, col, a);
+  }
+}
+
+template <typename T>
+int launch(GemmP& p, int a_k, int b_k, int nz, hipStream_t st) {
+  dim3 grid(p.tiles_m * p.tiles_n, 1, nz * p.splitk);
+#define EA_GEMM_CASE(AKV, BKV)                                                      \
+  if (a_k == AKV && b_k == BKV) {                                                   \
+    hipLaunchKernelGGL((gemm_kernel<T, AKV, BKV>), grid, dim3(NT), 0, st, p);       \
+  }
+  EA_GEMM_CASE(true, true)
+  else EA_GEMM_CASE(true, false)
+  else EA_GEMM_CASE(false, true)
+  else EA_GEMM_CASE(false, false)
+#undef EA_GEMM_CASE
+  EA_LAUNCH_CHECK();
+  return 0;
+}
+
+}  // namespace
+
+extern "C" int ea_gemm(int dtype, int a_kmajor, int b_kmajor, int M, int N, int K,
+                       const void* A, long lda, long sAb, long sAh,
+                       const void* B, long ldb, long sBb, long sBh,
+                       int batch, int nh,
+                       void* C, int c_dtype, long ldc, long sCb, long sCh,
+                       const ea_epilogue* epi, float* workspace, long ws_elems, void* stream) {
+  EA_CHECK_ARG(epi != nullptr && M >= 0 && N >= 0 && K >= 0 && batch >= 1 && nh >= 1);
+  EA_CHECK_ARG(dtype == EA_F32 || dtype == EA_BF16);
+  if (M == 0 || N == 0) return 0;
+  const int E = dtype == EA_BF16 ? 8 : 4;
+  const int esz = dtype == EA_BF16 ? 2 : 4;
+  EA_CHECK_ARG(lda % E == 0 && ldb % E == 0 && sAb % E == 0 && sAh % E == 0 &&
+               sBb % E == 0 && sBh % E == 0);
+  EA_CHECK_ARG(((uintptr_t)A % 16) == 0 && ((uintptr_t)B % 16) == 0);
+  (void)esz;
+  if (epi->kind == EA_EPI_RESID) EA_CHECK_ARG(c_dtype == EA_F32);
+  GemmP p;
+  p.M = M; p.N = N; p.K = K;
+  p.A = A; p.lda = lda; p.sAb = sAb; p.sAh = sAh;
+  p.B = B; p.ldb = ldb; p.sBb = sBb; p.sBh = sBh;
+  p.nh = nh;
+  p.C = C; p.c_dtype = c_dtype; p.ldc = ldc; p.sCb = sCb; p.sCh = sCh;
+  p.epi = *epi;
+  p.ws = workspace;
+  p.tiles_m = ea_cdiv(M, BM);
+  p.tiles_n = ea_cdiv(N, BN);
+  const int KT = dtype == EA_BF16 ? KCfg<bf16>::KT : KCfg<float>::KT;
+  const int nz = batch * nh;
+  // split-K when the output grid cannot fill the 256 CUs and K is long (dW GEMMs)
+  int splitk = 1;
+  const long tiles = (long)p.tiles_m * p.tiles_n * nz;
+  if (workspace && epi->kind == EA_EPI_STORE && tiles < 256 && K >= 4 * KT) {
+    splitk = (int)((512 + tiles - 1) / tiles);
+    splitk = min(splitk, K / (2 * KT));
+    splitk = min(splitk, 32);
+    while (splitk > 1 && (long)splitk * nz * M * N > ws_elems) --splitk;
+    if (splitk < 1) splitk = 1;
+  }
+  int kchunk = K;
+  if (splitk > 1) {
+    kchunk = ea_cdiv(ea_cdiv(K, splitk), KT) * KT;
+    splitk = ea_cdiv(K, kchunk);
+  }
+  p.splitk = splitk;
+  p.kchunk = kchunk;
+  hipStream_t st = (hipStream_t)stream;
+  int rc = dtype == EA_BF16 ? launch<bf16>(p, a_kmajor, b_kmajor, nz, st)
+                            : launch<float>(p, a_kmajor, b_kmajor, nz, st);
+  if (rc) return rc;
+  if (splitk > 1) {
+    const long MN = (long)M * N;
+    dim3 grid(ea_grid_cap(ea_cdiv(MN, 256), 1024), nz);
+    hipLaunchKernelGGL(splitk_reduce, grid, dim3(256), 0, st, p);
+    EA_LAUNCH_CHECK();
+  }
+  return 0;
+}

@@ -1,0 +1,132 @@
+"""Tensor-level launchers for the HIP kernels in libespnet_amd.so.
+
+Torch tensors are used only as device-memory handles (data_ptr / shape / stride) and for
+the current HIP stream; every computation is one of the library's kernels.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import torch
+
+from ._lib import (ACT_NONE, BF16, EPI_ACT, EPI_DACT, EPI_RESID, EPI_STORE, F32, Epilogue,
+                   HipError, lib)
+
+__all__ = ["dt", "stream", "gemm", "linear", "linear_dx", "linear_dw", "workspace"]
+
+_DT = {torch.float32: F32, torch.bfloat16: BF16}
+
+
+def dt(t: torch.Tensor) -> int:
+    try:
+        return _DT[t.dtype]
+    except KeyError:
+        raise HipError(f"unsupported dtype {t.dtype}") from None
+
+
+def stream() -> int:
+    return torch.cuda.current_stream().cuda_stream
+
+
+def ptr(t):
+    return None if t is None else t.data_ptr()
+
+
+_WS = {}
+
+
+def workspace(numel: int, device) -> torch.Tensor:
+    """Persistent f32 scratch (split-K slabs, partial sums); grows monotonically."""
+    key = (str(device), "f32")
+    ws = _WS.get(key)
+    if ws is None or ws.numel() < numel:
+        ws = torch.empty(max(numel, 1 << 20), dtype=torch.float32, device=device)
+        _WS[key] = ws
+    return ws
+
+
+_SPLITK_WS = 1 << 25  # 32M floats
+
+
+def make_epi(kind=EPI_STORE, *, alpha=1.0, beta=0.0, bias=None, post_scale=1.0, act=ACT_NONE,
+             aux=None, resid=None, rscale=1.0, drop_p=0.0, seed=0):
+    e = Epilogue()
+    e.kind = kind
+    e.act = act
+    e.alpha = alpha
+    e.beta = beta
+    e.post_scale = post_scale
+    e.rscale = rscale
+    e.drop_p = drop_p
+    e.seed = seed & 0xFFFFFFFFFFFFFFFF
+    e.bias = ptr(bias)
+    if aux is not None:
+        e.aux = aux.data_ptr()
+        e.aux_dtype = dt(aux)
+        e.ldaux = aux.stride(-2)
+    if resid is not None:
+        e.resid = resid.data_ptr()
+        e.ldr = resid.stride(-2)
+    return e
+
+
+def gemm(A, B, C, *, M, N, K, a_kmajor, b_kmajor, lda, ldb, ldc,
+         batch=1, nh=1, sA=(0, 0), sB=(0, 0), sC=(0, 0), epi: Epilogue = None, splitk=True):
+    """Raw batched GEMM (see include/espnet_amd.h: ea_gemm)."""
+    if A.dtype != B.dtype:
+        raise HipError(f"gemm operand dtypes differ: {A.dtype} vs {B.dtype}")
+    if epi is None:
+        epi = make_epi()
+    ws = workspace(_SPLITK_WS, A.device) if splitk else None
+    lib.ea_gemm(dt(A), int(a_kmajor), int(b_kmajor), M, N, K,
+                A.data_ptr(), lda, sA[0], sA[1],
+                B.data_ptr(), ldb, sB[0], sB[1],
+                batch, nh,
+                C.data_ptr(), dt(C), ldc, sC[0], sC[1],
+                ctypes.byref(epi), ptr(ws), 0 if ws is None else ws.numel(), stream())
+    return C
+
+
+def _rows(x):
+    """(…, K) tensor with unit inner stride -> (rows, K, ld)."""
+    if x.stride(-1) != 1:
+        raise HipError("inner dimension must be contiguous")
+    K = x.shape[-1]
+    rows = x.numel() // K if K else 0
+    ld = x.stride(-2) if x.dim() >= 2 else K
+    if x.dim() > 2:
+        # leading dims must collapse onto a single row stride
+        exp = ld
+        for d in range(x.dim() - 2, 0, -1):
+            exp *= x.shape[d]
+            if x.shape[d - 1] > 1 and x.stride(d - 1) != exp:
+                raise HipError("leading dims do not collapse onto one row stride")
+    return rows, K, ld
+
+
+def linear(x, w, out, *, epi: Epilogue = None):
+    """out[r, n] = epi(sum_k x[r, k] * w[n, k]) — torch.nn.Linear forward."""
+    M, K, lda = _rows(x)
+    N = w.shape[0]
+    _, _, ldc = _rows(out)
+    return gemm(x, w, out, M=M, N=N, K=K, a_kmajor=1, b_kmajor=1, lda=lda, ldb=w.stride(0),
+                ldc=ldc, epi=epi)
+
+
+def linear_dx(dy, w, out, *, epi: Epilogue = None):
+    """out[r, k] = epi(sum_n dy[r, n] * w[n, k]) — Linear input gradient."""
+    M, N, lda = _rows(dy)
+    K = w.shape[1]
+    _, _, ldc = _rows(out)
+    return gemm(dy, w, out, M=M, N=K, K=N, a_kmajor=1, b_kmajor=0, lda=lda, ldb=w.stride(0),
+                ldc=ldc, epi=epi)
+
+
+def linear_dw(dy, x, dw, *, accumulate=False):
+    """dw[n, k] (+)= sum_r dy[r, n] * x[r, k] — Linear weight gradient (f32 out)."""
+    R, N, lddy = _rows(dy)
+    R2, K, ldx = _rows(x)
+    if R != R2:
+        raise HipError("row mismatch in linear_dw")
+    return gemm(dy, x, dw, M=N, N=K, K=R, a_kmajor=0, b_kmajor=0, lda=lddy, ldb=ldx,
+                ldc=dw.stride(0), epi=make_epi(beta=1.0 if accumulate else 0.0))

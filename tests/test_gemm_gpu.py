@@ -1,0 +1,153 @@
+"""ea_gemm (MFMA GEMM + epilogues) vs a plain PyTorch fp64 reference of the same op."""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _ops():
+    from espnet_amd import hip_ops
+    from espnet_amd import _lib
+    return hip_ops, _lib
+
+
+def ref_mm(A, B, a_k, b_k, M, N, K):
+    a = A.double().cpu()
+    b = B.double().cpu()
+    a = a[:M, :K] if a_k else a[:K, :M].t()
+    b = b[:N, :K].t() if b_k else b[:K, :N]
+    return a @ b
+
+
+def mk(shape, dtype, gen, scale=1.0):
+    return (torch.randn(shape, generator=gen) * scale).to(dtype).cuda()
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("a_k,b_k", [(1, 1), (1, 0), (0, 1), (0, 0)])
+@pytest.mark.parametrize("MNK", [(128, 128, 64), (100, 72, 40), (257, 130, 300), (33, 260, 129)])
+def test_gemm_layouts(dtype, a_k, b_k, MNK):
+    ops, L = _ops()
+    M, N, K = MNK
+    g = torch.Generator().manual_seed(M * 7 + N + K)
+    up = lambda n: (n + 7) // 8 * 8 + 8  # leading dims must be 16-B multiples
+    A = mk((M, up(K)) if a_k else (K, up(M)), dtype, g)
+    B = mk((N, up(K)) if b_k else (K, up(N)), dtype, g)
+    C = torch.full((M, N + 3), 7.0, device="cuda")
+    ops.gemm(A, B, C, M=M, N=N, K=K, a_kmajor=a_k, b_kmajor=b_k, lda=A.stride(0),
+             ldb=B.stride(0), ldc=C.stride(0))
+    ref = ref_mm(A, B, a_k, b_k, M, N, K)
+    tol = 1e-5 if dtype == torch.float32 else 2e-3
+    torch.testing.assert_close(C[:, :N].double().cpu(), ref, atol=tol * K ** 0.5, rtol=tol)
+    assert (C[:, N:] == 7.0).all(), "wrote outside ldc columns"
+
+
+def test_gemm_identity_asymmetric():
+    ops, L = _ops()
+    n = 64
+    A = torch.eye(n, device="cuda")
+    B = torch.arange(n * n, dtype=torch.float32, device="cuda").view(n, n) / 100.0
+    C = torch.zeros(n, n, device="cuda")
+    ops.gemm(A, B, C, M=n, N=n, K=n, a_kmajor=1, b_kmajor=0, lda=n, ldb=n, ldc=n)
+    torch.testing.assert_close(C, B, atol=0, rtol=0)
+    ops.gemm(A, B, C, M=n, N=n, K=n, a_kmajor=1, b_kmajor=1, lda=n, ldb=n, ldc=n)
+    torch.testing.assert_close(C, B.t(), atol=0, rtol=0)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_gemm_epilogues(dtype):
+    ops, L = _ops()
+    g = torch.Generator().manual_seed(3)
+    M, N, K = 200, 96, 80
+    x = mk((M, K), dtype, g)
+    w = mk((N, K), dtype, g, 0.2)
+    bias = mk((N,), torch.float32, g)
+    ref = (x.double().cpu() @ w.double().cpu().t()) + bias.double().cpu()
+    tol = dict(atol=1e-4, rtol=1e-4) if dtype == torch.float32 else dict(atol=3e-2, rtol=2e-2)
+    # STORE with bias + post_scale, f32 out
+    C = torch.empty(M, N, device="cuda")
+    ops.linear(x, w, C, epi=ops.make_epi(bias=bias, post_scale=2.0))
+    torch.testing.assert_close(C.double().cpu(), ref * 2.0, **tol)
+    # ACT swish: aux = pre-activation, C = swish(h)
+    aux = torch.empty(M, N, device="cuda", dtype=dtype)
+    Ca = torch.empty(M, N, device="cuda", dtype=dtype)
+    ops.linear(x, w, Ca, epi=ops.make_epi(L.EPI_ACT, bias=bias, act=L.ACT_SWISH, aux=aux))
+    torch.testing.assert_close(aux.double().cpu(), ref, **tol)
+    torch.testing.assert_close(Ca.double().cpu(), ref * torch.sigmoid(ref), **tol)
+    # RESID: C = resid + 0.5 * v   (in place)
+    R = torch.randn(M, N, generator=g).cuda()
+    R0 = R.clone()
+    ops.linear(x, w, R, epi=ops.make_epi(L.EPI_RESID, bias=bias, resid=R, rscale=0.5))
+    torch.testing.assert_close(R.double().cpu(), R0.double().cpu() + 0.5 * ref, **tol)
+    # DACT: dh = (dy . w^T...) * swish'(aux)
+    Cd = torch.empty(M, N, device="cuda")
+    ops.linear(x, w, Cd, epi=ops.make_epi(L.EPI_DACT, act=L.ACT_SWISH, aux=aux))
+    h = aux.double().cpu()
+    s = torch.sigmoid(h)
+    torch.testing.assert_close(Cd.double().cpu(), (ref - bias.double().cpu()) * s * (1 + h * (1 - s)), **tol)
+    # beta accumulate
+    Cb = torch.ones(M, N, device="cuda")
+    ops.linear(x, w, Cb, epi=ops.make_epi(beta=1.0))
+    torch.testing.assert_close(Cb.double().cpu(), ref - bias.double().cpu() + 1.0, **tol)
+
+
+def test_gemm_dropout_mask_consistency():
+    ops, L = _ops()
+    g = torch.Generator().manual_seed(5)
+    M, N, K = 256, 256, 64
+    x = mk((M, K), torch.float32, g)
+    w = mk((N, K), torch.float32, g)
+    aux = torch.empty(M, N, device="cuda")
+    y = torch.empty(M, N, device="cuda")
+    p = 0.25
+    ops.linear(x, w, y, epi=ops.make_epi(L.EPI_ACT, act=L.ACT_NONE, aux=aux, drop_p=p, seed=1234))
+    kept = (y != 0)
+    frac = kept.float().mean().item()
+    assert abs(frac - (1 - p)) < 0.01, frac
+    torch.testing.assert_close(y[kept], aux[kept] / (1 - p))
+    # backward regenerates the same mask
+    d = torch.empty(M, N, device="cuda")
+    ops.linear(x, w, d, epi=ops.make_epi(L.EPI_DACT, act=L.ACT_NONE, aux=aux, drop_p=p, seed=1234))
+    assert torch.equal(d != 0, kept)
+    # different seed -> different mask
+    y2 = torch.empty(M, N, device="cuda")
+    ops.linear(x, w, y2, epi=ops.make_epi(L.EPI_ACT, aux=aux, drop_p=p, seed=99))
+    assert not torch.equal(y2 != 0, kept)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_gemm_batched_heads(dtype):
+    """scores[b,h] = q[b,:,h,:] . k[b,:,h,:]^T with (B,T,H,dk) layouts (attention)."""
+    ops, L = _ops()
+    g = torch.Generator().manual_seed(9)
+    Bn, T, H, dk = 3, 37, 4, 64
+    q = mk((Bn, T, 3 * H * dk), dtype, g)  # fused qkv rows
+    k = q[:, :, H * dk:2 * H * dk]
+    qq = q[:, :, :H * dk]
+    S = torch.zeros(Bn, H, T, 40, device="cuda")
+    ops.gemm(qq, k, S, M=T, N=T, K=dk, a_kmajor=1, b_kmajor=1, lda=3 * H * dk, ldb=3 * H * dk,
+             ldc=40, batch=Bn, nh=H, sA=(T * 3 * H * dk, dk), sB=(T * 3 * H * dk, dk),
+             sC=(H * T * 40, T * 40), epi=ops.make_epi(alpha=0.125))
+    qr = qq.double().cpu().view(Bn, T, H, dk).transpose(1, 2)
+    kr = k.double().cpu().reshape(Bn, T, H, dk).transpose(1, 2)
+    ref = qr @ kr.transpose(-1, -2) * 0.125
+    tol = dict(atol=1e-4, rtol=1e-4) if dtype == torch.float32 else dict(atol=5e-2, rtol=2e-2)
+    torch.testing.assert_close(S[..., :T].double().cpu(), ref, **tol)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_gemm_splitk_dw(dtype):
+    ops, L = _ops()
+    g = torch.Generator().manual_seed(4)
+    R, N, K = 3000, 96, 136
+    dy = mk((R, N), dtype, g)
+    x = mk((R, K), dtype, g)
+    dw = torch.ones(N, K, device="cuda")
+    ops.linear_dw(dy, x, dw, accumulate=True)
+    ref = dy.double().cpu().t() @ x.double().cpu() + 1.0
+    tol = dict(atol=2e-3, rtol=1e-4) if dtype == torch.float32 else dict(atol=0.3, rtol=2e-2)
+    torch.testing.assert_close(dw.double().cpu(), ref, **tol)
+    dx = torch.empty(R, K, device="cuda")
+    w = mk((N, K), dtype, g)
+    ops.linear_dx(dy, w, dx)
+    torch.testing.assert_close(dx.double().cpu(), dy.double().cpu() @ w.double().cpu(), **tol)
