@@ -120,5 +120,5 @@ EA_DEV double block_sum_d(double v, double* red) {
   return t;
 }
 
-static inline int ea_cdiv(long a, long b) { return (int)((a + b - 1) / b); }
+__host__ __device__ static inline int ea_cdiv(long a, long b) { return (int)((a + b - 1) / b); }
 static inline int ea_grid_cap(long blocks, int cap = 4096) { return (int)(blocks < cap ? (blocks > 0 ? blocks : 1) : cap); }

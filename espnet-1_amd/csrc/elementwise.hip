@@ -1,0 +1,546 @@
+// Memory-bound kernels of the ASR step: input prep (utterance MVN, subsampled lengths,
+// sos/eos), dropout/cast, weight repacking, GLU, q+pos_bias, embeddings, argmax.
+// All grid-stride, coalesced along the contiguous (channel) dimension.
+#include "common.h"
+
+namespace {
+
+// ---------------------------------------------------------------- input prep
+// utterance_mvn(norm_means=True, norm_vars=False), layers/utterance_mvn.py:45-88:
+// zero padded frames, subtract the mean over valid frames.  One block per (b, feature tile).
+__global__ void mvn_kernel(int B, int T, int F, const float* __restrict__ x, const long long* __restrict__ lens,
+                           float* __restrict__ y) {
+  const int b = blockIdx.x;
+  const int f = threadIdx.x;  // blockDim.x >= F
+  __shared__ double red[1024];
+  const long long L = lens[b];
+  double s = 0.0;
+  // each thread owns feature f; rows split across blockDim.y
+  const int ty = threadIdx.y, ny = blockDim.y;
+  if (f < F)
+    for (int t = ty; t < T; t += ny)
+      if (t < L) s += x[((long)b * T + t) * F + f];
+  red[ty * blockDim.x + f] = s;
+  __syncthreads();
+  if (ty == 0 && f < F) {
+    double a = 0.0;
+    for (int k = 0; k < ny; ++k) a += red[k * blockDim.x + f];
+    red[f] = a;
+  }
+  __syncthreads();
+  if (f >= F) return;
+  // the reference computes the mean in the input dtype: sum (f32) / len
+  const float mean = (float)red[f] / (float)L;
+  for (int t = ty; t < T; t += ny) {
+    const long i = ((long)b * T + t) * F + f;
+    y[i] = (t < L ? x[i] : 0.f) - mean;
+  }
+}
+
+// lengths after Conv2dSubsampling as the reference derives them from the sliced mask
+// x_mask[:, :, :-2:2][:, :, :-2:2] (subsampling.py:91): l -> ceil(min(l, T-2)/2) twice.
+__global__ void subsample_lens_kernel(int B, int T, const long long* __restrict__ ilens, long long* __restrict__ olens) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= B) return;
+  long long l = ilens[b];
+  const long long T1 = (T - 1) / 2;  // len(range(0, T-2, 2))
+  long long l1 = min(l, (long long)T - 2);
+  l1 = l1 > 0 ? (l1 + 1) / 2 : 0;
+  long long l2 = min(l1, T1 - 2);
+  l2 = l2 > 0 ? (l2 + 1) / 2 : 0;
+  olens[b] = l2;
+}
+
+// add_sos_eos + pad_list (transformer/add_sos_eos.py:12-31)
+__global__ void sos_eos_kernel(int B, int L, const long long* __restrict__ ys, long ldys, const long long* __restrict__ ylens,
+                               int sos, int eos, int ignore_id, long long* __restrict__ ys_in,
+                               long long* __restrict__ ys_out, long long* __restrict__ ys_in_lens) {
+  const int b = blockIdx.x;
+  const long long l = ylens[b];
+  for (int t = threadIdx.x; t <= L; t += blockDim.x) {
+    long long vin, vout;
+    if (t == 0) vin = sos;
+    else if (t <= l) vin = ys[(long)b * ldys + t - 1];
+    else vin = eos;
+    if (t < l) vout = ys[(long)b * ldys + t];
+    else if (t == l) vout = eos;
+    else vout = ignore_id;
+    ys_in[(long)b * (L + 1) + t] = vin;
+    ys_out[(long)b * (L + 1) + t] = vout;
+  }
+  if (threadIdx.x == 0) ys_in_lens[b] = l + 1;
+}
+
+// ---------------------------------------------------------------- dropout / cast / scale
+template <typename TI, typename TO>
+__global__ void scale_drop_kernel(long n, int cols, const TI* __restrict__ x, long ldx, TO* __restrict__ y, long ldy,
+                                  float scale, float p, uint64_t seed) {
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+    const long r = i / cols, c = i % cols;
+    float v = to_f(x[r * ldx + c]) * scale;
+    if (p > 0.f) v *= drop_scale(seed, (uint64_t)i, p);
+    y[r * ldy + c] = from_f<TO>(v);
+  }
+}
+
+// y[r,c] += alpha * x[r,c]
+template <typename TI, typename TO>
+__global__ void add2d_kernel(long n, int cols, const TI* __restrict__ x, long ldx, TO* __restrict__ y, long ldy, float alpha) {
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+    const long r = i / cols, c = i % cols;
+    TO* o = y + r * ldy + c;
+    *o = from_f<TO>(to_f(*o) + alpha * to_f(x[r * ldx + c]));
+  }
+}
+
+// dst[a][c][b] (+)= src[a][b][c]  (weight repack: conv (Co,Ci,9)<->(Co,9,Ci), linear (O,C,F)<->(O,F,C))
+template <typename TI, typename TO>
+__global__ void permute3_kernel(int A, int Bd, int Cd, const TI* __restrict__ src, TO* __restrict__ dst, int accumulate) {
+  const long n = (long)A * Bd * Cd;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+    const long a = i / ((long)Bd * Cd);
+    const long rem = i % ((long)Bd * Cd);
+    const long c = rem / Bd, b = rem % Bd;  // i indexes dst[a][c][b]
+    const float v = to_f(src[(a * Bd + b) * Cd + c]);
+    dst[i] = from_f<TO>(accumulate ? to_f(dst[i]) + v : v);
+  }
+}
+
+// ---------------------------------------------------------------- subsampling im2col
+// conv1 (1->C, k3 s2) as a GEMM: rows = (b, t1, f1), 16 columns (9 taps + zero pad)
+template <typename TO>
+__global__ void im2col_conv1_kernel(int B, int T, int F, int T1, int F1, const float* __restrict__ x, TO* __restrict__ col) {
+  const long n = (long)B * T1 * F1 * 16;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+    const int k = (int)(i & 15);
+    const long r = i >> 4;
+    const int f1 = (int)(r % F1);
+    const long bt = r / F1;
+    const int t1 = (int)(bt % T1), b = (int)(bt / T1);
+    float v = 0.f;
+    if (k < 9) {
+      const int kh = k / 3, kw = k % 3;
+      v = x[((long)b * T + 2 * t1 + kh) * F + 2 * f1 + kw];
+    }
+    col[i] = from_f<TO>(v);
+  }
+}
+
+// conv2 (C->C, k3 s2) im2col from NHWC x1 (B,T1,F1,C): row (b,t2,f2), column (kh,kw,c)
+template <typename T>
+__global__ void im2col_conv2_kernel(int B, int T1, int F1, int C, int T2, int F2, const T* __restrict__ x1, T* __restrict__ col) {
+  const int C8 = C / 8;
+  const long n = (long)B * T2 * F2 * 9 * C8;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+    const int c8 = (int)(i % C8);
+    long r = i / C8;
+    const int k = (int)(r % 9);
+    r /= 9;
+    const int f2 = (int)(r % F2);
+    const long bt = r / F2;
+    const int t2 = (int)(bt % T2), b = (int)(bt / T2);
+    const int kh = k / 3, kw = k % 3;
+    const T* src = x1 + (((long)b * T1 + 2 * t2 + kh) * F1 + 2 * f2 + kw) * C + c8 * 8;
+    T* dst = col + (r * 9 + k) * (long)C + c8 * 8;
+    if (sizeof(T) == 2) *(uint4*)dst = *(const uint4*)src;
+    else { *(uint4*)dst = *(const uint4*)src; *(uint4*)(dst + 4) = *(const uint4*)(src + 4); }
+  }
+}
+
+// col2im for conv2's input gradient, gather form: dx1[b,t1,f1,c] = relu'(x1) *
+//   sum over taps (kh,kw) with t1 = 2*t2+kh, f1 = 2*f2+kw of dcol[(b,t2,f2),(kh,kw,c)]
+template <typename TI, typename TO>
+__global__ void col2im_conv2_kernel(int B, int T1, int F1, int C, int T2, int F2, const TI* __restrict__ dcol,
+                                    const TO* __restrict__ x1, TO* __restrict__ dx1) {
+  const long n = (long)B * T1 * F1 * C;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+    const int c = (int)(i % C);
+    long r = i / C;
+    const int f1 = (int)(r % F1);
+    const long bt = r / F1;
+    const int t1 = (int)(bt % T1), b = (int)(bt / T1);
+    float acc = 0.f;
+    if (to_f(x1[i]) > 0.f) {
+#pragma unroll
+      for (int kh = 0; kh < 3; ++kh) {
+        const int tt = t1 - kh;
+        if (tt < 0 || (tt & 1) || (tt >> 1) >= T2) continue;
+#pragma unroll
+        for (int kw = 0; kw < 3; ++kw) {
+          const int ff = f1 - kw;
+          if (ff < 0 || (ff & 1) || (ff >> 1) >= F2) continue;
+          const long row = ((long)b * T2 + (tt >> 1)) * F2 + (ff >> 1);
+          acc += to_f(dcol[(row * 9 + kh * 3 + kw) * (long)C + c]);
+        }
+      }
+    }
+    dx1[i] = from_f<TO>(acc);
+  }
+}
+
+// ---------------------------------------------------------------- GLU (conv module)
+// out[r,c] = x[r,c] * sigmoid(x[r,c+C])   (nn.functional.glu(dim=channels))
+template <typename TI, typename TO>
+__global__ void glu_fwd_kernel(long rows, int C, const TI* __restrict__ x, TO* __restrict__ y) {
+  const long n = rows * C;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+    const long r = i / C;
+    const int c = (int)(i % C);
+    const float a = to_f(x[r * 2 * C + c]), g = to_f(x[r * 2 * C + C + c]);
+    y[i] = from_f<TO>(a * sigmoidf_(g));
+  }
+}
+template <typename TI, typename TO>
+__global__ void glu_bwd_kernel(long rows, int C, const TI* __restrict__ x, const float* __restrict__ dy, TO* __restrict__ dx) {
+  const long n = rows * C;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+    const long r = i / C;
+    const int c = (int)(i % C);
+    const float a = to_f(x[r * 2 * C + c]), g = to_f(x[r * 2 * C + C + c]);
+    const float s = sigmoidf_(g), d = dy[i];
+    dx[r * 2 * C + c] = from_f<TO>(d * s);
+    dx[r * 2 * C + C + c] = from_f<TO>(d * a * s * (1.f - s));
+  }
+}
+
+// ---------------------------------------------------------------- depthwise conv1d
+// y[b,t,c] = bias[c] + sum_k w[c,k] x[b, t+k-P, c] (zero padded per utterance)
+constexpr int DW_TT = 32;   // time rows per block
+constexpr int DW_CT = 64;   // channels per block
+__global__ __launch_bounds__(256) void dwconv_fwd_kernel(int B, int T, int C, int K, const float* __restrict__ x,
+                                                         const float* __restrict__ w, const float* __restrict__ bias,
+                                                         float* __restrict__ y) {
+  extern __shared__ float tile[];  // (DW_TT + K - 1) x DW_CT
+  const int P = (K - 1) / 2;
+  const int ntt = ea_cdiv(T, DW_TT);
+  const int b = blockIdx.x / ntt, t0 = (blockIdx.x % ntt) * DW_TT;
+  const int c0 = blockIdx.y * DW_CT;
+  const int rowsL = DW_TT + K - 1;
+  for (int i = threadIdx.x; i < rowsL * DW_CT; i += blockDim.x) {
+    const int rr = i / DW_CT, cc = i % DW_CT;
+    const int t = t0 + rr - P, c = c0 + cc;
+    tile[i] = (t >= 0 && t < T && c < C) ? x[((long)b * T + t) * C + c] : 0.f;
+  }
+  __syncthreads();
+  const int cc = threadIdx.x % DW_CT, tq = threadIdx.x / DW_CT;  // 4 time groups of 8
+  const int c = c0 + cc;
+  if (c >= C) return;
+  float acc[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) acc[j] = bias ? bias[c] : 0.f;
+  for (int k = 0; k < K; ++k) {
+    const float wk = w[c * K + k];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[j] += wk * tile[(tq * 8 + j + k) * DW_CT + cc];
+  }
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int t = t0 + tq * 8 + j;
+    if (t < T) y[((long)b * T + t) * C + c] = acc[j];
+  }
+}
+
+// dx[b,t,c] = sum_k w[c,k] dy[b, t-k+P, c];  part[blk][c*K+k] = sum_t dy[b,t,c] x[b,t+k-P,c]
+__global__ __launch_bounds__(256) void dwconv_bwd_kernel(int B, int T, int C, int K, const float* __restrict__ x,
+                                                         const float* __restrict__ w, const float* __restrict__ dy,
+                                                         float* __restrict__ dx, float* __restrict__ part) {
+  extern __shared__ float sm[];
+  const int P = (K - 1) / 2;
+  const int ntt = ea_cdiv(T, DW_TT);
+  const int b = blockIdx.x / ntt, t0 = (blockIdx.x % ntt) * DW_TT;
+  const int c0 = blockIdx.y * DW_CT;
+  const int rowsL = DW_TT + K - 1;
+  float* tdy = sm;                    // dy rows t0-(K-1-P) .. t0+DW_TT-1+P
+  float* tx = sm + rowsL * DW_CT;     // x rows  t0-P .. t0+DW_TT-1+(K-1-P)
+  float* tin = tx + rowsL * DW_CT;    // dy rows t0 .. t0+DW_TT-1 (for dw)
+  for (int i = threadIdx.x; i < rowsL * DW_CT; i += blockDim.x) {
+    const int rr = i / DW_CT, cc = i % DW_CT, c = c0 + cc;
+    const int td = t0 + rr - (K - 1 - P);
+    const int tx_ = t0 + rr - P;
+    tdy[i] = (td >= 0 && td < T && c < C) ? dy[((long)b * T + td) * C + c] : 0.f;
+    tx[i] = (tx_ >= 0 && tx_ < T && c < C) ? x[((long)b * T + tx_) * C + c] : 0.f;
+  }
+  for (int i = threadIdx.x; i < DW_TT * DW_CT; i += blockDim.x) {
+    const int rr = i / DW_CT, cc = i % DW_CT, c = c0 + cc, t = t0 + rr;
+    tin[i] = (t < T && c < C) ? dy[((long)b * T + t) * C + c] : 0.f;
+  }
+  __syncthreads();
+  const int cc = threadIdx.x % DW_CT, tq = threadIdx.x / DW_CT;
+  const int c = c0 + cc;
+  if (c < C) {
+    float acc[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[j] = 0.f;
+    // dx[t] = sum_k w[k] dy[t - k + P]; tdy row index for dy[t'] is t' - t0 + (K-1-P)
+    for (int k = 0; k < K; ++k) {
+      const float wk = w[c * K + k];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[j] += wk * tdy[(tq * 8 + j - k + (K - 1)) * DW_CT + cc];
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int t = t0 + tq * 8 + j;
+      if (t < T) dx[((long)b * T + t) * C + c] = acc[j];
+    }
+  }
+  // dw partials: 4 thread-groups split the K taps
+  const long blk = (long)blockIdx.x;
+  if (c < C) {
+    for (int k = tq; k < K; k += 4) {
+      float a = 0.f;
+      for (int r = 0; r < DW_TT; ++r) a += tin[r * DW_CT + cc] * tx[(r + k) * DW_CT + cc];
+      part[blk * (long)C * K + (long)c * K + k] = a;
+    }
+  }
+}
+
+// ---------------------------------------------------------------- attention helpers
+// qu = q + u[h], qv = q + v[h] for q rows of (N, H*dk) inside a fused qkv buffer
+template <typename T>
+__global__ void add_pos_bias_kernel(long N, int H, int dk, const T* __restrict__ q, long ldq, const float* __restrict__ u,
+                                    const float* __restrict__ v, T* __restrict__ qu, T* __restrict__ qv) {
+  const int d = H * dk;
+  const long n = N * d;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+    const long r = i / d;
+    const int c = (int)(i % d);
+    const float x = to_f(q[r * ldq + c]);
+    qu[i] = from_f<T>(x + u[c]);
+    qv[i] = from_f<T>(x + v[c]);
+  }
+}
+
+// ---------------------------------------------------------------- embeddings (decoder)
+// y[r] = dropout(E[tok[r]] * xscale + pe[pos(r)]), pos(r) = r % L
+__global__ void embed_fwd_kernel(long rows, int d, int L, const long long* __restrict__ tok, const float* __restrict__ E,
+                                 float xscale, const float* __restrict__ pe, float p, uint64_t seed, float* __restrict__ y) {
+  const long n = rows * d;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+    const long r = i / d;
+    const int c = (int)(i % d);
+    float v = E[tok[r] * d + c] * xscale + pe[(r % L) * d + c];
+    if (p > 0.f) v *= drop_scale(seed, (uint64_t)i, p);
+    y[i] = v;
+  }
+}
+// dE[tok[r]] += xscale * dropout_mask * dy[r]   (float atomics)
+__global__ void embed_bwd_kernel(long rows, int d, const long long* __restrict__ tok, const float* __restrict__ dy,
+                                 float xscale, float p, uint64_t seed, float* __restrict__ dE) {
+  const long n = rows * d;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+    const long r = i / d;
+    const int c = (int)(i % d);
+    float v = dy[i] * xscale;
+    if (p > 0.f) v *= drop_scale(seed, (uint64_t)i, p);
+    atomicAdd(&dE[tok[r] * d + c], v);
+  }
+}
+
+// ---------------------------------------------------------------- argmax rows (CTC align)
+__global__ void argmax_rows_kernel(long rows, int V, const float* __restrict__ x, long ld, long long* __restrict__ out) {
+  const int lane = threadIdx.x & 63;
+  const long r = blockIdx.x * (long)(blockDim.x >> 6) + (threadIdx.x >> 6);
+  if (r >= rows) return;
+  const float* xr = x + r * ld;
+  float best = -INFINITY;
+  int bi = 0x7fffffff;
+  for (int v = lane; v < V; v += 64) {
+    const float t = xr[v];
+    if (t > best || (t == best && v < bi) || (t != t && best == best)) { best = t; bi = v; }
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const float ob = __shfl_xor(best, o, 64);
+    const int oi = __shfl_xor(bi, o, 64);
+    if (ob > best || (ob == best && oi < bi)) { best = ob; bi = oi; }
+  }
+  if (lane == 0) out[r] = bi;
+}
+
+}  // namespace
+
+#define EA_GRID(n) dim3(ea_grid_cap(ea_cdiv((n), 256))), dim3(256), 0, (hipStream_t)stream
+
+extern "C" int ea_utterance_mvn(int B, int T, int F, const float* x, const long long* lens, float* y, void* stream) {
+  EA_CHECK_ARG(F <= 256 && F > 0);
+  const int bx = F <= 64 ? 64 : (F <= 128 ? 128 : 256);
+  const int by = 1024 / bx;
+  hipLaunchKernelGGL(mvn_kernel, dim3(B), dim3(bx, by), 0, (hipStream_t)stream, B, T, F, x, lens, y);
+  EA_LAUNCH_CHECK();
+  return 0;
+}
+
+extern "C" int ea_subsample_lens(int B, int T, const long long* ilens, long long* olens, void* stream) {
+  hipLaunchKernelGGL(subsample_lens_kernel, dim3(ea_cdiv(B, 64)), dim3(64), 0, (hipStream_t)stream, B, T, ilens, olens);
+  EA_LAUNCH_CHECK();
+  return 0;
+}
+
+extern "C" int ea_add_sos_eos(int B, int L, const long long* ys, long ldys, const long long* ylens, int sos, int eos,
+                              int ignore_id, long long* ys_in, long long* ys_out, long long* ys_in_lens, void* stream) {
+  hipLaunchKernelGGL(sos_eos_kernel, dim3(B), dim3(64), 0, (hipStream_t)stream, B, L, ys, ldys, ylens, sos, eos,
+                     ignore_id, ys_in, ys_out, ys_in_lens);
+  EA_LAUNCH_CHECK();
+  return 0;
+}
+
+extern "C" int ea_scale_dropout(long rows, int cols, const void* x, int x_dtype, long ldx, void* y, int y_dtype,
+                                long ldy, float scale, float p, unsigned long long seed, void* stream) {
+  const long n = rows * cols;
+  if (n == 0) return 0;
+#define EA_SD(TI, TO) hipLaunchKernelGGL((scale_drop_kernel<TI, TO>), EA_GRID(n), n, cols, (const TI*)x, ldx, (TO*)y, ldy, scale, p, (uint64_t)seed)
+  if (x_dtype == EA_BF16 && y_dtype == EA_BF16) EA_SD(bf16, bf16);
+  else if (x_dtype == EA_BF16) EA_SD(bf16, float);
+  else if (y_dtype == EA_BF16) EA_SD(float, bf16);
+  else EA_SD(float, float);
+#undef EA_SD
+  EA_LAUNCH_CHECK();
+  return 0;
+}
+
+extern "C" int ea_add_2d(long rows, int cols, const void* x, int x_dtype, long ldx, void* y, int y_dtype,
+                          long ldy, float alpha, void* stream) {
+  const long n = rows * cols;
+  if (n == 0) return 0;
+#define EA_A2(TI, TO) hipLaunchKernelGGL((add2d_kernel<TI, TO>), EA_GRID(n), n, cols, (const TI*)x, ldx, (TO*)y, ldy, alpha)
+  if (x_dtype == EA_BF16 && y_dtype == EA_BF16) EA_A2(bf16, bf16);
+  else if (x_dtype == EA_BF16) EA_A2(bf16, float);
+  else if (y_dtype == EA_BF16) EA_A2(float, bf16);
+  else EA_A2(float, float);
+#undef EA_A2
+  EA_LAUNCH_CHECK();
+  return 0;
+}
+
+extern "C" int ea_permute3(int A, int Bd, int Cd, const void* src, int src_dtype, void* dst, int dst_dtype,
+                           int accumulate, void* stream) {
+  const long n = (long)A * Bd * Cd;
+  if (n == 0) return 0;
+#define EA_P3(TI, TO) hipLaunchKernelGGL((permute3_kernel<TI, TO>), EA_GRID(n), A, Bd, Cd, (const TI*)src, (TO*)dst, accumulate)
+  if (src_dtype == EA_BF16 && dst_dtype == EA_BF16) EA_P3(bf16, bf16);
+  else if (src_dtype == EA_BF16) EA_P3(bf16, float);
+  else if (dst_dtype == EA_BF16) EA_P3(float, bf16);
+  else EA_P3(float, float);
+#undef EA_P3
+  EA_LAUNCH_CHECK();
+  return 0;
+}
+
+extern "C" int ea_im2col_conv1(int B, int T, int F, const float* x, void* col, int col_dtype, void* stream) {
+  const int T1 = (T - 3) / 2 + 1, F1 = (F - 3) / 2 + 1;
+  const long n = (long)B * T1 * F1 * 16;
+  if (col_dtype == EA_BF16)
+    hipLaunchKernelGGL(im2col_conv1_kernel<bf16>, EA_GRID(n), B, T, F, T1, F1, x, (bf16*)col);
+  else
+    hipLaunchKernelGGL(im2col_conv1_kernel<float>, EA_GRID(n), B, T, F, T1, F1, x, (float*)col);
+  EA_LAUNCH_CHECK();
+  return 0;
+}
+
+extern "C" int ea_im2col_conv2(int B, int T1, int F1, int C, const void* x1, void* col, int dtype, void* stream) {
+  EA_CHECK_ARG(C % 8 == 0);
+  const int T2 = (T1 - 3) / 2 + 1, F2 = (F1 - 3) / 2 + 1;
+  const long n = (long)B * T2 * F2 * 9 * (C / 8);
+  if (dtype == EA_BF16)
+    hipLaunchKernelGGL(im2col_conv2_kernel<bf16>, EA_GRID(n), B, T1, F1, C, T2, F2, (const bf16*)x1, (bf16*)col);
+  else
+    hipLaunchKernelGGL(im2col_conv2_kernel<float>, EA_GRID(n), B, T1, F1, C, T2, F2, (const float*)x1, (float*)col);
+  EA_LAUNCH_CHECK();
+  return 0;
+}
+
+extern "C" int ea_col2im_conv2(int B, int T1, int F1, int C, const void* dcol, int dcol_dtype, const void* x1,
+                               void* dx1, int dtype, void* stream) {
+  const int T2 = (T1 - 3) / 2 + 1, F2 = (F1 - 3) / 2 + 1;
+  const long n = (long)B * T1 * F1 * C;
+#define EA_C2I(TI, TO) hipLaunchKernelGGL((col2im_conv2_kernel<TI, TO>), EA_GRID(n), B, T1, F1, C, T2, F2, (const TI*)dcol, (const TO*)x1, (TO*)dx1)
+  if (dcol_dtype == EA_BF16 && dtype == EA_BF16) EA_C2I(bf16, bf16);
+  else if (dcol_dtype == EA_BF16) EA_C2I(bf16, float);
+  else if (dtype == EA_BF16) EA_C2I(float, bf16);
+  else EA_C2I(float, float);
+#undef EA_C2I
+  EA_LAUNCH_CHECK();
+  return 0;
+}
+
+extern "C" int ea_glu_fwd(long rows, int C, const void* x, int x_dtype, void* y, int y_dtype, void* stream) {
+  const long n = rows * C;
+#define EA_G(TI, TO) hipLaunchKernelGGL((glu_fwd_kernel<TI, TO>), EA_GRID(n), rows, C, (const TI*)x, (TO*)y)
+  if (x_dtype == EA_BF16 && y_dtype == EA_BF16) EA_G(bf16, bf16);
+  else if (x_dtype == EA_BF16) EA_G(bf16, float);
+  else if (y_dtype == EA_BF16) EA_G(float, bf16);
+  else EA_G(float, float);
+#undef EA_G
+  EA_LAUNCH_CHECK();
+  return 0;
+}
+
+extern "C" int ea_glu_bwd(long rows, int C, const void* x, int x_dtype, const float* dy, void* dx, void* stream) {
+  const long n = rows * C;
+  if (x_dtype == EA_BF16)
+    hipLaunchKernelGGL((glu_bwd_kernel<bf16, bf16>), EA_GRID(n), rows, C, (const bf16*)x, dy, (bf16*)dx);
+  else
+    hipLaunchKernelGGL((glu_bwd_kernel<float, float>), EA_GRID(n), rows, C, (const float*)x, dy, (float*)dx);
+  EA_LAUNCH_CHECK();
+  return 0;
+}
+
+extern "C" int ea_dwconv_fwd(int B, int T, int C, int K, const float* x, const float* w, const float* bias, float* y,
+                             void* stream) {
+  EA_CHECK_ARG(K % 2 == 1);
+  dim3 grid(B * ea_cdiv(T, DW_TT), ea_cdiv(C, DW_CT));
+  const size_t sm = (size_t)(DW_TT + K - 1) * DW_CT * sizeof(float);
+  hipLaunchKernelGGL(dwconv_fwd_kernel, grid, dim3(256), sm, (hipStream_t)stream, B, T, C, K, x, w, bias, y);
+  EA_LAUNCH_CHECK();
+  return 0;
+}
+
+extern "C" int ea_dwconv_bwd(int B, int T, int C, int K, const float* x, const float* w, const float* dy, float* dx,
+                             float* dw, float* dbias, int accumulate_params, float* workspace, long ws_elems,
+                             void* stream) {
+  EA_CHECK_ARG(K % 2 == 1);
+  const int nblk = B * ea_cdiv(T, DW_TT);
+  EA_CHECK_ARG((long)nblk * C * K <= ws_elems);
+  dim3 grid(nblk, ea_cdiv(C, DW_CT));
+  const size_t sm = (size_t)(2 * (DW_TT + K - 1) + DW_TT) * DW_CT * sizeof(float);
+  hipStream_t st = (hipStream_t)stream;
+  hipLaunchKernelGGL(dwconv_bwd_kernel, grid, dim3(256), sm, st, B, T, C, K, x, w, dy, dx, workspace);
+  EA_LAUNCH_CHECK();
+  int rc = ea_reduce_partials(nblk, C * K, workspace, (long)C * K, dw, accumulate_params, stream);
+  if (rc) return rc;
+  if (dbias) return ea_colsum(B * T, C, dy, EA_F32, C, dbias, accumulate_params, workspace, ws_elems, stream);
+  return 0;
+}
+
+extern "C" int ea_add_pos_bias(long N, int H, int dk, const void* q, long ldq, const float* u, const float* v,
+                               void* qu, void* qv, int dtype, void* stream) {
+  const long n = N * H * dk;
+  if (dtype == EA_BF16)
+    hipLaunchKernelGGL(add_pos_bias_kernel<bf16>, EA_GRID(n), N, H, dk, (const bf16*)q, ldq, u, v, (bf16*)qu, (bf16*)qv);
+  else
+    hipLaunchKernelGGL(add_pos_bias_kernel<float>, EA_GRID(n), N, H, dk, (const float*)q, ldq, u, v, (float*)qu, (float*)qv);
+  EA_LAUNCH_CHECK();
+  return 0;
+}
+
+extern "C" int ea_embed_fwd(long rows, int d, int L, const long long* tok, const float* E, float xscale,
+                            const float* pe, float p, unsigned long long seed, float* y, void* stream) {
+  const long n = rows * d;
+  hipLaunchKernelGGL(embed_fwd_kernel, EA_GRID(n), rows, d, L, tok, E, xscale, pe, p, (uint64_t)seed, y);
+  EA_LAUNCH_CHECK();
+  return 0;
+}
+
+extern "C" int ea_embed_bwd(long rows, int d, const long long* tok, const float* dy, float xscale, float p,
+                            unsigned long long seed, float* dE, void* stream) {
+  const long n = rows * d;
+  hipLaunchKernelGGL(embed_bwd_kernel, EA_GRID(n), rows, d, tok, dy, xscale, p, (uint64_t)seed, dE);
+  EA_LAUNCH_CHECK();
+  return 0;
+}
+
+extern "C" int ea_argmax_rows(long rows, int V, const float* x, long ld, long long* out, void* stream) {
+  hipLaunchKernelGGL(argmax_rows_kernel, dim3(ea_cdiv(rows, 4)), dim3(256), 0, (hipStream_t)stream, rows, V, x, ld, out);
+  EA_LAUNCH_CHECK();
+  return 0;
+}

@@ -35,6 +35,7 @@ struct GemmP {
   ea_epilogue epi;
   float* ws;  // split-K partial slabs [z][s][M][N]
   int tiles_m, tiles_n;
+  int vec_a, vec_b;  // 16-B vector loads allowed (aligned base, ld and batch strides)
 };
 
 EA_DEV int swz_k(int row) { return (row >> 1) & 7; }                         // K-major rows
@@ -44,7 +45,7 @@ EA_DEV int swz_mn_f32(int k) { return (k & 1) * 4; }                         // 
 // ---------------------------------------------------------------- global -> registers
 template <typename T, bool KMAJ>
 EA_DEV void load_tile(const T* __restrict__ base, long ld, int mn0, int MN, int k0, int K,
-                      uint4 (&v)[4]) {
+                      int vec, uint4 (&v)[4]) {
   constexpr int E = KCfg<T>::E;
   constexpr int CPR = KMAJ ? 8 : (128 * (int)sizeof(T)) / 16;  // 16-B chunks per LDS row
 #pragma unroll
@@ -55,7 +56,7 @@ EA_DEV void load_tile(const T* __restrict__ base, long ld, int mn0, int MN, int 
     if (KMAJ) { mn = mn0 + row; k = k0 + ch * E; }
     else      { k = k0 + row; mn = mn0 + ch * E; }
     const T* p = KMAJ ? base + (long)mn * ld + k : base + (long)k * ld + mn;
-    const bool full = KMAJ ? (mn < MN && k + E <= K) : (k < K && mn + E <= MN);
+    const bool full = vec && (KMAJ ? (mn < MN && k + E <= K) : (k < K && mn + E <= MN));
     if (full) {
       v[i] = *(const uint4*)p;
     } else {
@@ -136,7 +137,7 @@ EA_DEV void epi_one(const GemmP& p, int z, int zb, int zh, int row, int col, flo
     store_from_f(p.C, cidx, p.c_dtype, v);
   } else if constexpr (KIND == EA_EPI_ACT) {
     if (e.bias) v += e.bias[col];
-    store_from_f(e.aux, (long)row * e.ldaux + col, e.aux_dtype, v);
+    if (e.aux) store_from_f(e.aux, (long)row * e.ldaux + col, e.aux_dtype, v);
     float a = act_fwd(e.act, v);
     if (e.drop_p > 0.f) a *= drop_scale(e.seed, didx, e.drop_p);
     store_from_f(p.C, cidx, p.c_dtype, a);
@@ -216,8 +217,8 @@ __global__ __launch_bounds__(NT, 2) void gemm_kernel(GemmP p) {
 
   uint4 ra[4], rb[4];
   if (nkt > 0) {
-    load_tile<T, AK>(A, p.lda, m0, p.M, kbeg, kend, ra);
-    load_tile<T, BKM>(B, p.ldb, n0, p.N, kbeg, kend, rb);
+    load_tile<T, AK>(A, p.lda, m0, p.M, kbeg, kend, p.vec_a, ra);
+    load_tile<T, BKM>(B, p.ldb, n0, p.N, kbeg, kend, p.vec_b, rb);
     store_tile<T, AK>(smem[0][0], ra);
     store_tile<T, BKM>(smem[0][1], rb);
   }
@@ -227,8 +228,8 @@ __global__ __launch_bounds__(NT, 2) void gemm_kernel(GemmP p) {
     const int cur = kt & 1;
     const bool more = kt + 1 < nkt;
     if (more) {
-      load_tile<T, AK>(A, p.lda, m0, p.M, kbeg + (kt + 1) * KT, kend, ra);
-      load_tile<T, BKM>(B, p.ldb, n0, p.N, kbeg + (kt + 1) * KT, kend, rb);
+      load_tile<T, AK>(A, p.lda, m0, p.M, kbeg + (kt + 1) * KT, kend, p.vec_a, ra);
+      load_tile<T, BKM>(B, p.ldb, n0, p.N, kbeg + (kt + 1) * KT, kend, p.vec_b, rb);
     }
     const char* la = smem[cur][0];
     const char* lb = smem[cur][1];
@@ -331,9 +332,6 @@ extern "C" int ea_gemm(int dtype, int a_kmajor, int b_kmajor, int M, int N, int 
   if (M == 0 || N == 0) return 0;
   const int E = dtype == EA_BF16 ? 8 : 4;
   const int esz = dtype == EA_BF16 ? 2 : 4;
-  EA_CHECK_ARG(lda % E == 0 && ldb % E == 0 && sAb % E == 0 && sAh % E == 0 &&
-               sBb % E == 0 && sBh % E == 0);
-  EA_CHECK_ARG(((uintptr_t)A % 16) == 0 && ((uintptr_t)B % 16) == 0);
   (void)esz;
   if (epi->kind == EA_EPI_RESID) EA_CHECK_ARG(c_dtype == EA_F32);
   GemmP p;
@@ -346,6 +344,9 @@ extern "C" int ea_gemm(int dtype, int a_kmajor, int b_kmajor, int M, int N, int 
   p.ws = workspace;
   p.tiles_m = ea_cdiv(M, BM);
   p.tiles_n = ea_cdiv(N, BN);
+  // unaligned operands (odd vocab / leading dims) take the element-wise load path
+  p.vec_a = (lda % E == 0 && sAb % E == 0 && sAh % E == 0 && ((uintptr_t)A % 16) == 0);
+  p.vec_b = (ldb % E == 0 && sBb % E == 0 && sBh % E == 0 && ((uintptr_t)B % 16) == 0);
   const int KT = dtype == EA_BF16 ? KCfg<bf16>::KT : KCfg<float>::KT;
   const int nz = batch * nh;
   // split-K when the output grid cannot fill the 256 CUs and K is long (dW GEMMs)

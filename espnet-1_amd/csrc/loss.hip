@@ -1,0 +1,317 @@
+// Losses of the hybrid CTC/attention objective (espnet2/asr/espnet_model.py:320-325):
+//  * CTC (espnet2/asr/ctc.py:52-97, builtin = torch CTCLoss(reduction=none,
+//    zero_infinity=True, blank=0) on log_softmax, then sum / B): row log-sum-exp,
+//    alpha/beta lattice in log space (fp64, one workgroup per utterance, states across
+//    threads, the previous time step in LDS), and a fused gradient w.r.t. the logits
+//    (softmax - occupancy), i.e. CTCLoss backward composed with log_softmax backward.
+//  * LabelSmoothingLoss (transformer/label_smoothing_loss.py:41-63: KLDiv(reduction=none)
+//    vs the smoothed target, ignore_id rows zeroed, sum / (B or #tokens)) fused with
+//    th_accuracy (nets_utils.py:304-324) and its gradient.
+#include "common.h"
+
+namespace {
+
+// ---------------------------------------------------------------- row log-sum-exp
+__global__ __launch_bounds__(256) void lse_rows_kernel(long rows, int V, const float* __restrict__ x, long ld,
+                                                       float* __restrict__ lse) {
+  const int lane = threadIdx.x & 63;
+  const long r = blockIdx.x * 4L + (threadIdx.x >> 6);
+  if (r >= rows) return;
+  const float* xr = x + r * ld;
+  float mx = -INFINITY;
+  for (int v = lane; v < V; v += 64) mx = fmaxf(mx, xr[v]);
+  mx = wave_max(mx);
+  double s = 0.0;
+  for (int v = lane; v < V; v += 64) s += (double)__expf(xr[v] - mx);
+  s = wave_sum_d(s);
+  if (lane == 0) lse[r] = mx + (float)log(s);
+}
+
+EA_DEV double lae(double a, double b) {  // log(exp a + exp b)
+  if (a == -INFINITY) return b;
+  if (b == -INFINITY) return a;
+  const double m = fmax(a, b);
+  return m + log(exp(a - m) + exp(b - m));
+}
+
+struct CtcP {
+  int B, T, V, Lmax, Smax;
+  const float* logits; long ldt;     // row (b,t) at (b*T + t)*ldt
+  const float* lse;                  // [B*T]
+  const long long* hlens;            // [B]
+  const long long* ys; long ldys;    // [B][ldys]
+  const long long* ylens;
+  double* alpha; double* beta;       // [B][T][Smax]
+  double* nll;                       // [B]
+  float* loss_utt;                   // [B]  (0 for infeasible, zero_infinity)
+};
+
+EA_DEV int ctc_label(const CtcP& p, int b, int s) {
+  return (s & 1) ? (int)p.ys[(long)b * p.ldys + (s >> 1)] : 0;
+}
+EA_DEV double ctc_lp(const CtcP& p, int b, int t, int lab) {
+  const long row = (long)b * p.T + t;
+  return (double)p.logits[row * p.ldt + lab] - (double)p.lse[row];
+}
+
+__global__ __launch_bounds__(256) void ctc_lattice_kernel(CtcP p) {
+  extern __shared__ double sh[];  // 2 x Smax
+  const int b = blockIdx.x;
+  const int Tb = (int)min((long long)p.T, p.hlens[b]);
+  const int L = (int)p.ylens[b];
+  const int S = 2 * L + 1;
+  double* prev = sh;
+  double* cur = sh + p.Smax;
+  double* A = p.alpha + (long)b * p.T * p.Smax;
+  double* Bt = p.beta + (long)b * p.T * p.Smax;
+  if (Tb <= 0) {
+    if (threadIdx.x == 0) { p.nll[b] = (L == 0) ? 0.0 : INFINITY; p.loss_utt[b] = 0.f; }
+    return;
+  }
+  // ---- alpha
+  for (int s = threadIdx.x; s < S; s += blockDim.x) {
+    double a = -INFINITY;
+    if (s < 2) a = ctc_lp(p, b, 0, ctc_label(p, b, s));
+    prev[s] = a;
+    A[s] = a;
+  }
+  __syncthreads();
+  for (int t = 1; t < Tb; ++t) {
+    for (int s = threadIdx.x; s < S; s += blockDim.x) {
+      const int lab = ctc_label(p, b, s);
+      double a = prev[s];
+      if (s >= 1) a = lae(a, prev[s - 1]);
+      if (s >= 2 && lab != 0 && lab != ctc_label(p, b, s - 2)) a = lae(a, prev[s - 2]);
+      a = a == -INFINITY ? a : a + ctc_lp(p, b, t, lab);
+      cur[s] = a;
+      A[(long)t * p.Smax + s] = a;
+    }
+    __syncthreads();
+    double* tmp = prev; prev = cur; cur = tmp;
+  }
+  // nll
+  __shared__ double ll;
+  if (threadIdx.x == 0) {
+    double l = prev[S - 1];
+    if (S >= 2) l = lae(l, prev[S - 2]);
+    ll = -l;
+    p.nll[b] = -l;
+    p.loss_utt[b] = isinf(-l) ? 0.f : (float)(-l);  // zero_infinity
+  }
+  __syncthreads();
+  // ---- beta
+  for (int s = threadIdx.x; s < S; s += blockDim.x) {
+    double v = -INFINITY;
+    if (s >= S - 2) v = ctc_lp(p, b, Tb - 1, ctc_label(p, b, s));
+    prev[s] = v;
+    Bt[(long)(Tb - 1) * p.Smax + s] = v;
+  }
+  __syncthreads();
+  for (int t = Tb - 2; t >= 0; --t) {
+    for (int s = threadIdx.x; s < S; s += blockDim.x) {
+      const int lab = ctc_label(p, b, s);
+      double v = prev[s];
+      if (s + 1 < S) v = lae(v, prev[s + 1]);
+      if (s + 2 < S && lab != 0 && lab != ctc_label(p, b, s + 2)) v = lae(v, prev[s + 2]);
+      v = v == -INFINITY ? v : v + ctc_lp(p, b, t, lab);
+      cur[s] = v;
+      Bt[(long)t * p.Smax + s] = v;
+    }
+    __syncthreads();
+    double* tmp = prev; prev = cur; cur = tmp;
+  }
+}
+
+// loss = sum_b loss_utt / B  (ctc.py:58-60); one block
+__global__ void ctc_reduce_kernel(int B, const float* __restrict__ loss_utt, float* __restrict__ loss) {
+  __shared__ double red[16];
+  double a = 0.0;
+  for (int b = threadIdx.x; b < B; b += blockDim.x) a += loss_utt[b];
+  a = block_sum_d(a, red);
+  if (threadIdx.x == 0) loss[0] = (float)(a / B);
+}
+
+// grad[b,t,v] = g_b * (softmax(x)[v] - sum_{s: l'(s)=v} exp(alpha+beta+nll-lp))
+template <typename TO>
+__global__ __launch_bounds__(256) void ctc_grad_kernel(CtcP p, const float* __restrict__ gscale, float coef,
+                                                       TO* __restrict__ grad, long ldg) {
+  extern __shared__ float acc[];  // V
+  const long row = blockIdx.x;
+  const int b = (int)(row / p.T), t = (int)(row % p.T);
+  const int Tb = (int)min((long long)p.T, p.hlens[b]);
+  const double nll = p.nll[b];
+  TO* gr = grad + row * ldg;
+  if (t >= Tb || isinf(nll) || isnan(nll)) {
+    for (int v = threadIdx.x; v < p.V; v += blockDim.x) gr[v] = from_f<TO>(0.f);
+    return;
+  }
+  for (int v = threadIdx.x; v < p.V; v += blockDim.x) acc[v] = 0.f;
+  __syncthreads();
+  const int L = (int)p.ylens[b];
+  const int S = 2 * L + 1;
+  const double* A = p.alpha + ((long)b * p.T + t) * p.Smax;
+  const double* Bt = p.beta + ((long)b * p.T + t) * p.Smax;
+  for (int s = threadIdx.x; s < S; s += blockDim.x) {
+    const int lab = ctc_label(p, b, s);
+    const double ab = A[s] + Bt[s];
+    if (ab != -INFINITY) atomicAdd(&acc[lab], (float)exp(ab + nll - ctc_lp(p, b, t, lab)));
+  }
+  __syncthreads();
+  const float g = gscale[0] * coef;
+  const float* xr = p.logits + row * p.ldt;
+  const float l = p.lse[row];
+  for (int v = threadIdx.x; v < p.V; v += blockDim.x) gr[v] = from_f<TO>(g * (__expf(xr[v] - l) - acc[v]));
+}
+
+// ---------------------------------------------------------------- label smoothing
+struct LsmP {
+  long rows; int V;
+  const float* x; long ldx;
+  const long long* tgt;
+  float smoothing; int ignore_id;
+  float* lse;          // [rows]
+  double* loss_row;    // [rows]
+  int* stat;           // [0] correct, [1] valid
+};
+
+__global__ __launch_bounds__(256) void lsm_fwd_kernel(LsmP p) {
+  const int lane = threadIdx.x & 63;
+  const long r = blockIdx.x * 4L + (threadIdx.x >> 6);
+  if (r >= p.rows) return;
+  const float* xr = p.x + r * p.ldx;
+  float mx = -INFINITY;
+  int am = 0x7fffffff;
+  double sx = 0.0;
+  for (int v = lane; v < p.V; v += 64) {
+    const float t = xr[v];
+    if (t > mx || (t == mx && v < am)) { mx = t; am = v; }
+    sx += t;
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const float om = __shfl_xor(mx, o, 64);
+    const int oi = __shfl_xor(am, o, 64);
+    if (om > mx || (om == mx && oi < am)) { mx = om; am = oi; }
+  }
+  sx = wave_sum_d(sx);
+  double se = 0.0;
+  for (int v = lane; v < p.V; v += 64) se += (double)__expf(xr[v] - mx);
+  se = wave_sum_d(se);
+  if (lane != 0) return;
+  const double lse = (double)mx + log(se);
+  p.lse[r] = (float)lse;
+  const long long t = p.tgt[r];
+  if (t == p.ignore_id) { p.loss_row[r] = 0.0; return; }
+  // true_dist = eps everywhere, conf at target (label_smoothing_loss.py:55-60), in the
+  // logits' dtype (f32) like the reference
+  const float epsf = p.smoothing / (p.V - 1);
+  const float conf = 1.f - p.smoothing;
+  const double eps = epsf, cf = conf;
+  const double xt = xr[t];
+  const double qlogq = (eps > 0 ? (p.V - 1) * eps * log(eps) : 0.0) + (cf > 0 ? cf * log(cf) : 0.0);
+  const double qx = eps * (sx - xt) + cf * xt;
+  const double qsum = eps * (p.V - 1) + cf;
+  p.loss_row[r] = qlogq - (qx - lse * qsum);
+  atomicAdd(&p.stat[1], 1);
+  if (am == t) atomicAdd(&p.stat[0], 1);
+}
+
+// out[0] = loss = sum rows / denom, out[1] = acc, out[2] = 1/denom
+__global__ void lsm_finalize_kernel(long rows, const double* __restrict__ loss_row, const int* __restrict__ stat,
+                                    int normalize_length, float batch, float* __restrict__ loss_out,
+                                    float* __restrict__ acc_out, float* __restrict__ inv_out) {
+  __shared__ double red[16];
+  double a = 0.0;
+  for (long r = threadIdx.x; r < rows; r += blockDim.x) a += loss_row[r];
+  a = block_sum_d(a, red);
+  if (threadIdx.x == 0) {
+    const double denom = normalize_length ? (double)stat[1] : (double)batch;
+    loss_out[0] = (float)(a / denom);
+    acc_out[0] = stat[1] > 0 ? (float)((double)stat[0] / (double)stat[1]) : 0.f;
+    inv_out[0] = (float)(1.0 / denom);
+  }
+}
+
+template <typename TO>
+__global__ void lsm_bwd_kernel(LsmP p, const float* __restrict__ gscale, const float* __restrict__ coef_dev,
+                               float coef, TO* __restrict__ grad, long ldg) {
+  const long r = blockIdx.x;
+  const long long t = p.tgt[r];
+  TO* gr = grad + r * ldg;
+  if (t == p.ignore_id) {
+    for (int v = threadIdx.x; v < p.V; v += blockDim.x) gr[v] = from_f<TO>(0.f);
+    return;
+  }
+  const float g = gscale[0] * coef_dev[0] * coef;
+  const float eps = p.smoothing / (p.V - 1), conf = 1.f - p.smoothing;
+  const float* xr = p.x + r * p.ldx;
+  const float l = p.lse[r];
+  for (int v = threadIdx.x; v < p.V; v += blockDim.x) {
+    const float q = v == t ? conf : eps;
+    gr[v] = from_f<TO>(g * (__expf(xr[v] - l) - q));
+  }
+}
+
+}  // namespace
+
+extern "C" int ea_ctc_loss_fwd(int B, int T, int V, const float* logits, long ldt, const long long* hlens,
+                               const long long* ys, long ldys, const long long* ylens, int Lmax, float* lse,
+                               double* alpha, double* beta, double* nll, float* loss_utt, float* loss,
+                               void* stream) {
+  hipStream_t st = (hipStream_t)stream;
+  const long rows = (long)B * T;
+  hipLaunchKernelGGL(lse_rows_kernel, dim3(ea_cdiv(rows, 4)), dim3(256), 0, st, rows, V, logits, ldt, lse);
+  EA_LAUNCH_CHECK();
+  const int Smax = 2 * Lmax + 1;
+  CtcP p{B, T, V, Lmax, Smax, logits, ldt, lse, hlens, ys, ldys, ylens, alpha, beta, nll, loss_utt};
+  hipLaunchKernelGGL(ctc_lattice_kernel, dim3(B), dim3(256), 2 * Smax * sizeof(double), st, p);
+  EA_LAUNCH_CHECK();
+  hipLaunchKernelGGL(ctc_reduce_kernel, dim3(1), dim3(256), 0, st, B, loss_utt, loss);
+  EA_LAUNCH_CHECK();
+  return 0;
+}
+
+extern "C" int ea_ctc_loss_bwd(int B, int T, int V, const float* logits, long ldt, const long long* hlens,
+                               const long long* ys, long ldys, const long long* ylens, int Lmax, const float* lse,
+                               const double* alpha, const double* beta, const double* nll,
+                               const float* gscale, float coef, void* grad, int grad_dtype, long ldg,
+                               void* stream) {
+  EA_CHECK_ARG(V <= 16384);
+  const int Smax = 2 * Lmax + 1;
+  CtcP p{B, T, V, Lmax, Smax, logits, ldt, lse, hlens, ys, ldys, ylens, (double*)alpha, (double*)beta,
+         (double*)nll, nullptr};
+  hipStream_t st = (hipStream_t)stream;
+  const size_t sm = (size_t)V * sizeof(float);
+  if (grad_dtype == EA_BF16)
+    hipLaunchKernelGGL(ctc_grad_kernel<bf16>, dim3((long)B * T), dim3(256), sm, st, p, gscale, coef, (bf16*)grad, ldg);
+  else
+    hipLaunchKernelGGL(ctc_grad_kernel<float>, dim3((long)B * T), dim3(256), sm, st, p, gscale, coef, (float*)grad, ldg);
+  EA_LAUNCH_CHECK();
+  return 0;
+}
+
+extern "C" int ea_lsm_loss_fwd(long rows, int V, const float* x, long ldx, const long long* tgt, float smoothing,
+                               int ignore_id, int normalize_length, float batch, float* lse, double* loss_row,
+                               int* stat, float* loss, float* acc, float* inv_denom, void* stream) {
+  hipStream_t st = (hipStream_t)stream;
+  hipMemsetAsync(stat, 0, 2 * sizeof(int), st);
+  LsmP p{rows, V, x, ldx, tgt, smoothing, ignore_id, lse, loss_row, stat};
+  hipLaunchKernelGGL(lsm_fwd_kernel, dim3(ea_cdiv(rows, 4)), dim3(256), 0, st, p);
+  EA_LAUNCH_CHECK();
+  hipLaunchKernelGGL(lsm_finalize_kernel, dim3(1), dim3(256), 0, st, rows, loss_row, stat, normalize_length, batch, loss, acc, inv_denom);
+  EA_LAUNCH_CHECK();
+  return 0;
+}
+
+extern "C" int ea_lsm_loss_bwd(long rows, int V, const float* x, long ldx, const long long* tgt, float smoothing,
+                               int ignore_id, const float* lse, const float* gscale, const float* inv_denom,
+                               float coef, void* grad, int grad_dtype, long ldg, void* stream) {
+  LsmP p{rows, V, x, ldx, tgt, smoothing, ignore_id, (float*)lse, nullptr, nullptr};
+  hipStream_t st = (hipStream_t)stream;
+  if (grad_dtype == EA_BF16)
+    hipLaunchKernelGGL(lsm_bwd_kernel<bf16>, dim3(rows), dim3(256), 0, st, p, gscale, inv_denom, coef, (bf16*)grad, ldg);
+  else
+    hipLaunchKernelGGL(lsm_bwd_kernel<float>, dim3(rows), dim3(256), 0, st, p, gscale, inv_denom, coef, (float*)grad, ldg);
+  EA_LAUNCH_CHECK();
+  return 0;
+}

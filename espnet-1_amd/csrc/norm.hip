@@ -1,0 +1,384 @@
+// LayerNorm (eps 1e-12, transformer/layer_norm.py:12-42) and the conv-module BatchNorm1d
+// (conformer/convolution.py:45,75) forward/backward, plus the shared partial-sum reducer.
+//
+// LayerNorm: one wave64 per row, the row held in registers (d <= 64*MAXE), two-pass
+// mean/variance in f32; backward fuses dgamma/dbeta per-block partials (deterministic
+// second pass, ea_reduce_partials) and accumulates dx into the f32 residual gradient.
+#include "common.h"
+
+namespace {
+
+template <int MAXE, typename TO>
+__global__ __launch_bounds__(256) void ln_fwd_kernel(int rows, int d, const float* __restrict__ x, long ldx,
+                                                     const float* __restrict__ g, const float* __restrict__ b,
+                                                     float eps, TO* __restrict__ y, long ldy,
+                                                     float* __restrict__ mean_out, float* __restrict__ rstd_out) {
+  const int lane = threadIdx.x & 63;
+  const int nw = gridDim.x * (blockDim.x >> 6);
+  for (int r = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); r < rows; r += nw) {
+    const float* xr = x + (long)r * ldx;
+    float v[MAXE];
+    float s = 0.f;
+#pragma unroll
+    for (int i = 0; i < MAXE; ++i) {
+      const int c = i * 64 + lane;
+      v[i] = c < d ? xr[c] : 0.f;
+      s += v[i];
+    }
+    const float mean = wave_sum(s) / d;
+    float ss = 0.f;
+#pragma unroll
+    for (int i = 0; i < MAXE; ++i) {
+      const int c = i * 64 + lane;
+      const float t = c < d ? v[i] - mean : 0.f;
+      ss += t * t;
+    }
+    const float rstd = rsqrtf(wave_sum(ss) / d + eps);
+    TO* yr = y + (long)r * ldy;
+#pragma unroll
+    for (int i = 0; i < MAXE; ++i) {
+      const int c = i * 64 + lane;
+      if (c < d) yr[c] = from_f<TO>((v[i] - mean) * rstd * g[c] + b[c]);
+    }
+    if (lane == 0) {
+      mean_out[r] = mean;
+      rstd_out[r] = rstd;
+    }
+  }
+}
+
+// dx (+)= rstd*(dxh - mean(dxh) - xh*mean(dxh*xh)),  dxh = dy*gamma
+// part[blk][0:d] = sum dy*xh, part[blk][d:2d] = sum dy   (this block's rows)
+template <int MAXE, typename TI>
+__global__ __launch_bounds__(256) void ln_bwd_kernel(int rows, int d, const TI* __restrict__ dy, long lddy,
+                                                     const float* __restrict__ x, long ldx,
+                                                     const float* __restrict__ g, const float* __restrict__ mean,
+                                                     const float* __restrict__ rstd, float* __restrict__ dx,
+                                                     long lddx, int accumulate, float* __restrict__ part) {
+  __shared__ float red[4][2][64 * MAXE];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int nw = gridDim.x * 4;
+  float pg[MAXE], pb[MAXE];
+#pragma unroll
+  for (int i = 0; i < MAXE; ++i) pg[i] = pb[i] = 0.f;
+  for (int r = blockIdx.x * 4 + w; r < rows; r += nw) {
+    const float mu = mean[r], rs = rstd[r];
+    float xh[MAXE], dg[MAXE];
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int i = 0; i < MAXE; ++i) {
+      const int c = i * 64 + lane;
+      if (c < d) {
+        const float dyv = to_f(dy[(long)r * lddy + c]);
+        xh[i] = (x[(long)r * ldx + c] - mu) * rs;
+        dg[i] = dyv * g[c];
+        s1 += dg[i];
+        s2 += dg[i] * xh[i];
+        pg[i] += dyv * xh[i];
+        pb[i] += dyv;
+      } else {
+        xh[i] = dg[i] = 0.f;
+      }
+    }
+    s1 = wave_sum(s1) / d;
+    s2 = wave_sum(s2) / d;
+#pragma unroll
+    for (int i = 0; i < MAXE; ++i) {
+      const int c = i * 64 + lane;
+      if (c < d) {
+        float v = rs * (dg[i] - s1 - xh[i] * s2);
+        float* o = dx + (long)r * lddx + c;
+        *o = accumulate ? *o + v : v;
+      }
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < MAXE; ++i) {
+    red[w][0][i * 64 + lane] = pg[i];
+    red[w][1][i * 64 + lane] = pb[i];
+  }
+  __syncthreads();
+  for (int c = threadIdx.x; c < d; c += blockDim.x) {
+    float a = 0.f, bb = 0.f;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      a += red[k][0][c];
+      bb += red[k][1][c];
+    }
+    part[(long)blockIdx.x * 2 * d + c] = a;
+    part[(long)blockIdx.x * 2 * d + d + c] = bb;
+  }
+}
+
+// out[c] (+)= sum_p part[p*stride + c], c < n   (fixed order -> deterministic)
+__global__ void reduce_partials_kernel(int nparts, int n, const float* __restrict__ part, long stride,
+                                       float* __restrict__ out, int accumulate) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= n) return;
+  double a = 0.0;
+  for (int p = 0; p < nparts; ++p) a += part[(long)p * stride + c];
+  out[c] = accumulate ? out[c] + (float)a : (float)a;
+}
+
+// column partial sums of x (rows x n, dtype) : part[blk][c] = sum over this block's rows
+template <typename T>
+__global__ void colsum_partial_kernel(int rows, int n, const T* __restrict__ x, long ld, int rows_per_blk,
+                                      float* __restrict__ part) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= n) return;
+  const int r0 = blockIdx.y * rows_per_blk;
+  const int r1 = min(rows, r0 + rows_per_blk);
+  float a = 0.f;
+  for (int r = r0; r < r1; ++r) a += to_f(x[(long)r * ld + c]);
+  part[(long)blockIdx.y * n + c] = a;
+}
+
+// ---------------------------------------------------------------- BatchNorm1d (train)
+// Stats over all rows (padding included, as the reference's BatchNorm1d sees them).
+// Pass 1: per-block shifted sums (shift = row 0) -> fp64 combine in bn_finalize.
+__global__ void bn_partial_kernel(int rows, int C, const float* __restrict__ y, int rows_per_blk,
+                                  float* __restrict__ part) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  const float sh = y[c];
+  const int r0 = blockIdx.y * rows_per_blk, r1 = min(rows, r0 + rows_per_blk);
+  float s = 0.f, ss = 0.f;
+  for (int r = r0; r < r1; ++r) {
+    const float t = y[(long)r * C + c] - sh;
+    s += t;
+    ss += t * t;
+  }
+  part[(long)blockIdx.y * 2 * C + c] = s;
+  part[(long)blockIdx.y * 2 * C + C + c] = ss;
+}
+
+__global__ void bn_finalize_kernel(int rows, int C, int nparts, const float* __restrict__ y,
+                                   const float* __restrict__ part, float eps, float momentum,
+                                   float* __restrict__ mean, float* __restrict__ rstd,
+                                   float* __restrict__ run_mean, float* __restrict__ run_var,
+                                   long long* __restrict__ nbt) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c == 0 && nbt) nbt[0] += 1;
+  if (c >= C) return;
+  double s = 0.0, ss = 0.0;
+  for (int p = 0; p < nparts; ++p) {
+    s += part[(long)p * 2 * C + c];
+    ss += part[(long)p * 2 * C + C + c];
+  }
+  const double n = rows;
+  const double m = s / n;
+  double var = ss / n - m * m;
+  if (var < 0) var = 0;
+  const double mu = m + (double)y[c];
+  mean[c] = (float)mu;
+  rstd[c] = (float)(1.0 / sqrt(var + (double)eps));
+  if (run_mean) {
+    run_mean[c] = (float)((1.0 - momentum) * run_mean[c] + momentum * mu);
+    run_var[c] = (float)((1.0 - momentum) * run_var[c] + momentum * var * n / (n > 1 ? n - 1 : 1));
+  }
+}
+
+__global__ void bn_eval_stats_kernel(int C, const float* __restrict__ rm, const float* __restrict__ rv, float eps,
+                                     float* __restrict__ mean, float* __restrict__ rstd) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  mean[c] = rm[c];
+  rstd[c] = rsqrtf(rv[c] + eps);
+}
+
+// z = act(xhat*gamma + beta) (train: batch mean/rstd; eval: running stats passed in)
+template <typename TO>
+__global__ void bn_apply_act_kernel(long total, int C, const float* __restrict__ y, const float* __restrict__ mean,
+                                    const float* __restrict__ rstd, const float* __restrict__ g,
+                                    const float* __restrict__ b, int act, TO* __restrict__ z) {
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    const int c = (int)(i % C);
+    const float h = (y[i] - mean[c]) * rstd[c] * g[c] + b[c];
+    z[i] = from_f<TO>(act_fwd(act, h));
+  }
+}
+
+// backward pass 1: dh = dz*act'(h); part = [sum dh*xhat | sum dh] per block
+template <typename TI>
+__global__ void bn_bwd_partial_kernel(int rows, int C, const TI* __restrict__ dz, const float* __restrict__ y,
+                                      const float* __restrict__ mean, const float* __restrict__ rstd,
+                                      const float* __restrict__ g, const float* __restrict__ b, int act,
+                                      int rows_per_blk, float* __restrict__ part) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  const int r0 = blockIdx.y * rows_per_blk, r1 = min(rows, r0 + rows_per_blk);
+  const float mu = mean[c], rs = rstd[c], gg = g[c], bb = b[c];
+  float s1 = 0.f, s2 = 0.f;
+  for (int r = r0; r < r1; ++r) {
+    const long i = (long)r * C + c;
+    const float xh = (y[i] - mu) * rs;
+    const float dh = to_f(dz[i]) * act_bwd(act, xh * gg + bb);
+    s1 += dh * xh;
+    s2 += dh;
+  }
+  part[(long)blockIdx.y * 2 * C + c] = s1;
+  part[(long)blockIdx.y * 2 * C + C + c] = s2;
+}
+
+// backward pass 2: dy = gamma*rstd/N * (N*dh - sum(dh) - xhat*sum(dh*xhat))
+template <typename TI>
+__global__ void bn_bwd_apply_kernel(long total, int C, int rows, const TI* __restrict__ dz, const float* __restrict__ y,
+                                    const float* __restrict__ mean, const float* __restrict__ rstd,
+                                    const float* __restrict__ g, const float* __restrict__ b, int act,
+                                    const float* __restrict__ dgamma, const float* __restrict__ dbeta,
+                                    float* __restrict__ dy) {
+  const float invn = 1.f / rows;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    const int c = (int)(i % C);
+    const float xh = (y[i] - mean[c]) * rstd[c];
+    const float dh = to_f(dz[i]) * act_bwd(act, xh * g[c] + b[c]);
+    dy[i] = g[c] * rstd[c] * (dh - dbeta[c] * invn - xh * dgamma[c] * invn);
+  }
+}
+
+int ln_blocks(int rows) { return ea_grid_cap(ea_cdiv(rows, 4), 2048); }
+
+}  // namespace
+
+#define EA_LN_DISPATCH(KER, TYPE, ...)                                                        \
+  do {                                                                                        \
+    if (d <= 64) hipLaunchKernelGGL((KER<1, TYPE>), __VA_ARGS__);                             \
+    else if (d <= 256) hipLaunchKernelGGL((KER<4, TYPE>), __VA_ARGS__);                       \
+    else if (d <= 512) hipLaunchKernelGGL((KER<8, TYPE>), __VA_ARGS__);                       \
+    else if (d <= 1024) hipLaunchKernelGGL((KER<16, TYPE>), __VA_ARGS__);                     \
+    else return EA_ERR_BAD_ARG;                                                               \
+  } while (0)
+
+extern "C" int ea_layernorm_fwd(int rows, int d, const float* x, long ldx, const float* gamma,
+                                const float* beta, float eps, void* y, int y_dtype, long ldy,
+                                float* mean, float* rstd, void* stream) {
+  if (rows == 0) return 0;
+  dim3 grid(ln_blocks(rows)), blk(256);
+  hipStream_t st = (hipStream_t)stream;
+  if (y_dtype == EA_BF16)
+    EA_LN_DISPATCH(ln_fwd_kernel, bf16, grid, blk, 0, st, rows, d, x, ldx, gamma, beta, eps, (bf16*)y, ldy, mean, rstd);
+  else
+    EA_LN_DISPATCH(ln_fwd_kernel, float, grid, blk, 0, st, rows, d, x, ldx, gamma, beta, eps, (float*)y, ldy, mean, rstd);
+  EA_LAUNCH_CHECK();
+  return 0;
+}
+
+extern "C" int ea_layernorm_bwd(int rows, int d, const void* dy, int dy_dtype, long lddy, const float* x,
+                                long ldx, const float* gamma, const float* mean, const float* rstd,
+                                float* dx, long lddx, int accumulate, float* dgamma, float* dbeta,
+                                int accumulate_params, float* workspace, long ws_elems, void* stream) {
+  if (rows == 0) return 0;
+  const int nb = min(ln_blocks(rows), 512);
+  EA_CHECK_ARG(ws_elems >= (long)nb * 2 * d);
+  EA_CHECK_ARG(dbeta == dgamma + d);  // grads of (weight, bias) are adjacent in the arena
+  dim3 grid(nb), blk(256);
+  hipStream_t st = (hipStream_t)stream;
+  if (dy_dtype == EA_BF16)
+    EA_LN_DISPATCH(ln_bwd_kernel, bf16, grid, blk, 0, st, rows, d, (const bf16*)dy, lddy, x, ldx, gamma, mean, rstd, dx, lddx, accumulate, workspace);
+  else
+    EA_LN_DISPATCH(ln_bwd_kernel, float, grid, blk, 0, st, rows, d, (const float*)dy, lddy, x, ldx, gamma, mean, rstd, dx, lddx, accumulate, workspace);
+  EA_LAUNCH_CHECK();
+  hipLaunchKernelGGL(reduce_partials_kernel, dim3(ea_cdiv(2 * d, 256)), dim3(256), 0, st, nb, 2 * d,
+                     workspace, (long)2 * d, dgamma, accumulate_params);
+  EA_LAUNCH_CHECK();
+  return 0;
+}
+
+extern "C" int ea_reduce_partials(int nparts, int n, const float* part, long stride, float* out,
+                                  int accumulate, void* stream) {
+  if (n == 0) return 0;
+  hipLaunchKernelGGL(reduce_partials_kernel, dim3(ea_cdiv(n, 256)), dim3(256), 0, (hipStream_t)stream,
+                     nparts, n, part, stride, out, accumulate);
+  EA_LAUNCH_CHECK();
+  return 0;
+}
+
+extern "C" int ea_colsum(int rows, int n, const void* x, int x_dtype, long ld, float* out, int accumulate,
+                         float* workspace, long ws_elems, void* stream) {
+  if (n == 0) return 0;
+  hipStream_t st = (hipStream_t)stream;
+  int rpb = 64;
+  int nparts = ea_cdiv(rows, rpb);
+  while ((long)nparts * n > ws_elems && rpb < (1 << 20)) {
+    rpb *= 2;
+    nparts = ea_cdiv(rows, rpb);
+  }
+  EA_CHECK_ARG((long)nparts * n <= ws_elems);
+  if (rows == 0) nparts = 0;
+  dim3 grid(ea_cdiv(n, 256), max(nparts, 1));
+  if (nparts > 0) {
+    if (x_dtype == EA_BF16)
+      hipLaunchKernelGGL(colsum_partial_kernel<bf16>, grid, dim3(256), 0, st, rows, n, (const bf16*)x, ld, rpb, workspace);
+    else
+      hipLaunchKernelGGL(colsum_partial_kernel<float>, grid, dim3(256), 0, st, rows, n, (const float*)x, ld, rpb, workspace);
+    EA_LAUNCH_CHECK();
+  }
+  hipLaunchKernelGGL(reduce_partials_kernel, dim3(ea_cdiv(n, 256)), dim3(256), 0, st, nparts, n, workspace,
+                     (long)n, out, accumulate);
+  EA_LAUNCH_CHECK();
+  return 0;
+}
+
+extern "C" int ea_batchnorm_fwd(int rows, int C, const float* y, const float* gamma, const float* beta,
+                                float eps, float momentum, int training, float* mean, float* rstd,
+                                float* running_mean, float* running_var, long long* num_batches_tracked,
+                                int act, void* z, int z_dtype, float* workspace, long ws_elems,
+                                void* stream) {
+  hipStream_t st = (hipStream_t)stream;
+  const long total = (long)rows * C;
+  if (training) {
+    const int rpb = 32;
+    const int nparts = ea_cdiv(rows, rpb);
+    EA_CHECK_ARG((long)nparts * 2 * C <= ws_elems && rows > 0);
+    hipLaunchKernelGGL(bn_partial_kernel, dim3(ea_cdiv(C, 256), nparts), dim3(256), 0, st, rows, C, y, rpb, workspace);
+    EA_LAUNCH_CHECK();
+    hipLaunchKernelGGL(bn_finalize_kernel, dim3(ea_cdiv(C, 256)), dim3(256), 0, st, rows, C, nparts, y, workspace,
+                       eps, momentum, mean, rstd, running_mean, running_var, num_batches_tracked);
+    EA_LAUNCH_CHECK();
+  } else {
+    EA_CHECK_ARG(running_mean && running_var);
+    hipLaunchKernelGGL(bn_eval_stats_kernel, dim3(ea_cdiv(C, 256)), dim3(256), 0, st, C, running_mean, running_var,
+                       eps, mean, rstd);
+    EA_LAUNCH_CHECK();
+  }
+  dim3 grid(ea_grid_cap(ea_cdiv(total, 256)));
+  if (z_dtype == EA_BF16)
+    hipLaunchKernelGGL(bn_apply_act_kernel<bf16>, grid, dim3(256), 0, st, total, C, y, mean, rstd, gamma, beta, act, (bf16*)z);
+  else
+    hipLaunchKernelGGL(bn_apply_act_kernel<float>, grid, dim3(256), 0, st, total, C, y, mean, rstd, gamma, beta, act, (float*)z);
+  EA_LAUNCH_CHECK();
+  return 0;
+}
+
+extern "C" int ea_batchnorm_bwd(int rows, int C, const void* dz, int dz_dtype, const float* y, const float* mean,
+                                const float* rstd, const float* gamma, const float* beta, int act, float* dy,
+                                float* dgamma, float* dbeta, int accumulate_params, float* workspace,
+                                long ws_elems, void* stream) {
+  hipStream_t st = (hipStream_t)stream;
+  const long total = (long)rows * C;
+  const int rpb = 32;
+  const int nparts = ea_cdiv(rows, rpb);
+  EA_CHECK_ARG((long)nparts * 2 * C + 2 * C <= ws_elems && rows > 0);
+  EA_CHECK_ARG(dbeta == dgamma + C);
+  float* sums = workspace + (long)nparts * 2 * C;  // [sum dh*xhat | sum dh] for this batch
+  dim3 g1(ea_cdiv(C, 256), nparts);
+  if (dz_dtype == EA_BF16)
+    hipLaunchKernelGGL(bn_bwd_partial_kernel<bf16>, g1, dim3(256), 0, st, rows, C, (const bf16*)dz, y, mean, rstd, gamma, beta, act, rpb, workspace);
+  else
+    hipLaunchKernelGGL(bn_bwd_partial_kernel<float>, g1, dim3(256), 0, st, rows, C, (const float*)dz, y, mean, rstd, gamma, beta, act, rpb, workspace);
+  EA_LAUNCH_CHECK();
+  hipLaunchKernelGGL(reduce_partials_kernel, dim3(ea_cdiv(2 * C, 256)), dim3(256), 0, st, nparts, 2 * C, workspace,
+                     (long)2 * C, sums, 0);
+  EA_LAUNCH_CHECK();
+  dim3 g2(ea_grid_cap(ea_cdiv(total, 256)));
+  if (dz_dtype == EA_BF16)
+    hipLaunchKernelGGL(bn_bwd_apply_kernel<bf16>, g2, dim3(256), 0, st, total, C, rows, (const bf16*)dz, y, mean, rstd, gamma, beta, act, sums, sums + C, dy);
+  else
+    hipLaunchKernelGGL(bn_bwd_apply_kernel<float>, g2, dim3(256), 0, st, total, C, rows, (const float*)dz, y, mean, rstd, gamma, beta, act, sums, sums + C, dy);
+  EA_LAUNCH_CHECK();
+  // parameter grads: dgamma = sum dh*xhat, dbeta = sum dh
+  hipLaunchKernelGGL(reduce_partials_kernel, dim3(ea_cdiv(2 * C, 256)), dim3(256), 0, st, 1, 2 * C, sums,
+                     (long)2 * C, dgamma, accumulate_params);
+  EA_LAUNCH_CHECK();
+  return 0;
+}

@@ -1,0 +1,116 @@
+// Optimizer step over the flat parameter arena (one launch for all 615 tensors):
+// clip_grad_norm_(max_norm, 2) (trainer.py:653-657) + skip-on-non-finite
+// (trainer.py:662-678) + torch.optim.Adam (L2 weight decay, bias correction), plus the
+// f32 -> bf16 weight shadow for the AMP GEMMs, and small scalar helpers.
+// The clip coefficient and the finite check are read from device memory: no host sync.
+#include "common.h"
+
+namespace {
+
+__global__ __launch_bounds__(256) void sqnorm_partial_kernel(long n, const float* __restrict__ x, double* __restrict__ part) {
+  __shared__ double red[16];
+  double a = 0.0;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+    const double v = x[i];
+    a += v * v;
+  }
+  a = block_sum_d(a, red);
+  if (threadIdx.x == 0) part[blockIdx.x] = a;
+}
+
+__global__ void sqnorm_final_kernel(int nparts, const double* __restrict__ part, float* __restrict__ norm) {
+  __shared__ double red[16];
+  double a = 0.0;
+  for (int i = threadIdx.x; i < nparts; i += blockDim.x) a += part[i];
+  a = block_sum_d(a, red);
+  if (threadIdx.x == 0) norm[0] = (float)sqrt(a);
+}
+
+struct AdamP {
+  long n;
+  float* p; const float* g; float* m; float* v; bf16* p16;
+  float lr, b1, b2, eps, wd;
+  float bc1, bc2_sqrt;   // 1-b1^t, sqrt(1-b2^t)
+  const float* norm; float max_norm;
+};
+
+__global__ __launch_bounds__(256) void adam_kernel(AdamP a) {
+  const float nrm = a.norm ? a.norm[0] : 0.f;
+  if (a.norm && !isfinite(nrm)) return;  // trainer.py:662: skip the update
+  float coef = 1.f;
+  if (a.norm && a.max_norm > 0.f) coef = fminf(a.max_norm / (nrm + 1e-6f), 1.f);
+  const float step_size = a.lr / a.bc1;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < a.n; i += (long)gridDim.x * blockDim.x) {
+    float p = a.p[i];
+    float g = a.g[i] * coef;
+    if (a.wd != 0.f) g += a.wd * p;
+    float m = a.m[i];
+    m = m + (1.f - a.b1) * (g - m);  // lerp, as torch Adam
+    float v = a.v[i] * a.b2 + (1.f - a.b2) * g * g;
+    const float denom = sqrtf(v) / a.bc2_sqrt + a.eps;
+    p -= step_size * (m / denom);
+    a.p[i] = p;
+    a.m[i] = m;
+    a.v[i] = v;
+    if (a.p16) a.p16[i] = (bf16)p;
+  }
+}
+
+__global__ void cast_kernel(long n, const float* __restrict__ x, bf16* __restrict__ y) {
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) y[i] = (bf16)x[i];
+}
+
+__global__ void scale_inplace_kernel(long n, float* __restrict__ x, const float* __restrict__ s, float c) {
+  const float k = s[0] * c;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) x[i] *= k;
+}
+
+// out = wa*a + wb*b (device scalars; b may be null)
+__global__ void axpby_scalar_kernel(const float* a, float wa, const float* b, float wb, float* out) {
+  out[0] = wa * a[0] + (b ? wb * b[0] : 0.f);
+}
+
+}  // namespace
+
+extern "C" int ea_sqnorm(long n, const float* x, double* workspace, float* norm, void* stream) {
+  hipStream_t st = (hipStream_t)stream;
+  const int nb = ea_grid_cap(ea_cdiv(n, 256), 2048);
+  hipLaunchKernelGGL(sqnorm_partial_kernel, dim3(nb), dim3(256), 0, st, n, x, workspace);
+  EA_LAUNCH_CHECK();
+  hipLaunchKernelGGL(sqnorm_final_kernel, dim3(1), dim3(256), 0, st, nb, workspace, norm);
+  EA_LAUNCH_CHECK();
+  return 0;
+}
+
+extern "C" int ea_adam_step(long n, float* params, const float* grads, float* exp_avg, float* exp_avg_sq,
+                            void* params_bf16, float lr, float beta1, float beta2, float eps, float weight_decay,
+                            long step, const float* grad_norm, float max_norm, void* stream) {
+  EA_CHECK_ARG(step >= 1);
+  AdamP a;
+  a.n = n; a.p = params; a.g = grads; a.m = exp_avg; a.v = exp_avg_sq; a.p16 = (bf16*)params_bf16;
+  a.lr = lr; a.b1 = beta1; a.b2 = beta2; a.eps = eps; a.wd = weight_decay;
+  a.bc1 = (float)(1.0 - pow((double)beta1, (double)step));
+  a.bc2_sqrt = (float)sqrt(1.0 - pow((double)beta2, (double)step));
+  a.norm = grad_norm; a.max_norm = max_norm;
+  hipLaunchKernelGGL(adam_kernel, dim3(ea_grid_cap(ea_cdiv(n, 256), 4096)), dim3(256), 0, (hipStream_t)stream, a);
+  EA_LAUNCH_CHECK();
+  return 0;
+}
+
+extern "C" int ea_cast_f32_bf16(long n, const float* x, void* y, void* stream) {
+  hipLaunchKernelGGL(cast_kernel, dim3(ea_grid_cap(ea_cdiv(n, 256), 4096)), dim3(256), 0, (hipStream_t)stream, n, x, (bf16*)y);
+  EA_LAUNCH_CHECK();
+  return 0;
+}
+
+extern "C" int ea_scale_by_scalar(long n, float* x, const float* s, float c, void* stream) {
+  hipLaunchKernelGGL(scale_inplace_kernel, dim3(ea_grid_cap(ea_cdiv(n, 256), 4096)), dim3(256), 0, (hipStream_t)stream, n, x, s, c);
+  EA_LAUNCH_CHECK();
+  return 0;
+}
+
+extern "C" int ea_axpby_scalar(const float* a, float wa, const float* b, float wb, float* out, void* stream) {
+  hipLaunchKernelGGL(axpby_scalar_kernel, dim3(1), dim3(1), 0, (hipStream_t)stream, a, wa, b, wb, out);
+  EA_LAUNCH_CHECK();
+  return 0;
+}

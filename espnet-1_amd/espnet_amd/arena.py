@@ -1,0 +1,112 @@
+"""Flat parameter arena: every parameter of the model lives in ONE f32 device buffer
+(plus one f32 grad buffer and, in bf16 mode, one bf16 weight shadow).
+
+Why (MI355X-first): the optimizer, grad-norm, zero_grad and the f32->bf16 weight cast
+become single launches over 116 M contiguous floats instead of 615 small kernels, and
+the data-parallel all-reduce works on large contiguous buckets (bucket = byte range of
+the arena).  Groups of parameters that one fused GEMM consumes (q/k/v weights, the six
+decoder layers' cross-attention k/v) are laid out adjacently, so the fused weight is a
+plain view.
+
+nn.Parameters stay the reference's (same names, shapes, state_dict layout — SURVEY.md
+§8b); after `ParamArena(model)` each Parameter's storage IS a view into the arena and
+its `.grad` a view into the grad arena, so `state_dict()`, `load_state_dict()` and
+`parameters()` keep working unchanged.
+"""
+from __future__ import annotations
+
+from typing import Dict, List, Sequence
+
+import torch
+
+ALIGN = 64  # elements: keeps every view 256-B aligned in f32 and 128-B aligned in bf16
+
+
+class ParamArena:
+    def __init__(self, model: torch.nn.Module, device, order: Sequence[Sequence[str]] = (),
+                 shadow_dtype=None):
+        named = dict(model.named_parameters())
+        seen = set()
+        chunks: List[List[str]] = []  # each chunk is packed back to back, chunk starts aligned
+        # explicit adjacency groups first (in the given order), then the rest one by one in
+        # registration order
+        for group in order:
+            g = [n for n in group if n in named and n not in seen]
+            seen.update(g)
+            if g:
+                chunks.append(g)
+        for n in named:
+            if n not in seen:
+                chunks.append([n])
+                seen.add(n)
+        self.offsets: Dict[str, int] = {}
+        layout: List[str] = []
+        off = 0
+        for chunk in chunks:
+            off = (off + ALIGN - 1) // ALIGN * ALIGN
+            for n in chunk:
+                self.offsets[n] = off
+                off += named[n].numel()
+                layout.append(n)
+        self.numel = (off + ALIGN - 1) // ALIGN * ALIGN
+        self.device = torch.device(device)
+        self.data = torch.zeros(self.numel, dtype=torch.float32, device=self.device)
+        self.grad = torch.zeros(self.numel, dtype=torch.float32, device=self.device)
+        self.shadow = None
+        if shadow_dtype is not None and shadow_dtype != torch.float32:
+            self.shadow = torch.zeros(self.numel, dtype=shadow_dtype, device=self.device)
+        self.names = layout
+        self._params = named
+        with torch.no_grad():
+            for n in layout:
+                p = named[n]
+                o = self.offsets[n]
+                view = self.data[o:o + p.numel()].view(p.shape)
+                view.copy_(p.data.to(self.device, torch.float32))
+                p.data = view
+                p.grad = self.grad[o:o + p.numel()].view(p.shape)
+        self.refresh_shadow()
+
+    # ------------------------------------------------------------------ views
+    def contiguous_span(self, names: Sequence[str]):
+        o0 = self.offsets[names[0]]
+        end = o0
+        for n in names:
+            if self.offsets[n] != end:
+                raise RuntimeError(f"arena: {names} are not adjacent")
+            end += self._params[n].numel()
+        return o0, end
+
+    def view(self, names: Sequence[str] | str, shape=None, which="data"):
+        if isinstance(names, str):
+            names = [names]
+        o0, end = self.contiguous_span(names)
+        buf = {"data": self.data, "grad": self.grad, "shadow": self.shadow}[which]
+        if buf is None:
+            buf = self.data
+        t = buf[o0:end]
+        if shape is None:
+            shape = self._params[names[0]].shape if len(names) == 1 else (end - o0,)
+        return t.view(shape)
+
+    # ------------------------------------------------------------------ housekeeping
+    def zero_grad(self):
+        self.grad.zero_()
+
+    def refresh_shadow(self):
+        if self.shadow is not None:
+            from . import hip_ops
+            from ._lib import lib
+            lib.ea_cast_f32_bf16(self.numel, self.data.data_ptr(), self.shadow.data_ptr(),
+                                 hip_ops.stream())
+
+    def rebind(self):
+        """Re-point Parameters at the arena (after an external .data / .grad reassignment)."""
+        for n in self.names:
+            p = self._params[n]
+            o = self.offsets[n]
+            if p.data.data_ptr() != self.data[o:].data_ptr():
+                with torch.no_grad():
+                    self.data[o:o + p.numel()].view(p.shape).copy_(p.data)
+                p.data = self.data[o:o + p.numel()].view(p.shape)
+            p.grad = self.grad[o:o + p.numel()].view(p.shape)

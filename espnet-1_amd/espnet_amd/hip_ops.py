@@ -130,3 +130,85 @@ def linear_dw(dy, x, dw, *, accumulate=False):
         raise HipError("row mismatch in linear_dw")
     return gemm(dy, x, dw, M=N, N=K, K=R, a_kmajor=0, b_kmajor=0, lda=lddy, ldb=ldx,
                 ldc=dw.stride(0), epi=make_epi(beta=1.0 if accumulate else 0.0))
+
+
+# ----------------------------------------------------------------------------- scratch
+_SCRATCH = {}
+
+
+def scratch(numel: int, device, tag="ws") -> torch.Tensor:
+    """Stream-ordered f32 scratch shared by consecutive kernels (partials, reductions)."""
+    key = (str(device), tag)
+    t = _SCRATCH.get(key)
+    if t is None or t.numel() < numel:
+        t = torch.empty(max(numel, 1 << 22), dtype=torch.float32, device=device)
+        _SCRATCH[key] = t
+    return t
+
+
+def _ws(device, numel=1 << 22):
+    w = scratch(numel, device)
+    return w.data_ptr(), w.numel()
+
+
+# ----------------------------------------------------------------------------- norms
+def layernorm_fwd(x, gamma, beta, y, mean, rstd, eps=1e-12):
+    rows, d, ldx = _rows(x)
+    lib.ea_layernorm_fwd(rows, d, x.data_ptr(), ldx, gamma.data_ptr(), beta.data_ptr(), eps,
+                         y.data_ptr(), dt(y), y.stride(-2) if y.dim() > 1 else d,
+                         mean.data_ptr(), rstd.data_ptr(), stream())
+
+
+def layernorm_bwd(dy, x, gamma, mean, rstd, dx, dgamma, dbeta, accumulate=True):
+    rows, d, ldx = _rows(x)
+    _, _, lddy = _rows(dy)
+    _, _, lddx = _rows(dx)
+    w, n = _ws(x.device, max(1 << 22, 1024 * d))
+    lib.ea_layernorm_bwd(rows, d, dy.data_ptr(), dt(dy), lddy, x.data_ptr(), ldx, gamma.data_ptr(),
+                         mean.data_ptr(), rstd.data_ptr(), dx.data_ptr(), lddx, int(accumulate),
+                         dgamma.data_ptr(), dbeta.data_ptr(), 1, w, n, stream())
+
+
+def colsum(x, out, accumulate=True):
+    rows, n, ld = _rows(x)
+    w, wn = _ws(x.device)
+    lib.ea_colsum(rows, n, x.data_ptr(), dt(x), ld, out.data_ptr(), int(accumulate), w, wn, stream())
+
+
+def batchnorm_fwd(y, gamma, beta, mean, rstd, run_mean, run_var, nbt, z, training, act,
+                  eps=1e-5, momentum=0.1):
+    rows, C, _ = _rows(y)
+    w, wn = _ws(y.device, (rows // 32 + 2) * 2 * C)
+    lib.ea_batchnorm_fwd(rows, C, y.data_ptr(), gamma.data_ptr(), beta.data_ptr(), eps, momentum,
+                         int(training), mean.data_ptr(), rstd.data_ptr(), ptr(run_mean), ptr(run_var),
+                         ptr(nbt), act, z.data_ptr(), dt(z), w, wn, stream())
+
+
+def batchnorm_bwd(dz, y, mean, rstd, gamma, beta, act, dy, dgamma, dbeta):
+    rows, C, _ = _rows(y)
+    w, wn = _ws(y.device, (rows // 32 + 4) * 2 * C)
+    lib.ea_batchnorm_bwd(rows, C, dz.data_ptr(), dt(dz), y.data_ptr(), mean.data_ptr(), rstd.data_ptr(),
+                         gamma.data_ptr(), beta.data_ptr(), act, dy.data_ptr(), dgamma.data_ptr(),
+                         dbeta.data_ptr(), 1, w, wn, stream())
+
+
+# ----------------------------------------------------------------------------- elementwise
+def scale_dropout(x, y, scale=1.0, p=0.0, seed=0):
+    rows, cols, ldx = _rows(x)
+    _, _, ldy = _rows(y)
+    lib.ea_scale_dropout(rows, cols, x.data_ptr(), dt(x), ldx, y.data_ptr(), dt(y), ldy,
+                         float(scale), float(p), seed & 0xFFFFFFFFFFFFFFFF, stream())
+    return y
+
+
+def cast(x, dtype):
+    """Copy-convert (f32 <-> bf16) through ea_scale_dropout; returns x if already dtype."""
+    if x.dtype == dtype:
+        return x
+    y = torch.empty(x.shape, dtype=dtype, device=x.device)
+    scale_dropout(x.reshape(-1, x.shape[-1]), y.view(-1, y.shape[-1]))
+    return y
+
+
+def permute3(src, dst, A, Bd, Cd, accumulate=False):
+    lib.ea_permute3(A, Bd, Cd, src.data_ptr(), dt(src), dst.data_ptr(), dt(dst), int(accumulate), stream())

@@ -1,0 +1,152 @@
+"""Shared plumbing of the block-level autograd Functions.
+
+Each Function's forward launches the block's HIP kernels and keeps its intermediates;
+its backward launches the hand-written backward kernels and writes parameter gradients
+straight into the gradient arena (the Parameters are views, autograd never sees them).
+Only activations flow through autograd, so a whole training step is ~25 autograd nodes.
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+
+from .. import hip_ops as ops
+from .._lib import (ACT_NONE, ACT_RELU, ACT_SWISH, EPI_ACT, EPI_DACT, EPI_RESID, EPI_STORE,
+                    lib)
+
+__all__ = ["Bound", "rup", "empty", "ops", "lib", "EPI_ACT", "EPI_DACT", "EPI_RESID",
+           "EPI_STORE", "ACT_NONE", "ACT_RELU", "ACT_SWISH", "site_seed", "attn_fwd", "attn_bwd",
+           "LayerNormFn", "ln_fwd", "ln_bwd", "math", "F32"]
+
+F32 = torch.float32
+
+
+def rup(n, m=8):
+    return (n + m - 1) // m * m
+
+
+def empty(*shape, dtype=F32, device="cuda"):
+    if len(shape) == 1 and isinstance(shape[0], (tuple, list, torch.Size)):
+        shape = tuple(shape[0])
+    return torch.empty(shape, dtype=dtype, device=device)
+
+
+def site_seed(base: int, layer: int, site: int) -> int:
+    """Distinct dropout stream per (step, layer, site); forward and backward share it."""
+    z = (base * 0x9E3779B97F4A7C15 + layer * 0xBF58476D1CE4E5B9 + site * 0x94D049BB133111EB)
+    return z & 0xFFFFFFFFFFFFFFFF
+
+
+class Bound:
+    """Arena views of one module's parameters: w() in the compute dtype (the bf16 shadow
+    under AMP), f() the f32 master, g() the f32 gradient."""
+
+    def __init__(self, arena, prefix: str, cd):
+        self.arena = arena
+        self.prefix = prefix
+        self.cd = cd
+        self._cache = {}
+
+    def _v(self, which, names, shape):
+        key = (which, names, shape)
+        t = self._cache.get(key)
+        if t is None:
+            t = self.arena.view([self.prefix + n for n in names], shape, which)
+            self._cache[key] = t
+        return t
+
+    def w(self, *names, shape=None):
+        return self._v("shadow" if self.cd != F32 else "data", names, shape)
+
+    def f(self, *names, shape=None):
+        return self._v("data", names, shape)
+
+    def g(self, *names, shape=None):
+        return self._v("grad", names, shape)
+
+
+def _n(name, leaf):
+    return f"{name}.{leaf}" if name else leaf
+
+
+def ln_fwd(x2d, b: Bound, name: str, out_dtype):
+    N, d = x2d.shape
+    y = empty(N, d, dtype=out_dtype, device=x2d.device)
+    mu = empty(N, device=x2d.device)
+    rs = empty(N, device=x2d.device)
+    ops.layernorm_fwd(x2d, b.f(_n(name, "weight")), b.f(_n(name, "bias")), y, mu, rs)
+    return y, mu, rs
+
+
+def ln_bwd(dy, x2d, b: Bound, name: str, mu, rs, dx, accumulate=True):
+    ops.layernorm_bwd(dy, x2d, b.f(_n(name, "weight")), mu, rs, dx, b.g(_n(name, "weight")),
+                      b.g(_n(name, "bias")), accumulate=accumulate)
+
+
+class LayerNormFn(torch.autograd.Function):
+    """LayerNorm (eps 1e-12) on the f32 residual stream -> f32 (after_norm)."""
+
+    @staticmethod
+    def forward(ctx, x, module):
+        shp = x.shape
+        x2 = x.reshape(-1, shp[-1])
+        y, mu, rs = ln_fwd(x2, module._b, "", F32)
+        if torch.is_grad_enabled() or x.requires_grad:
+            ctx.save = (x2, mu, rs, module)
+        return y.view(shp)
+
+    @staticmethod
+    def backward(ctx, dy):
+        x2, mu, rs, module = ctx.save
+        dy2 = dy.reshape(-1, x2.shape[-1]).contiguous()
+        dx = torch.empty_like(x2)
+        ln_bwd(dy2, x2, module._b, "", mu, rs, dx, accumulate=False)
+        return dx.view(dy.shape), None
+
+
+# ----------------------------------------------------------------------------- attention core
+def attn_fwd(q, k, v, *, B, H, T1, T2, dk, ldq, ldk, ldv, klen, causal, scale, p, seed, cd,
+             bd=None, ldbd=0):
+    """softmax(scale*(q k^T [+ rel_shift(bd)]) masked) -> dropout -> @ v, all (b,h) at once.
+    q/k/v are row views (row strides ldq/ldk/ldv, head h at column h*dk).  Returns
+    O (B*T1, H*dk) cd, P (f32 softmax), Pd (dropout(P) in cd), ldT."""
+    dev = q.device
+    ldT = rup(T2, 8)
+    S = empty(B * H * T1 * ldT, device=dev)
+    ops.gemm(q, k, S, M=T1, N=T2, K=dk, a_kmajor=1, b_kmajor=1, lda=ldq, ldb=ldk, ldc=ldT,
+             batch=B, nh=H, sA=(T1 * ldq, dk), sB=(T2 * ldk, dk), sC=(H * T1 * ldT, T1 * ldT),
+             splitk=False)
+    Pd = empty(B * H * T1 * ldT, dtype=cd, device=dev)
+    lib.ea_attn_softmax_fwd(B, H, T1, T2, scale, S.data_ptr(), ldT,
+                            0 if bd is None else bd.data_ptr(), ldbd,
+                            0 if klen is None else klen.data_ptr(), int(causal), float(p),
+                            seed, S.data_ptr(), ldT, Pd.data_ptr(), ops.dt(Pd), ldT, ops.stream())
+    O = empty(B * T1, H * dk, dtype=cd, device=dev)
+    ops.gemm(Pd, v, O, M=T1, N=dk, K=T2, a_kmajor=1, b_kmajor=0, lda=ldT, ldb=ldv, ldc=H * dk,
+             batch=B, nh=H, sA=(H * T1 * ldT, T1 * ldT), sB=(T2 * ldv, dk), sC=(T1 * H * dk, dk),
+             splitk=False)
+    return O, S, Pd, ldT
+
+
+def attn_bwd(dO, q, k, v, P, Pd, ldT, *, B, H, T1, T2, dk, ldq, ldk, ldv, scale, p, seed, cd,
+             dq, lddq, dk_, lddk, dv, lddv, dbd=None, ldbd=0):
+    """Backward of attn_fwd: writes dq (scaled scores grad . k), dk_, dv; optionally the
+    rel-pos band gradient dbd [h][b][i][ldbd]."""
+    dev = dO.device
+    d = H * dk
+    dPd = empty(B * H * T1 * ldT, device=dev)
+    ops.gemm(dO, v, dPd, M=T1, N=T2, K=dk, a_kmajor=1, b_kmajor=1, lda=d, ldb=ldv, ldc=ldT,
+             batch=B, nh=H, sA=(T1 * d, dk), sB=(T2 * ldv, dk), sC=(H * T1 * ldT, T1 * ldT),
+             splitk=False)
+    dS = empty(B * H * T1 * ldT, dtype=cd, device=dev)
+    lib.ea_attn_softmax_bwd(B, H, T1, T2, scale, dPd.data_ptr(), ldT, P.data_ptr(), ldT, float(p),
+                            seed, dS.data_ptr(), ops.dt(dS), ldT,
+                            0 if dbd is None else dbd.data_ptr(), ldbd, ops.stream())
+    zs = (H * T1 * ldT, T1 * ldT)
+    ops.gemm(dS, k, dq, M=T1, N=dk, K=T2, a_kmajor=1, b_kmajor=0, lda=ldT, ldb=ldk, ldc=lddq,
+             batch=B, nh=H, sA=zs, sB=(T2 * ldk, dk), sC=(T1 * lddq, dk), splitk=False)
+    ops.gemm(dS, q, dk_, M=T2, N=dk, K=T1, a_kmajor=0, b_kmajor=0, lda=ldT, ldb=ldq, ldc=lddk,
+             batch=B, nh=H, sA=zs, sB=(T1 * ldq, dk), sC=(T2 * lddk, dk), splitk=False)
+    ops.gemm(Pd, dO, dv, M=T2, N=dk, K=T1, a_kmajor=0, b_kmajor=0, lda=ldT, ldb=d, ldc=lddv,
+             batch=B, nh=H, sA=zs, sB=(T1 * d, dk), sC=(T2 * lddv, dk), splitk=False)

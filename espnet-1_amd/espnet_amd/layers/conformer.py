@@ -1,0 +1,319 @@
+"""Conformer encoder block — espnet/nets/pytorch_backend/conformer/encoder_layer.py:79-179
+(normalize_before=True, concat_after=False, macaron FFN, rel-pos MHSA, conv module).
+
+Parameter holders keep the reference's attribute names, constructor order and torch
+default initialisation (so the same seed gives the same weights and the same state_dict
+keys); the computation is `ConformerBlockFn`: one autograd node per block running the
+block's HIP kernels forward and its hand-written backward.
+
+Data layout (channel-last, token-major): x (B*T, d) f32 residual stream; GEMM operands in
+the compute dtype cd (f32, or bf16 under AMP); the fused qkv (B*T, 3d) keeps heads as
+column blocks so attention reads q/k/v with strides, no transposes.
+"""
+from __future__ import annotations
+
+import torch
+from torch import nn
+
+from .common import (ACT_SWISH, EPI_ACT, EPI_DACT, EPI_RESID, EPI_STORE, F32, Bound, attn_bwd,
+                     attn_fwd, empty, lib, ln_bwd, ln_fwd, math, ops, rup, site_seed)
+
+
+# ----------------------------------------------------------------------------- holders
+class PositionwiseFeedForward(nn.Module):
+    """positionwise_feed_forward.py:12-32 (w_2(dropout(act(w_1 x))))."""
+
+    def __init__(self, idim, hidden_units, dropout_rate, activation="swish"):
+        super().__init__()
+        self.w_1 = nn.Linear(idim, hidden_units)
+        self.w_2 = nn.Linear(hidden_units, idim)
+        self.dropout_rate = dropout_rate
+        self.activation = activation
+
+
+class MultiHeadedAttention(nn.Module):
+    """transformer/attention.py:15-37 parameter set."""
+
+    def __init__(self, n_head, n_feat, dropout_rate):
+        super().__init__()
+        assert n_feat % n_head == 0
+        self.d_k = n_feat // n_head
+        self.h = n_head
+        self.linear_q = nn.Linear(n_feat, n_feat)
+        self.linear_k = nn.Linear(n_feat, n_feat)
+        self.linear_v = nn.Linear(n_feat, n_feat)
+        self.linear_out = nn.Linear(n_feat, n_feat)
+        self.dropout_rate = dropout_rate
+
+
+class RelPositionMultiHeadedAttention(MultiHeadedAttention):
+    """transformer/attention.py:209-235 parameter set (linear_pos, pos_bias_u/v)."""
+
+    def __init__(self, n_head, n_feat, dropout_rate, zero_triu=False):
+        super().__init__(n_head, n_feat, dropout_rate)
+        if zero_triu:
+            raise NotImplementedError("zero_triu=True is not on the ASR hot path")
+        self.linear_pos = nn.Linear(n_feat, n_feat, bias=False)
+        self.pos_bias_u = nn.Parameter(torch.Tensor(self.h, self.d_k))
+        self.pos_bias_v = nn.Parameter(torch.Tensor(self.h, self.d_k))
+        torch.nn.init.xavier_uniform_(self.pos_bias_u)
+        torch.nn.init.xavier_uniform_(self.pos_bias_v)
+
+
+class ConvolutionModule(nn.Module):
+    """conformer/convolution.py:13-54 parameter set."""
+
+    def __init__(self, channels, kernel_size, activation="swish", bias=True):
+        super().__init__()
+        assert (kernel_size - 1) % 2 == 0
+        self.pointwise_conv1 = nn.Conv1d(channels, 2 * channels, 1, 1, 0, bias=bias)
+        self.depthwise_conv = nn.Conv1d(channels, channels, kernel_size, 1, (kernel_size - 1) // 2,
+                                        groups=channels, bias=bias)
+        self.norm = nn.BatchNorm1d(channels)
+        self.pointwise_conv2 = nn.Conv1d(channels, channels, 1, 1, 0, bias=bias)
+        self.kernel_size = kernel_size
+
+
+def LayerNorm(n):  # transformer/layer_norm.py:12 (eps=1e-12 applied by the kernels)
+    return nn.LayerNorm(n, eps=1e-12)
+
+
+class EncoderLayer(nn.Module):
+    """conformer/encoder_layer.py:43-77 parameter set + HIP forward."""
+
+    def __init__(self, size, self_attn, feed_forward, feed_forward_macaron, conv_module,
+                 dropout_rate, normalize_before=True, concat_after=False, stochastic_depth_rate=0.0):
+        super().__init__()
+        if not normalize_before or concat_after or stochastic_depth_rate > 0:
+            raise NotImplementedError("only normalize_before=True, concat_after=False, "
+                                      "stochastic_depth_rate=0 (the ASR recipes) are implemented")
+        if conv_module is None:
+            raise NotImplementedError("use_cnn_module=False is not on the hot path")
+        self.self_attn = self_attn
+        self.feed_forward = feed_forward
+        self.feed_forward_macaron = feed_forward_macaron
+        self.conv_module = conv_module
+        self.norm_ff = LayerNorm(size)
+        self.norm_mha = LayerNorm(size)
+        if feed_forward_macaron is not None:
+            self.norm_ff_macaron = LayerNorm(size)
+            self.ff_scale = 0.5
+        else:
+            self.ff_scale = 1.0
+        self.norm_conv = LayerNorm(size)
+        self.norm_final = LayerNorm(size)
+        self.size = size
+        self.dropout_rate = dropout_rate
+        self.layer_idx = 0
+        self._b = None
+
+    def bind(self, arena, prefix, cd):
+        self._b = Bound(arena, prefix, cd)
+
+    @staticmethod
+    def arena_groups(prefix):
+        a = prefix + "self_attn."
+        return [[a + "linear_q.weight", a + "linear_k.weight", a + "linear_v.weight"],
+                [a + "linear_q.bias", a + "linear_k.bias", a + "linear_v.bias"]]
+
+    def forward(self, x, pos_emb, olens, seed):
+        return ConformerBlockFn.apply(x, pos_emb, olens, self, seed, self.training)
+
+
+# ----------------------------------------------------------------------------- forward pieces
+def _ffn_fwd(L, b, x_in, pre, ln_name, p, seed_in, seed_out):
+    cd = b.cd
+    N, d = x_in.shape
+    Fh = L.feed_forward.w_1.out_features
+    xn, mu, rs = ln_fwd(x_in, b, ln_name, cd)
+    h = empty(N, Fh, dtype=cd, device=x_in.device)
+    a = empty(N, Fh, dtype=cd, device=x_in.device)
+    ops.linear(xn, b.w(pre + ".w_1.weight"), a,
+               epi=ops.make_epi(EPI_ACT, bias=b.f(pre + ".w_1.bias"), act=ACT_SWISH, aux=h,
+                                drop_p=p, seed=seed_in))
+    x_out = empty(N, d, device=x_in.device)
+    ops.linear(a, b.w(pre + ".w_2.weight"), x_out,
+               epi=ops.make_epi(EPI_RESID, bias=b.f(pre + ".w_2.bias"), resid=x_in,
+                                rscale=L.ff_scale, drop_p=p, seed=seed_out))
+    return x_out, (xn, mu, rs, h, a)
+
+
+def _ffn_bwd(L, b, dx, x_in, saved, pre, ln_name, p, seed_in, seed_out):
+    """dx: f32 (N,d) grad of the sub-block output; updated in place to grad of x_in."""
+    cd = b.cd
+    xn, mu, rs, h, a = saved
+    N, d = dx.shape
+    dv = empty(N, d, dtype=cd, device=dx.device)
+    ops.scale_dropout(dx, dv, scale=L.ff_scale, p=p, seed=seed_out)
+    ops.colsum(dv, b.g(pre + ".w_2.bias"))
+    ops.linear_dw(dv, a, b.g(pre + ".w_2.weight"), accumulate=True)
+    dh = empty(*h.shape, dtype=cd, device=dx.device)
+    ops.linear_dx(dv, b.w(pre + ".w_2.weight"), dh,
+                  epi=ops.make_epi(EPI_DACT, act=ACT_SWISH, aux=h, drop_p=p, seed=seed_in))
+    ops.colsum(dh, b.g(pre + ".w_1.bias"))
+    ops.linear_dw(dh, xn, b.g(pre + ".w_1.weight"), accumulate=True)
+    dxn = empty(N, d, dtype=cd, device=dx.device)
+    ops.linear_dx(dh, b.w(pre + ".w_1.weight"), dxn)
+    ln_bwd(dxn, x_in, b, ln_name, mu, rs, dx, accumulate=True)
+
+
+class ConformerBlockFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, pos, olens, L: EncoderLayer, seed, training):
+        b = L._b
+        cd = b.cd
+        B, T, d = x.shape
+        N = B * T
+        dev = x.device
+        H = L.self_attn.h
+        dk = d // H
+        P2 = 2 * T - 1
+        p = L.dropout_rate if training else 0.0
+        pa = L.self_attn.dropout_rate if training else 0.0
+        li = L.layer_idx
+        sd = lambda s: site_seed(seed, li, s)  # noqa: E731
+        x0 = x.reshape(N, d)
+        # ---- macaron FFN  (encoder_layer.py:115-123)
+        x1, s_ff1 = _ffn_fwd(L, b, x0, "feed_forward_macaron", "norm_ff_macaron", p, sd(1), sd(2))
+        # ---- rel-pos MHSA (encoder_layer.py:126-149, attention.py:262-305)
+        xn2, mu2, rs2 = ln_fwd(x1, b, "norm_mha", cd)
+        A = "self_attn."
+        qkv = empty(N, 3 * d, dtype=cd, device=dev)
+        ops.linear(xn2, b.w(A + "linear_q.weight", A + "linear_k.weight", A + "linear_v.weight",
+                            shape=(3 * d, d)), qkv,
+                   epi=ops.make_epi(bias=b.f(A + "linear_q.bias", A + "linear_k.bias",
+                                             A + "linear_v.bias", shape=(3 * d,))))
+        pp = empty(P2, d, dtype=cd, device=dev)
+        ops.linear(pos, b.w(A + "linear_pos.weight"), pp)
+        qu = empty(N, d, dtype=cd, device=dev)
+        qv = empty(N, d, dtype=cd, device=dev)
+        lib.ea_add_pos_bias(N, H, dk, qkv.data_ptr(), 3 * d, b.f(A + "pos_bias_u").data_ptr(),
+                            b.f(A + "pos_bias_v").data_ptr(), qu.data_ptr(), qv.data_ptr(),
+                            ops.dt(qu), ops.stream())
+        ldbd = rup(P2, 8)
+        bd = empty(H * B * T * ldbd, device=dev)
+        ops.gemm(qv, pp, bd, M=T, N=P2, K=dk, a_kmajor=1, b_kmajor=1, lda=d, ldb=d, ldc=ldbd,
+                 batch=B, nh=H, sA=(T * d, dk), sB=(0, dk), sC=(T * ldbd, B * T * ldbd), splitk=False)
+        scale = 1.0 / math.sqrt(dk)
+        O, P, Pd, ldT = attn_fwd(qu, qkv[:, d:], qkv[:, 2 * d:], B=B, H=H, T1=T, T2=T, dk=dk,
+                                 ldq=d, ldk=3 * d, ldv=3 * d, klen=olens, causal=False, scale=scale,
+                                 p=pa, seed=sd(3), cd=cd, bd=bd, ldbd=ldbd)
+        del bd
+        x2 = empty(N, d, device=dev)
+        ops.linear(O, b.w(A + "linear_out.weight"), x2,
+                   epi=ops.make_epi(EPI_RESID, bias=b.f(A + "linear_out.bias"), resid=x1,
+                                    drop_p=p, seed=sd(4)))
+        # ---- conv module (encoder_layer.py:152-158, convolution.py:56-79)
+        C = "conv_module."
+        K = L.conv_module.kernel_size
+        xn3, mu3, rs3 = ln_fwd(x2, b, "norm_conv", cd)
+        g2 = empty(N, 2 * d, dtype=cd, device=dev)
+        ops.linear(xn3, b.w(C + "pointwise_conv1.weight", shape=(2 * d, d)), g2,
+                   epi=ops.make_epi(bias=b.f(C + "pointwise_conv1.bias")))
+        glu = empty(N, d, device=dev)
+        lib.ea_glu_fwd(N, d, g2.data_ptr(), ops.dt(g2), glu.data_ptr(), 0, ops.stream())
+        y = empty(N, d, device=dev)
+        lib.ea_dwconv_fwd(B, T, d, K, glu.data_ptr(), b.f(C + "depthwise_conv.weight").data_ptr(),
+                          b.f(C + "depthwise_conv.bias").data_ptr(), y.data_ptr(), ops.stream())
+        z = empty(N, d, dtype=cd, device=dev)
+        bn_mean = empty(d, device=dev)
+        bn_rstd = empty(d, device=dev)
+        bn = L.conv_module.norm
+        ops.batchnorm_fwd(y, b.f(C + "norm.weight"), b.f(C + "norm.bias"), bn_mean, bn_rstd,
+                          bn.running_mean, bn.running_var, bn.num_batches_tracked, z,
+                          training, ACT_SWISH, eps=bn.eps, momentum=bn.momentum)
+        x3 = empty(N, d, device=dev)
+        ops.linear(z, b.w(C + "pointwise_conv2.weight", shape=(d, d)), x3,
+                   epi=ops.make_epi(EPI_RESID, bias=b.f(C + "pointwise_conv2.bias"), resid=x2,
+                                    drop_p=p, seed=sd(5)))
+        # ---- FFN (encoder_layer.py:161-168) + norm_final (:170-171)
+        x4, s_ff2 = _ffn_fwd(L, b, x3, "feed_forward", "norm_ff", p, sd(6), sd(7))
+        out, mu5, rs5 = ln_fwd(x4, b, "norm_final", F32)
+        ctx.L = L
+        ctx.meta = (B, T, d, H, dk, p, pa, seed, scale, ldT)
+        ctx.save = (x0, x1, x2, x3, x4, s_ff1, (xn2, mu2, rs2, qkv, pp, qu, qv, O, P, Pd),
+                    (xn3, mu3, rs3, g2, glu, y, z, bn_mean, bn_rstd), s_ff2, (mu5, rs5), pos, olens)
+        return out.view(B, T, d)
+
+    @staticmethod
+    def backward(ctx, dout):
+        L = ctx.L
+        b = L._b
+        cd = b.cd
+        B, T, d, H, dk, p, pa, seed, scale, ldT = ctx.meta
+        (x0, x1, x2, x3, x4, s_ff1, s_att, s_conv, s_ff2, (mu5, rs5), pos, olens) = ctx.save
+        ctx.save = None
+        li = L.layer_idx
+        sd = lambda s: site_seed(seed, li, s)  # noqa: E731
+        N = B * T
+        dev = dout.device
+        P2 = 2 * T - 1
+        dx = empty(N, d, device=dev)
+        ln_bwd(dout.reshape(N, d).contiguous(), x4, b, "norm_final", mu5, rs5, dx, accumulate=False)
+        # ---- FFN
+        _ffn_bwd(L, b, dx, x3, s_ff2, "feed_forward", "norm_ff", p, sd(6), sd(7))
+        # ---- conv module
+        C = "conv_module."
+        K = L.conv_module.kernel_size
+        xn3, mu3, rs3, g2, glu, y, z, bn_mean, bn_rstd = s_conv
+        dv = empty(N, d, dtype=cd, device=dev)
+        ops.scale_dropout(dx, dv, p=p, seed=sd(5))
+        ops.colsum(dv, b.g(C + "pointwise_conv2.bias"))
+        ops.linear_dw(dv, z, b.g(C + "pointwise_conv2.weight", shape=(d, d)), accumulate=True)
+        dz = empty(N, d, dtype=cd, device=dev)
+        ops.linear_dx(dv, b.w(C + "pointwise_conv2.weight", shape=(d, d)), dz)
+        dy = empty(N, d, device=dev)
+        ops.batchnorm_bwd(dz, y, bn_mean, bn_rstd, b.f(C + "norm.weight"), b.f(C + "norm.bias"),
+                          ACT_SWISH, dy, b.g(C + "norm.weight"), b.g(C + "norm.bias"))
+        dglu = empty(N, d, device=dev)
+        w, wn = ops._ws(dev, B * ((T + 31) // 32) * d * K + 1024)
+        lib.ea_dwconv_bwd(B, T, d, K, glu.data_ptr(), b.f(C + "depthwise_conv.weight").data_ptr(),
+                          dy.data_ptr(), dglu.data_ptr(), b.g(C + "depthwise_conv.weight").data_ptr(),
+                          b.g(C + "depthwise_conv.bias").data_ptr(), 1, w, wn, ops.stream())
+        dg2 = empty(N, 2 * d, dtype=cd, device=dev)
+        lib.ea_glu_bwd(N, d, g2.data_ptr(), ops.dt(g2), dglu.data_ptr(), dg2.data_ptr(), ops.stream())
+        ops.colsum(dg2, b.g(C + "pointwise_conv1.bias"))
+        ops.linear_dw(dg2, xn3, b.g(C + "pointwise_conv1.weight", shape=(2 * d, d)), accumulate=True)
+        dxn3 = empty(N, d, dtype=cd, device=dev)
+        ops.linear_dx(dg2, b.w(C + "pointwise_conv1.weight", shape=(2 * d, d)), dxn3)
+        ln_bwd(dxn3, x2, b, "norm_conv", mu3, rs3, dx, accumulate=True)
+        # ---- rel-pos MHSA
+        A = "self_attn."
+        xn2, mu2, rs2, qkv, pp, qu, qv, O, P, Pd = s_att
+        dv = empty(N, d, dtype=cd, device=dev)
+        ops.scale_dropout(dx, dv, p=p, seed=sd(4))
+        ops.colsum(dv, b.g(A + "linear_out.bias"))
+        ops.linear_dw(dv, O, b.g(A + "linear_out.weight"), accumulate=True)
+        dO = empty(N, d, dtype=cd, device=dev)
+        ops.linear_dx(dv, b.w(A + "linear_out.weight"), dO)
+        dqkv = empty(N, 3 * d, dtype=cd, device=dev)
+        ldbd = rup(P2, 8)
+        dbd = empty(H * B * T * ldbd, dtype=cd, device=dev)
+        attn_bwd(dO, qu, qkv[:, d:], qkv[:, 2 * d:], P, Pd, ldT, B=B, H=H, T1=T, T2=T, dk=dk,
+                 ldq=d, ldk=3 * d, ldv=3 * d, scale=scale, p=pa, seed=sd(3), cd=cd,
+                 dq=dqkv, lddq=3 * d, dk_=dqkv[:, d:], lddk=3 * d, dv=dqkv[:, 2 * d:], lddv=3 * d,
+                 dbd=dbd, ldbd=ldbd)
+        # q_u = q + u: du = sum dq_u ; q_v = q + v path: dq_v = dBD . p_h, dv_bias = sum dq_v
+        dqv = empty(N, d, dtype=cd, device=dev)
+        ops.gemm(dbd, pp, dqv, M=T, N=dk, K=P2, a_kmajor=1, b_kmajor=0, lda=ldbd, ldb=d, ldc=d,
+                 batch=B, nh=H, sA=(T * ldbd, B * T * ldbd), sB=(0, dk), sC=(T * d, dk), splitk=False)
+        ops.colsum(dqkv[:, :d], b.g(A + "pos_bias_u", shape=(d,)))
+        ops.colsum(dqv, b.g(A + "pos_bias_v", shape=(d,)))
+        lib.ea_add_2d(N, d, dqv.data_ptr(), ops.dt(dqv), d, dqkv.data_ptr(), ops.dt(dqkv), 3 * d, 1.0,
+                      ops.stream())
+        # linear_pos: dp[h] = sum_b dBD[h][b]^T qv[b, :, h]  (K = B*T), dWpos = dp^T pos
+        dpp = empty(P2, d, dtype=cd, device=dev)
+        ops.gemm(dbd, qv, dpp, M=P2, N=dk, K=B * T, a_kmajor=0, b_kmajor=0, lda=ldbd, ldb=d, ldc=d,
+                 batch=1, nh=H, sA=(0, B * T * ldbd), sB=(0, dk), sC=(0, dk), splitk=False)
+        del dbd
+        ops.linear_dw(dpp, pos, b.g(A + "linear_pos.weight"), accumulate=True)
+        qkv_w = b.w(A + "linear_q.weight", A + "linear_k.weight", A + "linear_v.weight", shape=(3 * d, d))
+        ops.colsum(dqkv, b.g(A + "linear_q.bias", A + "linear_k.bias", A + "linear_v.bias", shape=(3 * d,)))
+        ops.linear_dw(dqkv, xn2, b.g(A + "linear_q.weight", A + "linear_k.weight", A + "linear_v.weight",
+                                      shape=(3 * d, d)), accumulate=True)
+        dxn2 = empty(N, d, dtype=cd, device=dev)
+        ops.linear_dx(dqkv, qkv_w, dxn2)
+        ln_bwd(dxn2, x1, b, "norm_mha", mu2, rs2, dx, accumulate=True)
+        # ---- macaron FFN
+        _ffn_bwd(L, b, dx, x0, s_ff1, "feed_forward_macaron", "norm_ff_macaron", p, sd(1), sd(2))
+        return dx.view(B, T, d), None, None, None, None, None

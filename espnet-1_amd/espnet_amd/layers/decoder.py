@@ -1,0 +1,257 @@
+"""TransformerDecoder training forward — espnet2/asr/decoder/transformer_decoder.py:92-145
+with DecoderLayer (transformer/decoder_layer.py:63-134, normalize_before=True,
+concat_after=False), Embedding + PositionalEncoding (embedding.py:81-92) and the output
+Linear — as ONE autograd node (`DecoderFn`).
+
+MI355X layout choice: the encoder memory is projected to the cross-attention keys and
+values of ALL decoder layers by a single GEMM (N = 2*d*num_blocks = 6144 columns for C3)
+— the six layers' src_attn.linear_k/linear_v weights are adjacent in the parameter arena —
+and its backward is likewise one dW GEMM and one dX GEMM with K = 6144.
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+from torch import nn
+
+from .common import (ACT_RELU, EPI_ACT, EPI_DACT, EPI_RESID, EPI_STORE, F32, Bound, attn_bwd,
+                     attn_fwd, empty, lib, ln_bwd, ln_fwd, ops, site_seed)
+from .conformer import LayerNorm, MultiHeadedAttention, PositionwiseFeedForward
+
+
+def sinusoid_table(n, d):
+    """PositionalEncoding.extend_pe (embedding.py:60-79), a construction-time constant."""
+    pe = torch.zeros(n, d)
+    pos = torch.arange(0, n, dtype=torch.float32).unsqueeze(1)
+    div = torch.exp(torch.arange(0, d, 2, dtype=torch.float32) * -(math.log(10000.0) / d))
+    pe[:, 0::2] = torch.sin(pos * div)
+    pe[:, 1::2] = torch.cos(pos * div)
+    return pe
+
+
+class PositionalEncoding(nn.Module):
+    def __init__(self, d_model, dropout_rate, max_len=5000):
+        super().__init__()
+        self.d_model = d_model
+        self.xscale = math.sqrt(d_model)
+        self.dropout_rate = dropout_rate
+        self.max_len = max_len
+        self._pe = None
+
+    def table(self, L, device):
+        if self._pe is None or self._pe.shape[0] < L or self._pe.device != device:
+            self._pe = sinusoid_table(max(self.max_len, L), self.d_model).to(device)
+        return self._pe
+
+
+class DecoderLayer(nn.Module):
+    """transformer/decoder_layer.py:22-61 parameter set."""
+
+    def __init__(self, size, self_attn, src_attn, feed_forward, dropout_rate,
+                 normalize_before=True, concat_after=False):
+        super().__init__()
+        if not normalize_before or concat_after:
+            raise NotImplementedError("only normalize_before=True, concat_after=False")
+        self.size = size
+        self.self_attn = self_attn
+        self.src_attn = src_attn
+        self.feed_forward = feed_forward
+        self.norm1 = LayerNorm(size)
+        self.norm2 = LayerNorm(size)
+        self.norm3 = LayerNorm(size)
+        self.dropout_rate = dropout_rate
+
+
+def decoder_arena_groups(prefix, num_blocks):
+    g = []
+    for i in range(num_blocks):
+        a = f"{prefix}decoders.{i}.self_attn."
+        g.append([a + "linear_q.weight", a + "linear_k.weight", a + "linear_v.weight"])
+        g.append([a + "linear_q.bias", a + "linear_k.bias", a + "linear_v.bias"])
+    kw, kb = [], []
+    for i in range(num_blocks):
+        a = f"{prefix}decoders.{i}.src_attn."
+        kw += [a + "linear_k.weight", a + "linear_v.weight"]
+        kb += [a + "linear_k.bias", a + "linear_v.bias"]
+    return g + [kw, kb]
+
+
+def _kv_names(nb):
+    w, b = [], []
+    for i in range(nb):
+        a = f"decoders.{i}.src_attn."
+        w += [a + "linear_k.weight", a + "linear_v.weight"]
+        b += [a + "linear_k.bias", a + "linear_v.bias"]
+    return w, b
+
+
+class DecoderFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, memory, hlens, ys_in, ys_in_lens, dec, seed, training):
+        b = dec._b
+        cd = b.cd
+        B, Tm, d = memory.shape
+        L = ys_in.shape[1]
+        N, Nm = B * L, B * Tm
+        nb = len(dec.decoders)
+        H = dec.decoders[0].self_attn.h
+        dk = d // H
+        V = dec.output_layer.out_features
+        dev = memory.device
+        p = dec.dropout_rate if training else 0.0
+        p_sa = dec.self_attention_dropout_rate if training else 0.0
+        p_src = dec.src_attention_dropout_rate if training else 0.0
+        p_pos = dec.embed[1].dropout_rate if training else 0.0
+        sd = lambda l, s: site_seed(seed, 100 + l, s)  # noqa: E731
+        scale = 1.0 / math.sqrt(dk)
+        mem = ops.cast(memory.reshape(Nm, d), cd)
+        kvw, kvb = _kv_names(nb)
+        kv = empty(Nm, 2 * d * nb, dtype=cd, device=dev)
+        ops.linear(mem, b.w(*kvw, shape=(2 * d * nb, d)), kv,
+                   epi=ops.make_epi(bias=b.f(*kvb, shape=(2 * d * nb,))))
+        pe = dec.embed[1]
+        x = empty(N, d, device=dev)
+        lib.ea_embed_fwd(N, d, L, ys_in.data_ptr(), b.f("embed.0.weight").data_ptr(), pe.xscale,
+                         pe.table(L, dev).data_ptr(), p_pos, sd(0, 0), x.data_ptr(), ops.stream())
+        saved = []
+        ldkv = 2 * d * nb
+        for l in range(nb):
+            n = f"decoders.{l}."
+            sa, xa = n + "self_attn.", n + "src_attn."
+            # self-attention (causal & target padding mask, transformer_decoder.py:117-122)
+            xn1, mu1, rs1 = ln_fwd(x, b, n + "norm1", cd)
+            qkv = empty(N, 3 * d, dtype=cd, device=dev)
+            ops.linear(xn1, b.w(sa + "linear_q.weight", sa + "linear_k.weight", sa + "linear_v.weight",
+                                shape=(3 * d, d)), qkv,
+                       epi=ops.make_epi(bias=b.f(sa + "linear_q.bias", sa + "linear_k.bias",
+                                                 sa + "linear_v.bias", shape=(3 * d,))))
+            O1, P1, Pd1, ldT1 = attn_fwd(qkv, qkv[:, d:], qkv[:, 2 * d:], B=B, H=H, T1=L, T2=L, dk=dk,
+                                         ldq=3 * d, ldk=3 * d, ldv=3 * d, klen=ys_in_lens, causal=True,
+                                         scale=scale, p=p_sa, seed=sd(l, 1), cd=cd)
+            x1 = empty(N, d, device=dev)
+            ops.linear(O1, b.w(sa + "linear_out.weight"), x1,
+                       epi=ops.make_epi(EPI_RESID, bias=b.f(sa + "linear_out.bias"), resid=x,
+                                        drop_p=p, seed=sd(l, 2)))
+            # source attention over the encoder memory (memory_mask, :125-127)
+            xn2, mu2, rs2 = ln_fwd(x1, b, n + "norm2", cd)
+            q2 = empty(N, d, dtype=cd, device=dev)
+            ops.linear(xn2, b.w(xa + "linear_q.weight"), q2, epi=ops.make_epi(bias=b.f(xa + "linear_q.bias")))
+            k2 = kv[:, 2 * d * l:]
+            v2 = kv[:, 2 * d * l + d:]
+            O2, P2, Pd2, ldT2 = attn_fwd(q2, k2, v2, B=B, H=H, T1=L, T2=Tm, dk=dk, ldq=d, ldk=ldkv,
+                                         ldv=ldkv, klen=hlens, causal=False, scale=scale, p=p_src,
+                                         seed=sd(l, 3), cd=cd)
+            x2 = empty(N, d, device=dev)
+            ops.linear(O2, b.w(xa + "linear_out.weight"), x2,
+                       epi=ops.make_epi(EPI_RESID, bias=b.f(xa + "linear_out.bias"), resid=x1,
+                                        drop_p=p, seed=sd(l, 4)))
+            # feed-forward (ReLU)
+            xn3, mu3, rs3 = ln_fwd(x2, b, n + "norm3", cd)
+            Fh = dec.decoders[l].feed_forward.w_1.out_features
+            h = empty(N, Fh, dtype=cd, device=dev)
+            a = empty(N, Fh, dtype=cd, device=dev)
+            ff = n + "feed_forward."
+            ops.linear(xn3, b.w(ff + "w_1.weight"), a,
+                       epi=ops.make_epi(EPI_ACT, bias=b.f(ff + "w_1.bias"), act=ACT_RELU, aux=h,
+                                        drop_p=p, seed=sd(l, 5)))
+            x3 = empty(N, d, device=dev)
+            ops.linear(a, b.w(ff + "w_2.weight"), x3,
+                       epi=ops.make_epi(EPI_RESID, bias=b.f(ff + "w_2.bias"), resid=x2,
+                                        drop_p=p, seed=sd(l, 6)))
+            saved.append((x, x1, x2, (xn1, mu1, rs1, qkv, O1, P1, Pd1, ldT1),
+                          (xn2, mu2, rs2, q2, O2, P2, Pd2, ldT2), (xn3, mu3, rs3, h, a)))
+            x = x3
+        xf, muf, rsf = ln_fwd(x, b, "after_norm", cd)
+        logits = empty(N, V, device=dev)
+        ops.linear(xf, b.w("output_layer.weight"), logits,
+                   epi=ops.make_epi(bias=b.f("output_layer.bias")))
+        ctx.dec = dec
+        ctx.meta = (B, Tm, L, d, H, dk, nb, p, p_sa, p_src, p_pos, seed, scale)
+        ctx.save = (mem, kv, ys_in, saved, x, xf, muf, rsf)
+        return logits.view(B, L, V)
+
+    @staticmethod
+    def backward(ctx, dlogits):
+        dec = ctx.dec
+        b = dec._b
+        cd = b.cd
+        B, Tm, L, d, H, dk, nb, p, p_sa, p_src, p_pos, seed, scale = ctx.meta
+        mem, kv, ys_in, saved, xlast, xf, muf, rsf = ctx.save
+        ctx.save = None
+        sd = lambda l, s: site_seed(seed, 100 + l, s)  # noqa: E731
+        N, Nm = B * L, B * Tm
+        V = dlogits.shape[-1]
+        dev = dlogits.device
+        dlog = ops.cast(dlogits.reshape(N, V).contiguous(), cd)
+        ops.colsum(dlog, b.g("output_layer.bias"))
+        ops.linear_dw(dlog, xf, b.g("output_layer.weight"), accumulate=True)
+        dxf = empty(N, d, dtype=cd, device=dev)
+        ops.linear_dx(dlog, b.w("output_layer.weight"), dxf)
+        dx = empty(N, d, device=dev)
+        ln_bwd(dxf, xlast, b, "after_norm", muf, rsf, dx, accumulate=False)
+        ldkv = 2 * d * nb
+        dkv = empty(Nm, ldkv, dtype=cd, device=dev)
+        for l in reversed(range(nb)):
+            n = f"decoders.{l}."
+            sa, xa, ff = n + "self_attn.", n + "src_attn.", n + "feed_forward."
+            x0, x1, x2, s1, s2, s3 = saved[l]
+            # feed-forward
+            xn3, mu3, rs3, h, a = s3
+            dv = empty(N, d, dtype=cd, device=dev)
+            ops.scale_dropout(dx, dv, p=p, seed=sd(l, 6))
+            ops.colsum(dv, b.g(ff + "w_2.bias"))
+            ops.linear_dw(dv, a, b.g(ff + "w_2.weight"), accumulate=True)
+            dh = empty(*h.shape, dtype=cd, device=dev)
+            ops.linear_dx(dv, b.w(ff + "w_2.weight"), dh,
+                          epi=ops.make_epi(EPI_DACT, act=ACT_RELU, aux=h, drop_p=p, seed=sd(l, 5)))
+            ops.colsum(dh, b.g(ff + "w_1.bias"))
+            ops.linear_dw(dh, xn3, b.g(ff + "w_1.weight"), accumulate=True)
+            dxn = empty(N, d, dtype=cd, device=dev)
+            ops.linear_dx(dh, b.w(ff + "w_1.weight"), dxn)
+            ln_bwd(dxn, x2, b, n + "norm3", mu3, rs3, dx, accumulate=True)
+            # source attention
+            xn2, mu2, rs2, q2, O2, P2, Pd2, ldT2 = s2
+            dv = empty(N, d, dtype=cd, device=dev)
+            ops.scale_dropout(dx, dv, p=p, seed=sd(l, 4))
+            ops.colsum(dv, b.g(xa + "linear_out.bias"))
+            ops.linear_dw(dv, O2, b.g(xa + "linear_out.weight"), accumulate=True)
+            dO = empty(N, d, dtype=cd, device=dev)
+            ops.linear_dx(dv, b.w(xa + "linear_out.weight"), dO)
+            dq = empty(N, d, dtype=cd, device=dev)
+            attn_bwd(dO, q2, kv[:, 2 * d * l:], kv[:, 2 * d * l + d:], P2, Pd2, ldT2, B=B, H=H, T1=L,
+                     T2=Tm, dk=dk, ldq=d, ldk=ldkv, ldv=ldkv, scale=scale, p=p_src, seed=sd(l, 3), cd=cd,
+                     dq=dq, lddq=d, dk_=dkv[:, 2 * d * l:], lddk=ldkv, dv=dkv[:, 2 * d * l + d:], lddv=ldkv)
+            ops.colsum(dq, b.g(xa + "linear_q.bias"))
+            ops.linear_dw(dq, xn2, b.g(xa + "linear_q.weight"), accumulate=True)
+            dxn = empty(N, d, dtype=cd, device=dev)
+            ops.linear_dx(dq, b.w(xa + "linear_q.weight"), dxn)
+            ln_bwd(dxn, x1, b, n + "norm2", mu2, rs2, dx, accumulate=True)
+            # self attention
+            xn1, mu1, rs1, qkv, O1, P1, Pd1, ldT1 = s1
+            dv = empty(N, d, dtype=cd, device=dev)
+            ops.scale_dropout(dx, dv, p=p, seed=sd(l, 2))
+            ops.colsum(dv, b.g(sa + "linear_out.bias"))
+            ops.linear_dw(dv, O1, b.g(sa + "linear_out.weight"), accumulate=True)
+            dO = empty(N, d, dtype=cd, device=dev)
+            ops.linear_dx(dv, b.w(sa + "linear_out.weight"), dO)
+            dqkv = empty(N, 3 * d, dtype=cd, device=dev)
+            attn_bwd(dO, qkv, qkv[:, d:], qkv[:, 2 * d:], P1, Pd1, ldT1, B=B, H=H, T1=L, T2=L, dk=dk,
+                     ldq=3 * d, ldk=3 * d, ldv=3 * d, scale=scale, p=p_sa, seed=sd(l, 1), cd=cd,
+                     dq=dqkv, lddq=3 * d, dk_=dqkv[:, d:], lddk=3 * d, dv=dqkv[:, 2 * d:], lddv=3 * d)
+            wn = (sa + "linear_q.weight", sa + "linear_k.weight", sa + "linear_v.weight")
+            bn = (sa + "linear_q.bias", sa + "linear_k.bias", sa + "linear_v.bias")
+            ops.colsum(dqkv, b.g(*bn, shape=(3 * d,)))
+            ops.linear_dw(dqkv, xn1, b.g(*wn, shape=(3 * d, d)), accumulate=True)
+            dxn = empty(N, d, dtype=cd, device=dev)
+            ops.linear_dx(dqkv, b.w(*wn, shape=(3 * d, d)), dxn)
+            ln_bwd(dxn, x0, b, n + "norm1", mu1, rs1, dx, accumulate=True)
+        pe = dec.embed[1]
+        lib.ea_embed_bwd(N, d, ys_in.data_ptr(), dx.data_ptr(), pe.xscale, p_pos, sd(0, 0),
+                         b.g("embed.0.weight").data_ptr(), ops.stream())
+        kvw, kvb = _kv_names(nb)
+        ops.colsum(dkv, b.g(*kvb, shape=(ldkv,)))
+        ops.linear_dw(dkv, mem, b.g(*kvw, shape=(ldkv, d)), accumulate=True)
+        dmem = empty(Nm, d, device=dev)
+        ops.linear_dx(dkv, b.w(*kvw, shape=(ldkv, d)), dmem)
+        return dmem.view(B, Tm, d), None, None, None, None, None, None

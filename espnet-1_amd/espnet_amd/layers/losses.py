@@ -1,0 +1,125 @@
+"""Loss nodes: CTC head (ctc.py:72-97), LabelSmoothingLoss + th_accuracy
+(label_smoothing_loss.py:41-63, nets_utils.py:304-324) and the hybrid combination
+(espnet_model.py:320-325).  Gradient scales are read from device memory (the autograd
+grad_output), so nothing here synchronises with the host."""
+from __future__ import annotations
+
+import torch
+
+from .common import F32, empty, lib, ops
+
+
+def _g(t):
+    t = t.contiguous()
+    if t.dtype != F32:
+        raise RuntimeError("loss gradients must be float32")
+    return t
+
+
+class CTCFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, hs, hlens, ys, ylens, ctc, Lmax):
+        b = ctc._b
+        cd = b.cd
+        B, T, d = hs.shape
+        V = ctc.ctc_lo.out_features
+        dev = hs.device
+        N = B * T
+        h = empty(N, d, dtype=cd, device=dev)
+        ops.scale_dropout(hs.reshape(N, d), h, p=ctc.dropout_rate, seed=ctc._seed)
+        logits = empty(N, V, device=dev)
+        ops.linear(h, b.w("ctc_lo.weight"), logits, epi=ops.make_epi(bias=b.f("ctc_lo.bias")))
+        S = 2 * Lmax + 1
+        lse = empty(N, device=dev)
+        alpha = torch.empty(B * T * S, dtype=torch.float64, device=dev)
+        beta = torch.empty(B * T * S, dtype=torch.float64, device=dev)
+        nll = torch.empty(B, dtype=torch.float64, device=dev)
+        loss_utt = empty(B, device=dev)
+        loss = empty((), device=dev)
+        lib.ea_ctc_loss_fwd(B, T, V, logits.data_ptr(), V, hlens.data_ptr(), ys.data_ptr(), ys.stride(0),
+                            ylens.data_ptr(), Lmax, lse.data_ptr(), alpha.data_ptr(), beta.data_ptr(),
+                            nll.data_ptr(), loss_utt.data_ptr(), loss.data_ptr(), ops.stream())
+        ctx.ctc = ctc
+        ctx.meta = (B, T, V, Lmax, d)
+        ctx.save = (h, logits, lse, alpha, beta, nll, hlens, ys, ylens)
+        ctx.logits = logits
+        return loss
+
+    @staticmethod
+    def backward(ctx, gl):
+        ctc = ctx.ctc
+        b = ctc._b
+        cd = b.cd
+        B, T, V, Lmax, d = ctx.meta
+        h, logits, lse, alpha, beta, nll, hlens, ys, ylens = ctx.save
+        ctx.save = None
+        N = B * T
+        dev = gl.device
+        dl = empty(N, V, dtype=cd, device=dev)
+        lib.ea_ctc_loss_bwd(B, T, V, logits.data_ptr(), V, hlens.data_ptr(), ys.data_ptr(), ys.stride(0),
+                            ylens.data_ptr(), Lmax, lse.data_ptr(), alpha.data_ptr(), beta.data_ptr(),
+                            nll.data_ptr(), _g(gl).data_ptr(), 1.0 / B, dl.data_ptr(), ops.dt(dl), V,
+                            ops.stream())
+        ops.colsum(dl, b.g("ctc_lo.bias"))
+        ops.linear_dw(dl, h, b.g("ctc_lo.weight"), accumulate=True)
+        dh = empty(N, d, device=dev)
+        ops.linear_dx(dl, b.w("ctc_lo.weight"), dh)
+        if ctc.dropout_rate > 0:
+            ops.scale_dropout(dh, dh, p=ctc.dropout_rate, seed=ctc._seed)
+        return dh.view(B, T, d), None, None, None, None, None
+
+
+class LabelSmoothingLossFn(torch.autograd.Function):
+    """-> (loss, acc); acc is not differentiable."""
+
+    @staticmethod
+    def forward(ctx, x, target, crit):
+        B, L, V = x.shape
+        rows = B * L
+        dev = x.device
+        x2 = x.reshape(rows, V)
+        lse = empty(rows, device=dev)
+        loss_row = torch.empty(rows, dtype=torch.float64, device=dev)
+        stat = torch.empty(2, dtype=torch.int32, device=dev)
+        loss = empty((), device=dev)
+        acc = empty((), device=dev)
+        inv = empty(1, device=dev)
+        tgt = target.reshape(rows).contiguous()
+        lib.ea_lsm_loss_fwd(rows, V, x2.data_ptr(), V, tgt.data_ptr(), crit.smoothing, crit.padding_idx,
+                            int(crit.normalize_length), float(B), lse.data_ptr(), loss_row.data_ptr(),
+                            stat.data_ptr(), loss.data_ptr(), acc.data_ptr(), inv.data_ptr(), ops.stream())
+        ctx.save = (x2, tgt, lse, inv, crit)
+        ctx.shape = (B, L, V)
+        ctx.mark_non_differentiable(acc)
+        return loss, acc
+
+    @staticmethod
+    def backward(ctx, gloss, gacc):
+        x2, tgt, lse, inv, crit = ctx.save
+        ctx.save = None
+        B, L, V = ctx.shape
+        grad = empty(B, L, V, device=x2.device)
+        lib.ea_lsm_loss_bwd(B * L, V, x2.data_ptr(), V, tgt.data_ptr(), crit.smoothing, crit.padding_idx,
+                            lse.data_ptr(), _g(gloss).data_ptr(), inv.data_ptr(), 1.0, grad.data_ptr(),
+                            0, V, ops.stream())
+        return grad, None, None
+
+
+class CombineFn(torch.autograd.Function):
+    """loss = w*a + (1-w)*b  (espnet_model.py:325)."""
+
+    @staticmethod
+    def forward(ctx, a, b, w):
+        out = empty((), device=a.device)
+        lib.ea_axpby_scalar(a.data_ptr(), w, b.data_ptr(), 1.0 - w, out.data_ptr(), ops.stream())
+        ctx.w = w
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        g = _g(g)
+        ga = empty((), device=g.device)
+        gb = empty((), device=g.device)
+        lib.ea_axpby_scalar(g.data_ptr(), ctx.w, 0, 0.0, ga.data_ptr(), ops.stream())
+        lib.ea_axpby_scalar(g.data_ptr(), 1.0 - ctx.w, 0, 0.0, gb.data_ptr(), ops.stream())
+        return ga, gb, None

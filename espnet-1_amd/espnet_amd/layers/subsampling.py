@@ -1,0 +1,157 @@
+"""Conv2dSubsampling (espnet/nets/pytorch_backend/transformer/subsampling.py:46-91) +
+RelPositionalEncoding (transformer/embedding.py:260-331), MI355X layout.
+
+The reference runs NCHW Conv2d(1,d,3,2)+ReLU, Conv2d(d,d,3,2)+ReLU, then
+x.transpose(1,2).view(b, t, c*f) -> Linear(d*F'', d) -> x*sqrt(d) -> dropout.
+Here activations are channel-last (B, T, F, C): both convolutions are MFMA GEMMs over
+im2col rows (conv1: 9 taps padded to 16; conv2: K = 9*C, the implicit-GEMM hot spot that
+is ~32% of the step's FLOPs), ReLU fused in the GEMM epilogue, and the Linear consumes
+the (t, f*C + c) order directly — its weight (d, C, F'') is repacked to (d, F'', C) per step
+(5 M elements) instead of transposing the 310 MB activation.
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+from torch import nn
+
+from .common import (ACT_RELU, EPI_ACT, EPI_DACT, EPI_STORE, F32, Bound, empty, lib, ops, rup)
+
+
+def rel_pos_table(n, d):
+    """RelPositionalEncoding.extend_pe (embedding.py:282-313): rows = relative positions
+    n-1 ... -(n-1).  A constant computed once at construction, like the reference."""
+    pos = torch.arange(0, n, dtype=torch.float32).unsqueeze(1)
+    div = torch.exp(torch.arange(0, d, 2, dtype=torch.float32) * -(math.log(10000.0) / d))
+    pp = torch.zeros(n, d)
+    pn = torch.zeros(n, d)
+    pp[:, 0::2] = torch.sin(pos * div)
+    pp[:, 1::2] = torch.cos(pos * div)
+    pn[:, 0::2] = torch.sin(-1 * pos * div)
+    pn[:, 1::2] = torch.cos(-1 * pos * div)
+    return torch.cat([torch.flip(pp, [0]), pn[1:]], 0)
+
+
+class RelPositionalEncoding(nn.Module):
+    """Holds the constant table; forward returns dropout(table slice) in the compute dtype."""
+
+    def __init__(self, d_model, dropout_rate, max_len=5000):
+        super().__init__()
+        self.d_model = d_model
+        self.xscale = math.sqrt(d_model)
+        self.dropout_rate = dropout_rate
+        self.max_len = max_len
+        self._pe = None  # device copy, built lazily (not a buffer: not in the state_dict)
+
+    def table(self, T, device):
+        n = max(self.max_len, T)
+        if self._pe is None or self._pe.shape[0] < 2 * T - 1 or self._pe.device != device:
+            self._pe = rel_pos_table(n, self.d_model).to(device)
+        return self._pe
+
+    def pos_emb(self, T, device, cd, training, seed):
+        pe = self.table(T, device)
+        c = pe.shape[0] // 2
+        src = pe[c - T + 1: c + T]
+        out = empty(2 * T - 1, self.d_model, dtype=cd, device=device)
+        ops.scale_dropout(src, out, 1.0, self.dropout_rate if training else 0.0, seed)
+        return out
+
+
+class Conv2dSubsampling(nn.Module):
+    """Parameter holder with the reference's names: conv.0 / conv.2 / out.0 (+ pos_enc)."""
+
+    def __init__(self, idim, odim, dropout_rate, pos_enc=None):
+        super().__init__()
+        self.conv = nn.Sequential(nn.Conv2d(1, odim, 3, 2), nn.ReLU(), nn.Conv2d(odim, odim, 3, 2), nn.ReLU())
+        self.F1 = (idim - 1) // 2
+        self.F2 = (self.F1 - 1) // 2
+        self.out = nn.Sequential(nn.Linear(odim * self.F2, odim),
+                                 pos_enc if pos_enc is not None else RelPositionalEncoding(odim, dropout_rate))
+        self.odim = odim
+        self.idim = idim
+        self._b = None
+
+    def bind(self, arena, prefix, cd):
+        self._b = Bound(arena, prefix, cd)
+
+    def forward(self, feats, seed):
+        return SubsampleFn.apply(feats, self._anchor, self, seed, self.training)
+
+
+class SubsampleFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, feats, anchor, m: Conv2dSubsampling, seed, training):
+        b = m._b
+        cd = b.cd
+        B, T, Fin = feats.shape
+        C = m.odim
+        T1, F1 = (T - 3) // 2 + 1, (Fin - 3) // 2 + 1
+        T2, F2 = (T1 - 3) // 2 + 1, (F1 - 3) // 2 + 1
+        dev = feats.device
+        pe = m.out[1]
+        # conv1: im2col (P1 x 16) . W1p^T -> relu -> x1 (B,T1,F1,C)
+        P1 = B * T1 * F1
+        col1 = empty(P1, 16, dtype=cd, device=dev)
+        lib.ea_im2col_conv1(B, T, Fin, feats.data_ptr(), col1.data_ptr(), ops.dt(col1), ops.stream())
+        w1 = empty(C, 16, dtype=cd, device=dev)
+        w1.zero_()
+        ops.scale_dropout(b.f("conv.0.weight", shape=(C, 9)), w1[:, :9])
+        x1 = empty(P1, C, dtype=cd, device=dev)
+        ops.linear(col1, w1, x1, epi=ops.make_epi(EPI_ACT, bias=b.f("conv.0.bias"), act=ACT_RELU))
+        # conv2: im2col (P2 x 9C) . W2p^T -> relu -> x2 (B,T2,F2,C)
+        P2 = B * T2 * F2
+        col2 = empty(P2, 9 * C, dtype=cd, device=dev)
+        lib.ea_im2col_conv2(B, T1, F1, C, x1.data_ptr(), col2.data_ptr(), ops.dt(col2), ops.stream())
+        w2 = empty(C, 9 * C, dtype=cd, device=dev)
+        ops.permute3(b.f("conv.2.weight"), w2, C, C, 9)  # (Co,Ci,9) -> (Co,9,Ci)
+        x2 = empty(P2, C, dtype=cd, device=dev)
+        ops.linear(col2, w2, x2, epi=ops.make_epi(EPI_ACT, bias=b.f("conv.2.bias"), act=ACT_RELU))
+        # out.0 Linear on (t, f*C + c) rows, * sqrt(d), dropout (embedding.py:326)
+        wl = empty(C, F2 * C, dtype=cd, device=dev)
+        ops.permute3(b.f("out.0.weight"), wl, C, C, F2)  # (d, C, F2) -> (d, F2, C)
+        y = empty(B * T2, C, device=dev)
+        p = pe.dropout_rate if training else 0.0
+        ops.linear(x2.view(B * T2, F2 * C), wl, y,
+                   epi=ops.make_epi(bias=b.f("out.0.bias"), post_scale=pe.xscale, drop_p=p, seed=seed))
+        ctx.m = m
+        ctx.meta = (B, T, Fin, T1, F1, T2, F2, p, seed)
+        ctx.save = (col1, x1, col2, w2, x2, wl)
+        return y.view(B, T2, C)
+
+    @staticmethod
+    def backward(ctx, dy):
+        m = ctx.m
+        b = m._b
+        cd = b.cd
+        B, T, Fin, T1, F1, T2, F2, p, seed = ctx.meta
+        col1, x1, col2, w2, x2, wl = ctx.save
+        ctx.save = None
+        C = m.odim
+        dev = dy.device
+        dv = empty(B * T2, C, dtype=cd, device=dev)
+        ops.scale_dropout(dy.reshape(B * T2, C).contiguous(), dv, scale=m.out[1].xscale, p=p, seed=seed)
+        ops.colsum(dv, b.g("out.0.bias"))
+        dwl = empty(C, F2 * C, device=dev)
+        x2r = x2.view(B * T2, F2 * C)
+        ops.linear_dw(dv, x2r, dwl, accumulate=False)
+        ops.permute3(dwl, b.g("out.0.weight"), C, F2, C, accumulate=True)  # (d,F2,C) -> (d,C,F2)
+        dx2 = empty(B * T2, F2 * C, dtype=cd, device=dev)
+        ops.linear_dx(dv, wl, dx2, epi=ops.make_epi(EPI_DACT, act=ACT_RELU, aux=x2r))
+        dx2 = dx2.view(-1, C)
+        ops.colsum(dx2, b.g("conv.2.bias"))
+        dw2 = empty(C, 9 * C, device=dev)
+        ops.linear_dw(dx2, col2, dw2, accumulate=False)
+        ops.permute3(dw2, b.g("conv.2.weight"), C, 9, C, accumulate=True)  # (Co,9,Ci) -> (Co,Ci,9)
+        dcol2 = empty(*col2.shape, dtype=cd, device=dev)
+        ops.linear_dx(dx2, w2, dcol2)
+        del col2
+        dx1 = empty(*x1.shape, dtype=cd, device=dev)
+        lib.ea_col2im_conv2(B, T1, F1, C, dcol2.data_ptr(), ops.dt(dcol2), x1.data_ptr(), dx1.data_ptr(),
+                            ops.dt(dx1), ops.stream())
+        del dcol2
+        ops.colsum(dx1, b.g("conv.0.bias"))
+        ops.gemm(dx1, col1, b.g("conv.0.weight", shape=(C, 9)), M=C, N=9, K=dx1.shape[0],
+                 a_kmajor=0, b_kmajor=0, lda=C, ldb=16, ldc=9, epi=ops.make_epi(beta=1.0))
+        return None, None, None, None, None

@@ -53,7 +53,7 @@ typedef struct ea_epilogue {
  *  a_kmajor=1: A[m,k] at A[m*lda + k]   (row-major M x K)   else A[k*lda + m]
  *  b_kmajor=1: B[k,n] at B[n*ldb + k]   (torch Linear weight N x K) else B[k*ldb + n]
  *  z in [0, batch*nh): zb = z / nh, zh = z % nh; operand offset = zb*s?b + zh*s?h.
- *  lda/ldb and the A/B base pointers must be 16-byte aligned in elements.
+ *  16-B aligned bases / leading dims take 16-B vector loads; others an element-wise path.
  *  workspace (f32, ws_elems) enables split-K for EA_EPI_STORE; NULL disables it.
  * Replaces: torch.nn.Linear / torch.matmul in transformer/attention.py:54-93,262-305,
  * positionwise_feed_forward.py:30-32, conformer/convolution.py:71-77 (1x1 convs),
@@ -64,6 +64,172 @@ int ea_gemm(int dtype, int a_kmajor, int b_kmajor, int M, int N, int K,
             int batch, int nh,
             void* C, int c_dtype, long ldc, long sCb, long sCh,
             const ea_epilogue* epi, float* workspace, long ws_elems, void* stream);
+
+
+/* ---------------------------------------------------------------- normalisation */
+
+/* LayerNorm(eps) over the last dim, one wave64 per row; y in y_dtype, saves mean/rstd.
+ * Replaces torch.nn.LayerNorm in transformer/layer_norm.py:12-42 (eps 1e-12), used
+ * 5x per conformer block (encoder_layer.py:61-70), after_norm, decoder norm1-3. */
+int ea_layernorm_fwd(int rows, int d, const float* x, long ldx, const float* gamma,
+                     const float* beta, float eps, void* y, int y_dtype, long ldy,
+                     float* mean, float* rstd, void* stream);
+
+/* LayerNorm backward: dx (+)= ..., dgamma/dbeta (+)= (dbeta must equal dgamma + d:
+ * weight and bias grads are adjacent in the parameter arena).
+ * workspace >= min(ceil(rows/4),512) * 2d floats. */
+int ea_layernorm_bwd(int rows, int d, const void* dy, int dy_dtype, long lddy, const float* x,
+                     long ldx, const float* gamma, const float* mean, const float* rstd,
+                     float* dx, long lddx, int accumulate, float* dgamma, float* dbeta,
+                     int accumulate_params, float* workspace, long ws_elems, void* stream);
+
+/* out[c] (+)= sum_p part[p*stride + c] in fixed order (deterministic). */
+int ea_reduce_partials(int nparts, int n, const float* part, long stride, float* out,
+                       int accumulate, void* stream);
+
+/* out[c] (+)= sum_r x[r*ld + c]  — Linear bias gradients (autograd sum over rows). */
+int ea_colsum(int rows, int n, const void* x, int x_dtype, long ld, float* out, int accumulate,
+              float* workspace, long ws_elems, void* stream);
+
+/* BatchNorm1d (training: batch stats over ALL rows incl. padding, running stats update
+ * with momentum and unbiased var, num_batches_tracked += 1; eval: given mean/rstd) fused
+ * with the following activation: z = act(BN(y)).  y, z: (rows, C) channel-last.
+ * Replaces conformer/convolution.py:45,75 (norm + Swish). */
+int ea_batchnorm_fwd(int rows, int C, const float* y, const float* gamma, const float* beta,
+                     float eps, float momentum, int training, float* mean, float* rstd,
+                     float* running_mean, float* running_var, long long* num_batches_tracked,
+                     int act, void* z, int z_dtype, float* workspace, long ws_elems, void* stream);
+
+/* Backward of z = act(BN_train(y)): dy, dgamma/dbeta (dbeta == dgamma + C). */
+int ea_batchnorm_bwd(int rows, int C, const void* dz, int dz_dtype, const float* y, const float* mean,
+                     const float* rstd, const float* gamma, const float* beta, int act, float* dy,
+                     float* dgamma, float* dbeta, int accumulate_params, float* workspace,
+                     long ws_elems, void* stream);
+
+/* ---------------------------------------------------------------- elementwise / layout */
+
+/* utterance_mvn(norm_means=True, norm_vars=False), espnet2/layers/utterance_mvn.py:45-88:
+ * x (B,T,F) f32 -> y = (x masked to valid frames) - per-utterance mean. F <= 256. */
+int ea_utterance_mvn(int B, int T, int F, const float* x, const long long* lens, float* y, void* stream);
+
+/* encoder_out_lens of Conv2dSubsampling from the sliced mask, subsampling.py:91 +
+ * conformer_encoder.py:374. */
+int ea_subsample_lens(int B, int T, const long long* ilens, long long* olens, void* stream);
+
+/* add_sos_eos + pad_list (transformer/add_sos_eos.py:12-31); ys_in/ys_out (B, L+1). */
+int ea_add_sos_eos(int B, int L, const long long* ys, long ldys, const long long* ylens, int sos,
+                   int eos, int ignore_id, long long* ys_in, long long* ys_out,
+                   long long* ys_in_lens, void* stream);
+
+/* y = dropout(x * scale) with the counter-based mask (index = r*cols + c). */
+int ea_scale_dropout(long rows, int cols, const void* x, int x_dtype, long ldx, void* y,
+                     int y_dtype, long ldy, float scale, float p, unsigned long long seed,
+                     void* stream);
+
+/* y[r, c] += alpha * x[r, c] (mixed dtypes) — autograd's gradient accumulation of a
+ * tensor consumed twice (q + pos_bias_u and q + pos_bias_v, attention.py:287-301). */
+int ea_add_2d(long rows, int cols, const void* x, int x_dtype, long ldx, void* y, int y_dtype,
+              long ldy, float alpha, void* stream);
+
+/* dst[a][c][b] (+)= src[a][b][c]: weight repacks (Conv2d (Co,Ci,9) <-> (Co,9,Ci); the
+ * subsampling Linear's (O, C, F) <-> (O, F, C) for channel-last activations). */
+int ea_permute3(int A, int Bd, int Cd, const void* src, int src_dtype, void* dst, int dst_dtype,
+                int accumulate, void* stream);
+
+/* Conv2dSubsampling (subsampling.py:60-65) as GEMMs over channel-last activations:
+ * conv1 rows (b,t1,f1) x 16 taps (9 used); conv2 rows (b,t2,f2) x (kh,kw,c); the input
+ * gradient of conv2 by a gather col2im fused with conv1's ReLU mask. */
+int ea_im2col_conv1(int B, int T, int F, const float* x, void* col, int col_dtype, void* stream);
+int ea_im2col_conv2(int B, int T1, int F1, int C, const void* x1, void* col, int dtype, void* stream);
+int ea_col2im_conv2(int B, int T1, int F1, int C, const void* dcol, int dcol_dtype, const void* x1,
+                    void* dx1, int dtype, void* stream);
+
+/* GLU over channels (conformer/convolution.py:72): y = x[:, :C] * sigmoid(x[:, C:]). */
+int ea_glu_fwd(long rows, int C, const void* x, int x_dtype, void* y, int y_dtype, void* stream);
+int ea_glu_bwd(long rows, int C, const void* x, int x_dtype, const float* dy, void* dx, void* stream);
+
+/* Depthwise Conv1d(C, C, K, pad (K-1)/2, groups=C) over time, channel-last (B,T,C) f32
+ * (conformer/convolution.py:38-45,75).  bwd: dx, dw (C,K), dbias. */
+int ea_dwconv_fwd(int B, int T, int C, int K, const float* x, const float* w, const float* bias,
+                  float* y, void* stream);
+int ea_dwconv_bwd(int B, int T, int C, int K, const float* x, const float* w, const float* dy,
+                  float* dx, float* dw, float* dbias, int accumulate_params, float* workspace,
+                  long ws_elems, void* stream);
+
+/* q + pos_bias_u / q + pos_bias_v (attention.py:287-290) for the fused qkv rows. */
+int ea_add_pos_bias(long N, int H, int dk, const void* q, long ldq, const float* u, const float* v,
+                    void* qu, void* qv, int dtype, void* stream);
+
+/* Decoder Embedding + PositionalEncoding (x*sqrt(d) + pe, dropout), embedding.py:81-92;
+ * backward scatter-adds into the embedding gradient. */
+int ea_embed_fwd(long rows, int d, int L, const long long* tok, const float* E, float xscale,
+                 const float* pe, float p, unsigned long long seed, float* y, void* stream);
+int ea_embed_bwd(long rows, int d, const long long* tok, const float* dy, float xscale, float p,
+                 unsigned long long seed, float* dE, void* stream);
+
+/* CTC.argmax (ctc.py:119-127): first maximal index per row (bit-exact alignment). */
+int ea_argmax_rows(long rows, int V, const float* x, long ld, long long* out, void* stream);
+
+/* ---------------------------------------------------------------- attention */
+
+/* P = masked_softmax(scale*(S + rel_shift(BD))), Pd = dropout(P) — attention.py:63-93,
+ * 262-305.  S [z][i][ldS] (z = b*H + h), BD [h][b][i][ldBD] (rel-pos, T1 == T2) or NULL,
+ * key j valid iff j < klen[b] (klen NULL: all) and (!causal || j <= i). */
+int ea_attn_softmax_fwd(int B, int H, int T1, int T2, float scale, const float* S, long ldS,
+                        const float* BD, long ldBD, const long long* klen, int causal, float p,
+                        unsigned long long seed, float* P, long ldP, void* Pd, int pd_dtype,
+                        long ldPd, void* stream);
+
+/* dS = scale * P*(dP - rowsum(P*dP)), dP = dropout_bwd(dPd); if dBD != NULL also
+ * dBD[h][b][i][r] = dS[i, r-(T1-1-i)] (0 off the band) for r < 2*T1-1. */
+int ea_attn_softmax_bwd(int B, int H, int T1, int T2, float scale, const float* dPd, long ldd,
+                        const float* P, long ldP, float p, unsigned long long seed, void* dS,
+                        int ds_dtype, long ldS, void* dBD, long ldBD, void* stream);
+
+/* ---------------------------------------------------------------- losses */
+
+/* CTC forward (ctc.py:52-97 builtin; torch CTCLoss reduction=none, zero_infinity=True,
+ * blank=0, on log_softmax(logits)): per-utterance loss (0 if infeasible) and
+ * loss = sum / B.  logits rows (b*T + t)*ldt; alpha/beta [B][T][2*Lmax+1] f64. */
+int ea_ctc_loss_fwd(int B, int T, int V, const float* logits, long ldt, const long long* hlens,
+                    const long long* ys, long ldys, const long long* ylens, int Lmax, float* lse,
+                    double* alpha, double* beta, double* nll, float* loss_utt, float* loss,
+                    void* stream);
+
+/* d loss / d logits = gscale[0]*coef*(softmax - occupancy); 0 past hlens or if infeasible. */
+int ea_ctc_loss_bwd(int B, int T, int V, const float* logits, long ldt, const long long* hlens,
+                    const long long* ys, long ldys, const long long* ylens, int Lmax, const float* lse,
+                    const double* alpha, const double* beta, const double* nll,
+                    const float* gscale, float coef, void* grad, int grad_dtype, long ldg,
+                    void* stream);
+
+/* LabelSmoothingLoss + th_accuracy (label_smoothing_loss.py:41-63, nets_utils.py:304-324):
+ * loss[0], acc[0] (correct/valid tokens), inv_denom[0] = 1/(#tokens or batch). */
+int ea_lsm_loss_fwd(long rows, int V, const float* x, long ldx, const long long* tgt, float smoothing,
+                    int ignore_id, int normalize_length, float batch, float* lse, double* loss_row,
+                    int* stat, float* loss, float* acc, float* inv_denom, void* stream);
+int ea_lsm_loss_bwd(long rows, int V, const float* x, long ldx, const long long* tgt, float smoothing,
+                    int ignore_id, const float* lse, const float* gscale, const float* inv_denom,
+                    float coef, void* grad, int grad_dtype, long ldg, void* stream);
+
+/* ---------------------------------------------------------------- optimizer */
+
+/* norm[0] = ||x||_2 (fp64 accumulation); workspace >= 2048 doubles. */
+int ea_sqnorm(long n, const float* x, double* workspace, float* norm, void* stream);
+
+/* torch.optim.Adam step (L2 weight decay) over the flat arena with
+ * clip_grad_norm_(max_norm) folded in (coef = min(1, max_norm/(norm+1e-6))) and the
+ * update skipped on device when norm is not finite (trainer.py:653-678).
+ * Optionally refreshes the bf16 weight shadow. */
+int ea_adam_step(long n, float* params, const float* grads, float* exp_avg, float* exp_avg_sq,
+                 void* params_bf16, float lr, float beta1, float beta2, float eps, float weight_decay,
+                 long step, const float* grad_norm, float max_norm, void* stream);
+
+int ea_cast_f32_bf16(long n, const float* x, void* y, void* stream);
+/* x *= s[0]*c (device scalar) */
+int ea_scale_by_scalar(long n, float* x, const float* s, float c, void* stream);
+/* out[0] = wa*a[0] + wb*b[0] (b may be NULL) — loss = w*ctc + (1-w)*att, espnet_model.py:325 */
+int ea_axpby_scalar(const float* a, float wa, const float* b, float wb, float* out, void* stream);
 
 #ifdef __cplusplus
 }

@@ -151,3 +151,17 @@ def test_gemm_splitk_dw(dtype):
     w = mk((N, K), dtype, g)
     ops.linear_dx(dy, w, dx)
     torch.testing.assert_close(dx.double().cpu(), dy.double().cpu() @ w.double().cpu(), **tol)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("a_k,b_k", [(1, 1), (1, 0), (0, 1), (0, 0)])
+def test_gemm_unaligned_leading_dims(dtype, a_k, b_k):
+    ops, L = _ops()
+    M, N, K = 52, 50, 67
+    g = torch.Generator().manual_seed(17)
+    A = mk((M, K) if a_k else (K, M), dtype, g)   # ld = K or M: not 16-B multiples
+    B = mk((N, K) if b_k else (K, N), dtype, g)
+    C = torch.empty(M, N, device="cuda")
+    ops.gemm(A, B, C, M=M, N=N, K=K, a_kmajor=a_k, b_kmajor=b_k, lda=A.stride(0), ldb=B.stride(0), ldc=N)
+    tol = 1e-5 if dtype == torch.float32 else 2e-3
+    torch.testing.assert_close(C.double().cpu(), ref_mm(A, B, a_k, b_k, M, N, K), atol=tol * K ** 0.5, rtol=tol)

@@ -1,0 +1,75 @@
+"""Whole-model parity on the MI355X: the HIP training step (forward + backward through
+libespnet_amd.so) against golden vectors captured from the reference
+(oracle/make_goldens.py) — loss, stats, encoder output, CTC alignment (bit-exact),
+decoder logits, every parameter gradient and the BatchNorm running stats."""
+import numpy as np
+import pytest
+import torch
+
+from goldens import load, section
+from test_model_build import build
+
+pytestmark = pytest.mark.gpu
+
+
+def run(name, amp=False):
+    cfg, d = load(name)
+    torch.manual_seed(0)
+    m = build(cfg)
+    w = {k: torch.from_numpy(v) for k, v in section(d, "w").items()}
+    if cfg["model_conf"]["ctc_weight"] == 1.0:
+        w = {k: v for k, v in w.items() if not k.startswith("decoder.")}
+    m.load_state_dict(w)
+    m.prepare("cuda", amp=amp)
+    m.train()
+    inp = {k: torch.from_numpy(v) for k, v in section(d, "in").items()}
+    loss, stats, weight = m(**inp)
+    loss.backward()
+    torch.cuda.synchronize()
+    return cfg, d, m, loss, stats, weight
+
+
+@pytest.mark.parametrize("name", ["tiny_hybrid", "tiny_ctc", "medium_hybrid"])
+def test_model_fp32_parity(name):
+    cfg, d, m, loss, stats, weight = run(name)
+    # fp32 atol 1e-4 on loss/logits (BASELINE.json north_star); + a relative term for
+    # losses of magnitude 10^2 (fp32 ulp(128) = 1.5e-5, SURVEY.md §7 "Tolerance vs magnitude")
+    np.testing.assert_allclose(loss.item(), d["out.loss"], rtol=2e-6, atol=1e-4)
+    assert weight.item() == d["out.weight"]
+    for k, v in section(d, "stat").items():
+        np.testing.assert_allclose(stats[k].item(), v, rtol=2e-6, atol=1e-4, err_msg=k)
+    enc, olens = m._last_encoder_out
+    np.testing.assert_array_equal(olens.cpu().numpy(), d["out.encoder_out_lens"])
+    np.testing.assert_allclose(enc.detach().cpu().numpy(), d["out.encoder_out"], atol=1e-4, rtol=1e-4)
+    np.testing.assert_allclose(m.ctc.logits(enc.detach()).cpu().numpy(), d["out.ctc_logits"], atol=1e-4,
+                               rtol=1e-4)
+    am = m.ctc.argmax(enc.detach()).cpu().numpy()
+    np.testing.assert_array_equal(am, d["out.ctc_argmax"])  # bit-exact alignment indices
+    if "out.decoder_out" in d:
+        np.testing.assert_allclose(m._last_decoder_out.detach().cpu().numpy(), d["out.decoder_out"],
+                                   atol=1e-4, rtol=1e-4)
+    params = dict(m.named_parameters())
+    for k, g in section(d, "g").items():
+        np.testing.assert_allclose(params[k].grad.cpu().numpy(), g, atol=2e-5, rtol=2e-4, err_msg=k)
+    for k, gn in section(d, "gn").items():
+        mine = params[k].grad.double().cpu()
+        np.testing.assert_allclose(mine.norm().item(), gn, rtol=1e-4, err_msg=k)
+        np.testing.assert_allclose(mine.reshape(-1)[:256].float().numpy(), d["gh." + k],
+                                   atol=2e-5, rtol=2e-4, err_msg=k)
+    sd = m.state_dict()
+    for k, v in section(d, "buf_after").items():
+        np.testing.assert_allclose(sd[k].cpu().numpy(), v, atol=1e-5, rtol=1e-5, err_msg=k)
+
+
+@pytest.mark.parametrize("name", ["tiny_hybrid", "medium_hybrid"])
+def test_model_bf16_amp_close(name):
+    """AMP (bf16 MFMA operands, f32 accumulation/normalisation/losses) stays close."""
+    cfg, d, m, loss, stats, weight = run(name, amp=True)
+    np.testing.assert_allclose(loss.item(), d["out.loss"], rtol=2e-2)
+    params = dict(m.named_parameters())
+    num = den = 0.0
+    for k, g in section(d, "g").items():
+        mine = params[k].grad.double().cpu()
+        num += float(((mine - torch.from_numpy(g).double()) ** 2).sum())
+        den += float((torch.from_numpy(g).double() ** 2).sum())
+    assert (num / den) ** 0.5 < 5e-2, (num / den) ** 0.5
