@@ -1,0 +1,213 @@
+"""Benchmark: ESPnet2 ASR training step (ESPnetASRModel, Conformer-L + Transformer decoder,
+hybrid CTC/attention) on MI355X — BASELINE.json metric "utterances/sec + step-time,
+Conformer-L T=1000 batch=32 @1/2/4/8 GPU".
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c3|c2] [--fp32]
+    torchrun --nproc-per-node N bench.py --gpus N ...      (one rank per GPU, RCCL)
+
+A step = forward + backward + RCCL gradient all-reduce (N>1) + clip_grad_norm(5) + Adam +
+WarmupLR + zero_grad over one synthetic batch per rank (speech ~ N(0,1) (32, 1000, 80),
+text uniform in [2, V-2], L=40 — SURVEY.md §8d), inputs resident in HBM before timing.
+Weak scaling: 32 utterances per GPU.  Prints ONE JSON line on rank 0.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "espnet-1_amd"))
+sys.path.insert(0, ROOT)
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+METRIC = "utterances/sec + step-time, Conformer-L T=1000 batch=32 @1/2/4/8 GPU"
+PEAK = {"bf16": 2500.0, "f32": 157.3}  # dense MFMA TFLOP/s, MI355X_MICROARCH.md
+
+
+def c3_config():
+    """egs2/librispeech/asr1/conf/tuning/train_asr_conformer8.yaml:2-34 with input_size 80."""
+    return dict(
+        input_size=80, vocab_size=5000, B=32, T=1000, L=40,
+        encoder_conf=dict(output_size=512, attention_heads=8, linear_units=2048, num_blocks=12,
+                          dropout_rate=0.1, positional_dropout_rate=0.1, attention_dropout_rate=0.1,
+                          input_layer="conv2d", normalize_before=True, macaron_style=True,
+                          rel_pos_type="latest", pos_enc_layer_type="rel_pos",
+                          selfattention_layer_type="rel_selfattn", activation_type="swish",
+                          use_cnn_module=True, cnn_module_kernel=31),
+        decoder="transformer",
+        decoder_conf=dict(attention_heads=8, linear_units=2048, num_blocks=6, dropout_rate=0.1,
+                          positional_dropout_rate=0.1, self_attention_dropout_rate=0.1,
+                          src_attention_dropout_rate=0.1),
+        model_conf=dict(ctc_weight=0.3, lsm_weight=0.1, length_normalized_loss=False),
+        optim=dict(lr=0.0025, weight_decay=1e-6), warmup_steps=40000,
+        gflop_per_step=6643.0,
+    )
+
+
+def c2_config():
+    c = c3_config()
+    c.update(B=16, T=500, L=20, decoder=None, gflop_per_step=282.8)
+    c["encoder_conf"] = dict(c["encoder_conf"], output_size=256, attention_heads=4, linear_units=1024,
+                             num_blocks=6)
+    c["model_conf"] = dict(ctc_weight=1.0, lsm_weight=0.0, length_normalized_loss=False)
+    return c
+
+
+def token_list(V):
+    return ["<blank>", "<unk>"] + [f"t{i}" for i in range(V - 3)] + ["<sos/eos>"]
+
+
+def build(cfg, seed=0):
+    from espnet_amd.tasks.asr import build_model
+    torch.manual_seed(seed)
+    args = dict(token_list=token_list(cfg["vocab_size"]), input_size=cfg["input_size"], encoder="conformer",
+                encoder_conf=cfg["encoder_conf"], decoder=cfg["decoder"],
+                decoder_conf=cfg["decoder_conf"], model_conf=cfg["model_conf"], normalize="utterance_mvn")
+    return build_model(args)
+
+
+def synthetic_batch(cfg, seed):
+    g = torch.Generator().manual_seed(seed)
+    B, T, L, V = cfg["B"], cfg["T"], cfg["L"], cfg["vocab_size"]
+    return dict(speech=torch.randn(B, T, cfg["input_size"], generator=g),
+                speech_lengths=torch.full((B,), T, dtype=torch.long),
+                text=torch.randint(2, V - 1, (B, L), generator=g),
+                text_lengths=torch.full((B,), L, dtype=torch.long))
+
+
+def cpu_baseline(cfg, seconds_budget=25.0):
+    """The oracle (oracle/asr_oracle.py, PyTorch-CPU restatement of the reference step) on
+    the host cores: fwd + bwd + clip + Adam on a bounded sample (B=4 of the same shapes)."""
+    from oracle.asr_oracle import OracleASR, OracleTrainer
+    torch.set_num_threads(min(os.cpu_count() or 1, int(os.environ.get("OMP_NUM_THREADS", "16"))))
+    sample = dict(cfg, B=4)
+    model_cpu = build(cfg)
+    ocfg = dict(vocab_size=cfg["vocab_size"], encoder_conf=cfg["encoder_conf"],
+                decoder_conf=cfg["decoder_conf"] or {}, model_conf=cfg["model_conf"])
+    ora = OracleASR(ocfg, {k: v.detach() for k, v in model_cpu.state_dict().items()})
+    tr = OracleTrainer(ora, cfg["optim"]["lr"], cfg["optim"]["weight_decay"], cfg["warmup_steps"])
+    batch = synthetic_batch(sample, 1)
+    times = []
+    t_start = time.perf_counter()
+    while True:
+        t0 = time.perf_counter()
+        tr.step(batch)
+        times.append(time.perf_counter() - t0)
+        if time.perf_counter() - t_start > seconds_budget or len(times) >= 6:
+            break
+    steady = sorted(times[1:] if len(times) > 1 else times)
+    t = steady[len(steady) // 2]
+    return dict(value=round(sample["B"] / t, 4), unit="utterances/s", cores=torch.get_num_threads(),
+                kind="port",
+                sample=f"oracle step (fwd+bwd+clip+Adam, dropout 0.1, fp32) at B={sample['B']}, "
+                       f"T={cfg['T']}, L={cfg['L']}; median of {len(steady)} steps "
+                       f"({t:.2f} s/step)")
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--config", default="c3", choices=["c3", "c2"])
+    ap.add_argument("--fp32", action="store_true", help="exact-f32 MFMA instead of bf16 AMP")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--profile-steps", type=int, default=0)
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    if world > 1:
+        os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+
+    from espnet_amd import hip_ops
+    from espnet_amd.optim.adam import ArenaAdam
+    from espnet_amd.schedulers.warmup_lr import WarmupLR
+    from espnet_amd.train.distributed import ArenaDataParallel
+    from espnet_amd.train.trainer import Trainer
+
+    cfg = c3_config() if args.config == "c3" else c2_config()
+    amp = not args.fp32
+    model = build(cfg)
+    model.prepare(dev, amp=amp, seed=1234)
+    model.train()
+    opt = ArenaAdam(model, lr=cfg["optim"]["lr"], weight_decay=cfg["optim"]["weight_decay"])
+    sched = WarmupLR(opt, warmup_steps=cfg["warmup_steps"])
+    dp = ArenaDataParallel(model) if world > 1 else None
+    host = synthetic_batch(cfg, 1 + rank)  # abs_task.py:1566-1575: each rank its own shard
+    batch = dict(speech=host["speech"].to(dev), text=host["text"].to(dev),
+                 speech_lengths=host["speech_lengths"], text_lengths=host["text_lengths"])
+
+    def step():
+        return Trainer.train_one_step(model, batch, opt, sched, grad_clip=5.0, dp=dp)
+
+    for _ in range(args.warmup):
+        step()
+    probe = hip_ops.KernelProbe(["conv2_gemm"])
+    hip_ops.PROBE = probe
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        loss, stats, weight, gn = step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t1 = time.perf_counter()
+    hip_ops.PROBE = None
+    elapsed = t1 - t0
+    if world > 1:
+        t = torch.tensor([elapsed], device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    ms = elapsed / args.steps * 1e3
+    utt = cfg["B"] * world * args.steps / elapsed
+    conv_ms, n_conv = probe.mean_ms("conv2_gemm")
+    B, T = cfg["B"], cfg["T"]
+    T1, F1 = (T - 3) // 2 + 1, (80 - 3) // 2 + 1
+    T2, F2 = (T1 - 3) // 2 + 1, (F1 - 3) // 2 + 1
+    C = cfg["encoder_conf"]["output_size"]
+    conv_flop = 2.0 * B * T2 * F2 * C * 9 * C
+    dtype = "bf16" if amp else "f32"
+    achieved = conv_flop / (conv_ms * 1e-3) / 1e12
+    loss_v = float(loss.item())
+    if rank == 0:
+        out = {
+            "metric": METRIC, "value": round(utt, 3), "unit": "utterances/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms, 3),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": dtype,
+            "data": "synthetic (speech ~N(0,1) fbank-shaped, uniform tokens; random-init weights)",
+            "config": {"workload": f"{args.config.upper()} " + (
+                "Conformer-L (12x512, 8 heads, ff 2048, cnn 31) + 6-layer Transformer decoder, "
+                "hybrid CTC/att 0.3/0.7, lsm 0.1, V=5000, T=1000 frames x 80, L=40, dropout 0.1, "
+                "Adam+WarmupLR+clip 5" if args.config == "c3" else
+                "Conformer-S (6x256, 4 heads, ff 1024), CTC only, V=5000, T=500, L=20"),
+                "global_batch": B * world, "seq_len": T, "parallelism": f"dp{world}"},
+            "model_tflops_per_s": round(cfg["gflop_per_step"] * world / (ms * 1e-3) / 1e3, 2),
+            "roofline": {"bound": "mfma", "kernel": "gemm_kernel<bf16> conv2 implicit-GEMM (subsampling, "
+                                                    f"M={B * T2 * F2} N={C} K={9 * C})",
+                         "achieved": round(achieved, 2), "peak": PEAK[dtype], "unit": "TFLOP/s",
+                         "frac": round(achieved / PEAK[dtype], 4), "traffic": None,
+                         "launch_ms": round(conv_ms, 4), "launches": n_conv},
+            "loss": round(loss_v, 4),
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            out["cpu_baseline"] = cpu_baseline(cfg)
+            out["speedup_vs_cpu"] = round(utt / out["cpu_baseline"]["value"], 1)
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -158,6 +158,7 @@ extern "C" int ea_attn_softmax_fwd(int B, int H, int T1, int T2, float scale, co
                                    const float* BD, long ldBD, const long long* klen, int causal, float p,
                                    unsigned long long seed, float* P, long ldP, void* Pd, int pd_dtype,
                                    long ldPd, void* stream) {
+  EA_ENTRY();
   if ((long)B * H * T1 == 0) return 0;
   if (BD) EA_CHECK_ARG(T1 == T2);
   SmP a{B, H, T1, T2, scale, S, ldS, BD, ldBD, klen, causal, p, (uint64_t)seed, P, ldP, Pd, pd_dtype, ldPd};
@@ -169,6 +170,7 @@ extern "C" int ea_attn_softmax_fwd(int B, int H, int T1, int T2, float scale, co
 extern "C" int ea_attn_softmax_bwd(int B, int H, int T1, int T2, float scale, const float* dPd, long ldd,
                                    const float* P, long ldP, float p, unsigned long long seed, void* dS,
                                    int ds_dtype, long ldS, void* dBD, long ldBD, void* stream) {
+  EA_ENTRY();
   if ((long)B * H * T1 == 0) return 0;
   if (dBD) EA_CHECK_ARG(T1 == T2);
   SmBP a{B, H, T1, T2, scale, dPd, ldd, P, ldP, p, (uint64_t)seed, dS, ds_dtype, ldS, dBD, ldBD, 2 * T1 - 1};

@@ -18,6 +18,10 @@ typedef __attribute__((ext_vector_type(4))) float f32x4;
     if (_e != hipSuccess) return (int)_e;                  \
   } while (0)
 
+// Clear a stale thread-local HIP error left by another library (e.g. the host framework's
+// device probing) so EA_LAUNCH_CHECK reports only this entry point's own launches.
+#define EA_ENTRY() ((void)hipGetLastError())
+
 #define EA_CHECK_ARG(cond)                                 \
   do {                                                     \
     if (!(cond)) return EA_ERR_BAD_ARG;                    \

@@ -362,6 +362,7 @@ __global__ void argmax_rows_kernel(long rows, int V, const float* __restrict__ x
 #define EA_GRID(n) dim3(ea_grid_cap(ea_cdiv((n), 256))), dim3(256), 0, (hipStream_t)stream
 
 extern "C" int ea_utterance_mvn(int B, int T, int F, const float* x, const long long* lens, float* y, void* stream) {
+  EA_ENTRY();
   EA_CHECK_ARG(F <= 256 && F > 0);
   const int bx = F <= 64 ? 64 : (F <= 128 ? 128 : 256);
   const int by = 1024 / bx;
@@ -371,6 +372,7 @@ extern "C" int ea_utterance_mvn(int B, int T, int F, const float* x, const long 
 }
 
 extern "C" int ea_subsample_lens(int B, int T, const long long* ilens, long long* olens, void* stream) {
+  EA_ENTRY();
   hipLaunchKernelGGL(subsample_lens_kernel, dim3(ea_cdiv(B, 64)), dim3(64), 0, (hipStream_t)stream, B, T, ilens, olens);
   EA_LAUNCH_CHECK();
   return 0;
@@ -378,6 +380,7 @@ extern "C" int ea_subsample_lens(int B, int T, const long long* ilens, long long
 
 extern "C" int ea_add_sos_eos(int B, int L, const long long* ys, long ldys, const long long* ylens, int sos, int eos,
                               int ignore_id, long long* ys_in, long long* ys_out, long long* ys_in_lens, void* stream) {
+  EA_ENTRY();
   hipLaunchKernelGGL(sos_eos_kernel, dim3(B), dim3(64), 0, (hipStream_t)stream, B, L, ys, ldys, ylens, sos, eos,
                      ignore_id, ys_in, ys_out, ys_in_lens);
   EA_LAUNCH_CHECK();
@@ -386,6 +389,7 @@ extern "C" int ea_add_sos_eos(int B, int L, const long long* ys, long ldys, cons
 
 extern "C" int ea_scale_dropout(long rows, int cols, const void* x, int x_dtype, long ldx, void* y, int y_dtype,
                                 long ldy, float scale, float p, unsigned long long seed, void* stream) {
+  EA_ENTRY();
   const long n = rows * cols;
   if (n == 0) return 0;
 #define EA_SD(TI, TO) hipLaunchKernelGGL((scale_drop_kernel<TI, TO>), EA_GRID(n), n, cols, (const TI*)x, ldx, (TO*)y, ldy, scale, p, (uint64_t)seed)
@@ -400,6 +404,7 @@ extern "C" int ea_scale_dropout(long rows, int cols, const void* x, int x_dtype,
 
 extern "C" int ea_add_2d(long rows, int cols, const void* x, int x_dtype, long ldx, void* y, int y_dtype,
                           long ldy, float alpha, void* stream) {
+  EA_ENTRY();
   const long n = rows * cols;
   if (n == 0) return 0;
 #define EA_A2(TI, TO) hipLaunchKernelGGL((add2d_kernel<TI, TO>), EA_GRID(n), n, cols, (const TI*)x, ldx, (TO*)y, ldy, alpha)
@@ -414,6 +419,7 @@ extern "C" int ea_add_2d(long rows, int cols, const void* x, int x_dtype, long l
 
 extern "C" int ea_permute3(int A, int Bd, int Cd, const void* src, int src_dtype, void* dst, int dst_dtype,
                            int accumulate, void* stream) {
+  EA_ENTRY();
   const long n = (long)A * Bd * Cd;
   if (n == 0) return 0;
 #define EA_P3(TI, TO) hipLaunchKernelGGL((permute3_kernel<TI, TO>), EA_GRID(n), A, Bd, Cd, (const TI*)src, (TO*)dst, accumulate)
@@ -427,6 +433,7 @@ extern "C" int ea_permute3(int A, int Bd, int Cd, const void* src, int src_dtype
 }
 
 extern "C" int ea_im2col_conv1(int B, int T, int F, const float* x, void* col, int col_dtype, void* stream) {
+  EA_ENTRY();
   const int T1 = (T - 3) / 2 + 1, F1 = (F - 3) / 2 + 1;
   const long n = (long)B * T1 * F1 * 16;
   if (col_dtype == EA_BF16)
@@ -438,6 +445,7 @@ extern "C" int ea_im2col_conv1(int B, int T, int F, const float* x, void* col, i
 }
 
 extern "C" int ea_im2col_conv2(int B, int T1, int F1, int C, const void* x1, void* col, int dtype, void* stream) {
+  EA_ENTRY();
   EA_CHECK_ARG(C % 8 == 0);
   const int T2 = (T1 - 3) / 2 + 1, F2 = (F1 - 3) / 2 + 1;
   const long n = (long)B * T2 * F2 * 9 * (C / 8);
@@ -451,6 +459,7 @@ extern "C" int ea_im2col_conv2(int B, int T1, int F1, int C, const void* x1, voi
 
 extern "C" int ea_col2im_conv2(int B, int T1, int F1, int C, const void* dcol, int dcol_dtype, const void* x1,
                                void* dx1, int dtype, void* stream) {
+  EA_ENTRY();
   const int T2 = (T1 - 3) / 2 + 1, F2 = (F1 - 3) / 2 + 1;
   const long n = (long)B * T1 * F1 * C;
 #define EA_C2I(TI, TO) hipLaunchKernelGGL((col2im_conv2_kernel<TI, TO>), EA_GRID(n), B, T1, F1, C, T2, F2, (const TI*)dcol, (const TO*)x1, (TO*)dx1)
@@ -464,6 +473,7 @@ extern "C" int ea_col2im_conv2(int B, int T1, int F1, int C, const void* dcol, i
 }
 
 extern "C" int ea_glu_fwd(long rows, int C, const void* x, int x_dtype, void* y, int y_dtype, void* stream) {
+  EA_ENTRY();
   const long n = rows * C;
 #define EA_G(TI, TO) hipLaunchKernelGGL((glu_fwd_kernel<TI, TO>), EA_GRID(n), rows, C, (const TI*)x, (TO*)y)
   if (x_dtype == EA_BF16 && y_dtype == EA_BF16) EA_G(bf16, bf16);
@@ -476,6 +486,7 @@ extern "C" int ea_glu_fwd(long rows, int C, const void* x, int x_dtype, void* y,
 }
 
 extern "C" int ea_glu_bwd(long rows, int C, const void* x, int x_dtype, const float* dy, void* dx, void* stream) {
+  EA_ENTRY();
   const long n = rows * C;
   if (x_dtype == EA_BF16)
     hipLaunchKernelGGL((glu_bwd_kernel<bf16, bf16>), EA_GRID(n), rows, C, (const bf16*)x, dy, (bf16*)dx);
@@ -487,6 +498,7 @@ extern "C" int ea_glu_bwd(long rows, int C, const void* x, int x_dtype, const fl
 
 extern "C" int ea_dwconv_fwd(int B, int T, int C, int K, const float* x, const float* w, const float* bias, float* y,
                              void* stream) {
+  EA_ENTRY();
   EA_CHECK_ARG(K % 2 == 1);
   dim3 grid(B * ea_cdiv(T, DW_TT), ea_cdiv(C, DW_CT));
   const size_t sm = (size_t)(DW_TT + K - 1) * DW_CT * sizeof(float);
@@ -498,6 +510,7 @@ extern "C" int ea_dwconv_fwd(int B, int T, int C, int K, const float* x, const f
 extern "C" int ea_dwconv_bwd(int B, int T, int C, int K, const float* x, const float* w, const float* dy, float* dx,
                              float* dw, float* dbias, int accumulate_params, float* workspace, long ws_elems,
                              void* stream) {
+  EA_ENTRY();
   EA_CHECK_ARG(K % 2 == 1);
   const int nblk = B * ea_cdiv(T, DW_TT);
   EA_CHECK_ARG((long)nblk * C * K <= ws_elems);
@@ -514,6 +527,7 @@ extern "C" int ea_dwconv_bwd(int B, int T, int C, int K, const float* x, const f
 
 extern "C" int ea_add_pos_bias(long N, int H, int dk, const void* q, long ldq, const float* u, const float* v,
                                void* qu, void* qv, int dtype, void* stream) {
+  EA_ENTRY();
   const long n = N * H * dk;
   if (dtype == EA_BF16)
     hipLaunchKernelGGL(add_pos_bias_kernel<bf16>, EA_GRID(n), N, H, dk, (const bf16*)q, ldq, u, v, (bf16*)qu, (bf16*)qv);
@@ -525,6 +539,7 @@ extern "C" int ea_add_pos_bias(long N, int H, int dk, const void* q, long ldq, c
 
 extern "C" int ea_embed_fwd(long rows, int d, int L, const long long* tok, const float* E, float xscale,
                             const float* pe, float p, unsigned long long seed, float* y, void* stream) {
+  EA_ENTRY();
   const long n = rows * d;
   hipLaunchKernelGGL(embed_fwd_kernel, EA_GRID(n), rows, d, L, tok, E, xscale, pe, p, (uint64_t)seed, y);
   EA_LAUNCH_CHECK();
@@ -533,6 +548,7 @@ extern "C" int ea_embed_fwd(long rows, int d, int L, const long long* tok, const
 
 extern "C" int ea_embed_bwd(long rows, int d, const long long* tok, const float* dy, float xscale, float p,
                             unsigned long long seed, float* dE, void* stream) {
+  EA_ENTRY();
   const long n = rows * d;
   hipLaunchKernelGGL(embed_bwd_kernel, EA_GRID(n), rows, d, tok, dy, xscale, p, (uint64_t)seed, dE);
   EA_LAUNCH_CHECK();
@@ -540,6 +556,7 @@ extern "C" int ea_embed_bwd(long rows, int d, const long long* tok, const float*
 }
 
 extern "C" int ea_argmax_rows(long rows, int V, const float* x, long ld, long long* out, void* stream) {
+  EA_ENTRY();
   hipLaunchKernelGGL(argmax_rows_kernel, dim3(ea_cdiv(rows, 4)), dim3(256), 0, (hipStream_t)stream, rows, V, x, ld, out);
   EA_LAUNCH_CHECK();
   return 0;

@@ -327,6 +327,7 @@ extern "C" int ea_gemm(int dtype, int a_kmajor, int b_kmajor, int M, int N, int 
                        int batch, int nh,
                        void* C, int c_dtype, long ldc, long sCb, long sCh,
                        const ea_epilogue* epi, float* workspace, long ws_elems, void* stream) {
+  EA_ENTRY();
   EA_CHECK_ARG(epi != nullptr && M >= 0 && N >= 0 && K >= 0 && batch >= 1 && nh >= 1);
   EA_CHECK_ARG(dtype == EA_F32 || dtype == EA_BF16);
   if (M == 0 || N == 0) return 0;

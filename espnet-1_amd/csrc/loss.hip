@@ -258,6 +258,7 @@ extern "C" int ea_ctc_loss_fwd(int B, int T, int V, const float* logits, long ld
                                const long long* ys, long ldys, const long long* ylens, int Lmax, float* lse,
                                double* alpha, double* beta, double* nll, float* loss_utt, float* loss,
                                void* stream) {
+  EA_ENTRY();
   hipStream_t st = (hipStream_t)stream;
   const long rows = (long)B * T;
   hipLaunchKernelGGL(lse_rows_kernel, dim3(ea_cdiv(rows, 4)), dim3(256), 0, st, rows, V, logits, ldt, lse);
@@ -276,6 +277,7 @@ extern "C" int ea_ctc_loss_bwd(int B, int T, int V, const float* logits, long ld
                                const double* alpha, const double* beta, const double* nll,
                                const float* gscale, float coef, void* grad, int grad_dtype, long ldg,
                                void* stream) {
+  EA_ENTRY();
   EA_CHECK_ARG(V <= 16384);
   const int Smax = 2 * Lmax + 1;
   CtcP p{B, T, V, Lmax, Smax, logits, ldt, lse, hlens, ys, ldys, ylens, (double*)alpha, (double*)beta,
@@ -293,6 +295,7 @@ extern "C" int ea_ctc_loss_bwd(int B, int T, int V, const float* logits, long ld
 extern "C" int ea_lsm_loss_fwd(long rows, int V, const float* x, long ldx, const long long* tgt, float smoothing,
                                int ignore_id, int normalize_length, float batch, float* lse, double* loss_row,
                                int* stat, float* loss, float* acc, float* inv_denom, void* stream) {
+  EA_ENTRY();
   hipStream_t st = (hipStream_t)stream;
   hipMemsetAsync(stat, 0, 2 * sizeof(int), st);
   LsmP p{rows, V, x, ldx, tgt, smoothing, ignore_id, lse, loss_row, stat};
@@ -306,6 +309,7 @@ extern "C" int ea_lsm_loss_fwd(long rows, int V, const float* x, long ldx, const
 extern "C" int ea_lsm_loss_bwd(long rows, int V, const float* x, long ldx, const long long* tgt, float smoothing,
                                int ignore_id, const float* lse, const float* gscale, const float* inv_denom,
                                float coef, void* grad, int grad_dtype, long ldg, void* stream) {
+  EA_ENTRY();
   LsmP p{rows, V, x, ldx, tgt, smoothing, ignore_id, (float*)lse, nullptr, nullptr};
   hipStream_t st = (hipStream_t)stream;
   if (grad_dtype == EA_BF16)

@@ -252,6 +252,7 @@ int ln_blocks(int rows) { return ea_grid_cap(ea_cdiv(rows, 4), 2048); }
 extern "C" int ea_layernorm_fwd(int rows, int d, const float* x, long ldx, const float* gamma,
                                 const float* beta, float eps, void* y, int y_dtype, long ldy,
                                 float* mean, float* rstd, void* stream) {
+  EA_ENTRY();
   if (rows == 0) return 0;
   dim3 grid(ln_blocks(rows)), blk(256);
   hipStream_t st = (hipStream_t)stream;
@@ -267,6 +268,7 @@ extern "C" int ea_layernorm_bwd(int rows, int d, const void* dy, int dy_dtype, l
                                 long ldx, const float* gamma, const float* mean, const float* rstd,
                                 float* dx, long lddx, int accumulate, float* dgamma, float* dbeta,
                                 int accumulate_params, float* workspace, long ws_elems, void* stream) {
+  EA_ENTRY();
   if (rows == 0) return 0;
   const int nb = min(ln_blocks(rows), 512);
   EA_CHECK_ARG(ws_elems >= (long)nb * 2 * d);
@@ -286,6 +288,7 @@ extern "C" int ea_layernorm_bwd(int rows, int d, const void* dy, int dy_dtype, l
 
 extern "C" int ea_reduce_partials(int nparts, int n, const float* part, long stride, float* out,
                                   int accumulate, void* stream) {
+  EA_ENTRY();
   if (n == 0) return 0;
   hipLaunchKernelGGL(reduce_partials_kernel, dim3(ea_cdiv(n, 256)), dim3(256), 0, (hipStream_t)stream,
                      nparts, n, part, stride, out, accumulate);
@@ -295,6 +298,7 @@ extern "C" int ea_reduce_partials(int nparts, int n, const float* part, long str
 
 extern "C" int ea_colsum(int rows, int n, const void* x, int x_dtype, long ld, float* out, int accumulate,
                          float* workspace, long ws_elems, void* stream) {
+  EA_ENTRY();
   if (n == 0) return 0;
   hipStream_t st = (hipStream_t)stream;
   int rpb = 64;
@@ -324,6 +328,7 @@ extern "C" int ea_batchnorm_fwd(int rows, int C, const float* y, const float* ga
                                 float* running_mean, float* running_var, long long* num_batches_tracked,
                                 int act, void* z, int z_dtype, float* workspace, long ws_elems,
                                 void* stream) {
+  EA_ENTRY();
   hipStream_t st = (hipStream_t)stream;
   const long total = (long)rows * C;
   if (training) {
@@ -354,6 +359,7 @@ extern "C" int ea_batchnorm_bwd(int rows, int C, const void* dz, int dz_dtype, c
                                 const float* rstd, const float* gamma, const float* beta, int act, float* dy,
                                 float* dgamma, float* dbeta, int accumulate_params, float* workspace,
                                 long ws_elems, void* stream) {
+  EA_ENTRY();
   hipStream_t st = (hipStream_t)stream;
   const long total = (long)rows * C;
   const int rpb = 32;

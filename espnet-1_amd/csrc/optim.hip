@@ -73,6 +73,7 @@ __global__ void axpby_scalar_kernel(const float* a, float wa, const float* b, fl
 }  // namespace
 
 extern "C" int ea_sqnorm(long n, const float* x, double* workspace, float* norm, void* stream) {
+  EA_ENTRY();
   hipStream_t st = (hipStream_t)stream;
   const int nb = ea_grid_cap(ea_cdiv(n, 256), 2048);
   hipLaunchKernelGGL(sqnorm_partial_kernel, dim3(nb), dim3(256), 0, st, n, x, workspace);
@@ -85,6 +86,7 @@ extern "C" int ea_sqnorm(long n, const float* x, double* workspace, float* norm,
 extern "C" int ea_adam_step(long n, float* params, const float* grads, float* exp_avg, float* exp_avg_sq,
                             void* params_bf16, float lr, float beta1, float beta2, float eps, float weight_decay,
                             long step, const float* grad_norm, float max_norm, void* stream) {
+  EA_ENTRY();
   EA_CHECK_ARG(step >= 1);
   AdamP a;
   a.n = n; a.p = params; a.g = grads; a.m = exp_avg; a.v = exp_avg_sq; a.p16 = (bf16*)params_bf16;
@@ -98,18 +100,21 @@ extern "C" int ea_adam_step(long n, float* params, const float* grads, float* ex
 }
 
 extern "C" int ea_cast_f32_bf16(long n, const float* x, void* y, void* stream) {
+  EA_ENTRY();
   hipLaunchKernelGGL(cast_kernel, dim3(ea_grid_cap(ea_cdiv(n, 256), 4096)), dim3(256), 0, (hipStream_t)stream, n, x, (bf16*)y);
   EA_LAUNCH_CHECK();
   return 0;
 }
 
 extern "C" int ea_scale_by_scalar(long n, float* x, const float* s, float c, void* stream) {
+  EA_ENTRY();
   hipLaunchKernelGGL(scale_inplace_kernel, dim3(ea_grid_cap(ea_cdiv(n, 256), 4096)), dim3(256), 0, (hipStream_t)stream, n, x, s, c);
   EA_LAUNCH_CHECK();
   return 0;
 }
 
 extern "C" int ea_axpby_scalar(const float* a, float wa, const float* b, float wb, float* out, void* stream) {
+  EA_ENTRY();
   hipLaunchKernelGGL(axpby_scalar_kernel, dim3(1), dim3(1), 0, (hipStream_t)stream, a, wa, b, wb, out);
   EA_LAUNCH_CHECK();
   return 0;

@@ -10,6 +10,12 @@ import ctypes
 import os
 import re
 
+# torch must be loaded BEFORE libespnet_amd.so: the PyTorch-ROCm wheel bundles its own
+# libamdhip64.so (soname libamdhip64.so.7).  Loading torch first makes our library's
+# libamdhip64.so.7 dependency resolve to that already-loaded runtime, so torch's streams
+# and allocations and our kernel launches share ONE HIP runtime in the process.
+import torch  # noqa: F401,E402
+
 _PKG = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_PKG, "lib", "libespnet_amd.so")
 HEADER = os.path.join(os.path.dirname(os.path.dirname(_PKG)), "include", "espnet_amd.h")

@@ -17,6 +17,35 @@ __all__ = ["dt", "stream", "gemm", "linear", "linear_dx", "linear_dw", "workspac
 _DT = {torch.float32: F32, torch.bfloat16: BF16}
 
 
+class KernelProbe:
+    """HIP-event brackets around named launches on the launching (current) stream, used by
+    bench.py to time the dominant kernel inside the timed region."""
+
+    def __init__(self, names):
+        self.names = set(names)
+        self.pairs = {n: [] for n in names}
+        self.active = True
+
+    def begin(self, name):
+        if self.active and name in self.names:
+            e = torch.cuda.Event(enable_timing=True)
+            e.record()
+            self.pairs[name].append([e, None])
+
+    def end(self, name):
+        if self.active and name in self.names:
+            e = torch.cuda.Event(enable_timing=True)
+            e.record()
+            self.pairs[name][-1][1] = e
+
+    def mean_ms(self, name):
+        ts = [a.elapsed_time(b) for a, b in self.pairs[name] if b is not None]
+        return sum(ts) / len(ts) if ts else float("nan"), len(ts)
+
+
+PROBE = None
+
+
 def dt(t: torch.Tensor) -> int:
     try:
         return _DT[t.dtype]

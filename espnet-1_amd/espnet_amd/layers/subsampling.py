@@ -107,7 +107,12 @@ class SubsampleFn(torch.autograd.Function):
         w2 = empty(C, 9 * C, dtype=cd, device=dev)
         ops.permute3(b.f("conv.2.weight"), w2, C, C, 9)  # (Co,Ci,9) -> (Co,9,Ci)
         x2 = empty(P2, C, dtype=cd, device=dev)
+        probe = ops.PROBE
+        if probe is not None:
+            probe.begin("conv2_gemm")
         ops.linear(col2, w2, x2, epi=ops.make_epi(EPI_ACT, bias=b.f("conv.2.bias"), act=ACT_RELU))
+        if probe is not None:
+            probe.end("conv2_gemm")
         # out.0 Linear on (t, f*C + c) rows, * sqrt(d), dropout (embedding.py:326)
         wl = empty(C, F2 * C, dtype=cd, device=dev)
         ops.permute3(b.f("out.0.weight"), wl, C, C, F2)  # (d, C, F2) -> (d, F2, C)

@@ -1,0 +1,81 @@
+"""torch.optim.Adam over the flat parameter arena (espnet2/tasks/abs_task.py:79-90 'adam').
+
+One kernel updates all parameters (plus the bf16 weight shadow) and folds in
+clip_grad_norm_ and the skip-on-non-finite rule of trainer.py:653-678, reading the grad
+norm from device memory — the step never synchronises with the host.
+state_dict() exposes the per-parameter torch.optim.Adam layout (exp_avg / exp_avg_sq
+views, step) so checkpoints interoperate with the reference's.
+"""
+from __future__ import annotations
+
+import torch
+
+from .. import hip_ops as ops
+from .._lib import lib
+
+
+class ArenaAdam(torch.optim.Optimizer):
+    def __init__(self, model, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.0, amsgrad=False):
+        if amsgrad:
+            raise NotImplementedError("amsgrad")
+        arena = model.arena
+        if arena is None:
+            raise RuntimeError("call model.prepare(device) before building the optimizer")
+        super().__init__(list(model.parameters()),
+                         dict(lr=lr, betas=betas, eps=eps, weight_decay=weight_decay, amsgrad=False))
+        self.arena = arena
+        self.exp_avg = torch.zeros_like(arena.data)
+        self.exp_avg_sq = torch.zeros_like(arena.data)
+        self.step_count = 0
+        self.grad_norm = torch.zeros(1, device=arena.device)
+        self._ws = torch.empty(4096, dtype=torch.float64, device=arena.device)
+
+    @torch.no_grad()
+    def compute_grad_norm(self):
+        """||all grads||_2 on device (clip_grad_norm_ norm_type=2)."""
+        a = self.arena
+        lib.ea_sqnorm(a.numel, a.grad.data_ptr(), self._ws.data_ptr(), self.grad_norm.data_ptr(), ops.stream())
+        return self.grad_norm
+
+    @torch.no_grad()
+    def step(self, closure=None, grad_norm=None, max_norm=0.0):
+        """Adam step; with grad_norm (device tensor) the clip coefficient
+        min(1, max_norm/(norm+1e-6)) is applied and a non-finite norm skips the update."""
+        g = self.param_groups[0]
+        self.step_count += 1
+        a = self.arena
+        b1, b2 = g["betas"]
+        lib.ea_adam_step(a.numel, a.data.data_ptr(), a.grad.data_ptr(), self.exp_avg.data_ptr(),
+                         self.exp_avg_sq.data_ptr(), ops.ptr(a.shadow), float(g["lr"]), b1, b2,
+                         float(g["eps"]), float(g["weight_decay"]), self.step_count,
+                         ops.ptr(grad_norm), float(max_norm), ops.stream())
+
+    def zero_grad(self, set_to_none: bool = False):
+        self.arena.grad.zero_()
+
+    def state_dict(self):
+        sd = super().state_dict()
+        st = {}
+        for i, n in enumerate(self.arena.names):
+            st[i] = dict(step=torch.tensor(float(self.step_count)),
+                         exp_avg=self.arena_view(self.exp_avg, n).clone(),
+                         exp_avg_sq=self.arena_view(self.exp_avg_sq, n).clone())
+        sd["state"] = st
+        return sd
+
+    def arena_view(self, buf, name):
+        o = self.arena.offsets[name]
+        p = self.arena._params[name]
+        return buf[o:o + p.numel()].view(p.shape)
+
+    def load_state_dict(self, state_dict):
+        st = state_dict["state"]
+        for i, n in enumerate(self.arena.names):
+            if i in st:
+                self.arena_view(self.exp_avg, n).copy_(st[i]["exp_avg"])
+                self.arena_view(self.exp_avg_sq, n).copy_(st[i]["exp_avg_sq"])
+                self.step_count = int(st[i]["step"])
+        for g, sg in zip(self.param_groups, state_dict["param_groups"]):
+            for k in ("lr", "betas", "eps", "weight_decay"):
+                if k in sg:
+                    g[k] = sg[k]
