@@ -110,14 +110,23 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(int rows, int d, const TI* 
   }
 }
 
-// out[c] (+)= sum_p part[p*stride + c], c < n   (fixed order -> deterministic)
-__global__ void reduce_partials_kernel(int nparts, int n, const float* __restrict__ part, long stride,
-                                       float* __restrict__ out, int accumulate) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= n) return;
+// out[c] (+)= sum_p part[p*stride + c], c < n.  Block = 64 columns x 4 part-lanes; each
+// lane sums a fixed strided subset of the parts, lanes combine in fixed order through LDS
+// (deterministic).  Keep nparts small (<= ~128) upstream: this is latency-, not BW-bound.
+__global__ __launch_bounds__(256) void reduce_partials_kernel(int nparts, int n, const float* __restrict__ part,
+                                                              long stride, float* __restrict__ out, int accumulate) {
+  __shared__ double red[4][64];
+  const int cx = threadIdx.x & 63, py = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + cx;
   double a = 0.0;
-  for (int p = 0; p < nparts; ++p) a += part[(long)p * stride + c];
-  out[c] = accumulate ? out[c] + (float)a : (float)a;
+  if (c < n)
+    for (int p = py; p < nparts; p += 4) a += part[(long)p * stride + c];
+  red[py][cx] = a;
+  __syncthreads();
+  if (py == 0 && c < n) {
+    const double t = (red[0][cx] + red[1][cx]) + (red[2][cx] + red[3][cx]);
+    out[c] = accumulate ? out[c] + (float)t : (float)t;
+  }
 }
 
 // column partial sums of x (rows x n, dtype) : part[blk][c] = sum over this block's rows
@@ -270,7 +279,7 @@ extern "C" int ea_layernorm_bwd(int rows, int d, const void* dy, int dy_dtype, l
                                 int accumulate_params, float* workspace, long ws_elems, void* stream) {
   EA_ENTRY();
   if (rows == 0) return 0;
-  const int nb = min(ln_blocks(rows), 512);
+  const int nb = min(ln_blocks(rows), 128);
   EA_CHECK_ARG(ws_elems >= (long)nb * 2 * d);
   EA_CHECK_ARG(dbeta == dgamma + d);  // grads of (weight, bias) are adjacent in the arena
   dim3 grid(nb), blk(256);
@@ -280,7 +289,7 @@ extern "C" int ea_layernorm_bwd(int rows, int d, const void* dy, int dy_dtype, l
   else
     EA_LN_DISPATCH(ln_bwd_kernel, float, grid, blk, 0, st, rows, d, (const float*)dy, lddy, x, ldx, gamma, mean, rstd, dx, lddx, accumulate, workspace);
   EA_LAUNCH_CHECK();
-  hipLaunchKernelGGL(reduce_partials_kernel, dim3(ea_cdiv(2 * d, 256)), dim3(256), 0, st, nb, 2 * d,
+  hipLaunchKernelGGL(reduce_partials_kernel, dim3(ea_cdiv(2 * d, 64)), dim3(256), 0, st, nb, 2 * d,
                      workspace, (long)2 * d, dgamma, accumulate_params);
   EA_LAUNCH_CHECK();
   return 0;
@@ -290,7 +299,7 @@ extern "C" int ea_reduce_partials(int nparts, int n, const float* part, long str
                                   int accumulate, void* stream) {
   EA_ENTRY();
   if (n == 0) return 0;
-  hipLaunchKernelGGL(reduce_partials_kernel, dim3(ea_cdiv(n, 256)), dim3(256), 0, (hipStream_t)stream,
+  hipLaunchKernelGGL(reduce_partials_kernel, dim3(ea_cdiv(n, 64)), dim3(256), 0, (hipStream_t)stream,
                      nparts, n, part, stride, out, accumulate);
   EA_LAUNCH_CHECK();
   return 0;
@@ -301,7 +310,7 @@ extern "C" int ea_colsum(int rows, int n, const void* x, int x_dtype, long ld, f
   EA_ENTRY();
   if (n == 0) return 0;
   hipStream_t st = (hipStream_t)stream;
-  int rpb = 64;
+  int rpb = max(16, ea_cdiv(rows, 64));
   int nparts = ea_cdiv(rows, rpb);
   while ((long)nparts * n > ws_elems && rpb < (1 << 20)) {
     rpb *= 2;
@@ -317,7 +326,7 @@ extern "C" int ea_colsum(int rows, int n, const void* x, int x_dtype, long ld, f
       hipLaunchKernelGGL(colsum_partial_kernel<float>, grid, dim3(256), 0, st, rows, n, (const float*)x, ld, rpb, workspace);
     EA_LAUNCH_CHECK();
   }
-  hipLaunchKernelGGL(reduce_partials_kernel, dim3(ea_cdiv(n, 256)), dim3(256), 0, st, nparts, n, workspace,
+  hipLaunchKernelGGL(reduce_partials_kernel, dim3(ea_cdiv(n, 64)), dim3(256), 0, st, nparts, n, workspace,
                      (long)n, out, accumulate);
   EA_LAUNCH_CHECK();
   return 0;
@@ -332,7 +341,7 @@ extern "C" int ea_batchnorm_fwd(int rows, int C, const float* y, const float* ga
   hipStream_t st = (hipStream_t)stream;
   const long total = (long)rows * C;
   if (training) {
-    const int rpb = 32;
+    const int rpb = max(32, ea_cdiv(rows, 64));
     const int nparts = ea_cdiv(rows, rpb);
     EA_CHECK_ARG((long)nparts * 2 * C <= ws_elems && rows > 0);
     hipLaunchKernelGGL(bn_partial_kernel, dim3(ea_cdiv(C, 256), nparts), dim3(256), 0, st, rows, C, y, rpb, workspace);
@@ -362,7 +371,7 @@ extern "C" int ea_batchnorm_bwd(int rows, int C, const void* dz, int dz_dtype, c
   EA_ENTRY();
   hipStream_t st = (hipStream_t)stream;
   const long total = (long)rows * C;
-  const int rpb = 32;
+  const int rpb = max(32, ea_cdiv(rows, 64));
   const int nparts = ea_cdiv(rows, rpb);
   EA_CHECK_ARG((long)nparts * 2 * C + 2 * C <= ws_elems && rows > 0);
   EA_CHECK_ARG(dbeta == dgamma + C);
@@ -373,7 +382,7 @@ extern "C" int ea_batchnorm_bwd(int rows, int C, const void* dz, int dz_dtype, c
   else
     hipLaunchKernelGGL(bn_bwd_partial_kernel<float>, g1, dim3(256), 0, st, rows, C, (const float*)dz, y, mean, rstd, gamma, beta, act, rpb, workspace);
   EA_LAUNCH_CHECK();
-  hipLaunchKernelGGL(reduce_partials_kernel, dim3(ea_cdiv(2 * C, 256)), dim3(256), 0, st, nparts, 2 * C, workspace,
+  hipLaunchKernelGGL(reduce_partials_kernel, dim3(ea_cdiv(2 * C, 64)), dim3(256), 0, st, nparts, 2 * C, workspace,
                      (long)2 * C, sums, 0);
   EA_LAUNCH_CHECK();
   dim3 g2(ea_grid_cap(ea_cdiv(total, 256)));
@@ -383,7 +392,7 @@ extern "C" int ea_batchnorm_bwd(int rows, int C, const void* dz, int dz_dtype, c
     hipLaunchKernelGGL(bn_bwd_apply_kernel<float>, g2, dim3(256), 0, st, total, C, rows, (const float*)dz, y, mean, rstd, gamma, beta, act, sums, sums + C, dy);
   EA_LAUNCH_CHECK();
   // parameter grads: dgamma = sum dh*xhat, dbeta = sum dh
-  hipLaunchKernelGGL(reduce_partials_kernel, dim3(ea_cdiv(2 * C, 256)), dim3(256), 0, st, 1, 2 * C, sums,
+  hipLaunchKernelGGL(reduce_partials_kernel, dim3(ea_cdiv(2 * C, 64)), dim3(256), 0, st, 1, 2 * C, sums,
                      (long)2 * C, dgamma, accumulate_params);
   EA_LAUNCH_CHECK();
   return 0;
