@@ -289,6 +289,163 @@ __global__ __launch_bounds__(NT, 2) void gemm_kernel(GemmP p) {
   }
 }
 
+
+// ---------------------------------------------------------------- bf16 LDS-DMA kernel
+// Same tile/fragment/epilogue scheme as gemm_kernel, but operands move HBM -> LDS with
+// global_load_lds_dwordx4 (no staging registers) into a STAGES-deep ring: the tile kt+S-1
+// is in flight while tile kt is multiplied; one raw s_barrier per K-tile, counted
+// vmcnt waits (never a vmcnt(0) inside the loop).  The LDS image is the same swizzled
+// image as gemm_kernel: the swizzle is applied to each lane's SOURCE address since an
+// LDS-DMA writes lane-linearly.  M/N edges clamp the source row (results discarded);
+// a K remainder (< 64) is loaded once through registers with zero fill.
+template <int N>
+EA_DEV void wait_vmcnt() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+EA_DEV void lds_barrier() {
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
+template <bool AK, bool BKM, int STAGES>
+__global__ __launch_bounds__(NT, 1) void gemm_bf16_lds(GemmP p) {
+  constexpr int BK = 64;
+  constexpr int STAGE_BYTES = 2 * TILE_BYTES;
+  __shared__ __attribute__((aligned(1024))) char smem[STAGES * STAGE_BYTES];
+
+  const int nt = p.tiles_m * p.tiles_n;
+  const int bid = blockIdx.x;
+  const int q = nt / 8, r = nt % 8, xcd = bid % 8;
+  const int t = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + bid / 8;
+  const int GM = 8;
+  const int grp = t / (GM * p.tiles_n);
+  const int gm0 = grp * GM;
+  const int gsz = min(GM, p.tiles_m - gm0);
+  const int tm = gm0 + (t % (GM * p.tiles_n)) % gsz;
+  const int tn = (t % (GM * p.tiles_n)) / gsz;
+  const int m0 = tm * BM, n0 = tn * BN;
+
+  const int z = blockIdx.z / p.splitk, sk = blockIdx.z % p.splitk;
+  const int zb = z / p.nh, zh = z % p.nh;
+  const bf16* A = (const bf16*)p.A + zb * p.sAb + zh * p.sAh;
+  const bf16* B = (const bf16*)p.B + zb * p.sBb + zh * p.sBh;
+  const int kbeg = sk * p.kchunk;
+  const int kend = min(p.K, kbeg + p.kchunk);
+  const int nfull = max(0, (kend - kbeg) / BK);
+  const bool tail = kbeg + nfull * BK < kend;
+
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int wm = (w >> 1) * 64, wn = (w & 1) * 64;
+
+  // per-thread DMA sources (4 chunks of A, 4 of B per K-tile)
+  const bf16* asrc[4];
+  const bf16* bsrc[4];
+  long astep, bstep;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int ci = (i * 4 + w) * 64 + lane;
+    if (AK) {
+      const int row = ci >> 3, c = (ci & 7) ^ swz_k(ci >> 3);
+      asrc[i] = A + (long)min(m0 + row, p.M - 1) * p.lda + kbeg + c * 8;
+    } else {
+      const int k = ci >> 4, c = (ci & 15) ^ swz_mn_bf16(ci >> 4);
+      asrc[i] = A + (long)(kbeg + k) * p.lda + min((long)(m0 + c * 8), p.lda - 8);
+    }
+    if (BKM) {
+      const int row = ci >> 3, c = (ci & 7) ^ swz_k(ci >> 3);
+      bsrc[i] = B + (long)min(n0 + row, p.N - 1) * p.ldb + kbeg + c * 8;
+    } else {
+      const int k = ci >> 4, c = (ci & 15) ^ swz_mn_bf16(ci >> 4);
+      bsrc[i] = B + (long)(kbeg + k) * p.ldb + min((long)(n0 + c * 8), p.ldb - 8);
+    }
+  }
+  astep = AK ? BK : (long)BK * p.lda;
+  bstep = BKM ? BK : (long)BK * p.ldb;
+
+  auto issue = [&](int kt, int stg) {
+    char* base = smem + stg * STAGE_BYTES;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)(asrc[i] + kt * astep),
+                                       (__attribute__((address_space(3))) void*)(base + (i * 4 + w) * 1024), 16, 0, 0);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)(bsrc[i] + kt * bstep),
+                                       (__attribute__((address_space(3))) void*)(base + TILE_BYTES + (i * 4 + w) * 1024),
+                                       16, 0, 0);
+  };
+
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+  auto compute = [&](int stg) {
+    const char* la = smem + stg * STAGE_BYTES;
+    const char* lb = la + TILE_BYTES;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      bf16x8 fa[4], fb[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) fa[i] = frag_bf16<AK>(la, wm + i * 16, ks, lane);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) fb[j] = frag_bf16<BKM>(lb, wn + j * 16, ks, lane);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+    }
+  };
+
+  const int npre = min(STAGES - 1, nfull);
+  for (int kt = 0; kt < npre; ++kt) issue(kt, kt);
+  for (int kt = 0; kt < nfull; ++kt) {
+    const int after = min(STAGES - 2, nfull - 1 - kt);  // newer tiles allowed in flight
+    if (after >= 2) wait_vmcnt<16>();
+    else if (after == 1) wait_vmcnt<8>();
+    else wait_vmcnt<0>();
+    lds_barrier();
+    if (kt + STAGES - 1 < nfull) issue(kt + STAGES - 1, (kt + STAGES - 1) % STAGES);
+    compute(kt % STAGES);
+  }
+  if (tail) {
+    uint4 ra[4], rb[4];
+    const int k0 = kbeg + nfull * BK;
+    load_tile<bf16, AK>(A, p.lda, m0, p.M, k0, kend, 1, ra);
+    load_tile<bf16, BKM>(B, p.ldb, n0, p.N, k0, kend, 1, rb);
+    __syncthreads();
+    char* base = smem + (nfull % STAGES) * STAGE_BYTES;
+    store_tile<bf16, AK>(base, ra);
+    store_tile<bf16, BKM>(base + TILE_BYTES, rb);
+    __syncthreads();
+    compute(nfull % STAGES);
+  }
+
+  if (p.splitk > 1) {
+    const int rq = (lane >> 4) * 4, cc = lane & 15;
+    float* slab = p.ws + ((long)z * p.splitk + sk) * (long)p.M * p.N;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int rr = 0; rr < 4; ++rr) {
+          const int row = m0 + wm + i * 16 + rq + rr, col = n0 + wn + j * 16 + cc;
+          if (row < p.M && col < p.N) slab[(long)row * p.N + col] = acc[i][j][rr];
+        }
+    return;
+  }
+  switch (p.epi.kind) {
+    case EA_EPI_STORE: epi_tile<EA_EPI_STORE>(p, z, zb, zh, m0 + wm, n0 + wn, lane, acc); break;
+    case EA_EPI_ACT: epi_tile<EA_EPI_ACT>(p, z, zb, zh, m0 + wm, n0 + wn, lane, acc); break;
+    case EA_EPI_RESID: epi_tile<EA_EPI_RESID>(p, z, zb, zh, m0 + wm, n0 + wn, lane, acc); break;
+    default: epi_tile<EA_EPI_DACT>(p, z, zb, zh, m0 + wm, n0 + wn, lane, acc); break;
+  }
+}
+
 // split-K combine: C = epi(sum_s slab[s]) for EA_EPI_STORE
 __global__ void splitk_reduce(GemmP p) {
   const long MN = (long)p.M * p.N;
@@ -303,8 +460,27 @@ __global__ void splitk_reduce(GemmP p) {
   }
 }
 
+int g_gemm_stages = 2;  // LDS ring depth of gemm_bf16_lds (2: 64 KiB, 2 blocks/CU; 3: 96 KiB)
+
+int launch_lds(GemmP& p, int a_k, int b_k, int nz, hipStream_t st) {
+  dim3 grid(p.tiles_m * p.tiles_n, 1, nz * p.splitk);
+#define EA_GL_CASE(AKV, BKV)                                                                        \
+  if (a_k == AKV && b_k == BKV) {                                                                   \
+    if (g_gemm_stages >= 3) hipLaunchKernelGGL((gemm_bf16_lds<AKV, BKV, 3>), grid, dim3(NT), 0, st, p); \
+    else hipLaunchKernelGGL((gemm_bf16_lds<AKV, BKV, 2>), grid, dim3(NT), 0, st, p);               \
+  }
+  EA_GL_CASE(true, true)
+  else EA_GL_CASE(true, false)
+  else EA_GL_CASE(false, true)
+  else EA_GL_CASE(false, false)
+#undef EA_GL_CASE
+  EA_LAUNCH_CHECK();
+  return 0;
+}
+
 template <typename T>
 int launch(GemmP& p, int a_k, int b_k, int nz, hipStream_t st) {
+  if (sizeof(T) == 2 && p.vec_a && p.vec_b && g_gemm_stages > 0) return launch_lds(p, a_k, b_k, nz, st);
   dim3 grid(p.tiles_m * p.tiles_n, 1, nz * p.splitk);
 #define EA_GEMM_CASE(AKV, BKV)                                                      \
   if (a_k == AKV && b_k == BKV) {                                                   \
@@ -320,6 +496,13 @@ int launch(GemmP& p, int a_k, int b_k, int nz, hipStream_t st) {
 }
 
 }  // namespace
+
+extern "C" int ea_gemm_set_pipeline(int stages) {
+  EA_ENTRY();
+  EA_CHECK_ARG(stages == 0 || stages == 2 || stages == 3);
+  g_gemm_stages = stages;
+  return 0;
+}
 
 extern "C" int ea_gemm(int dtype, int a_kmajor, int b_kmajor, int M, int N, int K,
                        const void* A, long lda, long sAb, long sAh,

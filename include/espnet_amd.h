@@ -66,6 +66,10 @@ int ea_gemm(int dtype, int a_kmajor, int b_kmajor, int M, int N, int K,
             const ea_epilogue* epi, float* workspace, long ws_elems, void* stream);
 
 
+/* Select the bf16 GEMM main loop: 2 or 3 = LDS-DMA (global_load_lds) ring of that depth
+ * (default 2), 0 = register-staged loop.  Process-wide; for A/B measurements. */
+int ea_gemm_set_pipeline(int stages);
+
 /* ---------------------------------------------------------------- normalisation */
 
 /* LayerNorm(eps) over the last dim, one wave64 per row; y in y_dtype, saves mean/rstd.

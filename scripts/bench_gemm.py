@@ -18,11 +18,21 @@ def bench(name, dtype, M, N, K, a_k, b_k, iters=20):
     ms = e0.elapsed_time(e1) / iters
     print(f"{name:28s} {str(dtype):15s} M={M:6d} N={N:5d} K={K:5d} ak={a_k} bk={b_k}: {ms*1e3:8.1f} us  {2*M*N*K/ms/1e9:7.1f} TF/s", flush=True)
 
-for dt in (torch.bfloat16, torch.float32):
+from espnet_amd._lib import lib
+import sys as _s
+pipes = [int(x) for x in (_s.argv[1].split(",") if len(_s.argv) > 1 else ["2"])]
+for pipe in pipes:
+  lib.ea_gemm_set_pipeline(pipe)
+  print("pipeline", pipe)
+  for dt in (torch.bfloat16,):
     bench("ffn_w1 fwd", dt, 7968, 2048, 512, 1, 1)
     bench("ffn_w2 fwd", dt, 7968, 512, 2048, 1, 1)
     bench("qkv fwd", dt, 7968, 1536, 512, 1, 1)
     bench("ffn_w1 dX", dt, 7968, 512, 2048, 1, 0)
     bench("ffn_w1 dW", dt, 2048, 512, 7968, 0, 0)
-    bench("conv2 implicit (im2col)", dt, 151392, 512, 4608, 1, 1, iters=3)
+    bench("ctc_lo fwd", dt, 7968, 5000, 512, 1, 1)
+    bench("conv2 fwd", dt, 151392, 512, 4608, 1, 1, iters=5)
+    bench("conv2 dcol", dt, 151392, 4608, 512, 1, 0, iters=5)
+    bench("conv2 dW", dt, 512, 4608, 151392, 0, 0, iters=5)
     bench("square 4096", dt, 4096, 4096, 4096, 1, 1, iters=5)
+    bench("square 8192", dt, 8192, 8192, 8192, 1, 1, iters=3)
