@@ -36,6 +36,7 @@ struct GemmP {
   float* ws;  // split-K partial slabs [z][s][M][N]
   int tiles_m, tiles_n;
   int vec_a, vec_b;  // 16-B vector loads allowed (aligned base, ld and batch strides)
+  int vec_c;         // 4-column vector epilogue allowed (aligned C/aux/resid/bias, N % 4 == 0)
 };
 
 EA_DEV int swz_k(int row) { return (row >> 1) & 7; }                         // K-major rows
@@ -177,6 +178,134 @@ EA_DEV void epi_tile(const GemmP& p, int z, int zb, int zh, int r0, int c0, int 
       }
 }
 
+
+// ---------------------------------------------------------------- vectorised epilogue
+// 4 consecutive columns per lane: 16-B f32 / 8-B bf16 loads and stores instead of the
+// MFMA layout's 2-4-B scattered accesses.  The accumulator tile is transposed through
+// LDS (each wave its own 64 x 68-float region) before this runs.
+EA_DEV void ld4(const void* p, long i, int dt, float (&v)[4]) {
+  if (dt == EA_BF16) {
+    const uint2 u = *(const uint2*)((const bf16*)p + i);
+    const bf16* b = (const bf16*)&u;
+    v[0] = (float)b[0]; v[1] = (float)b[1]; v[2] = (float)b[2]; v[3] = (float)b[3];
+  } else {
+    const float4 f = *(const float4*)((const float*)p + i);
+    v[0] = f.x; v[1] = f.y; v[2] = f.z; v[3] = f.w;
+  }
+}
+EA_DEV void st4(void* p, long i, int dt, const float (&v)[4]) {
+  if (dt == EA_BF16) {
+    uint2 u;
+    bf16* b = (bf16*)&u;
+    b[0] = (bf16)v[0]; b[1] = (bf16)v[1]; b[2] = (bf16)v[2]; b[3] = (bf16)v[3];
+    *(uint2*)((bf16*)p + i) = u;
+  } else {
+    *(float4*)((float*)p + i) = make_float4(v[0], v[1], v[2], v[3]);
+  }
+}
+
+template <int KIND>
+EA_DEV void epi_four(const GemmP& p, int z, int zb, int zh, int row, int col, const float (&acc)[4]) {
+  const ea_epilogue& e = p.epi;
+  const long cidx = zb * p.sCb + zh * p.sCh + (long)row * p.ldc + col;
+  const uint64_t didx = ((uint64_t)z * p.M + row) * (uint64_t)p.N + col;
+  float v[4];
+#pragma unroll
+  for (int c = 0; c < 4; ++c) v[c] = e.alpha * acc[c];
+  if (KIND != EA_EPI_DACT && e.bias) {
+    const float4 bb = *(const float4*)(e.bias + col);
+    v[0] += bb.x; v[1] += bb.y; v[2] += bb.z; v[3] += bb.w;
+  }
+  if constexpr (KIND == EA_EPI_STORE) {
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      v[c] *= e.post_scale;
+      if (e.drop_p > 0.f) v[c] *= drop_scale(e.seed, didx + c, e.drop_p);
+    }
+    if (e.beta != 0.f) {
+      float o[4];
+      ld4(p.C, cidx, p.c_dtype, o);
+#pragma unroll
+      for (int c = 0; c < 4; ++c) v[c] += e.beta * o[c];
+    }
+    st4(p.C, cidx, p.c_dtype, v);
+  } else if constexpr (KIND == EA_EPI_ACT) {
+    if (e.aux) st4(e.aux, (long)row * e.ldaux + col, e.aux_dtype, v);
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      v[c] = act_fwd(e.act, v[c]);
+      if (e.drop_p > 0.f) v[c] *= drop_scale(e.seed, didx + c, e.drop_p);
+    }
+    st4(p.C, cidx, p.c_dtype, v);
+  } else if constexpr (KIND == EA_EPI_RESID) {
+    float r[4] = {0.f, 0.f, 0.f, 0.f};
+    if (e.resid) ld4(e.resid, (long)row * e.ldr + col, EA_F32, r);
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      if (e.drop_p > 0.f) v[c] *= drop_scale(e.seed, didx + c, e.drop_p);
+      v[c] = r[c] + e.rscale * v[c];
+    }
+    st4(p.C, cidx, EA_F32, v);
+  } else {
+    float h[4];
+    ld4(e.aux, (long)row * e.ldaux + col, e.aux_dtype, h);
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      if (e.drop_p > 0.f) v[c] *= drop_scale(e.seed, didx + c, e.drop_p);
+      v[c] *= act_bwd(e.act, h[c]);
+    }
+    st4(p.C, cidx, p.c_dtype, v);
+  }
+}
+
+constexpr int EPI_LDT = 68;  // floats per LDS row of a wave's 64x64 accumulator tile
+
+// Transpose the wave's 64x64 accumulators through LDS, then apply the epilogue four
+// columns at a time.  `vec` (host-checked alignment of C/aux/resid/bias and N % 4 == 0)
+// selects the vector path; otherwise element-wise.
+template <int KIND>
+EA_DEV void epi_tile_lds(const GemmP& p, char* smem, int z, int zb, int zh, int r0, int c0, int lane, int w,
+                         const f32x4 (&acc)[4][4]) {
+  float* t = (float*)smem + w * 64 * EPI_LDT;
+  const int rq = (lane >> 4) * 4, cc = lane & 15;
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr) t[(i * 16 + rq + rr) * EPI_LDT + j * 16 + cc] = acc[i][j][rr];
+  __builtin_amdgcn_wave_barrier();
+  asm volatile("" ::: "memory");
+  const int lc = (lane & 15) * 4;
+#pragma unroll 4
+  for (int it = 0; it < 16; ++it) {
+    const int lr = it * 4 + (lane >> 4);
+    const int row = r0 + lr, col = c0 + lc;
+    if (row >= p.M || col >= p.N) continue;
+    const float4 f = *(const float4*)(t + lr * EPI_LDT + lc);
+    const float v[4] = {f.x, f.y, f.z, f.w};
+    if (p.vec_c && col + 3 < p.N) {
+      if (p.splitk > 1) {
+        float* slab = p.ws + ((long)z * p.splitk + (blockIdx.z % p.splitk)) * (long)p.M * p.N;
+        *(float4*)(slab + (long)row * p.N + col) = f;
+      } else {
+        epi_four<KIND>(p, z, zb, zh, row, col, v);
+      }
+    } else {
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        if (col + c >= p.N) break;
+        if (p.splitk > 1) {
+          float* slab = p.ws + ((long)z * p.splitk + (blockIdx.z % p.splitk)) * (long)p.M * p.N;
+          slab[(long)row * p.N + col + c] = v[c];
+        } else {
+          epi_one<KIND>(p, z, zb, zh, row, col + c, v[c]);
+        }
+      }
+    }
+  }
+}
+
 // ---------------------------------------------------------------- kernel
 template <typename T, bool AK, bool BKM>
 __global__ __launch_bounds__(NT, 2) void gemm_kernel(GemmP p) {
@@ -312,7 +441,9 @@ template <bool AK, bool BKM, int STAGES>
 __global__ __launch_bounds__(NT, 1) void gemm_bf16_lds(GemmP p) {
   constexpr int BK = 64;
   constexpr int STAGE_BYTES = 2 * TILE_BYTES;
-  __shared__ __attribute__((aligned(1024))) char smem[STAGES * STAGE_BYTES];
+  constexpr int EPI_BYTES = 4 * 64 * EPI_LDT * 4;
+  constexpr int SMEM = STAGES * STAGE_BYTES > EPI_BYTES ? STAGES * STAGE_BYTES : EPI_BYTES;
+  __shared__ __attribute__((aligned(1024))) char smem[SMEM];
 
   const int nt = p.tiles_m * p.tiles_n;
   const int bid = blockIdx.x;
@@ -424,39 +555,43 @@ __global__ __launch_bounds__(NT, 1) void gemm_bf16_lds(GemmP p) {
     compute(nfull % STAGES);
   }
 
-  if (p.splitk > 1) {
-    const int rq = (lane >> 4) * 4, cc = lane & 15;
-    float* slab = p.ws + ((long)z * p.splitk + sk) * (long)p.M * p.N;
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-#pragma unroll
-        for (int rr = 0; rr < 4; ++rr) {
-          const int row = m0 + wm + i * 16 + rq + rr, col = n0 + wn + j * 16 + cc;
-          if (row < p.M && col < p.N) slab[(long)row * p.N + col] = acc[i][j][rr];
-        }
-    return;
-  }
-  switch (p.epi.kind) {
-    case EA_EPI_STORE: epi_tile<EA_EPI_STORE>(p, z, zb, zh, m0 + wm, n0 + wn, lane, acc); break;
-    case EA_EPI_ACT: epi_tile<EA_EPI_ACT>(p, z, zb, zh, m0 + wm, n0 + wn, lane, acc); break;
-    case EA_EPI_RESID: epi_tile<EA_EPI_RESID>(p, z, zb, zh, m0 + wm, n0 + wn, lane, acc); break;
-    default: epi_tile<EA_EPI_DACT>(p, z, zb, zh, m0 + wm, n0 + wn, lane, acc); break;
+  __syncthreads();  // every wave is done reading the operand ring: reuse it for the epilogue
+  switch (p.splitk > 1 ? EA_EPI_STORE : p.epi.kind) {
+    case EA_EPI_STORE: epi_tile_lds<EA_EPI_STORE>(p, smem, z, zb, zh, m0 + wm, n0 + wn, lane, w, acc); break;
+    case EA_EPI_ACT: epi_tile_lds<EA_EPI_ACT>(p, smem, z, zb, zh, m0 + wm, n0 + wn, lane, w, acc); break;
+    case EA_EPI_RESID: epi_tile_lds<EA_EPI_RESID>(p, smem, z, zb, zh, m0 + wm, n0 + wn, lane, w, acc); break;
+    default: epi_tile_lds<EA_EPI_DACT>(p, smem, z, zb, zh, m0 + wm, n0 + wn, lane, w, acc); break;
   }
 }
 
-// split-K combine: C = epi(sum_s slab[s]) for EA_EPI_STORE
+// split-K combine: C = epi(sum_s slab[s]) (any epilogue kind), 4 columns per thread
 __global__ void splitk_reduce(GemmP p) {
   const long MN = (long)p.M * p.N;
   const int z = blockIdx.y;
   const int zb = z / p.nh, zh = z % p.nh;
-  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < MN; i += (long)gridDim.x * blockDim.x) {
-    const float* slab = p.ws + (long)z * p.splitk * MN + i;
-    float a = 0.f;
-    for (int s = 0; s < p.splitk; ++s) a += slab[s * MN];
-    const int row = (int)(i / p.N), col = (int)(i % p.N);
-    epi_apply(p, z, zb, zh, row, col, a);
+  const float* base = p.ws + (long)z * p.splitk * MN;
+  const bool vec = p.vec_c && (p.N % 4 == 0);
+  const long n4 = vec ? MN / 4 : MN;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n4; i += (long)gridDim.x * blockDim.x) {
+    if (vec) {
+      float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
+      for (int s = 0; s < p.splitk; ++s) {
+        const float4 b = *(const float4*)(base + s * MN + i * 4);
+        a.x += b.x; a.y += b.y; a.z += b.z; a.w += b.w;
+      }
+      const int row = (int)(i * 4 / p.N), col = (int)(i * 4 % p.N);
+      const float v[4] = {a.x, a.y, a.z, a.w};
+      switch (p.epi.kind) {
+        case EA_EPI_STORE: epi_four<EA_EPI_STORE>(p, z, zb, zh, row, col, v); break;
+        case EA_EPI_ACT: epi_four<EA_EPI_ACT>(p, z, zb, zh, row, col, v); break;
+        case EA_EPI_RESID: epi_four<EA_EPI_RESID>(p, z, zb, zh, row, col, v); break;
+        default: epi_four<EA_EPI_DACT>(p, z, zb, zh, row, col, v); break;
+      }
+    } else {
+      float a = 0.f;
+      for (int s = 0; s < p.splitk; ++s) a += base[s * MN + i];
+      epi_apply(p, z, zb, zh, (int)(i / p.N), (int)(i % p.N), a);
+    }
   }
 }
 
@@ -531,15 +666,23 @@ extern "C" int ea_gemm(int dtype, int a_kmajor, int b_kmajor, int M, int N, int 
   // unaligned operands (odd vocab / leading dims) take the element-wise load path
   p.vec_a = (lda % E == 0 && sAb % E == 0 && sAh % E == 0 && ((uintptr_t)A % 16) == 0);
   p.vec_b = (ldb % E == 0 && sBb % E == 0 && sBh % E == 0 && ((uintptr_t)B % 16) == 0);
+  {
+    const int ce = c_dtype == EA_BF16 ? 2 : 4;
+    bool vc = (N % 4 == 0) && ldc % 4 == 0 && sCb % 4 == 0 && sCh % 4 == 0 && ((uintptr_t)C % (4 * ce)) == 0;
+    if (epi->bias) vc = vc && ((uintptr_t)epi->bias % 16) == 0;
+    if (epi->aux) vc = vc && epi->ldaux % 4 == 0 && ((uintptr_t)epi->aux % (4 * (epi->aux_dtype == EA_BF16 ? 2 : 4))) == 0;
+    if (epi->resid) vc = vc && epi->ldr % 4 == 0 && ((uintptr_t)epi->resid % 16) == 0;
+    p.vec_c = vc;
+  }
   const int KT = dtype == EA_BF16 ? KCfg<bf16>::KT : KCfg<float>::KT;
   const int nz = batch * nh;
   // split-K when the output grid cannot fill the 256 CUs and K is long (dW GEMMs)
   int splitk = 1;
   const long tiles = (long)p.tiles_m * p.tiles_n * nz;
-  if (workspace && epi->kind == EA_EPI_STORE && tiles < 256 && K >= 4 * KT) {
-    splitk = (int)((512 + tiles - 1) / tiles);
-    splitk = min(splitk, K / (2 * KT));
-    splitk = min(splitk, 32);
+  if (workspace && tiles < 200 && K >= 8 * KT) {
+    splitk = (int)((384 + tiles - 1) / tiles);
+    splitk = min(splitk, K / (4 * KT));
+    splitk = min(splitk, 16);
     while (splitk > 1 && (long)splitk * nz * M * N > ws_elems) --splitk;
     if (splitk < 1) splitk = 1;
   }
@@ -556,7 +699,7 @@ extern "C" int ea_gemm(int dtype, int a_kmajor, int b_kmajor, int M, int N, int 
   if (rc) return rc;
   if (splitk > 1) {
     const long MN = (long)M * N;
-    dim3 grid(ea_grid_cap(ea_cdiv(MN, 256), 1024), nz);
+    dim3 grid(ea_grid_cap(ea_cdiv(MN / 4 + 1, 256), 2048), nz);
     hipLaunchKernelGGL(splitk_reduce, grid, dim3(256), 0, st, p);
     EA_LAUNCH_CHECK();
   }

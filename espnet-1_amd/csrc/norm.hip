@@ -142,6 +142,102 @@ __global__ void colsum_partial_kernel(int rows, int n, const T* __restrict__ x, 
   part[(long)blockIdx.y * n + c] = a;
 }
 
+
+// Column partial sums, 4 columns per lane (8-B bf16 / 16-B f32 loads): a wave covers 256
+// columns of one row, the 4 waves of a block interleave rows, the block writes one
+// partial row.  LN=true computes the LayerNorm parameter grads instead:
+// part[p][c] = sum dy*xhat, part[p][n + c] = sum dy.
+template <typename T, bool LN>
+__global__ __launch_bounds__(256) void colsum_vec_kernel(int rows, int n, const T* __restrict__ x, long ld,
+                                                         const float* __restrict__ xin, long ldxin,
+                                                         const float* __restrict__ mean, const float* __restrict__ rstd,
+                                                         int rows_per_part, float* __restrict__ part) {
+  __shared__ float red[4][2][256];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int c = blockIdx.x * 256 + lane * 4;
+  const int r0 = blockIdx.y * rows_per_part, r1 = min(rows, r0 + rows_per_part);
+  float a[4] = {0.f, 0.f, 0.f, 0.f}, g[4] = {0.f, 0.f, 0.f, 0.f};
+  if (c < n) {
+    for (int r = r0 + w; r < r1; r += 4) {
+      float v[4];
+      if (sizeof(T) == 2) {
+        const uint2 u = *(const uint2*)(x + (long)r * ld + c);
+        const bf16* b = (const bf16*)&u;
+        v[0] = (float)b[0]; v[1] = (float)b[1]; v[2] = (float)b[2]; v[3] = (float)b[3];
+      } else {
+        const float4 f = *(const float4*)(x + (long)r * ld + c);
+        v[0] = f.x; v[1] = f.y; v[2] = f.z; v[3] = f.w;
+      }
+      if (LN) {
+        const float mu = mean[r], rs = rstd[r];
+        const float4 xv = *(const float4*)(xin + (long)r * ldxin + c);
+        g[0] += v[0] * (xv.x - mu) * rs;
+        g[1] += v[1] * (xv.y - mu) * rs;
+        g[2] += v[2] * (xv.z - mu) * rs;
+        g[3] += v[3] * (xv.w - mu) * rs;
+      }
+#pragma unroll
+      for (int k = 0; k < 4; ++k) a[k] += v[k];
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    red[w][0][lane * 4 + k] = a[k];
+    red[w][1][lane * 4 + k] = g[k];
+  }
+  __syncthreads();
+  const int cc = blockIdx.x * 256 + threadIdx.x;
+  if (cc < n) {
+    const int t = threadIdx.x;
+    const float sa = (red[0][0][t] + red[1][0][t]) + (red[2][0][t] + red[3][0][t]);
+    if (LN) {
+      const float sg = (red[0][1][t] + red[1][1][t]) + (red[2][1][t] + red[3][1][t]);
+      part[(long)blockIdx.y * 2 * n + cc] = sg;
+      part[(long)blockIdx.y * 2 * n + n + cc] = sa;
+    } else {
+      part[(long)blockIdx.y * n + cc] = sa;
+    }
+  }
+}
+
+// LayerNorm backward, dx only (one wave per row, max parallelism)
+template <int MAXE, typename TI>
+__global__ __launch_bounds__(256) void ln_bwd_dx_kernel(int rows, int d, const TI* __restrict__ dy, long lddy,
+                                                        const float* __restrict__ x, long ldx,
+                                                        const float* __restrict__ g, const float* __restrict__ mean,
+                                                        const float* __restrict__ rstd, float* __restrict__ dx,
+                                                        long lddx, int accumulate) {
+  const int lane = threadIdx.x & 63;
+  const int r = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (r >= rows) return;
+  const float mu = mean[r], rs = rstd[r];
+  float xh[MAXE], dg[MAXE];
+  float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+  for (int i = 0; i < MAXE; ++i) {
+    const int c = i * 64 + lane;
+    if (c < d) {
+      xh[i] = (x[(long)r * ldx + c] - mu) * rs;
+      dg[i] = to_f(dy[(long)r * lddy + c]) * g[c];
+      s1 += dg[i];
+      s2 += dg[i] * xh[i];
+    } else {
+      xh[i] = dg[i] = 0.f;
+    }
+  }
+  s1 = wave_sum(s1) / d;
+  s2 = wave_sum(s2) / d;
+#pragma unroll
+  for (int i = 0; i < MAXE; ++i) {
+    const int c = i * 64 + lane;
+    if (c < d) {
+      const float v = rs * (dg[i] - s1 - xh[i] * s2);
+      float* o = dx + (long)r * lddx + c;
+      *o = accumulate ? *o + v : v;
+    }
+  }
+}
+
 // ---------------------------------------------------------------- BatchNorm1d (train)
 // Stats over all rows (padding included, as the reference's BatchNorm1d sees them).
 // Pass 1: per-block shifted sums (shift = row 0) -> fp64 combine in bn_finalize.
@@ -279,17 +375,40 @@ extern "C" int ea_layernorm_bwd(int rows, int d, const void* dy, int dy_dtype, l
                                 int accumulate_params, float* workspace, long ws_elems, void* stream) {
   EA_ENTRY();
   if (rows == 0) return 0;
-  const int nb = min(ln_blocks(rows), 128);
-  EA_CHECK_ARG(ws_elems >= (long)nb * 2 * d);
   EA_CHECK_ARG(dbeta == dgamma + d);  // grads of (weight, bias) are adjacent in the arena
-  dim3 grid(nb), blk(256);
   hipStream_t st = (hipStream_t)stream;
+  const bool vec = d % 4 == 0 && lddy % 4 == 0 && ldx % 4 == 0 && ((uintptr_t)x % 16) == 0 &&
+                   ((uintptr_t)dy % (dy_dtype == EA_BF16 ? 8 : 16)) == 0;
+  if (!vec) {  // generic fused path (row kernel + per-block partials)
+    const int nb = min(ln_blocks(rows), 128);
+    EA_CHECK_ARG(ws_elems >= (long)nb * 2 * d);
+    dim3 grid(nb), blk(256);
+    if (dy_dtype == EA_BF16)
+      EA_LN_DISPATCH(ln_bwd_kernel, bf16, grid, blk, 0, st, rows, d, (const bf16*)dy, lddy, x, ldx, gamma, mean, rstd, dx, lddx, accumulate, workspace);
+    else
+      EA_LN_DISPATCH(ln_bwd_kernel, float, grid, blk, 0, st, rows, d, (const float*)dy, lddy, x, ldx, gamma, mean, rstd, dx, lddx, accumulate, workspace);
+    EA_LAUNCH_CHECK();
+    hipLaunchKernelGGL(reduce_partials_kernel, dim3(ea_cdiv(2 * d, 64)), dim3(256), 0, st, nb, 2 * d,
+                       workspace, (long)2 * d, dgamma, accumulate_params);
+    EA_LAUNCH_CHECK();
+    return 0;
+  }
+  dim3 g1(ea_cdiv(rows, 4)), blk(256);
   if (dy_dtype == EA_BF16)
-    EA_LN_DISPATCH(ln_bwd_kernel, bf16, grid, blk, 0, st, rows, d, (const bf16*)dy, lddy, x, ldx, gamma, mean, rstd, dx, lddx, accumulate, workspace);
+    EA_LN_DISPATCH(ln_bwd_dx_kernel, bf16, g1, blk, 0, st, rows, d, (const bf16*)dy, lddy, x, ldx, gamma, mean, rstd, dx, lddx, accumulate);
   else
-    EA_LN_DISPATCH(ln_bwd_kernel, float, grid, blk, 0, st, rows, d, (const float*)dy, lddy, x, ldx, gamma, mean, rstd, dx, lddx, accumulate, workspace);
+    EA_LN_DISPATCH(ln_bwd_dx_kernel, float, g1, blk, 0, st, rows, d, (const float*)dy, lddy, x, ldx, gamma, mean, rstd, dx, lddx, accumulate);
   EA_LAUNCH_CHECK();
-  hipLaunchKernelGGL(reduce_partials_kernel, dim3(ea_cdiv(2 * d, 64)), dim3(256), 0, st, nb, 2 * d,
+  const int rpp = max(32, ea_cdiv(rows, 128));
+  const int nparts = ea_cdiv(rows, rpp);
+  EA_CHECK_ARG(ws_elems >= (long)nparts * 2 * d);
+  dim3 g2(ea_cdiv(d, 256), nparts);
+  if (dy_dtype == EA_BF16)
+    hipLaunchKernelGGL((colsum_vec_kernel<bf16, true>), g2, blk, 0, st, rows, d, (const bf16*)dy, lddy, x, ldx, mean, rstd, rpp, workspace);
+  else
+    hipLaunchKernelGGL((colsum_vec_kernel<float, true>), g2, blk, 0, st, rows, d, (const float*)dy, lddy, x, ldx, mean, rstd, rpp, workspace);
+  EA_LAUNCH_CHECK();
+  hipLaunchKernelGGL(reduce_partials_kernel, dim3(ea_cdiv(2 * d, 64)), dim3(256), 0, st, nparts, 2 * d,
                      workspace, (long)2 * d, dgamma, accumulate_params);
   EA_LAUNCH_CHECK();
   return 0;
@@ -310,6 +429,22 @@ extern "C" int ea_colsum(int rows, int n, const void* x, int x_dtype, long ld, f
   EA_ENTRY();
   if (n == 0) return 0;
   hipStream_t st = (hipStream_t)stream;
+  const bool vec = n % 4 == 0 && ld % 4 == 0 && ((uintptr_t)x % (x_dtype == EA_BF16 ? 8 : 16)) == 0 && rows > 0;
+  if (vec) {
+    const int rpp = max(32, ea_cdiv(rows, 128));
+    const int np = ea_cdiv(rows, rpp);
+    EA_CHECK_ARG((long)np * n <= ws_elems);
+    dim3 g(ea_cdiv(n, 256), np);
+    if (x_dtype == EA_BF16)
+      hipLaunchKernelGGL((colsum_vec_kernel<bf16, false>), g, dim3(256), 0, st, rows, n, (const bf16*)x, ld, nullptr, 0L, nullptr, nullptr, rpp, workspace);
+    else
+      hipLaunchKernelGGL((colsum_vec_kernel<float, false>), g, dim3(256), 0, st, rows, n, (const float*)x, ld, nullptr, 0L, nullptr, nullptr, rpp, workspace);
+    EA_LAUNCH_CHECK();
+    hipLaunchKernelGGL(reduce_partials_kernel, dim3(ea_cdiv(n, 64)), dim3(256), 0, st, np, n, workspace, (long)n, out,
+                       accumulate);
+    EA_LAUNCH_CHECK();
+    return 0;
+  }
   int rpb = max(16, ea_cdiv(rows, 64));
   int nparts = ea_cdiv(rows, rpb);
   while ((long)nparts * n > ws_elems && rpb < (1 << 20)) {

@@ -304,7 +304,7 @@ class ConformerBlockFn(torch.autograd.Function):
         # linear_pos: dp[h] = sum_b dBD[h][b]^T qv[b, :, h]  (K = B*T), dWpos = dp^T pos
         dpp = empty(P2, d, dtype=cd, device=dev)
         ops.gemm(dbd, qv, dpp, M=P2, N=dk, K=B * T, a_kmajor=0, b_kmajor=0, lda=ldbd, ldb=d, ldc=d,
-                 batch=1, nh=H, sA=(0, B * T * ldbd), sB=(0, dk), sC=(0, dk), splitk=False)
+                 batch=1, nh=H, sA=(0, B * T * ldbd), sB=(0, dk), sC=(0, dk))
         del dbd
         ops.linear_dw(dpp, pos, b.g(A + "linear_pos.weight"), accumulate=True)
         qkv_w = b.w(A + "linear_q.weight", A + "linear_k.weight", A + "linear_v.weight", shape=(3 * d, d))
