@@ -44,6 +44,12 @@ class KernelProbe:
 
 
 PROBE = None
+GRAD_READY = None  # callable(prefix): a block's parameter gradients are final (DP overlap)
+
+
+def grad_ready(bound):
+    if GRAD_READY is not None:
+        GRAD_READY(bound.prefix)
 
 
 def dt(t: torch.Tensor) -> int:

@@ -102,6 +102,7 @@ class LayerNormFn(torch.autograd.Function):
         dy2 = dy.reshape(-1, x2.shape[-1]).contiguous()
         dx = torch.empty_like(x2)
         ln_bwd(dy2, x2, module._b, "", mu, rs, dx, accumulate=False)
+        ops.grad_ready(module._b)
         return dx.view(dy.shape), None
 
 

@@ -316,4 +316,5 @@ class ConformerBlockFn(torch.autograd.Function):
         ln_bwd(dxn2, x1, b, "norm_mha", mu2, rs2, dx, accumulate=True)
         # ---- macaron FFN
         _ffn_bwd(L, b, dx, x0, s_ff1, "feed_forward_macaron", "norm_ff_macaron", p, sd(1), sd(2))
+        ops.grad_ready(b)
         return dx.view(B, T, d), None, None, None, None, None

@@ -254,4 +254,5 @@ class DecoderFn(torch.autograd.Function):
         ops.linear_dw(dkv, mem, b.g(*kvw, shape=(ldkv, d)), accumulate=True)
         dmem = empty(Nm, d, device=dev)
         ops.linear_dx(dkv, b.w(*kvw, shape=(ldkv, d)), dmem)
+        ops.grad_ready(b)
         return dmem.view(B, Tm, d), None, None, None, None, None, None

@@ -66,6 +66,7 @@ class CTCFn(torch.autograd.Function):
         ops.linear_dx(dl, b.w("ctc_lo.weight"), dh)
         if ctc.dropout_rate > 0:
             ops.scale_dropout(dh, dh, p=ctc.dropout_rate, seed=ctc._seed)
+        ops.grad_ready(b)
         return dh.view(B, T, d), None, None, None, None, None
 
 

@@ -159,4 +159,5 @@ class SubsampleFn(torch.autograd.Function):
         ops.colsum(dx1, b.g("conv.0.bias"))
         ops.gemm(dx1, col1, b.g("conv.0.weight", shape=(C, 9)), M=C, N=9, K=dx1.shape[0],
                  a_kmajor=0, b_kmajor=0, lda=C, ldb=16, ldc=9, epi=ops.make_epi(beta=1.0))
+        ops.grad_ready(b)
         return None, None, None, None, None

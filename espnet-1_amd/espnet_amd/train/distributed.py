@@ -1,17 +1,18 @@
-"""Data parallelism over the parameter arena (replaces DistributedDataParallel as used by
-espnet2/train/trainer.py:229-244; one process per GPU, RCCL over xGMI).
+"""Data parallelism over the parameter arena — replaces DistributedDataParallel as used by
+espnet2/train/trainer.py:229-244 (one process per GPU, RCCL over xGMI; gloo on CPU).
 
-* K3: parameters broadcast from rank 0 at construction (one call: the arena is one
-  buffer).
+* K3: parameters broadcast from rank 0 at construction (ONE call: the arena is one buffer).
 * K2: BatchNorm running stats broadcast from rank 0 before each forward
-  (broadcast_buffers=True semantics).
-* K1: gradients summed with all_reduce on contiguous byte ranges of the grad arena
-  ("buckets"), issued back-to-front so the bucket whose gradients are complete first
-  goes first; RCCL runs them on its own stream.
+  (broadcast_buffers=True semantics) — two calls (flat f32 + int64 buffer arenas).
+* K1: gradients summed with all_reduce over contiguous ranges of the grad arena
+  ("buckets", default 64 MiB — fewer, larger messages suit xGMI's point-to-point links).
+  Each block-level backward reports its module prefix when its gradients are final
+  (`grad_ready`); a bucket whose modules are all final is all-reduced immediately
+  (async), so RCCL's stream overlaps the rest of the backward pass.
 * K4-K6: the stats / weight all-reduces of recursive_average (recursive_op.py:8-47) are
   packed into ONE message.
-Loss weighting follows trainer.py:604-619: loss_r * w_r / sum(w) on every rank, and the
-SUM all-reduce of gradients then equals DDP's mean of (loss_r * w_r / sum(w) * world).
+Loss weighting follows trainer.py:604-619: loss_r * w_r / sum(w); with the SUM all-reduce
+of gradients this equals DDP's mean of (loss_r * w_r / sum(w) * world).
 """
 from __future__ import annotations
 
@@ -20,9 +21,11 @@ from typing import Dict, List
 import torch
 import torch.distributed as dist
 
+from .. import hip_ops
+
 
 class ArenaDataParallel:
-    def __init__(self, model, bucket_mb: float = 64.0, group=None):
+    def __init__(self, model, bucket_mb: float = 64.0, group=None, overlap: bool = True):
         self.model = model
         self.group = group
         self.world_size = dist.get_world_size(group) if dist.is_initialized() else 1
@@ -32,23 +35,41 @@ class ArenaDataParallel:
         n = arena.numel
         per = max(int(bucket_mb * 1024 * 1024 / 4) // 64 * 64, 64)
         # buckets back-to-front: the tail of the arena (decoder / CTC head, whose grads
-        # finish first in backward) is reduced first
+        # are final first in backward) is reduced first
         self.buckets: List[slice] = []
         end = n
         while end > 0:
             start = max(0, end - per)
             self.buckets.append(slice(start, end))
             end = start
-        self._bufs = [b for _, b in sorted(model.named_buffers()) if b.is_floating_point() or b.dtype == torch.long]
+        # module prefix -> buckets it overlaps (prefixes = the block-level autograd nodes)
+        self.prefixes = sorted({getattr(m, "_b").prefix for m in model.modules()
+                                if getattr(m, "_b", None) is not None}, key=len, reverse=True)
+        span = {}
+        for name in arena.names:
+            pre = next((p for p in self.prefixes if name.startswith(p)), None)
+            if pre is None:
+                raise RuntimeError(f"parameter {name} is not owned by a block-level node")
+            o = arena.offsets[name]
+            lo, hi = span.get(pre, (o, o))
+            span[pre] = (min(lo, o), max(hi, o + arena._params[name].numel()))
+        self._bucket_mods = []
+        for b in self.buckets:
+            self._bucket_mods.append({p for p, (lo, hi) in span.items() if lo < b.stop and hi > b.start})
+        self.overlap = overlap
+        self._pending = None
+        self._works = []
         if self.world_size > 1:
             dist.broadcast(arena.data, 0, group=group)
             arena.refresh_shadow()
             self.broadcast_buffers()
 
+    # ------------------------------------------------------------------ per step
     def broadcast_buffers(self):
         if self.world_size > 1:
-            for b in self._bufs:
-                dist.broadcast(b, 0, group=self.group)
+            for b in (self.arena.buf_f32, self.arena.buf_i64):
+                if b.numel():
+                    dist.broadcast(b, 0, group=self.group)
 
     def weighted_average(self, loss, stats: Dict[str, torch.Tensor], weight):
         """trainer.py:604-619 + recursive_average (recursive_op.py:30-47), one all-reduce."""
@@ -61,8 +82,34 @@ class ArenaDataParallel:
         loss = (loss * w).sum() / wsum
         return loss, new_stats, wsum.to(torch.long)
 
-    def allreduce_grads(self):
+    def begin_backward(self):
+        """Arm the grad-ready hooks for one backward pass."""
+        self._pending = [set(m) for m in self._bucket_mods]
+        self._works = []
+        if self.overlap and self.world_size > 1:
+            hip_ops.GRAD_READY = self.grad_ready
+
+    def grad_ready(self, prefix: str):
+        if self._pending is None:
+            return
         g = self.arena.grad
-        works = [dist.all_reduce(g[s], async_op=True, group=self.group) for s in self.buckets]
-        for w in works:
+        for i, mods in enumerate(self._pending):
+            if prefix in mods:
+                mods.discard(prefix)
+                if not mods:
+                    self._works.append(dist.all_reduce(g[self.buckets[i]], async_op=True, group=self.group))
+
+    def allreduce_grads(self):
+        """Finish the step's gradient reduction (launch what the hooks did not, wait all)."""
+        hip_ops.GRAD_READY = None
+        g = self.arena.grad
+        if self._pending is None:
+            self._pending = [set(m) for m in self._bucket_mods]
+        for i, mods in enumerate(self._pending):
+            if mods:
+                mods.clear()
+                self._works.append(dist.all_reduce(g[self.buckets[i]], async_op=True, group=self.group))
+        for w in self._works:
             w.wait()
+        self._works = []
+        self._pending = None

@@ -32,6 +32,8 @@ class Trainer:
         if dp is not None and dp.world_size > 1:
             loss, stats, weight = dp.weighted_average(loss, stats, weight)
         loss = loss / accum_grad if accum_grad > 1 else loss
+        if dp is not None and dp.world_size > 1:
+            dp.begin_backward()
         loss.backward()
         if dp is not None and dp.world_size > 1:
             dp.allreduce_grads()
