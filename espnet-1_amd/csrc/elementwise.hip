@@ -178,6 +178,47 @@ __global__ void col2im_conv2_kernel(int B, int T1, int F1, int C, int T2, int F2
   }
 }
 
+
+// vectorised bf16 col2im: 8 channels per thread (16-B loads/stores)
+__global__ void col2im_conv2_bf16x8_kernel(int B, int T1, int F1, int C, int T2, int F2, const bf16* __restrict__ dcol,
+                                           const bf16* __restrict__ x1, bf16* __restrict__ dx1) {
+  const int C8 = C / 8;
+  const long n = (long)B * T1 * F1 * C8;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+    const int c8 = (int)(i % C8);
+    long r = i / C8;
+    const int f1 = (int)(r % F1);
+    const long bt = r / F1;
+    const int t1 = (int)(bt % T1), b = (int)(bt / T1);
+    const long off = r * C + c8 * 8;
+    const uint4 xv = *(const uint4*)(x1 + off);
+    const bf16* xb = (const bf16*)&xv;
+    float acc[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) acc[e] = 0.f;
+#pragma unroll
+    for (int kh = 0; kh < 3; ++kh) {
+      const int tt = t1 - kh;
+      if (tt < 0 || (tt & 1) || (tt >> 1) >= T2) continue;
+#pragma unroll
+      for (int kw = 0; kw < 3; ++kw) {
+        const int ff = f1 - kw;
+        if (ff < 0 || (ff & 1) || (ff >> 1) >= F2) continue;
+        const long row = ((long)b * T2 + (tt >> 1)) * F2 + (ff >> 1);
+        const uint4 dv = *(const uint4*)(dcol + (row * 9 + kh * 3 + kw) * (long)C + c8 * 8);
+        const bf16* db = (const bf16*)&dv;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) acc[e] += (float)db[e];
+      }
+    }
+    uint4 out;
+    bf16* ob = (bf16*)&out;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) ob[e] = (bf16)((float)xb[e] > 0.f ? acc[e] : 0.f);
+    *(uint4*)(dx1 + off) = out;
+  }
+}
+
 // ---------------------------------------------------------------- GLU (conv module)
 // out[r,c] = x[r,c] * sigmoid(x[r,c+C])   (nn.functional.glu(dim=channels))
 template <typename TI, typename TO>
@@ -462,6 +503,12 @@ extern "C" int ea_col2im_conv2(int B, int T1, int F1, int C, const void* dcol, i
   EA_ENTRY();
   const int T2 = (T1 - 3) / 2 + 1, F2 = (F1 - 3) / 2 + 1;
   const long n = (long)B * T1 * F1 * C;
+  if (dcol_dtype == EA_BF16 && dtype == EA_BF16 && C % 8 == 0) {
+    hipLaunchKernelGGL(col2im_conv2_bf16x8_kernel, EA_GRID(n / 8), B, T1, F1, C, T2, F2, (const bf16*)dcol,
+                       (const bf16*)x1, (bf16*)dx1);
+    EA_LAUNCH_CHECK();
+    return 0;
+  }
 #define EA_C2I(TI, TO) hipLaunchKernelGGL((col2im_conv2_kernel<TI, TO>), EA_GRID(n), B, T1, F1, C, T2, F2, (const TI*)dcol, (const TO*)x1, (TO*)dx1)
   if (dcol_dtype == EA_BF16 && dtype == EA_BF16) EA_C2I(bf16, bf16);
   else if (dcol_dtype == EA_BF16) EA_C2I(bf16, float);

@@ -44,10 +44,60 @@ class KernelProbe:
 
 
 PROBE = None
+OVERLAP_WGRAD = True  # run weight-gradient GEMMs / bias reductions on a side stream
+_SIDE = {}
+
+
+class wgrad:
+    """Context for weight-gradient work (dW GEMMs, bias column sums) that is off the
+    backward critical path: it runs on a side HIP stream, ordered after everything the
+    main stream has issued so far; `join()` makes the main stream wait for it.
+    Tensors read on the side stream are record_stream()-ed so the caching allocator does
+    not recycle them under it."""
+
+    def __init__(self, *tensors):
+        self.tensors = tensors
+
+    def __enter__(self):
+        if not OVERLAP_WGRAD:
+            self.ctx = None
+            return self
+        main = torch.cuda.current_stream()
+        dev = main.device
+        side = _SIDE.get(dev)
+        if side is None:
+            side = _SIDE[dev] = torch.cuda.Stream(device=dev)
+        side.wait_stream(main)
+        for t in self.tensors:
+            if t is not None:
+                t.record_stream(side)
+        self.ctx = torch.cuda.stream(side)
+        self.ctx.__enter__()
+        return self
+
+    def __exit__(self, *exc):
+        if self.ctx is not None:
+            self.ctx.__exit__(*exc)
+        return False
+
+
+def join_wgrad(device=None):
+    """Main stream waits for all weight-gradient work issued so far."""
+    if not _SIDE:
+        return
+    main = torch.cuda.current_stream()
+    side = _SIDE.get(main.device)
+    if side is not None:
+        main.wait_stream(side)
+
+
 GRAD_READY = None  # callable(prefix): a block's parameter gradients are final (DP overlap)
 
 
 def grad_ready(bound):
+    """A block's backward is done: its parameter gradients (some written on the side
+    stream) are final once the main stream has joined the side stream."""
+    join_wgrad()
     if GRAD_READY is not None:
         GRAD_READY(bound.prefix)
 
@@ -71,8 +121,8 @@ _WS = {}
 
 
 def workspace(numel: int, device) -> torch.Tensor:
-    """Persistent f32 scratch (split-K slabs, partial sums); grows monotonically."""
-    key = (str(device), "f32")
+    """Persistent f32 scratch (split-K slabs), one per (device, stream); grows monotonically."""
+    key = (str(device), "f32", stream())
     ws = _WS.get(key)
     if ws is None or ws.numel() < numel:
         ws = torch.empty(max(numel, 1 << 20), dtype=torch.float32, device=device)
@@ -172,8 +222,9 @@ _SCRATCH = {}
 
 
 def scratch(numel: int, device, tag="ws") -> torch.Tensor:
-    """Stream-ordered f32 scratch shared by consecutive kernels (partials, reductions)."""
-    key = (str(device), tag)
+    """Stream-ordered f32 scratch shared by consecutive kernels (partials, reductions); one
+    per (device, stream) so the weight-gradient side stream never races the main one."""
+    key = (str(device), tag, stream())
     t = _SCRATCH.get(key)
     if t is None or t.numel() < numel:
         t = torch.empty(max(numel, 1 << 22), dtype=torch.float32, device=device)

@@ -145,13 +145,15 @@ def _ffn_bwd(L, b, dx, x_in, saved, pre, ln_name, p, seed_in, seed_out):
     N, d = dx.shape
     dv = empty(N, d, dtype=cd, device=dx.device)
     ops.scale_dropout(dx, dv, scale=L.ff_scale, p=p, seed=seed_out)
-    ops.colsum(dv, b.g(pre + ".w_2.bias"))
-    ops.linear_dw(dv, a, b.g(pre + ".w_2.weight"), accumulate=True)
+    with ops.wgrad(dv, a):
+        ops.colsum(dv, b.g(pre + ".w_2.bias"))
+        ops.linear_dw(dv, a, b.g(pre + ".w_2.weight"), accumulate=True)
     dh = empty(*h.shape, dtype=cd, device=dx.device)
     ops.linear_dx(dv, b.w(pre + ".w_2.weight"), dh,
                   epi=ops.make_epi(EPI_DACT, act=ACT_SWISH, aux=h, drop_p=p, seed=seed_in))
-    ops.colsum(dh, b.g(pre + ".w_1.bias"))
-    ops.linear_dw(dh, xn, b.g(pre + ".w_1.weight"), accumulate=True)
+    with ops.wgrad(dh, xn):
+        ops.colsum(dh, b.g(pre + ".w_1.bias"))
+        ops.linear_dw(dh, xn, b.g(pre + ".w_1.weight"), accumulate=True)
     dxn = empty(N, d, dtype=cd, device=dx.device)
     ops.linear_dx(dh, b.w(pre + ".w_1.weight"), dxn)
     ln_bwd(dxn, x_in, b, ln_name, mu, rs, dx, accumulate=True)
@@ -258,8 +260,9 @@ class ConformerBlockFn(torch.autograd.Function):
         xn3, mu3, rs3, g2, glu, y, z, bn_mean, bn_rstd = s_conv
         dv = empty(N, d, dtype=cd, device=dev)
         ops.scale_dropout(dx, dv, p=p, seed=sd(5))
-        ops.colsum(dv, b.g(C + "pointwise_conv2.bias"))
-        ops.linear_dw(dv, z, b.g(C + "pointwise_conv2.weight", shape=(d, d)), accumulate=True)
+        with ops.wgrad(dv, z):
+            ops.colsum(dv, b.g(C + "pointwise_conv2.bias"))
+            ops.linear_dw(dv, z, b.g(C + "pointwise_conv2.weight", shape=(d, d)), accumulate=True)
         dz = empty(N, d, dtype=cd, device=dev)
         ops.linear_dx(dv, b.w(C + "pointwise_conv2.weight", shape=(d, d)), dz)
         dy = empty(N, d, device=dev)
@@ -272,8 +275,9 @@ class ConformerBlockFn(torch.autograd.Function):
                           b.g(C + "depthwise_conv.bias").data_ptr(), 1, w, wn, ops.stream())
         dg2 = empty(N, 2 * d, dtype=cd, device=dev)
         lib.ea_glu_bwd(N, d, g2.data_ptr(), ops.dt(g2), dglu.data_ptr(), dg2.data_ptr(), ops.stream())
-        ops.colsum(dg2, b.g(C + "pointwise_conv1.bias"))
-        ops.linear_dw(dg2, xn3, b.g(C + "pointwise_conv1.weight", shape=(2 * d, d)), accumulate=True)
+        with ops.wgrad(dg2, xn3):
+            ops.colsum(dg2, b.g(C + "pointwise_conv1.bias"))
+            ops.linear_dw(dg2, xn3, b.g(C + "pointwise_conv1.weight", shape=(2 * d, d)), accumulate=True)
         dxn3 = empty(N, d, dtype=cd, device=dev)
         ops.linear_dx(dg2, b.w(C + "pointwise_conv1.weight", shape=(2 * d, d)), dxn3)
         ln_bwd(dxn3, x2, b, "norm_conv", mu3, rs3, dx, accumulate=True)
@@ -282,8 +286,9 @@ class ConformerBlockFn(torch.autograd.Function):
         xn2, mu2, rs2, qkv, pp, qu, qv, O, P, Pd = s_att
         dv = empty(N, d, dtype=cd, device=dev)
         ops.scale_dropout(dx, dv, p=p, seed=sd(4))
-        ops.colsum(dv, b.g(A + "linear_out.bias"))
-        ops.linear_dw(dv, O, b.g(A + "linear_out.weight"), accumulate=True)
+        with ops.wgrad(dv, O):
+            ops.colsum(dv, b.g(A + "linear_out.bias"))
+            ops.linear_dw(dv, O, b.g(A + "linear_out.weight"), accumulate=True)
         dO = empty(N, d, dtype=cd, device=dev)
         ops.linear_dx(dv, b.w(A + "linear_out.weight"), dO)
         dqkv = empty(N, 3 * d, dtype=cd, device=dev)
@@ -302,15 +307,17 @@ class ConformerBlockFn(torch.autograd.Function):
         lib.ea_add_2d(N, d, dqv.data_ptr(), ops.dt(dqv), d, dqkv.data_ptr(), ops.dt(dqkv), 3 * d, 1.0,
                       ops.stream())
         # linear_pos: dp[h] = sum_b dBD[h][b]^T qv[b, :, h]  (K = B*T), dWpos = dp^T pos
-        dpp = empty(P2, d, dtype=cd, device=dev)
-        ops.gemm(dbd, qv, dpp, M=P2, N=dk, K=B * T, a_kmajor=0, b_kmajor=0, lda=ldbd, ldb=d, ldc=d,
-                 batch=1, nh=H, sA=(0, B * T * ldbd), sB=(0, dk), sC=(0, dk))
+        with ops.wgrad(dbd, qv, pos):
+            dpp = empty(P2, d, dtype=cd, device=dev)
+            ops.gemm(dbd, qv, dpp, M=P2, N=dk, K=B * T, a_kmajor=0, b_kmajor=0, lda=ldbd, ldb=d, ldc=d,
+                     batch=1, nh=H, sA=(0, B * T * ldbd), sB=(0, dk), sC=(0, dk))
+            ops.linear_dw(dpp, pos, b.g(A + "linear_pos.weight"), accumulate=True)
         del dbd
-        ops.linear_dw(dpp, pos, b.g(A + "linear_pos.weight"), accumulate=True)
         qkv_w = b.w(A + "linear_q.weight", A + "linear_k.weight", A + "linear_v.weight", shape=(3 * d, d))
-        ops.colsum(dqkv, b.g(A + "linear_q.bias", A + "linear_k.bias", A + "linear_v.bias", shape=(3 * d,)))
-        ops.linear_dw(dqkv, xn2, b.g(A + "linear_q.weight", A + "linear_k.weight", A + "linear_v.weight",
-                                      shape=(3 * d, d)), accumulate=True)
+        with ops.wgrad(dqkv, xn2):
+            ops.colsum(dqkv, b.g(A + "linear_q.bias", A + "linear_k.bias", A + "linear_v.bias", shape=(3 * d,)))
+            ops.linear_dw(dqkv, xn2, b.g(A + "linear_q.weight", A + "linear_k.weight", A + "linear_v.weight",
+                                          shape=(3 * d, d)), accumulate=True)
         dxn2 = empty(N, d, dtype=cd, device=dev)
         ops.linear_dx(dqkv, qkv_w, dxn2)
         ln_bwd(dxn2, x1, b, "norm_mha", mu2, rs2, dx, accumulate=True)

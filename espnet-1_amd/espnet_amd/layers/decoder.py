@@ -184,8 +184,9 @@ class DecoderFn(torch.autograd.Function):
         V = dlogits.shape[-1]
         dev = dlogits.device
         dlog = ops.cast(dlogits.reshape(N, V).contiguous(), cd)
-        ops.colsum(dlog, b.g("output_layer.bias"))
-        ops.linear_dw(dlog, xf, b.g("output_layer.weight"), accumulate=True)
+        with ops.wgrad(dlog, xf):
+            ops.colsum(dlog, b.g("output_layer.bias"))
+            ops.linear_dw(dlog, xf, b.g("output_layer.weight"), accumulate=True)
         dxf = empty(N, d, dtype=cd, device=dev)
         ops.linear_dx(dlog, b.w("output_layer.weight"), dxf)
         dx = empty(N, d, device=dev)
@@ -200,13 +201,15 @@ class DecoderFn(torch.autograd.Function):
             xn3, mu3, rs3, h, a = s3
             dv = empty(N, d, dtype=cd, device=dev)
             ops.scale_dropout(dx, dv, p=p, seed=sd(l, 6))
-            ops.colsum(dv, b.g(ff + "w_2.bias"))
-            ops.linear_dw(dv, a, b.g(ff + "w_2.weight"), accumulate=True)
+            with ops.wgrad(dv, a):
+                ops.colsum(dv, b.g(ff + "w_2.bias"))
+                ops.linear_dw(dv, a, b.g(ff + "w_2.weight"), accumulate=True)
             dh = empty(*h.shape, dtype=cd, device=dev)
             ops.linear_dx(dv, b.w(ff + "w_2.weight"), dh,
                           epi=ops.make_epi(EPI_DACT, act=ACT_RELU, aux=h, drop_p=p, seed=sd(l, 5)))
-            ops.colsum(dh, b.g(ff + "w_1.bias"))
-            ops.linear_dw(dh, xn3, b.g(ff + "w_1.weight"), accumulate=True)
+            with ops.wgrad(dh, xn3):
+                ops.colsum(dh, b.g(ff + "w_1.bias"))
+                ops.linear_dw(dh, xn3, b.g(ff + "w_1.weight"), accumulate=True)
             dxn = empty(N, d, dtype=cd, device=dev)
             ops.linear_dx(dh, b.w(ff + "w_1.weight"), dxn)
             ln_bwd(dxn, x2, b, n + "norm3", mu3, rs3, dx, accumulate=True)
@@ -214,16 +217,18 @@ class DecoderFn(torch.autograd.Function):
             xn2, mu2, rs2, q2, O2, P2, Pd2, ldT2 = s2
             dv = empty(N, d, dtype=cd, device=dev)
             ops.scale_dropout(dx, dv, p=p, seed=sd(l, 4))
-            ops.colsum(dv, b.g(xa + "linear_out.bias"))
-            ops.linear_dw(dv, O2, b.g(xa + "linear_out.weight"), accumulate=True)
+            with ops.wgrad(dv, O2):
+                ops.colsum(dv, b.g(xa + "linear_out.bias"))
+                ops.linear_dw(dv, O2, b.g(xa + "linear_out.weight"), accumulate=True)
             dO = empty(N, d, dtype=cd, device=dev)
             ops.linear_dx(dv, b.w(xa + "linear_out.weight"), dO)
             dq = empty(N, d, dtype=cd, device=dev)
             attn_bwd(dO, q2, kv[:, 2 * d * l:], kv[:, 2 * d * l + d:], P2, Pd2, ldT2, B=B, H=H, T1=L,
                      T2=Tm, dk=dk, ldq=d, ldk=ldkv, ldv=ldkv, scale=scale, p=p_src, seed=sd(l, 3), cd=cd,
                      dq=dq, lddq=d, dk_=dkv[:, 2 * d * l:], lddk=ldkv, dv=dkv[:, 2 * d * l + d:], lddv=ldkv)
-            ops.colsum(dq, b.g(xa + "linear_q.bias"))
-            ops.linear_dw(dq, xn2, b.g(xa + "linear_q.weight"), accumulate=True)
+            with ops.wgrad(dq, xn2):
+                ops.colsum(dq, b.g(xa + "linear_q.bias"))
+                ops.linear_dw(dq, xn2, b.g(xa + "linear_q.weight"), accumulate=True)
             dxn = empty(N, d, dtype=cd, device=dev)
             ops.linear_dx(dq, b.w(xa + "linear_q.weight"), dxn)
             ln_bwd(dxn, x1, b, n + "norm2", mu2, rs2, dx, accumulate=True)
@@ -231,8 +236,9 @@ class DecoderFn(torch.autograd.Function):
             xn1, mu1, rs1, qkv, O1, P1, Pd1, ldT1 = s1
             dv = empty(N, d, dtype=cd, device=dev)
             ops.scale_dropout(dx, dv, p=p, seed=sd(l, 2))
-            ops.colsum(dv, b.g(sa + "linear_out.bias"))
-            ops.linear_dw(dv, O1, b.g(sa + "linear_out.weight"), accumulate=True)
+            with ops.wgrad(dv, O1):
+                ops.colsum(dv, b.g(sa + "linear_out.bias"))
+                ops.linear_dw(dv, O1, b.g(sa + "linear_out.weight"), accumulate=True)
             dO = empty(N, d, dtype=cd, device=dev)
             ops.linear_dx(dv, b.w(sa + "linear_out.weight"), dO)
             dqkv = empty(N, 3 * d, dtype=cd, device=dev)
@@ -241,8 +247,9 @@ class DecoderFn(torch.autograd.Function):
                      dq=dqkv, lddq=3 * d, dk_=dqkv[:, d:], lddk=3 * d, dv=dqkv[:, 2 * d:], lddv=3 * d)
             wn = (sa + "linear_q.weight", sa + "linear_k.weight", sa + "linear_v.weight")
             bn = (sa + "linear_q.bias", sa + "linear_k.bias", sa + "linear_v.bias")
-            ops.colsum(dqkv, b.g(*bn, shape=(3 * d,)))
-            ops.linear_dw(dqkv, xn1, b.g(*wn, shape=(3 * d, d)), accumulate=True)
+            with ops.wgrad(dqkv, xn1):
+                ops.colsum(dqkv, b.g(*bn, shape=(3 * d,)))
+                ops.linear_dw(dqkv, xn1, b.g(*wn, shape=(3 * d, d)), accumulate=True)
             dxn = empty(N, d, dtype=cd, device=dev)
             ops.linear_dx(dqkv, b.w(*wn, shape=(3 * d, d)), dxn)
             ln_bwd(dxn, x0, b, n + "norm1", mu1, rs1, dx, accumulate=True)
@@ -250,8 +257,9 @@ class DecoderFn(torch.autograd.Function):
         lib.ea_embed_bwd(N, d, ys_in.data_ptr(), dx.data_ptr(), pe.xscale, p_pos, sd(0, 0),
                          b.g("embed.0.weight").data_ptr(), ops.stream())
         kvw, kvb = _kv_names(nb)
-        ops.colsum(dkv, b.g(*kvb, shape=(ldkv,)))
-        ops.linear_dw(dkv, mem, b.g(*kvw, shape=(ldkv, d)), accumulate=True)
+        with ops.wgrad(dkv, mem):
+            ops.colsum(dkv, b.g(*kvb, shape=(ldkv,)))
+            ops.linear_dw(dkv, mem, b.g(*kvw, shape=(ldkv, d)), accumulate=True)
         dmem = empty(Nm, d, device=dev)
         ops.linear_dx(dkv, b.w(*kvw, shape=(ldkv, d)), dmem)
         ops.grad_ready(b)

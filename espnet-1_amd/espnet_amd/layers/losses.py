@@ -60,8 +60,9 @@ class CTCFn(torch.autograd.Function):
                             ylens.data_ptr(), Lmax, lse.data_ptr(), alpha.data_ptr(), beta.data_ptr(),
                             nll.data_ptr(), _g(gl).data_ptr(), 1.0 / B, dl.data_ptr(), ops.dt(dl), V,
                             ops.stream())
-        ops.colsum(dl, b.g("ctc_lo.bias"))
-        ops.linear_dw(dl, h, b.g("ctc_lo.weight"), accumulate=True)
+        with ops.wgrad(dl, h):
+            ops.colsum(dl, b.g("ctc_lo.bias"))
+            ops.linear_dw(dl, h, b.g("ctc_lo.weight"), accumulate=True)
         dh = empty(N, d, device=dev)
         ops.linear_dx(dl, b.w("ctc_lo.weight"), dh)
         if ctc.dropout_rate > 0:

@@ -137,18 +137,20 @@ class SubsampleFn(torch.autograd.Function):
         dev = dy.device
         dv = empty(B * T2, C, dtype=cd, device=dev)
         ops.scale_dropout(dy.reshape(B * T2, C).contiguous(), dv, scale=m.out[1].xscale, p=p, seed=seed)
-        ops.colsum(dv, b.g("out.0.bias"))
-        dwl = empty(C, F2 * C, device=dev)
         x2r = x2.view(B * T2, F2 * C)
-        ops.linear_dw(dv, x2r, dwl, accumulate=False)
-        ops.permute3(dwl, b.g("out.0.weight"), C, F2, C, accumulate=True)  # (d,F2,C) -> (d,C,F2)
+        with ops.wgrad(dv, x2):
+            ops.colsum(dv, b.g("out.0.bias"))
+            dwl = empty(C, F2 * C, device=dev)
+            ops.linear_dw(dv, x2r, dwl, accumulate=False)
+            ops.permute3(dwl, b.g("out.0.weight"), C, F2, C, accumulate=True)  # (d,F2,C) -> (d,C,F2)
         dx2 = empty(B * T2, F2 * C, dtype=cd, device=dev)
         ops.linear_dx(dv, wl, dx2, epi=ops.make_epi(EPI_DACT, act=ACT_RELU, aux=x2r))
         dx2 = dx2.view(-1, C)
-        ops.colsum(dx2, b.g("conv.2.bias"))
-        dw2 = empty(C, 9 * C, device=dev)
-        ops.linear_dw(dx2, col2, dw2, accumulate=False)
-        ops.permute3(dw2, b.g("conv.2.weight"), C, 9, C, accumulate=True)  # (Co,9,Ci) -> (Co,Ci,9)
+        with ops.wgrad(dx2, col2):
+            ops.colsum(dx2, b.g("conv.2.bias"))
+            dw2 = empty(C, 9 * C, device=dev)
+            ops.linear_dw(dx2, col2, dw2, accumulate=False)
+            ops.permute3(dw2, b.g("conv.2.weight"), C, 9, C, accumulate=True)  # (Co,9,Ci) -> (Co,Ci,9)
         dcol2 = empty(*col2.shape, dtype=cd, device=dev)
         ops.linear_dx(dx2, w2, dcol2)
         del col2
@@ -156,8 +158,9 @@ class SubsampleFn(torch.autograd.Function):
         lib.ea_col2im_conv2(B, T1, F1, C, dcol2.data_ptr(), ops.dt(dcol2), x1.data_ptr(), dx1.data_ptr(),
                             ops.dt(dx1), ops.stream())
         del dcol2
-        ops.colsum(dx1, b.g("conv.0.bias"))
-        ops.gemm(dx1, col1, b.g("conv.0.weight", shape=(C, 9)), M=C, N=9, K=dx1.shape[0],
-                 a_kmajor=0, b_kmajor=0, lda=C, ldb=16, ldc=9, epi=ops.make_epi(beta=1.0))
+        with ops.wgrad(dx1, col1):
+            ops.colsum(dx1, b.g("conv.0.bias"))
+            ops.gemm(dx1, col1, b.g("conv.0.weight", shape=(C, 9)), M=C, N=9, K=dx1.shape[0],
+                     a_kmajor=0, b_kmajor=0, lda=C, ldb=16, ldc=9, epi=ops.make_epi(beta=1.0))
         ops.grad_ready(b)
         return None, None, None, None, None
