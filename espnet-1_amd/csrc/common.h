@@ -34,6 +34,22 @@ template <typename T> EA_DEV T from_f(float x);
 template <> EA_DEV float from_f<float>(float x) { return x; }
 template <> EA_DEV bf16 from_f<bf16>(float x) { return (bf16)x; }
 
+// 4-wide vector load/store (16-B f32, 8-B bf16; caller guarantees alignment)
+EA_DEV void vld4(const float* p, float (&v)[4]) {
+  const float4 f = *(const float4*)p;
+  v[0] = f.x; v[1] = f.y; v[2] = f.z; v[3] = f.w;
+}
+EA_DEV void vld4(const bf16* p, float (&v)[4]) {
+  const uint2 u = *(const uint2*)p;
+  const bf16* b = (const bf16*)&u;
+  v[0] = (float)b[0]; v[1] = (float)b[1]; v[2] = (float)b[2]; v[3] = (float)b[3];
+}
+EA_DEV void vst4(float* p, const float (&v)[4]) { *(float4*)p = make_float4(v[0], v[1], v[2], v[3]); }
+EA_DEV void vst4(bf16* p, const float (&v)[4]) {
+  union { uint2 u; bf16 b[4]; } t;
+  t.b[0] = (bf16)v[0]; t.b[1] = (bf16)v[1]; t.b[2] = (bf16)v[2]; t.b[3] = (bf16)v[3];
+  *(uint2*)p = t.u;
+}
 EA_DEV float load_as_f(const void* p, long i, int dtype) {
   return dtype == EA_BF16 ? (float)((const bf16*)p)[i] : ((const float*)p)[i];
 }
@@ -46,22 +62,42 @@ EA_DEV void store_from_f(void* p, long i, int dtype, float v) {
 
 // ------------------------------------------------------------------ dropout RNG
 // Counter-based: the keep decision of element `idx` under stream `seed` is a pure
-// function, so backward regenerates the forward mask with no mask tensor.
-EA_DEV uint32_t ea_hash(uint64_t seed, uint64_t idx) {
-  uint64_t z = seed + (idx + 1) * 0x9E3779B97F4A7C15ull;
-  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
-  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
-  return (uint32_t)((z ^ (z >> 31)) >> 32);
+// function, so backward regenerates the forward mask with no mask tensor.  One 32-bit
+// hash (lowbias32 finaliser, two 32-bit multiplies) serves the element pair idx>>1, each
+// element using 16 of its bits; the 64-bit seed is folded into a 32-bit stream key that is
+// uniform across the launch (scalar unit, hoisted out of the loops).
+__host__ __device__ inline uint32_t ea_mix32(uint32_t x) {
+  x ^= x >> 16; x *= 0x7feb352dU; x ^= x >> 15; x *= 0x846ca68bU; x ^= x >> 16;
+  return x;
 }
+__host__ __device__ inline uint32_t ea_seed_key(uint64_t seed) {
+  return ea_mix32((uint32_t)seed ^ ea_mix32((uint32_t)(seed >> 32) ^ 0x5bd1e995U));
+}
+EA_DEV uint32_t ea_pair_hash(uint32_t key, uint64_t pair) {
+  return ea_mix32(((uint32_t)pair ^ ((uint32_t)(pair >> 32) * 0x85ebca6bU)) * 0x9e3779b9U + key);
+}
+EA_DEV uint32_t ea_drop_thr(float p) { return (uint32_t)fminf(p * 65536.f + 0.5f, 65536.f); }
 // returns scale (1/(1-p)) if kept, 0 if dropped; p<=0 -> 1
 EA_DEV float drop_scale(uint64_t seed, uint64_t idx, float p) {
   if (p <= 0.f) return 1.f;
-  const uint32_t thr = (uint32_t)fminf(p * 4294967296.0f, 4294967295.0f);
-  return ea_hash(seed, idx) >= thr ? 1.f / (1.f - p) : 0.f;
+  const uint32_t h = ea_pair_hash(ea_seed_key(seed), idx >> 1);
+  const uint32_t bits = (idx & 1) ? h >> 16 : h & 0xffffu;
+  return bits >= ea_drop_thr(p) ? 1.f / (1.f - p) : 0.f;
+}
+// four consecutive elements idx .. idx+3, idx even (two hashes); s[k] *= scale
+EA_DEV void drop_scale4(uint64_t seed, uint64_t idx, float p, float (&v)[4]) {
+  if (p <= 0.f) return;
+  const uint32_t key = ea_seed_key(seed), thr = ea_drop_thr(p);
+  const float sc = 1.f / (1.f - p);
+  const uint32_t h0 = ea_pair_hash(key, idx >> 1), h1 = ea_pair_hash(key, (idx >> 1) + 1);
+  v[0] *= (h0 & 0xffffu) >= thr ? sc : 0.f;
+  v[1] *= (h0 >> 16) >= thr ? sc : 0.f;
+  v[2] *= (h1 & 0xffffu) >= thr ? sc : 0.f;
+  v[3] *= (h1 >> 16) >= thr ? sc : 0.f;
 }
 
 // ------------------------------------------------------------------ activations
-EA_DEV float sigmoidf_(float x) { return 1.f / (1.f + __expf(-x)); }
+EA_DEV float sigmoidf_(float x) { return __builtin_amdgcn_rcpf(1.f + __expf(-x)); }
 EA_DEV float act_fwd(int act, float h) {
   if (act == EA_ACT_SWISH) return h * sigmoidf_(h);
   if (act == EA_ACT_RELU) return h > 0.f ? h : 0.f;
@@ -126,3 +162,7 @@ EA_DEV double block_sum_d(double v, double* red) {
 
 __host__ __device__ static inline int ea_cdiv(long a, long b) { return (int)((a + b - 1) / b); }
 static inline int ea_grid_cap(long blocks, int cap = 4096) { return (int)(blocks < cap ? (blocks > 0 ? blocks : 1) : cap); }
+
+// internal cross-file helper (norm.hip): reduce_partials with a transposed output
+int ea_reduce_partials_tr(int nparts, int n, const float* part, long stride, float* out, int accumulate,
+                          int tr_rows, int tr_cols, void* stream);

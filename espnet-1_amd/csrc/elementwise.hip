@@ -83,6 +83,36 @@ __global__ void scale_drop_kernel(long n, int cols, const TI* __restrict__ x, lo
   }
 }
 
+// 4 columns per thread (cols, lds % 4 == 0, aligned); same per-element dropout index as above
+template <typename TI, typename TO>
+__global__ __launch_bounds__(256) void scale_drop_vec_kernel(unsigned n4, unsigned cols4, const TI* __restrict__ x, long ldx,
+                                                             TO* __restrict__ y, long ldy, float scale, float p,
+                                                             uint64_t seed) {
+  for (unsigned i = blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += gridDim.x * blockDim.x) {
+    const unsigned r = i / cols4, c = (i - r * cols4) * 4;
+    float v[4];
+    vld4(x + (long)r * ldx + c, v);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) v[k] *= scale;
+    drop_scale4(seed, (uint64_t)i * 4, p, v);
+    vst4(y + (long)r * ldy + c, v);
+  }
+}
+
+template <typename TI, typename TO>
+__global__ __launch_bounds__(256) void add2d_vec_kernel(unsigned n4, unsigned cols4, const TI* __restrict__ x, long ldx,
+                                                        TO* __restrict__ y, long ldy, float alpha) {
+  for (unsigned i = blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += gridDim.x * blockDim.x) {
+    const unsigned r = i / cols4, c = (i - r * cols4) * 4;
+    float v[4], o[4];
+    vld4(x + (long)r * ldx + c, v);
+    vld4(y + (long)r * ldy + c, o);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) o[k] += alpha * v[k];
+    vst4(y + (long)r * ldy + c, o);
+  }
+}
+
 // y[r,c] += alpha * x[r,c]
 template <typename TI, typename TO>
 __global__ void add2d_kernel(long n, int cols, const TI* __restrict__ x, long ldx, TO* __restrict__ y, long ldy, float alpha) {
@@ -335,6 +365,140 @@ __global__ __launch_bounds__(256) void dwconv_bwd_kernel(int B, int T, int C, in
   }
 }
 
+// Register-window variants for a compile-time kernel width: each thread owns one channel and
+// 8 consecutive time rows, holds the 8+K-1 input rows it touches in registers (one LDS read
+// per row instead of one per tap) and does the 8*K taps from registers.
+template <int K>
+__global__ __launch_bounds__(256) void dwconv_fwd_k_kernel(int B, int T, int C, const float* __restrict__ x,
+                                                           const float* __restrict__ w,
+                                                           const float* __restrict__ bias, float* __restrict__ y) {
+  constexpr int P = (K - 1) / 2, RL = DW_TT + K - 1, WIN = 8 + K - 1;
+  __shared__ float tile[RL * DW_CT];
+  const int ntt = ea_cdiv(T, DW_TT);
+  const int b = blockIdx.x / ntt, t0 = (blockIdx.x % ntt) * DW_TT;
+  const int c0 = blockIdx.y * DW_CT;
+  const int cc = threadIdx.x % DW_CT, tq = threadIdx.x / DW_CT;
+  const int c = c0 + cc;
+  if (C % 4 == 0) {  // 16-B loads: 16 lanes cover one 64-channel row
+    for (int i = threadIdx.x; i < RL * (DW_CT / 4); i += 256) {
+      const int rr = i / (DW_CT / 4), c4 = (i % (DW_CT / 4)) * 4;
+      const int t = t0 + rr - P;
+      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (t >= 0 && t < T && c0 + c4 < C) v = *(const float4*)(x + ((long)b * T + t) * C + c0 + c4);
+      *(float4*)(tile + rr * DW_CT + c4) = v;
+    }
+  } else {
+    for (int rr = tq; rr < RL; rr += 4) {
+      const int t = t0 + rr - P;
+      tile[rr * DW_CT + cc] = (t >= 0 && t < T && c < C) ? x[((long)b * T + t) * C + c] : 0.f;
+    }
+  }
+  __syncthreads();
+  if (c >= C) return;
+  float win[WIN];
+#pragma unroll
+  for (int i = 0; i < WIN; ++i) win[i] = tile[(tq * 8 + i) * DW_CT + cc];
+  float acc[8];
+  const float b0 = bias ? bias[c] : 0.f;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) acc[j] = b0;
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    const float wk = w[c * K + k];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[j] += wk * win[j + k];
+  }
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int t = t0 + tq * 8 + j;
+    if (t < T) y[((long)b * T + t) * C + c] = acc[j];
+  }
+}
+
+// dx[t] = sum_k w[k] dy[t-k+P];  part[blk][k*C+c] = sum_t dy[t] x[t+k-P];  part[blk][K*C+c] = sum_t dy[t]
+template <int K>
+__global__ __launch_bounds__(256) void dwconv_bwd_k_kernel(int B, int T, int C, const float* __restrict__ x,
+                                                           const float* __restrict__ w, const float* __restrict__ dy,
+                                                           float* __restrict__ dx, float* __restrict__ part) {
+  constexpr int P = (K - 1) / 2, RL = DW_TT + K - 1, WIN = 8 + K - 1;
+  constexpr int SM = 2 * RL * DW_CT > 4 * (K + 1) * DW_CT ? 2 * RL * DW_CT : 4 * (K + 1) * DW_CT;
+  __shared__ float sm[SM];
+  float* tdy = sm;                 // dy rows t0-(K-1-P) .. t0+DW_TT-1+P
+  float* tx = sm + RL * DW_CT;     // x rows  t0-P .. t0+DW_TT-1+(K-1-P)
+  const int ntt = ea_cdiv(T, DW_TT);
+  const int b = blockIdx.x / ntt, t0 = (blockIdx.x % ntt) * DW_TT;
+  const int c0 = blockIdx.y * DW_CT;
+  const int cc = threadIdx.x % DW_CT, tq = threadIdx.x / DW_CT;
+  const int c = c0 + cc;
+  if (C % 4 == 0) {
+    for (int i = threadIdx.x; i < RL * (DW_CT / 4); i += 256) {
+      const int rr = i / (DW_CT / 4), c4 = (i % (DW_CT / 4)) * 4;
+      const int td = t0 + rr - (K - 1 - P), tx_ = t0 + rr - P;
+      const bool okc = c0 + c4 < C;
+      float4 a = make_float4(0.f, 0.f, 0.f, 0.f), bb = a;
+      if (okc && td >= 0 && td < T) a = *(const float4*)(dy + ((long)b * T + td) * C + c0 + c4);
+      if (okc && tx_ >= 0 && tx_ < T) bb = *(const float4*)(x + ((long)b * T + tx_) * C + c0 + c4);
+      *(float4*)(tdy + rr * DW_CT + c4) = a;
+      *(float4*)(tx + rr * DW_CT + c4) = bb;
+    }
+  } else {
+    for (int rr = tq; rr < RL; rr += 4) {
+      const int td = t0 + rr - (K - 1 - P), tx_ = t0 + rr - P;
+      const bool okc = c < C;
+      tdy[rr * DW_CT + cc] = (okc && td >= 0 && td < T) ? dy[((long)b * T + td) * C + c] : 0.f;
+      tx[rr * DW_CT + cc] = (okc && tx_ >= 0 && tx_ < T) ? x[((long)b * T + tx_) * C + c] : 0.f;
+    }
+  }
+  __syncthreads();
+  float aw[K + 1];
+  {
+    float win[WIN];
+#pragma unroll
+    for (int i = 0; i < WIN; ++i) win[i] = tdy[(tq * 8 + i) * DW_CT + cc];
+    if (c < C) {
+      float acc[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[j] = 0.f;
+#pragma unroll
+      for (int k = 0; k < K; ++k) {
+        const float wk = w[c * K + k];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc[j] += wk * win[j - k + K - 1];
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int t = t0 + tq * 8 + j;
+        if (t < T) dx[((long)b * T + t) * C + c] = acc[j];
+      }
+    }
+    // dy[t0 + tq*8 + j] = win[j + K-1-P]  (rows past T are zero)
+    float xw[WIN];
+#pragma unroll
+    for (int i = 0; i < WIN; ++i) xw[i] = tx[(tq * 8 + i) * DW_CT + cc];
+#pragma unroll
+    for (int k = 0; k <= K; ++k) aw[k] = 0.f;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float d = win[j + K - 1 - P];
+      aw[K] += d;
+#pragma unroll
+      for (int k = 0; k < K; ++k) aw[k] += d * xw[j + k];
+    }
+  }
+  __syncthreads();  // reuse the tiles for the 4-group reduction
+#pragma unroll
+  for (int k = 0; k <= K; ++k) sm[(tq * (K + 1) + k) * DW_CT + cc] = aw[k];
+  __syncthreads();
+  const long blk = (long)blockIdx.x;
+  for (int i = threadIdx.x; i < (K + 1) * DW_CT; i += blockDim.x) {
+    const int k = i / DW_CT, ci = i % DW_CT, cg = c0 + ci;
+    if (cg >= C) continue;
+    const float v = (sm[(0 * (K + 1) + k) * DW_CT + ci] + sm[(1 * (K + 1) + k) * DW_CT + ci]) +
+                    (sm[(2 * (K + 1) + k) * DW_CT + ci] + sm[(3 * (K + 1) + k) * DW_CT + ci]);
+    part[blk * (long)C * (K + 1) + (long)k * C + cg] = v;  // [k][c] (coalesced); k == K: dbias
+  }
+}
+
 // ---------------------------------------------------------------- attention helpers
 // qu = q + u[h], qv = q + v[h] for q rows of (N, H*dk) inside a fused qkv buffer
 template <typename T>
@@ -433,6 +597,19 @@ extern "C" int ea_scale_dropout(long rows, int cols, const void* x, int x_dtype,
   EA_ENTRY();
   const long n = rows * cols;
   if (n == 0) return 0;
+  const int xa = x_dtype == EA_BF16 ? 8 : 16, ya = y_dtype == EA_BF16 ? 8 : 16;
+  if (cols % 4 == 0 && ldx % 4 == 0 && ldy % 4 == 0 && (uintptr_t)x % xa == 0 && (uintptr_t)y % ya == 0 &&
+      n / 4 < (1L << 31)) {
+    const unsigned n4 = (unsigned)(n / 4), c4 = (unsigned)(cols / 4);
+#define EA_SDV(TI, TO) hipLaunchKernelGGL((scale_drop_vec_kernel<TI, TO>), EA_GRID(n4), n4, c4, (const TI*)x, ldx, (TO*)y, ldy, scale, p, (uint64_t)seed)
+    if (x_dtype == EA_BF16 && y_dtype == EA_BF16) EA_SDV(bf16, bf16);
+    else if (x_dtype == EA_BF16) EA_SDV(bf16, float);
+    else if (y_dtype == EA_BF16) EA_SDV(float, bf16);
+    else EA_SDV(float, float);
+#undef EA_SDV
+    EA_LAUNCH_CHECK();
+    return 0;
+  }
 #define EA_SD(TI, TO) hipLaunchKernelGGL((scale_drop_kernel<TI, TO>), EA_GRID(n), n, cols, (const TI*)x, ldx, (TO*)y, ldy, scale, p, (uint64_t)seed)
   if (x_dtype == EA_BF16 && y_dtype == EA_BF16) EA_SD(bf16, bf16);
   else if (x_dtype == EA_BF16) EA_SD(bf16, float);
@@ -448,6 +625,19 @@ extern "C" int ea_add_2d(long rows, int cols, const void* x, int x_dtype, long l
   EA_ENTRY();
   const long n = rows * cols;
   if (n == 0) return 0;
+  const int xa = x_dtype == EA_BF16 ? 8 : 16, ya = y_dtype == EA_BF16 ? 8 : 16;
+  if (cols % 4 == 0 && ldx % 4 == 0 && ldy % 4 == 0 && (uintptr_t)x % xa == 0 && (uintptr_t)y % ya == 0 &&
+      n / 4 < (1L << 31)) {
+    const unsigned n4 = (unsigned)(n / 4), c4 = (unsigned)(cols / 4);
+#define EA_A2V(TI, TO) hipLaunchKernelGGL((add2d_vec_kernel<TI, TO>), EA_GRID(n4), n4, c4, (const TI*)x, ldx, (TO*)y, ldy, alpha)
+    if (x_dtype == EA_BF16 && y_dtype == EA_BF16) EA_A2V(bf16, bf16);
+    else if (x_dtype == EA_BF16) EA_A2V(bf16, float);
+    else if (y_dtype == EA_BF16) EA_A2V(float, bf16);
+    else EA_A2V(float, float);
+#undef EA_A2V
+    EA_LAUNCH_CHECK();
+    return 0;
+  }
 #define EA_A2(TI, TO) hipLaunchKernelGGL((add2d_kernel<TI, TO>), EA_GRID(n), n, cols, (const TI*)x, ldx, (TO*)y, ldy, alpha)
   if (x_dtype == EA_BF16 && y_dtype == EA_BF16) EA_A2(bf16, bf16);
   else if (x_dtype == EA_BF16) EA_A2(bf16, float);
@@ -548,8 +738,16 @@ extern "C" int ea_dwconv_fwd(int B, int T, int C, int K, const float* x, const f
   EA_ENTRY();
   EA_CHECK_ARG(K % 2 == 1);
   dim3 grid(B * ea_cdiv(T, DW_TT), ea_cdiv(C, DW_CT));
-  const size_t sm = (size_t)(DW_TT + K - 1) * DW_CT * sizeof(float);
-  hipLaunchKernelGGL(dwconv_fwd_kernel, grid, dim3(256), sm, (hipStream_t)stream, B, T, C, K, x, w, bias, y);
+  hipStream_t st = (hipStream_t)stream;
+  switch (K) {
+#define EA_DWF(KK) case KK: hipLaunchKernelGGL(dwconv_fwd_k_kernel<KK>, grid, dim3(256), 0, st, B, T, C, x, w, bias, y); break;
+    EA_DWF(3) EA_DWF(5) EA_DWF(7) EA_DWF(15) EA_DWF(31)
+#undef EA_DWF
+    default: {
+      const size_t sm = (size_t)(DW_TT + K - 1) * DW_CT * sizeof(float);
+      hipLaunchKernelGGL(dwconv_fwd_kernel, grid, dim3(256), sm, st, B, T, C, K, x, w, bias, y);
+    }
+  }
   EA_LAUNCH_CHECK();
   return 0;
 }
@@ -560,8 +758,24 @@ extern "C" int ea_dwconv_bwd(int B, int T, int C, int K, const float* x, const f
   EA_ENTRY();
   EA_CHECK_ARG(K % 2 == 1);
   const int nblk = B * ea_cdiv(T, DW_TT);
-  EA_CHECK_ARG((long)nblk * C * K <= ws_elems);
   dim3 grid(nblk, ea_cdiv(C, DW_CT));
+  if (K == 3 || K == 5 || K == 7 || K == 15 || K == 31) {
+    // one fused pass: dx, and per-block partials of dw and dbias
+    const long rowlen = (long)C * (K + 1);
+    EA_CHECK_ARG((long)nblk * rowlen <= ws_elems);
+    hipStream_t st = (hipStream_t)stream;
+    switch (K) {
+#define EA_DWB(KK) case KK: hipLaunchKernelGGL(dwconv_bwd_k_kernel<KK>, grid, dim3(256), 0, st, B, T, C, x, w, dy, dx, workspace); break;
+      EA_DWB(3) EA_DWB(5) EA_DWB(7) EA_DWB(15) EA_DWB(31)
+#undef EA_DWB
+    }
+    EA_LAUNCH_CHECK();
+    // partial columns are [k][c]; dw is (C, 1, K): the reduction writes it transposed
+    int rc = ea_reduce_partials_tr(nblk, C * K, workspace, rowlen, dw, accumulate_params, C, K, stream);
+    if (rc || !dbias) return rc;
+    return ea_reduce_partials(nblk, C, workspace + (long)C * K, rowlen, dbias, accumulate_params, stream);
+  }
+  EA_CHECK_ARG((long)nblk * C * K <= ws_elems);
   const size_t sm = (size_t)(2 * (DW_TT + K - 1) + DW_TT) * DW_CT * sizeof(float);
   hipStream_t st = (hipStream_t)stream;
   hipLaunchKernelGGL(dwconv_bwd_kernel, grid, dim3(256), sm, st, B, T, C, K, x, w, dy, dx, workspace);

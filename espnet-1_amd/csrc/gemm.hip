@@ -37,6 +37,7 @@ struct GemmP {
   int tiles_m, tiles_n;
   int vec_a, vec_b;  // 16-B vector loads allowed (aligned base, ld and batch strides)
   int vec_c;         // 4-column vector epilogue allowed (aligned C/aux/resid/bias, N % 4 == 0)
+  int bm;            // output tile rows (128, or 64 for small grids with K-major A)
 };
 
 EA_DEV int swz_k(int row) { return (row >> 1) & 7; }                         // K-major rows
@@ -218,10 +219,8 @@ EA_DEV void epi_four(const GemmP& p, int z, int zb, int zh, int row, int col, co
   }
   if constexpr (KIND == EA_EPI_STORE) {
 #pragma unroll
-    for (int c = 0; c < 4; ++c) {
-      v[c] *= e.post_scale;
-      if (e.drop_p > 0.f) v[c] *= drop_scale(e.seed, didx + c, e.drop_p);
-    }
+    for (int c = 0; c < 4; ++c) v[c] *= e.post_scale;
+    drop_scale4(e.seed, didx, e.drop_p, v);
     if (e.beta != 0.f) {
       float o[4];
       ld4(p.C, cidx, p.c_dtype, o);
@@ -232,28 +231,22 @@ EA_DEV void epi_four(const GemmP& p, int z, int zb, int zh, int row, int col, co
   } else if constexpr (KIND == EA_EPI_ACT) {
     if (e.aux) st4(e.aux, (long)row * e.ldaux + col, e.aux_dtype, v);
 #pragma unroll
-    for (int c = 0; c < 4; ++c) {
-      v[c] = act_fwd(e.act, v[c]);
-      if (e.drop_p > 0.f) v[c] *= drop_scale(e.seed, didx + c, e.drop_p);
-    }
+    for (int c = 0; c < 4; ++c) v[c] = act_fwd(e.act, v[c]);
+    drop_scale4(e.seed, didx, e.drop_p, v);
     st4(p.C, cidx, p.c_dtype, v);
   } else if constexpr (KIND == EA_EPI_RESID) {
     float r[4] = {0.f, 0.f, 0.f, 0.f};
     if (e.resid) ld4(e.resid, (long)row * e.ldr + col, EA_F32, r);
+    drop_scale4(e.seed, didx, e.drop_p, v);
 #pragma unroll
-    for (int c = 0; c < 4; ++c) {
-      if (e.drop_p > 0.f) v[c] *= drop_scale(e.seed, didx + c, e.drop_p);
-      v[c] = r[c] + e.rscale * v[c];
-    }
+    for (int c = 0; c < 4; ++c) v[c] = r[c] + e.rscale * v[c];
     st4(p.C, cidx, EA_F32, v);
   } else {
     float h[4];
     ld4(e.aux, (long)row * e.ldaux + col, e.aux_dtype, h);
+    drop_scale4(e.seed, didx, e.drop_p, v);
 #pragma unroll
-    for (int c = 0; c < 4; ++c) {
-      if (e.drop_p > 0.f) v[c] *= drop_scale(e.seed, didx + c, e.drop_p);
-      v[c] *= act_bwd(e.act, h[c]);
-    }
+    for (int c = 0; c < 4; ++c) v[c] *= act_bwd(e.act, h[c]);
     st4(p.C, cidx, p.c_dtype, v);
   }
 }
@@ -263,13 +256,13 @@ constexpr int EPI_LDT = 68;  // floats per LDS row of a wave's 64x64 accumulator
 // Transpose the wave's 64x64 accumulators through LDS, then apply the epilogue four
 // columns at a time.  `vec` (host-checked alignment of C/aux/resid/bias and N % 4 == 0)
 // selects the vector path; otherwise element-wise.
-template <int KIND>
+template <int KIND, int MI = 4>
 EA_DEV void epi_tile_lds(const GemmP& p, char* smem, int z, int zb, int zh, int r0, int c0, int lane, int w,
-                         const f32x4 (&acc)[4][4]) {
-  float* t = (float*)smem + w * 64 * EPI_LDT;
+                         const f32x4 (&acc)[MI][4]) {
+  float* t = (float*)smem + w * (MI * 16) * EPI_LDT;
   const int rq = (lane >> 4) * 4, cc = lane & 15;
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
+  for (int i = 0; i < MI; ++i)
 #pragma unroll
     for (int j = 0; j < 4; ++j)
 #pragma unroll
@@ -278,7 +271,7 @@ EA_DEV void epi_tile_lds(const GemmP& p, char* smem, int z, int zb, int zh, int 
   asm volatile("" ::: "memory");
   const int lc = (lane & 15) * 4;
 #pragma unroll 4
-  for (int it = 0; it < 16; ++it) {
+  for (int it = 0; it < MI * 4; ++it) {
     const int lr = it * 4 + (lane >> 4);
     const int row = r0 + lr, col = c0 + lc;
     if (row >= p.M || col >= p.N) continue;
@@ -437,11 +430,53 @@ EA_DEV void lds_barrier() {
   asm volatile("" ::: "memory");
 }
 
-template <bool AK, bool BKM, int STAGES>
+// Tile-row-generic tail loader/storer (K-major ROWS x 64 or MN-major 64 x 128 images).
+template <bool KMAJ, int ROWS>
+EA_DEV void load_tile_r(const bf16* __restrict__ base, long ld, int mn0, int MN, int k0, int K, uint4 (&v)[4]) {
+  constexpr int CPR = KMAJ ? 8 : 16;
+  constexpr int NCH = KMAJ ? ROWS * 8 / NT : 4;
+#pragma unroll
+  for (int i = 0; i < NCH; ++i) {
+    const int c = threadIdx.x + NT * i;
+    const int row = c / CPR, ch = c % CPR;
+    int mn, k;
+    if (KMAJ) { mn = mn0 + row; k = k0 + ch * 8; }
+    else      { k = k0 + row; mn = mn0 + ch * 8; }
+    const bf16* pp = KMAJ ? base + (long)mn * ld + k : base + (long)k * ld + mn;
+    union { uint4 u; bf16 e[8]; } t;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const bool ok = KMAJ ? (mn < MN && k + e < K) : (k < K && mn + e < MN);
+      t.e[e] = ok ? pp[e] : (bf16)0.f;
+    }
+    v[i] = t.u;
+  }
+}
+template <bool KMAJ, int ROWS>
+EA_DEV void store_tile_r(char* lds, const uint4 (&v)[4]) {
+  constexpr int CPR = KMAJ ? 8 : 16;
+  constexpr int NCH = KMAJ ? ROWS * 8 / NT : 4;
+#pragma unroll
+  for (int i = 0; i < NCH; ++i) {
+    const int c = threadIdx.x + NT * i;
+    const int row = c / CPR, ch = c % CPR;
+    const int off = KMAJ ? row * 128 + ((ch ^ swz_k(row)) << 4) : row * 256 + ((ch ^ swz_mn_bf16(row)) << 4);
+    *(uint4*)(lds + off) = v[i];
+  }
+}
+
+// BM x 128 output tile (BM = 128, or 64 for K-major A on small grids: more blocks per CU).
+// 4 wave64s in 2 x 2, each (BM/2) x 64 = (BM/32) x 4 MFMA 16x16 blocks.  Fragments of k-step
+// ks+1 are read from LDS while the MFMAs of k-step ks run (register double buffer).
+template <int BM_, bool AK, bool BKM, int STAGES>
 __global__ __launch_bounds__(NT, 1) void gemm_bf16_lds(GemmP p) {
+  static_assert(AK || BM_ == 128, "MN-major A needs the 128-wide image");
   constexpr int BK = 64;
-  constexpr int STAGE_BYTES = 2 * TILE_BYTES;
-  constexpr int EPI_BYTES = 4 * 64 * EPI_LDT * 4;
+  constexpr int A_BYTES = BM_ * BK * 2;
+  constexpr int STAGE_BYTES = A_BYTES + TILE_BYTES;
+  constexpr int MI = BM_ / 32;          // MFMA row blocks per wave
+  constexpr int ACH = AK ? BM_ * 8 / NT : 4;  // A DMA chunks per thread per K-tile
+  constexpr int EPI_BYTES = 4 * (BM_ / 2) * EPI_LDT * 4;
   constexpr int SMEM = STAGES * STAGE_BYTES > EPI_BYTES ? STAGES * STAGE_BYTES : EPI_BYTES;
   __shared__ __attribute__((aligned(1024))) char smem[SMEM];
 
@@ -455,7 +490,7 @@ __global__ __launch_bounds__(NT, 1) void gemm_bf16_lds(GemmP p) {
   const int gsz = min(GM, p.tiles_m - gm0);
   const int tm = gm0 + (t % (GM * p.tiles_n)) % gsz;
   const int tn = (t % (GM * p.tiles_n)) / gsz;
-  const int m0 = tm * BM, n0 = tn * BN;
+  const int m0 = tm * BM_, n0 = tn * BN;
 
   const int z = blockIdx.z / p.splitk, sk = blockIdx.z % p.splitk;
   const int zb = z / p.nh, zh = z % p.nh;
@@ -467,14 +502,12 @@ __global__ __launch_bounds__(NT, 1) void gemm_bf16_lds(GemmP p) {
   const bool tail = kbeg + nfull * BK < kend;
 
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int wm = (w >> 1) * 64, wn = (w & 1) * 64;
+  const int wm = (w >> 1) * (BM_ / 2), wn = (w & 1) * 64;
 
-  // per-thread DMA sources (4 chunks of A, 4 of B per K-tile)
-  const bf16* asrc[4];
+  const bf16* asrc[ACH];
   const bf16* bsrc[4];
-  long astep, bstep;
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
+  for (int i = 0; i < ACH; ++i) {
     const int ci = (i * 4 + w) * 64 + lane;
     if (AK) {
       const int row = ci >> 3, c = (ci & 7) ^ swz_k(ci >> 3);
@@ -483,6 +516,10 @@ __global__ __launch_bounds__(NT, 1) void gemm_bf16_lds(GemmP p) {
       const int k = ci >> 4, c = (ci & 15) ^ swz_mn_bf16(ci >> 4);
       asrc[i] = A + (long)(kbeg + k) * p.lda + min((long)(m0 + c * 8), p.lda - 8);
     }
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int ci = (i * 4 + w) * 64 + lane;
     if (BKM) {
       const int row = ci >> 3, c = (ci & 7) ^ swz_k(ci >> 3);
       bsrc[i] = B + (long)min(n0 + row, p.N - 1) * p.ldb + kbeg + c * 8;
@@ -491,52 +528,59 @@ __global__ __launch_bounds__(NT, 1) void gemm_bf16_lds(GemmP p) {
       bsrc[i] = B + (long)(kbeg + k) * p.ldb + min((long)(n0 + c * 8), p.ldb - 8);
     }
   }
-  astep = AK ? BK : (long)BK * p.lda;
-  bstep = BKM ? BK : (long)BK * p.ldb;
+  const long astep = AK ? BK : (long)BK * p.lda;
+  const long bstep = BKM ? BK : (long)BK * p.ldb;
+  constexpr int GPT = ACH + 4;  // DMA instructions per thread per K-tile (vmcnt unit)
 
   auto issue = [&](int kt, int stg) {
     char* base = smem + stg * STAGE_BYTES;
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+    for (int i = 0; i < ACH; ++i)
       __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)(asrc[i] + kt * astep),
                                        (__attribute__((address_space(3))) void*)(base + (i * 4 + w) * 1024), 16, 0, 0);
 #pragma unroll
     for (int i = 0; i < 4; ++i)
       __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)(bsrc[i] + kt * bstep),
-                                       (__attribute__((address_space(3))) void*)(base + TILE_BYTES + (i * 4 + w) * 1024),
+                                       (__attribute__((address_space(3))) void*)(base + A_BYTES + (i * 4 + w) * 1024),
                                        16, 0, 0);
   };
 
-  f32x4 acc[4][4];
+  f32x4 acc[MI][4];
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
+  for (int i = 0; i < MI; ++i)
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
 
   auto compute = [&](int stg) {
     const char* la = smem + stg * STAGE_BYTES;
-    const char* lb = la + TILE_BYTES;
+    const char* lb = la + A_BYTES;
+    bf16x8 fa0[MI], fb0[4], fa1[MI], fb1[4];
 #pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
-      bf16x8 fa[4], fb[4];
+    for (int i = 0; i < MI; ++i) fa0[i] = frag_bf16<AK>(la, wm + i * 16, 0, lane);
 #pragma unroll
-      for (int i = 0; i < 4; ++i) fa[i] = frag_bf16<AK>(la, wm + i * 16, ks, lane);
+    for (int j = 0; j < 4; ++j) fb0[j] = frag_bf16<BKM>(lb, wn + j * 16, 0, lane);
 #pragma unroll
-      for (int j = 0; j < 4; ++j) fb[j] = frag_bf16<BKM>(lb, wn + j * 16, ks, lane);
+    for (int i = 0; i < MI; ++i) fa1[i] = frag_bf16<AK>(la, wm + i * 16, 1, lane);
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
+    for (int j = 0; j < 4; ++j) fb1[j] = frag_bf16<BKM>(lb, wn + j * 16, 1, lane);
 #pragma unroll
-        for (int j = 0; j < 4; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
-    }
+    for (int i = 0; i < MI; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa0[i], fb0[j], acc[i][j], 0, 0, 0);
+#pragma unroll
+    for (int i = 0; i < MI; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa1[i], fb1[j], acc[i][j], 0, 0, 0);
   };
 
   const int npre = min(STAGES - 1, nfull);
   for (int kt = 0; kt < npre; ++kt) issue(kt, kt);
   for (int kt = 0; kt < nfull; ++kt) {
     const int after = min(STAGES - 2, nfull - 1 - kt);  // newer tiles allowed in flight
-    if (after >= 2) wait_vmcnt<16>();
-    else if (after == 1) wait_vmcnt<8>();
+    if (after >= 2) wait_vmcnt<2 * GPT>();
+    else if (after == 1) wait_vmcnt<GPT>();
     else wait_vmcnt<0>();
     lds_barrier();
     if (kt + STAGES - 1 < nfull) issue(kt + STAGES - 1, (kt + STAGES - 1) % STAGES);
@@ -545,22 +589,22 @@ __global__ __launch_bounds__(NT, 1) void gemm_bf16_lds(GemmP p) {
   if (tail) {
     uint4 ra[4], rb[4];
     const int k0 = kbeg + nfull * BK;
-    load_tile<bf16, AK>(A, p.lda, m0, p.M, k0, kend, 1, ra);
-    load_tile<bf16, BKM>(B, p.ldb, n0, p.N, k0, kend, 1, rb);
+    load_tile_r<AK, BM_>(A, p.lda, m0, p.M, k0, kend, ra);
+    load_tile_r<BKM, 128>(B, p.ldb, n0, p.N, k0, kend, rb);
     __syncthreads();
     char* base = smem + (nfull % STAGES) * STAGE_BYTES;
-    store_tile<bf16, AK>(base, ra);
-    store_tile<bf16, BKM>(base + TILE_BYTES, rb);
+    store_tile_r<AK, BM_>(base, ra);
+    store_tile_r<BKM, 128>(base + A_BYTES, rb);
     __syncthreads();
     compute(nfull % STAGES);
   }
 
   __syncthreads();  // every wave is done reading the operand ring: reuse it for the epilogue
   switch (p.splitk > 1 ? EA_EPI_STORE : p.epi.kind) {
-    case EA_EPI_STORE: epi_tile_lds<EA_EPI_STORE>(p, smem, z, zb, zh, m0 + wm, n0 + wn, lane, w, acc); break;
-    case EA_EPI_ACT: epi_tile_lds<EA_EPI_ACT>(p, smem, z, zb, zh, m0 + wm, n0 + wn, lane, w, acc); break;
-    case EA_EPI_RESID: epi_tile_lds<EA_EPI_RESID>(p, smem, z, zb, zh, m0 + wm, n0 + wn, lane, w, acc); break;
-    default: epi_tile_lds<EA_EPI_DACT>(p, smem, z, zb, zh, m0 + wm, n0 + wn, lane, w, acc); break;
+    case EA_EPI_STORE: epi_tile_lds<EA_EPI_STORE, MI>(p, smem, z, zb, zh, m0 + wm, n0 + wn, lane, w, acc); break;
+    case EA_EPI_ACT: epi_tile_lds<EA_EPI_ACT, MI>(p, smem, z, zb, zh, m0 + wm, n0 + wn, lane, w, acc); break;
+    case EA_EPI_RESID: epi_tile_lds<EA_EPI_RESID, MI>(p, smem, z, zb, zh, m0 + wm, n0 + wn, lane, w, acc); break;
+    default: epi_tile_lds<EA_EPI_DACT, MI>(p, smem, z, zb, zh, m0 + wm, n0 + wn, lane, w, acc); break;
   }
 }
 
@@ -595,14 +639,21 @@ __global__ void splitk_reduce(GemmP p) {
   }
 }
 
-int g_gemm_stages = 2;  // LDS ring depth of gemm_bf16_lds (2: 64 KiB, 2 blocks/CU; 3: 96 KiB)
+int g_gemm_stages = 2;
+int g_gemm_bm64 = 1;  // LDS ring depth of gemm_bf16_lds (2: 64 KiB, 2 blocks/CU; 3: 96 KiB)
 
 int launch_lds(GemmP& p, int a_k, int b_k, int nz, hipStream_t st) {
   dim3 grid(p.tiles_m * p.tiles_n, 1, nz * p.splitk);
-#define EA_GL_CASE(AKV, BKV)                                                                        \
-  if (a_k == AKV && b_k == BKV) {                                                                   \
-    if (g_gemm_stages >= 3) hipLaunchKernelGGL((gemm_bf16_lds<AKV, BKV, 3>), grid, dim3(NT), 0, st, p); \
-    else hipLaunchKernelGGL((gemm_bf16_lds<AKV, BKV, 2>), grid, dim3(NT), 0, st, p);               \
+  if (p.bm == 64) {
+    if (b_k) hipLaunchKernelGGL((gemm_bf16_lds<64, true, true, 2>), grid, dim3(NT), 0, st, p);
+    else hipLaunchKernelGGL((gemm_bf16_lds<64, true, false, 2>), grid, dim3(NT), 0, st, p);
+    EA_LAUNCH_CHECK();
+    return 0;
+  }
+#define EA_GL_CASE(AKV, BKV)                                                                             \
+  if (a_k == AKV && b_k == BKV) {                                                                        \
+    if (g_gemm_stages >= 3) hipLaunchKernelGGL((gemm_bf16_lds<128, AKV, BKV, 3>), grid, dim3(NT), 0, st, p); \
+    else hipLaunchKernelGGL((gemm_bf16_lds<128, AKV, BKV, 2>), grid, dim3(NT), 0, st, p);               \
   }
   EA_GL_CASE(true, true)
   else EA_GL_CASE(true, false)
@@ -616,6 +667,7 @@ int launch_lds(GemmP& p, int a_k, int b_k, int nz, hipStream_t st) {
 template <typename T>
 int launch(GemmP& p, int a_k, int b_k, int nz, hipStream_t st) {
   if (sizeof(T) == 2 && p.vec_a && p.vec_b && g_gemm_stages > 0) return launch_lds(p, a_k, b_k, nz, st);
+  if (p.bm != 128) return EA_ERR_BAD_ARG;
   dim3 grid(p.tiles_m * p.tiles_n, 1, nz * p.splitk);
 #define EA_GEMM_CASE(AKV, BKV)                                                      \
   if (a_k == AKV && b_k == BKV) {                                                   \
@@ -634,8 +686,9 @@ int launch(GemmP& p, int a_k, int b_k, int nz, hipStream_t st) {
 
 extern "C" int ea_gemm_set_pipeline(int stages) {
   EA_ENTRY();
-  EA_CHECK_ARG(stages == 0 || stages == 2 || stages == 3);
-  g_gemm_stages = stages;
+  EA_CHECK_ARG(stages == 0 || stages == 2 || stages == 3 || stages == 12 || stages == 13);
+  g_gemm_bm64 = stages < 10;   // 12/13: same ring, 128-row tiles only (A/B measurements)
+  g_gemm_stages = stages % 10;
   return 0;
 }
 
@@ -661,8 +714,6 @@ extern "C" int ea_gemm(int dtype, int a_kmajor, int b_kmajor, int M, int N, int 
   p.C = C; p.c_dtype = c_dtype; p.ldc = ldc; p.sCb = sCb; p.sCh = sCh;
   p.epi = *epi;
   p.ws = workspace;
-  p.tiles_m = ea_cdiv(M, BM);
-  p.tiles_n = ea_cdiv(N, BN);
   // unaligned operands (odd vocab / leading dims) take the element-wise load path
   p.vec_a = (lda % E == 0 && sAb % E == 0 && sAh % E == 0 && ((uintptr_t)A % 16) == 0);
   p.vec_b = (ldb % E == 0 && sBb % E == 0 && sBh % E == 0 && ((uintptr_t)B % 16) == 0);
@@ -674,6 +725,12 @@ extern "C" int ea_gemm(int dtype, int a_kmajor, int b_kmajor, int M, int N, int 
     if (epi->resid) vc = vc && epi->ldr % 4 == 0 && ((uintptr_t)epi->resid % 16) == 0;
     p.vec_c = vc;
   }
+  p.bm = 128;
+  if (g_gemm_bm64 && dtype == EA_BF16 && a_kmajor && p.vec_a && p.vec_b && g_gemm_stages > 0 &&
+      (long)ea_cdiv(M, 128) * ea_cdiv(N, BN) * batch * nh < 480)
+    p.bm = 64;  // < ~2 tiles per CU at 128 rows: halve the tile to double the blocks
+  p.tiles_m = ea_cdiv(M, p.bm);
+  p.tiles_n = ea_cdiv(N, BN);
   const int KT = dtype == EA_BF16 ? KCfg<bf16>::KT : KCfg<float>::KT;
   const int nz = batch * nh;
   // split-K when the output grid cannot fill the 256 CUs and K is long (dW GEMMs)

@@ -111,21 +111,33 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(int rows, int d, const TI* 
 }
 
 // out[c] (+)= sum_p part[p*stride + c], c < n.  Block = 64 columns x 4 part-lanes; each
-// lane sums a fixed strided subset of the parts, lanes combine in fixed order through LDS
-// (deterministic).  Keep nparts small (<= ~128) upstream: this is latency-, not BW-bound.
+// lane sums a fixed strided subset of the parts (8 loads in flight per lane: the loop is
+// latency-, not bandwidth-bound), lanes combine in fixed order through LDS (deterministic).
+// tr_rows > 0: column j = k*tr_rows + c is written to out[c*tr_cols + k] (transposed output).
 __global__ __launch_bounds__(256) void reduce_partials_kernel(int nparts, int n, const float* __restrict__ part,
-                                                              long stride, float* __restrict__ out, int accumulate) {
+                                                              long stride, float* __restrict__ out, int accumulate,
+                                                              int tr_rows = 0, int tr_cols = 0) {
   __shared__ double red[4][64];
   const int cx = threadIdx.x & 63, py = threadIdx.x >> 6;
   const int c = blockIdx.x * 64 + cx;
   double a = 0.0;
-  if (c < n)
-    for (int p = py; p < nparts; p += 4) a += part[(long)p * stride + c];
+  if (c < n) {
+    int p = py;
+    for (; p + 28 < nparts; p += 32) {
+      float v[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = part[(long)(p + 4 * j) * stride + c];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) a += v[j];
+    }
+    for (; p < nparts; p += 4) a += part[(long)p * stride + c];
+  }
   red[py][cx] = a;
   __syncthreads();
   if (py == 0 && c < n) {
     const double t = (red[0][cx] + red[1][cx]) + (red[2][cx] + red[3][cx]);
-    out[c] = accumulate ? out[c] + (float)t : (float)t;
+    const long o = tr_rows > 0 ? (long)(c % tr_rows) * tr_cols + c / tr_rows : c;
+    out[o] = accumulate ? out[o] + (float)t : (float)t;
   }
 }
 
@@ -157,27 +169,44 @@ __global__ __launch_bounds__(256) void colsum_vec_kernel(int rows, int n, const 
   const int c = blockIdx.x * 256 + lane * 4;
   const int r0 = blockIdx.y * rows_per_part, r1 = min(rows, r0 + rows_per_part);
   float a[4] = {0.f, 0.f, 0.f, 0.f}, g[4] = {0.f, 0.f, 0.f, 0.f};
+  auto load4 = [&](int r, float (&v)[4]) {
+    if (sizeof(T) == 2) {
+      const uint2 u = *(const uint2*)(x + (long)r * ld + c);
+      const bf16* b = (const bf16*)&u;
+      v[0] = (float)b[0]; v[1] = (float)b[1]; v[2] = (float)b[2]; v[3] = (float)b[3];
+    } else {
+      const float4 f = *(const float4*)(x + (long)r * ld + c);
+      v[0] = f.x; v[1] = f.y; v[2] = f.z; v[3] = f.w;
+    }
+  };
+  auto acc_row = [&](int r, const float (&v)[4], float4 xv) {
+    if (LN) {
+      const float mu = mean[r], rs = rstd[r];
+      g[0] += v[0] * (xv.x - mu) * rs;
+      g[1] += v[1] * (xv.y - mu) * rs;
+      g[2] += v[2] * (xv.z - mu) * rs;
+      g[3] += v[3] * (xv.w - mu) * rs;
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) a[k] += v[k];
+  };
   if (c < n) {
-    for (int r = r0 + w; r < r1; r += 4) {
-      float v[4];
-      if (sizeof(T) == 2) {
-        const uint2 u = *(const uint2*)(x + (long)r * ld + c);
-        const bf16* b = (const bf16*)&u;
-        v[0] = (float)b[0]; v[1] = (float)b[1]; v[2] = (float)b[2]; v[3] = (float)b[3];
-      } else {
-        const float4 f = *(const float4*)(x + (long)r * ld + c);
-        v[0] = f.x; v[1] = f.y; v[2] = f.z; v[3] = f.w;
-      }
-      if (LN) {
-        const float mu = mean[r], rs = rstd[r];
-        const float4 xv = *(const float4*)(xin + (long)r * ldxin + c);
-        g[0] += v[0] * (xv.x - mu) * rs;
-        g[1] += v[1] * (xv.y - mu) * rs;
-        g[2] += v[2] * (xv.z - mu) * rs;
-        g[3] += v[3] * (xv.w - mu) * rs;
+    int r = r0 + w;
+    for (; r + 12 < r1; r += 16) {  // 4 rows per wave in flight
+      float v[4][4];
+      float4 xv[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        load4(r + 4 * j, v[j]);
+        if (LN) xv[j] = *(const float4*)(xin + (long)(r + 4 * j) * ldxin + c);
       }
 #pragma unroll
-      for (int k = 0; k < 4; ++k) a[k] += v[k];
+      for (int j = 0; j < 4; ++j) acc_row(r + 4 * j, v[j], LN ? xv[j] : make_float4(0.f, 0.f, 0.f, 0.f));
+    }
+    for (; r < r1; r += 4) {
+      float v[4];
+      load4(r, v);
+      acc_row(r, v, LN ? *(const float4*)(xin + (long)r * ldxin + c) : make_float4(0.f, 0.f, 0.f, 0.f));
     }
   }
 #pragma unroll
@@ -341,6 +370,200 @@ __global__ void bn_bwd_apply_kernel(long total, int C, int rows, const TI* __res
   }
 }
 
+// ---- vectorised BatchNorm passes (C % 4 == 0, 16-B aligned rows): 4 channels per lane,
+// the 4 waves of a block interleave rows, 4 rows per wave in flight; one partial row per block.
+__global__ __launch_bounds__(256) void bn_partial_vec_kernel(int rows, int C, const float* __restrict__ y,
+                                                             int rows_per_blk, float* __restrict__ part) {
+  __shared__ float red[4][2][256];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int c = blockIdx.x * 256 + lane * 4;
+  const int r0 = blockIdx.y * rows_per_blk, r1 = min(rows, r0 + rows_per_blk);
+  float s[4] = {0.f, 0.f, 0.f, 0.f}, ss[4] = {0.f, 0.f, 0.f, 0.f};
+  if (c < C) {
+    const float4 sh = *(const float4*)(y + c);
+    const float shv[4] = {sh.x, sh.y, sh.z, sh.w};
+    int r = r0 + w;
+    for (; r + 12 < r1; r += 16) {
+      float4 v[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) v[j] = *(const float4*)(y + (long)(r + 4 * j) * C + c);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float t[4] = {v[j].x - shv[0], v[j].y - shv[1], v[j].z - shv[2], v[j].w - shv[3]};
+#pragma unroll
+        for (int k = 0; k < 4; ++k) { s[k] += t[k]; ss[k] += t[k] * t[k]; }
+      }
+    }
+    for (; r < r1; r += 4) {
+      const float4 v = *(const float4*)(y + (long)r * C + c);
+      const float t[4] = {v.x - shv[0], v.y - shv[1], v.z - shv[2], v.w - shv[3]};
+#pragma unroll
+      for (int k = 0; k < 4; ++k) { s[k] += t[k]; ss[k] += t[k] * t[k]; }
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < 4; ++k) { red[w][0][lane * 4 + k] = s[k]; red[w][1][lane * 4 + k] = ss[k]; }
+  __syncthreads();
+  const int cc = blockIdx.x * 256 + threadIdx.x;
+  if (cc < C) {
+    const int t = threadIdx.x;
+    part[(long)blockIdx.y * 2 * C + cc] = (red[0][0][t] + red[1][0][t]) + (red[2][0][t] + red[3][0][t]);
+    part[(long)blockIdx.y * 2 * C + C + cc] = (red[0][1][t] + red[1][1][t]) + (red[2][1][t] + red[3][1][t]);
+  }
+}
+
+// parallel finalize: 64 channels x 4 part-lanes per block, fp64 combine in fixed order
+__global__ __launch_bounds__(256) void bn_finalize_par_kernel(int rows, int C, int nparts, const float* __restrict__ y,
+                                                              const float* __restrict__ part, float eps, float momentum,
+                                                              float* __restrict__ mean, float* __restrict__ rstd,
+                                                              float* __restrict__ run_mean, float* __restrict__ run_var,
+                                                              long long* __restrict__ nbt) {
+  __shared__ double red[2][4][64];
+  const int cx = threadIdx.x & 63, py = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + cx;
+  if (blockIdx.x == 0 && threadIdx.x == 0 && nbt) nbt[0] += 1;
+  double s = 0.0, ss = 0.0;
+  if (c < C) {
+    int p = py;
+    for (; p + 12 < nparts; p += 16) {
+      float a[4], b[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        a[j] = part[(long)(p + 4 * j) * 2 * C + c];
+        b[j] = part[(long)(p + 4 * j) * 2 * C + C + c];
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) { s += a[j]; ss += b[j]; }
+    }
+    for (; p < nparts; p += 4) {
+      s += part[(long)p * 2 * C + c];
+      ss += part[(long)p * 2 * C + C + c];
+    }
+  }
+  red[0][py][cx] = s;
+  red[1][py][cx] = ss;
+  __syncthreads();
+  if (py != 0 || c >= C) return;
+  s = (red[0][0][cx] + red[0][1][cx]) + (red[0][2][cx] + red[0][3][cx]);
+  ss = (red[1][0][cx] + red[1][1][cx]) + (red[1][2][cx] + red[1][3][cx]);
+  const double n = rows;
+  const double m = s / n;
+  double var = ss / n - m * m;
+  if (var < 0) var = 0;
+  const double mu = m + (double)y[c];
+  mean[c] = (float)mu;
+  rstd[c] = (float)(1.0 / sqrt(var + (double)eps));
+  if (run_mean) {
+    run_mean[c] = (float)((1.0 - momentum) * run_mean[c] + momentum * mu);
+    run_var[c] = (float)((1.0 - momentum) * run_var[c] + momentum * var * n / (n > 1 ? n - 1 : 1));
+  }
+}
+
+template <typename TO>
+__global__ __launch_bounds__(256) void bn_apply_act_vec_kernel(int rows, int C, const float* __restrict__ y,
+                                                               const float* __restrict__ mean,
+                                                               const float* __restrict__ rstd,
+                                                               const float* __restrict__ g, const float* __restrict__ b,
+                                                               int act, TO* __restrict__ z) {
+  const int c4 = C / 4;
+  const long total4 = (long)rows * c4;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total4; i += (long)gridDim.x * blockDim.x) {
+    const int c = (int)(i % c4) * 4;
+    const float4 v = *(const float4*)(y + i * 4);
+    const float4 mu = *(const float4*)(mean + c), rs = *(const float4*)(rstd + c);
+    const float4 gg = *(const float4*)(g + c), bb = *(const float4*)(b + c);
+    float o[4];
+    o[0] = act_fwd(act, (v.x - mu.x) * rs.x * gg.x + bb.x);
+    o[1] = act_fwd(act, (v.y - mu.y) * rs.y * gg.y + bb.y);
+    o[2] = act_fwd(act, (v.z - mu.z) * rs.z * gg.z + bb.z);
+    o[3] = act_fwd(act, (v.w - mu.w) * rs.w * gg.w + bb.w);
+    vst4(z + i * 4, o);
+  }
+}
+
+template <typename TI>
+__global__ __launch_bounds__(256) void bn_bwd_partial_vec_kernel(int rows, int C, const TI* __restrict__ dz,
+                                                                 const float* __restrict__ y,
+                                                                 const float* __restrict__ mean,
+                                                                 const float* __restrict__ rstd,
+                                                                 const float* __restrict__ g,
+                                                                 const float* __restrict__ b, int act,
+                                                                 int rows_per_blk, float* __restrict__ part) {
+  __shared__ float red[4][2][256];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int c = blockIdx.x * 256 + lane * 4;
+  const int r0 = blockIdx.y * rows_per_blk, r1 = min(rows, r0 + rows_per_blk);
+  float s1[4] = {0.f, 0.f, 0.f, 0.f}, s2[4] = {0.f, 0.f, 0.f, 0.f};
+  if (c < C) {
+    float mu[4], rs[4], gg[4], bb[4];
+    vld4(mean + c, mu); vld4(rstd + c, rs); vld4(g + c, gg); vld4(b + c, bb);
+    auto accum = [&](const float (&yv)[4], const float (&dv)[4]) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const float xh = (yv[k] - mu[k]) * rs[k];
+        const float dh = dv[k] * act_bwd(act, xh * gg[k] + bb[k]);
+        s1[k] += dh * xh;
+        s2[k] += dh;
+      }
+    };
+    int r = r0 + w;
+    for (; r + 4 < r1; r += 8) {
+      float yv[2][4], dv[2][4];
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        vld4(y + (long)(r + 4 * j) * C + c, yv[j]);
+        vld4(dz + (long)(r + 4 * j) * C + c, dv[j]);
+      }
+#pragma unroll
+      for (int j = 0; j < 2; ++j) accum(yv[j], dv[j]);
+    }
+    for (; r < r1; r += 4) {
+      float yv[4], dv[4];
+      vld4(y + (long)r * C + c, yv);
+      vld4(dz + (long)r * C + c, dv);
+      accum(yv, dv);
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < 4; ++k) { red[w][0][lane * 4 + k] = s1[k]; red[w][1][lane * 4 + k] = s2[k]; }
+  __syncthreads();
+  const int cc = blockIdx.x * 256 + threadIdx.x;
+  if (cc < C) {
+    const int t = threadIdx.x;
+    part[(long)blockIdx.y * 2 * C + cc] = (red[0][0][t] + red[1][0][t]) + (red[2][0][t] + red[3][0][t]);
+    part[(long)blockIdx.y * 2 * C + C + cc] = (red[0][1][t] + red[1][1][t]) + (red[2][1][t] + red[3][1][t]);
+  }
+}
+
+template <typename TI>
+__global__ __launch_bounds__(256) void bn_bwd_apply_vec_kernel(int rows, int C, const TI* __restrict__ dz,
+                                                               const float* __restrict__ y,
+                                                               const float* __restrict__ mean,
+                                                               const float* __restrict__ rstd,
+                                                               const float* __restrict__ g,
+                                                               const float* __restrict__ b, int act,
+                                                               const float* __restrict__ dgamma,
+                                                               const float* __restrict__ dbeta,
+                                                               float* __restrict__ dy) {
+  const float invn = 1.f / rows;
+  const int c4 = C / 4;
+  const long total4 = (long)rows * c4;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total4; i += (long)gridDim.x * blockDim.x) {
+    const int c = (int)(i % c4) * 4;
+    float yv[4], dv[4], mu[4], rs[4], gg[4], bb[4], dg[4], db[4], o[4];
+    vld4(y + i * 4, yv); vld4(dz + i * 4, dv);
+    vld4(mean + c, mu); vld4(rstd + c, rs); vld4(g + c, gg); vld4(b + c, bb);
+    vld4(dgamma + c, dg); vld4(dbeta + c, db);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const float xh = (yv[k] - mu[k]) * rs[k];
+      const float dh = dv[k] * act_bwd(act, xh * gg[k] + bb[k]);
+      o[k] = gg[k] * rs[k] * (dh - db[k] * invn - xh * dg[k] * invn);
+    }
+    vst4(dy + i * 4, o);
+  }
+}
+
 int ln_blocks(int rows) { return ea_grid_cap(ea_cdiv(rows, 4), 2048); }
 
 }  // namespace
@@ -424,6 +647,16 @@ extern "C" int ea_reduce_partials(int nparts, int n, const float* part, long str
   return 0;
 }
 
+// internal (not exported): transposed-output variant used by the depthwise-conv backward
+int ea_reduce_partials_tr(int nparts, int n, const float* part, long stride, float* out, int accumulate,
+                          int tr_rows, int tr_cols, void* stream) {
+  if (n == 0) return 0;
+  hipLaunchKernelGGL(reduce_partials_kernel, dim3(ea_cdiv(n, 64)), dim3(256), 0, (hipStream_t)stream,
+                     nparts, n, part, stride, out, accumulate, tr_rows, tr_cols);
+  EA_LAUNCH_CHECK();
+  return 0;
+}
+
 extern "C" int ea_colsum(int rows, int n, const void* x, int x_dtype, long ld, float* out, int accumulate,
                          float* workspace, long ws_elems, void* stream) {
   EA_ENTRY();
@@ -475,13 +708,17 @@ extern "C" int ea_batchnorm_fwd(int rows, int C, const float* y, const float* ga
   EA_ENTRY();
   hipStream_t st = (hipStream_t)stream;
   const long total = (long)rows * C;
+  const bool vec = C % 4 == 0 && ((uintptr_t)y % 16) == 0 && ((uintptr_t)z % (z_dtype == EA_BF16 ? 8 : 16)) == 0;
   if (training) {
     const int rpb = max(32, ea_cdiv(rows, 64));
     const int nparts = ea_cdiv(rows, rpb);
     EA_CHECK_ARG((long)nparts * 2 * C <= ws_elems && rows > 0);
-    hipLaunchKernelGGL(bn_partial_kernel, dim3(ea_cdiv(C, 256), nparts), dim3(256), 0, st, rows, C, y, rpb, workspace);
+    if (vec)
+      hipLaunchKernelGGL(bn_partial_vec_kernel, dim3(ea_cdiv(C, 256), nparts), dim3(256), 0, st, rows, C, y, rpb, workspace);
+    else
+      hipLaunchKernelGGL(bn_partial_kernel, dim3(ea_cdiv(C, 256), nparts), dim3(256), 0, st, rows, C, y, rpb, workspace);
     EA_LAUNCH_CHECK();
-    hipLaunchKernelGGL(bn_finalize_kernel, dim3(ea_cdiv(C, 256)), dim3(256), 0, st, rows, C, nparts, y, workspace,
+    hipLaunchKernelGGL(bn_finalize_par_kernel, dim3(ea_cdiv(C, 64)), dim3(256), 0, st, rows, C, nparts, y, workspace,
                        eps, momentum, mean, rstd, running_mean, running_var, num_batches_tracked);
     EA_LAUNCH_CHECK();
   } else {
@@ -491,7 +728,13 @@ extern "C" int ea_batchnorm_fwd(int rows, int C, const float* y, const float* ga
     EA_LAUNCH_CHECK();
   }
   dim3 grid(ea_grid_cap(ea_cdiv(total, 256)));
-  if (z_dtype == EA_BF16)
+  if (vec) {
+    dim3 g4(ea_grid_cap(ea_cdiv(total / 4, 256)));
+    if (z_dtype == EA_BF16)
+      hipLaunchKernelGGL(bn_apply_act_vec_kernel<bf16>, g4, dim3(256), 0, st, rows, C, y, mean, rstd, gamma, beta, act, (bf16*)z);
+    else
+      hipLaunchKernelGGL(bn_apply_act_vec_kernel<float>, g4, dim3(256), 0, st, rows, C, y, mean, rstd, gamma, beta, act, (float*)z);
+  } else if (z_dtype == EA_BF16)
     hipLaunchKernelGGL(bn_apply_act_kernel<bf16>, grid, dim3(256), 0, st, total, C, y, mean, rstd, gamma, beta, act, (bf16*)z);
   else
     hipLaunchKernelGGL(bn_apply_act_kernel<float>, grid, dim3(256), 0, st, total, C, y, mean, rstd, gamma, beta, act, (float*)z);
@@ -512,7 +755,13 @@ extern "C" int ea_batchnorm_bwd(int rows, int C, const void* dz, int dz_dtype, c
   EA_CHECK_ARG(dbeta == dgamma + C);
   float* sums = workspace + (long)nparts * 2 * C;  // [sum dh*xhat | sum dh] for this batch
   dim3 g1(ea_cdiv(C, 256), nparts);
-  if (dz_dtype == EA_BF16)
+  const bool vec = C % 4 == 0 && ((uintptr_t)y % 16) == 0 && ((uintptr_t)dy % 16) == 0 &&
+                   ((uintptr_t)dz % (dz_dtype == EA_BF16 ? 8 : 16)) == 0;
+  if (vec && dz_dtype == EA_BF16)
+    hipLaunchKernelGGL(bn_bwd_partial_vec_kernel<bf16>, g1, dim3(256), 0, st, rows, C, (const bf16*)dz, y, mean, rstd, gamma, beta, act, rpb, workspace);
+  else if (vec)
+    hipLaunchKernelGGL(bn_bwd_partial_vec_kernel<float>, g1, dim3(256), 0, st, rows, C, (const float*)dz, y, mean, rstd, gamma, beta, act, rpb, workspace);
+  else if (dz_dtype == EA_BF16)
     hipLaunchKernelGGL(bn_bwd_partial_kernel<bf16>, g1, dim3(256), 0, st, rows, C, (const bf16*)dz, y, mean, rstd, gamma, beta, act, rpb, workspace);
   else
     hipLaunchKernelGGL(bn_bwd_partial_kernel<float>, g1, dim3(256), 0, st, rows, C, (const float*)dz, y, mean, rstd, gamma, beta, act, rpb, workspace);
@@ -521,7 +770,13 @@ extern "C" int ea_batchnorm_bwd(int rows, int C, const void* dz, int dz_dtype, c
                      (long)2 * C, sums, 0);
   EA_LAUNCH_CHECK();
   dim3 g2(ea_grid_cap(ea_cdiv(total, 256)));
-  if (dz_dtype == EA_BF16)
+  if (vec) {
+    dim3 g4(ea_grid_cap(ea_cdiv(total / 4, 256)));
+    if (dz_dtype == EA_BF16)
+      hipLaunchKernelGGL(bn_bwd_apply_vec_kernel<bf16>, g4, dim3(256), 0, st, rows, C, (const bf16*)dz, y, mean, rstd, gamma, beta, act, sums, sums + C, dy);
+    else
+      hipLaunchKernelGGL(bn_bwd_apply_vec_kernel<float>, g4, dim3(256), 0, st, rows, C, (const float*)dz, y, mean, rstd, gamma, beta, act, sums, sums + C, dy);
+  } else if (dz_dtype == EA_BF16)
     hipLaunchKernelGGL(bn_bwd_apply_kernel<bf16>, g2, dim3(256), 0, st, total, C, rows, (const bf16*)dz, y, mean, rstd, gamma, beta, act, sums, sums + C, dy);
   else
     hipLaunchKernelGGL(bn_bwd_apply_kernel<float>, g2, dim3(256), 0, st, total, C, rows, (const float*)dz, y, mean, rstd, gamma, beta, act, sums, sums + C, dy);

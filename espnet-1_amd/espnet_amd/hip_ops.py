@@ -6,6 +6,7 @@ the current HIP stream; every computation is one of the library's kernels.
 from __future__ import annotations
 
 import ctypes
+import os
 
 import torch
 
@@ -44,7 +45,8 @@ class KernelProbe:
 
 
 PROBE = None
-OVERLAP_WGRAD = True  # run weight-gradient GEMMs / bias reductions on a side stream
+# run weight-gradient GEMMs / bias reductions on a side stream (EA_OVERLAP_WGRAD=0: serial, for profiling)
+OVERLAP_WGRAD = os.environ.get("EA_OVERLAP_WGRAD", "1") != "0"
 _SIDE = {}
 
 

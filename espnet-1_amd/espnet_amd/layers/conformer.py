@@ -269,7 +269,7 @@ class ConformerBlockFn(torch.autograd.Function):
         ops.batchnorm_bwd(dz, y, bn_mean, bn_rstd, b.f(C + "norm.weight"), b.f(C + "norm.bias"),
                           ACT_SWISH, dy, b.g(C + "norm.weight"), b.g(C + "norm.bias"))
         dglu = empty(N, d, device=dev)
-        w, wn = ops._ws(dev, B * ((T + 31) // 32) * d * K + 1024)
+        w, wn = ops._ws(dev, B * ((T + 31) // 32) * d * (K + 1) + 1024)
         lib.ea_dwconv_bwd(B, T, d, K, glu.data_ptr(), b.f(C + "depthwise_conv.weight").data_ptr(),
                           dy.data_ptr(), dglu.data_ptr(), b.g(C + "depthwise_conv.weight").data_ptr(),
                           b.g(C + "depthwise_conv.bias").data_ptr(), 1, w, wn, ops.stream())
