@@ -37,7 +37,8 @@ struct GemmP {
   int tiles_m, tiles_n;
   int vec_a, vec_b;  // 16-B vector loads allowed (aligned base, ld and batch strides)
   int vec_c;         // 4-column vector epilogue allowed (aligned C/aux/resid/bias, N % 4 == 0)
-  int bm;            // output tile rows (128, or 64 for small grids with K-major A)
+  int lds;           // bf16 LDS-DMA kernel eligible (aligned operands < 4 GB)
+  int bm, bn;        // output tile (LDS-DMA bf16 kernel: 64/128/256 x 128/256; else 128 x 128)
 };
 
 EA_DEV int swz_k(int row) { return (row >> 1) & 7; }                         // K-major rows
@@ -430,18 +431,33 @@ EA_DEV void lds_barrier() {
   asm volatile("" ::: "memory");
 }
 
-// Tile-row-generic tail loader/storer (K-major ROWS x 64 or MN-major 64 x 128 images).
-template <bool KMAJ, int ROWS>
-EA_DEV void load_tile_r(const bf16* __restrict__ base, long ld, int mn0, int MN, int k0, int K, uint4 (&v)[4]) {
-  constexpr int CPR = KMAJ ? 8 : 16;
-  constexpr int NCH = KMAJ ? ROWS * 8 / NT : 4;
+// Operand images are built from 128-wide panels of one 64-deep K-tile (16 KB bf16):
+//  * K-major operand, R rows: [R][64] (128-B rows, chunk swizzle swz_k)  = R*128 bytes
+//  * MN-major operand, R = 128*P cols: [P][64 k][128] panels (swz_mn_bf16)
+// A 16-B chunk index c (0 .. R*8-1) maps to (row, chunk) / (panel, k, chunk) the same way
+// for the LDS-DMA sources and for the register tail path.
+template <bool KMAJ>
+EA_DEV int img_off(int c) {  // byte offset of chunk c's LDS slot (the swizzled position)
+  if (KMAJ) {
+    const int row = c >> 3, ch = c & 7;
+    return row * 128 + ((ch ^ swz_k(row)) << 4);
+  } else {
+    const int pnl = c >> 10, cj = c & 1023, k = cj >> 4, ch = cj & 15;
+    return pnl * 16384 + k * 256 + ((ch ^ swz_mn_bf16(k)) << 4);
+  }
+}
+
+// register tail loader/storer for a K remainder (< 64), zero-filled
+template <bool KMAJ, int ROWS, int NTT>
+EA_DEV void load_tile_r(const bf16* __restrict__ base, long ld, int mn0, int MN, int k0, int K,
+                        uint4 (&v)[ROWS * 8 / NTT]) {
+  constexpr int NCH = ROWS * 8 / NTT;
 #pragma unroll
   for (int i = 0; i < NCH; ++i) {
-    const int c = threadIdx.x + NT * i;
-    const int row = c / CPR, ch = c % CPR;
+    const int c = threadIdx.x + NTT * i;
     int mn, k;
-    if (KMAJ) { mn = mn0 + row; k = k0 + ch * 8; }
-    else      { k = k0 + row; mn = mn0 + ch * 8; }
+    if (KMAJ) { mn = mn0 + (c >> 3); k = k0 + (c & 7) * 8; }
+    else      { const int cj = c & 1023; k = k0 + (cj >> 4); mn = mn0 + (c >> 10) * 128 + (cj & 15) * 8; }
     const bf16* pp = KMAJ ? base + (long)mn * ld + k : base + (long)k * ld + mn;
     union { uint4 u; bf16 e[8]; } t;
 #pragma unroll
@@ -452,32 +468,96 @@ EA_DEV void load_tile_r(const bf16* __restrict__ base, long ld, int mn0, int MN,
     v[i] = t.u;
   }
 }
-template <bool KMAJ, int ROWS>
-EA_DEV void store_tile_r(char* lds, const uint4 (&v)[4]) {
-  constexpr int CPR = KMAJ ? 8 : 16;
-  constexpr int NCH = KMAJ ? ROWS * 8 / NT : 4;
+template <bool KMAJ, int ROWS, int NTT>
+EA_DEV void store_tile_r(char* lds, const uint4 (&v)[ROWS * 8 / NTT]) {
 #pragma unroll
-  for (int i = 0; i < NCH; ++i) {
-    const int c = threadIdx.x + NT * i;
-    const int row = c / CPR, ch = c % CPR;
-    const int off = KMAJ ? row * 128 + ((ch ^ swz_k(row)) << 4) : row * 256 + ((ch ^ swz_mn_bf16(row)) << 4);
-    *(uint4*)(lds + off) = v[i];
+  for (int i = 0; i < ROWS * 8 / NTT; ++i) {
+    const int c = threadIdx.x + NTT * i;
+    *(uint4*)(lds + img_off<KMAJ>(c)) = v[i];
   }
 }
 
-// BM x 128 output tile (BM = 128, or 64 for K-major A on small grids: more blocks per CU).
-// 4 wave64s in 2 x 2, each (BM/2) x 64 = (BM/32) x 4 MFMA 16x16 blocks.  Fragments of k-step
-// ks+1 are read from LDS while the MFMAs of k-step ks run (register double buffer).
-template <int BM_, bool AK, bool BKM, int STAGES>
-__global__ __launch_bounds__(NT, 1) void gemm_bf16_lds(GemmP p) {
-  static_assert(AK || BM_ == 128, "MN-major A needs the 128-wide image");
+// fragment of 16 rows/cols starting at r (multiple of 16) from an operand image
+template <bool KMAJ>
+EA_DEV bf16x8 frag_img(const char* img, int r, int ks, int lane) {
+  if (KMAJ) return frag_bf16<true>(img, r, ks, lane);
+  return frag_bf16<false>(img + (r >> 7) * 16384, r & 127, ks, lane);
+}
+
+// Epilogue of one wave's (MI*16) x (NJ*16) accumulator tile, in 64 x 64 chunks transposed
+// through the wave's private LDS region (64 x EPI_LDT floats).
+template <int KIND, int MI, int NJ>
+EA_DEV void epi_wave(const GemmP& p, char* smem, int z, int zb, int zh, int r0, int c0, int lane, int w,
+                     const f32x4 (&acc)[MI][NJ]) {
+  constexpr int RC = MI < 4 ? MI : 4;  // row blocks per chunk
+  float* t = (float*)smem + w * (RC * 16) * EPI_LDT;
+  const int rq = (lane >> 4) * 4, cc = lane & 15, lc = (lane & 15) * 4;
+#pragma unroll
+  for (int ri = 0; ri < MI / RC; ++ri) {
+#pragma unroll
+    for (int cj = 0; cj < NJ / 4; ++cj) {
+      if (ri + cj > 0) {
+        __builtin_amdgcn_wave_barrier();
+        asm volatile("" ::: "memory");
+      }
+#pragma unroll
+      for (int i = 0; i < RC; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+          for (int rr = 0; rr < 4; ++rr)
+            t[(i * 16 + rq + rr) * EPI_LDT + j * 16 + cc] = acc[ri * RC + i][cj * 4 + j][rr];
+      __builtin_amdgcn_wave_barrier();
+      asm volatile("" ::: "memory");
+      const int rb = r0 + ri * RC * 16, cb = c0 + cj * 64;
+#pragma unroll 4
+      for (int it = 0; it < RC * 4; ++it) {
+        const int lr = it * 4 + (lane >> 4);
+        const int row = rb + lr, col = cb + lc;
+        if (row >= p.M || col >= p.N) continue;
+        const float4 f = *(const float4*)(t + lr * EPI_LDT + lc);
+        const float v[4] = {f.x, f.y, f.z, f.w};
+        if (p.vec_c && col + 3 < p.N) {
+          if (p.splitk > 1) {
+            float* slab = p.ws + ((long)z * p.splitk + (blockIdx.z % p.splitk)) * (long)p.M * p.N;
+            *(float4*)(slab + (long)row * p.N + col) = f;
+          } else {
+            epi_four<KIND>(p, z, zb, zh, row, col, v);
+          }
+        } else {
+#pragma unroll
+          for (int c = 0; c < 4; ++c) {
+            if (col + c >= p.N) break;
+            if (p.splitk > 1) {
+              float* slab = p.ws + ((long)z * p.splitk + (blockIdx.z % p.splitk)) * (long)p.M * p.N;
+              slab[(long)row * p.N + col + c] = v[c];
+            } else {
+              epi_one<KIND>(p, z, zb, zh, row, col + c, v[c]);
+            }
+          }
+        }
+      }
+    }
+  }
+}
+
+// BM x BN output tile, 2 x WN wave64s, each (BM/2) x (BN/WN) = MI x NJ MFMA 16x16 blocks.
+// (BM, BN, WN) in {(64,128,2) K-major A only, (128,128,2), (256,128,2), (256,256,4)}.
+// Small wave tiles read the fragments of both k-steps up front (register double buffer);
+// 128-row wave tiles read one k-step at a time.
+template <int BM_, int BN_, int WN, bool AK, bool BKM, int STAGES>
+__global__ __launch_bounds__(128 * WN, 1) void gemm_bf16_lds(GemmP p) {
+  constexpr int NW = 2 * WN, NTT = 64 * NW;
+  static_assert(AK || BM_ >= 128, "MN-major A needs 128-wide panels");
+  static_assert(BKM || BN_ >= 128, "MN-major B needs 128-wide panels");
   constexpr int BK = 64;
-  constexpr int A_BYTES = BM_ * BK * 2;
-  constexpr int STAGE_BYTES = A_BYTES + TILE_BYTES;
-  constexpr int MI = BM_ / 32;          // MFMA row blocks per wave
-  constexpr int ACH = AK ? BM_ * 8 / NT : 4;  // A DMA chunks per thread per K-tile
-  constexpr int EPI_BYTES = 4 * (BM_ / 2) * EPI_LDT * 4;
+  constexpr int A_BYTES = BM_ * BK * 2, B_BYTES = BN_ * BK * 2;
+  constexpr int STAGE_BYTES = A_BYTES + B_BYTES;
+  constexpr int MI = BM_ / 32, NJ = BN_ / (16 * WN);
+  constexpr int ACH = A_BYTES / (NTT * 16), BCH = B_BYTES / (NTT * 16);  // DMA chunks/thread/K-tile
+  constexpr int EPI_BYTES = NW * (MI < 4 ? MI : 4) * 16 * EPI_LDT * 4;
   constexpr int SMEM = STAGES * STAGE_BYTES > EPI_BYTES ? STAGES * STAGE_BYTES : EPI_BYTES;
+  constexpr bool DB = MI * NJ <= 16;
   __shared__ __attribute__((aligned(1024))) char smem[SMEM];
 
   const int nt = p.tiles_m * p.tiles_n;
@@ -490,7 +570,7 @@ __global__ __launch_bounds__(NT, 1) void gemm_bf16_lds(GemmP p) {
   const int gsz = min(GM, p.tiles_m - gm0);
   const int tm = gm0 + (t % (GM * p.tiles_n)) % gsz;
   const int tn = (t % (GM * p.tiles_n)) / gsz;
-  const int m0 = tm * BM_, n0 = tn * BN;
+  const int m0 = tm * BM_, n0 = tn * BN_;
 
   const int z = blockIdx.z / p.splitk, sk = blockIdx.z % p.splitk;
   const int zb = z / p.nh, zh = z % p.nh;
@@ -502,77 +582,90 @@ __global__ __launch_bounds__(NT, 1) void gemm_bf16_lds(GemmP p) {
   const bool tail = kbeg + nfull * BK < kend;
 
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int wm = (w >> 1) * (BM_ / 2), wn = (w & 1) * 64;
+  const int wm = (w / WN) * (BM_ / 2), wn = (w % WN) * (BN_ / WN);
 
-  const bf16* asrc[ACH];
-  const bf16* bsrc[4];
-#pragma unroll
-  for (int i = 0; i < ACH; ++i) {
-    const int ci = (i * 4 + w) * 64 + lane;
-    if (AK) {
+  // per-lane DMA sources: chunk ci = (i*NW + w)*64 + lane lands lane-linearly at ci*16;
+  // the source is the global chunk whose swizzled slot that is.  Sources are 32-bit byte
+  // offsets from a wave-uniform base (scalar base + vector offset addressing; the host
+  // keeps operands < 4 GB on this path).
+  auto src = [&](long ld, int mn0, int MN, bool kmaj, int ci) -> uint32_t {
+    if (kmaj) {
       const int row = ci >> 3, c = (ci & 7) ^ swz_k(ci >> 3);
-      asrc[i] = A + (long)min(m0 + row, p.M - 1) * p.lda + kbeg + c * 8;
-    } else {
-      const int k = ci >> 4, c = (ci & 15) ^ swz_mn_bf16(ci >> 4);
-      asrc[i] = A + (long)(kbeg + k) * p.lda + min((long)(m0 + c * 8), p.lda - 8);
+      return (uint32_t)(((long)min(mn0 + row, MN - 1) * ld + c * 8) * 2);
     }
-  }
+    const int pnl = ci >> 10, cj = ci & 1023, k = cj >> 4, c = (cj & 15) ^ swz_mn_bf16(k);
+    return (uint32_t)(((long)k * ld + min((long)(mn0 + pnl * 128 + c * 8), ld - 8)) * 2);
+  };
+  const char* abase = (const char*)(A + (AK ? (long)kbeg : (long)kbeg * p.lda));
+  const char* bbase = (const char*)(B + (BKM ? (long)kbeg : (long)kbeg * p.ldb));
+  uint32_t aoff[ACH], boff[BCH];
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int ci = (i * 4 + w) * 64 + lane;
-    if (BKM) {
-      const int row = ci >> 3, c = (ci & 7) ^ swz_k(ci >> 3);
-      bsrc[i] = B + (long)min(n0 + row, p.N - 1) * p.ldb + kbeg + c * 8;
-    } else {
-      const int k = ci >> 4, c = (ci & 15) ^ swz_mn_bf16(ci >> 4);
-      bsrc[i] = B + (long)(kbeg + k) * p.ldb + min((long)(n0 + c * 8), p.ldb - 8);
-    }
-  }
-  const long astep = AK ? BK : (long)BK * p.lda;
-  const long bstep = BKM ? BK : (long)BK * p.ldb;
-  constexpr int GPT = ACH + 4;  // DMA instructions per thread per K-tile (vmcnt unit)
+  for (int i = 0; i < ACH; ++i) aoff[i] = src(p.lda, m0, p.M, AK, (i * NW + w) * 64 + lane);
+#pragma unroll
+  for (int i = 0; i < BCH; ++i) boff[i] = src(p.ldb, n0, p.N, BKM, (i * NW + w) * 64 + lane);
+  const long astep = (AK ? BK : (long)BK * p.lda) * 2;  // bytes per K-tile
+  const long bstep = (BKM ? BK : (long)BK * p.ldb) * 2;
+  constexpr int GPT = ACH + BCH;  // DMA instructions per thread per K-tile (vmcnt unit)
 
   auto issue = [&](int kt, int stg) {
     char* base = smem + stg * STAGE_BYTES;
+    const char* ak = abase + kt * astep;
+    const char* bk = bbase + kt * bstep;
 #pragma unroll
     for (int i = 0; i < ACH; ++i)
-      __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)(asrc[i] + kt * astep),
-                                       (__attribute__((address_space(3))) void*)(base + (i * 4 + w) * 1024), 16, 0, 0);
+      __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)(ak + aoff[i]),
+                                       (__attribute__((address_space(3))) void*)(base + (i * NW + w) * 1024), 16, 0, 0);
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
-      __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)(bsrc[i] + kt * bstep),
-                                       (__attribute__((address_space(3))) void*)(base + A_BYTES + (i * 4 + w) * 1024),
+    for (int i = 0; i < BCH; ++i)
+      __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)(bk + boff[i]),
+                                       (__attribute__((address_space(3))) void*)(base + A_BYTES + (i * NW + w) * 1024),
                                        16, 0, 0);
   };
 
-  f32x4 acc[MI][4];
+  f32x4 acc[MI][NJ];
 #pragma unroll
   for (int i = 0; i < MI; ++i)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < NJ; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
 
   auto compute = [&](int stg) {
     const char* la = smem + stg * STAGE_BYTES;
     const char* lb = la + A_BYTES;
-    bf16x8 fa0[MI], fb0[4], fa1[MI], fb1[4];
+    if constexpr (DB) {
+      bf16x8 fa0[MI], fb0[NJ], fa1[MI], fb1[NJ];
 #pragma unroll
-    for (int i = 0; i < MI; ++i) fa0[i] = frag_bf16<AK>(la, wm + i * 16, 0, lane);
+      for (int i = 0; i < MI; ++i) fa0[i] = frag_img<AK>(la, wm + i * 16, 0, lane);
 #pragma unroll
-    for (int j = 0; j < 4; ++j) fb0[j] = frag_bf16<BKM>(lb, wn + j * 16, 0, lane);
+      for (int j = 0; j < NJ; ++j) fb0[j] = frag_img<BKM>(lb, wn + j * 16, 0, lane);
 #pragma unroll
-    for (int i = 0; i < MI; ++i) fa1[i] = frag_bf16<AK>(la, wm + i * 16, 1, lane);
+      for (int i = 0; i < MI; ++i) fa1[i] = frag_img<AK>(la, wm + i * 16, 1, lane);
 #pragma unroll
-    for (int j = 0; j < 4; ++j) fb1[j] = frag_bf16<BKM>(lb, wn + j * 16, 1, lane);
+      for (int j = 0; j < NJ; ++j) fb1[j] = frag_img<BKM>(lb, wn + j * 16, 1, lane);
 #pragma unroll
-    for (int i = 0; i < MI; ++i)
+      for (int i = 0; i < MI; ++i)
 #pragma unroll
-      for (int j = 0; j < 4; ++j)
-        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa0[i], fb0[j], acc[i][j], 0, 0, 0);
+        for (int j = 0; j < NJ; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa0[i], fb0[j], acc[i][j], 0, 0, 0);
 #pragma unroll
-    for (int i = 0; i < MI; ++i)
+      for (int i = 0; i < MI; ++i)
 #pragma unroll
-      for (int j = 0; j < 4; ++j)
-        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa1[i], fb1[j], acc[i][j], 0, 0, 0);
+        for (int j = 0; j < NJ; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa1[i], fb1[j], acc[i][j], 0, 0, 0);
+    } else {
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        bf16x8 fb[NJ];
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) fb[j] = frag_img<BKM>(lb, wn + j * 16, ks, lane);
+#pragma unroll
+        for (int i = 0; i < MI; ++i) {
+          const bf16x8 fa = frag_img<AK>(la, wm + i * 16, ks, lane);
+#pragma unroll
+          for (int j = 0; j < NJ; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa, fb[j], acc[i][j], 0, 0, 0);
+        }
+      }
+    }
   };
 
   const int npre = min(STAGES - 1, nfull);
@@ -587,24 +680,24 @@ __global__ __launch_bounds__(NT, 1) void gemm_bf16_lds(GemmP p) {
     compute(kt % STAGES);
   }
   if (tail) {
-    uint4 ra[4], rb[4];
+    uint4 ra[BM_ * 8 / NTT], rb[BN_ * 8 / NTT];
     const int k0 = kbeg + nfull * BK;
-    load_tile_r<AK, BM_>(A, p.lda, m0, p.M, k0, kend, ra);
-    load_tile_r<BKM, 128>(B, p.ldb, n0, p.N, k0, kend, rb);
+    load_tile_r<AK, BM_, NTT>(A, p.lda, m0, p.M, k0, kend, ra);
+    load_tile_r<BKM, BN_, NTT>(B, p.ldb, n0, p.N, k0, kend, rb);
     __syncthreads();
     char* base = smem + (nfull % STAGES) * STAGE_BYTES;
-    store_tile_r<AK, BM_>(base, ra);
-    store_tile_r<BKM, 128>(base + A_BYTES, rb);
+    store_tile_r<AK, BM_, NTT>(base, ra);
+    store_tile_r<BKM, BN_, NTT>(base + A_BYTES, rb);
     __syncthreads();
     compute(nfull % STAGES);
   }
 
   __syncthreads();  // every wave is done reading the operand ring: reuse it for the epilogue
   switch (p.splitk > 1 ? EA_EPI_STORE : p.epi.kind) {
-    case EA_EPI_STORE: epi_tile_lds<EA_EPI_STORE, MI>(p, smem, z, zb, zh, m0 + wm, n0 + wn, lane, w, acc); break;
-    case EA_EPI_ACT: epi_tile_lds<EA_EPI_ACT, MI>(p, smem, z, zb, zh, m0 + wm, n0 + wn, lane, w, acc); break;
-    case EA_EPI_RESID: epi_tile_lds<EA_EPI_RESID, MI>(p, smem, z, zb, zh, m0 + wm, n0 + wn, lane, w, acc); break;
-    default: epi_tile_lds<EA_EPI_DACT, MI>(p, smem, z, zb, zh, m0 + wm, n0 + wn, lane, w, acc); break;
+    case EA_EPI_STORE: epi_wave<EA_EPI_STORE, MI, NJ>(p, smem, z, zb, zh, m0 + wm, n0 + wn, lane, w, acc); break;
+    case EA_EPI_ACT: epi_wave<EA_EPI_ACT, MI, NJ>(p, smem, z, zb, zh, m0 + wm, n0 + wn, lane, w, acc); break;
+    case EA_EPI_RESID: epi_wave<EA_EPI_RESID, MI, NJ>(p, smem, z, zb, zh, m0 + wm, n0 + wn, lane, w, acc); break;
+    default: epi_wave<EA_EPI_DACT, MI, NJ>(p, smem, z, zb, zh, m0 + wm, n0 + wn, lane, w, acc); break;
   }
 }
 
@@ -644,30 +737,61 @@ int g_gemm_bm64 = 1;  // LDS ring depth of gemm_bf16_lds (2: 64 KiB, 2 blocks/CU
 
 int launch_lds(GemmP& p, int a_k, int b_k, int nz, hipStream_t st) {
   dim3 grid(p.tiles_m * p.tiles_n, 1, nz * p.splitk);
+#define EA_GL(BMV, BNV, AKV, BKV, S) \
+  hipLaunchKernelGGL((gemm_bf16_lds<BMV, BNV, (BNV == 256 ? 4 : 2), AKV, BKV, S>), grid, dim3(BNV == 256 ? 512 : 256), 0, st, p)
+#define EA_GL4(BMV, BNV, S)                            \
+  if (a_k && b_k) EA_GL(BMV, BNV, true, true, S);      \
+  else if (a_k) EA_GL(BMV, BNV, true, false, S);       \
+  else if (b_k) EA_GL(BMV, BNV, false, true, S);       \
+  else EA_GL(BMV, BNV, false, false, S);
   if (p.bm == 64) {
-    if (b_k) hipLaunchKernelGGL((gemm_bf16_lds<64, true, true, 2>), grid, dim3(NT), 0, st, p);
-    else hipLaunchKernelGGL((gemm_bf16_lds<64, true, false, 2>), grid, dim3(NT), 0, st, p);
-    EA_LAUNCH_CHECK();
-    return 0;
+    if (b_k) EA_GL(64, 128, true, true, 2);
+    else EA_GL(64, 128, true, false, 2);
+  } else if (p.bm == 256 && p.bn == 256) {
+    EA_GL4(256, 256, 2)
+  } else if (p.bm == 256) {
+    EA_GL4(256, 128, 2)
+  } else if (g_gemm_stages >= 3) {
+    EA_GL4(128, 128, 3)
+  } else {
+    EA_GL4(128, 128, 2)
   }
-#define EA_GL_CASE(AKV, BKV)                                                                             \
-  if (a_k == AKV && b_k == BKV) {                                                                        \
-    if (g_gemm_stages >= 3) hipLaunchKernelGGL((gemm_bf16_lds<128, AKV, BKV, 3>), grid, dim3(NT), 0, st, p); \
-    else hipLaunchKernelGGL((gemm_bf16_lds<128, AKV, BKV, 2>), grid, dim3(NT), 0, st, p);               \
-  }
-  EA_GL_CASE(true, true)
-  else EA_GL_CASE(true, false)
-  else EA_GL_CASE(false, true)
-  else EA_GL_CASE(false, false)
-#undef EA_GL_CASE
+#undef EA_GL4
+#undef EA_GL
   EA_LAUNCH_CHECK();
   return 0;
 }
 
+// Output tile choice by a two-term time model fitted to measured launches on MI355X
+// (scripts/gemm_tiles.py): rounds of co-resident blocks each pay a fixed prologue/epilogue
+// cost t0 (us), and each CU's share of the flops runs at the tile's steady-state rate
+// (TFLOP/s per CU; larger tiles need fewer L2 bytes per flop).  g_force_bm/bn pin a shape.
+int g_force_bm = 0, g_force_bn = 0;
+void choose_tile(GemmP& p, int a_k, long nz) {
+  struct Cfg { int bm, bn, occ; double t0, rcu; bool ak_only; };
+  static const Cfg cfgs[] = {{256, 256, 1, 12.4, 4.49, false}, {128, 128, 2, 8.3, 2.9, false},
+                             {64, 128, 3, 6.8, 2.8, true}};
+  p.bm = 128; p.bn = 128;
+  if (g_force_bm) {
+    if (g_force_bm == 64 && !a_k) return;  // 64-row tiles need K-major A: keep 128 x 128
+    p.bm = g_force_bm; p.bn = g_force_bn;
+    return;
+  }
+  double best = 1e300;
+  for (const Cfg& c : cfgs) {
+    if (c.ak_only && (!a_k || !g_gemm_bm64)) continue;
+    const long tiles = (long)ea_cdiv(p.M, c.bm) * ea_cdiv(p.N, c.bn) * nz;
+    const double rounds = (double)((tiles + 256L * c.occ - 1) / (256L * c.occ));
+    const double per_cu = (double)((tiles + 255) / 256) * 2.0 * c.bm * c.bn * (double)p.K * 1e-6;
+    const double est = rounds * c.t0 + per_cu / c.rcu;
+    if (est < best * 0.999) { best = est; p.bm = c.bm; p.bn = c.bn; }
+  }
+}
+
 template <typename T>
 int launch(GemmP& p, int a_k, int b_k, int nz, hipStream_t st) {
-  if (sizeof(T) == 2 && p.vec_a && p.vec_b && g_gemm_stages > 0) return launch_lds(p, a_k, b_k, nz, st);
-  if (p.bm != 128) return EA_ERR_BAD_ARG;
+  if (sizeof(T) == 2 && p.lds) return launch_lds(p, a_k, b_k, nz, st);
+  if (p.bm != 128 || p.bn != 128) return EA_ERR_BAD_ARG;
   dim3 grid(p.tiles_m * p.tiles_n, 1, nz * p.splitk);
 #define EA_GEMM_CASE(AKV, BKV)                                                      \
   if (a_k == AKV && b_k == BKV) {                                                   \
@@ -689,6 +813,15 @@ extern "C" int ea_gemm_set_pipeline(int stages) {
   EA_CHECK_ARG(stages == 0 || stages == 2 || stages == 3 || stages == 12 || stages == 13);
   g_gemm_bm64 = stages < 10;   // 12/13: same ring, 128-row tiles only (A/B measurements)
   g_gemm_stages = stages % 10;
+  return 0;
+}
+
+extern "C" int ea_gemm_set_tile(int bm, int bn) {
+  EA_ENTRY();
+  EA_CHECK_ARG((bm == 0 && bn == 0) || (bm == 64 && bn == 128) || (bm == 128 && bn == 128) ||
+               (bm == 256 && (bn == 128 || bn == 256)));
+  g_force_bm = bm;
+  g_force_bn = bn;
   return 0;
 }
 
@@ -725,17 +858,23 @@ extern "C" int ea_gemm(int dtype, int a_kmajor, int b_kmajor, int M, int N, int 
     if (epi->resid) vc = vc && epi->ldr % 4 == 0 && ((uintptr_t)epi->resid % 16) == 0;
     p.vec_c = vc;
   }
-  p.bm = 128;
-  if (g_gemm_bm64 && dtype == EA_BF16 && a_kmajor && p.vec_a && p.vec_b && g_gemm_stages > 0 &&
-      (long)ea_cdiv(M, 128) * ea_cdiv(N, BN) * batch * nh < 480)
-    p.bm = 64;  // < ~2 tiles per CU at 128 rows: halve the tile to double the blocks
+  p.bm = 128; p.bn = 128;
+  // operand extent per batch slice (bytes) must fit the kernel's 32-bit source offsets
+  const double a_ext = 2.0 * ((a_kmajor ? (double)M : (double)K) * lda);
+  const double b_ext = 2.0 * ((b_kmajor ? (double)N : (double)K) * ldb);
+  const bool lds_path = dtype == EA_BF16 && p.vec_a && p.vec_b && g_gemm_stages > 0 &&
+                        a_ext < 4.0e9 && b_ext < 4.0e9;
+  p.lds = lds_path;
+  if (lds_path) choose_tile(p, a_kmajor, (long)batch * nh);
+  if (p.bm == 64 && !a_kmajor) return EA_ERR_BAD_ARG;
   p.tiles_m = ea_cdiv(M, p.bm);
-  p.tiles_n = ea_cdiv(N, BN);
+  p.tiles_n = ea_cdiv(N, p.bn);
   const int KT = dtype == EA_BF16 ? KCfg<bf16>::KT : KCfg<float>::KT;
   const int nz = batch * nh;
   // split-K when the output grid cannot fill the 256 CUs and K is long (dW GEMMs)
   int splitk = 1;
-  const long tiles = (long)p.tiles_m * p.tiles_n * nz;
+  // 128x128-equivalent tiles: split K only when the grid cannot fill the CUs
+  const long tiles = max(1L, (long)p.tiles_m * p.tiles_n * nz * (p.bm * p.bn) / (128 * 128));
   if (workspace && tiles < 200 && K >= 8 * KT) {
     splitk = (int)((384 + tiles - 1) / tiles);
     splitk = min(splitk, K / (4 * KT));

@@ -165,3 +165,60 @@ def test_gemm_unaligned_leading_dims(dtype, a_k, b_k):
     ops.gemm(A, B, C, M=M, N=N, K=K, a_kmajor=a_k, b_kmajor=b_k, lda=A.stride(0), ldb=B.stride(0), ldc=N)
     tol = 1e-5 if dtype == torch.float32 else 2e-3
     torch.testing.assert_close(C.double().cpu(), ref_mm(A, B, a_k, b_k, M, N, K), atol=tol * K ** 0.5, rtol=tol)
+
+
+TILES = [(64, 128), (128, 128), (256, 128), (256, 256)]
+
+
+@pytest.fixture
+def forced_tile(request):
+    ops, L = _ops()
+    bm, bn = request.param
+    L.lib.ea_gemm_set_tile(bm, bn)
+    yield (bm, bn)
+    L.lib.ea_gemm_set_tile(0, 0)
+
+
+@pytest.mark.parametrize("forced_tile", TILES, indirect=True, ids=lambda t: f"{t[0]}x{t[1]}")
+@pytest.mark.parametrize("a_k,b_k", [(1, 1), (1, 0), (0, 1), (0, 0)])
+@pytest.mark.parametrize("MNK", [(300, 520, 200), (513, 257, 64), (40, 300, 130), (256, 256, 128)])
+def test_gemm_bf16_tiles(forced_tile, a_k, b_k, MNK):
+    """Every LDS-DMA tile shape (edges in M, N and a K remainder) vs fp64."""
+    ops, L = _ops()
+    M, N, K = MNK
+    g = torch.Generator().manual_seed(M + 3 * N + 7 * K + a_k * 11 + b_k * 13)
+    up = lambda n: (n + 7) // 8 * 8 + 8
+    A = mk((M, up(K)) if a_k else (K, up(M)), torch.bfloat16, g)
+    B = mk((N, up(K)) if b_k else (K, up(N)), torch.bfloat16, g)
+    C = torch.full((M, N + 4), 7.0, device="cuda")
+    ops.gemm(A, B, C, M=M, N=N, K=K, a_kmajor=a_k, b_kmajor=b_k, lda=A.stride(0),
+             ldb=B.stride(0), ldc=C.stride(0), splitk=False)
+    ref = ref_mm(A, B, a_k, b_k, M, N, K)
+    torch.testing.assert_close(C[:, :N].double().cpu(), ref, atol=2e-3 * K ** 0.5, rtol=2e-3)
+    assert (C[:, N:] == 7.0).all(), "wrote outside ldc columns"
+
+
+@pytest.mark.parametrize("forced_tile", TILES, indirect=True, ids=lambda t: f"{t[0]}x{t[1]}")
+def test_gemm_bf16_tiles_epilogue_splitk(forced_tile):
+    """Fused ACT epilogue and split-K dW under each tile shape."""
+    ops, L = _ops()
+    g = torch.Generator().manual_seed(21)
+    M, N, K = 260, 384, 192
+    x = mk((M, K), torch.bfloat16, g)
+    w = mk((N, K), torch.bfloat16, g, 0.2)
+    bias = mk((N,), torch.float32, g)
+    ref = (x.double().cpu() @ w.double().cpu().t()) + bias.double().cpu()
+    aux = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
+    Ca = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
+    ops.linear(x, w, Ca, epi=ops.make_epi(L.EPI_ACT, bias=bias, act=L.ACT_SWISH, aux=aux))
+    tol = dict(atol=3e-2, rtol=2e-2)
+    torch.testing.assert_close(aux.double().cpu(), ref, **tol)
+    torch.testing.assert_close(Ca.double().cpu(), ref * torch.sigmoid(ref), **tol)
+    # dW = dY^T X over many rows (split-K path)
+    R = 4000
+    dy = mk((R, 96), torch.bfloat16, g)
+    xx = mk((R, 160), torch.bfloat16, g)
+    dw = torch.zeros(96, 160, device="cuda")
+    ops.linear_dw(dy, xx, dw)
+    refw = dy.double().cpu().t() @ xx.double().cpu()
+    torch.testing.assert_close(dw.double().cpu(), refw, atol=2e-3 * R ** 0.5, rtol=2e-3)
