@@ -18,7 +18,7 @@ struct SmP {
   const float* BD; long ldBD;      // [h][b][i][ldBD] or null
   const long long* klen;           // [B] or null
   int causal;
-  float p; uint64_t seed;
+  float p; uint64_t seed; const unsigned long long* salt;
   float* P; long ldP;              // f32 softmax [z][i][ldP] (may alias S)
   void* Pd; int pd_dtype; long ldPd;  // dropout(P) in compute dtype
 };
@@ -63,13 +63,14 @@ __global__ __launch_bounds__(256) void softmax_fwd_kernel(SmP a) {
     const float inv = lim > 0 ? 1.f / sum : 0.f;
     float* prow = a.P + r * a.ldP;
     const uint64_t base = (uint64_t)r * a.T2;
+    const uint64_t seed = ea_salted(a.seed, a.salt);
 #pragma unroll
     for (int e = 0; e < MAXE; ++e) {
       const int j = e * 64 + lane;
       if (j < a.T2) {
         const float pj = v[e] * inv;
         prow[j] = pj;
-        const float pd = a.p > 0.f ? pj * drop_scale(a.seed, base + j, a.p) : pj;
+        const float pd = a.p > 0.f ? pj * drop_scale(seed, base + j, a.p) : pj;
         store_from_f(a.Pd, r * a.ldPd + j, a.pd_dtype, pd);
       }
     }
@@ -81,7 +82,7 @@ struct SmBP {
   float scale;
   const float* dPd; long ldd;      // d(dropout(P)) [z][i][ldd] f32
   const float* P; long ldP;
-  float p; uint64_t seed;
+  float p; uint64_t seed; const unsigned long long* salt;
   void* dS; int ds_dtype; long ldS;    // scale * dS [z][i][ldS]
   void* dBD; long ldBD; int nbd;       // [h][b][i][ldBD], rows of nbd = 2*T1-1 entries, or null
 };
@@ -99,6 +100,7 @@ __global__ __launch_bounds__(256) void softmax_bwd_kernel(SmBP a) {
     const float* drow = a.dPd + r * a.ldd;
     const float* prow = a.P + r * a.ldP;
     const uint64_t base = (uint64_t)r * a.T2;
+    const uint64_t seed = ea_salted(a.seed, a.salt);
     float pv[MAXE], dv[MAXE];
     float dot = 0.f;
 #pragma unroll
@@ -107,7 +109,7 @@ __global__ __launch_bounds__(256) void softmax_bwd_kernel(SmBP a) {
       if (j < a.T2) {
         pv[e] = prow[j];
         float d = drow[j];
-        if (a.p > 0.f) d *= drop_scale(a.seed, base + j, a.p);
+        if (a.p > 0.f) d *= drop_scale(seed, base + j, a.p);
         dv[e] = d;
         dot += pv[e] * d;
       } else {
@@ -161,7 +163,7 @@ extern "C" int ea_attn_softmax_fwd(int B, int H, int T1, int T2, float scale, co
   EA_ENTRY();
   if ((long)B * H * T1 == 0) return 0;
   if (BD) EA_CHECK_ARG(T1 == T2);
-  SmP a{B, H, T1, T2, scale, S, ldS, BD, ldBD, klen, causal, p, (uint64_t)seed, P, ldP, Pd, pd_dtype, ldPd};
+  SmP a{B, H, T1, T2, scale, S, ldS, BD, ldBD, klen, causal, p, (uint64_t)seed, ea_g_rng_salt, P, ldP, Pd, pd_dtype, ldPd};
   EA_SM_DISPATCH(softmax_fwd_kernel, T2, a);
   EA_LAUNCH_CHECK();
   return 0;
@@ -173,7 +175,7 @@ extern "C" int ea_attn_softmax_bwd(int B, int H, int T1, int T2, float scale, co
   EA_ENTRY();
   if ((long)B * H * T1 == 0) return 0;
   if (dBD) EA_CHECK_ARG(T1 == T2);
-  SmBP a{B, H, T1, T2, scale, dPd, ldd, P, ldP, p, (uint64_t)seed, dS, ds_dtype, ldS, dBD, ldBD, 2 * T1 - 1};
+  SmBP a{B, H, T1, T2, scale, dPd, ldd, P, ldP, p, (uint64_t)seed, ea_g_rng_salt, dS, ds_dtype, ldS, dBD, ldBD, 2 * T1 - 1};
   EA_SM_DISPATCH(softmax_bwd_kernel, T2, a);
   EA_LAUNCH_CHECK();
   return 0;

@@ -76,6 +76,14 @@ __host__ __device__ inline uint32_t ea_seed_key(uint64_t seed) {
 EA_DEV uint32_t ea_pair_hash(uint32_t key, uint64_t pair) {
   return ea_mix32(((uint32_t)pair ^ ((uint32_t)(pair >> 32) * 0x85ebca6bU)) * 0x9e3779b9U + key);
 }
+// Per-step salt of every dropout stream (ea_set_rng_salt): launchers pass the process-wide
+// device pointer ea_g_rng_salt to their kernels, which mix *salt into the site seed.  The
+// salt lives in device memory so a captured hipGraph draws fresh masks on every replay
+// (ea_rng_advance is part of the graph); salt 0 leaves the seed unchanged.
+extern const unsigned long long* ea_g_rng_salt;
+EA_DEV uint64_t ea_salted(uint64_t seed, const unsigned long long* salt) {
+  return salt ? seed ^ (*salt * 0x9E3779B97F4A7C15ull) : seed;
+}
 EA_DEV uint32_t ea_drop_thr(float p) { return (uint32_t)fminf(p * 65536.f + 0.5f, 65536.f); }
 // returns scale (1/(1-p)) if kept, 0 if dropped; p<=0 -> 1
 EA_DEV float drop_scale(uint64_t seed, uint64_t idx, float p) {

@@ -74,7 +74,8 @@ __global__ void sos_eos_kernel(int B, int L, const long long* __restrict__ ys, l
 // ---------------------------------------------------------------- dropout / cast / scale
 template <typename TI, typename TO>
 __global__ void scale_drop_kernel(long n, int cols, const TI* __restrict__ x, long ldx, TO* __restrict__ y, long ldy,
-                                  float scale, float p, uint64_t seed) {
+                                  float scale, float p, uint64_t seed, const unsigned long long* salt) {
+  if (p > 0.f) seed = ea_salted(seed, salt);
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
     const long r = i / cols, c = i % cols;
     float v = to_f(x[r * ldx + c]) * scale;
@@ -87,7 +88,8 @@ __global__ void scale_drop_kernel(long n, int cols, const TI* __restrict__ x, lo
 template <typename TI, typename TO>
 __global__ __launch_bounds__(256) void scale_drop_vec_kernel(unsigned n4, unsigned cols4, const TI* __restrict__ x, long ldx,
                                                              TO* __restrict__ y, long ldy, float scale, float p,
-                                                             uint64_t seed) {
+                                                             uint64_t seed, const unsigned long long* salt) {
+  if (p > 0.f) seed = ea_salted(seed, salt);
   for (unsigned i = blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += gridDim.x * blockDim.x) {
     const unsigned r = i / cols4, c = (i - r * cols4) * 4;
     float v[4];
@@ -518,7 +520,9 @@ __global__ void add_pos_bias_kernel(long N, int H, int dk, const T* __restrict__
 // ---------------------------------------------------------------- embeddings (decoder)
 // y[r] = dropout(E[tok[r]] * xscale + pe[pos(r)]), pos(r) = r % L
 __global__ void embed_fwd_kernel(long rows, int d, int L, const long long* __restrict__ tok, const float* __restrict__ E,
-                                 float xscale, const float* __restrict__ pe, float p, uint64_t seed, float* __restrict__ y) {
+                                 float xscale, const float* __restrict__ pe, float p, uint64_t seed,
+                                 const unsigned long long* salt, float* __restrict__ y) {
+  if (p > 0.f) seed = ea_salted(seed, salt);
   const long n = rows * d;
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
     const long r = i / d;
@@ -528,16 +532,37 @@ __global__ void embed_fwd_kernel(long rows, int d, int L, const long long* __res
     y[i] = v;
   }
 }
-// dE[tok[r]] += xscale * dropout_mask * dy[r]   (float atomics)
-__global__ void embed_bwd_kernel(long rows, int d, const long long* __restrict__ tok, const float* __restrict__ dy,
-                                 float xscale, float p, uint64_t seed, float* __restrict__ dE) {
-  const long n = rows * d;
-  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
-    const long r = i / d;
-    const int c = (int)(i % d);
-    float v = dy[i] * xscale;
-    if (p > 0.f) v *= drop_scale(seed, (uint64_t)i, p);
-    atomicAdd(&dE[tok[r] * d + c], v);
+// dE[tok[r]] += xscale * dropout_mask * dy[r], deterministic: one block per row r; the
+// block of a token's FIRST row sums all of that token's rows in increasing order and owns
+// the update of dE[tok] (no atomics, bit-reproducible).  tok staged in LDS (rows <= 4096).
+constexpr int EMBED_BWD_MAXROWS = 4096;
+__global__ __launch_bounds__(256) void embed_bwd_kernel(int rows, int d, const long long* __restrict__ tok,
+                                                        const float* __restrict__ dy, float xscale, float p,
+                                                        uint64_t seed, const unsigned long long* salt,
+                                                        float* __restrict__ dE) {
+  __shared__ int stok[EMBED_BWD_MAXROWS];
+  __shared__ int dup;
+  if (p > 0.f) seed = ea_salted(seed, salt);
+  const int r = blockIdx.x;
+  const long long me = tok[r];
+  if (threadIdx.x == 0) dup = 0;
+  __syncthreads();
+  for (int q = threadIdx.x; q < rows; q += blockDim.x) {
+    stok[q] = (int)tok[q];
+    if (q < r && tok[q] == me) dup = 1;
+  }
+  __syncthreads();
+  if (dup) return;
+  for (int c = threadIdx.x; c < d; c += blockDim.x) {
+    float a = 0.f;
+    for (int q = r; q < rows; ++q) {
+      if (stok[q] != (int)me) continue;
+      const uint64_t i = (uint64_t)q * d + c;
+      float v = dy[i] * xscale;
+      if (p > 0.f) v *= drop_scale(seed, i, p);
+      a += v;
+    }
+    dE[me * d + c] += a;
   }
 }
 
@@ -592,6 +617,26 @@ extern "C" int ea_add_sos_eos(int B, int L, const long long* ys, long ldys, cons
   return 0;
 }
 
+const unsigned long long* ea_g_rng_salt = nullptr;
+
+namespace {
+__global__ void rng_advance_kernel(unsigned long long* salt) { salt[0] += 1ull; }
+}  // namespace
+
+extern "C" int ea_set_rng_salt(const unsigned long long* salt) {
+  EA_ENTRY();
+  ea_g_rng_salt = salt;
+  return 0;
+}
+
+extern "C" int ea_rng_advance(unsigned long long* salt, void* stream) {
+  EA_ENTRY();
+  EA_CHECK_ARG(salt != nullptr);
+  hipLaunchKernelGGL(rng_advance_kernel, dim3(1), dim3(1), 0, (hipStream_t)stream, salt);
+  EA_LAUNCH_CHECK();
+  return 0;
+}
+
 extern "C" int ea_scale_dropout(long rows, int cols, const void* x, int x_dtype, long ldx, void* y, int y_dtype,
                                 long ldy, float scale, float p, unsigned long long seed, void* stream) {
   EA_ENTRY();
@@ -601,7 +646,7 @@ extern "C" int ea_scale_dropout(long rows, int cols, const void* x, int x_dtype,
   if (cols % 4 == 0 && ldx % 4 == 0 && ldy % 4 == 0 && (uintptr_t)x % xa == 0 && (uintptr_t)y % ya == 0 &&
       n / 4 < (1L << 31)) {
     const unsigned n4 = (unsigned)(n / 4), c4 = (unsigned)(cols / 4);
-#define EA_SDV(TI, TO) hipLaunchKernelGGL((scale_drop_vec_kernel<TI, TO>), EA_GRID(n4), n4, c4, (const TI*)x, ldx, (TO*)y, ldy, scale, p, (uint64_t)seed)
+#define EA_SDV(TI, TO) hipLaunchKernelGGL((scale_drop_vec_kernel<TI, TO>), EA_GRID(n4), n4, c4, (const TI*)x, ldx, (TO*)y, ldy, scale, p, (uint64_t)seed, ea_g_rng_salt)
     if (x_dtype == EA_BF16 && y_dtype == EA_BF16) EA_SDV(bf16, bf16);
     else if (x_dtype == EA_BF16) EA_SDV(bf16, float);
     else if (y_dtype == EA_BF16) EA_SDV(float, bf16);
@@ -610,7 +655,7 @@ extern "C" int ea_scale_dropout(long rows, int cols, const void* x, int x_dtype,
     EA_LAUNCH_CHECK();
     return 0;
   }
-#define EA_SD(TI, TO) hipLaunchKernelGGL((scale_drop_kernel<TI, TO>), EA_GRID(n), n, cols, (const TI*)x, ldx, (TO*)y, ldy, scale, p, (uint64_t)seed)
+#define EA_SD(TI, TO) hipLaunchKernelGGL((scale_drop_kernel<TI, TO>), EA_GRID(n), n, cols, (const TI*)x, ldx, (TO*)y, ldy, scale, p, (uint64_t)seed, ea_g_rng_salt)
   if (x_dtype == EA_BF16 && y_dtype == EA_BF16) EA_SD(bf16, bf16);
   else if (x_dtype == EA_BF16) EA_SD(bf16, float);
   else if (y_dtype == EA_BF16) EA_SD(float, bf16);
@@ -802,7 +847,7 @@ extern "C" int ea_embed_fwd(long rows, int d, int L, const long long* tok, const
                             const float* pe, float p, unsigned long long seed, float* y, void* stream) {
   EA_ENTRY();
   const long n = rows * d;
-  hipLaunchKernelGGL(embed_fwd_kernel, EA_GRID(n), rows, d, L, tok, E, xscale, pe, p, (uint64_t)seed, y);
+  hipLaunchKernelGGL(embed_fwd_kernel, EA_GRID(n), rows, d, L, tok, E, xscale, pe, p, (uint64_t)seed, ea_g_rng_salt, y);
   EA_LAUNCH_CHECK();
   return 0;
 }
@@ -810,8 +855,10 @@ extern "C" int ea_embed_fwd(long rows, int d, int L, const long long* tok, const
 extern "C" int ea_embed_bwd(long rows, int d, const long long* tok, const float* dy, float xscale, float p,
                             unsigned long long seed, float* dE, void* stream) {
   EA_ENTRY();
-  const long n = rows * d;
-  hipLaunchKernelGGL(embed_bwd_kernel, EA_GRID(n), rows, d, tok, dy, xscale, p, (uint64_t)seed, dE);
+  EA_CHECK_ARG(rows >= 0 && rows <= EMBED_BWD_MAXROWS);
+  if (rows == 0) return 0;
+  hipLaunchKernelGGL(embed_bwd_kernel, dim3((unsigned)rows), dim3(256), 0, (hipStream_t)stream, (int)rows, d, tok,
+                     dy, xscale, p, (uint64_t)seed, ea_g_rng_salt, dE);
   EA_LAUNCH_CHECK();
   return 0;
 }

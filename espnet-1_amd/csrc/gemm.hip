@@ -39,7 +39,21 @@ struct GemmP {
   int vec_c;         // 4-column vector epilogue allowed (aligned C/aux/resid/bias, N % 4 == 0)
   int lds;           // bf16 LDS-DMA kernel eligible (aligned operands < 4 GB)
   int bm, bn;        // output tile (LDS-DMA bf16 kernel: 64/128/256 x 128/256; else 128 x 128)
+  const unsigned long long* salt;  // per-step dropout salt (device), see ea_set_rng_salt
+  unsigned long long* stamp;       // kernel-span probe [first block start, last block end] or null
 };
+
+// In-kernel span probe (ea_gemm_set_probe): s_memrealtime is the GPU's constant 100 MHz
+// clock; the first block to start and the last to finish bound the launch's execution.
+EA_DEV void probe_start(const GemmP& p) {
+  if (p.stamp && threadIdx.x == 0) atomicMin(&p.stamp[0], (unsigned long long)__builtin_amdgcn_s_memrealtime());
+}
+EA_DEV void probe_end(const GemmP& p) {
+  if (p.stamp) {
+    __syncthreads();
+    if (threadIdx.x == 0) atomicMax(&p.stamp[1], (unsigned long long)__builtin_amdgcn_s_memrealtime());
+  }
+}
 
 EA_DEV int swz_k(int row) { return (row >> 1) & 7; }                         // K-major rows
 EA_DEV int swz_mn_bf16(int k) { return 2 * ((k & 3) | (((k >> 3) & 1) << 2)); }  // [k][128] bf16
@@ -131,26 +145,27 @@ EA_DEV void epi_one(const GemmP& p, int z, int zb, int zh, int row, int col, flo
   const ea_epilogue& e = p.epi;
   const long cidx = zb * p.sCb + zh * p.sCh + (long)row * p.ldc + col;
   const uint64_t didx = ((uint64_t)z * p.M + row) * (uint64_t)p.N + col;
+  const uint64_t seed = e.drop_p > 0.f ? ea_salted(e.seed, p.salt) : 0;
   float v = e.alpha * acc;
   if constexpr (KIND == EA_EPI_STORE) {
     if (e.bias) v += e.bias[col];
     v *= e.post_scale;
-    if (e.drop_p > 0.f) v *= drop_scale(e.seed, didx, e.drop_p);
+    if (e.drop_p > 0.f) v *= drop_scale(seed, didx, e.drop_p);
     if (e.beta != 0.f) v += e.beta * load_as_f(p.C, cidx, p.c_dtype);
     store_from_f(p.C, cidx, p.c_dtype, v);
   } else if constexpr (KIND == EA_EPI_ACT) {
     if (e.bias) v += e.bias[col];
     if (e.aux) store_from_f(e.aux, (long)row * e.ldaux + col, e.aux_dtype, v);
     float a = act_fwd(e.act, v);
-    if (e.drop_p > 0.f) a *= drop_scale(e.seed, didx, e.drop_p);
+    if (e.drop_p > 0.f) a *= drop_scale(seed, didx, e.drop_p);
     store_from_f(p.C, cidx, p.c_dtype, a);
   } else if constexpr (KIND == EA_EPI_RESID) {
     if (e.bias) v += e.bias[col];
-    if (e.drop_p > 0.f) v *= drop_scale(e.seed, didx, e.drop_p);
+    if (e.drop_p > 0.f) v *= drop_scale(seed, didx, e.drop_p);
     const float r = e.resid ? e.resid[(long)row * e.ldr + col] : 0.f;
     ((float*)p.C)[cidx] = r + e.rscale * v;
   } else {  // EA_EPI_DACT
-    if (e.drop_p > 0.f) v *= drop_scale(e.seed, didx, e.drop_p);
+    if (e.drop_p > 0.f) v *= drop_scale(seed, didx, e.drop_p);
     v *= act_bwd(e.act, load_as_f(e.aux, (long)row * e.ldaux + col, e.aux_dtype));
     store_from_f(p.C, cidx, p.c_dtype, v);
   }
@@ -211,6 +226,7 @@ EA_DEV void epi_four(const GemmP& p, int z, int zb, int zh, int row, int col, co
   const ea_epilogue& e = p.epi;
   const long cidx = zb * p.sCb + zh * p.sCh + (long)row * p.ldc + col;
   const uint64_t didx = ((uint64_t)z * p.M + row) * (uint64_t)p.N + col;
+  const uint64_t seed = e.drop_p > 0.f ? ea_salted(e.seed, p.salt) : 0;
   float v[4];
 #pragma unroll
   for (int c = 0; c < 4; ++c) v[c] = e.alpha * acc[c];
@@ -221,7 +237,7 @@ EA_DEV void epi_four(const GemmP& p, int z, int zb, int zh, int row, int col, co
   if constexpr (KIND == EA_EPI_STORE) {
 #pragma unroll
     for (int c = 0; c < 4; ++c) v[c] *= e.post_scale;
-    drop_scale4(e.seed, didx, e.drop_p, v);
+    drop_scale4(seed, didx, e.drop_p, v);
     if (e.beta != 0.f) {
       float o[4];
       ld4(p.C, cidx, p.c_dtype, o);
@@ -233,19 +249,19 @@ EA_DEV void epi_four(const GemmP& p, int z, int zb, int zh, int row, int col, co
     if (e.aux) st4(e.aux, (long)row * e.ldaux + col, e.aux_dtype, v);
 #pragma unroll
     for (int c = 0; c < 4; ++c) v[c] = act_fwd(e.act, v[c]);
-    drop_scale4(e.seed, didx, e.drop_p, v);
+    drop_scale4(seed, didx, e.drop_p, v);
     st4(p.C, cidx, p.c_dtype, v);
   } else if constexpr (KIND == EA_EPI_RESID) {
     float r[4] = {0.f, 0.f, 0.f, 0.f};
     if (e.resid) ld4(e.resid, (long)row * e.ldr + col, EA_F32, r);
-    drop_scale4(e.seed, didx, e.drop_p, v);
+    drop_scale4(seed, didx, e.drop_p, v);
 #pragma unroll
     for (int c = 0; c < 4; ++c) v[c] = r[c] + e.rscale * v[c];
     st4(p.C, cidx, EA_F32, v);
   } else {
     float h[4];
     ld4(e.aux, (long)row * e.ldaux + col, e.aux_dtype, h);
-    drop_scale4(e.seed, didx, e.drop_p, v);
+    drop_scale4(seed, didx, e.drop_p, v);
 #pragma unroll
     for (int c = 0; c < 4; ++c) v[c] *= act_bwd(e.act, h[c]);
     st4(p.C, cidx, p.c_dtype, v);
@@ -559,6 +575,7 @@ __global__ __launch_bounds__(128 * WN, 1) void gemm_bf16_lds(GemmP p) {
   constexpr int SMEM = STAGES * STAGE_BYTES > EPI_BYTES ? STAGES * STAGE_BYTES : EPI_BYTES;
   constexpr bool DB = MI * NJ <= 16;
   __shared__ __attribute__((aligned(1024))) char smem[SMEM];
+  probe_start(p);
 
   const int nt = p.tiles_m * p.tiles_n;
   const int bid = blockIdx.x;
@@ -699,6 +716,7 @@ __global__ __launch_bounds__(128 * WN, 1) void gemm_bf16_lds(GemmP p) {
     case EA_EPI_RESID: epi_wave<EA_EPI_RESID, MI, NJ>(p, smem, z, zb, zh, m0 + wm, n0 + wn, lane, w, acc); break;
     default: epi_wave<EA_EPI_DACT, MI, NJ>(p, smem, z, zb, zh, m0 + wm, n0 + wn, lane, w, acc); break;
   }
+  probe_end(p);
 }
 
 // split-K combine: C = epi(sum_s slab[s]) (any epilogue kind), 4 columns per thread
@@ -733,6 +751,7 @@ __global__ void splitk_reduce(GemmP p) {
 }
 
 int g_gemm_stages = 2;
+unsigned long long* g_probe = nullptr;  // ea_gemm_set_probe
 int g_gemm_bm64 = 1;  // LDS ring depth of gemm_bf16_lds (2: 64 KiB, 2 blocks/CU; 3: 96 KiB)
 
 int launch_lds(GemmP& p, int a_k, int b_k, int nz, hipStream_t st) {
@@ -816,6 +835,35 @@ extern "C" int ea_gemm_set_pipeline(int stages) {
   return 0;
 }
 
+namespace {
+__global__ void probe_begin_kernel(unsigned long long* s) { s[0] = ~0ull; s[1] = 0ull; }
+__global__ void probe_end_kernel(unsigned long long* s) {
+  if (s[1] > s[0]) { s[2] += s[1] - s[0]; s[3] += 1ull; }
+}
+}  // namespace
+
+extern "C" int ea_gemm_set_probe(unsigned long long* slots) {
+  EA_ENTRY();
+  g_probe = slots;
+  return 0;
+}
+
+extern "C" int ea_probe_begin(unsigned long long* slots, void* stream) {
+  EA_ENTRY();
+  EA_CHECK_ARG(slots != nullptr);
+  hipLaunchKernelGGL(probe_begin_kernel, dim3(1), dim3(1), 0, (hipStream_t)stream, slots);
+  EA_LAUNCH_CHECK();
+  return 0;
+}
+
+extern "C" int ea_probe_end(unsigned long long* slots, void* stream) {
+  EA_ENTRY();
+  EA_CHECK_ARG(slots != nullptr);
+  hipLaunchKernelGGL(probe_end_kernel, dim3(1), dim3(1), 0, (hipStream_t)stream, slots);
+  EA_LAUNCH_CHECK();
+  return 0;
+}
+
 extern "C" int ea_gemm_set_tile(int bm, int bn) {
   EA_ENTRY();
   EA_CHECK_ARG((bm == 0 && bn == 0) || (bm == 64 && bn == 128) || (bm == 128 && bn == 128) ||
@@ -847,6 +895,8 @@ extern "C" int ea_gemm(int dtype, int a_kmajor, int b_kmajor, int M, int N, int 
   p.C = C; p.c_dtype = c_dtype; p.ldc = ldc; p.sCb = sCb; p.sCh = sCh;
   p.epi = *epi;
   p.ws = workspace;
+  p.salt = ea_g_rng_salt;
+  p.stamp = g_probe;
   // unaligned operands (odd vocab / leading dims) take the element-wise load path
   p.vec_a = (lda % E == 0 && sAb % E == 0 && sAh % E == 0 && ((uintptr_t)A % 16) == 0);
   p.vec_b = (ldb % E == 0 && sBb % E == 0 && sBh % E == 0 && ((uintptr_t)B % 16) == 0);

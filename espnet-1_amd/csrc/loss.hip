@@ -145,17 +145,34 @@ __global__ __launch_bounds__(256) void ctc_grad_kernel(CtcP p, const float* __re
     for (int v = threadIdx.x; v < p.V; v += blockDim.x) gr[v] = from_f<TO>(0.f);
     return;
   }
+  __shared__ double red[16];
   for (int v = threadIdx.x; v < p.V; v += blockDim.x) acc[v] = 0.f;
   __syncthreads();
   const int L = (int)p.ylens[b];
   const int S = 2 * L + 1;
   const double* A = p.alpha + ((long)b * p.T + t) * p.Smax;
   const double* Bt = p.beta + ((long)b * p.T + t) * p.Smax;
-  for (int s = threadIdx.x; s < S; s += blockDim.x) {
-    const int lab = ctc_label(p, b, s);
+  // occupancy per label, summed in a fixed order (no atomics: bit-reproducible):
+  // blank (every even s) by a block reduction; a label at odd s by the thread owning its
+  // first occurrence, over all its occurrences in increasing s
+  auto occ = [&](int s, int lab) -> double {
     const double ab = A[s] + Bt[s];
-    if (ab != -INFINITY) atomicAdd(&acc[lab], (float)exp(ab + nll - ctc_lp(p, b, t, lab)));
+    return ab != -INFINITY ? exp(ab + nll - ctc_lp(p, b, t, lab)) : 0.0;
+  };
+  double bsum = 0.0;
+  for (int s = 2 * threadIdx.x; s < S; s += 2 * blockDim.x) bsum += occ(s, 0);
+  bsum = block_sum_d(bsum, red);
+  for (int s = 2 * threadIdx.x + 1; s < S; s += 2 * blockDim.x) {
+    const int lab = ctc_label(p, b, s);
+    bool first = true;
+    for (int q = 1; q < s; q += 2) first = first && ctc_label(p, b, q) != lab;
+    if (!first) continue;
+    double a = 0.0;
+    for (int q = s; q < S; q += 2)
+      if (ctc_label(p, b, q) == lab) a += occ(q, lab);
+    acc[lab] = (float)a;
   }
+  if (threadIdx.x == 0) acc[0] = (float)bsum;
   __syncthreads();
   const float g = gscale[0] * coef;
   const float* xr = p.logits + row * p.ldt;

@@ -32,14 +32,45 @@ struct AdamP {
   float lr, b1, b2, eps, wd;
   float bc1, bc2_sqrt;   // 1-b1^t, sqrt(1-b2^t)
   const float* norm; float max_norm;
+  const ea_opt_state* st;  // device step state: lr / bias corrections / skip come from here
 };
 
+// Device-resident step bookkeeping (ea_adam_step_dev): runs before the update, one thread.
+// A non-finite norm skips both optimizer.step() and scheduler.step() (trainer.py:662-697),
+// so the step counter only advances on an applied update.
+__global__ void adam_prep_kernel(ea_opt_state* st, ea_lr_schedule sc, float b1, float b2, const float* norm,
+                                 float max_norm) {
+  const float nrm = norm ? norm[0] : 0.f;
+  st->last_norm = nrm;
+  if (norm && !isfinite(nrm)) {
+    st->skip = 1;
+    return;
+  }
+  st->skip = 0;
+  const long long t = st->step + 1;
+  st->step = t;
+  double lr = sc.base_lr;
+  if (sc.kind == EA_SCHED_WARMUP) {  // espnet2/schedulers/warmup_lr.py:40-50, s = t
+    const double s = (double)t, w = sc.warmup_steps;
+    lr = sc.base_lr * sqrt(w) * fmin(1.0 / sqrt(s), s * pow(w, -1.5));
+  }
+  st->lr = (float)lr;
+  st->bc1 = (float)(1.0 - pow((double)b1, (double)t));
+  st->bc2_sqrt = (float)sqrt(1.0 - pow((double)b2, (double)t));
+  st->coef = (norm && max_norm > 0.f) ? fminf(max_norm / (nrm + 1e-6f), 1.f) : 1.f;
+}
+
 __global__ __launch_bounds__(256) void adam_kernel(AdamP a) {
-  const float nrm = a.norm ? a.norm[0] : 0.f;
-  if (a.norm && !isfinite(nrm)) return;  // trainer.py:662: skip the update
-  float coef = 1.f;
-  if (a.norm && a.max_norm > 0.f) coef = fminf(a.max_norm / (nrm + 1e-6f), 1.f);
-  const float step_size = a.lr / a.bc1;
+  float coef = 1.f, lr = a.lr, bc1 = a.bc1, bc2s = a.bc2_sqrt;
+  if (a.st) {
+    if (a.st->skip) return;
+    coef = a.st->coef; lr = a.st->lr; bc1 = a.st->bc1; bc2s = a.st->bc2_sqrt;
+  } else {
+    const float nrm = a.norm ? a.norm[0] : 0.f;
+    if (a.norm && !isfinite(nrm)) return;  // trainer.py:662: skip the update
+    if (a.norm && a.max_norm > 0.f) coef = fminf(a.max_norm / (nrm + 1e-6f), 1.f);
+  }
+  const float step_size = lr / bc1;
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < a.n; i += (long)gridDim.x * blockDim.x) {
     float p = a.p[i];
     float g = a.g[i] * coef;
@@ -47,7 +78,7 @@ __global__ __launch_bounds__(256) void adam_kernel(AdamP a) {
     float m = a.m[i];
     m = m + (1.f - a.b1) * (g - m);  // lerp, as torch Adam
     float v = a.v[i] * a.b2 + (1.f - a.b2) * g * g;
-    const float denom = sqrtf(v) / a.bc2_sqrt + a.eps;
+    const float denom = sqrtf(v) / bc2s + a.eps;
     p -= step_size * (m / denom);
     a.p[i] = p;
     a.m[i] = m;
@@ -94,7 +125,29 @@ extern "C" int ea_adam_step(long n, float* params, const float* grads, float* ex
   a.bc1 = (float)(1.0 - pow((double)beta1, (double)step));
   a.bc2_sqrt = (float)sqrt(1.0 - pow((double)beta2, (double)step));
   a.norm = grad_norm; a.max_norm = max_norm;
+  a.st = nullptr;
   hipLaunchKernelGGL(adam_kernel, dim3(ea_grid_cap(ea_cdiv(n, 256), 4096)), dim3(256), 0, (hipStream_t)stream, a);
+  EA_LAUNCH_CHECK();
+  return 0;
+}
+
+extern "C" int ea_adam_step_dev(long n, float* params, const float* grads, float* exp_avg, float* exp_avg_sq,
+                                void* params_bf16, const ea_lr_schedule* sched, float beta1, float beta2, float eps,
+                                float weight_decay, ea_opt_state* state, const float* grad_norm, float max_norm,
+                                void* stream) {
+  EA_ENTRY();
+  EA_CHECK_ARG(sched != nullptr && state != nullptr);
+  EA_CHECK_ARG(sched->kind == EA_SCHED_CONSTANT || (sched->kind == EA_SCHED_WARMUP && sched->warmup_steps > 0.f));
+  hipStream_t st = (hipStream_t)stream;
+  hipLaunchKernelGGL(adam_prep_kernel, dim3(1), dim3(1), 0, st, state, *sched, beta1, beta2, grad_norm, max_norm);
+  EA_LAUNCH_CHECK();
+  AdamP a;
+  a.n = n; a.p = params; a.g = grads; a.m = exp_avg; a.v = exp_avg_sq; a.p16 = (bf16*)params_bf16;
+  a.lr = 0.f; a.b1 = beta1; a.b2 = beta2; a.eps = eps; a.wd = weight_decay;
+  a.bc1 = 1.f; a.bc2_sqrt = 1.f;
+  a.norm = grad_norm; a.max_norm = max_norm;
+  a.st = state;
+  hipLaunchKernelGGL(adam_kernel, dim3(ea_grid_cap(ea_cdiv(n, 256), 4096)), dim3(256), 0, st, a);
   EA_LAUNCH_CHECK();
   return 0;
 }

@@ -38,6 +38,17 @@ class Epilogue(ctypes.Structure):
     ]
 
 
+SCHED_CONSTANT, SCHED_WARMUP = 0, 1
+
+
+class LrSchedule(ctypes.Structure):
+    _fields_ = [("kind", ctypes.c_int), ("warmup_steps", ctypes.c_float), ("base_lr", ctypes.c_double)]
+
+
+# ea_opt_state (device memory, 32 B): step i64 | lr bc1 bc2_sqrt coef last_norm f32 | skip i32
+OPT_STATE_BYTES = 32
+
+
 _CTYPES = {
     "int": ctypes.c_int,
     "long": ctypes.c_long,

@@ -165,12 +165,20 @@ class ESPnetASRModel(AbsESPnetModel):
             self.ctc.bind(self.arena, "ctc.", cd)
         self.seed = seed
         self._device = device
+        # per-step dropout salt in device memory (ea_set_rng_salt): advanced on the stream at
+        # every training forward, so eager steps and hipGraph replays draw fresh masks alike
+        self._rng_salt = torch.zeros(1, dtype=torch.int64, device=device)
         return self
 
     def _next_seed(self):
-        self._step += 1
+        """Site seeds are fixed per (model seed, rank); the per-step variation of every
+        dropout mask comes from the device salt, advanced here (on the stream)."""
+        lib.ea_set_rng_salt(self._rng_salt.data_ptr())
+        if self.training:
+            self._step += 1
+            lib.ea_rng_advance(self._rng_salt.data_ptr(), ops.stream())
         rank = torch.distributed.get_rank() if torch.distributed.is_initialized() else 0
-        return site_seed(self.seed + 1, self._step, 1000 + rank)
+        return site_seed(self.seed + 1, 0, 1000 + rank)
 
     def _dev(self, t, dtype=None):
         if t.device != self._device:
@@ -187,9 +195,14 @@ class ESPnetASRModel(AbsESPnetModel):
             (speech.shape, speech_lengths.shape, text.shape, text_lengths.shape)
         batch_size = speech.shape[0]
         seed = self._next_seed()
-        # host-side maxima (the reference syncs here too: text_lengths.max(), :218/:420)
-        tl_max = int(text_lengths.max())
-        sl_max = int(speech_lengths.max())
+        # host-side maxima (the reference syncs here too: text_lengths.max(), :218/:420);
+        # a captured step (train/graph.py) passes them in, its lengths live on the device
+        maxlens = kwargs.get("_maxlens")
+        if maxlens is not None:
+            sl_max, tl_max = maxlens
+        else:
+            tl_max = int(text_lengths.max())
+            sl_max = int(speech_lengths.max())
         text = self._dev(text)[:, :tl_max]
         if self.ignore_id != -1:
             text = text.masked_fill(text == -1, self.ignore_id)

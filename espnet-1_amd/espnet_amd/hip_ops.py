@@ -19,29 +19,37 @@ _DT = {torch.float32: F32, torch.bfloat16: BF16}
 
 
 class KernelProbe:
-    """HIP-event brackets around named launches on the launching (current) stream, used by
-    bench.py to time the dominant kernel inside the timed region."""
+    """Measures named GEMM launches from inside the kernel (bench.py): the launch stamps its
+    first-block start and last-block end on the GPU's constant 100 MHz clock
+    (ea_gemm_set_probe); stream-ordered begin/end kernels accumulate the span, so a launch
+    captured into a hipGraph is re-measured on every replay."""
 
-    def __init__(self, names):
+    TICK_MS = 1e-5  # s_memrealtime: 100 MHz
+
+    def __init__(self, names, device=None):
         self.names = set(names)
-        self.pairs = {n: [] for n in names}
+        dev = device or torch.device("cuda", torch.cuda.current_device())
+        self.slots = {n: torch.zeros(4, dtype=torch.int64, device=dev) for n in names}
         self.active = True
 
     def begin(self, name):
         if self.active and name in self.names:
-            e = torch.cuda.Event(enable_timing=True)
-            e.record()
-            self.pairs[name].append([e, None])
+            s = self.slots[name].data_ptr()
+            lib.ea_probe_begin(s, stream())
+            lib.ea_gemm_set_probe(s)
 
     def end(self, name):
         if self.active and name in self.names:
-            e = torch.cuda.Event(enable_timing=True)
-            e.record()
-            self.pairs[name][-1][1] = e
+            lib.ea_gemm_set_probe(None)
+            lib.ea_probe_end(self.slots[name].data_ptr(), stream())
+
+    def reset(self):
+        for t in self.slots.values():
+            t.zero_()
 
     def mean_ms(self, name):
-        ts = [a.elapsed_time(b) for a, b in self.pairs[name] if b is not None]
-        return sum(ts) / len(ts) if ts else float("nan"), len(ts)
+        tot, cnt = (int(x) for x in self.slots[name][2:4].tolist())
+        return (tot / cnt * self.TICK_MS if cnt else float("nan")), cnt
 
 
 PROBE = None

@@ -1,0 +1,110 @@
+"""A whole training step captured as one hipGraph and replayed.
+
+The eager step (trainer.py's Trainer.train_one_step: forward, backward, RCCL gradient
+all-reduce, clip_grad_norm_, Adam, WarmupLR, zero_grad — espnet2/train/trainer.py:567-701)
+issues ~1,400 kernel launches through Python; on MI355X the host then needs longer to
+issue a C3 step than the GPU needs to run it.  Every launch of the step takes its
+per-step values from device memory (dropout salt: ea_rng_advance; step count, lr, bias
+corrections, clip coefficient and skip flag: ea_adam_step_dev; lengths: device tensors),
+so the launch sequence is identical from step to step and can be captured once per input
+shape and replayed with a single host call.
+
+Semantics per call are exactly one training step on the given batch:
+  * the first `warmup` calls for a new shape run eagerly (on a side stream, as graph
+    capture requires: lazy allocations, scratch buffers and the RCCL communicator are
+    created there);
+  * the next call captures the step (capture executes nothing) and replays it once;
+  * later calls copy the batch into the graph's static input buffers and replay.
+Shapes (B, T_max, F, L_max) key the graphs; lengths below the maxima vary freely since the
+kernels read them from device memory.  Outputs (loss, stats, weight, grad_norm) are views
+of graph memory, overwritten by the next replay of the same graph.
+"""
+from __future__ import annotations
+
+from typing import Dict, Optional
+
+import torch
+
+from .trainer import Trainer
+
+
+class _Captured:
+    __slots__ = ("graph", "inputs", "outputs", "maxlens")
+
+
+class CapturedTrainStep:
+    def __init__(self, model, optimizer, scheduler=None, *, grad_clip: float = 5.0, dp=None,
+                 warmup: int = 2, enabled: bool = True):
+        self.model = model
+        self.optimizer = optimizer
+        self.scheduler = scheduler
+        self.grad_clip = grad_clip
+        self.dp = dp
+        self.warmup = max(1, int(warmup))
+        self.enabled = enabled
+        self.graphs: Dict[tuple, _Captured] = {}
+        self._seen: Dict[tuple, int] = {}
+        self._pool = None
+        self._side = None
+
+    # ------------------------------------------------------------------ helpers
+    def _eager(self, batch, maxlens):
+        return Trainer.train_one_step(self.model, batch, self.optimizer, self.scheduler,
+                                      grad_clip=self.grad_clip, dp=self.dp, maxlens=maxlens)
+
+    def _device_batch(self, batch, maxlens):
+        dev = self.model._device
+        sl, tl = maxlens
+        return dict(speech=batch["speech"][:, :sl].to(dev, non_blocking=True).contiguous(),
+                    speech_lengths=batch["speech_lengths"].to(dev, non_blocking=True),
+                    text=batch["text"][:, :tl].to(dev, non_blocking=True).contiguous(),
+                    text_lengths=batch["text_lengths"].to(dev, non_blocking=True))
+
+    @staticmethod
+    def _maxlens(batch):
+        return int(batch["speech_lengths"].max()), int(batch["text_lengths"].max())
+
+    # ------------------------------------------------------------------ step
+    def __call__(self, batch: Dict[str, torch.Tensor], maxlens: Optional[tuple] = None):
+        """One training step on `batch`; returns (loss, stats, weight, grad_norm)."""
+        if maxlens is None:
+            maxlens = self._maxlens(batch)
+        if not self.enabled:
+            return self._eager(batch, None)
+        B, _, F = batch["speech"].shape
+        key = (B, maxlens[0], F, maxlens[1])
+        cap = self.graphs.get(key)
+        if cap is not None:
+            for k, v in cap.inputs.items():
+                v.copy_(batch[k][:, :v.shape[1]] if v.dim() > 1 else batch[k], non_blocking=True)
+            cap.graph.replay()
+            return cap.outputs
+        n = self._seen.get(key, 0)
+        self._seen[key] = n + 1
+        dbatch = self._device_batch(batch, maxlens)
+        if n < self.warmup:
+            if self._side is None:
+                self._side = torch.cuda.Stream(device=self.model._device)
+            main = torch.cuda.current_stream()
+            self._side.wait_stream(main)
+            with torch.cuda.stream(self._side):
+                out = self._eager(dbatch, maxlens)
+            main.wait_stream(self._side)
+            return out
+        return self._capture(key, dbatch, maxlens)
+
+    def _capture(self, key, dbatch, maxlens):
+        cap = _Captured()
+        cap.inputs = dbatch  # static input buffers (own storage)
+        cap.maxlens = maxlens
+        g = torch.cuda.CUDAGraph()
+        torch.cuda.synchronize()
+        with torch.cuda.graph(g, pool=self._pool):
+            out = self._eager(cap.inputs, maxlens)
+        if self._pool is None:
+            self._pool = g.pool()
+        cap.graph = g
+        cap.outputs = out
+        self.graphs[key] = cap
+        g.replay()  # capture executes nothing: run this batch's step now
+        return out

@@ -24,10 +24,13 @@ from ..optim.adam import ArenaAdam
 class Trainer:
     @staticmethod
     def train_one_step(model, batch: Dict[str, torch.Tensor], optimizer: ArenaAdam, scheduler=None, *,
-                       grad_clip: float = 5.0, accum_grad: int = 1, iiter: int = 1, dp=None):
+                       grad_clip: float = 5.0, accum_grad: int = 1, iiter: int = 1, dp=None, maxlens=None):
         if dp is not None and dp.world_size > 1:
             dp.broadcast_buffers()
-        loss, stats, weight = model(**batch)
+        if maxlens is not None:
+            loss, stats, weight = model(**batch, _maxlens=maxlens)
+        else:
+            loss, stats, weight = model(**batch)
         stats = {k: v for k, v in stats.items() if v is not None}
         if dp is not None and dp.world_size > 1:
             loss, stats, weight = dp.weighted_average(loss, stats, weight)

@@ -75,6 +75,17 @@ int ea_gemm_set_pipeline(int stages);
  * 0,0 = automatic choice by grid size.  Process-wide; for tests and tuning. */
 int ea_gemm_set_tile(int bm, int bn);
 
+/* Kernel-span probe for measurement (bench.py): slots = 4 device u64
+ * {span start, span end, sum of spans, count} in units of the GPU's constant 100 MHz
+ * clock (s_memrealtime).  ea_probe_begin resets the span; ea_gemm launches made while
+ * ea_gemm_set_probe(slots) is set stamp their first-block start / last-block end into it;
+ * ea_probe_end adds the span to the sum.  All three are stream-ordered kernels, so a
+ * captured hipGraph re-measures on every replay (torch-ROCm refuses timing events inside
+ * captured graphs).  The LDS-DMA bf16 GEMM path only. */
+int ea_gemm_set_probe(unsigned long long* slots);
+int ea_probe_begin(unsigned long long* slots, void* stream);
+int ea_probe_end(unsigned long long* slots, void* stream);
+
 /* ---------------------------------------------------------------- normalisation */
 
 /* LayerNorm(eps) over the last dim, one wave64 per row; y in y_dtype, saves mean/rstd.
@@ -170,11 +181,18 @@ int ea_add_pos_bias(long N, int H, int dk, const void* q, long ldq, const float*
                     void* qu, void* qv, int dtype, void* stream);
 
 /* Decoder Embedding + PositionalEncoding (x*sqrt(d) + pe, dropout), embedding.py:81-92;
- * backward scatter-adds into the embedding gradient. */
+ * backward adds into the embedding gradient in a fixed order (no atomics; rows <= 4096). */
 int ea_embed_fwd(long rows, int d, int L, const long long* tok, const float* E, float xscale,
                  const float* pe, float p, unsigned long long seed, float* y, void* stream);
 int ea_embed_bwd(long rows, int d, const long long* tok, const float* dy, float xscale, float p,
                  unsigned long long seed, float* dE, void* stream);
+
+/* Dropout salt: all later launches read a per-step salt from device memory `salt`
+ * (NULL: none) and mix it into their site seeds; ea_rng_advance adds 1 on the stream.
+ * A captured hipGraph of a training step thus draws a fresh mask stream on each replay,
+ * as the reference's torch.nn.Dropout (bernoulli_) does per call. */
+int ea_set_rng_salt(const unsigned long long* salt);
+int ea_rng_advance(unsigned long long* salt, void* stream);
 
 /* CTC.argmax (ctc.py:119-127): first maximal index per row (bit-exact alignment). */
 int ea_argmax_rows(long rows, int V, const float* x, long ld, long long* out, void* stream);
@@ -233,6 +251,32 @@ int ea_sqnorm(long n, const float* x, double* workspace, float* norm, void* stre
 int ea_adam_step(long n, float* params, const float* grads, float* exp_avg, float* exp_avg_sq,
                  void* params_bf16, float lr, float beta1, float beta2, float eps, float weight_decay,
                  long step, const float* grad_norm, float max_norm, void* stream);
+
+/* Device-resident optimizer step (graph-capturable: nothing on the host changes per step).
+ * state (device memory) holds the count of APPLIED updates (torch Adam state['step'] and
+ * the batch-step scheduler's last_epoch): a prep kernel reads grad_norm, sets skip on a
+ * non-finite norm (trainer.py:662-697 skips optimizer.step() and scheduler.step()), else
+ * advances step to t and stores lr(t) from `sched` (EA_SCHED_WARMUP:
+ * base*w^0.5*min(t^-0.5, t*w^-1.5), espnet2/schedulers/warmup_lr.py:40-50), the bias
+ * corrections and the clip coefficient; the update kernel reads them. */
+enum { EA_SCHED_CONSTANT = 0, EA_SCHED_WARMUP = 1 };
+typedef struct ea_lr_schedule {
+  int kind;            /* EA_SCHED_* */
+  float warmup_steps;
+  double base_lr;
+} ea_lr_schedule;
+typedef struct ea_opt_state {  /* device memory, zero-initialised; 32 bytes */
+  long long step;      /* applied updates so far */
+  float lr;            /* lr of the last applied update */
+  float bc1, bc2_sqrt; /* 1-b1^t, sqrt(1-b2^t) */
+  float coef;          /* clip coefficient min(1, max_norm/(norm+1e-6)) */
+  float last_norm;     /* grad norm seen by the last call */
+  int skip;            /* 1: the last call skipped the update (non-finite norm) */
+} ea_opt_state;
+int ea_adam_step_dev(long n, float* params, const float* grads, float* exp_avg, float* exp_avg_sq,
+                     void* params_bf16, const ea_lr_schedule* sched, float beta1, float beta2, float eps,
+                     float weight_decay, ea_opt_state* state, const float* grad_norm, float max_norm,
+                     void* stream);
 
 int ea_cast_f32_bf16(long n, const float* x, void* y, void* stream);
 /* x *= s[0]*c (device scalar) */
