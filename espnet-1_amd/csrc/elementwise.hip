@@ -71,6 +71,116 @@ __global__ void sos_eos_kernel(int B, int L, const long long* __restrict__ ys, l
   if (threadIdx.x == 0) ys_in_lens[b] = l + 1;
 }
 
+// ---------------------------------------------------------------- conv1 direct (phase-split out)
+// Conv2dSubsampling's first Conv2d(1, C, 3, stride 2) + ReLU (subsampling.py:60-61) as a
+// direct kernel: 9 MACs per output, so a GEMM (K = 9) would only move bytes.  Output in the
+// phase-split layout of ea_conv_geo: pixel (t1, f1) -> plane (t1&1, f1&1), row (b, t1>>1, f1>>1).
+// One thread = 8 channels of one pixel (16-B bf16 stores); weights stay in registers.
+struct PhaseGeo {
+  int T1, F1, nI0, nI1, nJ0, nJ1;
+  long plane[4];
+};
+EA_DEV long phase_row(const PhaseGeo& g, int b, int t1, int f1) {
+  const int a = t1 & 1, e = f1 & 1;
+  const int nI = a ? g.nI1 : g.nI0, nJ = e ? g.nJ1 : g.nJ0;
+  return g.plane[a * 2 + e] + ((long)(b * nI + (t1 >> 1)) * nJ + (f1 >> 1));
+}
+template <typename TO>
+__global__ __launch_bounds__(256) void conv1_fwd_kernel(int B, int T, int F, PhaseGeo g, int C,
+                                                        const float* __restrict__ x, const float* __restrict__ w,
+                                                        const float* __restrict__ bias, TO* __restrict__ y) {
+  const int groups = C / 8;
+  const int cg = threadIdx.x % groups;  // blockDim.x is a multiple of C/8
+  const int c0 = cg * 8;
+  float wr[8][9], br[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    br[k] = bias[c0 + k];
+#pragma unroll
+    for (int t = 0; t < 9; ++t) wr[k][t] = w[(c0 + k) * 9 + t];
+  }
+  const long npix = (long)B * g.T1 * g.F1;
+  const int ppb = blockDim.x / groups;
+  for (long pix = (long)blockIdx.x * ppb + threadIdx.x / groups; pix < npix; pix += (long)gridDim.x * ppb) {
+    const int f1 = (int)(pix % g.F1);
+    const long bt = pix / g.F1;
+    const int t1 = (int)(bt % g.T1), b = (int)(bt / g.T1);
+    const float* xp = x + ((long)b * T + 2 * t1) * F + 2 * f1;
+    float xv[9];
+#pragma unroll
+    for (int kh = 0; kh < 3; ++kh)
+#pragma unroll
+      for (int kw = 0; kw < 3; ++kw) xv[kh * 3 + kw] = xp[kh * F + kw];
+    float o[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      float a = br[k];
+#pragma unroll
+      for (int t = 0; t < 9; ++t) a = fmaf(wr[k][t], xv[t], a);
+      o[k] = a > 0.f ? a : 0.f;
+    }
+    TO* yp = y + phase_row(g, b, t1, f1) * C + c0;
+    float lo[4] = {o[0], o[1], o[2], o[3]}, hi[4] = {o[4], o[5], o[6], o[7]};
+    vst4(yp, lo);
+    vst4(yp + 4, hi);
+  }
+}
+
+// conv1 weight/bias gradient from the (ReLU-masked) phase-split gradient dh (= d conv1
+// pre-activation): part[blk][t*C + c] = sum over the block's pixels of dh[p,c]*x_t(p),
+// t < 9, and part[blk][9*C + c] = sum dh[p,c]; reduced over blocks in fixed order.
+template <typename TI>
+__global__ __launch_bounds__(256) void conv1_wgrad_kernel(int B, int T, int F, PhaseGeo g, int C,
+                                                          const float* __restrict__ x, const TI* __restrict__ dh,
+                                                          float* __restrict__ part) {
+  __shared__ float red[256 * 10];
+  const int groups = C / 8;
+  const int cg = threadIdx.x % groups, c0 = cg * 8;
+  const int ppb = blockDim.x / groups, pl = threadIdx.x / groups;
+  float acc[10][8];
+#pragma unroll
+  for (int t = 0; t < 10; ++t)
+#pragma unroll
+    for (int k = 0; k < 8; ++k) acc[t][k] = 0.f;
+  const long npix = (long)B * g.T1 * g.F1;
+  for (long pix = (long)blockIdx.x * ppb + pl; pix < npix; pix += (long)gridDim.x * ppb) {
+    const int f1 = (int)(pix % g.F1);
+    const long bt = pix / g.F1;
+    const int t1 = (int)(bt % g.T1), b = (int)(bt / g.T1);
+    const float* xp = x + ((long)b * T + 2 * t1) * F + 2 * f1;
+    float xv[10];
+#pragma unroll
+    for (int kh = 0; kh < 3; ++kh)
+#pragma unroll
+      for (int kw = 0; kw < 3; ++kw) xv[kh * 3 + kw] = xp[kh * F + kw];
+    xv[9] = 1.f;
+    const TI* dp = dh + phase_row(g, b, t1, f1) * C + c0;
+    float d[8], lo[4], hi[4];
+    vld4(dp, lo);
+    vld4(dp + 4, hi);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) { d[k] = lo[k]; d[k + 4] = hi[k]; }
+#pragma unroll
+    for (int t = 0; t < 10; ++t)
+#pragma unroll
+      for (int k = 0; k < 8; ++k) acc[t][k] = fmaf(d[k], xv[t], acc[t][k]);
+  }
+  // combine the block's pixel lanes in fixed order: one (t, k) column at a time via LDS
+  for (int t = 0; t < 10; ++t) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      __syncthreads();
+      red[threadIdx.x] = acc[t][k];
+      __syncthreads();
+      if (pl == 0) {
+        float a = 0.f;
+        for (int q = 0; q < ppb; ++q) a += red[q * groups + cg];
+        part[(long)blockIdx.x * 10 * C + (long)t * C + c0 + k] = a;
+      }
+    }
+  }
+}
+
 // ---------------------------------------------------------------- dropout / cast / scale
 template <typename TI, typename TO>
 __global__ void scale_drop_kernel(long n, int cols, const TI* __restrict__ x, long ldx, TO* __restrict__ y, long ldy,
@@ -868,4 +978,59 @@ extern "C" int ea_argmax_rows(long rows, int V, const float* x, long ld, long lo
   hipLaunchKernelGGL(argmax_rows_kernel, dim3(ea_cdiv(rows, 4)), dim3(256), 0, (hipStream_t)stream, rows, V, x, ld, out);
   EA_LAUNCH_CHECK();
   return 0;
+}
+
+static PhaseGeo phase_geo(int B, int T1, int F1, int C) {
+  PhaseGeo g;
+  g.T1 = T1; g.F1 = F1;
+  g.nI0 = (T1 + 1) / 2; g.nI1 = T1 / 2; g.nJ0 = (F1 + 1) / 2; g.nJ1 = F1 / 2;
+  // plane offsets in ROWS (pixels); callers scale by C
+  g.plane[0] = 0;
+  g.plane[1] = (long)B * g.nI0 * g.nJ0;
+  g.plane[2] = g.plane[1] + (long)B * g.nI0 * g.nJ1;
+  g.plane[3] = g.plane[2] + (long)B * g.nI1 * g.nJ0;
+  return g;
+}
+
+extern "C" int ea_conv1_fwd(int B, int T, int F, int C, const float* x, const float* w, const float* bias,
+                            void* x1p, int dtype, void* stream) {
+  EA_ENTRY();
+  EA_CHECK_ARG(C % 8 == 0 && 256 % (C / 8) == 0 && T >= 3 && F >= 3);
+  const int T1 = (T - 3) / 2 + 1, F1 = (F - 3) / 2 + 1;
+  const PhaseGeo g = phase_geo(B, T1, F1, C);
+  const long npix = (long)B * T1 * F1;
+  const int ppb = 256 / (C / 8);
+  dim3 grid(ea_grid_cap(ea_cdiv(npix, ppb), 4096));
+  if (dtype == EA_BF16)
+    hipLaunchKernelGGL(conv1_fwd_kernel<bf16>, grid, dim3(256), 0, (hipStream_t)stream, B, T, F, g, C, x, w, bias,
+                       (bf16*)x1p);
+  else
+    hipLaunchKernelGGL(conv1_fwd_kernel<float>, grid, dim3(256), 0, (hipStream_t)stream, B, T, F, g, C, x, w, bias,
+                       (float*)x1p);
+  EA_LAUNCH_CHECK();
+  return 0;
+}
+
+extern "C" int ea_conv1_wgrad(int B, int T, int F, int C, const float* x, const void* dh, int dtype, float* dw,
+                              float* dbias, float* workspace, long ws_elems, void* stream) {
+  EA_ENTRY();
+  EA_CHECK_ARG(C % 8 == 0 && 256 % (C / 8) == 0 && T >= 3 && F >= 3);
+  const int T1 = (T - 3) / 2 + 1, F1 = (F - 3) / 2 + 1;
+  const PhaseGeo g = phase_geo(B, T1, F1, C);
+  const long npix = (long)B * T1 * F1;
+  const int ppb = 256 / (C / 8);
+  int nb = ea_grid_cap(ea_cdiv(npix, ppb * 16), 1024);
+  if ((long)nb > ws_elems / (10L * C)) nb = (int)(ws_elems / (10L * C));
+  EA_CHECK_ARG(nb >= 1);
+  hipStream_t st = (hipStream_t)stream;
+  if (dtype == EA_BF16)
+    hipLaunchKernelGGL(conv1_wgrad_kernel<bf16>, dim3(nb), dim3(256), 0, st, B, T, F, g, C, x, (const bf16*)dh, workspace);
+  else
+    hipLaunchKernelGGL(conv1_wgrad_kernel<float>, dim3(nb), dim3(256), 0, st, B, T, F, g, C, x, (const float*)dh,
+                       workspace);
+  EA_LAUNCH_CHECK();
+  // weight: partial column t*C + c -> dw[c*9 + t]; bias: columns 9C .. 10C-1
+  int rc = ea_reduce_partials_tr(nb, 9 * C, workspace, 10L * C, dw, 1, C, 9, stream);
+  if (rc) return rc;
+  return ea_reduce_partials(nb, C, workspace + 9L * C, 10L * C, dbias, 1, stream);
 }

@@ -41,6 +41,7 @@ struct GemmP {
   int bm, bn;        // output tile (LDS-DMA bf16 kernel: 64/128/256 x 128/256; else 128 x 128)
   const unsigned long long* salt;  // per-step dropout salt (device), see ea_set_rng_salt
   unsigned long long* stamp;       // kernel-span probe [first block start, last block end] or null
+  ea_conv_geo g;                   // implicit-GEMM operand geometry (g.mode 0: dense operands)
 };
 
 // In-kernel span probe (ea_gemm_set_probe): s_memrealtime is the GPU's constant 100 MHz
@@ -557,12 +558,37 @@ EA_DEV void epi_wave(const GemmP& p, char* smem, int z, int zb, int zh, int r0, 
   }
 }
 
+// ---------------------------------------------------------------- implicit-GEMM gathers
+// Conv2dSubsampling's conv2 (3x3, stride 2) over the phase-split conv1 output x1p: class
+// plane (a, e) holds pixels t1 = 2i + a, f1 = 2j + e as a dense [b][i][j][C] block, so
+// every tap of every output pixel is one contiguous C-row of one plane (see ea_conv_geo).
+EA_DEV int fdiv(int n, int d) {  // exact n / d for 0 <= n < 2^24 (float estimate + fix-up)
+  int q = (int)((float)n * __builtin_amdgcn_rcpf((float)d));
+  if (q * d > n) --q;
+  if ((q + 1) * d <= n) ++q;
+  return q;
+}
+// element offset of x1p[pixel (b, t2, f2) shifted by tap (kh, kw)] (conv2 input row)
+EA_DEV long x1p_row(const ea_conv_geo& g, int b, int t2, int f2, int kh, int kw) {
+  const int a = kh & 1, e = kw & 1;
+  return g.plane[a * 2 + e] + (((long)b * g.nI[a] + t2 + (kh >> 1)) * g.nJ[e] + f2 + (kw >> 1)) * g.C;
+}
+// DGRAD tap q of class (a, e): kh in {0,2} (a = 0) or {1}; kw likewise
+EA_DEV void dgrad_tap(const ea_conv_geo& g, int q, int& kh, int& kw) {
+  const int nkw = g.e ? 1 : 2;
+  const int qh = q / nkw, qw = q - qh * nkw;
+  kh = g.a ? 1 : 2 * qh;
+  kw = g.e ? 1 : 2 * qw;
+}
+
 // BM x BN output tile, 2 x WN wave64s, each (BM/2) x (BN/WN) = MI x NJ MFMA 16x16 blocks.
 // (BM, BN, WN) in {(64,128,2) K-major A only, (128,128,2), (256,128,2), (256,256,4)}.
 // Small wave tiles read the fragments of both k-steps up front (register double buffer);
 // 128-row wave tiles read one k-step at a time.
-template <int BM_, int BN_, int WN, bool AK, bool BKM, int STAGES>
+template <int BM_, int BN_, int WN, bool AK, bool BKM, int STAGES, int MODE = 0>
 __global__ __launch_bounds__(128 * WN, 1) void gemm_bf16_lds(GemmP p) {
+  static_assert(MODE == 0 || (MODE == EA_CONV_FWD && AK && BKM) || (MODE == EA_CONV_DGRAD && AK && !BKM) ||
+                (MODE == EA_CONV_WGRAD && !AK && !BKM), "conv gather layouts");
   constexpr int NW = 2 * WN, NTT = 64 * NW;
   static_assert(AK || BM_ >= 128, "MN-major A needs 128-wide panels");
   static_assert(BKM || BN_ >= 128, "MN-major B needs 128-wide panels");
@@ -624,19 +650,112 @@ __global__ __launch_bounds__(128 * WN, 1) void gemm_bf16_lds(GemmP p) {
   const long bstep = (BKM ? BK : (long)BK * p.ldb) * 2;
   constexpr int GPT = ACH + BCH;  // DMA instructions per thread per K-tile (vmcnt unit)
 
+  // gather modes.  A rows (FWD / DGRAD): each chunk's row decoded once; its source offset
+  // (elements, < 2^31) is rebuilt only when the K-tile enters a new tap, so a K-tile costs
+  // one add per chunk.  B rows (WGRAD, k = pixel): each chunk's pixel advances by 64 per
+  // K-tile with an incremental (b, t2, f2) carry instead of divisions.
+  int gb[ACH], gt[ACH], gf[ACH], cur[ACH];
+  const int ktg0 = kbeg / BK;  // global K-tile index of this split's first tile
+  const int CT = p.g.C / BK;   // K-tiles per tap (gather modes)
+  if constexpr (MODE == EA_CONV_FWD || MODE == EA_CONV_DGRAD) {
+    const int n2 = MODE == EA_CONV_FWD ? p.g.T2 : p.g.nI[p.g.a];
+    const int n3 = MODE == EA_CONV_FWD ? p.g.F2 : p.g.nJ[p.g.e];
+#pragma unroll
+    for (int i = 0; i < ACH; ++i) {
+      const int m = min(m0 + (((i * NW + w) * 64 + lane) >> 3), p.M - 1);
+      const int bt = fdiv(m, n3);
+      gf[i] = m - bt * n3;
+      gb[i] = fdiv(bt, n2);
+      gt[i] = bt - gb[i] * n2;
+      cur[i] = 0;
+    }
+  }
+  auto a_tap = [&](int q) {  // rebuild the A chunk offsets for tap q (FWD / DGRAD)
+#pragma unroll
+    for (int i = 0; i < ACH; ++i) {
+      const int ci = (i * NW + w) * 64 + lane;
+      const int cc = ((ci & 7) ^ swz_k(ci >> 3)) * 8;
+      if constexpr (MODE == EA_CONV_FWD) {
+        const int kh = q / 3, kw = q - 3 * (q / 3);
+        cur[i] = (int)x1p_row(p.g, gb[i], gt[i], gf[i], kh, kw) + cc;
+      } else {
+        int kh, kw;
+        dgrad_tap(p.g, q, kh, kw);
+        const int t2 = gt[i] - (kh >> 1), f2 = gf[i] - (kw >> 1);  // t1 = 2*t2 + kh
+        cur[i] = (t2 >= 0 && t2 < p.g.T2 && f2 >= 0 && f2 < p.g.F2)
+                     ? ((gb[i] * p.g.T2 + t2) * p.g.F2 + f2) * p.g.C + cc
+                     : (int)p.g.zero + (i * 8 + lane / 8) % 64 * p.g.C + cc;  // spread over 64 zero rows
+      }
+    }
+  };
+  // WGRAD B chunks: fixed column (tap, ci) per chunk, pixel state advanced per K-tile
+  int wb[BCH], wt[BCH], wf[BCH], wpix[BCH], wbase[BCH], wnI[BCH], wnJ[BCH];
+  if constexpr (MODE == EA_CONV_WGRAD) {
+#pragma unroll
+    for (int i = 0; i < BCH; ++i) {
+      const int ci = (i * NW + w) * 64 + lane;
+      const int pnl = ci >> 10, cj = ci & 1023, k = cj >> 4, c = (cj & 15) ^ swz_mn_bf16(k);
+      const int n = min(n0 + pnl * 128 + c * 8, p.N - 8);
+      const int tap = n / p.g.C, cin = n - tap * p.g.C;
+      const int kh = tap / 3, kw = tap - 3 * kh, a = kh & 1, e = kw & 1;
+      wnI[i] = p.g.nI[a];
+      wnJ[i] = p.g.nJ[e];
+      // row (b*nI + t2 + kh/2)*nJ + f2 + kw/2 of plane (a, e): fold the tap shift into the base
+      wbase[i] = (int)p.g.plane[a * 2 + e] + ((kh >> 1) * wnJ[i] + (kw >> 1)) * p.g.C + cin;
+      const int pix = ktg0 * BK + k;
+      wpix[i] = pix;
+      const int bt = fdiv(pix, p.g.F2);
+      wf[i] = pix - bt * p.g.F2;
+      wb[i] = fdiv(bt, p.g.T2);
+      wt[i] = bt - wb[i] * p.g.T2;
+    }
+  }
+  const int dF = BK % max(p.g.F2, 1), dT = BK / max(p.g.F2, 1);
+
   auto issue = [&](int kt, int stg) {
     char* base = smem + stg * STAGE_BYTES;
     const char* ak = abase + kt * astep;
     const char* bk = bbase + kt * bstep;
+    if constexpr (MODE == EA_CONV_FWD || MODE == EA_CONV_DGRAD) {
+      const int ktg = ktg0 + kt, q = ktg / CT, c0 = (ktg - q * CT) * BK;
+      if (c0 == 0 || kt == 0) a_tap(q);
 #pragma unroll
-    for (int i = 0; i < ACH; ++i)
-      __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)(ak + aoff[i]),
-                                       (__attribute__((address_space(3))) void*)(base + (i * NW + w) * 1024), 16, 0, 0);
+      for (int i = 0; i < ACH; ++i)
+        __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)((const char*)A + (long)(cur[i] + c0) * 2),
+                                         (__attribute__((address_space(3))) void*)(base + (i * NW + w) * 1024), 16, 0, 0);
+      if constexpr (MODE == EA_CONV_DGRAD) {  // W2t [9][co][ci]: k-tile = 64 co of one tap
+        int kh, kw;
+        dgrad_tap(p.g, q, kh, kw);
+        bk = (const char*)(B + ((long)(kh * 3 + kw) * p.g.C + c0) * p.g.C);
+      }
+    } else {
 #pragma unroll
-    for (int i = 0; i < BCH; ++i)
-      __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)(bk + boff[i]),
-                                       (__attribute__((address_space(3))) void*)(base + A_BYTES + (i * NW + w) * 1024),
-                                       16, 0, 0);
+      for (int i = 0; i < ACH; ++i)
+        __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)(ak + aoff[i]),
+                                         (__attribute__((address_space(3))) void*)(base + (i * NW + w) * 1024), 16, 0, 0);
+    }
+    if constexpr (MODE == EA_CONV_WGRAD) {  // B[k = pixel][n = (tap, ci)] gathered from x1p
+#pragma unroll
+      for (int i = 0; i < BCH; ++i) {
+        const int off = wpix[i] < p.g.P ? wbase[i] + ((wb[i] * wnI[i] + wt[i]) * wnJ[i] + wf[i]) * p.g.C
+                                        : (int)p.g.zero + (lane & 63) * p.g.C + (wbase[i] % p.g.C);
+        __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)((const char*)B + (long)off * 2),
+                                         (__attribute__((address_space(3))) void*)(base + A_BYTES + (i * NW + w) * 1024),
+                                         16, 0, 0);
+        // advance this chunk's pixel by one K-tile (64 pixels)
+        wpix[i] += BK;
+        wf[i] += dF;
+        wt[i] += dT;
+        if (wf[i] >= p.g.F2) { wf[i] -= p.g.F2; ++wt[i]; }
+        while (wt[i] >= p.g.T2) { wt[i] -= p.g.T2; ++wb[i]; }
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < BCH; ++i)
+        __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)(bk + boff[i]),
+                                         (__attribute__((address_space(3))) void*)(base + A_BYTES + (i * NW + w) * 1024),
+                                         16, 0, 0);
+    }
   };
 
   f32x4 acc[MI][NJ];
@@ -756,6 +875,21 @@ int g_gemm_bm64 = 1;  // LDS ring depth of gemm_bf16_lds (2: 64 KiB, 2 blocks/CU
 
 int launch_lds(GemmP& p, int a_k, int b_k, int nz, hipStream_t st) {
   dim3 grid(p.tiles_m * p.tiles_n, 1, nz * p.splitk);
+  if (p.g.mode != 0) {  // implicit-GEMM conv2 modes: fixed layouts, 128x128 or 256x256 tiles
+#define EA_GC(BMV, BNV, AKV, BKV, MD) \
+  hipLaunchKernelGGL((gemm_bf16_lds<BMV, BNV, (BNV == 256 ? 4 : 2), AKV, BKV, 2, MD>), grid, dim3(BNV == 256 ? 512 : 256), 0, st, p)
+    const bool big = p.bm == 256;
+    if (p.g.mode == EA_CONV_FWD) {
+      if (big) EA_GC(256, 256, true, true, EA_CONV_FWD); else EA_GC(128, 128, true, true, EA_CONV_FWD);
+    } else if (p.g.mode == EA_CONV_DGRAD) {
+      if (big) EA_GC(256, 256, true, false, EA_CONV_DGRAD); else EA_GC(128, 128, true, false, EA_CONV_DGRAD);
+    } else {
+      if (big) EA_GC(256, 256, false, false, EA_CONV_WGRAD); else EA_GC(128, 128, false, false, EA_CONV_WGRAD);
+    }
+#undef EA_GC
+    EA_LAUNCH_CHECK();
+    return 0;
+  }
 #define EA_GL(BMV, BNV, AKV, BKV, S) \
   hipLaunchKernelGGL((gemm_bf16_lds<BMV, BNV, (BNV == 256 ? 4 : 2), AKV, BKV, S>), grid, dim3(BNV == 256 ? 512 : 256), 0, st, p)
 #define EA_GL4(BMV, BNV, S)                            \
@@ -873,13 +1007,13 @@ extern "C" int ea_gemm_set_tile(int bm, int bn) {
   return 0;
 }
 
-extern "C" int ea_gemm(int dtype, int a_kmajor, int b_kmajor, int M, int N, int K,
-                       const void* A, long lda, long sAb, long sAh,
-                       const void* B, long ldb, long sBb, long sBh,
-                       int batch, int nh,
-                       void* C, int c_dtype, long ldc, long sCb, long sCh,
-                       const ea_epilogue* epi, float* workspace, long ws_elems, void* stream) {
-  EA_ENTRY();
+static int gemm_impl(int dtype, int a_kmajor, int b_kmajor, int M, int N, int K,
+                     const void* A, long lda, long sAb, long sAh,
+                     const void* B, long ldb, long sBb, long sBh,
+                     int batch, int nh,
+                     void* C, int c_dtype, long ldc, long sCb, long sCh,
+                     const ea_epilogue* epi, float* workspace, long ws_elems, void* stream,
+                     const ea_conv_geo* geo) {
   EA_CHECK_ARG(epi != nullptr && M >= 0 && N >= 0 && K >= 0 && batch >= 1 && nh >= 1);
   EA_CHECK_ARG(dtype == EA_F32 || dtype == EA_BF16);
   if (M == 0 || N == 0) return 0;
@@ -897,6 +1031,7 @@ extern "C" int ea_gemm(int dtype, int a_kmajor, int b_kmajor, int M, int N, int 
   p.ws = workspace;
   p.salt = ea_g_rng_salt;
   p.stamp = g_probe;
+  p.g = geo ? *geo : ea_conv_geo{};
   // unaligned operands (odd vocab / leading dims) take the element-wise load path
   p.vec_a = (lda % E == 0 && sAb % E == 0 && sAh % E == 0 && ((uintptr_t)A % 16) == 0);
   p.vec_b = (ldb % E == 0 && sBb % E == 0 && sBh % E == 0 && ((uintptr_t)B % 16) == 0);
@@ -915,7 +1050,16 @@ extern "C" int ea_gemm(int dtype, int a_kmajor, int b_kmajor, int M, int N, int 
   const bool lds_path = dtype == EA_BF16 && p.vec_a && p.vec_b && g_gemm_stages > 0 &&
                         a_ext < 4.0e9 && b_ext < 4.0e9;
   p.lds = lds_path;
-  if (lds_path) choose_tile(p, a_kmajor, (long)batch * nh);
+  if (geo && geo->mode != 0) {
+    // gather modes: LDS-DMA path only, K a whole number of 64-deep tiles within taps
+    if (!lds_path || K % 64 != 0 || geo->C % 64 != 0 || batch * nh != 1) return EA_ERR_BAD_ARG;
+    if ((geo->mode == EA_CONV_WGRAD) == (a_kmajor != 0) || (geo->mode == EA_CONV_FWD) != (b_kmajor != 0))
+      return EA_ERR_BAD_ARG;
+    choose_tile(p, 0, 1);
+    if (p.bm != 256 || p.bn != 256) { p.bm = 128; p.bn = 128; }
+  } else if (lds_path) {
+    choose_tile(p, a_kmajor, (long)batch * nh);
+  }
   if (p.bm == 64 && !a_kmajor) return EA_ERR_BAD_ARG;
   p.tiles_m = ea_cdiv(M, p.bm);
   p.tiles_n = ea_cdiv(N, p.bn);
@@ -950,4 +1094,24 @@ extern "C" int ea_gemm(int dtype, int a_kmajor, int b_kmajor, int M, int N, int 
     EA_LAUNCH_CHECK();
   }
   return 0;
+}
+
+extern "C" int ea_gemm(int dtype, int a_kmajor, int b_kmajor, int M, int N, int K,
+                       const void* A, long lda, long sAb, long sAh,
+                       const void* B, long ldb, long sBb, long sBh,
+                       int batch, int nh,
+                       void* C, int c_dtype, long ldc, long sCb, long sCh,
+                       const ea_epilogue* epi, float* workspace, long ws_elems, void* stream) {
+  EA_ENTRY();
+  return gemm_impl(dtype, a_kmajor, b_kmajor, M, N, K, A, lda, sAb, sAh, B, ldb, sBb, sBh, batch, nh, C, c_dtype,
+                   ldc, sCb, sCh, epi, workspace, ws_elems, stream, nullptr);
+}
+
+extern "C" int ea_gemm_conv(const ea_conv_geo* geo, int a_kmajor, int b_kmajor, int M, int N, int K,
+                            const void* A, long lda, const void* B, long ldb, void* C, int c_dtype, long ldc,
+                            const ea_epilogue* epi, float* workspace, long ws_elems, void* stream) {
+  EA_ENTRY();
+  EA_CHECK_ARG(geo != nullptr && geo->mode >= EA_CONV_FWD && geo->mode <= EA_CONV_WGRAD);
+  return gemm_impl(EA_BF16, a_kmajor, b_kmajor, M, N, K, A, lda, 0, 0, B, ldb, 0, 0, 1, 1, C, c_dtype, ldc, 0, 0,
+                   epi, workspace, ws_elems, stream, geo);
 }

@@ -39,6 +39,14 @@ class Epilogue(ctypes.Structure):
 
 
 SCHED_CONSTANT, SCHED_WARMUP = 0, 1
+CONV_FWD, CONV_DGRAD, CONV_WGRAD = 1, 2, 3
+
+
+class ConvGeo(ctypes.Structure):
+    """ea_conv_geo: phase-split implicit-GEMM geometry of the subsampling conv2."""
+    _fields_ = [("mode", ctypes.c_int), ("B", ctypes.c_int), ("T2", ctypes.c_int), ("F2", ctypes.c_int),
+                ("C", ctypes.c_int), ("P", ctypes.c_int), ("nI", ctypes.c_int * 2), ("nJ", ctypes.c_int * 2),
+                ("a", ctypes.c_int), ("e", ctypes.c_int), ("plane", ctypes.c_long * 4), ("zero", ctypes.c_long)]
 
 
 class LrSchedule(ctypes.Structure):

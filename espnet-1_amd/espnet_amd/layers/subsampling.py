@@ -11,12 +11,36 @@ the (t, f*C + c) order directly — its weight (d, C, F'') is repacked to (d, F'
 """
 from __future__ import annotations
 
+import ctypes
 import math
 
 import torch
 from torch import nn
 
+from .._lib import CONV_DGRAD, CONV_FWD, CONV_WGRAD, ConvGeo
 from .common import (ACT_RELU, EPI_ACT, EPI_DACT, EPI_STORE, F32, Bound, empty, lib, ops, rup)
+
+
+def phase_geo(B, T1, F1, T2, F2, C, mode, a=0, e=0, zero=0):
+    """ea_conv_geo of the phase-split conv1 output x1p (include/espnet_amd.h): class plane
+    (a, e) holds pixels t1 = 2i+a, f1 = 2j+e as [b][i][j][C]."""
+    g = ConvGeo()
+    g.mode, g.B, g.T2, g.F2, g.C, g.P = mode, B, T2, F2, C, B * T2 * F2
+    nI = ((T1 + 1) // 2, T1 // 2)
+    nJ = ((F1 + 1) // 2, F1 // 2)
+    g.nI[0], g.nI[1] = nI
+    g.nJ[0], g.nJ[1] = nJ
+    rows = [B * nI[0] * nJ[0], B * nI[0] * nJ[1], B * nI[1] * nJ[0], B * nI[1] * nJ[1]]
+    off = 0
+    for i in range(4):
+        g.plane[i] = off * C
+        off += rows[i]
+    g.a, g.e, g.zero = a, e, zero
+    return g, nI, nJ, rows
+
+
+def _implicit_ok(cd, C):
+    return cd == torch.bfloat16 and C % 64 == 0 and 256 % (C // 8) == 0
 
 
 def rel_pos_table(n, d):
@@ -91,6 +115,9 @@ class SubsampleFn(torch.autograd.Function):
         T2, F2 = (T1 - 3) // 2 + 1, (F1 - 3) // 2 + 1
         dev = feats.device
         pe = m.out[1]
+        if _implicit_ok(cd, C):
+            return SubsampleFn._forward_implicit(ctx, feats, m, seed, training, B, T, Fin, C, T1, F1, T2, F2)
+        ctx.implicit = False
         # conv1: im2col (P1 x 16) . W1p^T -> relu -> x1 (B,T1,F1,C)
         P1 = B * T1 * F1
         col1 = empty(P1, 16, dtype=cd, device=dev)
@@ -126,7 +153,109 @@ class SubsampleFn(torch.autograd.Function):
         return y.view(B, T2, C)
 
     @staticmethod
+    def _forward_implicit(ctx, feats, m, seed, training, B, T, Fin, C, T1, F1, T2, F2):
+        """bf16 path: conv1 direct into the phase-split x1p, conv2 as an implicit GEMM
+        gathering x1p rows (ea_gemm_conv EA_CONV_FWD) — no im2col buffers."""
+        b = m._b
+        cd = b.cd
+        dev = feats.device
+        pe = m.out[1]
+        P1, P2 = B * T1 * F1, B * T2 * F2
+        x1p = empty(P1 + 64, C, dtype=cd, device=dev)  # + 64 zero rows (wgrad gather padding)
+        x1p[P1:].zero_()
+        lib.ea_conv1_fwd(B, T, Fin, C, feats.data_ptr(), b.f("conv.0.weight").data_ptr(),
+                         b.f("conv.0.bias").data_ptr(), x1p.data_ptr(), ops.dt(x1p), ops.stream())
+        w2 = empty(C, 9 * C, dtype=cd, device=dev)
+        ops.permute3(b.f("conv.2.weight"), w2, C, C, 9)  # (Co,Ci,9) -> (Co,9,Ci)
+        x2 = empty(P2, C, dtype=cd, device=dev)
+        geo, _, _, _ = phase_geo(B, T1, F1, T2, F2, C, CONV_FWD)
+        probe = ops.PROBE
+        if probe is not None:
+            probe.begin("conv2_gemm")
+        epi = ops.make_epi(EPI_ACT, bias=b.f("conv.2.bias"), act=ACT_RELU)
+        ws = ops.workspace(ops._SPLITK_WS, dev)
+        lib.ea_gemm_conv(ctypes.byref(geo), 1, 1, P2, C, 9 * C, x1p.data_ptr(), C, w2.data_ptr(), 9 * C,
+                         x2.data_ptr(), ops.dt(x2), C, ctypes.byref(epi), ws.data_ptr(), ws.numel(), ops.stream())
+        if probe is not None:
+            probe.end("conv2_gemm")
+        wl = empty(C, F2 * C, dtype=cd, device=dev)
+        ops.permute3(b.f("out.0.weight"), wl, C, C, F2)  # (d, C, F2) -> (d, F2, C)
+        y = empty(B * T2, C, device=dev)
+        p = pe.dropout_rate if training else 0.0
+        ops.linear(x2.view(B * T2, F2 * C), wl, y,
+                   epi=ops.make_epi(bias=b.f("out.0.bias"), post_scale=pe.xscale, drop_p=p, seed=seed))
+        ctx.m = m
+        ctx.implicit = True
+        ctx.meta = (B, T, Fin, T1, F1, T2, F2, p, seed)
+        ctx.save = (feats, x1p, w2, x2, wl)
+        return y.view(B, T2, C)
+
+    @staticmethod
+    def _backward_implicit(ctx, dy):
+        m = ctx.m
+        b = m._b
+        cd = b.cd
+        B, T, Fin, T1, F1, T2, F2, p, seed = ctx.meta
+        feats, x1p, w2, x2, wl = ctx.save
+        ctx.save = None
+        C = m.odim
+        dev = dy.device
+        P1, P2 = B * T1 * F1, B * T2 * F2
+        dv = empty(B * T2, C, dtype=cd, device=dev)
+        ops.scale_dropout(dy.reshape(B * T2, C).contiguous(), dv, scale=m.out[1].xscale, p=p, seed=seed)
+        x2r = x2.view(B * T2, F2 * C)
+        with ops.wgrad(dv, x2):
+            ops.colsum(dv, b.g("out.0.bias"))
+            dwl = empty(C, F2 * C, device=dev)
+            ops.linear_dw(dv, x2r, dwl, accumulate=False)
+            ops.permute3(dwl, b.g("out.0.weight"), C, F2, C, accumulate=True)  # (d,F2,C) -> (d,C,F2)
+        # dY2 (relu-masked) with >= 64 zero rows after P2: the wgrad K padding and the dgrad
+        # gather's off-grid rows
+        K2 = rup(P2, 64)
+        dx2 = empty(P2 + 128, C, dtype=cd, device=dev)
+        dx2[P2:].zero_()
+        ops.linear_dx(dv, wl, dx2[:P2].view(B * T2, F2 * C), epi=ops.make_epi(EPI_DACT, act=ACT_RELU, aux=x2r))
+        ws_side = None
+        with ops.wgrad(dx2, x1p):
+            ops.colsum(dx2[:P2], b.g("conv.2.bias"))
+            dw2 = empty(C, 9 * C, device=dev)
+            geo, _, _, _ = phase_geo(B, T1, F1, T2, F2, C, CONV_WGRAD, zero=P1 * C)
+            epi = ops.make_epi()
+            ws_side = ops.workspace(ops._SPLITK_WS, dev)
+            lib.ea_gemm_conv(ctypes.byref(geo), 0, 0, C, 9 * C, K2, dx2.data_ptr(), C, x1p.data_ptr(), C,
+                             dw2.data_ptr(), ops.dt(dw2), 9 * C, ctypes.byref(epi), ws_side.data_ptr(),
+                             ws_side.numel(), ops.stream())
+            ops.permute3(dw2, b.g("conv.2.weight"), C, 9, C, accumulate=True)  # (Co,9,Ci) -> (Co,Ci,9)
+        # input gradient per parity class (a, e): sub-pixel decomposition of the transposed
+        # conv, ReLU mask of conv1 fused (DACT with aux = x1p)
+        dx1p = empty(P1, C, dtype=cd, device=dev)
+        ws = ops.workspace(ops._SPLITK_WS, dev)
+        w2t = empty(9, C, C, dtype=cd, device=dev)  # tap-major: every tap's (co, ci) block dense
+        ops.permute3(b.f("conv.2.weight"), w2t, 1, C * C, 9)  # (Co,Ci,9) -> (9,Co,Ci)
+        for a in (0, 1):
+            for e in (0, 1):
+                geo, nI, nJ, rows = phase_geo(B, T1, F1, T2, F2, C, CONV_DGRAD, a=a, e=e, zero=P2 * C)
+                Mc = rows[a * 2 + e]
+                if Mc == 0:
+                    continue
+                ntaps = (1 if a else 2) * (1 if e else 2)
+                o = geo.plane[a * 2 + e] // C
+                aux = x1p[o:o + Mc]
+                epi = ops.make_epi(EPI_DACT, act=ACT_RELU, aux=aux)
+                lib.ea_gemm_conv(ctypes.byref(geo), 1, 0, Mc, C, ntaps * C, dx2.data_ptr(), C, w2t.data_ptr(),
+                                 C, dx1p[o:o + Mc].data_ptr(), ops.dt(dx1p), C, ctypes.byref(epi),
+                                 ws.data_ptr(), ws.numel(), ops.stream())
+        with ops.wgrad(dx1p, feats):
+            w, wn = ops._ws(dev, 1024 * 10 * C)
+            lib.ea_conv1_wgrad(B, T, Fin, C, feats.data_ptr(), dx1p.data_ptr(), ops.dt(dx1p),
+                               b.g("conv.0.weight").data_ptr(), b.g("conv.0.bias").data_ptr(), w, wn, ops.stream())
+        ops.grad_ready(b)
+        return None, None, None, None, None
+
+    @staticmethod
     def backward(ctx, dy):
+        if ctx.implicit:
+            return SubsampleFn._backward_implicit(ctx, dy)
         m = ctx.m
         b = m._b
         cd = b.cd

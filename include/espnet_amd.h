@@ -66,6 +66,37 @@ int ea_gemm(int dtype, int a_kmajor, int b_kmajor, int M, int N, int K,
             const ea_epilogue* epi, float* workspace, long ws_elems, void* stream);
 
 
+/* Implicit GEMMs of Conv2dSubsampling's second Conv2d(C, C, 3, stride 2) (subsampling.py:
+ * 60-65) over a phase-split conv1 output x1p: class plane (a, e) = pixels t1 = 2i+a,
+ * f1 = 2j+e stored dense as [b][i][j][C] (dims nI[a] x nJ[e]) at element offset
+ * plane[a*2+e].  Every tap of every conv2 pixel is then one contiguous C-row, gathered by
+ * the LDS-DMA loader (no im2col buffer):
+ *  EA_CONV_FWD  : A[m = (b,t2,f2)][k = (kh,kw,c)] = x1p row; B = W2p [Co][9*C] K-major
+ *                 (a_kmajor = b_kmajor = 1); out (P, Co).
+ *  EA_CONV_DGRAD: input gradient for one parity class (a, e) (sub-pixel decomposition of the
+ *                 transposed conv): A[m = (b,i,j)][k = (tap of class, co)] = dY2 row of
+ *                 (t2, f2) = ((2i+a-kh)/2, (2j+e-kw)/2), or one of 64 zero rows at `zero`
+ *                 (element offset from A; 64*C zeros: spread so off-grid reads do not all
+ *                 hit one L2 channel) off the grid; B = W2t [9][co][ci] (tap-major) N-major
+ *                 (b_kmajor = 0, ldb = C); out = the class plane of dx1p (M = B*nI*nJ).
+ *  EA_CONV_WGRAD: weight gradient: A = dY2 (P x Co) read M-major (a_kmajor = 0, lda = Co),
+ *                 B[k = pixel][n = (tap, ci)] = x1p row gathered (b_kmajor = 0); K = P
+ *                 rounded up to 64 with dY2 rows P..K-1 zero and 64 zero rows of x1p at `zero`.
+ * bf16 operands only; C % 64 == 0; K % 64 == 0.  Replaces the im2col + GEMM + col2im of the
+ * channel-last conv2 (and torch's cudnn/miopen conv) on the AMP path. */
+enum { EA_CONV_FWD = 1, EA_CONV_DGRAD = 2, EA_CONV_WGRAD = 3 };
+typedef struct ea_conv_geo {
+  int mode;              /* EA_CONV_* */
+  int B, T2, F2, C, P;   /* conv2 output grid (P = B*T2*F2 pixels), channels */
+  int nI[2], nJ[2];      /* class-plane dims: nI[a] = (T1 - a + 1) / 2, nJ[e] = (F1 - e + 1) / 2 */
+  int a, e;              /* DGRAD: the parity class */
+  long plane[4];         /* element offsets of the 4 class planes in x1p */
+  long zero;             /* element offset of 64 zero rows (64*C) in the gathered operand */
+} ea_conv_geo;
+int ea_gemm_conv(const ea_conv_geo* geo, int a_kmajor, int b_kmajor, int M, int N, int K,
+                 const void* A, long lda, const void* B, long ldb, void* C, int c_dtype, long ldc,
+                 const ea_epilogue* epi, float* workspace, long ws_elems, void* stream);
+
 /* Select the bf16 GEMM main loop: 2 or 3 = LDS-DMA (global_load_lds) ring of that depth
  * (default 2), 0 = register-staged loop; 12/13 = same ring without 64-row tiles.
  * Process-wide; for A/B measurements. */
@@ -163,6 +194,16 @@ int ea_im2col_conv1(int B, int T, int F, const float* x, void* col, int col_dtyp
 int ea_im2col_conv2(int B, int T1, int F1, int C, const void* x1, void* col, int dtype, void* stream);
 int ea_col2im_conv2(int B, int T1, int F1, int C, const void* dcol, int dcol_dtype, const void* x1,
                     void* dx1, int dtype, void* stream);
+
+/* conv1 of Conv2dSubsampling (Conv2d(1, C, 3, stride 2) + ReLU, subsampling.py:60-61) as a
+ * direct kernel writing the phase-split layout of ea_conv_geo (x1p, B*T1*F1 rows of C);
+ * w (C, 9) f32.  ea_conv1_wgrad: dw[c*9 + t] += sum_p dh[p,c] x_t(p), dbias[c] += sum_p
+ * dh[p,c] from the phase-split pre-activation gradient dh (deterministic block partials;
+ * workspace >= 10*C floats per block, up to 1024 blocks). */
+int ea_conv1_fwd(int B, int T, int F, int C, const float* x, const float* w, const float* bias,
+                 void* x1p, int dtype, void* stream);
+int ea_conv1_wgrad(int B, int T, int F, int C, const float* x, const void* dh, int dtype, float* dw,
+                   float* dbias, float* workspace, long ws_elems, void* stream);
 
 /* GLU over channels (conformer/convolution.py:72): y = x[:, :C] * sigmoid(x[:, C:]). */
 int ea_glu_fwd(long rows, int C, const void* x, int x_dtype, void* y, int y_dtype, void* stream);
