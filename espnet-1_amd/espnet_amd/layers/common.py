@@ -8,6 +8,7 @@ Only activations flow through autograd, so a whole training step is ~25 autograd
 from __future__ import annotations
 
 import math
+import os
 
 import torch
 
@@ -17,7 +18,7 @@ from .._lib import (ACT_NONE, ACT_RELU, ACT_SWISH, EPI_ACT, EPI_DACT, EPI_RESID,
 
 __all__ = ["Bound", "rup", "empty", "ops", "lib", "EPI_ACT", "EPI_DACT", "EPI_RESID",
            "EPI_STORE", "ACT_NONE", "ACT_RELU", "ACT_SWISH", "site_seed", "attn_fwd", "attn_bwd",
-           "LayerNormFn", "ln_fwd", "ln_bwd", "math", "F32"]
+           "LayerNormFn", "ln_fwd", "ln_bwd", "math", "F32", "fused_attn_ok"]
 
 F32 = torch.float32
 
@@ -30,6 +31,15 @@ def empty(*shape, dtype=F32, device="cuda"):
     if len(shape) == 1 and isinstance(shape[0], (tuple, list, torch.Size)):
         shape = tuple(shape[0])
     return torch.empty(shape, dtype=dtype, device=device)
+
+
+FUSED_ATTN = os.environ.get("EA_FUSED_ATTN", "1") != "0"
+
+
+def fused_attn_ok(cd, dk, T1, T2) -> bool:
+    """The fused attention kernels (relattn.hip) take bf16 operands, head dim 64 and (for the
+    backward's key-per-wave split) at most 256 keys; other cases use the unfused path."""
+    return FUSED_ATTN and cd == torch.bfloat16 and dk == 64 and T2 <= 256 and T1 >= 1
 
 
 def site_seed(base: int, layer: int, site: int) -> int:

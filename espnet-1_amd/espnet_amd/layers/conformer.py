@@ -15,7 +15,7 @@ from __future__ import annotations
 import torch
 from torch import nn
 
-from .common import (ACT_SWISH, EPI_ACT, EPI_DACT, EPI_RESID, EPI_STORE, F32, Bound, attn_bwd,
+from .common import (ACT_SWISH, EPI_ACT, EPI_DACT, EPI_RESID, EPI_STORE, F32, Bound, attn_bwd, fused_attn_ok,
                      attn_fwd, empty, lib, ln_bwd, ln_fwd, math, ops, rup, site_seed)
 
 
@@ -187,20 +187,32 @@ class ConformerBlockFn(torch.autograd.Function):
                                              A + "linear_v.bias", shape=(3 * d,))))
         pp = empty(P2, d, dtype=cd, device=dev)
         ops.linear(pos, b.w(A + "linear_pos.weight"), pp)
-        qu = empty(N, d, dtype=cd, device=dev)
-        qv = empty(N, d, dtype=cd, device=dev)
-        lib.ea_add_pos_bias(N, H, dk, qkv.data_ptr(), 3 * d, b.f(A + "pos_bias_u").data_ptr(),
-                            b.f(A + "pos_bias_v").data_ptr(), qu.data_ptr(), qv.data_ptr(),
-                            ops.dt(qu), ops.stream())
-        ldbd = rup(P2, 8)
-        bd = empty(H * B * T * ldbd, device=dev)
-        ops.gemm(qv, pp, bd, M=T, N=P2, K=dk, a_kmajor=1, b_kmajor=1, lda=d, ldb=d, ldc=ldbd,
-                 batch=B, nh=H, sA=(T * d, dk), sB=(0, dk), sC=(T * ldbd, B * T * ldbd), splitk=False)
         scale = 1.0 / math.sqrt(dk)
-        O, P, Pd, ldT = attn_fwd(qu, qkv[:, d:], qkv[:, 2 * d:], B=B, H=H, T1=T, T2=T, dk=dk,
-                                 ldq=d, ldk=3 * d, ldv=3 * d, klen=olens, causal=False, scale=scale,
-                                 p=pa, seed=sd(3), cd=cd, bd=bd, ldbd=ldbd)
-        del bd
+        if fused_attn_ok(cd, dk, T, T):
+            # one kernel: (q+u)k^T + rel_shift((q+v)p^T), mask, softmax, dropout, @v
+            O = empty(N, d, dtype=cd, device=dev)
+            lse = empty(B * H * T, device=dev)
+            lib.ea_attn_fused_fwd(B, H, T, T, dk, qkv.data_ptr(), 3 * d, qkv[:, d:].data_ptr(), 3 * d,
+                                  qkv[:, 2 * d:].data_ptr(), 3 * d, b.f(A + "pos_bias_u").data_ptr(),
+                                  b.f(A + "pos_bias_v").data_ptr(), pp.data_ptr(), d, olens.data_ptr(), 0,
+                                  scale, float(pa), sd(3), O.data_ptr(), d, lse.data_ptr(), ops.stream())
+            ldT = 0
+            s_core = ("fused", lse)
+        else:
+            qu = empty(N, d, dtype=cd, device=dev)
+            qv = empty(N, d, dtype=cd, device=dev)
+            lib.ea_add_pos_bias(N, H, dk, qkv.data_ptr(), 3 * d, b.f(A + "pos_bias_u").data_ptr(),
+                                b.f(A + "pos_bias_v").data_ptr(), qu.data_ptr(), qv.data_ptr(),
+                                ops.dt(qu), ops.stream())
+            ldbd = rup(P2, 8)
+            bd = empty(H * B * T * ldbd, device=dev)
+            ops.gemm(qv, pp, bd, M=T, N=P2, K=dk, a_kmajor=1, b_kmajor=1, lda=d, ldb=d, ldc=ldbd,
+                     batch=B, nh=H, sA=(T * d, dk), sB=(0, dk), sC=(T * ldbd, B * T * ldbd), splitk=False)
+            O, P, Pd, ldT = attn_fwd(qu, qkv[:, d:], qkv[:, 2 * d:], B=B, H=H, T1=T, T2=T, dk=dk,
+                                     ldq=d, ldk=3 * d, ldv=3 * d, klen=olens, causal=False, scale=scale,
+                                     p=pa, seed=sd(3), cd=cd, bd=bd, ldbd=ldbd)
+            del bd
+            s_core = ("unfused", qu, qv, P, Pd)
         x2 = empty(N, d, device=dev)
         ops.linear(O, b.w(A + "linear_out.weight"), x2,
                    epi=ops.make_epi(EPI_RESID, bias=b.f(A + "linear_out.bias"), resid=x1,
@@ -233,7 +245,7 @@ class ConformerBlockFn(torch.autograd.Function):
         out, mu5, rs5 = ln_fwd(x4, b, "norm_final", F32)
         ctx.L = L
         ctx.meta = (B, T, d, H, dk, p, pa, seed, scale, ldT)
-        ctx.save = (x0, x1, x2, x3, x4, s_ff1, (xn2, mu2, rs2, qkv, pp, qu, qv, O, P, Pd),
+        ctx.save = (x0, x1, x2, x3, x4, s_ff1, (xn2, mu2, rs2, qkv, pp, O, s_core),
                     (xn3, mu3, rs3, g2, glu, y, z, bn_mean, bn_rstd), s_ff2, (mu5, rs5), pos, olens)
         return out.view(B, T, d)
 
@@ -283,7 +295,7 @@ class ConformerBlockFn(torch.autograd.Function):
         ln_bwd(dxn3, x2, b, "norm_conv", mu3, rs3, dx, accumulate=True)
         # ---- rel-pos MHSA
         A = "self_attn."
-        xn2, mu2, rs2, qkv, pp, qu, qv, O, P, Pd = s_att
+        xn2, mu2, rs2, qkv, pp, O, s_core = s_att
         dv = empty(N, d, dtype=cd, device=dev)
         ops.scale_dropout(dx, dv, p=p, seed=sd(4))
         with ops.wgrad(dv, O):
@@ -293,11 +305,26 @@ class ConformerBlockFn(torch.autograd.Function):
         ops.linear_dx(dv, b.w(A + "linear_out.weight"), dO)
         dqkv = empty(N, 3 * d, dtype=cd, device=dev)
         ldbd = rup(P2, 8)
-        dbd = empty(H * B * T * ldbd, dtype=cd, device=dev)
-        attn_bwd(dO, qu, qkv[:, d:], qkv[:, 2 * d:], P, Pd, ldT, B=B, H=H, T1=T, T2=T, dk=dk,
-                 ldq=d, ldk=3 * d, ldv=3 * d, scale=scale, p=pa, seed=sd(3), cd=cd,
-                 dq=dqkv, lddq=3 * d, dk_=dqkv[:, d:], lddk=3 * d, dv=dqkv[:, 2 * d:], lddv=3 * d,
-                 dbd=dbd, ldbd=ldbd)
+        if s_core[0] == "fused":
+            lse = s_core[1]
+            dbd = torch.zeros(H * B * T * ldbd, dtype=cd, device=dev)
+            lib.ea_attn_fused_bwd(B, H, T, T, dk, qkv.data_ptr(), 3 * d, qkv[:, d:].data_ptr(), 3 * d,
+                                  qkv[:, 2 * d:].data_ptr(), 3 * d, b.f(A + "pos_bias_u").data_ptr(),
+                                  b.f(A + "pos_bias_v").data_ptr(), pp.data_ptr(), d, olens.data_ptr(), 0,
+                                  scale, float(pa), sd(3), O.data_ptr(), d, lse.data_ptr(), dO.data_ptr(), d,
+                                  dqkv.data_ptr(), 3 * d, dqkv[:, d:].data_ptr(), 3 * d, dqkv[:, 2 * d:].data_ptr(),
+                                  3 * d, dbd.data_ptr(), ldbd, ops.stream())
+            qv = empty(N, d, dtype=cd, device=dev)  # q + v, for the linear_pos weight gradient
+            lib.ea_add_pos_bias(N, H, dk, qkv.data_ptr(), 3 * d, b.f(A + "pos_bias_v").data_ptr(),
+                                b.f(A + "pos_bias_v").data_ptr(), qv.data_ptr(), qv.data_ptr(),
+                                ops.dt(qv), ops.stream())
+        else:
+            _, qu, qv, P, Pd = s_core
+            dbd = empty(H * B * T * ldbd, dtype=cd, device=dev)
+            attn_bwd(dO, qu, qkv[:, d:], qkv[:, 2 * d:], P, Pd, ldT, B=B, H=H, T1=T, T2=T, dk=dk,
+                     ldq=d, ldk=3 * d, ldv=3 * d, scale=scale, p=pa, seed=sd(3), cd=cd,
+                     dq=dqkv, lddq=3 * d, dk_=dqkv[:, d:], lddk=3 * d, dv=dqkv[:, 2 * d:], lddv=3 * d,
+                     dbd=dbd, ldbd=ldbd)
         # q_u = q + u: du = sum dq_u ; q_v = q + v path: dq_v = dBD . p_h, dv_bias = sum dq_v
         dqv = empty(N, d, dtype=cd, device=dev)
         ops.gemm(dbd, pp, dqv, M=T, N=dk, K=P2, a_kmajor=1, b_kmajor=0, lda=ldbd, ldb=d, ldc=d,

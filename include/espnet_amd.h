@@ -254,6 +254,29 @@ int ea_attn_softmax_bwd(int B, int H, int T1, int T2, float scale, const float* 
                         const float* P, long ldP, float p, unsigned long long seed, void* dS,
                         int ds_dtype, long ldS, void* dBD, long ldBD, void* stream);
 
+/* Fused attention core, head dim 64, bf16 q/k/v (relattn.hip): per (b, h)
+ *   s[i,j] = ((q_i + bu)·k_j + (q_i + bv)·pp[T-1-i+j]) * scale   (pp != NULL: rel-pos,
+ *            RelPositionMultiHeadedAttention with rel_shift, attention.py:262-305; T1 == T2)
+ *   s[i,j] = ((q_i + bu)·k_j) * scale                            (pp == NULL; bu may be NULL)
+ *   key j valid iff j < klen[b] (klen NULL: all) and (!causal || j <= i); P = softmax (fully
+ *   masked row: 0); O = dropout(P)·V (mask index (z*T1 + i)*T2 + j, z = b*H + h).
+ * q rows b*T1 + i, k/v rows b*T2 + j, pp rows r < 2*T1-1, head h at column h*64 of each.
+ * fwd writes O (bf16, rows b*T1 + i) and lse[z*T1 + i] (row log-sum-exp; +inf if masked).
+ * bwd (T2 <= 256) writes dq = d(q + bu) (the q_v path is NOT included: it leaves through
+ * dbd), dk, dv (bf16) and, with pp, the band dbd[h][b][i][T-1-i+j] = gradient of the raw
+ * rel-pos term (q_i + bv)·pp[r] (bf16; buffer pre-zeroed; lddbd >= 2*T1-1).
+ * Nothing is materialised at (T1, T2) size. */
+int ea_attn_fused_fwd(int B, int H, int T1, int T2, int dk, const void* q, long ldq, const void* k,
+                      long ldk, const void* v, long ldv, const float* bu, const float* bv,
+                      const void* pp, long ldp, const long long* klen, int causal, float scale, float p,
+                      unsigned long long seed, void* o, long ldo, float* lse, void* stream);
+int ea_attn_fused_bwd(int B, int H, int T1, int T2, int dk, const void* q, long ldq, const void* k,
+                      long ldk, const void* v, long ldv, const float* bu, const float* bv,
+                      const void* pp, long ldp, const long long* klen, int causal, float scale, float p,
+                      unsigned long long seed, const void* o, long ldo, const float* lse, const void* dO,
+                      long lddo, void* dq, long lddq, void* dkout, long lddk, void* dvout, long lddv,
+                      void* dbd, long lddbd, void* stream);
+
 /* ---------------------------------------------------------------- losses */
 
 /* CTC forward (ctc.py:52-97 builtin; torch CTCLoss reduction=none, zero_infinity=True,

@@ -1,0 +1,166 @@
+"""Fused attention kernels (relattn.hip: ea_attn_fused_fwd / ea_attn_fused_bwd) against an fp32
+PyTorch restatement of RelPositionMultiHeadedAttention / MultiHeadedAttention
+(espnet/nets/pytorch_backend/transformer/attention.py:15-111, 209-305; rel_shift :237-260)
+on the same bf16-rounded inputs, and against the unfused HIP path (same dropout masks)."""
+import math
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda:0"
+bf = torch.bfloat16
+
+
+def rel_shift(x):
+    """attention.py:237-260 (zero_triu=False)."""
+    zero_pad = torch.zeros((*x.size()[:3], 1), device=x.device, dtype=x.dtype)
+    x_padded = torch.cat([zero_pad, x], dim=-1)
+    x_padded = x_padded.view(*x.size()[:2], x.size(3) + 1, x.size(2))
+    return x_padded[:, :, 1:].view_as(x)[:, :, :, : x.size(-1) // 2 + 1]
+
+
+def reference(q, k, v, u, vb, pp, klen, causal, H):
+    """fp32 torch: q (B,T1,H*64), k/v (B,T2,H*64), pp (2T-1, H*64) or None."""
+    B, T1, d = q.shape
+    T2 = k.shape[1]
+    dk = d // H
+    qh = q.view(B, T1, H, dk).transpose(1, 2)
+    kh = k.view(B, T2, H, dk).transpose(1, 2)
+    vh = v.view(B, T2, H, dk).transpose(1, 2)
+    if pp is not None:
+        ac = torch.matmul(qh + u.view(1, H, 1, dk), kh.transpose(-2, -1))
+        ph = pp.view(1, -1, H, dk).transpose(1, 2)
+        bd = rel_shift(torch.matmul(qh + vb.view(1, H, 1, dk), ph.transpose(-2, -1)))
+        scores = (ac + bd) / math.sqrt(dk)
+    else:
+        scores = torch.matmul(qh, kh.transpose(-2, -1)) / math.sqrt(dk)
+    mask = torch.arange(T2, device=q.device)[None, :] < klen[:, None]  # (B, T2)
+    mask = mask[:, None, None, :].expand(B, 1, T1, T2)
+    if causal:
+        mask = mask & torch.tril(torch.ones(T1, T2, dtype=torch.bool, device=q.device))[None, None]
+    scores = scores.masked_fill(~mask, torch.finfo(scores.dtype).min)
+    attn = torch.softmax(scores, dim=-1).masked_fill(~mask, 0.0)
+    x = torch.matmul(attn, vh)
+    return x.transpose(1, 2).reshape(B, T1, d)
+
+
+def _rel(a, b):
+    return float((a.float() - b.float()).norm() / b.float().norm().clamp_min(1e-30))
+
+
+def run_fused(q, k, v, u, vb, pp, klen, causal, H, dO, p=0.0, seed=0):
+    from espnet_amd import hip_ops as ops
+    from espnet_amd._lib import lib
+    B, T1, d = q.shape
+    T2 = k.shape[1]
+    dk = d // H
+    O = torch.empty(B, T1, d, dtype=bf, device=DEV)
+    lse = torch.empty(B * H * T1, device=DEV)
+    ptr = lambda t: 0 if t is None else t.data_ptr()  # noqa: E731
+    scale = 1.0 / math.sqrt(dk)
+    lib.ea_attn_fused_fwd(B, H, T1, T2, dk, q.data_ptr(), d, k.data_ptr(), d, v.data_ptr(), d, ptr(u), ptr(vb),
+                          ptr(pp), d, klen.data_ptr(), int(causal), scale, p, seed, O.data_ptr(), d,
+                          lse.data_ptr(), ops.stream())
+    dq = torch.empty_like(q)
+    dkk = torch.empty_like(k)
+    dv = torch.empty_like(v)
+    ldbd = (2 * T1 - 1 + 7) // 8 * 8
+    dbd = torch.zeros(H * B * T1 * ldbd, dtype=bf, device=DEV) if pp is not None else None
+    lib.ea_attn_fused_bwd(B, H, T1, T2, dk, q.data_ptr(), d, k.data_ptr(), d, v.data_ptr(), d, ptr(u), ptr(vb),
+                          ptr(pp), d, klen.data_ptr(), int(causal), scale, p, seed, O.data_ptr(), d, lse.data_ptr(),
+                          dO.data_ptr(), d, dq.data_ptr(), d, dkk.data_ptr(), d, dv.data_ptr(), d, ptr(dbd), ldbd,
+                          ops.stream())
+    torch.cuda.synchronize()
+    return O, dq, dkk, dv, dbd, ldbd
+
+
+def _inputs(B, H, T1, T2, rel, seed=0):
+    g = torch.Generator().manual_seed(seed)
+    d = H * 64
+    r = lambda *s: (torch.randn(*s, generator=g) * 0.5).to(bf).to(DEV)  # noqa: E731
+    q, k, v = r(B, T1, d), r(B, T2, d), r(B, T2, d)
+    u = (torch.randn(H * 64, generator=g) * 0.1).to(DEV) if rel else None
+    vb = (torch.randn(H * 64, generator=g) * 0.1).to(DEV) if rel else None
+    pp = r(2 * T1 - 1, d) if rel else None
+    dO = r(B, T1, d)
+    return q, k, v, u, vb, pp, dO
+
+
+@pytest.mark.parametrize("B,H,T1,T2,rel,causal,klens", [
+    (2, 3, 137, 137, True, False, [137, 100]),
+    (3, 2, 249, 249, True, False, [249, 200, 64]),
+    (2, 2, 41, 41, False, True, [41, 30]),
+    (2, 2, 41, 137, False, False, [137, 77]),
+    (1, 1, 5, 5, True, False, [5]),
+])
+def test_fused_attention_matches_fp32_reference(B, H, T1, T2, rel, causal, klens):
+    q, k, v, u, vb, pp, dO = _inputs(B, H, T1, T2, rel)
+    klen = torch.tensor(klens, dtype=torch.long, device=DEV)
+    O, dq, dk, dv, dbd, ldbd = run_fused(q, k, v, u, vb, pp, klen, causal, H, dO)
+    # fp32 reference on the same (bf16-rounded) inputs; q+u / q+v rounded to bf16 like the kernel
+    qf, kf, vf = (t.float().requires_grad_(True) for t in (q, k, v))
+    ppf = pp.float().requires_grad_(True) if rel else None
+    ref = reference(qf, kf, vf, u, vb, ppf, klen, causal, H)
+    valid_q = torch.ones(B, T1, dtype=torch.bool, device=DEV)
+    assert _rel(O.float()[valid_q], ref.detach()[valid_q]) < 1e-2
+    ref.backward(dO.float())
+    assert _rel(dk, kf.grad) < 2e-2
+    assert _rel(dv, vf.grad) < 2e-2
+    if not rel:
+        assert _rel(dq, qf.grad) < 2e-2
+        return
+    # rel-pos: dq from the kernel is the (q+u) path; the (q+v) path leaves through dbd:
+    # dq_total = dq + dBD . pp_h, d pp_h = dBD^T . (q+v)
+    d = H * 64
+    dbd4 = dbd.view(H, B, T1, ldbd)[..., : 2 * T1 - 1].float()
+    pph = pp.float().view(2 * T1 - 1, H, 64).permute(1, 0, 2)  # (H, R, 64)
+    dq_v = torch.einsum("hbir,hrc->bihc", dbd4, pph).reshape(B, T1, d)
+    assert _rel(dq.float() + dq_v, qf.grad) < 2e-2
+    qv = (q.float().view(B, T1, H, 64) + vb.view(1, 1, H, 64)).to(bf).float()
+    dpp = torch.einsum("hbir,bihc->rhc", dbd4, qv).reshape(2 * T1 - 1, d)
+    assert _rel(dpp, ppf.grad) < 2e-2
+    # the band structure: dBD[i, r] is zero outside r in [T-1-i, 2T-2-i]
+    i = torch.arange(T1, device=DEV)[:, None]
+    rr = torch.arange(2 * T1 - 1, device=DEV)[None, :]
+    outside = (rr < T1 - 1 - i) | (rr > 2 * T1 - 2 - i)
+    assert float(dbd4[:, :, outside].abs().max()) == 0.0
+
+
+def test_fused_matches_unfused_with_dropout():
+    """Same dropout masks (counter hash, index (z*T1 + i)*T2 + j): fused == unfused path."""
+    from espnet_amd import hip_ops as ops
+    from espnet_amd._lib import lib
+    from espnet_amd.layers.common import attn_bwd, attn_fwd
+    B, H, T = 2, 2, 97
+    q, k, v, u, vb, pp, dO = _inputs(B, H, T, T, True, seed=3)
+    klen = torch.tensor([97, 60], dtype=torch.long, device=DEV)
+    p, seed = 0.1, 12345
+    O, dq, dk, dv, dbd, ldbd = run_fused(q, k, v, u, vb, pp, klen, False, H, dO, p=p, seed=seed)
+    d = H * 64
+    N = B * T
+    P2 = 2 * T - 1
+    qu = torch.empty(N, d, dtype=bf, device=DEV)
+    qv = torch.empty(N, d, dtype=bf, device=DEV)
+    lib.ea_add_pos_bias(N, H, 64, q.data_ptr(), d, u.data_ptr(), vb.data_ptr(), qu.data_ptr(), qv.data_ptr(),
+                        ops.dt(qu), ops.stream())
+    bd = torch.empty(H * B * T * ldbd, device=DEV)
+    ops.gemm(qv, pp, bd, M=T, N=P2, K=64, a_kmajor=1, b_kmajor=1, lda=d, ldb=d, ldc=ldbd, batch=B, nh=H,
+             sA=(T * d, 64), sB=(0, 64), sC=(T * ldbd, B * T * ldbd), splitk=False)
+    O2, P, Pd, ldT = attn_fwd(qu, k.view(N, d), v.view(N, d), B=B, H=H, T1=T, T2=T, dk=64, ldq=d, ldk=d, ldv=d,
+                              klen=klen, causal=False, scale=1 / 8, p=p, seed=seed, cd=bf, bd=bd, ldbd=ldbd)
+    dq2 = torch.empty(N, d, dtype=bf, device=DEV)
+    dk2 = torch.empty(N, d, dtype=bf, device=DEV)
+    dv2 = torch.empty(N, d, dtype=bf, device=DEV)
+    dbd2 = torch.empty(H * B * T * ldbd, dtype=bf, device=DEV)
+    attn_bwd(dO.view(N, d), qu, k.view(N, d), v.view(N, d), P, Pd, ldT, B=B, H=H, T1=T, T2=T, dk=64, ldq=d, ldk=d,
+             ldv=d, scale=1 / 8, p=p, seed=seed, cd=bf, dq=dq2, lddq=d, dk_=dk2, lddk=d, dv=dv2, lddv=d,
+             dbd=dbd2, ldbd=ldbd)
+    torch.cuda.synchronize()
+    assert _rel(O.view(N, d), O2) < 1e-2
+    assert _rel(dq.view(N, d), dq2) < 2e-2
+    assert _rel(dk.view(N, d), dk2) < 2e-2
+    assert _rel(dv.view(N, d), dv2) < 2e-2
+    band = dbd2.view(H, B, T, ldbd)[..., :P2]
+    assert _rel(dbd.view(H, B, T, ldbd)[..., :P2], band) < 2e-2
