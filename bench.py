@@ -80,6 +80,21 @@ def synthetic_batch(cfg, seed):
                 text_lengths=torch.full((B,), L, dtype=torch.long))
 
 
+PMC_FILE = os.path.join(ROOT, "profiles", "r1_v10_pmc_conv2_fwd.json")
+
+
+def pmc_traffic():
+    """HBM bytes per launch of the roofline kernel from the committed PMC pass
+    (scripts/gpu_pmc.sh: rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE in separate runs, gfx950
+    FETCH_SIZE x2 correction applied); None if the file is absent."""
+    try:
+        with open(PMC_FILE) as f:
+            d = json.load(f)
+        return int(d["traffic_bytes_per_launch"]), os.path.relpath(PMC_FILE, ROOT)
+    except (OSError, KeyError, ValueError):
+        return None, None
+
+
 def cpu_baseline(cfg, seconds_budget=25.0):
     """The oracle (oracle/asr_oracle.py, PyTorch-CPU restatement of the reference step) on
     the host cores: fwd + bwd + clip + Adam on a bounded sample (B=4 of the same shapes)."""
@@ -188,6 +203,7 @@ def main():
     dtype = "bf16" if amp else "f32"
     achieved = conv_flop / (conv_ms * 1e-3) / 1e12
     loss_v = float(loss.item())
+    traffic, traffic_src = pmc_traffic() if (args.config == "c3" and amp) else (None, None)
     if rank == 0:
         out = {
             "metric": METRIC, "value": round(utt, 3), "unit": "utterances/s", "n_gpus": world,
@@ -204,7 +220,9 @@ def main():
             "roofline": {"bound": "mfma", "kernel": "gemm_kernel<bf16> conv2 implicit-GEMM (subsampling, "
                                                     f"M={B * T2 * F2} N={C} K={9 * C})",
                          "achieved": round(achieved, 2), "peak": PEAK[dtype], "unit": "TFLOP/s",
-                         "frac": round(achieved / PEAK[dtype], 4), "traffic": None,
+                         "frac": round(achieved / PEAK[dtype], 4), "traffic": traffic,
+                         "traffic_unit": "bytes/launch (HBM, PMC)", "traffic_source": traffic_src,
+                         "algorithmic_bytes": int(2 * (B * T1 * F1 * C + C * 9 * C + B * T2 * F2 * C)),
                          "launch_ms": round(conv_ms, 4), "launches": n_conv},
             "loss": round(loss_v, 4),
         }

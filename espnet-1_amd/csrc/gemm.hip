@@ -222,26 +222,66 @@ EA_DEV void st4(void* p, long i, int dt, const float (&v)[4]) {
   }
 }
 
+// Launch-uniform dropout parameters, computed once per block: the salt is read from device
+// memory here and nowhere else in the epilogue (a per-element re-read would be ordered after
+// every preceding C store, which the compiler must assume may alias it).
+struct EpiK {
+  uint32_t key, thr;
+  float sc;
+  bool drop;
+};
+EA_DEV EpiK make_epik(const GemmP& p) {
+  EpiK k;
+  k.drop = p.epi.drop_p > 0.f;
+  k.key = k.drop ? ea_seed_key(ea_salted(p.epi.seed, p.salt)) : 0u;
+  k.thr = ea_drop_thr(p.epi.drop_p);
+  k.sc = k.drop ? 1.f / (1.f - p.epi.drop_p) : 1.f;
+  return k;
+}
+EA_DEV void drop4k(const EpiK& k, uint64_t idx, float (&v)[4]) {  // idx even
+  if (!k.drop) return;
+  const uint32_t h0 = ea_pair_hash(k.key, idx >> 1), h1 = ea_pair_hash(k.key, (idx >> 1) + 1);
+  v[0] *= (h0 & 0xffffu) >= k.thr ? k.sc : 0.f;
+  v[1] *= (h0 >> 16) >= k.thr ? k.sc : 0.f;
+  v[2] *= (h1 & 0xffffu) >= k.thr ? k.sc : 0.f;
+  v[3] *= (h1 >> 16) >= k.thr ? k.sc : 0.f;
+}
+
+// The operand an epilogue kind reads besides the accumulator (4 columns at (row, col)):
+// STORE with beta != 0 reads C, RESID reads resid, DACT reads aux.  Returns false if none.
 template <int KIND>
-EA_DEV void epi_four(const GemmP& p, int z, int zb, int zh, int row, int col, const float (&acc)[4]) {
+EA_DEV bool epi_src(const GemmP& p, int zb, int zh, int row, int col, float (&o)[4]) {
+  const ea_epilogue& e = p.epi;
+  if constexpr (KIND == EA_EPI_STORE) {
+    if (e.beta == 0.f) return false;
+    ld4(p.C, zb * p.sCb + zh * p.sCh + (long)row * p.ldc + col, p.c_dtype, o);
+    return true;
+  } else if constexpr (KIND == EA_EPI_RESID) {
+    if (!e.resid) return false;
+    ld4(e.resid, (long)row * e.ldr + col, EA_F32, o);
+    return true;
+  } else if constexpr (KIND == EA_EPI_DACT) {
+    ld4(e.aux, (long)row * e.ldaux + col, e.aux_dtype, o);
+    return true;
+  }
+  return false;
+}
+
+// acc (4 columns) + the preloaded operand `o` -> stored outputs
+template <int KIND>
+EA_DEV void epi_four_pre(const GemmP& p, const EpiK& k, int z, int zb, int zh, int row, int col,
+                         const float (&acc)[4], const float (&bias)[4], bool has_o, const float (&o)[4]) {
   const ea_epilogue& e = p.epi;
   const long cidx = zb * p.sCb + zh * p.sCh + (long)row * p.ldc + col;
   const uint64_t didx = ((uint64_t)z * p.M + row) * (uint64_t)p.N + col;
-  const uint64_t seed = e.drop_p > 0.f ? ea_salted(e.seed, p.salt) : 0;
   float v[4];
 #pragma unroll
-  for (int c = 0; c < 4; ++c) v[c] = e.alpha * acc[c];
-  if (KIND != EA_EPI_DACT && e.bias) {
-    const float4 bb = *(const float4*)(e.bias + col);
-    v[0] += bb.x; v[1] += bb.y; v[2] += bb.z; v[3] += bb.w;
-  }
+  for (int c = 0; c < 4; ++c) v[c] = e.alpha * acc[c] + (KIND != EA_EPI_DACT ? bias[c] : 0.f);
   if constexpr (KIND == EA_EPI_STORE) {
 #pragma unroll
     for (int c = 0; c < 4; ++c) v[c] *= e.post_scale;
-    drop_scale4(seed, didx, e.drop_p, v);
-    if (e.beta != 0.f) {
-      float o[4];
-      ld4(p.C, cidx, p.c_dtype, o);
+    drop4k(k, didx, v);
+    if (has_o) {
 #pragma unroll
       for (int c = 0; c < 4; ++c) v[c] += e.beta * o[c];
     }
@@ -250,72 +290,60 @@ EA_DEV void epi_four(const GemmP& p, int z, int zb, int zh, int row, int col, co
     if (e.aux) st4(e.aux, (long)row * e.ldaux + col, e.aux_dtype, v);
 #pragma unroll
     for (int c = 0; c < 4; ++c) v[c] = act_fwd(e.act, v[c]);
-    drop_scale4(seed, didx, e.drop_p, v);
+    drop4k(k, didx, v);
     st4(p.C, cidx, p.c_dtype, v);
   } else if constexpr (KIND == EA_EPI_RESID) {
-    float r[4] = {0.f, 0.f, 0.f, 0.f};
-    if (e.resid) ld4(e.resid, (long)row * e.ldr + col, EA_F32, r);
-    drop_scale4(seed, didx, e.drop_p, v);
+    drop4k(k, didx, v);
 #pragma unroll
-    for (int c = 0; c < 4; ++c) v[c] = r[c] + e.rscale * v[c];
+    for (int c = 0; c < 4; ++c) v[c] = (has_o ? o[c] : 0.f) + e.rscale * v[c];
     st4(p.C, cidx, EA_F32, v);
   } else {
-    float h[4];
-    ld4(e.aux, (long)row * e.ldaux + col, e.aux_dtype, h);
-    drop_scale4(seed, didx, e.drop_p, v);
+    drop4k(k, didx, v);
 #pragma unroll
-    for (int c = 0; c < 4; ++c) v[c] *= act_bwd(e.act, h[c]);
+    for (int c = 0; c < 4; ++c) v[c] *= act_bwd(e.act, o[c]);
     st4(p.C, cidx, p.c_dtype, v);
+  }
+}
+
+template <int KIND>
+EA_DEV void epi_four(const GemmP& p, const EpiK& k, int z, int zb, int zh, int row, int col, const float (&acc)[4]) {
+  float bias[4] = {0.f, 0.f, 0.f, 0.f}, o[4];
+  if (p.epi.bias) {
+    const float4 bb = *(const float4*)(p.epi.bias + col);
+    bias[0] = bb.x; bias[1] = bb.y; bias[2] = bb.z; bias[3] = bb.w;
+  }
+  const bool has_o = epi_src<KIND>(p, zb, zh, row, col, o);
+  epi_four_pre<KIND>(p, k, z, zb, zh, row, col, acc, bias, has_o, o);
+}
+
+// NB independent 4-column groups (rows[i], cols[i]) of one thread: every operand load is
+// issued before the first store so their latencies overlap (stores to C may alias the
+// operands, so the compiler cannot hoist a later group's loads above an earlier store).
+// Out-of-range groups are skipped.  Vector path only (p.vec_c, which implies N % 4 == 0, so
+// a group is wholly inside or wholly outside); callers run epi_one element-wise otherwise.
+template <int KIND, int NB>
+EA_DEV void epi_batch(const GemmP& p, const EpiK& k, int z, int zb, int zh, const int (&rows)[NB],
+                      const int (&cols)[NB], const float (&v)[NB][4]) {
+  float o[NB][4];
+  bool has[NB];
+#pragma unroll
+  for (int i = 0; i < NB; ++i) {
+    has[i] = false;
+    if (rows[i] < p.M && cols[i] < p.N) has[i] = epi_src<KIND>(p, zb, zh, rows[i], cols[i], o[i]);
+  }
+#pragma unroll
+  for (int i = 0; i < NB; ++i) {
+    if (rows[i] >= p.M || cols[i] >= p.N) continue;
+    float bias[4] = {0.f, 0.f, 0.f, 0.f};
+    if (KIND != EA_EPI_DACT && p.epi.bias) {
+      const float4 bb = *(const float4*)(p.epi.bias + cols[i]);
+      bias[0] = bb.x; bias[1] = bb.y; bias[2] = bb.z; bias[3] = bb.w;
+    }
+    epi_four_pre<KIND>(p, k, z, zb, zh, rows[i], cols[i], v[i], bias, has[i], o[i]);
   }
 }
 
 constexpr int EPI_LDT = 68;  // floats per LDS row of a wave's 64x64 accumulator tile
-
-// Transpose the wave's 64x64 accumulators through LDS, then apply the epilogue four
-// columns at a time.  `vec` (host-checked alignment of C/aux/resid/bias and N % 4 == 0)
-// selects the vector path; otherwise element-wise.
-template <int KIND, int MI = 4>
-EA_DEV void epi_tile_lds(const GemmP& p, char* smem, int z, int zb, int zh, int r0, int c0, int lane, int w,
-                         const f32x4 (&acc)[MI][4]) {
-  float* t = (float*)smem + w * (MI * 16) * EPI_LDT;
-  const int rq = (lane >> 4) * 4, cc = lane & 15;
-#pragma unroll
-  for (int i = 0; i < MI; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j)
-#pragma unroll
-      for (int rr = 0; rr < 4; ++rr) t[(i * 16 + rq + rr) * EPI_LDT + j * 16 + cc] = acc[i][j][rr];
-  __builtin_amdgcn_wave_barrier();
-  asm volatile("" ::: "memory");
-  const int lc = (lane & 15) * 4;
-#pragma unroll 4
-  for (int it = 0; it < MI * 4; ++it) {
-    const int lr = it * 4 + (lane >> 4);
-    const int row = r0 + lr, col = c0 + lc;
-    if (row >= p.M || col >= p.N) continue;
-    const float4 f = *(const float4*)(t + lr * EPI_LDT + lc);
-    const float v[4] = {f.x, f.y, f.z, f.w};
-    if (p.vec_c && col + 3 < p.N) {
-      if (p.splitk > 1) {
-        float* slab = p.ws + ((long)z * p.splitk + (blockIdx.z % p.splitk)) * (long)p.M * p.N;
-        *(float4*)(slab + (long)row * p.N + col) = f;
-      } else {
-        epi_four<KIND>(p, z, zb, zh, row, col, v);
-      }
-    } else {
-#pragma unroll
-      for (int c = 0; c < 4; ++c) {
-        if (col + c >= p.N) break;
-        if (p.splitk > 1) {
-          float* slab = p.ws + ((long)z * p.splitk + (blockIdx.z % p.splitk)) * (long)p.M * p.N;
-          slab[(long)row * p.N + col + c] = v[c];
-        } else {
-          epi_one<KIND>(p, z, zb, zh, row, col + c, v[c]);
-        }
-      }
-    }
-  }
-}
 
 // ---------------------------------------------------------------- kernel
 template <typename T, bool AK, bool BKM>
@@ -502,13 +530,17 @@ EA_DEV bf16x8 frag_img(const char* img, int r, int ks, int lane) {
 }
 
 // Epilogue of one wave's (MI*16) x (NJ*16) accumulator tile, in 64 x 64 chunks transposed
-// through the wave's private LDS region (64 x EPI_LDT floats).
+// through the wave's private LDS region (64 x EPI_LDT floats); each lane then owns 4
+// consecutive columns of 16 rows per chunk, handled 8 rows at a time (epi_batch).  With
+// split-K (p.splitk > 1) the chunk goes to this slice's f32 slab instead.
 template <int KIND, int MI, int NJ>
-EA_DEV void epi_wave(const GemmP& p, char* smem, int z, int zb, int zh, int r0, int c0, int lane, int w,
-                     const f32x4 (&acc)[MI][NJ]) {
+EA_DEV void epi_wave(const GemmP& p, const EpiK& k, char* smem, int z, int zb, int zh, int r0, int c0, int lane,
+                     int w, const f32x4 (&acc)[MI][NJ]) {
   constexpr int RC = MI < 4 ? MI : 4;  // row blocks per chunk
+  constexpr int NB = MI * NJ >= 32 ? 4 : (RC * 4 < 8 ? RC * 4 : 8);  // fewer in flight beside big accumulators
   float* t = (float*)smem + w * (RC * 16) * EPI_LDT;
   const int rq = (lane >> 4) * 4, cc = lane & 15, lc = (lane & 15) * 4;
+  float* slab = p.splitk > 1 ? p.ws + ((long)z * p.splitk + (blockIdx.z % p.splitk)) * (long)p.M * p.N : nullptr;
 #pragma unroll
   for (int ri = 0; ri < MI / RC; ++ri) {
 #pragma unroll
@@ -526,32 +558,41 @@ EA_DEV void epi_wave(const GemmP& p, char* smem, int z, int zb, int zh, int r0, 
             t[(i * 16 + rq + rr) * EPI_LDT + j * 16 + cc] = acc[ri * RC + i][cj * 4 + j][rr];
       __builtin_amdgcn_wave_barrier();
       asm volatile("" ::: "memory");
-      const int rb = r0 + ri * RC * 16, cb = c0 + cj * 64;
-#pragma unroll 4
-      for (int it = 0; it < RC * 4; ++it) {
-        const int lr = it * 4 + (lane >> 4);
-        const int row = rb + lr, col = cb + lc;
-        if (row >= p.M || col >= p.N) continue;
-        const float4 f = *(const float4*)(t + lr * EPI_LDT + lc);
-        const float v[4] = {f.x, f.y, f.z, f.w};
-        if (p.vec_c && col + 3 < p.N) {
-          if (p.splitk > 1) {
-            float* slab = p.ws + ((long)z * p.splitk + (blockIdx.z % p.splitk)) * (long)p.M * p.N;
-            *(float4*)(slab + (long)row * p.N + col) = f;
-          } else {
-            epi_four<KIND>(p, z, zb, zh, row, col, v);
-          }
-        } else {
-#pragma unroll
+      const int rb = r0 + ri * RC * 16, col = c0 + cj * 64 + lc;
+      if (!p.vec_c) {  // cold path: element-wise straight from the LDS image
+#pragma unroll 1
+        for (int it = 0; it < RC * 4; ++it) {
+          const int lr = it * 4 + (lane >> 4), row = rb + lr;
+          if (row >= p.M) continue;
+#pragma unroll 1
           for (int c = 0; c < 4; ++c) {
             if (col + c >= p.N) break;
-            if (p.splitk > 1) {
-              float* slab = p.ws + ((long)z * p.splitk + (blockIdx.z % p.splitk)) * (long)p.M * p.N;
-              slab[(long)row * p.N + col + c] = v[c];
-            } else {
-              epi_one<KIND>(p, z, zb, zh, row, col + c, v[c]);
-            }
+            const float x = t[lr * EPI_LDT + lc + c];
+            if (slab) slab[(long)row * p.N + col + c] = x;
+            else epi_one<KIND>(p, z, zb, zh, row, col + c, x);
           }
+        }
+        continue;
+      }
+#pragma unroll 1
+      for (int it0 = 0; it0 < RC * 4; it0 += NB) {
+        int rows[NB], cols[NB];
+        float v[NB][4];
+#pragma unroll
+        for (int i = 0; i < NB; ++i) {
+          const int lr = (it0 + i) * 4 + (lane >> 4);
+          const float4 f = *(const float4*)(t + lr * EPI_LDT + lc);
+          rows[i] = rb + lr;
+          cols[i] = col;
+          v[i][0] = f.x; v[i][1] = f.y; v[i][2] = f.z; v[i][3] = f.w;
+        }
+        if (slab) {
+#pragma unroll
+          for (int i = 0; i < NB; ++i)
+            if (rows[i] < p.M && col < p.N)
+              *(float4*)(slab + (long)rows[i] * p.N + col) = make_float4(v[i][0], v[i][1], v[i][2], v[i][3]);
+        } else {
+          epi_batch<KIND, NB>(p, k, z, zb, zh, rows, cols, v);
         }
       }
     }
@@ -582,7 +623,7 @@ EA_DEV void dgrad_tap(const ea_conv_geo& g, int q, int& kh, int& kw) {
 }
 
 // BM x BN output tile, 2 x WN wave64s, each (BM/2) x (BN/WN) = MI x NJ MFMA 16x16 blocks.
-// (BM, BN, WN) in {(64,128,2) K-major A only, (128,128,2), (256,128,2), (256,256,4)}.
+// (BM, BN, WN) in {(64,128,2) K-major A only, (128,128,2), (256,256,4)}.
 // Small wave tiles read the fragments of both k-steps up front (register double buffer);
 // 128-row wave tiles read one k-step at a time.
 template <int BM_, int BN_, int WN, bool AK, bool BKM, int STAGES, int MODE = 0>
@@ -829,11 +870,12 @@ __global__ __launch_bounds__(128 * WN, 1) void gemm_bf16_lds(GemmP p) {
   }
 
   __syncthreads();  // every wave is done reading the operand ring: reuse it for the epilogue
+  const EpiK ek = make_epik(p);
   switch (p.splitk > 1 ? EA_EPI_STORE : p.epi.kind) {
-    case EA_EPI_STORE: epi_wave<EA_EPI_STORE, MI, NJ>(p, smem, z, zb, zh, m0 + wm, n0 + wn, lane, w, acc); break;
-    case EA_EPI_ACT: epi_wave<EA_EPI_ACT, MI, NJ>(p, smem, z, zb, zh, m0 + wm, n0 + wn, lane, w, acc); break;
-    case EA_EPI_RESID: epi_wave<EA_EPI_RESID, MI, NJ>(p, smem, z, zb, zh, m0 + wm, n0 + wn, lane, w, acc); break;
-    default: epi_wave<EA_EPI_DACT, MI, NJ>(p, smem, z, zb, zh, m0 + wm, n0 + wn, lane, w, acc); break;
+    case EA_EPI_STORE: epi_wave<EA_EPI_STORE, MI, NJ>(p, ek, smem, z, zb, zh, m0 + wm, n0 + wn, lane, w, acc); break;
+    case EA_EPI_ACT: epi_wave<EA_EPI_ACT, MI, NJ>(p, ek, smem, z, zb, zh, m0 + wm, n0 + wn, lane, w, acc); break;
+    case EA_EPI_RESID: epi_wave<EA_EPI_RESID, MI, NJ>(p, ek, smem, z, zb, zh, m0 + wm, n0 + wn, lane, w, acc); break;
+    default: epi_wave<EA_EPI_DACT, MI, NJ>(p, ek, smem, z, zb, zh, m0 + wm, n0 + wn, lane, w, acc); break;
   }
   probe_end(p);
 }
@@ -845,6 +887,7 @@ __global__ void splitk_reduce(GemmP p) {
   const int zb = z / p.nh, zh = z % p.nh;
   const float* base = p.ws + (long)z * p.splitk * MN;
   const bool vec = p.vec_c && (p.N % 4 == 0);
+  const EpiK ek = make_epik(p);
   const long n4 = vec ? MN / 4 : MN;
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n4; i += (long)gridDim.x * blockDim.x) {
     if (vec) {
@@ -856,10 +899,10 @@ __global__ void splitk_reduce(GemmP p) {
       const int row = (int)(i * 4 / p.N), col = (int)(i * 4 % p.N);
       const float v[4] = {a.x, a.y, a.z, a.w};
       switch (p.epi.kind) {
-        case EA_EPI_STORE: epi_four<EA_EPI_STORE>(p, z, zb, zh, row, col, v); break;
-        case EA_EPI_ACT: epi_four<EA_EPI_ACT>(p, z, zb, zh, row, col, v); break;
-        case EA_EPI_RESID: epi_four<EA_EPI_RESID>(p, z, zb, zh, row, col, v); break;
-        default: epi_four<EA_EPI_DACT>(p, z, zb, zh, row, col, v); break;
+        case EA_EPI_STORE: epi_four<EA_EPI_STORE>(p, ek, z, zb, zh, row, col, v); break;
+        case EA_EPI_ACT: epi_four<EA_EPI_ACT>(p, ek, z, zb, zh, row, col, v); break;
+        case EA_EPI_RESID: epi_four<EA_EPI_RESID>(p, ek, z, zb, zh, row, col, v); break;
+        default: epi_four<EA_EPI_DACT>(p, ek, z, zb, zh, row, col, v); break;
       }
     } else {
       float a = 0.f;
@@ -902,10 +945,6 @@ int launch_lds(GemmP& p, int a_k, int b_k, int nz, hipStream_t st) {
     else EA_GL(64, 128, true, false, 2);
   } else if (p.bm == 256 && p.bn == 256) {
     EA_GL4(256, 256, 2)
-  } else if (p.bm == 256) {
-    EA_GL4(256, 128, 2)
-  } else if (g_gemm_stages >= 3) {
-    EA_GL4(128, 128, 3)
   } else {
     EA_GL4(128, 128, 2)
   }
@@ -963,7 +1002,7 @@ int launch(GemmP& p, int a_k, int b_k, int nz, hipStream_t st) {
 
 extern "C" int ea_gemm_set_pipeline(int stages) {
   EA_ENTRY();
-  EA_CHECK_ARG(stages == 0 || stages == 2 || stages == 3 || stages == 12 || stages == 13);
+  EA_CHECK_ARG(stages == 0 || stages == 2 || stages == 12);
   g_gemm_bm64 = stages < 10;   // 12/13: same ring, 128-row tiles only (A/B measurements)
   g_gemm_stages = stages % 10;
   return 0;
@@ -1001,7 +1040,7 @@ extern "C" int ea_probe_end(unsigned long long* slots, void* stream) {
 extern "C" int ea_gemm_set_tile(int bm, int bn) {
   EA_ENTRY();
   EA_CHECK_ARG((bm == 0 && bn == 0) || (bm == 64 && bn == 128) || (bm == 128 && bn == 128) ||
-               (bm == 256 && (bn == 128 || bn == 256)));
+               (bm == 256 && bn == 256));
   g_force_bm = bm;
   g_force_bn = bn;
   return 0;

@@ -97,12 +97,12 @@ int ea_gemm_conv(const ea_conv_geo* geo, int a_kmajor, int b_kmajor, int M, int 
                  const void* A, long lda, const void* B, long ldb, void* C, int c_dtype, long ldc,
                  const ea_epilogue* epi, float* workspace, long ws_elems, void* stream);
 
-/* Select the bf16 GEMM main loop: 2 or 3 = LDS-DMA (global_load_lds) ring of that depth
- * (default 2), 0 = register-staged loop; 12/13 = same ring without 64-row tiles.
+/* Select the bf16 GEMM main loop: 2 = LDS-DMA (global_load_lds) 2-stage ring (default),
+ * 0 = register-staged loop; 12 = same ring without 64-row tiles.
  * Process-wide; for A/B measurements. */
 int ea_gemm_set_pipeline(int stages);
 
-/* Pin the bf16 LDS-DMA GEMM output tile (bm x bn in {64x128, 128x128, 256x128, 256x256});
+/* Pin the bf16 LDS-DMA GEMM output tile (bm x bn in {64x128, 128x128, 256x256});
  * 0,0 = automatic choice by grid size.  Process-wide; for tests and tuning. */
 int ea_gemm_set_tile(int bm, int bn);
 

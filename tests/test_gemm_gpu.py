@@ -167,7 +167,7 @@ def test_gemm_unaligned_leading_dims(dtype, a_k, b_k):
     torch.testing.assert_close(C.double().cpu(), ref_mm(A, B, a_k, b_k, M, N, K), atol=tol * K ** 0.5, rtol=tol)
 
 
-TILES = [(64, 128), (128, 128), (256, 128), (256, 256)]
+TILES = [(64, 128), (128, 128), (256, 256)]
 
 
 @pytest.fixture
@@ -222,3 +222,4 @@ def test_gemm_bf16_tiles_epilogue_splitk(forced_tile):
     ops.linear_dw(dy, xx, dw)
     refw = dy.double().cpu().t() @ xx.double().cpu()
     torch.testing.assert_close(dw.double().cpu(), refw, atol=2e-3 * R ** 0.5, rtol=2e-3)
+
