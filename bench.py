@@ -58,6 +58,47 @@ def c2_config():
     return c
 
 
+def c5_config():
+    """BASELINE.json configs[4] / SURVEY.md §8d C5: Conformer-L + SpecAug (conformer8.yaml:62-76),
+    bucketed variable-length utterances T ~ U[200, 2000], L = round(T/25), NumElements
+    batching with batch_bins sized so a batch holds ~32 utterances at T=1000 (per GPU)."""
+    c = c3_config()
+    c.update(B=None, T=2000, L=80, gflop_per_step=None, corpus=640, batch_bins=32 * 1000 * 80,
+             specaug_conf=dict(apply_time_warp=True, time_warp_window=5, time_warp_mode="bicubic",
+                               apply_freq_mask=True, freq_mask_width_range=[0, 27], num_freq_mask=2,
+                               apply_time_mask=True, time_mask_width_ratio_range=[0.0, 0.05],
+                               num_time_mask=10))
+    return c
+
+
+def c5_batches(cfg, rank, world, seed=7):
+    """Synthetic LibriSpeech-shaped corpus -> NumElementsBatchSampler batches (host), this
+    rank's share (batch[rank::world] of each global batch, abs_task.py:1566-1575)."""
+    from espnet_amd.samplers.num_elements_batch_sampler import NumElementsBatchSampler
+    g = torch.Generator().manual_seed(seed)
+    n, V, F = cfg["corpus"], cfg["vocab_size"], cfg["input_size"]
+    Ts = torch.randint(200, 2001, (n,), generator=g).tolist()
+    shapes = {f"utt{i:04d}": [t, F] for i, t in enumerate(Ts)}
+    sampler = NumElementsBatchSampler(cfg["batch_bins"] * world, utt2shapes=[shapes])
+    order = torch.randperm(len(sampler), generator=g).tolist()  # SequenceIterFactory shuffles batches
+    batches = []
+    for bi in order:
+        keys = list(sampler.batch_list[bi])[rank::world]
+        if not keys:
+            continue
+        lens = [shapes[k][0] for k in keys]
+        Ls = [max(1, round(t / 25)) for t in lens]
+        B, T, L = len(keys), max(lens), max(Ls)
+        speech = torch.zeros(B, T, F)
+        text = torch.full((B, L), -1, dtype=torch.long)
+        for i, (t, l) in enumerate(zip(lens, Ls)):
+            speech[i, :t] = torch.randn(t, F, generator=g)
+            text[i, :l] = torch.randint(2, V - 1, (l,), generator=g)
+        batches.append(dict(speech=speech, speech_lengths=torch.tensor(lens), text=text,
+                            text_lengths=torch.tensor(Ls), _lens_host=lens, _maxlens=(T, L)))
+    return batches
+
+
 def token_list(V):
     return ["<blank>", "<unk>"] + [f"t{i}" for i in range(V - 3)] + ["<sos/eos>"]
 
@@ -67,7 +108,8 @@ def build(cfg, seed=0):
     torch.manual_seed(seed)
     args = dict(token_list=token_list(cfg["vocab_size"]), input_size=cfg["input_size"], encoder="conformer",
                 encoder_conf=cfg["encoder_conf"], decoder=cfg["decoder"],
-                decoder_conf=cfg["decoder_conf"], model_conf=cfg["model_conf"], normalize="utterance_mvn")
+                decoder_conf=cfg["decoder_conf"], model_conf=cfg["model_conf"], normalize="utterance_mvn",
+                specaug="specaug" if cfg.get("specaug_conf") else None, specaug_conf=cfg.get("specaug_conf"))
     return build_model(args)
 
 
@@ -129,7 +171,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--config", default="c3", choices=["c3", "c2"])
+    ap.add_argument("--config", default="c3", choices=["c3", "c2", "c5"])
     ap.add_argument("--fp32", action="store_true", help="exact-f32 MFMA instead of bf16 AMP")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--profile-steps", type=int, default=0)
@@ -152,6 +194,8 @@ def main():
     from espnet_amd.train.distributed import ArenaDataParallel
     from espnet_amd.train.graph import CapturedTrainStep
 
+    if args.config == "c5":
+        return run_c5(args, world, rank, dev)
     cfg = c3_config() if args.config == "c3" else c2_config()
     amp = not args.fp32
     model = build(cfg)
@@ -230,6 +274,79 @@ def main():
             out["cpu_baseline"] = cpu_baseline(cfg)
             out["speedup_vs_cpu"] = round(utt / out["cpu_baseline"]["value"], 1)
         print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def run_c5(args, world, rank, dev):
+    """C5: bucketed variable-length batches + SpecAug, eager steps (shapes change every
+    step; SpecAug draws on the host like the reference).  value = utterances/s over all
+    ranks; frames/s and the padding fraction are reported alongside."""
+    from espnet_amd.optim.adam import ArenaAdam
+    from espnet_amd.schedulers.warmup_lr import WarmupLR
+    from espnet_amd.train.distributed import ArenaDataParallel
+    from espnet_amd.train.trainer import Trainer
+
+    cfg = c5_config()
+    amp = not args.fp32
+    model = build(cfg)
+    model.prepare(dev, amp=amp, seed=1234)
+    model.train()
+    opt = ArenaAdam(model, lr=cfg["optim"]["lr"], weight_decay=cfg["optim"]["weight_decay"])
+    sched = WarmupLR(opt, warmup_steps=cfg["warmup_steps"])
+    dp = ArenaDataParallel(model) if world > 1 else None
+    batches = c5_batches(cfg, rank, world)
+    dbatches = []
+    for b in batches:  # resident in HBM before timing
+        d = {k: (v.to(dev) if isinstance(v, torch.Tensor) else v) for k, v in b.items()}
+        dbatches.append(d)
+    nb = len(dbatches)
+    torch.manual_seed(1234 + rank)  # SpecAug's host draws
+
+    def step(i):
+        b = dict(dbatches[i % nb])
+        maxlens = b.pop("_maxlens")
+        return Trainer.train_one_step(model, b, opt, sched, grad_clip=5.0, dp=dp, maxlens=maxlens)
+
+    for i in range(args.warmup):
+        step(i)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    n_utt = n_frames = n_padded = 0
+    t0 = time.perf_counter()
+    for i in range(args.warmup, args.warmup + args.steps):
+        loss, stats, weight, gn = step(i)
+        b = dbatches[i % nb]
+        n_utt += len(b["_lens_host"])
+        n_frames += sum(b["_lens_host"])
+        n_padded += len(b["_lens_host"]) * b["_maxlens"][0]
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    tot = torch.tensor([elapsed, n_utt, n_frames, n_padded], dtype=torch.float64, device=dev)
+    if world > 1:
+        mx = tot[:1].clone()
+        dist.all_reduce(mx, op=dist.ReduceOp.MAX)
+        dist.all_reduce(tot, op=dist.ReduceOp.SUM)
+        elapsed = float(mx.item())
+    _, n_utt, n_frames, n_padded = (float(v) for v in tot.tolist())
+    if rank == 0:
+        print(json.dumps({
+            "metric": "utterances/sec, Conformer-L + SpecAug, bucketed T~U[200,2000] (C5)",
+            "value": round(n_utt / elapsed, 3), "unit": "utterances/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "bf16" if amp else "f32",
+            "data": "synthetic corpus (speech ~N(0,1), T~U[200,2000], L=round(T/25)); random-init weights",
+            "config": {"workload": "C5 Conformer-L + 6-layer decoder + SpecAug (conformer8), NumElements "
+                                   f"batch_bins {cfg['batch_bins']} per GPU, eager steps",
+                       "global_batch": None, "seq_len": "200-2000", "parallelism": f"dp{world}"},
+            "frames_per_s": round(n_frames / elapsed, 1),
+            "padding_fraction": round(1.0 - n_frames / n_padded, 4),
+            "batches_in_corpus_per_rank": nb, "loss": round(float(loss.item()), 4),
+        }), flush=True)
     if world > 1:
         dist.destroy_process_group()
 

@@ -95,8 +95,6 @@ class ESPnetASRModel(AbsESPnetModel):
         if frontend is not None or preencoder is not None or postencoder is not None:
             raise NotImplementedError("frontend/preencoder/postencoder are outside the HIP hot path "
                                       "(feed features: input_size set, SURVEY.md §2a)")
-        if specaug is not None:
-            raise NotImplementedError("SpecAugment (C5) is a §8(f) next item")
         if joint_network is not None or interctc_weight != 0.0 or lang_token_id != -1:
             raise NotImplementedError("transducer / interCTC / lang token are not on the path")
         self.blank_id = token_list.index(sym_blank) if sym_blank in token_list else 0
@@ -111,7 +109,7 @@ class ESPnetASRModel(AbsESPnetModel):
         self.aux_ctc = aux_ctc
         self.token_list = list(token_list)
         self.frontend = None
-        self.specaug = None
+        self.specaug = specaug
         self.normalize = normalize
         self.preencoder = None
         self.postencoder = None
@@ -207,7 +205,8 @@ class ESPnetASRModel(AbsESPnetModel):
         if self.ignore_id != -1:
             text = text.masked_fill(text == -1, self.ignore_id)
         text_lengths = self._dev(text_lengths, torch.long)
-        encoder_out, encoder_out_lens = self.encode(speech, speech_lengths, _seed=seed, _smax=sl_max)
+        encoder_out, encoder_out_lens = self.encode(speech, speech_lengths, _seed=seed, _smax=sl_max,
+                                                    _lens_host=kwargs.get("_lens_host"))
         self._last_encoder_out = (encoder_out, encoder_out_lens)
         stats = dict()
         loss_ctc = loss_att = acc_att = None
@@ -248,11 +247,17 @@ class ESPnetASRModel(AbsESPnetModel):
         smax = int(speech_lengths.max()) if smax is None else smax
         return self._dev(speech)[:, :smax], self._dev(speech_lengths, torch.long)
 
-    def encode(self, speech, speech_lengths, _seed=None, _smax=None):
-        """espnet_model.py:351-412 (feats -> normalize -> encoder)."""
+    def encode(self, speech, speech_lengths, _seed=None, _smax=None, _lens_host=None):
+        """espnet_model.py:351-412 (feats -> specaug (training) -> normalize -> encoder).
+        `_lens_host`: the lengths as host ints, when the caller has them (SpecAug's
+        equal-length test needs them on the host, time_warp.py:73)."""
         seed = self._next_seed() if _seed is None else _seed
+        if self.specaug is not None and self.training and _lens_host is None and speech_lengths.device.type == "cpu":
+            _lens_host = [int(v) for v in speech_lengths.tolist()]
         feats, feats_lengths = self._extract_feats(speech, speech_lengths, _smax)
         feats = feats.contiguous().float()
+        if self.specaug is not None and self.training:  # :365-366
+            feats, feats_lengths = self.specaug(feats, feats_lengths, lens_host=_lens_host)
         if self.normalize is not None:
             feats, feats_lengths = self.normalize(feats, feats_lengths)
         encoder_out, encoder_out_lens, _ = self.encoder(feats, feats_lengths, seed=seed)

@@ -3,7 +3,7 @@ class-choice registries of :109-188 for the names on the hot path.
 
 `build_model(args)` accepts the reference's YAML/argparse keys (input_size, token_list,
 encoder/encoder_conf, decoder/decoder_conf, ctc_conf, model_conf, normalize/normalize_conf,
-frontend, specaug) and builds the HIP-backed modules; names outside the hot path raise
+specaug/specaug_conf, frontend) and builds the HIP-backed modules; names outside the hot path raise
 NotImplementedError with the reason.
 """
 from __future__ import annotations
@@ -15,6 +15,7 @@ from ..asr.ctc import CTC
 from ..asr.decoder.transformer_decoder import TransformerDecoder
 from ..asr.encoder.conformer_encoder import ConformerEncoder
 from ..asr.espnet_model import ESPnetASRModel, UtteranceMVN
+from ..asr.specaug import SpecAug
 
 
 class ClassChoices:
@@ -44,6 +45,7 @@ decoder_choices = ClassChoices("decoder", dict(transformer=TransformerDecoder), 
 normalize_choices = ClassChoices("normalize", dict(utterance_mvn=UtteranceMVN),
                                  default="utterance_mvn", optional=True)
 model_choices = ClassChoices("model", dict(espnet=ESPnetASRModel), default="espnet")
+specaug_choices = ClassChoices("specaug", dict(specaug=SpecAug), default=None, optional=True)
 
 
 def _get(args, key, default=None):
@@ -63,8 +65,8 @@ def build_model(args) -> ESPnetASRModel:
     if input_size is None:
         raise NotImplementedError("feature frontends (STFT/log-mel) are a §8(f) next item: "
                                   "set input_size and feed features")
-    if _get(args, "specaug") not in (None, "none"):
-        raise NotImplementedError("specaug is a §8(f) next item")
+    spec_cls = specaug_choices.get_class(_get(args, "specaug"))
+    specaug = spec_cls(**(_get(args, "specaug_conf") or {})) if spec_cls else None
     norm_cls = normalize_choices.get_class(_get(args, "normalize", "utterance_mvn"))
     normalize = norm_cls(**(_get(args, "normalize_conf") or {})) if norm_cls else None
     enc_cls = encoder_choices.get_class(_get(args, "encoder", "conformer"))
@@ -76,6 +78,6 @@ def build_model(args) -> ESPnetASRModel:
                           **(_get(args, "decoder_conf") or {}))
     ctc = CTC(odim=vocab_size, encoder_output_size=encoder.output_size(), **(_get(args, "ctc_conf") or {}))
     model_cls = model_choices.get_class(_get(args, "model", "espnet") or "espnet")
-    return model_cls(vocab_size=vocab_size, frontend=None, specaug=None, normalize=normalize,
+    return model_cls(vocab_size=vocab_size, frontend=None, specaug=specaug, normalize=normalize,
                      preencoder=None, encoder=encoder, postencoder=None, decoder=decoder, ctc=ctc,
                      joint_network=None, token_list=token_list, **(_get(args, "model_conf") or {}))

@@ -35,6 +35,10 @@ class _Captured:
 class CapturedTrainStep:
     def __init__(self, model, optimizer, scheduler=None, *, grad_clip: float = 5.0, dp=None,
                  warmup: int = 2, enabled: bool = True):
+        if enabled and getattr(model, "specaug", None) is not None:
+            # SpecAug draws its warp/mask parameters on the host per step (the reference's
+            # torch.randint calls), which a replayed graph would freeze: run such steps eagerly
+            raise ValueError("CapturedTrainStep: a model with SpecAug trains eagerly (enabled=False)")
         self.model = model
         self.optimizer = optimizer
         self.scheduler = scheduler
@@ -70,7 +74,7 @@ class CapturedTrainStep:
         if maxlens is None:
             maxlens = self._maxlens(batch)
         if not self.enabled:
-            return self._eager(batch, None)
+            return self._eager(batch, maxlens)
         B, _, F = batch["speech"].shape
         key = (B, maxlens[0], F, maxlens[1])
         cap = self.graphs.get(key)

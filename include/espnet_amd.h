@@ -163,6 +163,19 @@ int ea_batchnorm_bwd(int rows, int C, const void* dz, int dz_dtype, const float*
  * x (B,T,F) f32 -> y = (x masked to valid frames) - per-utterance mean. F <= 256. */
 int ea_utterance_mvn(int B, int T, int F, const float* x, const long long* lens, float* y, void* stream);
 
+/* SpecAugment, espnet2/asr/specaug/specaug.py:95-102 = TimeWarp (layers/time_warp.py:9-88,
+ * bicubic, align_corners=False) -> MaskAlongAxis(freq) -> MaskAlongAxis(time)
+ * (layers/mask_along_axis.py:8-68, replace_with_zero), one pass over x (B,T,F) f32 -> y.
+ * The draws are the caller's (the reference's torch.randint calls, in its order):
+ *  warp  [B][2] (center, warped): center <= 0 leaves utterance b unwarped;
+ *  per_utt = 1: TimeWarp's per-utterance path (lengths differ): utterance b is warped over
+ *               its first lengths[b] frames and frames >= lengths[b] are zero (pad_list 0.0);
+ *          = 0: the equal-length path: the whole T axis is warped, nothing is zero-filled;
+ *  fmask [B][nf][2], tmask [B][nt][2]: (position, width) spans set to 0.
+ * Replaces the reference's per-utterance interpolate loop (time_warp.py:78-86). */
+int ea_specaug(int B, int T, int F, const float* x, const long long* lengths, const int* warp, int per_utt,
+               const int* fmask, int nf, const int* tmask, int nt, float* y, void* stream);
+
 /* encoder_out_lens of Conv2dSubsampling from the sliced mask, subsampling.py:91 +
  * conformer_encoder.py:374. */
 int ea_subsample_lens(int B, int T, const long long* ilens, long long* olens, void* stream);

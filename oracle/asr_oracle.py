@@ -405,3 +405,63 @@ class OracleTrainer:
             g["lr"] = warmup_lr(self.base_lr, self.step_num, self.warmup)
         self.opt.zero_grad()
         return loss.detach(), stats, gn
+
+
+# ---------------------------------------------------------------------------- SpecAug (C5)
+def _time_warp_one(x, window):
+    """layers/time_warp.py:9-46 on x (B, T, F): one draw, bicubic via ATen interpolate."""
+    t = x.shape[1]
+    if t - window <= window:
+        return x
+    center = torch.randint(window, t - window, (1,))[0]
+    warped = torch.randint(center - window, center + window, (1,))[0] + 1
+    x4 = x[:, None]
+    left = F.interpolate(x4[:, :, :center], (int(warped), x.shape[2]), mode="bicubic", align_corners=False)
+    right = F.interpolate(x4[:, :, center:], (t - int(warped), x.shape[2]), mode="bicubic", align_corners=False)
+    return torch.cat([left, right], dim=-2)[:, 0]
+
+
+def _mask_along_axis(spec, width_range, dim, num_mask):
+    """layers/mask_along_axis.py:8-68 (replace_with_zero=True)."""
+    B, D = spec.shape[0], spec.shape[dim]
+    length = torch.randint(width_range[0], width_range[1], (B, num_mask)).unsqueeze(2)
+    pos = torch.randint(0, max(1, D - int(length.max())), (B, num_mask)).unsqueeze(2)
+    aran = torch.arange(D)[None, None, :]
+    mask = ((pos <= aran) * (aran < (pos + length))).any(dim=1)
+    mask = mask.unsqueeze(2) if dim == 1 else mask.unsqueeze(1)
+    return spec.masked_fill(mask, 0.0)
+
+
+def specaug(x, lens, conf):
+    """specaug.py:95-102 with the conformer8 option set: TimeWarp (per-utterance when the
+    lengths differ, time_warp.py:73-86), freq MaskAlongAxis, time MaskAlongAxis or
+    MaskAlongAxisVariableMaxWidth (mask_along_axis.py:182-204).  Draws from torch's default
+    CPU generator in the reference's order."""
+    if conf.get("apply_time_warp", True):
+        w = conf.get("time_warp_window", 5)
+        if lens is None or all(int(le) == int(lens[0]) for le in lens):
+            x = _time_warp_one(x, w)
+        else:
+            ys = [_time_warp_one(x[i][None, : int(lens[i])], w)[0] for i in range(x.shape[0])]
+            out = x.new_zeros(x.shape[0], max(y.shape[0] for y in ys), x.shape[2])
+            for i, y in enumerate(ys):
+                out[i, : y.shape[0]] = y
+            x = out
+    if conf.get("apply_freq_mask", True):
+        r = conf.get("freq_mask_width_range", (0, 20))
+        r = (0, r) if isinstance(r, int) else tuple(r)
+        x = _mask_along_axis(x, r, 2, conf.get("num_freq_mask", 2))
+    if conf.get("apply_time_mask", True):
+        if conf.get("time_mask_width_range") is not None:
+            r = conf["time_mask_width_range"]
+            r = (0, r) if isinstance(r, int) else tuple(r)
+            x = _mask_along_axis(x, r, 1, conf.get("num_time_mask", 2))
+        else:
+            rr = conf["time_mask_width_ratio_range"]
+            rr = (0.0, rr) if isinstance(rr, float) else tuple(rr)
+            D = x.shape[1]
+            lo = max(0, math.floor(D * rr[0]))
+            hi = min(D, math.floor(D * rr[1]))
+            if hi > lo:
+                x = _mask_along_axis(x, (lo, hi), 1, conf.get("num_time_mask", 2))
+    return x

@@ -403,6 +403,91 @@ def capture_ddp(name="ddp2", cfg_name="tiny_hybrid"):
     print(f"{name}: -> {out_path}")
 
 
+SPECAUG_CONFS = {
+    # egs2/librispeech/asr1/conf/tuning/train_asr_conformer8.yaml:62-76
+    "conformer8": dict(apply_time_warp=True, time_warp_window=5, time_warp_mode="bicubic",
+                       apply_freq_mask=True, freq_mask_width_range=[0, 27], num_freq_mask=2,
+                       apply_time_mask=True, time_mask_width_ratio_range=[0.0, 0.05], num_time_mask=10),
+    # fixed-width time masks (MaskAlongAxis on time), no warp
+    "fixed_time": dict(apply_time_warp=False, apply_freq_mask=True, freq_mask_width_range=[0, 30],
+                       num_freq_mask=2, apply_time_mask=True, time_mask_width_range=[0, 40], num_time_mask=2),
+}
+
+
+def capture_specaug(name="specaug"):
+    """espnet2/asr/specaug/specaug.py under fixed torch seeds: equal-length batches (one
+    warp for the batch), ragged batches (per-utterance warp + zero padding, including an
+    utterance too short to warp) and the fixed-width time-mask variant."""
+    from espnet2.asr.specaug.specaug import SpecAug
+
+    cases = {
+        "eq": ("conformer8", [120, 120, 120], 80, 11),
+        "ragged": ("conformer8", [150, 97, 64, 9, 150], 80, 12),
+        "eq_long": ("conformer8", [1000, 1000], 80, 13),
+        "fixed": ("fixed_time", [200, 180], 80, 14),
+    }
+    out = {"cfg": np.array(json.dumps({"confs": SPECAUG_CONFS, "cases": cases}))}
+    for key, (conf_name, lens, Fd, seed) in cases.items():
+        gen = torch.Generator().manual_seed(100 + seed)
+        T = max(lens)
+        x = torch.randn(len(lens), T, Fd, generator=gen)
+        for i, le in enumerate(lens):
+            x[i, le:] = 0.0  # CommonCollateFn float_pad = 0.0
+        xl = torch.tensor(lens, dtype=torch.long)
+        torch.manual_seed(seed)
+        y, yl = SpecAug(**SPECAUG_CONFS[conf_name])(x.clone(), xl)
+        out[f"{key}.x"] = np32(x)
+        out[f"{key}.lens"] = xl.numpy()
+        out[f"{key}.y"] = np32(y)
+    path = os.path.join(OUT, f"{name}.npz")
+    np.savez_compressed(path, **out)
+    print(f"{name}: {sorted(out)} -> {path}")
+
+
+def capture_sampler(name="sampler"):
+    """espnet2/samplers/num_elements_batch_sampler.py on synthetic shape files: speech
+    (T, 80) and text (L,) shapes with ties, every sort option, min_batch_size
+    redistribution, drop_last and padding=False."""
+    import tempfile
+
+    from espnet2.samplers.num_elements_batch_sampler import NumElementsBatchSampler
+
+    rng = np.random.RandomState(5)
+    n = 60
+    Ts = rng.randint(200, 2001, size=n)
+    Ts[5] = Ts[6] = Ts[7]  # ties keep file order
+    d = tempfile.mkdtemp(prefix="shapes_")
+    sp, tx = os.path.join(d, "speech_shape"), os.path.join(d, "text_shape")
+    with open(sp, "w") as f:
+        for i, t in enumerate(Ts):
+            f.write(f"utt{i:03d} {t},80\n")
+    with open(tx, "w") as f:
+        for i, t in enumerate(Ts):
+            f.write(f"utt{i:03d} {max(1, round(t / 25))}\n")
+    settings = {
+        "default": dict(batch_bins=400000, shape_files=[sp]),
+        "two_files": dict(batch_bins=600000, shape_files=[sp, tx]),
+        "desc_asc": dict(batch_bins=300000, shape_files=[sp], sort_in_batch="ascending", sort_batch="descending"),
+        "min_bs": dict(batch_bins=1000000, shape_files=[sp], min_batch_size=9),
+        "drop_last": dict(batch_bins=700000, shape_files=[sp], drop_last=True),
+        "nopad": dict(batch_bins=500000, shape_files=[sp, tx], padding=False),
+    }
+    out = {"cfg": np.array(json.dumps({k: {kk: (vv if kk != "shape_files" else len(vv)) for kk, vv in v.items()}
+                                       for k, v in settings.items()})),
+           "T": Ts.astype(np.int64)}
+    for key, kw in settings.items():
+        s = NumElementsBatchSampler(**kw)
+        flat, sizes = [], []
+        for b in s:
+            flat += [int(k[3:]) for k in b]
+            sizes.append(len(b))
+        out[f"{key}.flat"] = np.array(flat, np.int64)
+        out[f"{key}.sizes"] = np.array(sizes, np.int64)
+    path = os.path.join(OUT, f"{name}.npz")
+    np.savez_compressed(path, **out)
+    print(f"{name}: {len(settings)} settings -> {path}")
+
+
 if __name__ == "__main__":
     os.makedirs(OUT, exist_ok=True)
     which = sys.argv[1:] or ["models", "train", "ops", "ddp"]
@@ -416,3 +501,7 @@ if __name__ == "__main__":
         capture_lsm_op()
     if "ddp" in which:
         capture_ddp()
+    if "specaug" in which:
+        capture_specaug()
+    if "sampler" in which:
+        capture_sampler()

@@ -73,3 +73,38 @@ def test_model_bf16_amp_close(name):
         num += float(((mine - torch.from_numpy(g).double()) ** 2).sum())
         den += float((torch.from_numpy(g).double() ** 2).sum())
     assert (num / den) ** 0.5 < 5e-2, (num / den) ** 0.5
+
+
+def test_model_with_specaug_matches_oracle():
+    """C5 path: ESPnetASRModel with SpecAug (conformer8 options) in training mode vs the
+    oracle's SpecAug restatement + OracleASR on the same weights under the same torch seed
+    (specaug.py draws come first in the step, espnet_model.py:365-366, so both draw the
+    same warp/mask parameters).  Dropout is 0 in the tiny config."""
+    from oracle.asr_oracle import OracleASR, specaug as ora_specaug
+    from espnet_amd.asr.specaug import SpecAug
+    conf = dict(apply_time_warp=True, time_warp_window=5, time_warp_mode="bicubic", apply_freq_mask=True,
+                freq_mask_width_range=[0, 27], num_freq_mask=2, apply_time_mask=True,
+                time_mask_width_ratio_range=[0.0, 0.05], num_time_mask=10)
+    cfg, d = load("tiny_hybrid")
+    torch.manual_seed(0)
+    m = build(cfg)
+    w = {k: torch.from_numpy(v) for k, v in section(d, "w").items()}
+    m.load_state_dict(w)
+    m.specaug = SpecAug(**conf)
+    m.prepare("cuda", amp=False)
+    m.train()
+    inp = {k: torch.from_numpy(v) for k, v in section(d, "in").items()}
+    torch.manual_seed(77)
+    loss, stats, _ = m(**inp)
+    loss.backward()
+    torch.cuda.synchronize()
+    ora = OracleASR(cfg, w)
+    torch.manual_seed(77)
+    T = int(inp["speech_lengths"].max())
+    sp = ora_specaug(inp["speech"][:, :T].clone(), inp["speech_lengths"], conf)
+    ref_loss, ref_stats, _ = ora(speech=sp, speech_lengths=inp["speech_lengths"], text=inp["text"].clone(),
+                                 text_lengths=inp["text_lengths"])
+    ref_loss.backward()
+    np.testing.assert_allclose(loss.item(), ref_loss.item(), rtol=1e-5, atol=1e-4)
+    g = dict(m.named_parameters())["encoder.embed.conv.0.weight"].grad.cpu().numpy()
+    np.testing.assert_allclose(g, ora.params["encoder.embed.conv.0.weight"].grad.numpy(), atol=5e-5, rtol=1e-3)
