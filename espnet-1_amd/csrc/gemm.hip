@@ -1108,7 +1108,9 @@ static int gemm_impl(int dtype, int a_kmajor, int b_kmajor, int M, int N, int K,
   int splitk = 1;
   // 128x128-equivalent tiles: split K only when the grid cannot fill the CUs
   const long tiles = max(1L, (long)p.tiles_m * p.tiles_n * nz * (p.bm * p.bn) / (128 * 128));
-  if (workspace && tiles < 200 && K >= 8 * KT) {
+  // K >= 1024: a K = 512 GEMM split two ways costs more in the reduce pass than it gains
+  // (decoder 1312x2048x512: 23.1 us split vs 10.5 us unsplit, scripts/gemm_splitk_ab.py)
+  if (workspace && tiles < 200 && K >= 16 * KT && K >= 1024) {
     splitk = (int)((384 + tiles - 1) / tiles);
     splitk = min(splitk, K / (4 * KT));
     splitk = min(splitk, 16);

@@ -122,6 +122,114 @@ __global__ __launch_bounds__(256) void ctc_lattice_kernel(CtcP p) {
   }
 }
 
+// Same recursion as ctc_lattice_kernel (identical arithmetic, bit-identical results), with
+// the serial chain's global loads taken off it: alpha and beta run in two workgroups of
+// their own (blockIdx.x = 2b + dir), each state's label / skip rule lives in registers, and
+// the emissions (logit of the state's label, row lse) for time steps are staged through LDS
+// in chunks of CTC_TC steps, the next chunk's loads in flight while the current chunk's
+// steps run.  One state per thread: S = 2L+1 <= 256; longer label sequences take the
+// one-workgroup kernel above.
+constexpr int CTC_TC = 32, CTC_NR = 16;  // steps per chunk; staged values per thread
+
+__global__ __launch_bounds__(256) void ctc_lattice2_kernel(CtcP p) {
+  extern __shared__ double sh[];
+  const int b = blockIdx.x >> 1, dir = blockIdx.x & 1, tid = threadIdx.x;
+  const int Tb = (int)min((long long)p.T, p.hlens[b]);
+  const int L = (int)p.ylens[b];
+  const int S = 2 * L + 1, U = p.Lmax + 1;
+  double* prev = sh;
+  double* cur = sh + 256;
+  float* em = (float*)(sh + 512);   // [2][CTC_TC][U] logit of unique label u at step k
+  float* ls = em + 2 * CTC_TC * U;  // [2][CTC_TC]    row lse at step k
+  double* out = (dir ? p.beta : p.alpha) + (long)b * p.T * p.Smax;
+  if (Tb <= 0) {
+    if (dir == 0 && tid == 0) { p.nll[b] = (L == 0) ? 0.0 : INFINITY; p.loss_utt[b] = 0.f; }
+    return;
+  }
+  const long long* ys = p.ys + (long)b * p.ldys;
+  // this thread's state: unique-label index u (0 = blank), label, skip transition allowed
+  const int s = tid;
+  const int u = (s & 1) ? (s + 1) >> 1 : 0;
+  const int lab = s < S ? ((s & 1) ? (int)ys[s >> 1] : 0) : 0;
+  const int s2 = dir ? s + 2 : s - 2;  // skip source state
+  const bool skip = s < S && s2 >= 0 && s2 < S && lab != 0 && lab != ((s2 & 1) ? (int)ys[s2 >> 1] : 0);
+  const int s1 = dir ? s + 1 : s - 1;
+  const bool step1 = s < S && s1 >= 0 && s1 < S;
+  auto tmap = [&](int k) { return dir ? Tb - 1 - k : k; };
+  // staged element e of a chunk: e < CTC_TC*U -> (kk = e / U, uu = e % U) logit; else lse of kk
+  const int NE = CTC_TC * U + CTC_TC;
+  auto fetch = [&](int k0, float (&r)[CTC_NR]) {
+#pragma unroll
+    for (int i = 0; i < CTC_NR; ++i) {
+      const int e = tid + 256 * i;
+      float v = 0.f;
+      if (e < NE) {
+        const int kk = e < CTC_TC * U ? e / U : e - CTC_TC * U;
+        const int k = k0 + kk;
+        if (k < Tb) {
+          const long row = (long)b * p.T + tmap(k);
+          if (e < CTC_TC * U) {
+            const int uu = e - kk * U;
+            const int lb = uu == 0 ? 0 : (uu <= L ? (int)ys[uu - 1] : 0);
+            v = p.logits[row * p.ldt + lb];
+          } else {
+            v = p.lse[row];
+          }
+        }
+      }
+      r[i] = v;
+    }
+  };
+  auto stash = [&](int buf, const float (&r)[CTC_NR]) {
+#pragma unroll
+    for (int i = 0; i < CTC_NR; ++i) {
+      const int e = tid + 256 * i;
+      if (e < CTC_TC * U) em[buf * CTC_TC * U + e] = r[i];
+      else if (e < NE) ls[buf * CTC_TC + e - CTC_TC * U] = r[i];
+    }
+  };
+  float r[CTC_NR];
+  fetch(0, r);
+  stash(0, r);
+  __syncthreads();
+  const int nchunk = (Tb + CTC_TC - 1) / CTC_TC;
+  for (int c = 0; c < nchunk; ++c) {
+    const int buf = c & 1;
+    if (c + 1 < nchunk) fetch((c + 1) * CTC_TC, r);  // in flight under this chunk's steps
+    const float* emc = em + buf * CTC_TC * U;
+    const float* lsc = ls + buf * CTC_TC;
+    const int kend = min(CTC_TC, Tb - c * CTC_TC);
+    for (int kk = 0; kk < kend; ++kk) {
+      const int k = c * CTC_TC + kk, t = tmap(k);
+      const double lp = (double)emc[kk * U + u] - (double)lsc[kk];
+      double a;
+      if (k == 0) {
+        a = -INFINITY;
+        if (s < S && (dir ? s >= S - 2 : s < 2)) a = lp;
+      } else {
+        a = prev[s];
+        if (step1) a = lae(a, prev[s1]);
+        if (skip) a = lae(a, prev[s2]);
+        a = a == -INFINITY ? a : a + lp;
+      }
+      if (s < S) {
+        cur[s] = a;
+        out[(long)t * p.Smax + s] = a;
+      }
+      __syncthreads();
+      double* tmp = prev; prev = cur; cur = tmp;
+    }
+    if (c + 1 < nchunk) stash(buf ^ 1, r);
+    __syncthreads();
+  }
+  if (dir == 0 && tid == 0) {
+    double l = prev[S - 1];
+    if (S >= 2) l = lae(l, prev[S - 2]);
+    p.nll[b] = -l;
+    p.loss_utt[b] = isinf(-l) ? 0.f : (float)(-l);  // zero_infinity
+  }
+}
+
 // loss = sum_b loss_utt / B  (ctc.py:58-60); one block
 __global__ void ctc_reduce_kernel(int B, const float* __restrict__ loss_utt, float* __restrict__ loss) {
   __shared__ double red[16];
@@ -282,7 +390,13 @@ extern "C" int ea_ctc_loss_fwd(int B, int T, int V, const float* logits, long ld
   EA_LAUNCH_CHECK();
   const int Smax = 2 * Lmax + 1;
   CtcP p{B, T, V, Lmax, Smax, logits, ldt, lse, hlens, ys, ldys, ylens, alpha, beta, nll, loss_utt};
-  hipLaunchKernelGGL(ctc_lattice_kernel, dim3(B), dim3(256), 2 * Smax * sizeof(double), st, p);
+  const int U = Lmax + 1;
+  if (Smax <= 256 && CTC_TC * U + CTC_TC <= 256 * CTC_NR) {
+    const size_t sm = 512 * sizeof(double) + (size_t)2 * CTC_TC * (U + 1) * sizeof(float);
+    hipLaunchKernelGGL(ctc_lattice2_kernel, dim3(2 * B), dim3(256), sm, st, p);
+  } else {
+    hipLaunchKernelGGL(ctc_lattice_kernel, dim3(B), dim3(256), 2 * Smax * sizeof(double), st, p);
+  }
   EA_LAUNCH_CHECK();
   hipLaunchKernelGGL(ctc_reduce_kernel, dim3(1), dim3(256), 0, st, B, loss_utt, loss);
   EA_LAUNCH_CHECK();

@@ -16,7 +16,37 @@ import torch
 from torch import nn
 
 from .common import (ACT_RELU, EPI_ACT, EPI_DACT, EPI_RESID, EPI_STORE, F32, Bound, attn_bwd,
-                     attn_fwd, empty, lib, ln_bwd, ln_fwd, ops, site_seed)
+                     attn_fwd, empty, fused_attn_ok, lib, ln_bwd, ln_fwd, ops, site_seed)
+
+
+def _mha_fwd(q, k, v, *, B, H, T1, T2, dk, ldq, ldk, ldv, klen, causal, scale, p, seed, cd):
+    """Scaled dot-product core of MultiHeadedAttention (attention.py:63-93) with the key
+    padding (+ causal) mask: the fused flash kernel (relattn.hip, no positional term) when
+    eligible, else the unfused GEMM + softmax path.  Returns (O, saved state)."""
+    if fused_attn_ok(cd, dk, T1, T2):
+        O = empty(B * T1, H * dk, dtype=cd, device=q.device)
+        lse = empty(B * H * T1, device=q.device)
+        lib.ea_attn_fused_fwd(B, H, T1, T2, dk, q.data_ptr(), ldq, k.data_ptr(), ldk, v.data_ptr(), ldv,
+                              None, None, None, 0, klen.data_ptr(), int(causal), scale, float(p), seed,
+                              O.data_ptr(), H * dk, lse.data_ptr(), ops.stream())
+        return O, ("fused", O, lse)
+    O, P, Pd, ldT = attn_fwd(q, k, v, B=B, H=H, T1=T1, T2=T2, dk=dk, ldq=ldq, ldk=ldk, ldv=ldv, klen=klen,
+                             causal=causal, scale=scale, p=p, seed=seed, cd=cd)
+    return O, ("unfused", P, Pd, ldT)
+
+
+def _mha_bwd(st, dO, q, k, v, *, B, H, T1, T2, dk, ldq, ldk, ldv, klen, causal, scale, p, seed, cd,
+             dq, lddq, dk_, lddk, dv, lddv):
+    if st[0] == "fused":
+        _, O, lse = st
+        lib.ea_attn_fused_bwd(B, H, T1, T2, dk, q.data_ptr(), ldq, k.data_ptr(), ldk, v.data_ptr(), ldv,
+                              None, None, None, 0, klen.data_ptr(), int(causal), scale, float(p), seed,
+                              O.data_ptr(), H * dk, lse.data_ptr(), dO.data_ptr(), H * dk, dq.data_ptr(), lddq,
+                              dk_.data_ptr(), lddk, dv.data_ptr(), lddv, None, 0, ops.stream())
+        return
+    _, P, Pd, ldT = st
+    attn_bwd(dO, q, k, v, P, Pd, ldT, B=B, H=H, T1=T1, T2=T2, dk=dk, ldq=ldq, ldk=ldk, ldv=ldv, scale=scale,
+             p=p, seed=seed, cd=cd, dq=dq, lddq=lddq, dk_=dk_, lddk=lddk, dv=dv, lddv=lddv)
 from .conformer import LayerNorm, MultiHeadedAttention, PositionwiseFeedForward
 
 
@@ -126,9 +156,9 @@ class DecoderFn(torch.autograd.Function):
                                 shape=(3 * d, d)), qkv,
                        epi=ops.make_epi(bias=b.f(sa + "linear_q.bias", sa + "linear_k.bias",
                                                  sa + "linear_v.bias", shape=(3 * d,))))
-            O1, P1, Pd1, ldT1 = attn_fwd(qkv, qkv[:, d:], qkv[:, 2 * d:], B=B, H=H, T1=L, T2=L, dk=dk,
-                                         ldq=3 * d, ldk=3 * d, ldv=3 * d, klen=ys_in_lens, causal=True,
-                                         scale=scale, p=p_sa, seed=sd(l, 1), cd=cd)
+            O1, st1 = _mha_fwd(qkv, qkv[:, d:], qkv[:, 2 * d:], B=B, H=H, T1=L, T2=L, dk=dk,
+                               ldq=3 * d, ldk=3 * d, ldv=3 * d, klen=ys_in_lens, causal=True,
+                               scale=scale, p=p_sa, seed=sd(l, 1), cd=cd)
             x1 = empty(N, d, device=dev)
             ops.linear(O1, b.w(sa + "linear_out.weight"), x1,
                        epi=ops.make_epi(EPI_RESID, bias=b.f(sa + "linear_out.bias"), resid=x,
@@ -139,9 +169,9 @@ class DecoderFn(torch.autograd.Function):
             ops.linear(xn2, b.w(xa + "linear_q.weight"), q2, epi=ops.make_epi(bias=b.f(xa + "linear_q.bias")))
             k2 = kv[:, 2 * d * l:]
             v2 = kv[:, 2 * d * l + d:]
-            O2, P2, Pd2, ldT2 = attn_fwd(q2, k2, v2, B=B, H=H, T1=L, T2=Tm, dk=dk, ldq=d, ldk=ldkv,
-                                         ldv=ldkv, klen=hlens, causal=False, scale=scale, p=p_src,
-                                         seed=sd(l, 3), cd=cd)
+            O2, st2 = _mha_fwd(q2, k2, v2, B=B, H=H, T1=L, T2=Tm, dk=dk, ldq=d, ldk=ldkv,
+                               ldv=ldkv, klen=hlens, causal=False, scale=scale, p=p_src,
+                               seed=sd(l, 3), cd=cd)
             x2 = empty(N, d, device=dev)
             ops.linear(O2, b.w(xa + "linear_out.weight"), x2,
                        epi=ops.make_epi(EPI_RESID, bias=b.f(xa + "linear_out.bias"), resid=x1,
@@ -159,8 +189,8 @@ class DecoderFn(torch.autograd.Function):
             ops.linear(a, b.w(ff + "w_2.weight"), x3,
                        epi=ops.make_epi(EPI_RESID, bias=b.f(ff + "w_2.bias"), resid=x2,
                                         drop_p=p, seed=sd(l, 6)))
-            saved.append((x, x1, x2, (xn1, mu1, rs1, qkv, O1, P1, Pd1, ldT1),
-                          (xn2, mu2, rs2, q2, O2, P2, Pd2, ldT2), (xn3, mu3, rs3, h, a)))
+            saved.append((x, x1, x2, (xn1, mu1, rs1, qkv, O1, st1),
+                          (xn2, mu2, rs2, q2, O2, st2), (xn3, mu3, rs3, h, a)))
             x = x3
         xf, muf, rsf = ln_fwd(x, b, "after_norm", cd)
         logits = empty(N, V, device=dev)
@@ -168,7 +198,7 @@ class DecoderFn(torch.autograd.Function):
                    epi=ops.make_epi(bias=b.f("output_layer.bias")))
         ctx.dec = dec
         ctx.meta = (B, Tm, L, d, H, dk, nb, p, p_sa, p_src, p_pos, seed, scale)
-        ctx.save = (mem, kv, ys_in, saved, x, xf, muf, rsf)
+        ctx.save = (mem, kv, ys_in, saved, x, xf, muf, rsf, hlens, ys_in_lens)
         return logits.view(B, L, V)
 
     @staticmethod
@@ -177,7 +207,7 @@ class DecoderFn(torch.autograd.Function):
         b = dec._b
         cd = b.cd
         B, Tm, L, d, H, dk, nb, p, p_sa, p_src, p_pos, seed, scale = ctx.meta
-        mem, kv, ys_in, saved, xlast, xf, muf, rsf = ctx.save
+        mem, kv, ys_in, saved, xlast, xf, muf, rsf, hlens, ys_in_lens = ctx.save
         ctx.save = None
         sd = lambda l, s: site_seed(seed, 100 + l, s)  # noqa: E731
         N, Nm = B * L, B * Tm
@@ -214,7 +244,7 @@ class DecoderFn(torch.autograd.Function):
             ops.linear_dx(dh, b.w(ff + "w_1.weight"), dxn)
             ln_bwd(dxn, x2, b, n + "norm3", mu3, rs3, dx, accumulate=True)
             # source attention
-            xn2, mu2, rs2, q2, O2, P2, Pd2, ldT2 = s2
+            xn2, mu2, rs2, q2, O2, st2 = s2
             dv = empty(N, d, dtype=cd, device=dev)
             ops.scale_dropout(dx, dv, p=p, seed=sd(l, 4))
             with ops.wgrad(dv, O2):
@@ -223,9 +253,10 @@ class DecoderFn(torch.autograd.Function):
             dO = empty(N, d, dtype=cd, device=dev)
             ops.linear_dx(dv, b.w(xa + "linear_out.weight"), dO)
             dq = empty(N, d, dtype=cd, device=dev)
-            attn_bwd(dO, q2, kv[:, 2 * d * l:], kv[:, 2 * d * l + d:], P2, Pd2, ldT2, B=B, H=H, T1=L,
-                     T2=Tm, dk=dk, ldq=d, ldk=ldkv, ldv=ldkv, scale=scale, p=p_src, seed=sd(l, 3), cd=cd,
-                     dq=dq, lddq=d, dk_=dkv[:, 2 * d * l:], lddk=ldkv, dv=dkv[:, 2 * d * l + d:], lddv=ldkv)
+            _mha_bwd(st2, dO, q2, kv[:, 2 * d * l:], kv[:, 2 * d * l + d:], B=B, H=H, T1=L, T2=Tm, dk=dk,
+                     ldq=d, ldk=ldkv, ldv=ldkv, klen=hlens, causal=False, scale=scale, p=p_src,
+                     seed=sd(l, 3), cd=cd, dq=dq, lddq=d, dk_=dkv[:, 2 * d * l:], lddk=ldkv,
+                     dv=dkv[:, 2 * d * l + d:], lddv=ldkv)
             with ops.wgrad(dq, xn2):
                 ops.colsum(dq, b.g(xa + "linear_q.bias"))
                 ops.linear_dw(dq, xn2, b.g(xa + "linear_q.weight"), accumulate=True)
@@ -233,7 +264,7 @@ class DecoderFn(torch.autograd.Function):
             ops.linear_dx(dq, b.w(xa + "linear_q.weight"), dxn)
             ln_bwd(dxn, x1, b, n + "norm2", mu2, rs2, dx, accumulate=True)
             # self attention
-            xn1, mu1, rs1, qkv, O1, P1, Pd1, ldT1 = s1
+            xn1, mu1, rs1, qkv, O1, st1 = s1
             dv = empty(N, d, dtype=cd, device=dev)
             ops.scale_dropout(dx, dv, p=p, seed=sd(l, 2))
             with ops.wgrad(dv, O1):
@@ -242,9 +273,10 @@ class DecoderFn(torch.autograd.Function):
             dO = empty(N, d, dtype=cd, device=dev)
             ops.linear_dx(dv, b.w(sa + "linear_out.weight"), dO)
             dqkv = empty(N, 3 * d, dtype=cd, device=dev)
-            attn_bwd(dO, qkv, qkv[:, d:], qkv[:, 2 * d:], P1, Pd1, ldT1, B=B, H=H, T1=L, T2=L, dk=dk,
-                     ldq=3 * d, ldk=3 * d, ldv=3 * d, scale=scale, p=p_sa, seed=sd(l, 1), cd=cd,
-                     dq=dqkv, lddq=3 * d, dk_=dqkv[:, d:], lddk=3 * d, dv=dqkv[:, 2 * d:], lddv=3 * d)
+            _mha_bwd(st1, dO, qkv, qkv[:, d:], qkv[:, 2 * d:], B=B, H=H, T1=L, T2=L, dk=dk,
+                     ldq=3 * d, ldk=3 * d, ldv=3 * d, klen=ys_in_lens, causal=True, scale=scale, p=p_sa,
+                     seed=sd(l, 1), cd=cd, dq=dqkv, lddq=3 * d, dk_=dqkv[:, d:], lddk=3 * d,
+                     dv=dqkv[:, 2 * d:], lddv=3 * d)
             wn = (sa + "linear_q.weight", sa + "linear_k.weight", sa + "linear_v.weight")
             bn = (sa + "linear_q.bias", sa + "linear_k.bias", sa + "linear_v.bias")
             with ops.wgrad(dqkv, xn1):

@@ -18,10 +18,3 @@ for tile in [(0, 0), (64, 128), (128, 128), (256, 256)]:
     bg.bench("ffn_w2 fwd RESID", dt, 7968, 512, 2048, 1, 1, epi="resid")
     bg.bench("ffn_w1 fwd bf16", dt, 7968, 2048, 512, 1, 1, cdt=torch.bfloat16)
 lib.ea_gemm_set_tile(0, 0)
-for mode in (0, 1):
-    lib.ea_gemm_set_splitk_mode(mode)
-    print("splitk inlaunch", mode)
-    bg.bench("ffn_w1 dW", dt, 2048, 512, 7968, 0, 0)
-    bg.bench("att dW", dt, 512, 512, 7968, 0, 0)
-    bg.bench("dec ffn w2 RESID", dt, 1312, 512, 2048, 1, 1, epi="resid")
-lib.ea_gemm_set_splitk_mode(1)
