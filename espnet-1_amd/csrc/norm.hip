@@ -267,6 +267,162 @@ __global__ __launch_bounds__(256) void ln_bwd_dx_kernel(int rows, int d, const T
   }
 }
 
+// ---------------------------------------------------------------- vectorised LayerNorm
+// One wave64 per row; lane l owns the 8-column chunks c = l + 64*j (j < NJ), moved with
+// 16-B loads/stores (f32: 2 x float4, bf16: 1 x uint4).  d % 8 == 0, d <= 512*NJ.
+template <typename T> EA_DEV void ld8(const T* p, float (&v)[8]);
+template <> EA_DEV void ld8<float>(const float* p, float (&v)[8]) {
+  const float4 a = *(const float4*)p, b = *(const float4*)(p + 4);
+  v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+}
+template <> EA_DEV void ld8<bf16>(const bf16* p, float (&v)[8]) {
+  const uint4 u = *(const uint4*)p;
+  const bf16* e = (const bf16*)&u;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) v[i] = (float)e[i];
+}
+template <typename T> EA_DEV void st8(T* p, const float (&v)[8]);
+template <> EA_DEV void st8<float>(float* p, const float (&v)[8]) {
+  *(float4*)p = make_float4(v[0], v[1], v[2], v[3]);
+  *(float4*)(p + 4) = make_float4(v[4], v[5], v[6], v[7]);
+}
+template <> EA_DEV void st8<bf16>(bf16* p, const float (&v)[8]) {
+  union { uint4 u; bf16 e[8]; } t;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) t.e[i] = (bf16)v[i];
+  *(uint4*)p = t.u;
+}
+
+template <int NJ, typename TO>
+__global__ __launch_bounds__(256) void ln_fwd_vec_kernel(int rows, int d, const float* __restrict__ x, long ldx,
+                                                         const float* __restrict__ g, const float* __restrict__ b,
+                                                         float eps, TO* __restrict__ y, long ldy,
+                                                         float* __restrict__ mean_out, float* __restrict__ rstd_out) {
+  const int lane = threadIdx.x & 63;
+  const int r = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (r >= rows) return;
+  const float* xr = x + (long)r * ldx;
+  float v[NJ][8];
+  float s = 0.f;
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) {
+    const int c = (lane + 64 * j) * 8;
+    if (c < d) {
+      ld8(xr + c, v[j]);
+    } else {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) v[j][i] = 0.f;
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i) s += v[j][i];
+  }
+  const float mu = wave_sum(s) / d;
+  float ss = 0.f;
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) {
+    const int c = (lane + 64 * j) * 8;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const float t = c < d ? v[j][i] - mu : 0.f;
+      ss += t * t;
+    }
+  }
+  const float rs = rsqrtf(wave_sum(ss) / d + eps);
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) {
+    const int c = (lane + 64 * j) * 8;
+    if (c >= d) continue;
+    float gg[8], bb[8], o[8];
+    ld8(g + c, gg);
+    ld8(b + c, bb);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) o[i] = (v[j][i] - mu) * rs * gg[i] + bb[i];
+    st8(y + (long)r * ldy + c, o);
+  }
+  if (lane == 0) {
+    mean_out[r] = mu;
+    rstd_out[r] = rs;
+  }
+}
+
+// dx (+)= rstd*(dxh - mean(dxh) - xh*mean(dxh*xh)) with dxh = dy*gamma, and this block's
+// partial dgamma = sum dy*xh, dbeta = sum dy over its rows (part[blk][0:d], part[blk][d:2d];
+// the 4 waves' sums combined in fixed order), all from one read of dy and x.
+template <int NJ, typename TI>
+__global__ __launch_bounds__(256) void ln_bwd_vec_kernel(int rows, int d, const TI* __restrict__ dy, long lddy,
+                                                         const float* __restrict__ x, long ldx,
+                                                         const float* __restrict__ g, const float* __restrict__ mean,
+                                                         const float* __restrict__ rstd, float* __restrict__ dx,
+                                                         long lddx, int accumulate, int rows_per_blk,
+                                                         float* __restrict__ part) {
+  __shared__ float red[4][2][512 * NJ];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  float gg[NJ][8], pg[NJ][8], pb[NJ][8];
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) {
+    const int c = (lane + 64 * j) * 8;
+    if (c < d) ld8(g + c, gg[j]);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) pg[j][i] = pb[j][i] = 0.f;
+  }
+  const int r0 = blockIdx.x * rows_per_blk, r1 = min(rows, r0 + rows_per_blk);
+  for (int r = r0 + w; r < r1; r += 4) {
+    const float mu = mean[r], rs = rstd[r];
+    float xh[NJ][8], dg[NJ][8];
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      const int c = (lane + 64 * j) * 8;
+      if (c < d) {
+        float xv[8], dv[8];
+        ld8(x + (long)r * ldx + c, xv);
+        ld8(dy + (long)r * lddy + c, dv);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          xh[j][i] = (xv[i] - mu) * rs;
+          dg[j][i] = dv[i] * gg[j][i];
+          s1 += dg[j][i];
+          s2 += dg[j][i] * xh[j][i];
+          pg[j][i] += dv[i] * xh[j][i];
+          pb[j][i] += dv[i];
+        }
+      } else {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) xh[j][i] = dg[j][i] = 0.f;
+      }
+    }
+    s1 = wave_sum(s1) / d;
+    s2 = wave_sum(s2) / d;
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      const int c = (lane + 64 * j) * 8;
+      if (c >= d) continue;
+      float* o = dx + (long)r * lddx + c;
+      float v[8], prev[8];
+      if (accumulate) ld8(o, prev);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) v[i] = rs * (dg[j][i] - s1 - xh[j][i] * s2) + (accumulate ? prev[i] : 0.f);
+      st8(o, v);
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) {
+    const int c = (lane + 64 * j) * 8;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      if (c + i < 512 * NJ) {
+        red[w][0][c + i] = pg[j][i];
+        red[w][1][c + i] = pb[j][i];
+      }
+    }
+  }
+  __syncthreads();
+  for (int c = threadIdx.x; c < d; c += blockDim.x) {
+    part[(long)blockIdx.x * 2 * d + c] = (red[0][0][c] + red[1][0][c]) + (red[2][0][c] + red[3][0][c]);
+    part[(long)blockIdx.x * 2 * d + d + c] = (red[0][1][c] + red[1][1][c]) + (red[2][1][c] + red[3][1][c]);
+  }
+}
+
 // ---------------------------------------------------------------- BatchNorm1d (train)
 // Stats over all rows (padding included, as the reference's BatchNorm1d sees them).
 // Pass 1: per-block shifted sums (shift = row 0) -> fp64 combine in bn_finalize.
@@ -582,8 +738,22 @@ extern "C" int ea_layernorm_fwd(int rows, int d, const float* x, long ldx, const
                                 float* mean, float* rstd, void* stream) {
   EA_ENTRY();
   if (rows == 0) return 0;
-  dim3 grid(ln_blocks(rows)), blk(256);
   hipStream_t st = (hipStream_t)stream;
+  const bool vec = d % 8 == 0 && d <= 1024 && ldx % 4 == 0 && ldy % 8 == 0 && ((uintptr_t)x % 16) == 0 &&
+                   ((uintptr_t)y % 16) == 0 && ((uintptr_t)gamma % 16) == 0 && ((uintptr_t)beta % 16) == 0;
+  if (vec) {
+    dim3 g1(ea_cdiv(rows, 4)), b1(256);
+#define EA_LNF(NJ)                                                                                       \
+  if (y_dtype == EA_BF16)                                                                                \
+    hipLaunchKernelGGL((ln_fwd_vec_kernel<NJ, bf16>), g1, b1, 0, st, rows, d, x, ldx, gamma, beta, eps, (bf16*)y, ldy, mean, rstd); \
+  else                                                                                                   \
+    hipLaunchKernelGGL((ln_fwd_vec_kernel<NJ, float>), g1, b1, 0, st, rows, d, x, ldx, gamma, beta, eps, (float*)y, ldy, mean, rstd);
+    if (d <= 512) { EA_LNF(1) } else { EA_LNF(2) }
+#undef EA_LNF
+    EA_LAUNCH_CHECK();
+    return 0;
+  }
+  dim3 grid(ln_blocks(rows)), blk(256);
   if (y_dtype == EA_BF16)
     EA_LN_DISPATCH(ln_fwd_kernel, bf16, grid, blk, 0, st, rows, d, x, ldx, gamma, beta, eps, (bf16*)y, ldy, mean, rstd);
   else
@@ -610,6 +780,28 @@ extern "C" int ea_layernorm_bwd(int rows, int d, const void* dy, int dy_dtype, l
       EA_LN_DISPATCH(ln_bwd_kernel, bf16, grid, blk, 0, st, rows, d, (const bf16*)dy, lddy, x, ldx, gamma, mean, rstd, dx, lddx, accumulate, workspace);
     else
       EA_LN_DISPATCH(ln_bwd_kernel, float, grid, blk, 0, st, rows, d, (const float*)dy, lddy, x, ldx, gamma, mean, rstd, dx, lddx, accumulate, workspace);
+    EA_LAUNCH_CHECK();
+    hipLaunchKernelGGL(reduce_partials_kernel, dim3(ea_cdiv(2 * d, 64)), dim3(256), 0, st, nb, 2 * d,
+                       workspace, (long)2 * d, dgamma, accumulate_params);
+    EA_LAUNCH_CHECK();
+    return 0;
+  }
+  const bool vec8 = d % 8 == 0 && d <= 1024 && lddy % 8 == 0 && ldx % 4 == 0 && lddx % 4 == 0 &&
+                    ((uintptr_t)x % 16) == 0 && ((uintptr_t)dy % 16) == 0 && ((uintptr_t)dx % 16) == 0 &&
+                    ((uintptr_t)gamma % 16) == 0;
+  if (vec8) {  // one pass: dx + per-block dgamma/dbeta partials, then the ordered reducer
+    const int rpb = max(16, ea_cdiv(rows, (int)max(1L, ws_elems / (2L * d))));
+    const int nb = ea_cdiv(rows, rpb);
+    EA_CHECK_ARG(ws_elems >= (long)nb * 2 * d);
+#define EA_LNB(NJ)                                                                                        \
+  if (dy_dtype == EA_BF16)                                                                                \
+    hipLaunchKernelGGL((ln_bwd_vec_kernel<NJ, bf16>), dim3(nb), dim3(256), 0, st, rows, d, (const bf16*)dy, lddy, x, ldx, \
+                       gamma, mean, rstd, dx, lddx, accumulate, rpb, workspace);                           \
+  else                                                                                                    \
+    hipLaunchKernelGGL((ln_bwd_vec_kernel<NJ, float>), dim3(nb), dim3(256), 0, st, rows, d, (const float*)dy, lddy, x, \
+                       ldx, gamma, mean, rstd, dx, lddx, accumulate, rpb, workspace);
+    if (d <= 512) { EA_LNB(1) } else { EA_LNB(2) }
+#undef EA_LNB
     EA_LAUNCH_CHECK();
     hipLaunchKernelGGL(reduce_partials_kernel, dim3(ea_cdiv(2 * d, 64)), dim3(256), 0, st, nb, 2 * d,
                        workspace, (long)2 * d, dgamma, accumulate_params);

@@ -1,0 +1,38 @@
+"""LayerNorm C-ABI (ea_layernorm_fwd / ea_layernorm_bwd) vs a plain fp64 torch LayerNorm
+(eps 1e-12, transformer/layer_norm.py): the vectorised one-pass kernels (d % 8 == 0) and
+the generic row kernels (other d), f32 and bf16 outputs / incoming gradients."""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("rows,d", [(7968, 512), (1312, 512), (333, 1024), (257, 256), (100, 80), (65, 100)])
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+def test_layernorm_fwd_bwd(rows, d, dt):
+    from espnet_amd import hip_ops as ops
+    g = torch.Generator().manual_seed(rows + d)
+    x = (torch.randn(rows, d, generator=g) * 3 + 1).cuda()
+    gamma = (torch.rand(d, generator=g) + 0.5).cuda()
+    beta = torch.randn(d, generator=g).cuda()
+    dy = torch.randn(rows, d, generator=g).to(dt).cuda()
+    y = torch.empty(rows, d, dtype=dt, device="cuda")
+    mu = torch.empty(rows, device="cuda")
+    rs = torch.empty(rows, device="cuda")
+    ops.layernorm_fwd(x, gamma, beta, y, mu, rs)
+    dx0 = torch.randn(rows, d, generator=g).cuda()
+    dx = dx0.clone()
+    pg = torch.randn(2 * d, generator=g).cuda()
+    dparams = pg.clone()
+    ops.layernorm_bwd(dy, x, gamma, mu, rs, dx, dparams[:d], dparams[d:], accumulate=True)
+    torch.cuda.synchronize()
+    xr = x.double().cpu().requires_grad_(True)
+    gr = gamma.double().cpu().requires_grad_(True)
+    br = beta.double().cpu().requires_grad_(True)
+    yr = torch.nn.functional.layer_norm(xr, (d,), gr, br, eps=1e-12)
+    yr.backward(dy.double().cpu())
+    ytol = dict(atol=1e-5, rtol=1e-5) if dt == torch.float32 else dict(atol=3e-2, rtol=1e-2)
+    torch.testing.assert_close(y.double().cpu(), yr.detach(), **ytol)
+    torch.testing.assert_close(dx.double().cpu(), dx0.double().cpu() + xr.grad, atol=2e-4, rtol=1e-4)
+    torch.testing.assert_close(dparams[:d].double().cpu(), pg[:d].double().cpu() + gr.grad, atol=2e-3, rtol=1e-4)
+    torch.testing.assert_close(dparams[d:].double().cpu(), pg[d:].double().cpu() + br.grad, atol=2e-3, rtol=1e-4)
