@@ -267,6 +267,44 @@ __global__ __launch_bounds__(256) void ln_bwd_dx_kernel(int rows, int d, const T
   }
 }
 
+// y = dropout(scale * x) (the residual-branch gradient entering a Linear's backward, same
+// element index (r*cols + c) and mask as ea_scale_dropout) fused with the column partial
+// sums of the stored y (the Linear's bias gradient): one read of x instead of two passes.
+// Layout as colsum_vec_kernel: 256 columns per block (4 per lane), the 4 waves interleave the
+// block's rows, part[blockIdx.y][c] = this row range's sum (waves combined in fixed order).
+template <typename TO>
+__global__ __launch_bounds__(256) void scale_drop_colsum_kernel(int rows, int n, const float* __restrict__ x, long ldx,
+                                                                TO* __restrict__ y, long ldy, float scale, float p,
+                                                                uint64_t seed, const unsigned long long* salt,
+                                                                int rows_per_part, float* __restrict__ part) {
+  __shared__ float red[4][256];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int c = blockIdx.x * 256 + lane * 4;
+  const int r0 = blockIdx.y * rows_per_part, r1 = min(rows, r0 + rows_per_part);
+  if (p > 0.f) seed = ea_salted(seed, salt);
+  float a[4] = {0.f, 0.f, 0.f, 0.f};
+  if (c < n) {
+    for (int r = r0 + w; r < r1; r += 4) {
+      float v[4];
+      vld4(x + (long)r * ldx + c, v);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) v[k] *= scale;
+      drop_scale4(seed, (uint64_t)r * n + c, p, v);
+      TO* yp = y + (long)r * ldy + c;
+      vst4(yp, v);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) a[k] += to_f(from_f<TO>(v[k]));  // sum what was stored
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < 4; ++k) red[w][lane * 4 + k] = a[k];
+  __syncthreads();
+  const int cc = blockIdx.x * 256 + threadIdx.x;
+  if (cc < n)
+    part[(long)blockIdx.y * n + cc] =
+        (red[0][threadIdx.x] + red[1][threadIdx.x]) + (red[2][threadIdx.x] + red[3][threadIdx.x]);
+}
+
 // ---------------------------------------------------------------- vectorised LayerNorm
 // One wave64 per row; lane l owns the 8-column chunks c = l + 64*j (j < NJ), moved with
 // 16-B loads/stores (f32: 2 x float4, bf16: 1 x uint4).  d % 8 == 0, d <= 512*NJ.
@@ -888,6 +926,37 @@ extern "C" int ea_colsum(int rows, int n, const void* x, int x_dtype, long ld, f
   }
   hipLaunchKernelGGL(reduce_partials_kernel, dim3(ea_cdiv(n, 64)), dim3(256), 0, st, nparts, n, workspace,
                      (long)n, out, accumulate);
+  EA_LAUNCH_CHECK();
+  return 0;
+}
+
+extern "C" int ea_scale_dropout_colsum(long rows, int cols, const float* x, long ldx, void* y, int y_dtype, long ldy,
+                                       float scale, float p, unsigned long long seed, float* colsum, int accumulate,
+                                       float* workspace, long ws_elems, void* stream) {
+  EA_ENTRY();
+  if (rows == 0 || cols == 0) return 0;
+  hipStream_t st = (hipStream_t)stream;
+  const int ya = y_dtype == EA_BF16 ? 8 : 16;
+  const bool vec = cols % 4 == 0 && ldx % 4 == 0 && ldy % 4 == 0 && (uintptr_t)x % 16 == 0 && (uintptr_t)y % ya == 0 &&
+                   rows * (long)cols < (1L << 31);
+  if (!vec) {
+    int rc = ea_scale_dropout(rows, cols, x, EA_F32, ldx, y, y_dtype, ldy, scale, p, seed, stream);
+    if (rc) return rc;
+    return ea_colsum((int)rows, cols, y, y_dtype, ldy, colsum, accumulate, workspace, ws_elems, stream);
+  }
+  const int rpp = max(32, ea_cdiv(rows, 128));
+  const int np = ea_cdiv(rows, rpp);
+  EA_CHECK_ARG((long)np * cols <= ws_elems);
+  dim3 g(ea_cdiv(cols, 256), np);
+  if (y_dtype == EA_BF16)
+    hipLaunchKernelGGL(scale_drop_colsum_kernel<bf16>, g, dim3(256), 0, st, (int)rows, cols, x, ldx, (bf16*)y, ldy, scale,
+                       p, (uint64_t)seed, ea_g_rng_salt, rpp, workspace);
+  else
+    hipLaunchKernelGGL(scale_drop_colsum_kernel<float>, g, dim3(256), 0, st, (int)rows, cols, x, ldx, (float*)y, ldy,
+                       scale, p, (uint64_t)seed, ea_g_rng_salt, rpp, workspace);
+  EA_LAUNCH_CHECK();
+  hipLaunchKernelGGL(reduce_partials_kernel, dim3(ea_cdiv(cols, 64)), dim3(256), 0, st, np, cols, workspace, (long)cols,
+                     colsum, accumulate);
   EA_LAUNCH_CHECK();
   return 0;
 }

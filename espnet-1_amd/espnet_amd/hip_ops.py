@@ -297,6 +297,29 @@ def scale_dropout(x, y, scale=1.0, p=0.0, seed=0):
     return y
 
 
+# off by default: on MI355X the two-pass form is faster (C3: 27.26 vs 27.43-28.07 ms/step,
+# scripts/ab_env.sh) since its column sums run on the weight-gradient side stream, off the
+# backward's critical path, while the fused kernel puts a reduction on it
+FUSE_DROP_COLSUM = os.environ.get("EA_FUSE_DROP_COLSUM", "0") != "0"
+
+
+def scale_dropout_colsum(x, y, out, scale=1.0, p=0.0, seed=0, accumulate=True):
+    """y = dropout(scale * x) and out (+)= column sums of y in one pass (ea_scale_dropout_colsum).
+    Default: the two-pass form (ea_scale_dropout, then ea_colsum on the weight-gradient side
+    stream); EA_FUSE_DROP_COLSUM=1 selects the fused kernel."""
+    if not FUSE_DROP_COLSUM:
+        scale_dropout(x, y, scale=scale, p=p, seed=seed)
+        with wgrad(y):
+            colsum(y, out, accumulate=accumulate)
+        return y
+    rows, cols, ldx = _rows(x)
+    _, _, ldy = _rows(y)
+    w, wn = _ws(x.device)
+    lib.ea_scale_dropout_colsum(rows, cols, x.data_ptr(), ldx, y.data_ptr(), dt(y), ldy, float(scale), float(p),
+                                seed & 0xFFFFFFFFFFFFFFFF, out.data_ptr(), int(accumulate), w, wn, stream())
+    return y
+
+
 def cast(x, dtype):
     """Copy-convert (f32 <-> bf16) through ea_scale_dropout; returns x if already dtype."""
     if x.dtype == dtype:

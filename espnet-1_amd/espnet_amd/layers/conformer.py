@@ -144,9 +144,8 @@ def _ffn_bwd(L, b, dx, x_in, saved, pre, ln_name, p, seed_in, seed_out):
     xn, mu, rs, h, a = saved
     N, d = dx.shape
     dv = empty(N, d, dtype=cd, device=dx.device)
-    ops.scale_dropout(dx, dv, scale=L.ff_scale, p=p, seed=seed_out)
+    ops.scale_dropout_colsum(dx, dv, b.g(pre + ".w_2.bias"), scale=L.ff_scale, p=p, seed=seed_out)
     with ops.wgrad(dv, a):
-        ops.colsum(dv, b.g(pre + ".w_2.bias"))
         ops.linear_dw(dv, a, b.g(pre + ".w_2.weight"), accumulate=True)
     dh = empty(*h.shape, dtype=cd, device=dx.device)
     ops.linear_dx(dv, b.w(pre + ".w_2.weight"), dh,
@@ -271,9 +270,8 @@ class ConformerBlockFn(torch.autograd.Function):
         K = L.conv_module.kernel_size
         xn3, mu3, rs3, g2, glu, y, z, bn_mean, bn_rstd = s_conv
         dv = empty(N, d, dtype=cd, device=dev)
-        ops.scale_dropout(dx, dv, p=p, seed=sd(5))
+        ops.scale_dropout_colsum(dx, dv, b.g(C + "pointwise_conv2.bias"), p=p, seed=sd(5))
         with ops.wgrad(dv, z):
-            ops.colsum(dv, b.g(C + "pointwise_conv2.bias"))
             ops.linear_dw(dv, z, b.g(C + "pointwise_conv2.weight", shape=(d, d)), accumulate=True)
         dz = empty(N, d, dtype=cd, device=dev)
         ops.linear_dx(dv, b.w(C + "pointwise_conv2.weight", shape=(d, d)), dz)
@@ -297,9 +295,8 @@ class ConformerBlockFn(torch.autograd.Function):
         A = "self_attn."
         xn2, mu2, rs2, qkv, pp, O, s_core = s_att
         dv = empty(N, d, dtype=cd, device=dev)
-        ops.scale_dropout(dx, dv, p=p, seed=sd(4))
+        ops.scale_dropout_colsum(dx, dv, b.g(A + "linear_out.bias"), p=p, seed=sd(4))
         with ops.wgrad(dv, O):
-            ops.colsum(dv, b.g(A + "linear_out.bias"))
             ops.linear_dw(dv, O, b.g(A + "linear_out.weight"), accumulate=True)
         dO = empty(N, d, dtype=cd, device=dev)
         ops.linear_dx(dv, b.w(A + "linear_out.weight"), dO)

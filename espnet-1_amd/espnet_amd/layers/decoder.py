@@ -230,9 +230,8 @@ class DecoderFn(torch.autograd.Function):
             # feed-forward
             xn3, mu3, rs3, h, a = s3
             dv = empty(N, d, dtype=cd, device=dev)
-            ops.scale_dropout(dx, dv, p=p, seed=sd(l, 6))
+            ops.scale_dropout_colsum(dx, dv, b.g(ff + "w_2.bias"), p=p, seed=sd(l, 6))
             with ops.wgrad(dv, a):
-                ops.colsum(dv, b.g(ff + "w_2.bias"))
                 ops.linear_dw(dv, a, b.g(ff + "w_2.weight"), accumulate=True)
             dh = empty(*h.shape, dtype=cd, device=dev)
             ops.linear_dx(dv, b.w(ff + "w_2.weight"), dh,
@@ -246,9 +245,8 @@ class DecoderFn(torch.autograd.Function):
             # source attention
             xn2, mu2, rs2, q2, O2, st2 = s2
             dv = empty(N, d, dtype=cd, device=dev)
-            ops.scale_dropout(dx, dv, p=p, seed=sd(l, 4))
+            ops.scale_dropout_colsum(dx, dv, b.g(xa + "linear_out.bias"), p=p, seed=sd(l, 4))
             with ops.wgrad(dv, O2):
-                ops.colsum(dv, b.g(xa + "linear_out.bias"))
                 ops.linear_dw(dv, O2, b.g(xa + "linear_out.weight"), accumulate=True)
             dO = empty(N, d, dtype=cd, device=dev)
             ops.linear_dx(dv, b.w(xa + "linear_out.weight"), dO)
@@ -266,9 +264,8 @@ class DecoderFn(torch.autograd.Function):
             # self attention
             xn1, mu1, rs1, qkv, O1, st1 = s1
             dv = empty(N, d, dtype=cd, device=dev)
-            ops.scale_dropout(dx, dv, p=p, seed=sd(l, 2))
+            ops.scale_dropout_colsum(dx, dv, b.g(sa + "linear_out.bias"), p=p, seed=sd(l, 2))
             with ops.wgrad(dv, O1):
-                ops.colsum(dv, b.g(sa + "linear_out.bias"))
                 ops.linear_dw(dv, O1, b.g(sa + "linear_out.weight"), accumulate=True)
             dO = empty(N, d, dtype=cd, device=dev)
             ops.linear_dx(dv, b.w(sa + "linear_out.weight"), dO)

@@ -202,10 +202,10 @@ class SubsampleFn(torch.autograd.Function):
         dev = dy.device
         P1, P2 = B * T1 * F1, B * T2 * F2
         dv = empty(B * T2, C, dtype=cd, device=dev)
-        ops.scale_dropout(dy.reshape(B * T2, C).contiguous(), dv, scale=m.out[1].xscale, p=p, seed=seed)
+        ops.scale_dropout_colsum(dy.reshape(B * T2, C).contiguous(), dv, b.g("out.0.bias"), scale=m.out[1].xscale,
+                                 p=p, seed=seed)
         x2r = x2.view(B * T2, F2 * C)
         with ops.wgrad(dv, x2):
-            ops.colsum(dv, b.g("out.0.bias"))
             dwl = empty(C, F2 * C, device=dev)
             ops.linear_dw(dv, x2r, dwl, accumulate=False)
             ops.permute3(dwl, b.g("out.0.weight"), C, F2, C, accumulate=True)  # (d,F2,C) -> (d,C,F2)
@@ -265,10 +265,10 @@ class SubsampleFn(torch.autograd.Function):
         C = m.odim
         dev = dy.device
         dv = empty(B * T2, C, dtype=cd, device=dev)
-        ops.scale_dropout(dy.reshape(B * T2, C).contiguous(), dv, scale=m.out[1].xscale, p=p, seed=seed)
+        ops.scale_dropout_colsum(dy.reshape(B * T2, C).contiguous(), dv, b.g("out.0.bias"), scale=m.out[1].xscale,
+                                 p=p, seed=seed)
         x2r = x2.view(B * T2, F2 * C)
         with ops.wgrad(dv, x2):
-            ops.colsum(dv, b.g("out.0.bias"))
             dwl = empty(C, F2 * C, device=dev)
             ops.linear_dw(dv, x2r, dwl, accumulate=False)
             ops.permute3(dwl, b.g("out.0.weight"), C, F2, C, accumulate=True)  # (d,F2,C) -> (d,C,F2)

@@ -190,6 +190,14 @@ int ea_scale_dropout(long rows, int cols, const void* x, int x_dtype, long ldx, 
                      int y_dtype, long ldy, float scale, float p, unsigned long long seed,
                      void* stream);
 
+/* ea_scale_dropout (f32 x) fused with the column sums of the stored y accumulated into
+ * colsum[cols] (deterministic two-level sum): the gradient entering a Linear on a dropped-out
+ * residual branch and that Linear's bias gradient (encoder_layer.py:115-168 backward) from
+ * one read of x.  Needs a workspace of ceil(rows/max(32, rows/128)) * cols floats. */
+int ea_scale_dropout_colsum(long rows, int cols, const float* x, long ldx, void* y, int y_dtype, long ldy,
+                            float scale, float p, unsigned long long seed, float* colsum, int accumulate,
+                            float* workspace, long ws_elems, void* stream);
+
 /* y[r, c] += alpha * x[r, c] (mixed dtypes) — autograd's gradient accumulation of a
  * tensor consumed twice (q + pos_bias_u and q + pos_bias_v, attention.py:287-301). */
 int ea_add_2d(long rows, int cols, const void* x, int x_dtype, long ldx, void* y, int y_dtype,

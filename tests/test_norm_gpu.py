@@ -36,3 +36,30 @@ def test_layernorm_fwd_bwd(rows, d, dt):
     torch.testing.assert_close(dx.double().cpu(), dx0.double().cpu() + xr.grad, atol=2e-4, rtol=1e-4)
     torch.testing.assert_close(dparams[:d].double().cpu(), pg[:d].double().cpu() + gr.grad, atol=2e-3, rtol=1e-4)
     torch.testing.assert_close(dparams[d:].double().cpu(), pg[d:].double().cpu() + br.grad, atol=2e-3, rtol=1e-4)
+
+
+@pytest.mark.parametrize("rows,cols,dt", [(7968, 512, torch.bfloat16), (1312, 2048, torch.float32),
+                                          (50, 30, torch.bfloat16)])
+def test_scale_dropout_colsum_matches_two_pass(rows, cols, dt):
+    """Fused y = dropout(scale*x) + bias-gradient column sums == ea_scale_dropout then
+    ea_colsum: identical y (same mask), column sums to f32 rounding (different partition)."""
+    from espnet_amd import hip_ops as ops
+    from espnet_amd._lib import lib
+    lib.ea_set_rng_salt(None)  # a model built by an earlier test may have left its (freed) salt
+    g = torch.Generator().manual_seed(rows)
+    x = torch.randn(rows, cols, generator=g).cuda()
+    y1 = torch.empty(rows, cols, dtype=dt, device="cuda")
+    y2 = torch.empty_like(y1)
+    c1 = torch.ones(cols, device="cuda")
+    c2 = torch.ones(cols, device="cuda")
+    w, wn = ops._ws(x.device)
+    lib.ea_scale_dropout_colsum(rows, cols, x.data_ptr(), cols, y1.data_ptr(), ops.dt(y1), cols, 0.5, 0.1, 1234,
+                                c1.data_ptr(), 1, w, wn, ops.stream())
+    ops.scale_dropout(x, y2, scale=0.5, p=0.1, seed=1234)
+    ops.colsum(y2, c2)
+    torch.cuda.synchronize()
+    assert torch.equal(y1, y2)
+    drop = (y1 == 0).float().mean().item()
+    assert 0.08 < drop < 0.12
+    torch.testing.assert_close(c1, c2, atol=1e-3, rtol=1e-5)
+    torch.testing.assert_close(c1.double().cpu(), 1 + y2.double().sum(0).cpu(), atol=1e-3, rtol=1e-5)
