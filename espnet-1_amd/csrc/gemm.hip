@@ -1095,6 +1095,9 @@ static int gemm_impl(int dtype, int a_kmajor, int b_kmajor, int M, int N, int K,
     if ((geo->mode == EA_CONV_WGRAD) == (a_kmajor != 0) || (geo->mode == EA_CONV_FWD) != (b_kmajor != 0))
       return EA_ERR_BAD_ARG;
     choose_tile(p, 0, 1);
+    // weight gradient: few output tiles over a huge K (pixels) -> 256x256 tiles (the higher
+    // per-CU MFMA rate) split over K to ~one block per CU (split rule below)
+    if (geo->mode == EA_CONV_WGRAD && !g_force_bm) { p.bm = 256; p.bn = 256; }
     if (p.bm != 256 || p.bn != 256) { p.bm = 128; p.bn = 128; }
   } else if (lds_path) {
     choose_tile(p, a_kmajor, (long)batch * nh);
@@ -1110,7 +1113,14 @@ static int gemm_impl(int dtype, int a_kmajor, int b_kmajor, int M, int N, int K,
   const long tiles = max(1L, (long)p.tiles_m * p.tiles_n * nz * (p.bm * p.bn) / (128 * 128));
   // K >= 1024: a K = 512 GEMM split two ways costs more in the reduce pass than it gains
   // (decoder 1312x2048x512: 23.1 us split vs 10.5 us unsplit, scripts/gemm_splitk_ab.py)
-  if (workspace && tiles < 200 && K >= 16 * KT && K >= 1024) {
+  if (geo && geo->mode == EA_CONV_WGRAD && p.bm == 256) {
+    if (workspace) {
+      splitk = max(1, 256 / (p.tiles_m * p.tiles_n));  // one 512-thread block per CU
+      splitk = min(splitk, K / (4 * KT));
+      while (splitk > 1 && (long)splitk * M * N > ws_elems) --splitk;
+      splitk = max(splitk, 1);
+    }
+  } else if (workspace && tiles < 200 && K >= 16 * KT && K >= 1024) {
     splitk = (int)((384 + tiles - 1) / tiles);
     splitk = min(splitk, K / (4 * KT));
     splitk = min(splitk, 16);
