@@ -29,6 +29,9 @@ class ArenaAdam(torch.optim.Optimizer):
         super().__init__(list(model.parameters()),
                          dict(lr=lr, betas=betas, eps=eps, weight_decay=weight_decay, amsgrad=False))
         self.arena = arena
+        # torch.optim.Adam numbers its per-parameter state by position in the param group,
+        # i.e. model.parameters() order (not the arena layout order)
+        self.param_names = [n for n, _ in model.named_parameters()]
         self.exp_avg = torch.zeros_like(arena.data)
         self.exp_avg_sq = torch.zeros_like(arena.data)
         # ea_opt_state: applied-update count, lr/bias corrections/clip coef of the last step
@@ -82,7 +85,7 @@ class ArenaAdam(torch.optim.Optimizer):
         sd = super().state_dict()
         st = {}
         step = float(self.step_count)
-        for i, n in enumerate(self.arena.names):
+        for i, n in enumerate(self.param_names):
             st[i] = dict(step=torch.tensor(step),
                          exp_avg=self.arena_view(self.exp_avg, n).clone(),
                          exp_avg_sq=self.arena_view(self.exp_avg_sq, n).clone())
@@ -96,7 +99,7 @@ class ArenaAdam(torch.optim.Optimizer):
 
     def load_state_dict(self, state_dict):
         st = state_dict["state"]
-        for i, n in enumerate(self.arena.names):
+        for i, n in enumerate(self.param_names):
             if i in st:
                 self.arena_view(self.exp_avg, n).copy_(st[i]["exp_avg"])
                 self.arena_view(self.exp_avg_sq, n).copy_(st[i]["exp_avg_sq"])

@@ -488,6 +488,45 @@ def capture_sampler(name="sampler"):
     print(f"{name}: {len(settings)} settings -> {path}")
 
 
+def capture_avg_nbest(name="avg_nbest"):
+    """espnet2/main_funcs/average_nbest_models.py on 4 epoch files of a small state dict
+    (float weights + an int64 BatchNorm counter), criteria valid.loss min / valid.acc max,
+    nbest [1, 2, 3] (the reference reuses the first loaded dict as accumulator)."""
+    import tempfile
+    from pathlib import Path
+
+    from espnet2.main_funcs.average_nbest_models import average_nbest_models
+    from espnet2.train.reporter import Reporter
+
+    d = Path(tempfile.mkdtemp(prefix="avg_"))
+    g = torch.Generator().manual_seed(9)
+    rep = Reporter()
+    losses = {1: 3.0, 2: 1.5, 3: 2.5, 4: 1.0}
+    accs = {1: 0.5, 2: 0.7, 3: 0.9, 4: 0.6}
+    out = {}
+    for e in (1, 2, 3, 4):
+        sd = {"w": torch.randn(5, 3, generator=g), "b": torch.randn(3, generator=g),
+              "bn.num_batches_tracked": torch.tensor(10 * e, dtype=torch.long)}
+        torch.save(sd, d / f"{e}epoch.pth")
+        for k, v in sd.items():
+            out[f"epoch{e}.{k}"] = v.numpy()
+        rep.set_epoch(e)
+        with rep.observe("valid") as sub:
+            sub.register({"loss": losses[e], "acc": accs[e]})
+    average_nbest_models(d, rep, [("valid", "loss", "min"), ("valid", "acc", "max")], [1, 2, 3])
+    files = sorted(p.name for p in d.iterdir())
+    links = {p.name: os.readlink(p) for p in d.iterdir() if p.is_symlink()}
+    for f in files:
+        if "ave" in f and not (d / f).is_symlink():
+            sd = torch.load(d / f, map_location="cpu", weights_only=True)
+            for k, v in sd.items():
+                out[f"{f}.{k}"] = v.numpy()
+    out["cfg"] = np.array(json.dumps({"losses": losses, "accs": accs, "files": files, "links": links}))
+    path = os.path.join(OUT, f"{name}.npz")
+    np.savez_compressed(path, **out)
+    print(f"{name}: {files} -> {path}")
+
+
 if __name__ == "__main__":
     os.makedirs(OUT, exist_ok=True)
     which = sys.argv[1:] or ["models", "train", "ops", "ddp"]
@@ -505,3 +544,5 @@ if __name__ == "__main__":
         capture_specaug()
     if "sampler" in which:
         capture_sampler()
+    if "avg" in which:
+        capture_avg_nbest()
