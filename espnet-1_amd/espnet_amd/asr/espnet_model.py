@@ -92,9 +92,8 @@ class ESPnetASRModel(AbsESPnetModel):
         assert 0.0 <= ctc_weight <= 1.0, ctc_weight
         assert 0.0 <= interctc_weight < 1.0, interctc_weight
         super().__init__()
-        if frontend is not None or preencoder is not None or postencoder is not None:
-            raise NotImplementedError("frontend/preencoder/postencoder are outside the HIP hot path "
-                                      "(feed features: input_size set, SURVEY.md §2a)")
+        if preencoder is not None or postencoder is not None:
+            raise NotImplementedError("preencoder/postencoder are outside the HIP hot path (SURVEY.md §2a)")
         if joint_network is not None or interctc_weight != 0.0 or lang_token_id != -1:
             raise NotImplementedError("transducer / interCTC / lang token are not on the path")
         self.blank_id = token_list.index(sym_blank) if sym_blank in token_list else 0
@@ -108,7 +107,7 @@ class ESPnetASRModel(AbsESPnetModel):
         self.interctc_weight = interctc_weight
         self.aux_ctc = aux_ctc
         self.token_list = list(token_list)
-        self.frontend = None
+        self.frontend = frontend
         self.specaug = specaug
         self.normalize = normalize
         self.preencoder = None
@@ -168,10 +167,24 @@ class ESPnetASRModel(AbsESPnetModel):
         self._rng_salt = torch.zeros(1, dtype=torch.int64, device=device)
         return self
 
+    def __del__(self):
+        # the library keeps a raw pointer to this model's salt buffer: drop it with the model
+        salt = getattr(self, "_rng_salt", None)
+        if salt is not None and ESPnetASRModel._salt_owner is self._salt_token:
+            try:
+                lib.ea_set_rng_salt(None)
+            except Exception:
+                pass
+            ESPnetASRModel._salt_owner = None
+
+    _salt_owner = None
+
     def _next_seed(self):
         """Site seeds are fixed per (model seed, rank); the per-step variation of every
         dropout mask comes from the device salt, advanced here (on the stream)."""
         lib.ea_set_rng_salt(self._rng_salt.data_ptr())
+        self._salt_token = object() if getattr(self, "_salt_token", None) is None else self._salt_token
+        ESPnetASRModel._salt_owner = self._salt_token
         if self.training:
             self._step += 1
             lib.ea_rng_advance(self._rng_salt.data_ptr(), ops.stream())
@@ -244,8 +257,13 @@ class ESPnetASRModel(AbsESPnetModel):
         return {"feats": feats, "feats_lengths": feats_lengths}
 
     def _extract_feats(self, speech, speech_lengths, smax=None):
+        """espnet_model.py:414-431: crop to the longest utterance, then the frontend (raw
+        waveform -> log-mel frames) when there is one."""
         smax = int(speech_lengths.max()) if smax is None else smax
-        return self._dev(speech)[:, :smax], self._dev(speech_lengths, torch.long)
+        speech, lens = self._dev(speech)[:, :smax], self._dev(speech_lengths, torch.long)
+        if self.frontend is not None:
+            return self.frontend(speech, lens)
+        return speech, lens
 
     def encode(self, speech, speech_lengths, _seed=None, _smax=None, _lens_host=None):
         """espnet_model.py:351-412 (feats -> specaug (training) -> normalize -> encoder).
@@ -255,6 +273,8 @@ class ESPnetASRModel(AbsESPnetModel):
         if self.specaug is not None and self.training and _lens_host is None and speech_lengths.device.type == "cpu":
             _lens_host = [int(v) for v in speech_lengths.tolist()]
         feats, feats_lengths = self._extract_feats(speech, speech_lengths, _smax)
+        if self.frontend is not None and _lens_host is not None:  # sample counts -> frame counts
+            _lens_host = [int(self.frontend.stft.frames_lens(int(v))) for v in _lens_host]
         feats = feats.contiguous().float()
         if self.specaug is not None and self.training:  # :365-366
             feats, feats_lengths = self.specaug(feats, feats_lengths, lens_host=_lens_host)

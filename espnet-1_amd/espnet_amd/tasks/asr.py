@@ -3,7 +3,7 @@ class-choice registries of :109-188 for the names on the hot path.
 
 `build_model(args)` accepts the reference's YAML/argparse keys (input_size, token_list,
 encoder/encoder_conf, decoder/decoder_conf, ctc_conf, model_conf, normalize/normalize_conf,
-specaug/specaug_conf, frontend) and builds the HIP-backed modules; names outside the hot path raise
+specaug/specaug_conf, frontend/frontend_conf) and builds the HIP-backed modules; names outside the hot path raise
 NotImplementedError with the reason.
 """
 from __future__ import annotations
@@ -15,6 +15,7 @@ from ..asr.ctc import CTC
 from ..asr.decoder.transformer_decoder import TransformerDecoder
 from ..asr.encoder.conformer_encoder import ConformerEncoder
 from ..asr.espnet_model import ESPnetASRModel, UtteranceMVN
+from ..asr.frontend.default import DefaultFrontend, GlobalMVN
 from ..asr.specaug import SpecAug
 
 
@@ -42,8 +43,9 @@ class ClassChoices:
 encoder_choices = ClassChoices("encoder", dict(conformer=ConformerEncoder), default="rnn")
 decoder_choices = ClassChoices("decoder", dict(transformer=TransformerDecoder), default=None,
                                optional=True)
-normalize_choices = ClassChoices("normalize", dict(utterance_mvn=UtteranceMVN),
+normalize_choices = ClassChoices("normalize", dict(utterance_mvn=UtteranceMVN, global_mvn=GlobalMVN),
                                  default="utterance_mvn", optional=True)
+frontend_choices = ClassChoices("frontend", dict(default=DefaultFrontend), default="default")
 model_choices = ClassChoices("model", dict(espnet=ESPnetASRModel), default="espnet")
 specaug_choices = ClassChoices("specaug", dict(specaug=SpecAug), default=None, optional=True)
 
@@ -62,9 +64,11 @@ def build_model(args) -> ESPnetASRModel:
     token_list = list(token_list)
     vocab_size = len(token_list)
     input_size = _get(args, "input_size")
-    if input_size is None:
-        raise NotImplementedError("feature frontends (STFT/log-mel) are a §8(f) next item: "
-                                  "set input_size and feed features")
+    frontend = None
+    if input_size is None:  # tasks/asr.py:491-501: raw waveform -> frontend -> features
+        fe_cls = frontend_choices.get_class(_get(args, "frontend") or "default")
+        frontend = fe_cls(**(_get(args, "frontend_conf") or {}))
+        input_size = frontend.output_size()
     spec_cls = specaug_choices.get_class(_get(args, "specaug"))
     specaug = spec_cls(**(_get(args, "specaug_conf") or {})) if spec_cls else None
     norm_cls = normalize_choices.get_class(_get(args, "normalize", "utterance_mvn"))
@@ -78,6 +82,6 @@ def build_model(args) -> ESPnetASRModel:
                           **(_get(args, "decoder_conf") or {}))
     ctc = CTC(odim=vocab_size, encoder_output_size=encoder.output_size(), **(_get(args, "ctc_conf") or {}))
     model_cls = model_choices.get_class(_get(args, "model", "espnet") or "espnet")
-    return model_cls(vocab_size=vocab_size, frontend=None, specaug=specaug, normalize=normalize,
+    return model_cls(vocab_size=vocab_size, frontend=frontend, specaug=specaug, normalize=normalize,
                      preencoder=None, encoder=encoder, postencoder=None, decoder=decoder, ctc=ctc,
                      joint_network=None, token_list=token_list, **(_get(args, "model_conf") or {}))

@@ -163,6 +163,27 @@ int ea_batchnorm_bwd(int rows, int C, const void* dz, int dz_dtype, const float*
  * x (B,T,F) f32 -> y = (x masked to valid frames) - per-utterance mean. F <= 256. */
 int ea_utterance_mvn(int B, int T, int F, const float* x, const long long* lens, float* y, void* stream);
 
+/* Raw-waveform frontend (espnet2/asr/frontend/default.py:17-140), four launches around two
+ * f32 GEMMs (ea_gemm, exact-f32 MFMA):
+ *  ea_stft_frames: frames[b*nF + f][k] = window[k] * x[b][reflect(f*hop + k - pad)], pad =
+ *    center ? n_fft/2 : 0 (torch.stft center/reflect, layers/stft.py:88-100); window has n_fft
+ *    entries (a shorter win_length zero-padded to the centre, as torch.stft does);
+ *  [GEMM frames x [cos | -sin] basis (n_fft x 2*nbins) -> spec (M, 2*nbins)]
+ *  ea_power_spectrum: power = re^2 + im^2, frames f >= flens[b] zero (stft.py:107-114);
+ *  [GEMM power x melmat (nbins x n_mels)]
+ *  ea_logmel_mvn: log(max(mel, 1e-10)), frames >= flens zero (layers/log_mel.py:60-84), and
+ *    when mean/std are given the GlobalMVN below fused in;
+ *  ea_global_mvn: (x - mean) zeroed past lens, / std (layers/global_mvn.py:73-104); mean/std
+ *    NULL skip that part (norm_means / norm_vars false). */
+int ea_stft_frames(int B, long Ns, int nF, int n_fft, int hop, int center, const float* x,
+                   const float* window, float* frames, void* stream);
+int ea_power_spectrum(long M, int nF, int nbins, const float* spec, long ld_spec, const long long* flens,
+                      float* power, long ld_power, void* stream);
+int ea_logmel_mvn(long M, int nF, int n_mels, const float* mel, long ld_mel, const long long* flens,
+                  const float* mean, const float* std, float* y, void* stream);
+int ea_global_mvn(int B, int T, int D, const float* x, const long long* lens, const float* mean,
+                  const float* std, float* y, void* stream);
+
 /* SpecAugment, espnet2/asr/specaug/specaug.py:95-102 = TimeWarp (layers/time_warp.py:9-88,
  * bicubic, align_corners=False) -> MaskAlongAxis(freq) -> MaskAlongAxis(time)
  * (layers/mask_along_axis.py:8-68, replace_with_zero), one pass over x (B,T,F) f32 -> y.

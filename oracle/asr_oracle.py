@@ -465,3 +465,28 @@ def specaug(x, lens, conf):
             if hi > lo:
                 x = _mask_along_axis(x, (lo, hi), 1, conf.get("num_time_mask", 2))
     return x
+
+
+# ---------------------------------------------------------------------------- frontend (f2)
+def default_frontend(x, lens, melmat, n_fft=512, hop=128, win_length=None, window="hann", center=True):
+    """frontend/default.py:89-127 single channel: torch.stft (layers/stft.py:88-114) ->
+    power -> LogMel (layers/log_mel.py:60-84, melmat (nbins, n_mels)); returns (feats, flens)."""
+    wl = n_fft if win_length is None else win_length
+    win = getattr(torch, f"{window}_window")(wl, dtype=x.dtype) if window else None
+    spec = torch.stft(x, n_fft=n_fft, win_length=wl, hop_length=hop, center=center, window=win,
+                      normalized=False, onesided=True, return_complex=False).transpose(1, 2)
+    flens = (lens + (2 * (n_fft // 2) if center else 0) - n_fft) // hop + 1
+    spec = spec.masked_fill(pad_mask(flens, spec.shape[1])[:, :, None, None], 0.0)
+    power = spec[..., 0] ** 2 + spec[..., 1] ** 2
+    mel = torch.clamp(torch.matmul(power, melmat), min=1e-10).log()
+    return mel.masked_fill(pad_mask(flens, mel.shape[1])[:, :, None], 0.0), flens
+
+
+def global_mvn(x, lens, mean, std, norm_means=True, norm_vars=True):
+    """layers/global_mvn.py:73-104."""
+    if norm_means:
+        x = x - mean.to(x.dtype)
+    x = x.masked_fill(pad_mask(lens, x.shape[1])[:, :, None], 0.0)
+    if norm_vars:
+        x = x / std.to(x.dtype)
+    return x

@@ -488,6 +488,52 @@ def capture_sampler(name="sampler"):
     print(f"{name}: {len(settings)} settings -> {path}")
 
 
+def capture_frontend(name="frontend"):
+    """espnet2/asr/frontend/default.py (Stft via torch.stft + LogMel with the restated
+    librosa mel matrix, oracle/shim/librosa/filters.py) and espnet2/layers/global_mvn.py on
+    ragged 16 kHz batches; two STFT settings (the 512/128 default and 400/160 windows)."""
+    import tempfile
+
+    from espnet2.asr.frontend.default import DefaultFrontend
+    from espnet2.layers.global_mvn import GlobalMVN
+
+    g = torch.Generator().manual_seed(21)
+    out = {}
+    cases = {"default": dict(fs=16000, n_fft=512, hop_length=128, n_mels=80),
+             "win400": dict(fs=16000, n_fft=512, win_length=400, hop_length=160, n_mels=80, fmin=20, fmax=7600)}
+    lens = [16000, 12345, 8000, 4097]
+    x = torch.randn(len(lens), max(lens), generator=g) * 0.1
+    for i, le in enumerate(lens):
+        x[i, le:] = 0.0
+    out["x"] = np32(x)
+    out["lens"] = np.array(lens, np.int64)
+    for key, conf in cases.items():
+        fe = DefaultFrontend(**conf, frontend_conf=None)
+        feats, flens = fe(x.clone(), torch.tensor(lens))
+        out[f"{key}.feats"] = np32(feats)
+        out[f"{key}.flens"] = flens.numpy()
+        out[f"{key}.melmat"] = np32(fe.logmel.melmat)
+    # GlobalMVN with an npz stats file of the default features
+    f = out["default.feats"]
+    fl = out["default.flens"]
+    valid = np.concatenate([f[i, :fl[i]] for i in range(len(lens))], 0).astype(np.float64)
+    d = tempfile.mkdtemp(prefix="mvn_")
+    sp = os.path.join(d, "feats_stats.npz")
+    np.savez(sp, count=np.array(valid.shape[0]), sum=valid.sum(0), sum_square=(valid ** 2).sum(0))
+    mvn = GlobalMVN(sp)
+    y, _ = mvn(torch.from_numpy(f).clone(), torch.from_numpy(fl))
+    out["mvn.count"] = np.array(valid.shape[0])
+    out["mvn.sum"] = valid.sum(0)
+    out["mvn.sum_square"] = (valid ** 2).sum(0)
+    out["mvn.y"] = np32(y)
+    out["mvn.mean"] = mvn.mean.numpy()
+    out["mvn.std"] = mvn.std.numpy()
+    out["cfg"] = np.array(json.dumps({"cases": cases, "lens": lens}))
+    path = os.path.join(OUT, f"{name}.npz")
+    np.savez_compressed(path, **out)
+    print(f"{name}: {sorted(out)} -> {path}")
+
+
 def capture_avg_nbest(name="avg_nbest"):
     """espnet2/main_funcs/average_nbest_models.py on 4 epoch files of a small state dict
     (float weights + an int64 BatchNorm counter), criteria valid.loss min / valid.acc max,
@@ -546,3 +592,5 @@ if __name__ == "__main__":
         capture_sampler()
     if "avg" in which:
         capture_avg_nbest()
+    if "frontend" in which:
+        capture_frontend()
