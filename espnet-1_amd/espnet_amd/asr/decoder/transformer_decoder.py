@@ -71,3 +71,30 @@ class TransformerDecoder(AbsDecoder):
         x = DecoderFn.apply(hs_pad.contiguous(), hlens, ys_in_pad.contiguous(), ys_in_lens, self,
                             seed, self.training)
         return x, ys_in_lens
+
+    # ------------------------------------------------------------------ inference scorer
+    @torch.no_grad()
+    def forward_one_step(self, tgt: torch.Tensor, tgt_mask: torch.Tensor, memory: torch.Tensor,
+                         cache=None):
+        """transformer_decoder.py:146-184: log-softmax of the next token after each prefix
+        in tgt (B, L) over memory (B, T, d), no memory mask.  The prefix is recomputed with
+        the fused kernels instead of extending per-layer caches (a causal decoder's prefix
+        outputs do not depend on later tokens, so the scores are the reference's); the
+        returned `cache` is the per-layer placeholder list the reference's API passes on."""
+        B, L = tgt.shape
+        dev = memory.device
+        hlens = torch.full((B,), memory.shape[1], dtype=torch.long, device=dev)
+        ylens = torch.full((B,), L, dtype=torch.long, device=dev)
+        logits = DecoderFn.apply(memory.contiguous(), hlens, tgt.to(dev).contiguous(), ylens, self, 0, False)
+        y = torch.log_softmax(logits[:, -1].float(), dim=-1)
+        return y, [None] * len(self.decoders)
+
+    def score(self, ys, state, x):
+        """transformer_decoder.py:186-192 (one hypothesis)."""
+        logp, state = self.forward_one_step(ys.unsqueeze(0), None, x.unsqueeze(0), cache=state)
+        return logp.squeeze(0), state
+
+    def batch_score(self, ys: torch.Tensor, states, xs: torch.Tensor):
+        """transformer_decoder.py:194-229: scores of the next token for a batch of prefixes."""
+        logp, st = self.forward_one_step(ys, None, xs, cache=None)
+        return logp, [[None] * len(self.decoders) for _ in range(len(ys))]

@@ -1,0 +1,81 @@
+"""Inference consumers of the trained model, on the same HIP kernels:
+
+* ``ctc_greedy`` — espnet2/asr/ctc.py:119-127 argmax + the greedy CTC collapse (repeats
+  merged, blanks dropped) over each utterance's encoder frames.
+* ``attention_greedy`` — espnet/nets/beam_search.py:346-432 with beam_size 1, the decoder as
+  the only scorer (ctc_weight 0, no LM, no length bonus): a hypothesis grows by the best
+  next token (decoder.batch_score, transformer_decoder.py:194-229) until <eos>, with <eos>
+  forced at maxlen (post_process, :462-467); maxlen = encoder frames for maxlenratio 0.
+  Each utterance is encoded alone, as Speech2Text does (a padded batch would let the
+  conformer's depthwise convolution see padding frames).
+
+Both run the model in eval mode (dropout off, BatchNorm running statistics).
+"""
+from __future__ import annotations
+
+from typing import List, Tuple
+
+import torch
+
+
+def _collapse(ids, blank=0):
+    out, prev = [], None
+    for t in ids:
+        if t != prev and t != blank:
+            out.append(int(t))
+        prev = t
+    return out
+
+
+@torch.no_grad()
+def ctc_greedy(model, speech: torch.Tensor, speech_lengths: torch.Tensor) -> List[List[int]]:
+    was = model.training
+    model.eval()
+    try:
+        res = []
+        for b in range(speech.shape[0]):
+            le = int(speech_lengths[b])
+            enc, olens = model.encode(speech[b:b + 1, :le], speech_lengths[b:b + 1])
+            ids = model.ctc.argmax(enc)[0, :int(olens[0])].tolist()
+            res.append(_collapse(ids, model.blank_id))
+        return res
+    finally:
+        model.train(was)
+
+
+@torch.no_grad()
+def attention_greedy(model, speech: torch.Tensor, speech_lengths: torch.Tensor, maxlenratio: float = 0.0,
+                     minlenratio: float = 0.0) -> List[Tuple[List[int], float]]:
+    if minlenratio != 0.0:
+        raise NotImplementedError("minlenratio > 0 (beam_search.py retry loop) is not implemented")
+    was = model.training
+    model.eval()
+    try:
+        res = []
+        sos, eos = model.sos, model.eos
+        for b in range(speech.shape[0]):
+            le = int(speech_lengths[b])
+            enc, olens = model.encode(speech[b:b + 1, :le], speech_lengths[b:b + 1])
+            T = enc.shape[1]
+            if maxlenratio == 0:
+                maxlen = T
+            elif maxlenratio < 0:
+                maxlen = -1 * int(maxlenratio)
+            else:
+                maxlen = max(1, int(maxlenratio * T))
+            yseq = [sos]
+            score = 0.0
+            for i in range(maxlen):
+                ys = torch.tensor([yseq], dtype=torch.long, device=enc.device)
+                logp, _ = model.decoder.batch_score(ys, [None], enc)
+                tok = int(torch.argmax(logp[0]))
+                score += float(logp[0, tok])
+                yseq.append(tok)
+                if i == maxlen - 1 and tok != eos:
+                    yseq.append(eos)
+                if yseq[-1] == eos:
+                    break
+            res.append((yseq[1:-1], score))
+        return res
+    finally:
+        model.train(was)

@@ -490,3 +490,54 @@ def global_mvn(x, lens, mean, std, norm_means=True, norm_vars=True):
     if norm_vars:
         x = x / std.to(x.dtype)
     return x
+
+
+# ---------------------------------------------------------------------------- inference (f4)
+@torch.no_grad()
+def oracle_encode_eval(ora, speech, speech_lengths):
+    """ESPnetASRModel.encode in eval mode (dropout off, BatchNorm running statistics)."""
+    speech = speech[:, : int(speech_lengths.max())]
+    feats = utterance_mvn(speech, speech_lengths)
+    return conformer_encoder(ora.params, feats, speech_lengths, ora.cfg["encoder_conf"], ora.bufs, False)
+
+
+@torch.no_grad()
+def oracle_attention_greedy(ora, speech, speech_lengths):
+    """beam_search.py:346-432, beam 1, decoder-only scoring: the prefix is re-run through
+    the full decoder each step (transformer_decoder.py:146-184 without cache)."""
+    out = []
+    for b in range(speech.shape[0]):
+        le = int(speech_lengths[b])
+        enc, olens = oracle_encode_eval(ora, speech[b:b + 1, :le], speech_lengths[b:b + 1])
+        T = enc.shape[1]
+        yseq, score = [ora.sos], 0.0
+        for i in range(T):
+            ys = torch.tensor([yseq])
+            logits = transformer_decoder(ora.params, enc, torch.tensor([T]), ys, torch.tensor([len(yseq)]),
+                                         ora.cfg["decoder_conf"], False)
+            logp = torch.log_softmax(logits[0, -1], dim=-1)
+            tok = int(torch.argmax(logp))
+            score += float(logp[tok])
+            yseq.append(tok)
+            if i == T - 1 and tok != ora.eos:
+                yseq.append(ora.eos)
+            if yseq[-1] == ora.eos:
+                break
+        out.append((yseq[1:-1], score))
+    return out
+
+
+@torch.no_grad()
+def oracle_ctc_greedy(ora, speech, speech_lengths):
+    out = []
+    for b in range(speech.shape[0]):
+        le = int(speech_lengths[b])
+        enc, olens = oracle_encode_eval(ora, speech[b:b + 1, :le], speech_lengths[b:b + 1])
+        ids = linear(ora.params, "ctc.ctc_lo", enc).argmax(-1)[0, : int(olens[0])].tolist()
+        seq, prev = [], None
+        for t in ids:
+            if t != prev and t != 0:
+                seq.append(int(t))
+            prev = t
+        out.append(seq)
+    return out

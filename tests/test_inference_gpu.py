@@ -1,0 +1,63 @@
+"""Inference consumers: CTC greedy decoding and beam-1 attention
+decoding (espnet/nets/beam_search.py with the decoder as the only scorer) through the HIP
+model in eval mode, against the oracle (CPU restatement, same weights) — token sequences
+bit-exact, hypothesis scores within 1e-3 (fp32 mode)."""
+import numpy as np
+import pytest
+import torch
+
+from goldens import load, section
+
+pytestmark = pytest.mark.gpu
+
+
+def _setup():
+    from oracle.asr_oracle import OracleASR
+    from test_model_build import build
+    cfg, d = load("tiny_hybrid")
+    torch.manual_seed(0)
+    m = build(cfg)
+    w = {k: torch.from_numpy(v) for k, v in section(d, "w").items()}
+    m.load_state_dict(w)
+    m.prepare("cuda", amp=False)
+    inp = {k: torch.from_numpy(v) for k, v in section(d, "in").items()}
+    return m, OracleASR(cfg, w), inp
+
+
+def test_ctc_greedy_matches_oracle():
+    from oracle.asr_oracle import oracle_ctc_greedy
+    from espnet_amd.asr.inference import ctc_greedy
+    m, ora, inp = _setup()
+    got = ctc_greedy(m, inp["speech"], inp["speech_lengths"])
+    ref = oracle_ctc_greedy(ora, inp["speech"], inp["speech_lengths"])
+    assert got == ref
+    assert m.training  # mode restored
+
+
+def test_attention_greedy_matches_oracle():
+    from oracle.asr_oracle import oracle_attention_greedy
+    from espnet_amd.asr.inference import attention_greedy
+    m, ora, inp = _setup()
+    got = attention_greedy(m, inp["speech"], inp["speech_lengths"])
+    ref = oracle_attention_greedy(ora, inp["speech"], inp["speech_lengths"])
+    for (gs, gsc), (rs, rsc) in zip(got, ref):
+        assert gs == rs
+        np.testing.assert_allclose(gsc, rsc, rtol=1e-4, atol=1e-3)
+
+
+def test_decoder_batch_score_matches_full_forward():
+    """batch_score over a batch of prefixes == the log-softmax of the last position of the
+    training-path decoder (eval mode) on the same prefixes."""
+    m, ora, inp = _setup()
+    m.eval()
+    with torch.no_grad():
+        enc, olens = m.encode(inp["speech"][:1, :int(inp["speech_lengths"][0])], inp["speech_lengths"][:1])
+        V = m.vocab_size
+        ys = torch.randint(1, V - 1, (3, 5))
+        ys[:, 0] = m.sos
+        xs = enc.expand(3, -1, -1).contiguous()
+        logp, states = m.decoder.batch_score(ys.cuda(), [None] * 3, xs)
+        full, _ = m.decoder(xs, torch.full((3,), xs.shape[1], dtype=torch.long, device=xs.device), ys.cuda(),
+                            torch.full((3,), 5, dtype=torch.long, device=xs.device))
+        torch.testing.assert_close(logp, torch.log_softmax(full[:, -1], -1), atol=1e-6, rtol=1e-6)
+    assert len(states) == 3 and len(states[0]) == len(m.decoder.decoders)
