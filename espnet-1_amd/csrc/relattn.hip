@@ -285,7 +285,8 @@ constexpr int B_WS = B_D + 2 * BQ * 4;                    // per-wave scratch
 constexpr int B_BDLD = 97;                                // BDfull row stride (floats)
 constexpr int B_XSZ = BQ * B_BDLD * 4 > BQ * 64 * 4 ? BQ * B_BDLD * 4 : BQ * 64 * 4;  // BD gather | dQ partial
 constexpr int B_WSZ = ((B_XSZ + 15) / 16) * 16 + BQ * 128; // + dS image
-constexpr int B_LDS = B_WS + NWAVE * B_WSZ;
+constexpr int B_BIAS = B_WS + NWAVE * B_WSZ;              // pos_bias_u, pos_bias_v of head h (f32)
+constexpr int B_LDS = B_BIAS + 2 * DK * 4;
 
 template <bool REL>
 __global__ __launch_bounds__(256, 1) void attn_bwd_kernel(AttnP a) {
@@ -317,34 +318,83 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_kernel(AttnP a) {
 #pragma unroll
     for (int n = 0; n < 4; ++n) dka[m][n] = dva[m][n] = (f32x4){0.f, 0.f, 0.f, 0.f};
 
+  // The next query tile's inputs are fetched into registers while the current tile's MFMA
+  // work runs (one workgroup per CU, so global latency is otherwise exposed): thread tid
+  // owns row tid>>3, 16-B chunk tid&7 of the Q / dO / O tiles (BQ * 8 == 256 pieces).
+  static_assert(BQ * 8 == 256, "one 16-B piece per thread");
   const bf16* qsrc = a.q + (long)b * a.T1 * a.ldq + h * DK;
+  const bf16* dosrc = a.dO + (long)b * a.T1 * a.lddo + h * DK;
+  const bf16* osrc = a.o + (long)b * a.T1 * a.ldo + h * DK;
+  const bf16* pbase = REL ? a.pp + h * DK : nullptr;
   const int nqt = (a.T1 + BQ - 1) / BQ;
+  const int prow = tid >> 3, pch = tid & 7;
+  float* bias_s = (float*)(sm + B_BIAS);  // [u | v], read at each tile's staging
+  if (tid < DK) {
+    bias_s[tid] = a.bu ? a.bu[h * DK + tid] : 0.f;
+    bias_s[DK + tid] = REL ? a.bv[h * DK + tid] : 0.f;
+  }  // ordered before the first read by the loop's first __syncthreads
+  struct Pre { uint4 q, dO, o; float lse; };
+  auto fetch = [&](int i0n, Pre& pr) {
+    const int i = i0n + prow;
+    pr.q = pr.dO = pr.o = make_uint4(0u, 0u, 0u, 0u);
+    pr.lse = INFINITY;
+    if (i < a.T1) {
+      pr.q = *(const uint4*)(qsrc + (long)i * a.ldq + pch * 8);
+      pr.dO = *(const uint4*)(dosrc + (long)i * a.lddo + pch * 8);
+      pr.o = *(const uint4*)(osrc + (long)i * a.ldo + pch * 8);
+      pr.lse = a.lse[(long)z * a.T1 + i];
+    }
+  };
+  auto tile_on = [&](int i0n) { return active && !(a.causal && jw > i0n + BQ - 1); };
+  // BDfull B fragments: band rows rs + 16t + lc, rs = T-1-(i0+31)+jw (clamped rows only
+  // feed BDfull entries the diagonal gather never reads)
+  auto fetch_band = [&](int i0n, bf16x8 (&pf)[6][2]) {
+    const int rs = a.T1 - 1 - (i0n + BQ - 1) + jw;
+#pragma unroll
+    for (int t = 0; t < 6; ++t) {
+      const int r = min(max(rs + 16 * t + lc, 0), 2 * a.T1 - 2);
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) pf[t][ks] = *(const bf16x8*)(pbase + (long)r * a.ldp + ks * 32 + g * 8);
+    }
+  };
+  Pre pre;
+  fetch(0, pre);
   for (int qt = 0; qt < nqt; ++qt) {
     const int i0 = qt * BQ;
     __syncthreads();  // previous tile's readers of the shared images / exchange are done
-    km_stage_bias(quimg, qsrc, a.ldq, i0, BQ, a.T1, a.bu ? a.bu + h * DK : nullptr, tid, 256);
-    if (REL) km_stage_bias(qvimg, qsrc, a.ldq, i0, BQ, a.T1, a.bv + h * DK, tid, 256);
-    km_stage(doimg, a.dO + (long)b * a.T1 * a.lddo + h * DK, a.lddo, i0, BQ, a.T1, tid, 256);
-    {  // D_i = dO_i . O_i (8 threads per row), lse_i
-      const int row = tid >> 3, part = tid & 7;
-      const int i = i0 + row;
-      float d = 0.f;
-      if (i < a.T1) {
-        union { uint4 u; bf16 e[8]; } x, y;
-        x.u = *(const uint4*)(a.dO + ((long)b * a.T1 + i) * a.lddo + h * DK + part * 8);
-        y.u = *(const uint4*)(a.o + ((long)b * a.T1 + i) * a.ldo + h * DK + part * 8);
+    {  // stage the Q + u, Q + v, dO images; D_i = dO_i . O_i (8 threads per row), lse_i
+      const bool ok = i0 + prow < a.T1;
+      union { uint4 u; bf16 e[8]; } x, y, qu, qv;
+      x.u = pre.q;
+      qu.u = qv.u = make_uint4(0u, 0u, 0u, 0u);
+      if (ok) {
 #pragma unroll
-        for (int e = 0; e < 8; ++e) d += (float)x.e[e] * (float)y.e[e];
+        for (int e = 0; e < 8; ++e) {
+          qu.e[e] = a.bu ? (bf16)((float)x.e[e] + bias_s[pch * 8 + e]) : x.e[e];
+          if (REL) qv.e[e] = (bf16)((float)x.e[e] + bias_s[DK + pch * 8 + e]);
+        }
       }
+      *(uint4*)(quimg + km_off(prow, pch)) = qu.u;
+      if (REL) *(uint4*)(qvimg + km_off(prow, pch)) = qv.u;
+      *(uint4*)(doimg + km_off(prow, pch)) = pre.dO;
+      x.u = pre.dO;
+      y.u = pre.o;
+      float d = 0.f;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) d += (float)x.e[e] * (float)y.e[e];
 #pragma unroll
       for (int o = 1; o < 8; o <<= 1) d += __shfl_xor(d, o, 64);
-      if (part == 0) {
-        Dv[row] = d;
-        Lv[row] = i < a.T1 ? a.lse[(long)z * a.T1 + i] : INFINITY;
+      if (pch == 0) {
+        Dv[prow] = d;
+        Lv[prow] = pre.lse;
       }
     }
     __syncthreads();
-    if (active && !(a.causal && jw > i0 + BQ - 1)) {
+    if (qt + 1 < nqt) fetch(i0 + BQ, pre);
+    if (tile_on(i0)) {
+      // band fragments issued before the AC MFMAs so their latency hides under them
+      bf16x8 pfc[6][2];
+      if (REL) fetch_band(i0, pfc);
       // scores (32 queries x 64 keys): s[mi][t], lane = key column 16t + lc, rows 16mi + 4g + r
       f32x4 s[2][4];
 #pragma unroll
@@ -357,9 +407,7 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_kernel(AttnP a) {
             s[mi][t] = mfma(km_frag(quimg, 16 * mi, ks, lane), km_frag(kimg, 16 * t, ks, lane), s[mi][t]);
         }
       if (REL) {
-        // BDfull (32 x 96): band rows r = rs + [0, 96), rs = T-1-(i0+31)+jw; B fragments from HBM/L2
-        const int rs = a.T1 - 1 - (i0 + BQ - 1) + jw;
-        const bf16* pbase = a.pp + h * DK;
+        // BDfull (32 x 96): band rows rs + [0, 96), B fragments prefetched into pfc
         bf16x8 bq[2][2];
 #pragma unroll
         for (int mi = 0; mi < 2; ++mi)
@@ -367,15 +415,11 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_kernel(AttnP a) {
           for (int ks = 0; ks < 2; ++ks) bq[mi][ks] = km_frag(qvimg, 16 * mi, ks, lane);
 #pragma unroll
         for (int t = 0; t < 6; ++t) {
-          const int r = min(max(rs + 16 * t + lc, 0), 2 * a.T1 - 2);
-          bf16x8 pf[2];
-#pragma unroll
-          for (int ks = 0; ks < 2; ++ks) pf[ks] = *(const bf16x8*)(pbase + (long)r * a.ldp + ks * 32 + g * 8);
 #pragma unroll
           for (int mi = 0; mi < 2; ++mi) {
             f32x4 bd = (f32x4){0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-            for (int ks = 0; ks < 2; ++ks) bd = mfma(bq[mi][ks], pf[ks], bd);
+            for (int ks = 0; ks < 2; ++ks) bd = mfma(bq[mi][ks], pfc[t][ks], bd);
 #pragma unroll
             for (int r2 = 0; r2 < 4; ++r2) xs[(16 * mi + 4 * g + r2) * B_BDLD + 16 * t + lc] = bd[r2];
           }

@@ -17,7 +17,8 @@ import re
 import torch  # noqa: F401,E402
 
 _PKG = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_PKG, "lib", "libespnet_amd.so")
+# EA_LIB_NAME selects another in-tree build of the same library (A/B measurements)
+LIB_PATH = os.path.join(_PKG, "lib", os.environ.get("EA_LIB_NAME", "libespnet_amd.so"))
 HEADER = os.path.join(os.path.dirname(os.path.dirname(_PKG)), "include", "espnet_amd.h")
 
 F32, BF16 = 0, 1
