@@ -110,32 +110,36 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(int rows, int d, const TI* 
   }
 }
 
-// out[c] (+)= sum_p part[p*stride + c], c < n.  Block = 64 columns x 4 part-lanes; each
+// out[c] (+)= sum_p part[p*stride + c], c < n.  Block = RP_CW columns x RP_PL part-lanes; each
 // lane sums a fixed strided subset of the parts (8 loads in flight per lane: the loop is
-// latency-, not bandwidth-bound), lanes combine in fixed order through LDS (deterministic).
+// latency-, not bandwidth-bound, so the parts are spread over many lanes and blocks), lanes
+// combine in fixed order through LDS (deterministic).
 // tr_rows > 0: column j = k*tr_rows + c is written to out[c*tr_cols + k] (transposed output).
+constexpr int RP_CW = 16, RP_PL = 16;
 __global__ __launch_bounds__(256) void reduce_partials_kernel(int nparts, int n, const float* __restrict__ part,
                                                               long stride, float* __restrict__ out, int accumulate,
                                                               int tr_rows = 0, int tr_cols = 0) {
-  __shared__ double red[4][64];
-  const int cx = threadIdx.x & 63, py = threadIdx.x >> 6;
-  const int c = blockIdx.x * 64 + cx;
+  __shared__ double red[RP_PL][RP_CW];
+  const int cx = threadIdx.x % RP_CW, py = threadIdx.x / RP_CW;
+  const int c = blockIdx.x * RP_CW + cx;
   double a = 0.0;
   if (c < n) {
     int p = py;
-    for (; p + 28 < nparts; p += 32) {
+    for (; p + 7 * RP_PL < nparts; p += 8 * RP_PL) {
       float v[8];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) v[j] = part[(long)(p + 4 * j) * stride + c];
+      for (int j = 0; j < 8; ++j) v[j] = part[(long)(p + RP_PL * j) * stride + c];
 #pragma unroll
       for (int j = 0; j < 8; ++j) a += v[j];
     }
-    for (; p < nparts; p += 4) a += part[(long)p * stride + c];
+    for (; p < nparts; p += RP_PL) a += part[(long)p * stride + c];
   }
   red[py][cx] = a;
   __syncthreads();
   if (py == 0 && c < n) {
-    const double t = (red[0][cx] + red[1][cx]) + (red[2][cx] + red[3][cx]);
+    double t = 0.0;
+#pragma unroll
+    for (int l = 0; l < RP_PL; ++l) t += red[l][cx];
     const long o = tr_rows > 0 ? (long)(c % tr_rows) * tr_cols + c / tr_rows : c;
     out[o] = accumulate ? out[o] + (float)t : (float)t;
   }
@@ -819,7 +823,7 @@ extern "C" int ea_layernorm_bwd(int rows, int d, const void* dy, int dy_dtype, l
     else
       EA_LN_DISPATCH(ln_bwd_kernel, float, grid, blk, 0, st, rows, d, (const float*)dy, lddy, x, ldx, gamma, mean, rstd, dx, lddx, accumulate, workspace);
     EA_LAUNCH_CHECK();
-    hipLaunchKernelGGL(reduce_partials_kernel, dim3(ea_cdiv(2 * d, 64)), dim3(256), 0, st, nb, 2 * d,
+    hipLaunchKernelGGL(reduce_partials_kernel, dim3(ea_cdiv(2 * d, RP_CW)), dim3(256), 0, st, nb, 2 * d,
                        workspace, (long)2 * d, dgamma, accumulate_params);
     EA_LAUNCH_CHECK();
     return 0;
@@ -841,7 +845,7 @@ extern "C" int ea_layernorm_bwd(int rows, int d, const void* dy, int dy_dtype, l
     if (d <= 512) { EA_LNB(1) } else { EA_LNB(2) }
 #undef EA_LNB
     EA_LAUNCH_CHECK();
-    hipLaunchKernelGGL(reduce_partials_kernel, dim3(ea_cdiv(2 * d, 64)), dim3(256), 0, st, nb, 2 * d,
+    hipLaunchKernelGGL(reduce_partials_kernel, dim3(ea_cdiv(2 * d, RP_CW)), dim3(256), 0, st, nb, 2 * d,
                        workspace, (long)2 * d, dgamma, accumulate_params);
     EA_LAUNCH_CHECK();
     return 0;
@@ -861,7 +865,7 @@ extern "C" int ea_layernorm_bwd(int rows, int d, const void* dy, int dy_dtype, l
   else
     hipLaunchKernelGGL((colsum_vec_kernel<float, true>), g2, blk, 0, st, rows, d, (const float*)dy, lddy, x, ldx, mean, rstd, rpp, workspace);
   EA_LAUNCH_CHECK();
-  hipLaunchKernelGGL(reduce_partials_kernel, dim3(ea_cdiv(2 * d, 64)), dim3(256), 0, st, nparts, 2 * d,
+  hipLaunchKernelGGL(reduce_partials_kernel, dim3(ea_cdiv(2 * d, RP_CW)), dim3(256), 0, st, nparts, 2 * d,
                      workspace, (long)2 * d, dgamma, accumulate_params);
   EA_LAUNCH_CHECK();
   return 0;
@@ -871,7 +875,7 @@ extern "C" int ea_reduce_partials(int nparts, int n, const float* part, long str
                                   int accumulate, void* stream) {
   EA_ENTRY();
   if (n == 0) return 0;
-  hipLaunchKernelGGL(reduce_partials_kernel, dim3(ea_cdiv(n, 64)), dim3(256), 0, (hipStream_t)stream,
+  hipLaunchKernelGGL(reduce_partials_kernel, dim3(ea_cdiv(n, RP_CW)), dim3(256), 0, (hipStream_t)stream,
                      nparts, n, part, stride, out, accumulate);
   EA_LAUNCH_CHECK();
   return 0;
@@ -881,7 +885,7 @@ extern "C" int ea_reduce_partials(int nparts, int n, const float* part, long str
 int ea_reduce_partials_tr(int nparts, int n, const float* part, long stride, float* out, int accumulate,
                           int tr_rows, int tr_cols, void* stream) {
   if (n == 0) return 0;
-  hipLaunchKernelGGL(reduce_partials_kernel, dim3(ea_cdiv(n, 64)), dim3(256), 0, (hipStream_t)stream,
+  hipLaunchKernelGGL(reduce_partials_kernel, dim3(ea_cdiv(n, RP_CW)), dim3(256), 0, (hipStream_t)stream,
                      nparts, n, part, stride, out, accumulate, tr_rows, tr_cols);
   EA_LAUNCH_CHECK();
   return 0;
@@ -903,7 +907,7 @@ extern "C" int ea_colsum(int rows, int n, const void* x, int x_dtype, long ld, f
     else
       hipLaunchKernelGGL((colsum_vec_kernel<float, false>), g, dim3(256), 0, st, rows, n, (const float*)x, ld, nullptr, 0L, nullptr, nullptr, rpp, workspace);
     EA_LAUNCH_CHECK();
-    hipLaunchKernelGGL(reduce_partials_kernel, dim3(ea_cdiv(n, 64)), dim3(256), 0, st, np, n, workspace, (long)n, out,
+    hipLaunchKernelGGL(reduce_partials_kernel, dim3(ea_cdiv(n, RP_CW)), dim3(256), 0, st, np, n, workspace, (long)n, out,
                        accumulate);
     EA_LAUNCH_CHECK();
     return 0;
@@ -924,7 +928,7 @@ extern "C" int ea_colsum(int rows, int n, const void* x, int x_dtype, long ld, f
       hipLaunchKernelGGL(colsum_partial_kernel<float>, grid, dim3(256), 0, st, rows, n, (const float*)x, ld, rpb, workspace);
     EA_LAUNCH_CHECK();
   }
-  hipLaunchKernelGGL(reduce_partials_kernel, dim3(ea_cdiv(n, 64)), dim3(256), 0, st, nparts, n, workspace,
+  hipLaunchKernelGGL(reduce_partials_kernel, dim3(ea_cdiv(n, RP_CW)), dim3(256), 0, st, nparts, n, workspace,
                      (long)n, out, accumulate);
   EA_LAUNCH_CHECK();
   return 0;
@@ -955,7 +959,7 @@ extern "C" int ea_scale_dropout_colsum(long rows, int cols, const float* x, long
     hipLaunchKernelGGL(scale_drop_colsum_kernel<float>, g, dim3(256), 0, st, (int)rows, cols, x, ldx, (float*)y, ldy,
                        scale, p, (uint64_t)seed, ea_g_rng_salt, rpp, workspace);
   EA_LAUNCH_CHECK();
-  hipLaunchKernelGGL(reduce_partials_kernel, dim3(ea_cdiv(cols, 64)), dim3(256), 0, st, np, cols, workspace, (long)cols,
+  hipLaunchKernelGGL(reduce_partials_kernel, dim3(ea_cdiv(cols, RP_CW)), dim3(256), 0, st, np, cols, workspace, (long)cols,
                      colsum, accumulate);
   EA_LAUNCH_CHECK();
   return 0;
@@ -1027,7 +1031,7 @@ extern "C" int ea_batchnorm_bwd(int rows, int C, const void* dz, int dz_dtype, c
   else
     hipLaunchKernelGGL(bn_bwd_partial_kernel<float>, g1, dim3(256), 0, st, rows, C, (const float*)dz, y, mean, rstd, gamma, beta, act, rpb, workspace);
   EA_LAUNCH_CHECK();
-  hipLaunchKernelGGL(reduce_partials_kernel, dim3(ea_cdiv(2 * C, 64)), dim3(256), 0, st, nparts, 2 * C, workspace,
+  hipLaunchKernelGGL(reduce_partials_kernel, dim3(ea_cdiv(2 * C, RP_CW)), dim3(256), 0, st, nparts, 2 * C, workspace,
                      (long)2 * C, sums, 0);
   EA_LAUNCH_CHECK();
   dim3 g2(ea_grid_cap(ea_cdiv(total, 256)));
@@ -1043,7 +1047,7 @@ extern "C" int ea_batchnorm_bwd(int rows, int C, const void* dz, int dz_dtype, c
     hipLaunchKernelGGL(bn_bwd_apply_kernel<float>, g2, dim3(256), 0, st, total, C, rows, (const float*)dz, y, mean, rstd, gamma, beta, act, sums, sums + C, dy);
   EA_LAUNCH_CHECK();
   // parameter grads: dgamma = sum dh*xhat, dbeta = sum dh
-  hipLaunchKernelGGL(reduce_partials_kernel, dim3(ea_cdiv(2 * C, 64)), dim3(256), 0, st, 1, 2 * C, sums,
+  hipLaunchKernelGGL(reduce_partials_kernel, dim3(ea_cdiv(2 * C, RP_CW)), dim3(256), 0, st, 1, 2 * C, sums,
                      (long)2 * C, dgamma, accumulate_params);
   EA_LAUNCH_CHECK();
   return 0;

@@ -39,7 +39,6 @@ struct AdamP {
   float bc1, bc2_sqrt;   // 1-b1^t, sqrt(1-b2^t)
   const float* norm; float max_norm;
   const ea_opt_state* st;  // device step state: lr / bias corrections / skip come from here
-  int vec;                 // all operands 16-B aligned (bf16 shadow 8-B): 4 elements per thread
 };
 
 // Device-resident step bookkeeping (ea_adam_step_dev): runs before the update, one thread.
@@ -78,35 +77,15 @@ __global__ __launch_bounds__(256) void adam_kernel(AdamP a) {
     if (a.norm && a.max_norm > 0.f) coef = fminf(a.max_norm / (nrm + 1e-6f), 1.f);
   }
   const float step_size = lr / bc1;
-  // per element exactly torch.optim.Adam's update (_single_tensor_adam), 4 elements per thread
-  auto upd = [&](float& p, float gr, float& m, float& v) {
-    float g = gr * coef;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < a.n; i += (long)gridDim.x * blockDim.x) {
+    float p = a.p[i];
+    float g = a.g[i] * coef;
     if (a.wd != 0.f) g += a.wd * p;
+    float m = a.m[i];
     m = m + (1.f - a.b1) * (g - m);  // lerp, as torch Adam
-    v = v * a.b2 + (1.f - a.b2) * g * g;
+    float v = a.v[i] * a.b2 + (1.f - a.b2) * g * g;
     const float denom = sqrtf(v) / bc2s + a.eps;
     p -= step_size * (m / denom);
-  };
-  const long n4 = a.vec ? a.n >> 2 : 0, stride = (long)gridDim.x * blockDim.x;
-  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n4; i += stride) {
-    float4 p = ((const float4*)a.p)[i], m = ((const float4*)a.m)[i], v = ((const float4*)a.v)[i];
-    const float4 g = ((const float4*)a.g)[i];
-    upd(p.x, g.x, m.x, v.x);
-    upd(p.y, g.y, m.y, v.y);
-    upd(p.z, g.z, m.z, v.z);
-    upd(p.w, g.w, m.w, v.w);
-    ((float4*)a.p)[i] = p;
-    ((float4*)a.m)[i] = m;
-    ((float4*)a.v)[i] = v;
-    if (a.p16) {
-      union { uint2 u; bf16 e[4]; } o;
-      o.e[0] = (bf16)p.x; o.e[1] = (bf16)p.y; o.e[2] = (bf16)p.z; o.e[3] = (bf16)p.w;
-      ((uint2*)a.p16)[i] = o.u;
-    }
-  }
-  for (long i = 4 * n4 + blockIdx.x * (long)blockDim.x + threadIdx.x; i < a.n; i += stride) {
-    float p = a.p[i], m = a.m[i], v = a.v[i];
-    upd(p, a.g[i], m, v);
     a.p[i] = p;
     a.m[i] = m;
     a.v[i] = v;
@@ -126,11 +105,6 @@ __global__ void scale_inplace_kernel(long n, float* __restrict__ x, const float*
 // out = wa*a + wb*b (device scalars; b may be null)
 __global__ void axpby_scalar_kernel(const float* a, float wa, const float* b, float wb, float* out) {
   out[0] = wa * a[0] + (b ? wb * b[0] : 0.f);
-}
-
-bool adam_vec(const AdamP& a) {
-  const auto al = [](const void* p, uintptr_t m) { return ((uintptr_t)p & (m - 1)) == 0; };
-  return al(a.p, 16) && al(a.g, 16) && al(a.m, 16) && al(a.v, 16) && al(a.p16, 8);
 }
 
 }  // namespace
@@ -158,8 +132,7 @@ extern "C" int ea_adam_step(long n, float* params, const float* grads, float* ex
   a.bc2_sqrt = (float)sqrt(1.0 - pow((double)beta2, (double)step));
   a.norm = grad_norm; a.max_norm = max_norm;
   a.st = nullptr;
-  a.vec = adam_vec(a);
-  hipLaunchKernelGGL(adam_kernel, dim3(ea_grid_cap(ea_cdiv(n, 1024), 4096)), dim3(256), 0, (hipStream_t)stream, a);
+  hipLaunchKernelGGL(adam_kernel, dim3(ea_grid_cap(ea_cdiv(n, 256), 4096)), dim3(256), 0, (hipStream_t)stream, a);
   EA_LAUNCH_CHECK();
   return 0;
 }
@@ -180,8 +153,7 @@ extern "C" int ea_adam_step_dev(long n, float* params, const float* grads, float
   a.bc1 = 1.f; a.bc2_sqrt = 1.f;
   a.norm = grad_norm; a.max_norm = max_norm;
   a.st = state;
-  a.vec = adam_vec(a);
-  hipLaunchKernelGGL(adam_kernel, dim3(ea_grid_cap(ea_cdiv(n, 1024), 4096)), dim3(256), 0, st, a);
+  hipLaunchKernelGGL(adam_kernel, dim3(ea_grid_cap(ea_cdiv(n, 256), 4096)), dim3(256), 0, st, a);
   EA_LAUNCH_CHECK();
   return 0;
 }
