@@ -541,3 +541,68 @@ def oracle_ctc_greedy(ora, speech, speech_lengths):
             prev = t
         out.append(seq)
     return out
+
+
+# ----------------------------------------------------------------------------- beam search
+def oracle_end_detect(ended, i, M=3, D_end=math.log(1 * math.exp(-10))):
+    """espnet/nets/e2e_asr_common.py:18-48 (ended: list of (yseq list, score float))."""
+    if len(ended) == 0:
+        return False
+    count = 0
+    best = sorted(ended, key=lambda x: x[1], reverse=True)[0]
+    for m in range(M):
+        same = [x for x in ended if len(x[0]) == i - m]
+        if len(same) > 0:
+            b = sorted(same, key=lambda x: x[1], reverse=True)[0]
+            if b[1] - best[1] < D_end:
+                count += 1
+    return count == M
+
+
+@torch.no_grad()
+def oracle_beam_search(ora, speech, speech_lengths, beam, lb_weight=0.0, maxlenratio=0.0):
+    """espnet/nets/beam_search.py:291-483 (BeamSearch.search / forward / post_process) with
+    the decoder (weight 1) and LengthBonus (weight lb_weight, skipped at 0) as the full
+    scorers, no partial scorers (so no pre-beam); f32 scores as in the reference.  Returns
+    per utterance the n-best list [(yseq incl. sos/eos, score, decoder score)]."""
+    out = []
+    V = ora.cfg["vocab_size"]
+    for b in range(speech.shape[0]):
+        le = int(speech_lengths[b])
+        enc, _ = oracle_encode_eval(ora, speech[b:b + 1, :le], speech_lengths[b:b + 1])
+        T = enc.shape[1]
+        if maxlenratio == 0:
+            maxlen = T
+        elif maxlenratio < 0:
+            maxlen = -1 * int(maxlenratio)
+        else:
+            maxlen = max(1, int(maxlenratio * T))
+        # hypothesis: (yseq list, score f32 tensor, decoder-score f32 tensor)
+        running = [([ora.sos], torch.tensor(0.0), torch.tensor(0.0))]
+        ended = []
+        for i in range(maxlen):
+            best = []
+            for ys, sc, dsc in running:
+                logits = transformer_decoder(ora.params, enc, torch.tensor([T]), torch.tensor([ys]),
+                                             torch.tensor([len(ys)]), ora.cfg["decoder_conf"], False)
+                dec = torch.log_softmax(logits[0, -1], dim=-1)
+                w = torch.zeros(V)
+                w += 1.0 * dec
+                if lb_weight != 0:
+                    w += lb_weight * torch.ones(V)
+                w += sc
+                for j in w.topk(beam)[1].tolist():
+                    best.append((ys + [j], w[j], dsc + dec[j]))
+                best = sorted(best, key=lambda h: float(h[1]), reverse=True)[: min(len(best), beam)]
+            if i == maxlen - 1:
+                best = [(ys + [ora.eos], sc, dsc) for ys, sc, dsc in best]
+            running = []
+            for h in best:
+                (ended if h[0][-1] == ora.eos else running).append(h)
+            if maxlenratio == 0.0 and oracle_end_detect([(h[0], float(h[1])) for h in ended], i):
+                break
+            if len(running) == 0:
+                break
+        nbest = sorted(ended, key=lambda h: float(h[1]), reverse=True)
+        out.append([(ys, float(sc), float(dsc)) for ys, sc, dsc in nbest])
+    return out

@@ -573,6 +573,46 @@ def capture_avg_nbest(name="avg_nbest"):
     print(f"{name}: {files} -> {path}")
 
 
+BEAM_CASES = [(3, 0.0, 0.0), (4, 0.5, 0.0), (3, 0.0, 0.5)]  # (beam, length_bonus weight, maxlenratio)
+
+
+def capture_beam(name="beam", cfg_name="tiny_hybrid"):
+    """espnet/nets/beam_search.py BeamSearch on the tiny hybrid model (weights of the
+    tiny_hybrid golden, eval mode), scorers: decoder (weight 1) + LengthBonus; each
+    utterance encoded alone as Speech2Text does.  Records every n-best hypothesis."""
+    from espnet.nets.beam_search import BeamSearch
+    from espnet.nets.scorers.length_bonus import LengthBonus
+    z = np.load(os.path.join(OUT, cfg_name + ".npz"))
+    cfg = json.loads(str(z["cfg"]))
+    model = build_reference_model(cfg)
+    model.load_state_dict({k[2:]: torch.from_numpy(z[k]) for k in z.files if k.startswith("w.")})
+    model.eval()
+    speech = torch.from_numpy(z["in.speech"])
+    lens = torch.from_numpy(z["in.speech_lengths"])
+    V = model.vocab_size
+    out = {}
+    meta = []
+    with torch.no_grad():
+        for ci, (beam, lb, mlr) in enumerate(BEAM_CASES):
+            bs = BeamSearch(scorers={"decoder": model.decoder, "length_bonus": LengthBonus(V)},
+                            weights={"decoder": 1.0, "length_bonus": lb}, beam_size=beam, vocab_size=V,
+                            sos=model.sos, eos=model.eos, token_list=None, pre_beam_score_key="full")
+            for u in range(speech.shape[0]):
+                le = int(lens[u])
+                enc, _ = model.encode(speech[u:u + 1, :le], lens[u:u + 1])
+                nbest = bs(x=enc[0], maxlenratio=mlr, minlenratio=0.0)
+                for r, h in enumerate(nbest):
+                    key = f"c{ci}.u{u}.h{r}"
+                    out[key + ".yseq"] = h.yseq.numpy().astype(np.int64)
+                    out[key + ".score"] = np.float64(float(h.score))
+                    out[key + ".decoder"] = np.float64(float(h.scores["decoder"]))
+                meta.append({"case": ci, "utt": u, "n": len(nbest)})
+    out["cfg"] = np.array(json.dumps({"cases": BEAM_CASES, "nbest": meta, "model": cfg_name}))
+    path = os.path.join(OUT, f"{name}.npz")
+    np.savez_compressed(path, **out)
+    print(f"{name}: {len(meta)} searches -> {path}")
+
+
 if __name__ == "__main__":
     os.makedirs(OUT, exist_ok=True)
     which = sys.argv[1:] or ["models", "train", "ops", "ddp"]
@@ -594,3 +634,5 @@ if __name__ == "__main__":
         capture_avg_nbest()
     if "frontend" in which:
         capture_frontend()
+    if "beam" in which:
+        capture_beam()

@@ -61,3 +61,25 @@ def test_decoder_batch_score_matches_full_forward():
                             torch.full((3,), 5, dtype=torch.long, device=xs.device))
         torch.testing.assert_close(logp, torch.log_softmax(full[:, -1], -1), atol=1e-6, rtol=1e-6)
     assert len(states) == 3 and len(states[0]) == len(m.decoder.decoders)
+
+
+def test_beam_search_matches_reference_goldens():
+    """BeamSearch (decoder + LengthBonus, beams 3/4, maxlenratio 0 with end detection and 0.5)
+    on the HIP model: every n-best hypothesis's token sequence equals the reference
+    BeamSearch's (tests/golden/beam.npz, oracle/make_goldens.py capture_beam); scores within
+    1e-3 (fp32 mode)."""
+    from espnet_amd.asr.inference import attention_beam_search
+    m, ora, inp = _setup()
+    bc, bd = load("beam")
+    for ci, (beam, lb, mlr) in enumerate(bc["cases"]):
+        got = attention_beam_search(m, inp["speech"], inp["speech_lengths"], beam, lb, mlr)
+        for u, nbest in enumerate(got):
+            n = [e["n"] for e in bc["nbest"] if e["case"] == ci and e["utt"] == u][0]
+            assert len(nbest) == n
+            for r, h in enumerate(nbest):
+                k = f"c{ci}.u{u}.h{r}"
+                assert h.yseq.tolist() == bd[k + ".yseq"].tolist(), (ci, u, r)
+                np.testing.assert_allclose(float(h.score), float(bd[k + ".score"]), rtol=1e-4, atol=1e-3)
+                np.testing.assert_allclose(float(h.scores["decoder"]), float(bd[k + ".decoder"]), rtol=1e-4,
+                                           atol=1e-3)
+    assert m.training
