@@ -16,6 +16,7 @@ from __future__ import annotations
 import math
 from typing import Dict, Optional
 
+import numpy as np
 import torch
 import torch.nn.functional as F
 
@@ -559,14 +560,69 @@ def oracle_end_detect(ended, i, M=3, D_end=math.log(1 * math.exp(-10))):
     return count == M
 
 
+class OracleCTCPrefixScore:
+    """espnet/nets/ctc_prefix_score.py:272-358 (CTCPrefixScore, numpy, float32): prefix
+    probabilities of candidate labels from the CTC forward variables r_t^n, r_t^b."""
+
+    logzero = -10000000000.0
+
+    def __init__(self, x, blank, eos):
+        self.x, self.blank, self.eos, self.T = x, blank, eos, len(x)
+
+    def initial_state(self):
+        r = np.full((self.T, 2), self.logzero, dtype=np.float32)
+        r[0, 1] = self.x[0, self.blank]
+        for i in range(1, self.T):
+            r[i, 1] = r[i - 1, 1] + self.x[i, self.blank]
+        return r
+
+    def __call__(self, y, cs, r_prev):
+        ol = len(y) - 1
+        r = np.full((self.T, 2, len(cs)), self.logzero, dtype=np.float32)  # unread rows: logzero
+        xs = self.x[:, cs]
+        if ol == 0:
+            r[0, 0] = xs[0]
+            r[0, 1] = self.logzero
+        else:
+            r[ol - 1] = self.logzero
+        r_sum = np.logaddexp(r_prev[:, 0], r_prev[:, 1])
+        last = y[-1]
+        if ol > 0 and last in cs:
+            log_phi = np.ndarray((self.T, len(cs)), dtype=np.float32)
+            for i in range(len(cs)):
+                log_phi[:, i] = r_sum if cs[i] != last else r_prev[:, 1]
+        else:
+            log_phi = r_sum
+        start = max(ol, 1)
+        log_psi = r[start - 1, 0]
+        for t in range(start, self.T):
+            r[t, 0] = np.logaddexp(r[t - 1, 0], log_phi[t - 1]) + xs[t]
+            r[t, 1] = np.logaddexp(r[t - 1, 0], r[t - 1, 1]) + self.x[t, self.blank]
+            log_psi = np.logaddexp(log_psi, log_phi[t - 1] + xs[t])
+        eos_pos = np.where(cs == self.eos)[0]
+        if len(eos_pos) > 0:
+            log_psi[eos_pos] = r_sum[-1]
+        blank_pos = np.where(cs == self.blank)[0]
+        if len(blank_pos) > 0:
+            log_psi[blank_pos] = self.logzero
+        return log_psi, np.rollaxis(r, 2)
+
+
 @torch.no_grad()
-def oracle_beam_search(ora, speech, speech_lengths, beam, lb_weight=0.0, maxlenratio=0.0):
-    """espnet/nets/beam_search.py:291-483 (BeamSearch.search / forward / post_process) with
-    the decoder (weight 1) and LengthBonus (weight lb_weight, skipped at 0) as the full
-    scorers, no partial scorers (so no pre-beam); f32 scores as in the reference.  Returns
-    per utterance the n-best list [(yseq incl. sos/eos, score, decoder score)]."""
+def oracle_beam_search(ora, speech, speech_lengths, beam, lb_weight=0.0, maxlenratio=0.0, ctc_weight=0.0,
+                       pre_beam_ratio=1.5):
+    """espnet/nets/beam_search.py:291-483 (BeamSearch.search / beam / forward /
+    post_process) with the decoder (weight 1 - ctc_weight) and LengthBonus (lb_weight) as
+    full scorers and, for ctc_weight > 0, CTCPrefixScorer (scorers/ctc.py:10-97, numpy
+    CTCPrefixScore) as the partial scorer on the pre-beam (key "full",
+    int(pre_beam_ratio * beam) candidates); scorers of weight 0 are dropped, as the
+    reference does.  f32 scores.  Returns per utterance the n-best list
+    [(yseq incl. sos/eos, score, decoder score, ctc score)]."""
     out = []
     V = ora.cfg["vocab_size"]
+    wd = 1.0 - ctc_weight
+    pre_beam = int(pre_beam_ratio * beam)
+    do_pre = ctc_weight != 0 and pre_beam < V
     for b in range(speech.shape[0]):
         le = int(speech_lengths[b])
         enc, _ = oracle_encode_eval(ora, speech[b:b + 1, :le], speech_lengths[b:b + 1])
@@ -577,25 +633,54 @@ def oracle_beam_search(ora, speech, speech_lengths, beam, lb_weight=0.0, maxlenr
             maxlen = -1 * int(maxlenratio)
         else:
             maxlen = max(1, int(maxlenratio * T))
-        # hypothesis: (yseq list, score f32 tensor, decoder-score f32 tensor)
-        running = [([ora.sos], torch.tensor(0.0), torch.tensor(0.0))]
+        impl = None
+        ctc_state0 = None
+        if ctc_weight != 0:
+            logp = torch.log_softmax(linear(ora.params, "ctc.ctc_lo", enc), dim=-1)[0].numpy()
+            impl = OracleCTCPrefixScore(logp, 0, ora.eos)
+            ctc_state0 = (0, impl.initial_state())
+        # hypothesis: (yseq list, score, decoder score, ctc score, ctc state)
+        running = [([ora.sos], torch.tensor(0.0), torch.tensor(0.0), torch.tensor(0.0), ctc_state0)]
         ended = []
         for i in range(maxlen):
             best = []
-            for ys, sc, dsc in running:
-                logits = transformer_decoder(ora.params, enc, torch.tensor([T]), torch.tensor([ys]),
-                                             torch.tensor([len(ys)]), ora.cfg["decoder_conf"], False)
-                dec = torch.log_softmax(logits[0, -1], dim=-1)
+            for ys, sc, dsc, csc, cst in running:
                 w = torch.zeros(V)
-                w += 1.0 * dec
+                dec = None
+                if wd != 0:
+                    logits = transformer_decoder(ora.params, enc, torch.tensor([T]), torch.tensor([ys]),
+                                                 torch.tensor([len(ys)]), ora.cfg["decoder_conf"], False)
+                    dec = torch.log_softmax(logits[0, -1], dim=-1)
+                    w += wd * dec
                 if lb_weight != 0:
                     w += lb_weight * torch.ones(V)
+                part_ids = torch.arange(V)
+                if do_pre:
+                    part_ids = torch.topk(w, pre_beam)[1]
+                pscore = pst = None
+                if impl is not None:
+                    prev_score, st = cst
+                    presub, new_st = impl(np.array(ys), part_ids.numpy(), st)
+                    pscore = torch.as_tensor(presub - prev_score, dtype=torch.float32)
+                    pst = (presub, new_st)
+                    w[part_ids] += ctc_weight * pscore
                 w += sc
-                for j in w.topk(beam)[1].tolist():
-                    best.append((ys + [j], w[j], dsc + dec[j]))
+                if w.size(0) == part_ids.size(0):
+                    top = w.topk(beam)[1]
+                    local = top
+                else:
+                    tmp = w[part_ids]
+                    w[:] = -float("inf")
+                    w[part_ids] = tmp
+                    top = w.topk(beam)[1]
+                    local = w[part_ids].topk(beam)[1]
+                for j, pj in zip(top.tolist(), local.tolist()):
+                    best.append((ys + [j], w[j], dsc + (dec[j] if dec is not None else 0.0),
+                                 csc + (pscore[pj] if pscore is not None else 0.0),
+                                 (pst[0][pj], pst[1][pj]) if pst is not None else None))
                 best = sorted(best, key=lambda h: float(h[1]), reverse=True)[: min(len(best), beam)]
             if i == maxlen - 1:
-                best = [(ys + [ora.eos], sc, dsc) for ys, sc, dsc in best]
+                best = [(h[0] + [ora.eos],) + h[1:] for h in best]
             running = []
             for h in best:
                 (ended if h[0][-1] == ora.eos else running).append(h)
@@ -604,5 +689,5 @@ def oracle_beam_search(ora, speech, speech_lengths, beam, lb_weight=0.0, maxlenr
             if len(running) == 0:
                 break
         nbest = sorted(ended, key=lambda h: float(h[1]), reverse=True)
-        out.append([(ys, float(sc), float(dsc)) for ys, sc, dsc in nbest])
+        out.append([(h[0], float(h[1]), float(h[2]), float(h[3])) for h in nbest])
     return out

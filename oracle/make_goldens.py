@@ -573,7 +573,9 @@ def capture_avg_nbest(name="avg_nbest"):
     print(f"{name}: {files} -> {path}")
 
 
-BEAM_CASES = [(3, 0.0, 0.0), (4, 0.5, 0.0), (3, 0.0, 0.5)]  # (beam, length_bonus weight, maxlenratio)
+# (beam, length_bonus weight, maxlenratio[, ctc_weight])
+BEAM_CASES = [(3, 0.0, 0.0), (4, 0.5, 0.0), (3, 0.0, 0.5), (3, 0.0, 0.0, 0.3), (4, 0.5, 0.0, 0.5),
+              (3, 0.0, 0.5, 0.3)]
 
 
 def capture_beam(name="beam", cfg_name="tiny_hybrid"):
@@ -581,6 +583,7 @@ def capture_beam(name="beam", cfg_name="tiny_hybrid"):
     tiny_hybrid golden, eval mode), scorers: decoder (weight 1) + LengthBonus; each
     utterance encoded alone as Speech2Text does.  Records every n-best hypothesis."""
     from espnet.nets.beam_search import BeamSearch
+    from espnet.nets.scorers.ctc import CTCPrefixScorer
     from espnet.nets.scorers.length_bonus import LengthBonus
     z = np.load(os.path.join(OUT, cfg_name + ".npz"))
     cfg = json.loads(str(z["cfg"]))
@@ -593,10 +596,14 @@ def capture_beam(name="beam", cfg_name="tiny_hybrid"):
     out = {}
     meta = []
     with torch.no_grad():
-        for ci, (beam, lb, mlr) in enumerate(BEAM_CASES):
-            bs = BeamSearch(scorers={"decoder": model.decoder, "length_bonus": LengthBonus(V)},
-                            weights={"decoder": 1.0, "length_bonus": lb}, beam_size=beam, vocab_size=V,
-                            sos=model.sos, eos=model.eos, token_list=None, pre_beam_score_key="full")
+        for ci, case in enumerate(BEAM_CASES):
+            beam, lb, mlr = case[:3]
+            cw = case[3] if len(case) > 3 else 0.0
+            bs = BeamSearch(scorers={"decoder": model.decoder, "ctc": CTCPrefixScorer(model.ctc, model.eos),
+                                     "length_bonus": LengthBonus(V)},
+                            weights={"decoder": 1.0 - cw, "ctc": cw, "length_bonus": lb}, beam_size=beam,
+                            vocab_size=V, sos=model.sos, eos=model.eos, token_list=None,
+                            pre_beam_score_key="full")
             for u in range(speech.shape[0]):
                 le = int(lens[u])
                 enc, _ = model.encode(speech[u:u + 1, :le], lens[u:u + 1])
@@ -606,6 +613,8 @@ def capture_beam(name="beam", cfg_name="tiny_hybrid"):
                     out[key + ".yseq"] = h.yseq.numpy().astype(np.int64)
                     out[key + ".score"] = np.float64(float(h.score))
                     out[key + ".decoder"] = np.float64(float(h.scores["decoder"]))
+                    if cw:
+                        out[key + ".ctc"] = np.float64(float(h.scores["ctc"]))
                 meta.append({"case": ci, "utt": u, "n": len(nbest)})
     out["cfg"] = np.array(json.dumps({"cases": BEAM_CASES, "nbest": meta, "model": cfg_name}))
     path = os.path.join(OUT, f"{name}.npz")
