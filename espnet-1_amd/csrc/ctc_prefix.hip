@@ -1,0 +1,129 @@
+// CTC prefix scoring for joint CTC/attention beam search:
+// espnet/nets/scorers/ctc.py:10-97 (CTCPrefixScorer) over espnet/nets/ctc_prefix_score.py:272-358
+// (CTCPrefixScore, Algorithm 2 of Watanabe et al., "Hybrid CTC/attention architecture").
+//
+// The reference runs the recursion in numpy on the host, one hypothesis at a time, after
+// copying the CTC posteriors off the device.  Here the posteriors stay in HBM and ONE launch
+// scores every (running hypothesis, pre-beam candidate) pair of a search step: one thread
+// per pair walks the T frames (the recursion is serial in t), reading its hypothesis's
+// forward variables r_{t}^{n,b}(g) and writing the candidate's r_t^{n,b}(h) for the next
+// step.  Arithmetic is float32 with numpy's logaddexp, as in the reference.
+#include "common.h"
+
+namespace {
+
+constexpr float kLogZero = -10000000000.0f;  // ctc_prefix_score.py:283
+
+// numpy npy_logaddexpf (float32)
+EA_DEV float np_logaddexpf(float x, float y) {
+  if (x == y) return x + 0.693147180559945309417232121458176568f;
+  const float tmp = x - y;
+  if (tmp > 0.f) return x + log1pf(expf(-tmp));
+  if (tmp <= 0.f) return y + log1pf(expf(tmp));
+  return tmp;  // NaN
+}
+
+// logp[t][v] = log_softmax(logits[t]) (one block per frame), then (block 0, thread 0)
+// r0[t] = (logzero, cumulative blank log-prob)  — initial_state(), :289-301
+__global__ __launch_bounds__(256) void ctc_logsoftmax_kernel(int V, const float* __restrict__ logits, long ldl,
+                                                             float* __restrict__ logp) {
+  __shared__ float red[256];
+  const int t = blockIdx.x;
+  const float* row = logits + (long)t * ldl;
+  float m = -INFINITY;
+  for (int v = threadIdx.x; v < V; v += 256) m = fmaxf(m, row[v]);
+  red[threadIdx.x] = m;
+  __syncthreads();
+  for (int s = 128; s > 0; s >>= 1) {
+    if (threadIdx.x < s) red[threadIdx.x] = fmaxf(red[threadIdx.x], red[threadIdx.x + s]);
+    __syncthreads();
+  }
+  m = red[0];
+  __syncthreads();
+  float acc = 0.f;
+  for (int v = threadIdx.x; v < V; v += 256) acc += expf(row[v] - m);
+  red[threadIdx.x] = acc;
+  __syncthreads();
+  for (int s = 128; s > 0; s >>= 1) {
+    if (threadIdx.x < s) red[threadIdx.x] += red[threadIdx.x + s];
+    __syncthreads();
+  }
+  const float lz = m + logf(red[0]);
+  for (int v = threadIdx.x; v < V; v += 256) logp[(long)t * V + v] = row[v] - lz;
+}
+
+__global__ void ctc_prefix_init_kernel(int T, int V, int blank, const float* __restrict__ logp, float* __restrict__ r0) {
+  float acc = 0.f;
+  for (int t = 0; t < T; ++t) {
+    acc = t == 0 ? logp[blank] : acc + logp[(long)t * V + blank];
+    r0[2 * t] = kLogZero;
+    r0[2 * t + 1] = acc;
+  }
+}
+
+// one thread per (hypothesis h, candidate c): __call__ (:303-358)
+__global__ __launch_bounds__(64) void ctc_prefix_score_kernel(int T, int V, int blank, int eos, int n_hyp,
+                                                              int n_cand, const float* __restrict__ logp,
+                                                              const unsigned long long* __restrict__ r_prev_ptr,
+                                                              const int* __restrict__ meta, float* __restrict__ log_psi,
+                                                              float* __restrict__ r_new) {
+  const int idx = blockIdx.x * 64 + threadIdx.x;
+  if (idx >= n_hyp * n_cand) return;
+  const int h = idx / n_cand;
+  const int ol = meta[h];                 // output length (prefix without <sos>)
+  const int last = meta[n_hyp + h];       // last label of the prefix
+  const int c = meta[2 * n_hyp + idx];    // candidate label
+  const float* rp = (const float*)r_prev_ptr[h];
+  float* r = r_new + (long)idx * T * 2;
+  const bool same = ol > 0 && c == last;  // log_phi = r^b(g) for a repeated label, else r^n + r^b
+  const int start = max(ol, 1);
+  for (int t = 0; t < min(start, T); ++t) { r[2 * t] = kLogZero; r[2 * t + 1] = kLogZero; }
+  float psi;
+  if (ol == 0) {
+    r[0] = logp[c];
+    psi = r[0];
+  } else {
+    psi = kLogZero;  // r[ol-1, 0]
+  }
+  float rn = start - 1 < T ? r[2 * (start - 1)] : kLogZero, rb = start - 1 < T ? r[2 * (start - 1) + 1] : kLogZero;
+  for (int t = start; t < T; ++t) {
+    const float phi = same ? rp[2 * (t - 1) + 1] : np_logaddexpf(rp[2 * (t - 1)], rp[2 * (t - 1) + 1]);
+    const float xc = logp[(long)t * V + c];
+    const float nrn = np_logaddexpf(rn, phi) + xc;
+    const float nrb = np_logaddexpf(rn, rb) + logp[(long)t * V + blank];
+    psi = np_logaddexpf(psi, phi + xc);
+    rn = nrn;
+    rb = nrb;
+    r[2 * t] = rn;
+    r[2 * t + 1] = rb;
+  }
+  if (c == eos) psi = np_logaddexpf(rp[2 * (T - 1)], rp[2 * (T - 1) + 1]);
+  if (c == blank) psi = kLogZero;
+  log_psi[idx] = psi;
+}
+
+}  // namespace
+
+extern "C" int ea_ctc_prefix_init(int T, int V, const float* logits, long ld_logits, int blank, float* logp,
+                                  float* r0, void* stream) {
+  EA_ENTRY();
+  EA_CHECK_ARG(T >= 1 && V >= 1 && blank >= 0 && blank < V && ld_logits >= V);
+  hipStream_t st = (hipStream_t)stream;
+  hipLaunchKernelGGL(ctc_logsoftmax_kernel, dim3(T), dim3(256), 0, st, V, logits, ld_logits, logp);
+  EA_LAUNCH_CHECK();
+  hipLaunchKernelGGL(ctc_prefix_init_kernel, dim3(1), dim3(1), 0, st, T, V, blank, logp, r0);
+  EA_LAUNCH_CHECK();
+  return 0;
+}
+
+extern "C" int ea_ctc_prefix_score(int T, int V, int blank, int eos, int n_hyp, int n_cand, const float* logp,
+                                   const unsigned long long* r_prev, const int* meta, float* log_psi, float* r_new,
+                                   void* stream) {
+  EA_ENTRY();
+  EA_CHECK_ARG(T >= 1 && V >= 1 && n_hyp >= 0 && n_cand >= 0);
+  if (n_hyp * n_cand == 0) return 0;
+  hipLaunchKernelGGL(ctc_prefix_score_kernel, dim3(ea_cdiv(n_hyp * n_cand, 64)), dim3(64), 0, (hipStream_t)stream, T,
+                     V, blank, eos, n_hyp, n_cand, logp, r_prev, meta, log_psi, r_new);
+  EA_LAUNCH_CHECK();
+  return 0;
+}

@@ -11,7 +11,9 @@ step ALL running hypotheses (they share a length) are scored in ONE batched call
 (n_hyps, vocab) score matrix comes back to the host for the selection, which is done in f32
 exactly as the reference does it.
 
-Partial scorers (CTCPrefixScorer, pre-beam) are not built yet: passing one raises.
+Partial scorers (CTCPrefixScorer, scorers/ctc.py) score only the pre-beam candidates of
+each hypothesis; every (hypothesis, candidate) pair of a step is scored by ONE launch of the
+CTC prefix kernel (csrc/ctc_prefix.hip) on posteriors that stay in HBM.
 """
 from __future__ import annotations
 
@@ -19,6 +21,9 @@ import math
 from typing import Any, Dict, List, NamedTuple, Optional, Union
 
 import torch
+
+from .. import hip_ops as ops
+from .._lib import lib
 
 
 class Hypothesis(NamedTuple):
@@ -69,8 +74,62 @@ def end_detect(ended_hyps, i, M=3, D_end=math.log(1 * math.exp(-10))):
     return count == M
 
 
+class CTCPrefixScorer:
+    """scorers/ctc.py:10-97 (CTCPrefixScorer over ctc_prefix_score.py CTCPrefixScore) on the
+    device: state of a hypothesis = (prefix score, its (T, 2) forward variables in HBM)."""
+
+    def __init__(self, ctc, eos: int, blank: int = 0):
+        self.ctc, self.eos, self.blank = ctc, eos, blank
+        self.logp = None
+
+    def init_state(self, x: torch.Tensor):
+        """ctc.py:25-37: x (T, d) encoder output of one utterance."""
+        lg = self.ctc.logits(x.unsqueeze(0))[0].float().contiguous()
+        T, V = lg.shape
+        self.logp = torch.empty(T, V, device=x.device)
+        r0 = torch.empty(T, 2, device=x.device)
+        lib.ea_ctc_prefix_init(T, V, lg.data_ptr(), V, self.blank, self.logp.data_ptr(), r0.data_ptr(), ops.stream())
+        return torch.tensor(0.0), r0
+
+    @staticmethod
+    def select_state(state, i, new_id=None):
+        sc, st = state
+        return sc[i], st[i]
+
+    def final_score(self, state):
+        return 0.0
+
+    def score_partial(self, y, ids, state, x):
+        """ctc.py:63-80 for one hypothesis."""
+        (sc,), (st,) = self.score_partial_multi([y], [ids], [state])
+        return sc, st
+
+    def score_partial_multi(self, ys, ids_list, states):
+        """score_partial for several hypotheses (same candidate count) in one launch:
+        -> ([scores (n_cand,) f32 host], [(prefix scores (n_cand,), r (n_cand, T, 2))])."""
+        n, P = len(ys), int(ids_list[0].numel())
+        T, V = self.logp.shape
+        dev = self.logp.device
+        meta = torch.tensor([len(y) - 1 for y in ys] + [int(y[-1]) for y in ys]
+                            + torch.cat([i.reshape(-1) for i in ids_list]).tolist(), dtype=torch.int32)
+        ptrs = torch.tensor([st.data_ptr() for _, st in states], dtype=torch.int64)
+        meta_d = meta.pin_memory().to(dev, non_blocking=True)
+        ptrs_d = ptrs.pin_memory().to(dev, non_blocking=True)
+        log_psi = torch.empty(n * P, device=dev)
+        r_new = torch.empty(n * P, T, 2, device=dev)
+        lib.ea_ctc_prefix_score(T, V, self.blank, self.eos, n, P, self.logp.data_ptr(), ptrs_d.data_ptr(),
+                                meta_d.data_ptr(), log_psi.data_ptr(), r_new.data_ptr(), ops.stream())
+        psi = log_psi.cpu()
+        scores, new_states = [], []
+        for h in range(n):
+            presub = psi[h * P:(h + 1) * P]
+            scores.append(presub - states[h][0])  # ctc.py:76-79: prefix score increment (f32)
+            new_states.append((presub, r_new[h * P:(h + 1) * P]))
+        return scores, new_states
+
+
 class BeamSearch(torch.nn.Module):
-    """beam_search.py:30-483 for full scorers (decoder, length bonus, LMs with batch_score)."""
+    """beam_search.py:30-483: full scorers (decoder, length bonus) and partial scorers (CTC prefix)."""
 
     def __init__(self, scorers: Dict[str, Any], weights: Dict[str, float], beam_size: int, vocab_size: int,
                  sos: int, eos: int, token_list: Optional[List[str]] = None, pre_beam_ratio: float = 1.5,
@@ -79,16 +138,20 @@ class BeamSearch(torch.nn.Module):
         self.weights = weights
         self.scorers = {}
         self.full_scorers = {}
+        self.part_scorers = {}
         for k, v in scorers.items():
             w = weights.get(k, 0)
             if w == 0 or v is None:
                 continue
-            if hasattr(v, "score_partial"):
-                raise NotImplementedError(f"partial scorer {k!r} (CTC prefix scoring) is not built yet")
-            if not hasattr(v, "batch_score"):
-                raise TypeError(f"{k} ({type(v)}) has no batch_score")
             self.scorers[k] = v
-            self.full_scorers[k] = v
+            if hasattr(v, "score_partial"):
+                if not hasattr(v, "score_partial_multi"):
+                    raise TypeError(f"{k} ({type(v)}) has no score_partial_multi")
+                self.part_scorers[k] = v
+            elif hasattr(v, "batch_score"):
+                self.full_scorers[k] = v
+            else:
+                raise TypeError(f"{k} ({type(v)}) has no batch_score")
         self.sos, self.eos = sos, eos
         self.hyp_primer = hyp_primer
         self.token_list = token_list
@@ -99,6 +162,8 @@ class BeamSearch(torch.nn.Module):
                 and pre_beam_score_key not in self.full_scorers:
             raise KeyError(f"{pre_beam_score_key} is not found in {self.full_scorers}")
         self.pre_beam_score_key = pre_beam_score_key
+        self.do_pre_beam = (pre_beam_score_key is not None and self.pre_beam_size < self.n_vocab
+                            and len(self.part_scorers) > 0)
 
     def init_hyp(self, x: torch.Tensor) -> List[Hypothesis]:
         states = {k: (d.init_state(x) if hasattr(d, "init_state") else None) for k, d in self.scorers.items()}
@@ -122,21 +187,55 @@ class BeamSearch(torch.nn.Module):
             out[k] = sc.float().cpu()
         return out
 
+    def beam(self, weighted_scores: torch.Tensor, ids: torch.Tensor):
+        """beam_search.py:209-237: top-k full ids and the matching pre-beam (local) ids."""
+        if weighted_scores.size(0) == ids.size(0):
+            top_ids = weighted_scores.topk(self.beam_size)[1]
+            return top_ids, top_ids
+        tmp = weighted_scores[ids]
+        weighted_scores[:] = -float("inf")
+        weighted_scores[ids] = tmp
+        top_ids = weighted_scores.topk(self.beam_size)[1]
+        local_ids = weighted_scores[ids].topk(self.beam_size)[1]
+        return top_ids, local_ids
+
     def search(self, running_hyps: List[Hypothesis], x: torch.Tensor) -> List[Hypothesis]:
-        """beam_search.py:291-344."""
-        best_hyps = []
+        """beam_search.py:291-344; the scorers run batched over all running hypotheses first
+        (full scorers, then partial scorers on each hypothesis's pre-beam), then the
+        reference's per-hypothesis selection runs on the host scores."""
         allsc = self._score_all(running_hyps, x)
-        for hi, hyp in enumerate(running_hyps):
-            weighted = torch.zeros(self.n_vocab, dtype=torch.float32)
-            scores = {k: allsc[k][hi] for k in self.full_scorers}
+        weighted, scores, part_ids = [], [], []
+        for hi in range(len(running_hyps)):
+            w = torch.zeros(self.n_vocab, dtype=torch.float32)
+            sc = {k: allsc[k][hi] for k in self.full_scorers}
             for k in self.full_scorers:
-                weighted += self.weights[k] * scores[k]
-            weighted += hyp.score
-            for j in weighted.topk(self.beam_size)[1].tolist():
-                best_hyps.append(Hypothesis(
-                    score=weighted[j], yseq=self.append_token(hyp.yseq, j),
-                    scores={k: hyp.scores[k] + v[j] for k, v in scores.items()},
-                    states=dict(hyp.states)))
+                w += self.weights[k] * sc[k]
+            ids = torch.arange(self.n_vocab)
+            if self.do_pre_beam:
+                pre = w if self.pre_beam_score_key == "full" else sc[self.pre_beam_score_key]
+                ids = torch.topk(pre, self.pre_beam_size)[1]
+            weighted.append(w)
+            scores.append(sc)
+            part_ids.append(ids)
+        part = {k: d.score_partial_multi([h.yseq for h in running_hyps], part_ids,
+                                         [h.states[k] for h in running_hyps])
+                for k, d in self.part_scorers.items()}
+        best_hyps = []
+        for hi, hyp in enumerate(running_hyps):
+            w, sc, ids = weighted[hi], scores[hi], part_ids[hi]
+            psc = {k: part[k][0][hi] for k in self.part_scorers}
+            pst = {k: part[k][1][hi] for k in self.part_scorers}
+            for k in self.part_scorers:
+                w[ids] += self.weights[k] * psc[k]
+            w += hyp.score
+            for j, pj in zip(*self.beam(w, ids)):
+                j, pj = int(j), int(pj)
+                new_scores = {k: hyp.scores[k] + v[j] for k, v in sc.items()}
+                new_scores.update({k: hyp.scores[k] + v[pj] for k, v in psc.items()})
+                new_states = {k: hyp.states[k] for k in self.full_scorers}
+                new_states.update({k: d.select_state(pst[k], pj) for k, d in self.part_scorers.items()})
+                best_hyps.append(Hypothesis(score=w[j], yseq=self.append_token(hyp.yseq, j), scores=new_scores,
+                                            states=new_states))
             best_hyps = sorted(best_hyps, key=lambda h: h.score, reverse=True)[: min(len(best_hyps), self.beam_size)]
         return best_hyps
 
@@ -148,7 +247,7 @@ class BeamSearch(torch.nn.Module):
         remained = []
         for hyp in running_hyps:
             if int(hyp.yseq[-1]) == self.eos:
-                for k, d in self.full_scorers.items():
+                for k, d in list(self.full_scorers.items()) + list(self.part_scorers.items()):
                     s = d.final_score(hyp.states[k]) if hasattr(d, "final_score") else 0.0
                     hyp.scores[k] += s
                     hyp = hyp._replace(score=hyp.score + self.weights[k] * s)

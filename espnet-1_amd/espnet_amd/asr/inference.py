@@ -83,18 +83,21 @@ def attention_greedy(model, speech: torch.Tensor, speech_lengths: torch.Tensor, 
 
 @torch.no_grad()
 def attention_beam_search(model, speech: torch.Tensor, speech_lengths: torch.Tensor, beam_size: int,
-                          length_bonus: float = 0.0, maxlenratio: float = 0.0, minlenratio: float = 0.0):
-    """Speech2Text-style decoding with BeamSearch (espnet/nets/beam_search.py) over the
-    decoder (weight 1) and LengthBonus (weight `length_bonus`): per utterance the n-best
-    list of Hypothesis records (yseq with <sos>/<eos>, score, per-scorer scores)."""
-    from .beam_search import BeamSearch, LengthBonus
+                          length_bonus: float = 0.0, maxlenratio: float = 0.0, minlenratio: float = 0.0,
+                          ctc_weight: float = 0.0):
+    """Speech2Text-style decoding (espnet2/bin/asr_inference.py:140-175) with BeamSearch
+    (espnet/nets/beam_search.py) over the decoder (weight 1 - ctc_weight), the CTC prefix
+    scorer (ctc_weight, pre-beam "full") and LengthBonus (length_bonus): per utterance the
+    n-best list of Hypothesis records (yseq with <sos>/<eos>, score, per-scorer scores)."""
+    from .beam_search import BeamSearch, CTCPrefixScorer, LengthBonus
     was = model.training
     model.eval()
     try:
         V = model.vocab_size
-        bs = BeamSearch(scorers={"decoder": model.decoder, "length_bonus": LengthBonus(V)},
-                        weights={"decoder": 1.0, "length_bonus": length_bonus}, beam_size=beam_size,
-                        vocab_size=V, sos=model.sos, eos=model.eos, pre_beam_score_key="full")
+        bs = BeamSearch(scorers={"decoder": model.decoder, "ctc": CTCPrefixScorer(model.ctc, model.eos),
+                                 "length_bonus": LengthBonus(V)},
+                        weights={"decoder": 1.0 - ctc_weight, "ctc": ctc_weight, "length_bonus": length_bonus},
+                        beam_size=beam_size, vocab_size=V, sos=model.sos, eos=model.eos, pre_beam_score_key="full")
         res = []
         for b in range(speech.shape[0]):
             le = int(speech_lengths[b])

@@ -390,6 +390,25 @@ int ea_scale_by_scalar(long n, float* x, const float* s, float c, void* stream);
 /* out[0] = wa*a[0] + wb*b[0] (b may be NULL) — loss = w*ctc + (1-w)*att, espnet_model.py:325 */
 int ea_axpby_scalar(const float* a, float wa, const float* b, float wb, float* out, void* stream);
 
+
+/* ---------------------------------------------------------------- joint CTC/attention decoding */
+
+/* CTCPrefixScorer.init_state (espnet/nets/scorers/ctc.py:25-37 + ctc_prefix_score.py:289-301):
+ * logp[t][v] = log_softmax(logits[t]) (T x V f32, dense) and the initial forward variables
+ * r0[t] = (r_t^n, r_t^b)(<sos>) = (logzero, sum_{s<=t} logp[s][blank]). */
+int ea_ctc_prefix_init(int T, int V, const float* logits, long ld_logits, int blank, float* logp,
+                       float* r0, void* stream);
+
+/* CTCPrefixScore.__call__ (ctc_prefix_score.py:303-358) for every (hypothesis h < n_hyp,
+ * candidate c < n_cand) pair of a beam-search step in one launch.  r_prev: device array of
+ * n_hyp device pointers, each to that hypothesis's (T x 2) f32 forward variables; meta:
+ * device int32 [n_hyp output lengths | n_hyp last labels | n_hyp*n_cand candidate labels].
+ * Writes log_psi[h*n_cand + c] (prefix log-probability; <eos>: full-sequence probability,
+ * blank: logzero) and r_new[(h*n_cand + c)][T][2]. */
+int ea_ctc_prefix_score(int T, int V, int blank, int eos, int n_hyp, int n_cand, const float* logp,
+                        const unsigned long long* r_prev, const int* meta, float* log_psi, float* r_new,
+                        void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -78,3 +78,46 @@ def test_ctc_long_sequences_vs_torch(B, T, V, L):
     (ref.sum() / B).backward()
     np.testing.assert_allclose(lu.numpy(), ref.detach().numpy(), rtol=2e-6, atol=1e-4)
     np.testing.assert_allclose(grad.numpy(), x.grad.numpy(), atol=2e-6, rtol=1e-4)
+
+
+def test_ctc_prefix_kernel_matches_numpy_restatement():
+    """ea_ctc_prefix_init / ea_ctc_prefix_score against the numpy CTCPrefixScore restatement
+    (oracle, pinned to the reference beam-search goldens): initial state, prefix scores and
+    next forward variables for prefixes of length 0..3, repeated labels, <eos> and blank
+    among the candidates."""
+    import numpy as np
+    import torch
+    from espnet_amd._lib import lib
+    from espnet_amd import hip_ops as ops
+    from oracle.asr_oracle import OracleCTCPrefixScore
+    g = torch.Generator().manual_seed(5)
+    T, V, eos = 37, 11, 10
+    logits = torch.randn(T, V, generator=g) * 2
+    logp_ref = torch.log_softmax(logits, -1).numpy()
+    impl = OracleCTCPrefixScore(logp_ref, 0, eos)
+    lg = logits.cuda()
+    logp = torch.empty(T, V, device="cuda")
+    r0 = torch.empty(T, 2, device="cuda")
+    lib.ea_ctc_prefix_init(T, V, lg.data_ptr(), V, 0, logp.data_ptr(), r0.data_ptr(), ops.stream())
+    np.testing.assert_allclose(logp.cpu().numpy(), logp_ref, atol=2e-6)
+    np.testing.assert_allclose(r0.cpu().numpy(), impl.initial_state(), rtol=1e-5, atol=1e-5)
+    cs = np.array([0, 3, 5, 7, eos], dtype=np.int64)
+    for y in ([eos], [eos, 3], [eos, 3, 5], [eos, 3, 5, 5]):
+        # previous state: the restatement's own recursion along y
+        r_prev = impl.initial_state()
+        for k in range(1, len(y)):
+            _, st = impl(np.array(y[:k]), np.array([y[k]]), r_prev)
+            r_prev = st[0]
+        psi_ref, r_ref = impl(np.array(y), cs, r_prev)
+        rp = torch.from_numpy(np.ascontiguousarray(r_prev)).cuda()
+        meta = torch.tensor([len(y) - 1, y[-1]] + cs.tolist(), dtype=torch.int32, device="cuda")
+        ptrs = torch.tensor([rp.data_ptr()], dtype=torch.int64, device="cuda")
+        psi = torch.empty(len(cs), device="cuda")
+        rn = torch.empty(len(cs), T, 2, device="cuda")
+        lib.ea_ctc_prefix_score(T, V, 0, eos, 1, len(cs), logp.data_ptr(), ptrs.data_ptr(), meta.data_ptr(),
+                                psi.data_ptr(), rn.data_ptr(), ops.stream())
+        torch.cuda.synchronize()
+        np.testing.assert_allclose(psi.cpu().numpy(), psi_ref, rtol=1e-5, atol=1e-4)
+        ol = len(y) - 1
+        lo = max(ol, 1) - 1  # rows below the start are never read by the reference
+        np.testing.assert_allclose(rn.cpu().numpy()[:, lo:], r_ref[:, lo:], rtol=1e-5, atol=1e-4)

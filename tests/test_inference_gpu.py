@@ -64,15 +64,17 @@ def test_decoder_batch_score_matches_full_forward():
 
 
 def test_beam_search_matches_reference_goldens():
-    """BeamSearch (decoder + LengthBonus, beams 3/4, maxlenratio 0 with end detection and 0.5)
-    on the HIP model: every n-best hypothesis's token sequence equals the reference
+    """BeamSearch (decoder + LengthBonus, and joint CTC/attention with the CTC prefix kernel at
+    ctc_weight 0.3/0.5; beams 3/4, maxlenratio 0 with end detection and 0.5) on the HIP model: every n-best hypothesis's token sequence equals the reference
     BeamSearch's (tests/golden/beam.npz, oracle/make_goldens.py capture_beam); scores within
     1e-3 (fp32 mode)."""
     from espnet_amd.asr.inference import attention_beam_search
     m, ora, inp = _setup()
     bc, bd = load("beam")
-    for ci, (beam, lb, mlr) in enumerate(bc["cases"]):
-        got = attention_beam_search(m, inp["speech"], inp["speech_lengths"], beam, lb, mlr)
+    for ci, case in enumerate(bc["cases"]):
+        beam, lb, mlr = case[:3]
+        cw = case[3] if len(case) > 3 else 0.0
+        got = attention_beam_search(m, inp["speech"], inp["speech_lengths"], beam, lb, mlr, ctc_weight=cw)
         for u, nbest in enumerate(got):
             n = [e["n"] for e in bc["nbest"] if e["case"] == ci and e["utt"] == u][0]
             assert len(nbest) == n
@@ -82,4 +84,6 @@ def test_beam_search_matches_reference_goldens():
                 np.testing.assert_allclose(float(h.score), float(bd[k + ".score"]), rtol=1e-4, atol=1e-3)
                 np.testing.assert_allclose(float(h.scores["decoder"]), float(bd[k + ".decoder"]), rtol=1e-4,
                                            atol=1e-3)
+                if cw:
+                    np.testing.assert_allclose(float(h.scores["ctc"]), float(bd[k + ".ctc"]), rtol=1e-4, atol=1e-3)
     assert m.training
