@@ -122,7 +122,7 @@ def synthetic_batch(cfg, seed):
                 text_lengths=torch.full((B,), L, dtype=torch.long))
 
 
-PMC_FILE = os.path.join(ROOT, "profiles", "r1_v10_pmc_conv2_fwd.json")
+PMC_FILE = os.path.join(ROOT, "profiles", "r1_v13_pmc_conv2_fwd.json")
 
 
 def pmc_traffic():
