@@ -86,16 +86,33 @@ __global__ __launch_bounds__(64) void ctc_prefix_score_kernel(int T, int V, int 
     psi = kLogZero;  // r[ol-1, 0]
   }
   float rn = start - 1 < T ? r[2 * (start - 1)] : kLogZero, rb = start - 1 < T ? r[2 * (start - 1) + 1] : kLogZero;
-  for (int t = start; t < T; ++t) {
-    const float phi = same ? rp[2 * (t - 1) + 1] : np_logaddexpf(rp[2 * (t - 1)], rp[2 * (t - 1) + 1]);
-    const float xc = logp[(long)t * V + c];
-    const float nrn = np_logaddexpf(rn, phi) + xc;
-    const float nrb = np_logaddexpf(rn, rb) + logp[(long)t * V + blank];
-    psi = np_logaddexpf(psi, phi + xc);
-    rn = nrn;
-    rb = nrb;
-    r[2 * t] = rn;
-    r[2 * t + 1] = rb;
+  // frames in chunks of CH: the chunk's loads (and its log_phi values, which do not depend on
+  // the recursion) are issued together, so one memory latency is exposed per chunk instead of
+  // one per frame; the serial recursion then runs from registers
+  constexpr int CH = 16;
+  for (int t0 = start; t0 < T; t0 += CH) {
+    float xc[CH], xb[CH], ph[CH];
+#pragma unroll
+    for (int k = 0; k < CH; ++k) {
+      const int t = min(t0 + k, T - 1);
+      xc[k] = logp[(long)t * V + c];
+      xb[k] = logp[(long)t * V + blank];
+      const float a = rp[2 * (t - 1)], b = rp[2 * (t - 1) + 1];
+      ph[k] = same ? b : np_logaddexpf(a, b);  // log_phi[t-1]
+    }
+#pragma unroll
+    for (int k = 0; k < CH; ++k) {
+      const int t = t0 + k;
+      if (t < T) {
+        const float nrn = np_logaddexpf(rn, ph[k]) + xc[k];
+        const float nrb = np_logaddexpf(rn, rb) + xb[k];
+        psi = np_logaddexpf(psi, ph[k] + xc[k]);
+        rn = nrn;
+        rb = nrb;
+        r[2 * t] = rn;
+        r[2 * t + 1] = rb;
+      }
+    }
   }
   if (c == eos) psi = np_logaddexpf(rp[2 * (T - 1)], rp[2 * (T - 1) + 1]);
   if (c == blank) psi = kLogZero;

@@ -110,11 +110,18 @@ class CTCPrefixScorer:
         n, P = len(ys), int(ids_list[0].numel())
         T, V = self.logp.shape
         dev = self.logp.device
-        meta = torch.tensor([len(y) - 1 for y in ys] + [int(y[-1]) for y in ys]
-                            + torch.cat([i.reshape(-1) for i in ids_list]).tolist(), dtype=torch.int32)
-        ptrs = torch.tensor([st.data_ptr() for _, st in states], dtype=torch.int64)
-        meta_d = meta.pin_memory().to(dev, non_blocking=True)
-        ptrs_d = ptrs.pin_memory().to(dev, non_blocking=True)
+        # one small host->device copy: [output lengths | last labels | candidates | r_prev pointers]
+        head = [len(y) - 1 for y in ys] + [int(y[-1]) for y in ys]
+        cand = torch.cat([i.reshape(-1) for i in ids_list]).to(torch.int32)
+        ptrs = torch.tensor([st.data_ptr() for _, st in states], dtype=torch.int64).view(torch.int32)
+        nmeta = 2 * n + n * P + (n * P) % 2  # keep the pointer block 8-B aligned
+        host = torch.zeros(nmeta + ptrs.numel(), dtype=torch.int32)
+        host[:2 * n] = torch.tensor(head, dtype=torch.int32)
+        host[2 * n:2 * n + n * P] = cand
+        host[nmeta:] = ptrs
+        dev_buf = host.to(dev)
+        meta_d = dev_buf[:nmeta]
+        ptrs_d = dev_buf[nmeta:]
         log_psi = torch.empty(n * P, device=dev)
         r_new = torch.empty(n * P, T, 2, device=dev)
         lib.ea_ctc_prefix_score(T, V, self.blank, self.eos, n, P, self.logp.data_ptr(), ptrs_d.data_ptr(),
@@ -200,43 +207,49 @@ class BeamSearch(torch.nn.Module):
         return top_ids, local_ids
 
     def search(self, running_hyps: List[Hypothesis], x: torch.Tensor) -> List[Hypothesis]:
-        """beam_search.py:291-344; the scorers run batched over all running hypotheses first
-        (full scorers, then partial scorers on each hypothesis's pre-beam), then the
-        reference's per-hypothesis selection runs on the host scores."""
+        """beam_search.py:291-344 for all running hypotheses at once: the scorers run batched
+        (full scorers, then the partial scorers on each hypothesis's pre-beam), the reference's
+        per-hypothesis arithmetic runs row-wise on the (n_hyps, vocab) host scores, and its
+        incremental sort-and-prune is one stable descending sort of the n_hyps x beam
+        candidates in hypothesis order (it keeps the same beam, ties included)."""
+        n, V = len(running_hyps), self.n_vocab
         allsc = self._score_all(running_hyps, x)
-        weighted, scores, part_ids = [], [], []
-        for hi in range(len(running_hyps)):
-            w = torch.zeros(self.n_vocab, dtype=torch.float32)
-            sc = {k: allsc[k][hi] for k in self.full_scorers}
-            for k in self.full_scorers:
-                w += self.weights[k] * sc[k]
-            ids = torch.arange(self.n_vocab)
-            if self.do_pre_beam:
-                pre = w if self.pre_beam_score_key == "full" else sc[self.pre_beam_score_key]
-                ids = torch.topk(pre, self.pre_beam_size)[1]
-            weighted.append(w)
-            scores.append(sc)
-            part_ids.append(ids)
-        part = {k: d.score_partial_multi([h.yseq for h in running_hyps], part_ids,
+        W = torch.zeros(n, V, dtype=torch.float32)
+        for k in self.full_scorers:
+            W += self.weights[k] * allsc[k]
+        if self.do_pre_beam:
+            pre = W if self.pre_beam_score_key == "full" else allsc[self.pre_beam_score_key]
+            ids = torch.topk(pre, self.pre_beam_size, dim=1)[1]
+        else:
+            ids = torch.arange(V).expand(n, V)
+        part = {k: d.score_partial_multi([h.yseq for h in running_hyps], list(ids),
                                          [h.states[k] for h in running_hyps])
                 for k, d in self.part_scorers.items()}
+        for k in self.part_scorers:
+            W.scatter_(1, ids, W.gather(1, ids) + self.weights[k] * torch.stack(part[k][0]))
+        W += torch.stack([torch.as_tensor(h.score, dtype=torch.float32) for h in running_hyps]).view(n, 1)
+        if ids.shape[1] == V:  # beam(): no pre-beam
+            top = W.topk(self.beam_size, dim=1)[1]
+            local = top
+        else:  # beam(): pruned candidates masked out
+            Wm = torch.full_like(W, -float("inf"))
+            Wm.scatter_(1, ids, W.gather(1, ids))
+            W = Wm
+            top = W.topk(self.beam_size, dim=1)[1]
+            local = W.gather(1, ids).topk(self.beam_size, dim=1)[1]
+        cand = W.gather(1, top).reshape(-1)
+        order = torch.sort(cand, descending=True, stable=True)[1][: self.beam_size].tolist()
         best_hyps = []
-        for hi, hyp in enumerate(running_hyps):
-            w, sc, ids = weighted[hi], scores[hi], part_ids[hi]
-            psc = {k: part[k][0][hi] for k in self.part_scorers}
-            pst = {k: part[k][1][hi] for k in self.part_scorers}
-            for k in self.part_scorers:
-                w[ids] += self.weights[k] * psc[k]
-            w += hyp.score
-            for j, pj in zip(*self.beam(w, ids)):
-                j, pj = int(j), int(pj)
-                new_scores = {k: hyp.scores[k] + v[j] for k, v in sc.items()}
-                new_scores.update({k: hyp.scores[k] + v[pj] for k, v in psc.items()})
-                new_states = {k: hyp.states[k] for k in self.full_scorers}
-                new_states.update({k: d.select_state(pst[k], pj) for k, d in self.part_scorers.items()})
-                best_hyps.append(Hypothesis(score=w[j], yseq=self.append_token(hyp.yseq, j), scores=new_scores,
-                                            states=new_states))
-            best_hyps = sorted(best_hyps, key=lambda h: h.score, reverse=True)[: min(len(best_hyps), self.beam_size)]
+        for o in order:
+            hi, r = divmod(o, self.beam_size)
+            hyp = running_hyps[hi]
+            j, pj = int(top[hi, r]), int(local[hi, r])
+            new_scores = {k: hyp.scores[k] + allsc[k][hi, j] for k in self.full_scorers}
+            new_scores.update({k: hyp.scores[k] + part[k][0][hi][pj] for k in self.part_scorers})
+            new_states = {k: hyp.states[k] for k in self.full_scorers}
+            new_states.update({k: d.select_state(part[k][1][hi], pj) for k, d in self.part_scorers.items()})
+            best_hyps.append(Hypothesis(score=W[hi, j], yseq=self.append_token(hyp.yseq, j), scores=new_scores,
+                                        states=new_states))
         return best_hyps
 
     def post_process(self, i: int, maxlen: int, maxlenratio: float, running_hyps: List[Hypothesis],
