@@ -87,3 +87,31 @@ def test_beam_search_matches_reference_goldens():
                 if cw:
                     np.testing.assert_allclose(float(h.scores["ctc"]), float(bd[k + ".ctc"]), rtol=1e-4, atol=1e-3)
     assert m.training
+
+
+def test_joint_beam_search_runs_in_bf16():
+    """The AMP (bf16) model decodes with the joint scorer: n-best lists are sorted, every
+    hypothesis is <sos> ... <eos>, and its score equals the weighted sum of its per-scorer
+    scores (decoder 0.7, ctc 0.3, length bonus 0.2 per emitted token)."""
+    from espnet_amd.asr.inference import attention_beam_search
+    from oracle.asr_oracle import OracleASR  # noqa: F401  (same setup as the other tests)
+    from test_model_build import build
+    cfg, d = load("tiny_hybrid")
+    torch.manual_seed(0)
+    m = build(cfg)
+    m.load_state_dict({k: torch.from_numpy(v) for k, v in section(d, "w").items()})
+    m.prepare("cuda", amp=True)
+    inp = {k: torch.from_numpy(v) for k, v in section(d, "in").items()}
+    res = attention_beam_search(m, inp["speech"], inp["speech_lengths"], 4, length_bonus=0.2, ctc_weight=0.3)
+    for nbest in res:
+        assert len(nbest) >= 1
+        scores = [float(h.score) for h in nbest]
+        assert scores == sorted(scores, reverse=True)
+        for h in nbest:
+            ys = h.yseq.tolist()
+            assert ys[0] == m.sos and ys[-1] == m.eos  # (<eos> <eos> when forced at maxlen, as in the reference)
+            lb = float(h.scores["length_bonus"])  # emitted tokens (an <eos> forced at maxlen is not scored)
+            assert lb in (len(ys) - 1, len(ys) - 2)
+            tot = 0.7 * float(h.scores["decoder"]) + 0.3 * float(h.scores["ctc"]) + 0.2 * lb
+            np.testing.assert_allclose(float(h.score), tot, rtol=1e-4, atol=1e-3)
+            assert np.isfinite(float(h.scores["ctc"]))
