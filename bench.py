@@ -175,6 +175,9 @@ def main():
     ap.add_argument("--fp32", action="store_true", help="exact-f32 MFMA instead of bf16 AMP")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--profile-steps", type=int, default=0)
+    ap.add_argument("--graph-dp", action="store_true",
+                    help="with N > 1, capture the step incl. its RCCL all-reduces as a hipGraph too "
+                         "(default for N > 1: eager steps, see DESIGN.md section 5)")
     ap.add_argument("--eager", action="store_true", help="launch every kernel from Python each step "
                     "(default: the step is captured once as a hipGraph and replayed)")
     args = ap.parse_args()
@@ -207,7 +210,10 @@ def main():
     host = synthetic_batch(cfg, 1 + rank)  # abs_task.py:1566-1575: each rank its own shard
     batch = {k: v.to(dev) for k, v in host.items()}  # resident in HBM before timing
     maxlens = (cfg["T"], cfg["L"])
-    runner = CapturedTrainStep(model, opt, sched, grad_clip=5.0, dp=dp, warmup=2, enabled=not args.eager)
+    # multi-GPU steps run eagerly unless --graph-dp: hipGraph capture of the RCCL collectives
+    # has not been exercised on a multi-GPU node yet
+    eager = args.eager or (world > 1 and not args.graph_dp)
+    runner = CapturedTrainStep(model, opt, sched, grad_clip=5.0, dp=dp, warmup=2, enabled=not eager)
 
     def step():
         return runner(batch, maxlens)
@@ -216,7 +222,7 @@ def main():
     # every replay; reset after warmup so only the timed region counts
     probe = hip_ops.KernelProbe(["conv2_gemm"], dev)
     hip_ops.PROBE = probe
-    for _ in range(max(args.warmup, 0 if args.eager else 3)):
+    for _ in range(max(args.warmup, 0 if eager else 3)):
         step()
     torch.cuda.synchronize()
     probe.reset()
