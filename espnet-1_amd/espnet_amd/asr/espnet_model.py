@@ -20,6 +20,7 @@ from ..arena import ParamArena
 from ..layers.common import site_seed
 from ..layers.losses import CombineFn, LabelSmoothingLossFn
 from .ctc import CTC
+from .error_calculator import ErrorCalculator
 
 
 class AbsESPnetModel(nn.Module):
@@ -123,6 +124,8 @@ class ESPnetASRModel(AbsESPnetModel):
             logging.warning("Set decoder to none as ctc_weight==1.0")
         self.decoder = decoder
         self.criterion_att = LabelSmoothingLoss(vocab_size, ignore_id, lsm_weight, length_normalized_loss)
+        if report_cer or report_wer:  # espnet_model.py:164-167 (used in eval mode only)
+            self.error_calculator = ErrorCalculator(token_list, sym_space, sym_blank, report_cer, report_wer)
         self.ctc = None if ctc_weight == 0.0 else ctc
         self.extract_feats_in_collect_stats = extract_feats_in_collect_stats
         self.is_encoder_whisper = False
@@ -228,6 +231,9 @@ class ESPnetASRModel(AbsESPnetModel):
                                 seed=site_seed(seed, 500, 1))
             stats["loss_ctc"] = loss_ctc.detach()
             stats["cer_ctc"] = None
+            if not self.training and self.error_calculator is not None:  # :571-575
+                ys_hat = self.ctc.argmax(encoder_out)
+                stats["cer_ctc"] = self.error_calculator(ys_hat.cpu(), text.cpu(), is_ctc=True)
         if self.ctc_weight != 1.0:
             loss_att, acc_att = self._calc_att_loss(encoder_out, encoder_out_lens, text, text_lengths,
                                                     seed=site_seed(seed, 600, 1))
@@ -235,6 +241,8 @@ class ESPnetASRModel(AbsESPnetModel):
             stats["acc"] = acc_att
             stats["cer"] = None
             stats["wer"] = None
+            if not self.training and self.error_calculator is not None:  # :551-557
+                stats["cer"], stats["wer"] = self.error_calculator(self._att_argmax(), text.cpu())
         else:
             stats["loss_att"] = None
             stats["acc"] = None
@@ -248,7 +256,9 @@ class ESPnetASRModel(AbsESPnetModel):
             loss = CombineFn.apply(loss_ctc, loss_att, float(self.ctc_weight))
         stats["loss"] = loss.detach()
         # force_gatherable (device_funcs.py:36-71): 0-d -> (1,), int weight -> int64 tensor
-        stats = {k: (v.view(1) if isinstance(v, torch.Tensor) else v) for k, v in stats.items()}
+        stats = {k: (v.view(1) if isinstance(v, torch.Tensor)
+                     else torch.tensor([v], dtype=torch.float, device=loss.device) if isinstance(v, float)
+                     else v) for k, v in stats.items()}
         weight = torch.full((1,), batch_size, dtype=torch.long, device=loss.device)
         return loss.view(1), stats, weight
 
@@ -282,6 +292,14 @@ class ESPnetASRModel(AbsESPnetModel):
             feats, feats_lengths = self.normalize(feats, feats_lengths)
         encoder_out, encoder_out_lens, _ = self.encoder(feats, feats_lengths, seed=seed)
         return encoder_out, encoder_out_lens
+
+    def _att_argmax(self):
+        """decoder_out.argmax(dim=-1) (espnet_model.py:555) on the device, first maximal index."""
+        lg = self._last_decoder_out.float().contiguous()
+        B, L1, V = lg.shape
+        out = torch.empty(B, L1, dtype=torch.long, device=lg.device)
+        lib.ea_argmax_rows(B * L1, V, lg.data_ptr(), V, out.data_ptr(), ops.stream())
+        return out.cpu()
 
     def _calc_att_loss(self, encoder_out, encoder_out_lens, ys_pad, ys_pad_lens, seed=0):
         """espnet_model.py:518-553 (training path: cer/wer None)."""
