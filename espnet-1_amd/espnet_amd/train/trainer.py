@@ -14,9 +14,11 @@ issues no host synchronisation; the grad norm is returned as a device tensor.
 from __future__ import annotations
 
 import time
-from typing import Dict, Optional
+import math
+from typing import Dict, Iterable, Optional
 
 import torch
+import torch.distributed as dist
 
 from ..optim.adam import ArenaAdam
 
@@ -48,3 +50,45 @@ class Trainer:
                 scheduler.step()
             optimizer.zero_grad()
         return loss.detach(), stats, weight, grad_norm
+
+    @staticmethod
+    @torch.no_grad()
+    def validate_one_epoch(model, iterator: Iterable, dp=None, device="cuda") -> Dict[str, float]:
+        """trainer.py:735-783 plus the epoch summary of SubReporter (reporter.py aggregate,
+        WeightedAverage): eval mode, one forward per minibatch (CER/WER come from the model's
+        ErrorCalculator), stats weighted-averaged across ranks per batch and then across
+        batches by batch weight, skipping None and non-finite values. Ranks whose iterators
+        run out first stop everyone through the reference's iterator_stop all-reduce.
+        `device` holds the stop flag: "cuda" for RCCL, "cpu" for gloo."""
+        was_training = model.training
+        model.eval()
+        distributed = dp is not None and dp.world_size > 1
+        group = dp.group if distributed else None
+        stop = torch.zeros((), dtype=torch.long, device=device)
+        sums: Dict[str, float] = {}
+        wsums: Dict[str, float] = {}
+        exhausted = True
+        for batch in iterator:
+            if isinstance(batch, tuple):  # (utt_id, batch) as the reference's iterators yield
+                batch = batch[1]
+            if distributed:
+                dist.all_reduce(stop, group=group)
+                if stop.item() > 0:
+                    exhausted = False
+                    break
+            loss, stats, weight = model(**batch)
+            stats = {k: v for k, v in stats.items() if v is not None}
+            if distributed:
+                _, stats, weight = dp.weighted_average(loss, stats, weight)
+            w = float(weight.sum())
+            for k, v in stats.items():
+                v = float(v.sum())
+                if math.isfinite(v) and math.isfinite(w):
+                    sums[k] = sums.get(k, 0.0) + v * w
+                    wsums[k] = wsums.get(k, 0.0) + w
+        if distributed and exhausted:
+            stop.fill_(1)
+            dist.all_reduce(stop, group=group)
+        if was_training:
+            model.train()
+        return {k: (sums[k] / wsums[k] if wsums[k] else float("nan")) for k in sums}

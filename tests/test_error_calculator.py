@@ -126,3 +126,43 @@ def test_eval_forward_reports_error_rates(name):
     m.train()
     _, stats, _ = m(**inp)
     assert stats["cer_ctc"] is None and stats["cer"] is None and stats["wer"] is None
+
+
+@pytest.mark.gpu
+def test_validate_one_epoch_matches_oracle():
+    """Trainer.validate_one_epoch over the tiny hybrid batch split in two minibatches equals
+    the batch-size-weighted average of the oracle's eval-mode stats (reporter.py aggregate)."""
+    from goldens import load, section
+    from oracle.asr_oracle import OracleASR
+    from test_model_build import build
+    from espnet_amd.train.trainer import Trainer
+    cfg, d = load("tiny_hybrid")
+    torch.manual_seed(0)
+    m = build(cfg)
+    w = {k: torch.from_numpy(v) for k, v in section(d, "w").items()}
+    m.load_state_dict(w)
+    m.prepare("cuda", amp=False)
+    inp = {k: torch.from_numpy(v) for k, v in section(d, "in").items()}
+    B = inp["speech"].shape[0]
+    assert B >= 2
+    cut = B // 2
+    parts = [{k: v[:cut] for k, v in inp.items()}, {k: v[cut:] for k, v in inp.items()}]
+    got = Trainer.validate_one_epoch(m, iter(parts))
+    assert m.training
+    ora = OracleASR(cfg, w)
+    ora.training = False
+    sums, wsum = {}, 0
+    for p in parts:
+        with torch.no_grad():
+            _, st, _ = ora(**{k: v.clone() for k, v in p.items()})
+        text = p["text"][:, : int(p["text_lengths"].max())].numpy()
+        st = {k: float(v) for k, v in st.items()}
+        st["cer_ctc"] = oracle_cer_ctc(ora.ctc_logits.argmax(-1).numpy(), text, m.token_list)
+        st["cer"], st["wer"] = oracle_cer_wer(ora.decoder_out.argmax(-1).numpy(), text, m.token_list)
+        n = p["speech"].shape[0]
+        for k, v in st.items():
+            sums[k] = sums.get(k, 0.0) + v * n
+        wsum += n
+    assert set(got) == set(sums)
+    for k in sums:
+        assert got[k] == pytest.approx(sums[k] / wsum, rel=1e-4, abs=1e-4), k
