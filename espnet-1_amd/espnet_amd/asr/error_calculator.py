@@ -15,20 +15,29 @@ from __future__ import annotations
 from itertools import groupby
 from typing import List, Optional, Sequence
 
+import numpy as np
+
 
 def edit_distance(hyp: Sequence, ref: Sequence) -> int:
-    """Unit-cost Levenshtein distance (editdistance.eval), two-row dynamic programme."""
+    """Unit-cost Levenshtein distance (editdistance.eval). One numpy pass per hypothesis
+    element: the substitution/deletion terms are elementwise over the previous row, and the
+    insertion chain cur[j] = min_k<=j (t[k] + j - k) is j + a cumulative minimum of t[k] - k,
+    so a row costs a few vector ops instead of a Python loop over the reference."""
     if len(hyp) < len(ref):
         hyp, ref = ref, hyp
-    if not ref:
+    if len(ref) == 0:
         return len(hyp)
-    prev = list(range(len(ref) + 1))
-    for i, h in enumerate(hyp, 1):
-        cur = [i] + [0] * len(ref)
-        for j, r in enumerate(ref, 1):
-            cur[j] = min(prev[j] + 1, cur[j - 1] + 1, prev[j - 1] + (h != r))
-        prev = cur
-    return prev[-1]
+    ids: dict = {}
+    h = np.fromiter((ids.setdefault(x, len(ids)) for x in hyp), dtype=np.int64, count=len(hyp))
+    r = np.fromiter((ids.setdefault(x, len(ids)) for x in ref), dtype=np.int64, count=len(ref))
+    ramp = np.arange(len(r) + 1, dtype=np.int64)
+    prev = ramp.copy()
+    t = np.empty_like(prev)
+    for i, x in enumerate(h, 1):
+        t[0] = i
+        np.minimum(prev[1:] + 1, prev[:-1] + (r != x), out=t[1:])
+        prev = np.minimum.accumulate(t - ramp) + ramp
+    return int(prev[-1])
 
 
 def _rows(t) -> List[List[int]]:
