@@ -42,7 +42,18 @@ struct GemmP {
   const unsigned long long* salt;  // per-step dropout salt (device), see ea_set_rng_salt
   unsigned long long* stamp;       // kernel-span probe [first block start, last block end] or null
   ea_conv_geo g;                   // implicit-GEMM operand geometry (g.mode 0: dense operands)
+  unsigned long long* diag;        // ea_gemm_set_diag: per-block [start, main loop done, end] s_memtime
 };
+
+// Diagnostic timeline (ea_gemm_set_diag): thread 0 of each block stamps the shader clock at
+// the block's start, after its main loop and at its end; off (null) in normal runs.
+EA_DEV void diag_stamp(const GemmP& p, int slot) {
+  if (p.diag && threadIdx.x == 0) {
+    const long b = blockIdx.x + (long)gridDim.x * blockIdx.z;
+    p.diag[b * 4 + slot] = __builtin_amdgcn_s_memtime();
+    if (slot == 0) p.diag[b * 4 + 3] = __builtin_amdgcn_s_memrealtime();
+  }
+}
 
 // In-kernel span probe (ea_gemm_set_probe): s_memrealtime is the GPU's constant 100 MHz
 // clock; the first block to start and the last to finish bound the launch's execution.
@@ -122,7 +133,7 @@ EA_DEV bf16x8 frag_bf16(const char* lds, int r0, int ks, int lane) {
       const int row = ks * 32 + 8 * (lane >> 4) + 4 * half + q;
       const char* a = lds + row * 256 + ((ch ^ swz_mn_bf16(row)) << 4) + within;
       out.h[half] = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-          (__attribute__((address_space(3))) s16x4*)(uintptr_t)(a));
+          (__attribute__((address_space(3))) s16x4*)(a));
     }
     return out.v;
   }
@@ -531,20 +542,25 @@ EA_DEV bf16x8 frag_img(const char* img, int r, int ks, int lane) {
 
 // Epilogue of one wave's (MI*16) x (NJ*16) accumulator tile, in 64 x 64 chunks transposed
 // through the wave's private LDS region (64 x EPI_LDT floats); each lane then owns 4
-// consecutive columns of 16 rows per chunk, handled 8 rows at a time (epi_batch).  With
-// split-K (p.splitk > 1) the chunk goes to this slice's f32 slab instead.
+// consecutive columns of 16 rows per chunk.  The operand the epilogue kind reads (aux /
+// resid / C for beta != 0) is loaded for all of the chunk's row groups at once, right after
+// the transposition has freed the chunk's accumulator registers: one load round trip per
+// chunk instead of one per small batch; bias is read once per chunk.  With split-K (p.splitk > 1) the chunk goes to this slice's f32 slab.
 template <int KIND, int MI, int NJ>
 EA_DEV void epi_wave(const GemmP& p, const EpiK& k, char* smem, int z, int zb, int zh, int r0, int c0, int lane,
                      int w, const f32x4 (&acc)[MI][NJ]) {
   constexpr int RC = MI < 4 ? MI : 4;  // row blocks per chunk
-  constexpr int NB = MI * NJ >= 32 ? 4 : (RC * 4 < 8 ? RC * 4 : 8);  // fewer in flight beside big accumulators
+  constexpr int NG = RC * 4;           // row groups (of 4 lanes' rows) per lane per chunk
   float* t = (float*)smem + w * (RC * 16) * EPI_LDT;
   const int rq = (lane >> 4) * 4, cc = lane & 15, lc = (lane & 15) * 4;
   float* slab = p.splitk > 1 ? p.ws + ((long)z * p.splitk + (blockIdx.z % p.splitk)) * (long)p.M * p.N : nullptr;
+  const bool reads = !slab && (KIND == EA_EPI_DACT || (KIND == EA_EPI_RESID && p.epi.resid) ||
+                               (KIND == EA_EPI_STORE && p.epi.beta != 0.f));
 #pragma unroll
   for (int ri = 0; ri < MI / RC; ++ri) {
 #pragma unroll
     for (int cj = 0; cj < NJ / 4; ++cj) {
+      const int rb = r0 + ri * RC * 16, col = c0 + cj * 64 + lc;
       if (ri + cj > 0) {
         __builtin_amdgcn_wave_barrier();
         asm volatile("" ::: "memory");
@@ -558,10 +574,9 @@ EA_DEV void epi_wave(const GemmP& p, const EpiK& k, char* smem, int z, int zb, i
             t[(i * 16 + rq + rr) * EPI_LDT + j * 16 + cc] = acc[ri * RC + i][cj * 4 + j][rr];
       __builtin_amdgcn_wave_barrier();
       asm volatile("" ::: "memory");
-      const int rb = r0 + ri * RC * 16, col = c0 + cj * 64 + lc;
       if (!p.vec_c) {  // cold path: element-wise straight from the LDS image
 #pragma unroll 1
-        for (int it = 0; it < RC * 4; ++it) {
+        for (int it = 0; it < NG; ++it) {
           const int lr = it * 4 + (lane >> 4), row = rb + lr;
           if (row >= p.M) continue;
 #pragma unroll 1
@@ -574,25 +589,32 @@ EA_DEV void epi_wave(const GemmP& p, const EpiK& k, char* smem, int z, int zb, i
         }
         continue;
       }
-#pragma unroll 1
-      for (int it0 = 0; it0 < RC * 4; it0 += NB) {
-        int rows[NB], cols[NB];
-        float v[NB][4];
+      float bias[4] = {0.f, 0.f, 0.f, 0.f};
+      if (!slab && KIND != EA_EPI_DACT && p.epi.bias && col < p.N) {
+        const float4 bb = *(const float4*)(p.epi.bias + col);
+        bias[0] = bb.x; bias[1] = bb.y; bias[2] = bb.z; bias[3] = bb.w;
+      }
+      // the chunk's operand loads in flight HB row groups at a time (the chunk's accumulators
+      // are in LDS now, so their registers hold the operand)
+      constexpr int HB = NG < 8 ? NG : 8;
 #pragma unroll
-        for (int i = 0; i < NB; ++i) {
-          const int lr = (it0 + i) * 4 + (lane >> 4);
-          const float4 f = *(const float4*)(t + lr * EPI_LDT + lc);
-          rows[i] = rb + lr;
-          cols[i] = col;
-          v[i][0] = f.x; v[i][1] = f.y; v[i][2] = f.z; v[i][3] = f.w;
+      for (int h0 = 0; h0 < NG; h0 += HB) {
+        float o[HB][4];
+        if (reads) {
+#pragma unroll
+          for (int it = 0; it < HB; ++it) {
+            const int row = rb + (h0 + it) * 4 + (lane >> 4);
+            if (row < p.M && col < p.N) epi_src<KIND>(p, zb, zh, row, col, o[it]);
+          }
         }
-        if (slab) {
 #pragma unroll
-          for (int i = 0; i < NB; ++i)
-            if (rows[i] < p.M && col < p.N)
-              *(float4*)(slab + (long)rows[i] * p.N + col) = make_float4(v[i][0], v[i][1], v[i][2], v[i][3]);
-        } else {
-          epi_batch<KIND, NB>(p, k, z, zb, zh, rows, cols, v);
+        for (int it = 0; it < HB; ++it) {
+          const int lr = (h0 + it) * 4 + (lane >> 4), row = rb + lr;
+          const float4 f = *(const float4*)(t + lr * EPI_LDT + lc);
+          if (row >= p.M || col >= p.N) continue;
+          const float v[4] = {f.x, f.y, f.z, f.w};
+          if (slab) *(float4*)(slab + (long)row * p.N + col) = f;
+          else epi_four_pre<KIND>(p, k, z, zb, zh, row, col, v, bias, reads, o[it]);
         }
       }
     }
@@ -880,6 +902,445 @@ __global__ __launch_bounds__(128 * WN, 1) void gemm_bf16_lds(GemmP p) {
   probe_end(p);
 }
 
+// ---------------------------------------------------------------- ping-pong 256x256 kernel
+// gemm_pipe: the 256x256 tile of gemm_bf16_lds with a ping-pong schedule.  K moves in 32-deep
+// slices through a 4-slot LDS ring (32 KiB per slot: A 256x32 + B 256x32 bf16), DMA issued
+// three slices ahead.  The eight wave64s form two groups, G0 = waves 0-3 (tile rows 0-127)
+// and G1 = waves 4-7 (rows 128-255); every SIMD holds one wave of each.  Each wave alternates
+// a LOAD segment (read its slice fragments LDS -> registers, issue its share of the DMA three
+// slices ahead, counted vmcnt for the next slice, lgkmcnt(0)) and a COMPUTE segment (32 MFMAs
+// over its 128 x 64 sub-tile), one s_barrier after each.  G1 runs one barrier behind G0, so
+// on every SIMD one wave's MFMAs overlap the other wave's loads:
+//
+//   segment:   2s          2s+1          2s+2
+//   G0:        LOAD(s)     COMPUTE(s)    LOAD(s+1)
+//   G1:        COMPUTE(s-1) LOAD(s)      COMPUTE(s)
+//
+// Slice s is readable once every wave has waited for its own DMA share of s (at the end of
+// its LOAD(s-1)) and a barrier has passed; the DMA of slice s+3 goes to the slot of slice s-1,
+// whose last reads (G1's LOAD(s-1)) retired before the barrier that opens G0's LOAD(s).
+//
+// LDS images of a 32-deep slice (16-B chunks, lane-linear DMA: the swizzle is applied to the
+// per-lane SOURCE address):
+//  * K-major operand: [256 rows][4 chunks] (64-B rows); logical chunk c of row r is stored at
+//    c ^ (((r >> 3) & 1) << 1), which makes every ds_read_b128 lane group of a 16-row
+//    fragment read 16 distinct 16-B bank slots (conflict-free).
+//  * MN-major operand: two [32 k][128] panels of 8 KiB with gemm_bf16_lds's swz_mn_bf16
+//    chunk swizzle, read with ds_read_b64_tr_b16.
+EA_DEV int swz32(int r) { return ((r >> 3) & 1) << 1; }
+
+template <bool KMAJ>
+EA_DEV int img32_off(int c) {  // byte offset of (logical) chunk c's LDS slot
+  if (KMAJ) {
+    const int row = c >> 2, ch = c & 3;
+    return row * 64 + ((ch ^ swz32(row)) << 4);
+  } else {
+    const int pnl = c >> 9, cj = c & 511, k = cj >> 4, ch = cj & 15;
+    return pnl * 8192 + k * 256 + ((ch ^ swz_mn_bf16(k)) << 4);
+  }
+}
+
+// ds_read_b64_tr_b16 as inline asm: hipcc's waitcnt pass puts a vmcnt(0) in front of every
+// tr-read builtin while an LDS-DMA is in flight (it cannot tell the two apart), which would
+// drain the DMA pipeline every slice.  The caller waits lgkmcnt(0) itself (then a
+// sched_barrier) before any use of the result.
+EA_DEV s16x4 tr_read_asm(const char* p) {
+  s16x4 v;
+  const uint32_t a = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) char*)p;
+  asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(v) : "v"(a) : "memory");
+  return v;
+}
+
+template <bool KMAJ>
+EA_DEV bf16x8 frag32(const char* img, int r, int lane) {  // 16 rows/cols from r (mult. of 16)
+  if (KMAJ) {
+    const int row = r + (lane & 15), ch = lane >> 4;
+    return *(const bf16x8*)(img + row * 64 + ((ch ^ swz32(row)) << 4));
+  }
+  // as frag_bf16<false> (8 consecutive k of column (lane&15) via two transposed 4 x 4 reads)
+  const char* pnl = img + (r >> 7) * 8192;
+  const int i = lane & 15, q = i >> 2, pp = i & 3;
+  const int col = (r & 127) + 4 * pp;
+  const int ch = col >> 3, within = (col & 7) * 2;
+  union { bf16x8 v; s16x4 h[2]; } out;
+#pragma unroll
+  for (int half = 0; half < 2; ++half) {
+    const int row = 8 * (lane >> 4) + 4 * half + q;
+    out.h[half] = tr_read_asm(pnl + row * 256 + ((ch ^ swz_mn_bf16(row)) << 4) + within);
+  }
+  return out.v;
+}
+
+namespace pipe {
+constexpr int BMP = 256, BNP = 256, BK = 32, NSLOT = 4, NW = 8, NTT = 512;
+constexpr int A_BYTES = BMP * BK * 2, B_BYTES = BNP * BK * 2, SLOT = A_BYTES + B_BYTES;
+constexpr int RING = NSLOT * SLOT;
+constexpr int EPI_BYTES = NW * 64 * EPI_LDT * 4;
+constexpr int SMEM = RING > EPI_BYTES ? RING : EPI_BYTES;
+constexpr int ACH = A_BYTES / (NTT * 16), BCH = B_BYTES / (NTT * 16);  // 2 + 2 DMA per thread
+constexpr int G = ACH + BCH;
+}  // namespace pipe
+
+// One 256x256 output tile over K range [kbeg, kend) into acc (the wave's 128 x 64 sub-tile);
+// A / B point at this tile's batch slice.  Returns with every wave done reading smem.
+template <bool AK, bool BKM, int MODE = 0>
+EA_DEV void pipe_tile(const GemmP& p, char* smem, const bf16* A, const bf16* B, int m0, int n0, int kbeg,
+                      int kend, f32x4 (&acc)[8][4]) {
+  static_assert(MODE == 0 || (MODE == EA_CONV_FWD && AK && BKM) || (MODE == EA_CONV_DGRAD && AK && !BKM) ||
+                (MODE == EA_CONV_WGRAD && !AK && !BKM), "conv gather layouts");
+  using namespace pipe;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int wm = (w >> 2) * 128, wn = (w & 3) * 64;
+  const int nsl = max(0, (kend - kbeg) / BK);
+  const bool tail = kbeg + nsl * BK < kend;
+
+
+  // per-lane DMA sources (32-bit byte offsets from the slice base): LDS chunk ci lands at
+  // ci*16; its source is the global chunk whose swizzled slot that is
+  auto src = [&](long ld, int mn0, int MN, bool kmaj, int ci) -> uint32_t {
+    if (kmaj) {
+      const int row = ci >> 2, c = (ci & 3) ^ swz32(ci >> 2);
+      return (uint32_t)(((long)min(mn0 + row, MN - 1) * ld + c * 8) * 2);
+    }
+    const int pnl = ci >> 9, cj = ci & 511, k = cj >> 4, c = (cj & 15) ^ swz_mn_bf16(k);
+    return (uint32_t)(((long)k * ld + min((long)(mn0 + pnl * 128 + c * 8), ld - 8)) * 2);
+  };
+  const char* abase = (const char*)(A + (AK ? (long)kbeg : (long)kbeg * p.lda));
+  const char* bbase = (const char*)(B + (BKM ? (long)kbeg : (long)kbeg * p.ldb));
+  uint32_t aoff[ACH], boff[BCH];
+#pragma unroll
+  for (int i = 0; i < ACH; ++i) aoff[i] = src(p.lda, m0, p.M, AK, (i * NW + w) * 64 + lane);
+#pragma unroll
+  for (int i = 0; i < BCH; ++i) boff[i] = src(p.ldb, n0, p.N, BKM, (i * NW + w) * 64 + lane);
+  const long astep = (AK ? BK : (long)BK * p.lda) * 2;  // bytes per slice
+  const long bstep = (BKM ? BK : (long)BK * p.ldb) * 2;
+
+  // implicit-GEMM gathers (gemm_bf16_lds's scheme on 32-deep slices; the host guarantees
+  // C % 64 == 0, so a slice never straddles two taps and K has no remainder).  A rows
+  // (FWD / DGRAD): each chunk's pixel decoded once, its source rebuilt when a slice enters a
+  // new tap.  B rows (WGRAD, k = pixel): each chunk's pixel advanced by 32 per slice.
+  const int ksl0 = kbeg / BK;                  // global slice index of this range's first slice
+  const int CS = MODE ? p.g.C / BK : 1;        // slices per tap
+  int gb[ACH], gt[ACH], gf[ACH], cur[ACH];
+  if constexpr (MODE == EA_CONV_FWD || MODE == EA_CONV_DGRAD) {
+    const int n2 = MODE == EA_CONV_FWD ? p.g.T2 : p.g.nI[p.g.a];
+    const int n3 = MODE == EA_CONV_FWD ? p.g.F2 : p.g.nJ[p.g.e];
+#pragma unroll
+    for (int i = 0; i < ACH; ++i) {
+      const int m = min(m0 + ((((i * NW + w) * 64 + lane)) >> 2), p.M - 1);
+      const int bt = fdiv(m, n3);
+      gf[i] = m - bt * n3;
+      gb[i] = fdiv(bt, n2);
+      gt[i] = bt - gb[i] * n2;
+      cur[i] = 0;
+    }
+  }
+  auto a_tap = [&](int q) {  // A chunk sources (elements) for tap q
+#pragma unroll
+    for (int i = 0; i < ACH; ++i) {
+      const int ci = (i * NW + w) * 64 + lane;
+      const int cc = ((ci & 3) ^ swz32(ci >> 2)) * 8;
+      if constexpr (MODE == EA_CONV_FWD) {
+        const int kh = q / 3, kw = q - 3 * (q / 3);
+        cur[i] = (int)x1p_row(p.g, gb[i], gt[i], gf[i], kh, kw) + cc;
+      } else {
+        int kh, kw;
+        dgrad_tap(p.g, q, kh, kw);
+        const int t2 = gt[i] - (kh >> 1), f2 = gf[i] - (kw >> 1);  // t1 = 2*t2 + kh
+        cur[i] = (t2 >= 0 && t2 < p.g.T2 && f2 >= 0 && f2 < p.g.F2)
+                     ? ((gb[i] * p.g.T2 + t2) * p.g.F2 + f2) * p.g.C + cc
+                     : (int)p.g.zero + ((ci >> 2) & 63) * p.g.C + cc;  // spread over 64 zero rows
+      }
+    }
+  };
+  int wb[BCH], wt[BCH], wf[BCH], wpix[BCH], wbase[BCH], wnI[BCH], wnJ[BCH];
+  if constexpr (MODE == EA_CONV_WGRAD) {
+#pragma unroll
+    for (int i = 0; i < BCH; ++i) {
+      const int ci = (i * NW + w) * 64 + lane;
+      const int pnl = ci >> 9, cj = ci & 511, k = cj >> 4, c = (cj & 15) ^ swz_mn_bf16(k);
+      const int n = min(n0 + pnl * 128 + c * 8, p.N - 8);
+      const int tap = n / p.g.C, cin = n - tap * p.g.C;
+      const int kh = tap / 3, kw = tap - 3 * kh, a = kh & 1, e = kw & 1;
+      wnI[i] = p.g.nI[a];
+      wnJ[i] = p.g.nJ[e];
+      // row (b*nI + t2 + kh/2)*nJ + f2 + kw/2 of plane (a, e): the tap shift folded into the base
+      wbase[i] = (int)p.g.plane[a * 2 + e] + ((kh >> 1) * wnJ[i] + (kw >> 1)) * p.g.C + cin;
+      const int pix = ksl0 * BK + k;
+      wpix[i] = pix;
+      const int bt = fdiv(pix, p.g.F2);
+      wf[i] = pix - bt * p.g.F2;
+      wb[i] = fdiv(bt, p.g.T2);
+      wt[i] = bt - wb[i] * p.g.T2;
+    }
+  }
+  const int dF = BK % max(p.g.F2, 1), dT = BK / max(p.g.F2, 1);
+
+  auto issue = [&](int sl) {  // called for sl = 0, 1, 2, ... in order (gather state advances)
+    char* base = smem + (sl & (NSLOT - 1)) * SLOT;
+    const char* ak = abase + sl * astep;
+    const char* bk = bbase + sl * bstep;
+    if constexpr (MODE == EA_CONV_FWD || MODE == EA_CONV_DGRAD) {
+      const int ks = ksl0 + sl, q = ks / CS, c0 = (ks - q * CS) * BK;
+      if (c0 == 0 || sl == 0) a_tap(q);
+#pragma unroll
+      for (int i = 0; i < ACH; ++i)
+        __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)((const char*)A + (long)(cur[i] + c0) * 2),
+                                         (__attribute__((address_space(3))) void*)(base + (i * NW + w) * 1024), 16, 0, 0);
+      if constexpr (MODE == EA_CONV_DGRAD) {  // W2t [9][co][ci]: a slice = 32 co of one tap
+        int kh, kw;
+        dgrad_tap(p.g, q, kh, kw);
+        bk = (const char*)(B + ((long)(kh * 3 + kw) * p.g.C + c0) * p.g.C);
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < ACH; ++i)
+        __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)(ak + aoff[i]),
+                                         (__attribute__((address_space(3))) void*)(base + (i * NW + w) * 1024), 16, 0, 0);
+    }
+    if constexpr (MODE == EA_CONV_WGRAD) {  // B[k = pixel][n = (tap, ci)] gathered from x1p
+#pragma unroll
+      for (int i = 0; i < BCH; ++i) {
+        const int off = wpix[i] < p.g.P ? wbase[i] + ((wb[i] * wnI[i] + wt[i]) * wnJ[i] + wf[i]) * p.g.C
+                                        : (int)p.g.zero + (lane & 63) * p.g.C + (wbase[i] % p.g.C);
+        __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)((const char*)B + (long)off * 2),
+                                         (__attribute__((address_space(3))) void*)(base + A_BYTES + (i * NW + w) * 1024),
+                                         16, 0, 0);
+        wpix[i] += BK;  // next slice: 32 pixels on
+        wf[i] += dF;
+        wt[i] += dT;
+        if (wf[i] >= p.g.F2) { wf[i] -= p.g.F2; ++wt[i]; }
+        while (wt[i] >= p.g.T2) { wt[i] -= p.g.T2; ++wb[i]; }
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < BCH; ++i)
+        __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)(bk + boff[i]),
+                                         (__attribute__((address_space(3))) void*)(base + A_BYTES + (i * NW + w) * 1024),
+                                         16, 0, 0);
+    }
+  };
+
+  auto rd_b = [&](int sl, bf16x8 (&fb)[4]) {
+    const char* lb = smem + (sl & (NSLOT - 1)) * SLOT + A_BYTES;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) fb[j] = frag32<BKM>(lb, wn + j * 16, lane);
+  };
+  auto rd_a = [&](int sl, bf16x8 (&fa)[8]) {
+    const char* la = smem + (sl & (NSLOT - 1)) * SLOT;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) fa[i] = frag32<AK>(la, wm + i * 16, lane);
+  };
+
+  const int g1 = w >> 2;  // wave group: G1 runs one barrier behind G0
+  const int npre = min(NSLOT - 1, nsl);
+  for (int sl = 0; sl < npre; ++sl) issue(sl);
+  // own share of slice 0 landed (slices 1, 2 may stay in flight), then everyone's
+  if (npre >= 3) wait_vmcnt<2 * G>();
+  else if (npre == 2) wait_vmcnt<G>();
+  else wait_vmcnt<0>();
+  lds_barrier();
+  if (g1) lds_barrier();  // the stagger
+  bf16x8 fa[8], fb[4];
+  for (int sl = 0; sl < nsl; ++sl) {
+    // ---- LOAD(sl)
+    __builtin_amdgcn_sched_barrier(0);
+    rd_b(sl, fb);
+    rd_a(sl, fa);
+    if (sl + NSLOT - 1 < nsl) issue(sl + NSLOT - 1);
+    // own share of slice sl+1 landed: the groups issued after it (sl+2, sl+3) may stay in flight
+    const int newer = min(2, nsl - 2 - sl);
+    if (newer >= 2) wait_vmcnt<2 * G>();
+    else if (newer == 1) wait_vmcnt<G>();
+    else wait_vmcnt<0>();
+    // fragments in registers before the barrier: the COMPUTE segment never waits on LDS, and
+    // this wave is done reading slot sl when the barrier releases its refill
+    if (!AK || !BKM) {  // asm tr-reads are invisible to the waitcnt pass
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i) asm volatile("" ::"v"(fa[i]));
+#pragma unroll
+    for (int j = 0; j < 4; ++j) asm volatile("" ::"v"(fb[j]));
+    __builtin_amdgcn_sched_barrier(0);
+    lds_barrier();
+    // ---- COMPUTE(sl)
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+    __builtin_amdgcn_sched_barrier(0);
+    lds_barrier();
+  }
+  if (!g1) lds_barrier();  // balance G1's extra barrier
+  if (tail) {  // K remainder (< 32) through registers, zero-filled, into slot 0
+    constexpr int NCH = (A_BYTES + B_BYTES) / 16 / NTT;  // 4 chunks per thread
+    uint4 v[NCH];
+    const int k0 = kbeg + nsl * BK;
+#pragma unroll
+    for (int i = 0; i < NCH; ++i) {
+      const int c = tid + NTT * i;
+      const bool isa = c < A_BYTES / 16;
+      const int cc = isa ? c : c - A_BYTES / 16;
+      const bool km = isa ? AK : BKM;
+      const bf16* base = isa ? A : B;
+      const long ld = isa ? p.lda : p.ldb;
+      const int MN = isa ? p.M : p.N, mn0 = isa ? m0 : n0;
+      int mn, k;
+      if (km) { mn = mn0 + (cc >> 2); k = k0 + (cc & 3) * 8; }
+      else    { const int cj = cc & 511; k = k0 + (cj >> 4); mn = mn0 + (cc >> 9) * 128 + (cj & 15) * 8; }
+      union { uint4 u; bf16 e[8]; } tv;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const bool ok = km ? (mn < MN && k + e < kend) : (k < kend && mn + e < MN);
+        tv.e[e] = ok ? (km ? base[(long)mn * ld + k + e] : base[(long)k * ld + mn + e]) : (bf16)0.f;
+      }
+      v[i] = tv.u;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < NCH; ++i) {
+      const int c = tid + NTT * i;
+      const bool isa = c < A_BYTES / 16;
+      const int cc = isa ? c : c - A_BYTES / 16;
+      const int off = isa ? (AK ? img32_off<true>(cc) : img32_off<false>(cc))
+                          : A_BYTES + (BKM ? img32_off<true>(cc) : img32_off<false>(cc));
+      *(uint4*)(smem + off) = v[i];
+    }
+    __syncthreads();
+    rd_b(0, fb);
+    rd_a(0, fa);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+  }
+
+  __syncthreads();  // every wave is done reading the ring
+}
+
+template <bool AK, bool BKM, int MODE = 0>
+__global__ __launch_bounds__(512, 1) void gemm_pipe(GemmP p) {
+  using namespace pipe;
+  __shared__ __attribute__((aligned(1024))) char smem[SMEM];
+  probe_start(p);
+
+  const int nt = p.tiles_m * p.tiles_n;
+  const int bid = blockIdx.x;
+  const int q8 = nt / 8, r8 = nt % 8, xcd = bid % 8;
+  const int t = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + bid / 8;
+  const int GM = 8;
+  const int grp = t / (GM * p.tiles_n);
+  const int gm0 = grp * GM;
+  const int gsz = min(GM, p.tiles_m - gm0);
+  const int tm = gm0 + (t % (GM * p.tiles_n)) % gsz;
+  const int tn = (t % (GM * p.tiles_n)) / gsz;
+  const int m0 = tm * BMP, n0 = tn * BNP;
+
+  const int z = blockIdx.z / p.splitk, sk = blockIdx.z % p.splitk;
+  const int zb = z / p.nh, zh = z % p.nh;
+  const bf16* A = (const bf16*)p.A + zb * p.sAb + zh * p.sAh;
+  const bf16* B = (const bf16*)p.B + zb * p.sBb + zh * p.sBh;
+  const int kbeg = sk * p.kchunk;
+  const int kend = min(p.K, kbeg + p.kchunk);
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int wm = (w >> 2) * 128, wn = (w & 3) * 64;
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  diag_stamp(p, 0);
+  pipe_tile<AK, BKM, MODE>(p, smem, A, B, m0, n0, kbeg, kend, acc);
+  diag_stamp(p, 1);
+  const EpiK ek = make_epik(p);
+  switch (p.splitk > 1 ? EA_EPI_STORE : p.epi.kind) {
+    case EA_EPI_STORE: epi_wave<EA_EPI_STORE, 8, 4>(p, ek, smem, z, zb, zh, m0 + wm, n0 + wn, lane, w, acc); break;
+    case EA_EPI_ACT: epi_wave<EA_EPI_ACT, 8, 4>(p, ek, smem, z, zb, zh, m0 + wm, n0 + wn, lane, w, acc); break;
+    case EA_EPI_RESID: epi_wave<EA_EPI_RESID, 8, 4>(p, ek, smem, z, zb, zh, m0 + wm, n0 + wn, lane, w, acc); break;
+    default: epi_wave<EA_EPI_DACT, 8, 4>(p, ek, smem, z, zb, zh, m0 + wm, n0 + wn, lane, w, acc); break;
+  }
+  if (p.diag) {
+    __syncthreads();
+    diag_stamp(p, 2);
+  }
+  probe_end(p);
+}
+
+// ---------------------------------------------------------------- grouped GEMM
+// gemm_grouped: many independent f32-output GEMMs in one launch (ea_gemm_grouped), each tile
+// a 256x256 pipe_tile over the problem's whole K (no split-K, no partial slabs): the Linear
+// weight gradients of a backward pass (dW = dY^T X, K = tokens) are deferred and issued
+// together, so ~1,400 full-K tiles fill the chip instead of ~60-tile launches that need a
+// split and a combine pass each.  The problem table and a tile -> problem map live in a
+// device workspace written by group_upload launches whose ARGUMENTS carry the descriptors
+// (so a captured hipGraph replays the same table); the host orders problems longest-K first.
+struct GroupProbD {
+  const bf16* A;
+  const bf16* B;
+  float* C;
+  int lda, ldb, ldc;
+  int M, N, K;
+  int tiles_n, tile0;
+  float beta;
+};
+constexpr int EA_GROUP_CHUNK = 60;
+struct GroupChunk {
+  int first, n;  // problems [first, first + n) of the table
+  GroupProbD pr[EA_GROUP_CHUNK];
+};
+static_assert(sizeof(GroupChunk) <= 4000, "kernel argument space");
+
+// table layout in the workspace: GroupProbD[nprob] then int map[ntiles]
+__global__ void group_upload(GroupChunk c, GroupProbD* table, int* map) {
+  for (int i = threadIdx.x; i < c.n; i += blockDim.x) table[c.first + i] = c.pr[i];
+  for (int i = 0; i < c.n; ++i) {
+    const GroupProbD& d = c.pr[i];
+    const int nt = ea_cdiv(d.M, 256) * d.tiles_n;
+    for (int t = threadIdx.x; t < nt; t += blockDim.x) map[d.tile0 + t] = c.first + i;
+  }
+}
+
+template <bool AK, bool BKM>
+__global__ __launch_bounds__(512, 1) void gemm_grouped(const GroupProbD* __restrict__ table,
+                                                       const int* __restrict__ map, int ntiles) {
+  using namespace pipe;
+  __shared__ __attribute__((aligned(1024))) char smem[SMEM];
+  const int nt = ntiles;
+  const int bid = blockIdx.x;
+  const int q8 = nt / 8, r8 = nt % 8, xcd = bid % 8;
+  const int t = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + bid / 8;
+  const GroupProbD q = table[__builtin_amdgcn_readfirstlane(map[t])];
+  const int lt = t - q.tile0;
+  const int tm = lt / q.tiles_n, tn = lt - tm * q.tiles_n;  // neighbours share the A panel
+  const int m0 = tm * BMP, n0 = tn * BNP;
+  GemmP p{};
+  p.M = q.M; p.N = q.N; p.K = q.K;
+  p.A = q.A; p.lda = q.lda;
+  p.B = q.B; p.ldb = q.ldb;
+  p.nh = 1; p.splitk = 1; p.kchunk = q.K;
+  p.C = q.C; p.c_dtype = EA_F32; p.ldc = q.ldc;
+  p.epi.kind = EA_EPI_STORE; p.epi.alpha = 1.f; p.epi.beta = q.beta; p.epi.post_scale = 1.f;
+  p.epi.rscale = 1.f;
+  p.vec_c = 1;  // host-checked: N % 4 == 0, ldc % 4 == 0, 16-B aligned C
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int wm = (w >> 2) * 128, wn = (w & 3) * 64;
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  pipe_tile<AK, BKM>(p, smem, q.A, q.B, m0, n0, 0, q.K, acc);
+  const EpiK ek = make_epik(p);
+  epi_wave<EA_EPI_STORE, 8, 4>(p, ek, smem, 0, 0, 0, m0 + wm, n0 + wn, lane, w, acc);
+}
+
 // split-K combine: C = epi(sum_s slab[s]) (any epilogue kind), 4 columns per thread
 __global__ void splitk_reduce(GemmP p) {
   const long MN = (long)p.M * p.N;
@@ -914,7 +1375,9 @@ __global__ void splitk_reduce(GemmP p) {
 
 int g_gemm_stages = 2;
 unsigned long long* g_probe = nullptr;  // ea_gemm_set_probe
-int g_gemm_bm64 = 1;  // LDS ring depth of gemm_bf16_lds (2: 64 KiB, 2 blocks/CU; 3: 96 KiB)
+unsigned long long* g_diag = nullptr;   // ea_gemm_set_diag
+int g_gemm_bm64 = 1;
+int g_gemm_pipe = 0;  // 256x256 dense tiles on gemm_pipe (ea_gemm_set_pipe)  // LDS ring depth of gemm_bf16_lds (2: 64 KiB, 2 blocks/CU; 3: 96 KiB)
 
 int launch_lds(GemmP& p, int a_k, int b_k, int nz, hipStream_t st) {
   dim3 grid(p.tiles_m * p.tiles_n, 1, nz * p.splitk);
@@ -922,6 +1385,13 @@ int launch_lds(GemmP& p, int a_k, int b_k, int nz, hipStream_t st) {
 #define EA_GC(BMV, BNV, AKV, BKV, MD) \
   hipLaunchKernelGGL((gemm_bf16_lds<BMV, BNV, (BNV == 256 ? 4 : 2), AKV, BKV, 2, MD>), grid, dim3(BNV == 256 ? 512 : 256), 0, st, p)
     const bool big = p.bm == 256;
+    if (big && g_gemm_pipe) {
+      if (p.g.mode == EA_CONV_FWD) hipLaunchKernelGGL((gemm_pipe<true, true, EA_CONV_FWD>), grid, dim3(512), 0, st, p);
+      else if (p.g.mode == EA_CONV_DGRAD) hipLaunchKernelGGL((gemm_pipe<true, false, EA_CONV_DGRAD>), grid, dim3(512), 0, st, p);
+      else hipLaunchKernelGGL((gemm_pipe<false, false, EA_CONV_WGRAD>), grid, dim3(512), 0, st, p);
+      EA_LAUNCH_CHECK();
+      return 0;
+    }
     if (p.g.mode == EA_CONV_FWD) {
       if (big) EA_GC(256, 256, true, true, EA_CONV_FWD); else EA_GC(128, 128, true, true, EA_CONV_FWD);
     } else if (p.g.mode == EA_CONV_DGRAD) {
@@ -944,7 +1414,15 @@ int launch_lds(GemmP& p, int a_k, int b_k, int nz, hipStream_t st) {
     if (b_k) EA_GL(64, 128, true, true, 2);
     else EA_GL(64, 128, true, false, 2);
   } else if (p.bm == 256 && p.bn == 256) {
-    EA_GL4(256, 256, 2)
+    if (g_gemm_pipe) {
+      dim3 g2 = grid;
+      if (a_k && b_k) hipLaunchKernelGGL((gemm_pipe<true, true>), g2, dim3(512), 0, st, p);
+      else if (a_k) hipLaunchKernelGGL((gemm_pipe<true, false>), g2, dim3(512), 0, st, p);
+      else if (b_k) hipLaunchKernelGGL((gemm_pipe<false, true>), g2, dim3(512), 0, st, p);
+      else hipLaunchKernelGGL((gemm_pipe<false, false>), g2, dim3(512), 0, st, p);
+    } else {
+      EA_GL4(256, 256, 2)
+    }
   } else {
     EA_GL4(128, 128, 2)
   }
@@ -1015,6 +1493,12 @@ __global__ void probe_end_kernel(unsigned long long* s) {
 }
 }  // namespace
 
+extern "C" int ea_gemm_set_diag(unsigned long long* buf) {
+  EA_ENTRY();
+  g_diag = buf;
+  return 0;
+}
+
 extern "C" int ea_gemm_set_probe(unsigned long long* slots) {
   EA_ENTRY();
   g_probe = slots;
@@ -1034,6 +1518,12 @@ extern "C" int ea_probe_end(unsigned long long* slots, void* stream) {
   EA_CHECK_ARG(slots != nullptr);
   hipLaunchKernelGGL(probe_end_kernel, dim3(1), dim3(1), 0, (hipStream_t)stream, slots);
   EA_LAUNCH_CHECK();
+  return 0;
+}
+
+extern "C" int ea_gemm_set_pipe(int on) {
+  EA_ENTRY();
+  g_gemm_pipe = on;
   return 0;
 }
 
@@ -1070,6 +1560,7 @@ static int gemm_impl(int dtype, int a_kmajor, int b_kmajor, int M, int N, int K,
   p.ws = workspace;
   p.salt = ea_g_rng_salt;
   p.stamp = g_probe;
+  p.diag = g_diag;
   p.g = geo ? *geo : ea_conv_geo{};
   // unaligned operands (odd vocab / leading dims) take the element-wise load path
   p.vec_a = (lda % E == 0 && sAb % E == 0 && sAh % E == 0 && ((uintptr_t)A % 16) == 0);
@@ -1165,4 +1656,63 @@ extern "C" int ea_gemm_conv(const ea_conv_geo* geo, int a_kmajor, int b_kmajor, 
   EA_CHECK_ARG(geo != nullptr && geo->mode >= EA_CONV_FWD && geo->mode <= EA_CONV_WGRAD);
   return gemm_impl(EA_BF16, a_kmajor, b_kmajor, M, N, K, A, lda, 0, 0, B, ldb, 0, 0, 1, 1, C, c_dtype, ldc, 0, 0,
                    epi, workspace, ws_elems, stream, geo);
+}
+
+static long grouped_ws_bytes(int n, long ntiles) { return (long)n * (long)sizeof(GroupProbD) + 4 * ntiles + 256; }
+
+extern "C" int ea_gemm_grouped_ws_bytes(int n, long ntiles, long* bytes) {
+  EA_CHECK_ARG(n >= 0 && ntiles >= 0 && bytes != nullptr);
+  *bytes = grouped_ws_bytes(n, ntiles);
+  return 0;
+}
+
+extern "C" int ea_gemm_grouped(int a_kmajor, int b_kmajor, int n, const ea_group_gemm* probs, void* ws,
+                               long ws_bytes, void* stream) {
+  EA_ENTRY();
+  EA_CHECK_ARG(n >= 0 && (n == 0 || (probs != nullptr && ws != nullptr)));
+  if (n == 0) return 0;
+  hipStream_t st = (hipStream_t)stream;
+  long ntiles = 0;
+  for (int i = 0; i < n; ++i) {
+    const ea_group_gemm& e = probs[i];
+    EA_CHECK_ARG(e.M > 0 && e.N > 0 && e.K > 0 && e.A && e.B && e.C);
+    // pipe_tile operand rules (16-B rows, 32-bit offsets) and the vector epilogue's
+    EA_CHECK_ARG(e.lda % 8 == 0 && e.ldb % 8 == 0 && ((uintptr_t)e.A % 16) == 0 && ((uintptr_t)e.B % 16) == 0);
+    EA_CHECK_ARG(e.N % 4 == 0 && e.ldc % 4 == 0 && ((uintptr_t)e.C % 16) == 0);
+    EA_CHECK_ARG(e.ldc >= e.N && e.lda >= (a_kmajor ? e.K : e.M) && e.ldb >= (b_kmajor ? e.K : e.N));
+    EA_CHECK_ARG(e.lda < (1L << 31) && e.ldb < (1L << 31) && e.ldc < (1L << 31));
+    const double a_ext = 2.0 * ((a_kmajor ? (double)e.M : (double)e.K) * e.lda);
+    const double b_ext = 2.0 * ((b_kmajor ? (double)e.N : (double)e.K) * e.ldb);
+    EA_CHECK_ARG(a_ext < 4.0e9 && b_ext < 4.0e9);
+    ntiles += (long)ea_cdiv(e.M, 256) * ea_cdiv(e.N, 256);
+  }
+  EA_CHECK_ARG(ntiles < (1L << 30) && grouped_ws_bytes(n, ntiles) <= ws_bytes);
+  GroupProbD* table = (GroupProbD*)ws;
+  int* map = (int*)((char*)ws + (long)n * sizeof(GroupProbD));
+  GroupChunk c{};
+  int tile0 = 0;
+  for (int i = 0; i < n; ++i) {
+    const ea_group_gemm& e = probs[i];
+    GroupProbD& d = c.pr[c.n++];
+    d.A = (const bf16*)e.A; d.B = (const bf16*)e.B; d.C = e.C;
+    d.lda = (int)e.lda; d.ldb = (int)e.ldb; d.ldc = (int)e.ldc;
+    d.M = e.M; d.N = e.N; d.K = e.K;
+    d.tiles_n = ea_cdiv(e.N, 256);
+    d.tile0 = tile0;
+    d.beta = e.beta;
+    tile0 += ea_cdiv(e.M, 256) * d.tiles_n;
+    if (c.n == EA_GROUP_CHUNK || i == n - 1) {
+      hipLaunchKernelGGL(group_upload, dim3(1), dim3(256), 0, st, c, table, map);
+      EA_LAUNCH_CHECK();
+      c.first += c.n;
+      c.n = 0;
+    }
+  }
+  const dim3 grid((unsigned)ntiles), block(512);
+  if (a_kmajor && b_kmajor) hipLaunchKernelGGL((gemm_grouped<true, true>), grid, block, 0, st, table, map, (int)ntiles);
+  else if (a_kmajor) hipLaunchKernelGGL((gemm_grouped<true, false>), grid, block, 0, st, table, map, (int)ntiles);
+  else if (b_kmajor) hipLaunchKernelGGL((gemm_grouped<false, true>), grid, block, 0, st, table, map, (int)ntiles);
+  else hipLaunchKernelGGL((gemm_grouped<false, false>), grid, block, 0, st, table, map, (int)ntiles);
+  EA_LAUNCH_CHECK();
+  return 0;
 }

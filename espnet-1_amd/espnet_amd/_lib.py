@@ -22,6 +22,7 @@ LIB_PATH = os.path.join(_PKG, "lib", os.environ.get("EA_LIB_NAME", "libespnet_am
 HEADER = os.path.join(os.path.dirname(os.path.dirname(_PKG)), "include", "espnet_amd.h")
 
 F32, BF16 = 0, 1
+GEMM_PIPE = int(os.environ.get("EA_GEMM_PIPE", "1"))
 ACT_NONE, ACT_SWISH, ACT_RELU = 0, 1, 2
 EPI_STORE, EPI_ACT, EPI_RESID, EPI_DACT = 0, 1, 2, 3
 ERR_BAD_ARG = 1000
@@ -37,6 +38,13 @@ class Epilogue(ctypes.Structure):
         ("aux", ctypes.c_void_p), ("aux_dtype", ctypes.c_int), ("ldaux", ctypes.c_long),
         ("resid", ctypes.c_void_p), ("ldr", ctypes.c_long),
     ]
+
+
+class GroupGemm(ctypes.Structure):
+    """ea_group_gemm: one problem of ea_gemm_grouped."""
+    _fields_ = [("A", ctypes.c_void_p), ("B", ctypes.c_void_p), ("C", ctypes.c_void_p),
+                ("lda", ctypes.c_long), ("ldb", ctypes.c_long), ("ldc", ctypes.c_long),
+                ("M", ctypes.c_int), ("N", ctypes.c_int), ("K", ctypes.c_int), ("beta", ctypes.c_float)]
 
 
 SCHED_CONSTANT, SCHED_WARMUP = 0, 1
@@ -114,6 +122,8 @@ class _Lib:
                 fn = getattr(dll, name)
                 fn.argtypes = argtypes
                 fn.restype = ctypes.c_int
+            # 256x256 GEMM tiles on the ping-pong kernel (gemm_pipe); EA_GEMM_PIPE=0 for A/B
+            dll.ea_gemm_set_pipe(GEMM_PIPE)
             self._dll = dll
         return self._dll
 

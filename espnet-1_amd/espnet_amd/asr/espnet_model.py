@@ -133,6 +133,14 @@ class ESPnetASRModel(AbsESPnetModel):
         self.arena = None
         self.seed = 0
         self._step = 0
+        # loading weights into a prepared model writes the f32 arena (the Parameters are its
+        # views); under AMP the GEMMs read the bf16 shadow, so refresh it after every load
+        self.register_load_state_dict_post_hook(ESPnetASRModel._refresh_shadow_after_load)
+
+    @staticmethod
+    def _refresh_shadow_after_load(module, incompatible_keys):
+        if module.arena is not None:
+            module.arena.refresh_shadow()
 
     # ------------------------------------------------------------------ runtime
     def arena_groups(self):
@@ -172,8 +180,10 @@ class ESPnetASRModel(AbsESPnetModel):
 
     def __del__(self):
         # the library keeps a raw pointer to this model's salt buffer: drop it with the model
-        salt = getattr(self, "_rng_salt", None)
-        if salt is not None and ESPnetASRModel._salt_owner is self._salt_token:
+        token = getattr(self, "_salt_token", None)
+        if token is None:  # prepared but never ran forward: the library never saw its salt
+            return
+        if ESPnetASRModel._salt_owner is token:
             try:
                 lib.ea_set_rng_salt(None)
             except Exception:

@@ -11,7 +11,7 @@ import os
 import torch
 
 from ._lib import (ACT_NONE, BF16, EPI_ACT, EPI_DACT, EPI_RESID, EPI_STORE, F32, Epilogue,
-                   HipError, lib)
+                   GroupGemm, HipError, lib)
 
 __all__ = ["dt", "stream", "gemm", "linear", "linear_dx", "linear_dw", "workspace"]
 
@@ -69,7 +69,7 @@ class wgrad:
         self.tensors = tensors
 
     def __enter__(self):
-        if not OVERLAP_WGRAD:
+        if not OVERLAP_WGRAD or not torch.cuda.is_available():  # (CPU: the gloo DP tests)
             self.ctx = None
             return self
         main = torch.cuda.current_stream()
@@ -105,11 +105,14 @@ GRAD_READY = None  # callable(prefix): a block's parameter gradients are final (
 
 
 def grad_ready(bound):
-    """A block's backward is done: its parameter gradients (some written on the side
-    stream) are final once the main stream has joined the side stream."""
-    join_wgrad()
+    """A block's backward is done.  Single process: its parameter gradients (some written on
+    the side stream) are final once the main stream has joined the side stream.  Data
+    parallel (GRAD_READY set): the hook flushes the deferred weight gradients and issues the
+    bucket all-reduces from the side stream, so the main stream goes on with the backward."""
     if GRAD_READY is not None:
         GRAD_READY(bound.prefix)
+    else:
+        join_wgrad()
 
 
 def dt(t: torch.Tensor) -> int:
@@ -217,14 +220,116 @@ def linear_dx(dy, w, out, *, epi: Epilogue = None):
                 ldc=ldc, epi=epi)
 
 
-def linear_dw(dy, x, dw, *, accumulate=False):
-    """dw[n, k] (+)= sum_r dy[r, n] * x[r, k] — Linear weight gradient (f32 out)."""
+def linear_dw(dy, x, dw, *, accumulate=False, post=None):
+    """dw[n, k] (+)= sum_r dy[r, n] * x[r, k] — Linear weight gradient (f32 out).  While the
+    weight-gradient queue is active (a training backward pass) the GEMM is deferred and
+    launched with the others of the pass by WGRAD_Q.flush(); `post` (a callable consuming dw,
+    e.g. a permute into the gradient arena) then runs right after that launch."""
     R, N, lddy = _rows(dy)
     R2, K, ldx = _rows(x)
     if R != R2:
         raise HipError("row mismatch in linear_dw")
-    return gemm(dy, x, dw, M=N, N=K, K=R, a_kmajor=0, b_kmajor=0, lda=lddy, ldb=ldx,
-                ldc=dw.stride(0), epi=make_epi(beta=1.0 if accumulate else 0.0))
+    beta = 1.0 if accumulate else 0.0
+    if WGRAD_Q.active and WGRAD_Q.add(dy, x, dw, M=N, N=K, K=R, lda=lddy, ldb=ldx, ldc=dw.stride(0), beta=beta,
+                                      post=post):
+        return dw
+    gemm(dy, x, dw, M=N, N=K, K=R, a_kmajor=0, b_kmajor=0, lda=lddy, ldb=ldx,
+         ldc=dw.stride(0), epi=make_epi(beta=beta))
+    if post is not None:
+        post()
+    return dw
+
+
+# ----------------------------------------------------------------------------- deferred weight gradients
+DEFER_WGRAD = os.environ.get("EA_DEFER_WGRAD", "1") != "0"
+_GWS = {}
+
+
+class WgradQueue:
+    """The Linear weight gradients of one backward pass (linear_dw: dW (+)= dY^T X, K = the
+    pass's token count), deferred and launched together as ONE grouped GEMM
+    (ea_gemm_grouped: every 256x256 tile over its problem's whole K on the pipelined main
+    loop) instead of one split-K GEMM + combine pass per Linear.  The queue keeps dY and X
+    alive until the flush.  Problems are ordered longest-K first; a problem whose output
+    overlaps a queued one flushes the queue first (a launch never holds two writers of one
+    element)."""
+
+    def __init__(self):
+        self.active = False
+        self.items = []
+        self.posts = []
+
+    def add(self, dy, x, dw, *, M, N, K, lda, ldb, ldc, beta, post=None) -> bool:
+        if not (dy.dtype == torch.bfloat16 and x.dtype == torch.bfloat16 and dw.dtype == torch.float32):
+            return False
+        if (lda % 8 or ldb % 8 or dy.data_ptr() % 16 or x.data_ptr() % 16 or N % 4 or ldc % 4
+                or dw.data_ptr() % 16 or M <= 0 or N <= 0 or K <= 0):
+            return False
+        if 2.0 * K * lda >= 4.0e9 or 2.0 * K * ldb >= 4.0e9:
+            return False
+        lo = dw.data_ptr()
+        hi = lo + ((M - 1) * ldc + N) * 4
+        if any(lo < it[-1] and it[-2] < hi for it in self.items):
+            self.flush()
+        self.items.append((K, dy, x, dw, M, N, lda, ldb, ldc, beta, lo, hi))
+        if post is not None:
+            self.posts.append(post)
+        return True
+
+    def flush(self):
+        """Launch the queued GEMMs on the current stream."""
+        if not self.items:
+            return
+        items = sorted(self.items, key=lambda t: -t[0])
+        posts = self.posts
+        self.items = []
+        self.posts = []
+        n = len(items)
+        cur = torch.cuda.current_stream()
+        for it in items:  # operands may come from another stream's pool: keep them until this launch ran
+            for t in it[1:4]:
+                t.record_stream(cur)
+        arr = (GroupGemm * n)()
+        ntiles = 0
+        for i, (K, dy, x, dw, M, N, lda, ldb, ldc, beta, _, _) in enumerate(items):
+            arr[i] = GroupGemm(dy.data_ptr(), x.data_ptr(), dw.data_ptr(), lda, ldb, ldc, M, N, K, beta)
+            ntiles += ((M + 255) // 256) * ((N + 255) // 256)
+        nbytes = ctypes.c_long(0)
+        lib.ea_gemm_grouped_ws_bytes(n, ntiles, ctypes.addressof(nbytes))
+        dev = items[0][1].device
+        key = (str(dev), stream())
+        ws = _GWS.get(key)
+        if ws is None or ws.numel() < nbytes.value:
+            ws = torch.empty(max(nbytes.value, 1 << 16), dtype=torch.uint8, device=dev)
+            _GWS[key] = ws
+        lib.ea_gemm_grouped(0, 0, n, ctypes.addressof(arr), ws.data_ptr(), ws.numel(), stream())
+        for post in posts:
+            post()
+
+    def tensors(self):
+        return [t for it in self.items for t in (it[1], it[2])]
+
+
+WGRAD_Q = WgradQueue()
+
+
+class deferred_wgrad:
+    """Context of a training backward pass: linear_dw calls inside are queued (EA_DEFER_WGRAD=0
+    turns this off) and flushed on exit, on the current stream."""
+
+    def __enter__(self):
+        self.prev = WGRAD_Q.active
+        WGRAD_Q.active = DEFER_WGRAD
+        return WGRAD_Q
+
+    def __exit__(self, *exc):
+        WGRAD_Q.active = self.prev
+        if exc[0] is None:
+            WGRAD_Q.flush()
+        else:
+            WGRAD_Q.items = []
+            WGRAD_Q.posts = []
+        return False
 
 
 # ----------------------------------------------------------------------------- scratch

@@ -207,8 +207,9 @@ class SubsampleFn(torch.autograd.Function):
         x2r = x2.view(B * T2, F2 * C)
         with ops.wgrad(dv, x2):
             dwl = empty(C, F2 * C, device=dev)
-            ops.linear_dw(dv, x2r, dwl, accumulate=False)
-            ops.permute3(dwl, b.g("out.0.weight"), C, F2, C, accumulate=True)  # (d,F2,C) -> (d,C,F2)
+            gw = b.g("out.0.weight")
+            ops.linear_dw(dv, x2r, dwl, accumulate=False,  # then (d,F2,C) -> (d,C,F2) into the arena
+                          post=lambda: ops.permute3(dwl, gw, C, F2, C, accumulate=True))
         # dY2 (relu-masked) with >= 64 zero rows after P2: the wgrad K padding and the dgrad
         # gather's off-grid rows
         K2 = rup(P2, 64)
@@ -270,16 +271,18 @@ class SubsampleFn(torch.autograd.Function):
         x2r = x2.view(B * T2, F2 * C)
         with ops.wgrad(dv, x2):
             dwl = empty(C, F2 * C, device=dev)
-            ops.linear_dw(dv, x2r, dwl, accumulate=False)
-            ops.permute3(dwl, b.g("out.0.weight"), C, F2, C, accumulate=True)  # (d,F2,C) -> (d,C,F2)
+            gw = b.g("out.0.weight")
+            ops.linear_dw(dv, x2r, dwl, accumulate=False,  # then (d,F2,C) -> (d,C,F2) into the arena
+                          post=lambda: ops.permute3(dwl, gw, C, F2, C, accumulate=True))
         dx2 = empty(B * T2, F2 * C, dtype=cd, device=dev)
         ops.linear_dx(dv, wl, dx2, epi=ops.make_epi(EPI_DACT, act=ACT_RELU, aux=x2r))
         dx2 = dx2.view(-1, C)
         with ops.wgrad(dx2, col2):
             ops.colsum(dx2, b.g("conv.2.bias"))
             dw2 = empty(C, 9 * C, device=dev)
-            ops.linear_dw(dx2, col2, dw2, accumulate=False)
-            ops.permute3(dw2, b.g("conv.2.weight"), C, 9, C, accumulate=True)  # (Co,9,Ci) -> (Co,Ci,9)
+            g2 = b.g("conv.2.weight")
+            ops.linear_dw(dx2, col2, dw2, accumulate=False,  # then (Co,9,Ci) -> (Co,Ci,9) into the arena
+                          post=lambda: ops.permute3(dw2, g2, C, 9, C, accumulate=True))
         dcol2 = empty(*col2.shape, dtype=cd, device=dev)
         ops.linear_dx(dx2, w2, dcol2)
         del col2

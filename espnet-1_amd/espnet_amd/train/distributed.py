@@ -72,13 +72,32 @@ class ArenaDataParallel:
                     dist.broadcast(b, 0, group=self.group)
 
     def weighted_average(self, loss, stats: Dict[str, torch.Tensor], weight):
-        """trainer.py:604-619 + recursive_average (recursive_op.py:30-47), one all-reduce."""
+        """trainer.py:604-619 + recursive_average (recursive_op.py:30-47), one all-reduce.
+
+        Every rank packs the SAME message: each key of `stats` (the model emits a fixed key
+        set; None entries included) contributes (value * w, w) or (0, 0) when the value is
+        None on this rank.  A key reduces to sum(v*w) / sum(w) over the ranks that had a
+        value — the reference's result whenever every rank has one — and to NaN when no
+        rank had one.  (The reference all-reduces per key and skips None keys, so a key that
+        is None on some ranks only would mismatch its collectives.)"""
         keys = sorted(stats)
         w = weight.to(torch.float32).view(1)
-        pack = torch.cat([w] + [stats[k].detach().float().view(1) * w for k in keys])
+        zero = torch.zeros(1, dtype=torch.float32, device=w.device)
+        parts = [w]
+        for k in keys:
+            v = stats[k]
+            parts += [zero, zero] if v is None else [v.detach().float().view(1) * w, w]
+        pack = torch.cat(parts)
         dist.all_reduce(pack, group=self.group)
         wsum = pack[0:1]
-        new_stats = {k: pack[i + 1:i + 2] / wsum for i, k in enumerate(keys)}
+        # no host read here (the step stays sync-free and capturable): a key no rank had
+        # comes back NaN, which the epoch averages skip like the reference reporter skips
+        # None / non-finite values
+        vals = pack[1:].view(-1, 2)
+        new_stats = {}
+        for i, k in enumerate(keys):
+            vw, ww = vals[i, 0:1], vals[i, 1:2]
+            new_stats[k] = torch.where(ww > 0, vw / ww.clamp_min(1e-30), torch.full_like(vw, float("nan")))
         loss = (loss * w).sum() / wsum
         return loss, new_stats, wsum.to(torch.long)
 
@@ -90,18 +109,33 @@ class ArenaDataParallel:
             hip_ops.GRAD_READY = self.grad_ready
 
     def grad_ready(self, prefix: str):
+        """A block's backward is done (hip_ops.grad_ready).  Its deferred weight-gradient
+        GEMMs are launched on the weight-gradient side stream, and every bucket this block
+        completes is all-reduced from that stream: RCCL waits for the side stream (which
+        already waited for the main stream's part of the block), and the main stream goes on
+        with the backward of the blocks below."""
         if self._pending is None:
+            hip_ops.join_wgrad()
             return
-        g = self.arena.grad
+        done = []
         for i, mods in enumerate(self._pending):
             if prefix in mods:
                 mods.discard(prefix)
                 if not mods:
-                    self._works.append(dist.all_reduce(g[self.buckets[i]], async_op=True, group=self.group))
+                    done.append(i)
+        if not done:
+            return  # the deferred GEMMs keep accumulating until a bucket needs them
+        g = self.arena.grad
+        with hip_ops.wgrad(*hip_ops.WGRAD_Q.tensors()):
+            hip_ops.WGRAD_Q.flush()
+            for i in done:
+                self._works.append(dist.all_reduce(g[self.buckets[i]], async_op=True, group=self.group))
 
     def allreduce_grads(self):
         """Finish the step's gradient reduction (launch what the hooks did not, wait all)."""
         hip_ops.GRAD_READY = None
+        hip_ops.WGRAD_Q.flush()
+        hip_ops.join_wgrad()
         g = self.arena.grad
         if self._pending is None:
             self._pending = [set(m) for m in self._bucket_mods]

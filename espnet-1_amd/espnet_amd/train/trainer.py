@@ -20,6 +20,7 @@ from typing import Dict, Iterable, Optional
 import torch
 import torch.distributed as dist
 
+from .. import hip_ops as ops
 from ..optim.adam import ArenaAdam
 
 
@@ -33,13 +34,21 @@ class Trainer:
             loss, stats, weight = model(**batch, _maxlens=maxlens)
         else:
             loss, stats, weight = model(**batch)
-        stats = {k: v for k, v in stats.items() if v is not None}
         if dp is not None and dp.world_size > 1:
+            # every rank packs the model's full (fixed) key set, None entries flagged, so
+            # the one stats all-reduce has the same size on every rank
+            present = {k for k, v in stats.items() if v is not None}
             loss, stats, weight = dp.weighted_average(loss, stats, weight)
+            stats = {k: v for k, v in stats.items() if k in present}
+        else:
+            stats = {k: v for k, v in stats.items() if v is not None}  # trainer.py:604
         loss = loss / accum_grad if accum_grad > 1 else loss
         if dp is not None and dp.world_size > 1:
             dp.begin_backward()
-        loss.backward()
+        # the Linear weight gradients of the pass are queued and run as grouped GEMMs (at the
+        # end of the pass, or per bucket from the DP hooks)
+        with ops.deferred_wgrad():
+            loss.backward()
         if dp is not None and dp.world_size > 1:
             dp.allreduce_grads()
         grad_norm = None
@@ -76,10 +85,14 @@ class Trainer:
                 if stop.item() > 0:
                     exhausted = False
                     break
-            loss, stats, weight = model(**batch)
-            stats = {k: v for k, v in stats.items() if v is not None}
             if distributed:
+                # DDP(broadcast_buffers=True) syncs the BatchNorm running stats from rank 0
+                # before every forward, eval forwards included (DDP._pre_forward)
+                dp.broadcast_buffers()
+            loss, stats, weight = model(**batch)
+            if distributed:  # full key set, None flagged: same message size on every rank
                 _, stats, weight = dp.weighted_average(loss, stats, weight)
+            stats = {k: v for k, v in stats.items() if v is not None}
             w = float(weight.sum())
             for k, v in stats.items():
                 v = float(v.sum())

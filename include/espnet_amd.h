@@ -105,6 +105,33 @@ int ea_gemm_set_pipeline(int stages);
 /* Pin the bf16 LDS-DMA GEMM output tile (bm x bn in {64x128, 128x128, 256x256});
  * 0,0 = automatic choice by grid size.  Process-wide; for tests and tuning. */
 int ea_gemm_set_tile(int bm, int bn);
+/* Route 256x256-tile bf16 GEMMs to the pipelined kernel (gemm_pipe: 4-slot ring of 32-deep
+ * K slices, counted vmcnt, one barrier per slice) when on != 0 (A/B switch). */
+int ea_gemm_set_pipe(int on);
+
+/* One problem of a grouped launch: C[M,N] (f32, row stride ldc) = beta*C + op(A) op(B), bf16
+ * operands in the layouts of ea_gemm (a_kmajor/b_kmajor shared by the group), lda/ldb
+ * multiples of 8 elements, 16-B aligned bases, N and ldc multiples of 4. */
+typedef struct ea_group_gemm {
+  const void* A;
+  const void* B;
+  float* C;
+  long lda, ldb, ldc;
+  int M, N, K;
+  float beta;
+} ea_group_gemm;
+/* n independent GEMMs in ONE launch, every tile 256x256 over the problem's whole K on the
+ * pipelined main loop (problems in the given order: put the longest K first).  Replaces the
+ * per-Linear weight-gradient GEMMs of a backward pass (torch.nn.Linear weight.grad
+ * accumulation, e.g. espnet/nets/pytorch_backend/transformer/positionwise_feed_forward.py:
+ * 30-32 w_1/w_2) when they are deferred to one batch.  `ws`: device workspace of at least
+ * ea_gemm_grouped_ws_bytes(n, ntiles) bytes (ntiles = sum of ceil(M/256)*ceil(N/256)) holding
+ * the problem table; it must stay untouched until the launch has run (stream order).
+ * Problems writing overlapping C must not share a call. */
+int ea_gemm_grouped(int a_kmajor, int b_kmajor, int n, const ea_group_gemm* probs, void* ws, long ws_bytes,
+                    void* stream);
+/* *bytes = workspace size ea_gemm_grouped needs for n problems with ntiles output tiles. */
+int ea_gemm_grouped_ws_bytes(int n, long ntiles, long* bytes);
 
 /* Kernel-span probe for measurement (bench.py): slots = 4 device u64
  * {span start, span end, sum of spans, count} in units of the GPU's constant 100 MHz
@@ -114,6 +141,10 @@ int ea_gemm_set_tile(int bm, int bn);
  * captured hipGraph re-measures on every replay (torch-ROCm refuses timing events inside
  * captured graphs).  The LDS-DMA bf16 GEMM path only. */
 int ea_gemm_set_probe(unsigned long long* slots);
+/* Diagnostics only: while buf != NULL, gemm_pipe launches write per block (block b = x + gridDim.x*z)
+ * buf[4b..4b+3] = {shader clock at start, after the main loop, at the end, 100 MHz clock at start}.
+ * buf must hold 4 * blocks entries. */
+int ea_gemm_set_diag(unsigned long long* buf);
 int ea_probe_begin(unsigned long long* slots, void* stream);
 int ea_probe_end(unsigned long long* slots, void* stream);
 

@@ -45,6 +45,22 @@ def timed_gemm(A, B, C, *, M, N, K, a_kmajor, b_kmajor, batch=1, nh=1, epi=None,
 
 
 ops.gemm = timed_gemm
+_orig_flush = ops.WgradQueue.flush
+
+
+def timed_flush(self):
+    if not self.items:
+        return
+    n, K0 = len(self.items), max(it[0] for it in self.items)
+    f = sum(2.0 * it[4] * it[5] * it[0] for it in self.items)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    _orig_flush(self)
+    e1.record()
+    records.append((("grouped", n, K0, f), e0, e1))
+
+
+ops.WgradQueue.flush = timed_flush
 for _ in range(2):
     Trainer.train_one_step(model, batch, opt, sched, grad_clip=5.0)
 torch.cuda.synchronize()
@@ -64,6 +80,12 @@ flops = 0.0
 print(f"step (serial wgrad) {step_ms:.3f} ms; GEMM total {tot:.3f} ms over {len(records)} calls")
 print(f"{'M':>7} {'N':>5} {'K':>6} ak bk  z epi drop out   calls   ms/step    us/call  TF/s  %step")
 for key, (n, ms) in sorted(agg.items(), key=lambda kv: -kv[1][1]):
+    if key[0] == "grouped":
+        _, nprob, K0, f = key
+        flops += f * n
+        print(f"grouped wgrad: {nprob} problems (max K {K0}) x{n}: {ms:9.3f} ms/step  {f * n / (ms * 1e-3) / 1e12:6.0f} TF/s"
+              f"  {100 * ms / step_ms:5.1f}%")
+        continue
     M, N, K, ak, bk, z, kind, drop, od = key
     f = 2.0 * M * N * K * z * n
     flops += f

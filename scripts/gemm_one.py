@@ -10,6 +10,11 @@ M, N, K, ak, bk = (int(v) for v in sys.argv[1:6])
 iters = int(sys.argv[6]) if len(sys.argv) > 6 else 20
 if len(sys.argv) > 7:
     lib.ea_gemm_set_pipeline(int(sys.argv[7]))
+if os.environ.get("EA_TILE"):  # force an output tile, e.g. EA_TILE=256
+    t = int(os.environ["EA_TILE"])
+    lib.ea_gemm_set_tile(t if t != 64 else 64, t if t != 64 else 128)
+if os.environ.get("EA_PIPE"):
+    lib.ea_gemm_set_pipe(int(os.environ["EA_PIPE"]))
 A = torch.randn((M, K) if ak else (K, M), device="cuda").to(torch.bfloat16)
 B = torch.randn((N, K) if bk else (K, N), device="cuda").to(torch.bfloat16)
 C = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)

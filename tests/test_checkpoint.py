@@ -107,3 +107,67 @@ def test_checkpoint_resume_continues_reference_run(tmp_path):
     for k, v in section(d, "w_after").items():
         if k in ora.params:
             np.testing.assert_allclose(ora.params[k].detach().numpy(), v, atol=tol(k), rtol=1e-5, err_msg=k)
+
+
+@pytest.mark.gpu
+def test_amp_resume_into_prepared_model_uses_loaded_weights(tmp_path):
+    """Under AMP the GEMMs read the bf16 weight shadow: loading weights into an already
+    prepared model (resume, n-best averaged models) must refresh it.  The first step after
+    resume() into a prepared, randomly initialised model must equal the first step of a
+    model that loaded the same checkpoint before prepare()."""
+    from test_model_build import build
+    from espnet_amd.optim.adam import ArenaAdam
+    from espnet_amd.schedulers.warmup_lr import WarmupLR
+    from espnet_amd.train.checkpoint import EpochReporter, resume, save_checkpoint
+    from espnet_amd.train.trainer import Trainer
+
+    tc, d = load("train2")
+    cfg, _ = load(tc["cfg_name"])
+    w0 = {k: torch.from_numpy(v) for k, v in section(d, "w").items()}
+    batch = lambda s: {k: torch.from_numpy(v) for k, v in section(d, f"in{s}").items()}  # noqa: E731
+
+    def opt_sched(m):
+        opt = ArenaAdam(m, lr=tc["lr"], weight_decay=tc["weight_decay"])
+        return opt, WarmupLR(opt, warmup_steps=tc["warmup_steps"])
+
+    torch.manual_seed(0)
+    m = build(cfg)
+    m.load_state_dict(w0)
+    m.prepare("cuda", amp=True)
+    m.train()
+    opt, sched = opt_sched(m)
+    Trainer.train_one_step(m, batch(0), opt, sched, grad_clip=tc["grad_clip"])
+    save_checkpoint(tmp_path, m, EpochReporter(epoch=1), [opt], [sched])
+
+    # resumed into a prepared model whose arena (and bf16 shadow) hold a different init
+    torch.manual_seed(123)
+    m2 = build(cfg)
+    m2.prepare("cuda", amp=True)
+    m2.train()
+    opt2, sched2 = opt_sched(m2)
+    resume(tmp_path / "checkpoint.pth", m2, EpochReporter(), [opt2], [sched2], ngpu=1)
+    loss2, _, _, _ = Trainer.train_one_step(m2, batch(1), opt2, sched2, grad_clip=tc["grad_clip"])
+
+    # reference: the checkpoint's weights loaded before prepare()
+    ck = torch.load(tmp_path / "checkpoint.pth", map_location="cpu", weights_only=True)
+    m3 = build(cfg)
+    m3.load_state_dict(ck["model"])
+    m3.prepare("cuda", amp=True)
+    m3.train()
+    opt3, sched3 = opt_sched(m3)
+    opt3.load_state_dict(ck["optimizers"][0])
+    sched3.load_state_dict(ck["schedulers"][0])
+    loss3, _, _, _ = Trainer.train_one_step(m3, batch(1), opt3, sched3, grad_clip=tc["grad_clip"])
+    torch.cuda.synchronize()
+    np.testing.assert_allclose(loss2.item(), loss3.item(), rtol=1e-6)
+    for k, v in m3.state_dict().items():
+        np.testing.assert_allclose(m2.state_dict()[k].cpu().numpy(), v.cpu().numpy(), atol=1e-6, rtol=1e-6,
+                                   err_msg=k)
+    # eval forward of an averaged / loaded model on a prepared AMP model, same check
+    m2.eval()
+    m3.eval()
+    m2.load_state_dict(w0)
+    m3.load_state_dict(w0)
+    l2, _, _ = m2(**batch(0))
+    l3, _, _ = m3(**batch(0))
+    np.testing.assert_allclose(l2.item(), l3.item(), rtol=1e-6)

@@ -167,21 +167,26 @@ def test_gemm_unaligned_leading_dims(dtype, a_k, b_k):
     torch.testing.assert_close(C.double().cpu(), ref_mm(A, B, a_k, b_k, M, N, K), atol=tol * K ** 0.5, rtol=tol)
 
 
-TILES = [(64, 128), (128, 128), (256, 256)]
+# (bm, bn, pipe): pipe=1 routes the 256x256 tile to gemm_pipe (4-slot ring of 32-deep slices)
+from espnet_amd._lib import GEMM_PIPE as PIPE_DEFAULT  # noqa: E402  (restored after each test)
+TILES = [(64, 128, 0), (128, 128, 0), (256, 256, 0), (256, 256, 1)]
 
 
 @pytest.fixture
 def forced_tile(request):
     ops, L = _ops()
-    bm, bn = request.param
+    bm, bn, pipe = request.param
     L.lib.ea_gemm_set_tile(bm, bn)
+    L.lib.ea_gemm_set_pipe(pipe)
     yield (bm, bn)
     L.lib.ea_gemm_set_tile(0, 0)
+    L.lib.ea_gemm_set_pipe(PIPE_DEFAULT)
 
 
-@pytest.mark.parametrize("forced_tile", TILES, indirect=True, ids=lambda t: f"{t[0]}x{t[1]}")
+@pytest.mark.parametrize("forced_tile", TILES, indirect=True, ids=lambda t: f"{t[0]}x{t[1]}{'p' if t[2] else ''}")
 @pytest.mark.parametrize("a_k,b_k", [(1, 1), (1, 0), (0, 1), (0, 0)])
-@pytest.mark.parametrize("MNK", [(300, 520, 200), (513, 257, 64), (40, 300, 130), (256, 256, 128)])
+@pytest.mark.parametrize("MNK", [(300, 520, 200), (513, 257, 64), (40, 300, 130), (256, 256, 128),
+                                 (600, 700, 1000), (260, 300, 32)])
 def test_gemm_bf16_tiles(forced_tile, a_k, b_k, MNK):
     """Every LDS-DMA tile shape (edges in M, N and a K remainder) vs fp64."""
     ops, L = _ops()
@@ -198,7 +203,7 @@ def test_gemm_bf16_tiles(forced_tile, a_k, b_k, MNK):
     assert (C[:, N:] == 7.0).all(), "wrote outside ldc columns"
 
 
-@pytest.mark.parametrize("forced_tile", TILES, indirect=True, ids=lambda t: f"{t[0]}x{t[1]}")
+@pytest.mark.parametrize("forced_tile", TILES, indirect=True, ids=lambda t: f"{t[0]}x{t[1]}{'p' if t[2] else ''}")
 def test_gemm_bf16_tiles_epilogue_splitk(forced_tile):
     """Fused ACT epilogue and split-K dW under each tile shape."""
     ops, L = _ops()
@@ -223,3 +228,65 @@ def test_gemm_bf16_tiles_epilogue_splitk(forced_tile):
     refw = dy.double().cpu().t() @ xx.double().cpu()
     torch.testing.assert_close(dw.double().cpu(), refw, atol=2e-3 * R ** 0.5, rtol=2e-3)
 
+
+
+def test_gemm_grouped_vs_fp64():
+    """ea_gemm_grouped: several (0,0)-layout f32-accumulating problems in one launch (edge
+    tiles in M and N, K remainders, beta 0 / 1, longest-K-first order) vs fp64."""
+    ops, L = _ops()
+    import ctypes
+    g = torch.Generator().manual_seed(5)
+    shapes = [(300, 520, 1000, 1.0), (513, 260, 64, 0.0), (40, 300, 130, 1.0), (256, 256, 7968, 1.0),
+              (1024, 512, 33, 0.0)]
+    probs = []
+    for M, N, K, beta in sorted(shapes, key=lambda s: -s[2]):
+        up = lambda n: (n + 7) // 8 * 8 + 8  # noqa: E731  (leading dims: 16-B multiples)
+        A = mk((K, up(M)), torch.bfloat16, g)      # dY: K rows of M
+        B = mk((K, up(N)), torch.bfloat16, g)      # X:  K rows of N
+        C = torch.randn(M, N + 4, generator=g).cuda()
+        C0 = C.clone()
+        probs.append((A, B, C, C0, M, N, K, beta))
+    arr = (L.GroupGemm * len(probs))()
+    ntiles = 0
+    for i, (A, B, C, C0, M, N, K, beta) in enumerate(probs):
+        arr[i] = L.GroupGemm(A.data_ptr(), B.data_ptr(), C.data_ptr(), A.stride(0), B.stride(0), C.stride(0),
+                             M, N, K, beta)
+        ntiles += ((M + 255) // 256) * ((N + 255) // 256)
+    nb = ctypes.c_long(0)
+    L.lib.ea_gemm_grouped_ws_bytes(len(probs), ntiles, ctypes.addressof(nb))
+    ws = torch.empty(nb.value, dtype=torch.uint8, device="cuda")
+    L.lib.ea_gemm_grouped(0, 0, len(probs), ctypes.addressof(arr), ws.data_ptr(), ws.numel(), ops.stream())
+    torch.cuda.synchronize()
+    for A, B, C, C0, M, N, K, beta in probs:
+        ref = beta * C0[:, :N].double().cpu() + ref_mm(A, B, 0, 0, M, N, K)
+        torch.testing.assert_close(C[:, :N].double().cpu(), ref, atol=2e-3 * K ** 0.5, rtol=2e-3)
+        assert torch.equal(C[:, N:], C0[:, N:]), "wrote outside the N columns"
+
+
+def test_deferred_linear_dw_queue():
+    """linear_dw inside deferred_wgrad(): nothing runs until the flush, then every queued
+    weight gradient (and its post-step) matches the immediate path bit for bit."""
+    ops, L = _ops()
+    g = torch.Generator().manual_seed(9)
+    R = 1000
+    dys = [mk((R, n), torch.bfloat16, g) for n in (96, 256, 512)]
+    xs = [mk((R, k), torch.bfloat16, g) for k in (160, 512, 64)]
+    want = []
+    for dy, x in zip(dys, xs):
+        w = torch.randn(dy.shape[1], x.shape[1], generator=g).cuda()
+        imm = w.clone()
+        ops.linear_dw(dy, x, imm, accumulate=True)
+        want.append((w, imm))
+    outs = []
+    posted = torch.zeros(96, 160, device="cuda")
+    with ops.deferred_wgrad() as q:
+        for (dy, x), (w, _) in zip(zip(dys, xs), want):
+            d = w.clone()
+            outs.append(d)
+            ops.linear_dw(dy, x, d, accumulate=True,
+                          post=(lambda d=d: posted.copy_(d)) if d.shape == (96, 160) else None)
+        assert len(q.items) == 3 if ops.DEFER_WGRAD else True
+    torch.cuda.synchronize()
+    for d, (_, imm) in zip(outs, want):
+        torch.testing.assert_close(d, imm, atol=1e-5 * R ** 0.5, rtol=1e-5)
+    torch.testing.assert_close(posted, outs[0])

@@ -55,3 +55,23 @@ def test_implicit_bf16_matches_im2col_and_f32(C, B, T):
     for k in g_f:
         ei, ec = _rel(g_i[k], g_f[k]), _rel(g_c[k], g_f[k])
         assert ei < 1e-1 and ei <= ec * 1.5 + 1e-3, (k, ei, ec)
+
+
+@pytest.mark.parametrize("C,B,T", [(64, 3, 61), (512, 2, 131), (256, 4, 300)])
+def test_implicit_pipe_kernel_matches_lds_kernel(C, B, T):
+    """The three conv2 gather modes (forward, per-class input gradient, split-K weight
+    gradient) on the ping-pong kernel (gemm_pipe) against gemm_bf16_lds, both on 256x256
+    tiles: the same K order and the same split, so the results agree to the bit."""
+    from espnet_amd._lib import GEMM_PIPE, lib
+    lib.ea_gemm_set_tile(256, 256)
+    try:
+        lib.ea_gemm_set_pipe(0)
+        y0, g0 = _run(C, B, T, True, torch.bfloat16)
+        lib.ea_gemm_set_pipe(1)
+        y1, g1 = _run(C, B, T, True, torch.bfloat16)
+    finally:
+        lib.ea_gemm_set_tile(0, 0)
+        lib.ea_gemm_set_pipe(GEMM_PIPE)
+    assert torch.equal(y0, y1)
+    for k in g0:
+        assert torch.equal(g0[k], g1[k]), k
