@@ -122,19 +122,32 @@ def synthetic_batch(cfg, seed):
                 text_lengths=torch.full((B,), L, dtype=torch.long))
 
 
-PMC_FILE = os.path.join(ROOT, "profiles", "r1_v13_pmc_conv2_fwd.json")
+PMC_FILE = os.path.join(ROOT, "profiles", "pmc_conv2_fwd.json")
+GEMM_SOURCES = [os.path.join(ROOT, "espnet-1_amd", "csrc", f) for f in ("gemm.hip", "common.h")]
+
+
+def gemm_src_sha():
+    """Hash of the GEMM kernel sources: ties a PMC traffic measurement to the build it ran on."""
+    import hashlib
+    h = hashlib.sha256()
+    for f in GEMM_SOURCES:
+        with open(f, "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()[:16]
 
 
 def pmc_traffic():
     """HBM bytes per launch of the roofline kernel from the committed PMC pass
     (scripts/gpu_pmc.sh: rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE in separate runs, gfx950
-    FETCH_SIZE x2 correction applied); None if the file is absent."""
+    FETCH_SIZE x2 correction applied), with whether it was measured on the GEMM sources of
+    this tree (the file records their hash); (None, None, False) if the file is absent."""
     try:
         with open(PMC_FILE) as f:
             d = json.load(f)
-        return int(d["traffic_bytes_per_launch"]), os.path.relpath(PMC_FILE, ROOT)
+        same = d.get("gemm_src_sha") == gemm_src_sha()
+        return int(d["traffic_bytes_per_launch"]), os.path.relpath(PMC_FILE, ROOT), same
     except (OSError, KeyError, ValueError):
-        return None, None
+        return None, None, False
 
 
 def cpu_baseline(cfg, seconds_budget=25.0):
@@ -199,6 +212,7 @@ def main():
     dev = torch.device("cuda", local)
 
     from espnet_amd import hip_ops
+    from espnet_amd._lib import GEMM_PIPE
     from espnet_amd.optim.adam import ArenaAdam
     from espnet_amd.schedulers.warmup_lr import WarmupLR
     from espnet_amd.train.distributed import ArenaDataParallel
@@ -260,7 +274,7 @@ def main():
     dtype = "bf16" if amp else "f32"
     achieved = conv_flop / (conv_ms * 1e-3) / 1e12
     loss_v = float(loss.item())
-    traffic, traffic_src = pmc_traffic() if (args.config == "c3" and amp) else (None, None)
+    traffic, traffic_src, traffic_same = pmc_traffic() if (args.config == "c3" and amp) else (None, None, False)
     if rank == 0:
         out = {
             "metric": METRIC, "value": round(utt, 3), "unit": "utterances/s", "n_gpus": world,
@@ -274,11 +288,12 @@ def main():
                 "Conformer-S (6x256, 4 heads, ff 1024), CTC only, V=5000, T=500, L=20"),
                 "global_batch": B * world, "seq_len": T, "parallelism": f"dp{world}"},
             "model_tflops_per_s": round(cfg["gflop_per_step"] * world / (ms * 1e-3) / 1e3, 2),
-            "roofline": {"bound": "mfma", "kernel": "gemm_kernel<bf16> conv2 implicit-GEMM (subsampling, "
-                                                    f"M={B * T2 * F2} N={C} K={9 * C})",
+            "roofline": {"bound": "mfma", "kernel": ("gemm_pipe" if GEMM_PIPE else "gemm_bf16_lds") +
+                         f" bf16 conv2 implicit GEMM (subsampling forward, M={B * T2 * F2} N={C} K={9 * C})",
                          "achieved": round(achieved, 2), "peak": PEAK[dtype], "unit": "TFLOP/s",
                          "frac": round(achieved / PEAK[dtype], 4), "traffic": traffic,
                          "traffic_unit": "bytes/launch (HBM, PMC)", "traffic_source": traffic_src,
+                         "traffic_measured_on_this_build": traffic_same,
                          "algorithmic_bytes": int(2 * (B * T1 * F1 * C + C * 9 * C + B * T2 * F2 * C)),
                          "launch_ms": round(conv_ms, 4), "launches": n_conv},
             "loss": round(loss_v, 4),

@@ -804,14 +804,15 @@ extern "C" int ea_layernorm_fwd(int rows, int d, const float* x, long ldx, const
   return 0;
 }
 
-extern "C" int ea_layernorm_bwd(int rows, int d, const void* dy, int dy_dtype, long lddy, const float* x,
-                                long ldx, const float* gamma, const float* mean, const float* rstd,
-                                float* dx, long lddx, int accumulate, float* dgamma, float* dbeta,
-                                int accumulate_params, float* workspace, long ws_elems, void* stream) {
-  EA_ENTRY();
+// LayerNorm backward: dx (+)= ..., and per-row-block partial sums of (dgamma | dbeta) in
+// workspace [nparts][2d]; with dgamma != nullptr the ordered reducer then sums them into
+// dgamma/dbeta, otherwise *nparts_out reports the partial count (deferred reduction).
+static int ln_bwd_impl(int rows, int d, const void* dy, int dy_dtype, long lddy, const float* x, long ldx,
+                       const float* gamma, const float* mean, const float* rstd, float* dx, long lddx, int accumulate,
+                       float* dgamma, int accumulate_params, float* workspace, long ws_elems, int* nparts_out,
+                       hipStream_t st) {
+  if (nparts_out) *nparts_out = 0;
   if (rows == 0) return 0;
-  EA_CHECK_ARG(dbeta == dgamma + d);  // grads of (weight, bias) are adjacent in the arena
-  hipStream_t st = (hipStream_t)stream;
   const bool vec = d % 4 == 0 && lddy % 4 == 0 && ldx % 4 == 0 && ((uintptr_t)x % 16) == 0 &&
                    ((uintptr_t)dy % (dy_dtype == EA_BF16 ? 8 : 16)) == 0;
   if (!vec) {  // generic fused path (row kernel + per-block partials)
@@ -823,6 +824,7 @@ extern "C" int ea_layernorm_bwd(int rows, int d, const void* dy, int dy_dtype, l
     else
       EA_LN_DISPATCH(ln_bwd_kernel, float, grid, blk, 0, st, rows, d, (const float*)dy, lddy, x, ldx, gamma, mean, rstd, dx, lddx, accumulate, workspace);
     EA_LAUNCH_CHECK();
+    if (!dgamma) { *nparts_out = nb; return 0; }
     hipLaunchKernelGGL(reduce_partials_kernel, dim3(ea_cdiv(2 * d, RP_CW)), dim3(256), 0, st, nb, 2 * d,
                        workspace, (long)2 * d, dgamma, accumulate_params);
     EA_LAUNCH_CHECK();
@@ -845,6 +847,7 @@ extern "C" int ea_layernorm_bwd(int rows, int d, const void* dy, int dy_dtype, l
     if (d <= 512) { EA_LNB(1) } else { EA_LNB(2) }
 #undef EA_LNB
     EA_LAUNCH_CHECK();
+    if (!dgamma) { *nparts_out = nb; return 0; }
     hipLaunchKernelGGL(reduce_partials_kernel, dim3(ea_cdiv(2 * d, RP_CW)), dim3(256), 0, st, nb, 2 * d,
                        workspace, (long)2 * d, dgamma, accumulate_params);
     EA_LAUNCH_CHECK();
@@ -865,10 +868,31 @@ extern "C" int ea_layernorm_bwd(int rows, int d, const void* dy, int dy_dtype, l
   else
     hipLaunchKernelGGL((colsum_vec_kernel<float, true>), g2, blk, 0, st, rows, d, (const float*)dy, lddy, x, ldx, mean, rstd, rpp, workspace);
   EA_LAUNCH_CHECK();
+  if (!dgamma) { *nparts_out = nparts; return 0; }
   hipLaunchKernelGGL(reduce_partials_kernel, dim3(ea_cdiv(2 * d, RP_CW)), dim3(256), 0, st, nparts, 2 * d,
                      workspace, (long)2 * d, dgamma, accumulate_params);
   EA_LAUNCH_CHECK();
   return 0;
+}
+
+extern "C" int ea_layernorm_bwd(int rows, int d, const void* dy, int dy_dtype, long lddy, const float* x,
+                                long ldx, const float* gamma, const float* mean, const float* rstd,
+                                float* dx, long lddx, int accumulate, float* dgamma, float* dbeta,
+                                int accumulate_params, float* workspace, long ws_elems, void* stream) {
+  EA_ENTRY();
+  EA_CHECK_ARG(dgamma != nullptr && dbeta == dgamma + d);  // grads of (weight, bias) are adjacent in the arena
+  return ln_bwd_impl(rows, d, dy, dy_dtype, lddy, x, ldx, gamma, mean, rstd, dx, lddx, accumulate, dgamma,
+                     accumulate_params, workspace, ws_elems, nullptr, (hipStream_t)stream);
+}
+
+extern "C" int ea_layernorm_bwd_partials(int rows, int d, const void* dy, int dy_dtype, long lddy, const float* x,
+                                         long ldx, const float* gamma, const float* mean, const float* rstd,
+                                         float* dx, long lddx, int accumulate, float* part, long part_elems,
+                                         int* nparts, void* stream) {
+  EA_ENTRY();
+  EA_CHECK_ARG(part != nullptr && nparts != nullptr);
+  return ln_bwd_impl(rows, d, dy, dy_dtype, lddy, x, ldx, gamma, mean, rstd, dx, lddx, accumulate, nullptr, 0,
+                     part, part_elems, nparts, (hipStream_t)stream);
 }
 
 extern "C" int ea_reduce_partials(int nparts, int n, const float* part, long stride, float* out,

@@ -47,6 +47,18 @@ class GroupGemm(ctypes.Structure):
                 ("M", ctypes.c_int), ("N", ctypes.c_int), ("K", ctypes.c_int), ("beta", ctypes.c_float)]
 
 
+class ColsumProb(ctypes.Structure):
+    """ea_colsum_prob: one column-sum problem of ea_colsum_grouped."""
+    _fields_ = [("x", ctypes.c_void_p), ("part", ctypes.c_void_p), ("ld", ctypes.c_long),
+                ("rows", ctypes.c_int), ("n", ctypes.c_int), ("dtype", ctypes.c_int), ("rpp", ctypes.c_int)]
+
+
+class ReduceProb(ctypes.Structure):
+    """ea_reduce_prob: one ordered partial-sum reduction of ea_reduce_grouped."""
+    _fields_ = [("part", ctypes.c_void_p), ("out", ctypes.c_void_p), ("stride", ctypes.c_long),
+                ("nparts", ctypes.c_int), ("n", ctypes.c_int), ("accumulate", ctypes.c_int)]
+
+
 SCHED_CONSTANT, SCHED_WARMUP = 0, 1
 CONV_FWD, CONV_DGRAD, CONV_WGRAD = 1, 2, 3
 

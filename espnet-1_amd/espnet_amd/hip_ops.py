@@ -10,8 +10,8 @@ import os
 
 import torch
 
-from ._lib import (ACT_NONE, BF16, EPI_ACT, EPI_DACT, EPI_RESID, EPI_STORE, F32, Epilogue,
-                   GroupGemm, HipError, lib)
+from ._lib import (ACT_NONE, BF16, EPI_ACT, EPI_DACT, EPI_RESID, EPI_STORE, F32, ColsumProb, Epilogue,
+                   GroupGemm, HipError, ReduceProb, lib)
 
 __all__ = ["dt", "stream", "gemm", "linear", "linear_dx", "linear_dw", "workspace"]
 
@@ -312,23 +312,124 @@ class WgradQueue:
 
 WGRAD_Q = WgradQueue()
 
+# ----------------------------------------------------------------------------- deferred gradient reductions
+DEFER_REDUCE = os.environ.get("EA_DEFER_REDUCE", "1") != "0"
+_RWS = {}
+
+
+def _table_ws(kind, nbytes, dev):
+    key = (str(dev), stream(), kind)
+    ws = _RWS.get(key)
+    if ws is None or ws.numel() < nbytes:
+        ws = torch.empty(max(nbytes, 1 << 16), dtype=torch.uint8, device=dev)
+        _RWS[key] = ws
+    return ws
+
+
+class ReduceQueue:
+    """The parameter-gradient reductions of one backward pass, deferred: bias column sums
+    (colsum: torch.nn.Linear bias.grad = dY summed over tokens) and the ordered sums of the
+    LayerNorm (dgamma | dbeta) row-block partials.  flush() runs every queued column sum in
+    ONE grouped launch (ea_colsum_grouped), then every reduction in ONE more
+    (ea_reduce_grouped) — instead of ~450 launches of a few microseconds per C3 step.  The
+    column sums use ea_colsum's row blocking, so results are bit-identical to the per-call
+    path.  Outputs that overlap a queued one flush the queue first."""
+
+    def __init__(self):
+        self.active = False
+        self.colsums = []
+        self.reduces = []
+        self.spans = []
+
+    def _claim(self, out, n):
+        lo = out.data_ptr()
+        hi = lo + 4 * n
+        if any(lo < h and l_ < hi for l_, h in self.spans):
+            self.flush()
+        self.spans.append((lo, hi))
+
+    def add_colsum(self, x, out, accumulate) -> bool:
+        if x.dtype not in (torch.bfloat16, torch.float32) or out.dtype != torch.float32 or not out.is_contiguous():
+            return False
+        rows, n, ld = _rows(x)
+        if rows <= 0 or n % 4 or ld % 4 or x.data_ptr() % (8 if x.dtype == torch.bfloat16 else 16):
+            return False
+        self._claim(out, n)
+        self.colsums.append((x, rows, n, ld, out, accumulate))
+        return True
+
+    def add_reduce(self, part, nparts, n, stride, out, accumulate=True):
+        self._claim(out, n)
+        self.reduces.append((part, nparts, n, stride, out, accumulate))
+
+    def tensors(self):
+        return [c[0] for c in self.colsums] + [r[0] for r in self.reduces]
+
+    def flush(self):
+        if not self.colsums and not self.reduces:
+            return
+        colsums, reduces = self.colsums, list(self.reduces)
+        self.colsums, self.reduces, self.spans = [], [], []
+        cur = torch.cuda.current_stream()
+        for t in [c[0] for c in colsums] + [r[0] for r in reduces]:
+            t.record_stream(cur)
+        dev = (colsums[0][0] if colsums else reduces[0][0]).device
+        cb, rb = ctypes.c_long(0), ctypes.c_long(0)
+        if colsums:
+            rpps = [max(32, (c[1] + 127) // 128) for c in colsums]  # ea_colsum's row blocking
+            nrbs = [(c[1] + r - 1) // r for c, r in zip(colsums, rpps)]
+            part = torch.empty(sum(nrb * c[2] for c, nrb in zip(colsums, nrbs)), dtype=torch.float32, device=dev)
+            arr = (ColsumProb * len(colsums))()
+            off = 0
+            for i, ((x, rows, n, ld, out, acc), rpp, nrb) in enumerate(zip(colsums, rpps, nrbs)):
+                arr[i] = ColsumProb(x.data_ptr(), part.data_ptr() + 4 * off, ld, rows, n, dt(x), rpp)
+                reduces.append((part, nrb, n, n, out, acc, off))
+                off += nrb * n
+            lib.ea_grouped_table_bytes(len(colsums), ctypes.addressof(cb), ctypes.addressof(rb))
+            ws = _table_ws("colsum", cb.value, dev)
+            lib.ea_colsum_grouped(len(colsums), ctypes.addressof(arr), ws.data_ptr(), ws.numel(), stream())
+        arr = (ReduceProb * len(reduces))()
+        for i, r in enumerate(reduces):
+            part, nparts, n, stride, out, acc = r[:6]
+            off = r[6] if len(r) > 6 else 0
+            arr[i] = ReduceProb(part.data_ptr() + 4 * off, out.data_ptr(), stride, nparts, n, int(acc))
+        lib.ea_grouped_table_bytes(len(reduces), ctypes.addressof(cb), ctypes.addressof(rb))
+        ws = _table_ws("reduce", rb.value, dev)
+        lib.ea_reduce_grouped(len(reduces), ctypes.addressof(arr), ws.data_ptr(), ws.numel(), stream())
+
+
+REDUCE_Q = ReduceQueue()
+
+
+def flush_deferred():
+    """Launch every deferred weight gradient and gradient reduction (current stream)."""
+    WGRAD_Q.flush()
+    REDUCE_Q.flush()
+
+
+def deferred_tensors():
+    return WGRAD_Q.tensors() + REDUCE_Q.tensors()
+
 
 class deferred_wgrad:
-    """Context of a training backward pass: linear_dw calls inside are queued (EA_DEFER_WGRAD=0
-    turns this off) and flushed on exit, on the current stream."""
+    """Context of a training backward pass: linear_dw calls inside are queued
+    (EA_DEFER_WGRAD=0 turns this off), so are the bias column sums and LayerNorm
+    parameter-gradient reductions (EA_DEFER_REDUCE=0); all are flushed on exit, on the
+    current stream."""
 
     def __enter__(self):
-        self.prev = WGRAD_Q.active
+        self.prev = (WGRAD_Q.active, REDUCE_Q.active)
         WGRAD_Q.active = DEFER_WGRAD
+        REDUCE_Q.active = DEFER_REDUCE
         return WGRAD_Q
 
     def __exit__(self, *exc):
-        WGRAD_Q.active = self.prev
+        WGRAD_Q.active, REDUCE_Q.active = self.prev
         if exc[0] is None:
-            WGRAD_Q.flush()
+            flush_deferred()
         else:
-            WGRAD_Q.items = []
-            WGRAD_Q.posts = []
+            WGRAD_Q.items, WGRAD_Q.posts = [], []
+            REDUCE_Q.colsums, REDUCE_Q.reduces, REDUCE_Q.spans = [], [], []
         return False
 
 
@@ -364,13 +465,28 @@ def layernorm_bwd(dy, x, gamma, mean, rstd, dx, dgamma, dbeta, accumulate=True):
     rows, d, ldx = _rows(x)
     _, _, lddy = _rows(dy)
     _, _, lddx = _rows(dx)
+    if REDUCE_Q.active and rows > 0 and dbeta.data_ptr() == dgamma.data_ptr() + 4 * d:
+        # dx now; the (dgamma | dbeta) row-block partials go to a buffer of their own and are
+        # summed with the pass's other parameter-gradient reductions (REDUCE_Q.flush)
+        nparts_max = max((rows + 15) // 16, 128)
+        part = torch.empty(nparts_max * 2 * d, dtype=torch.float32, device=x.device)
+        np_ = ctypes.c_int(0)
+        lib.ea_layernorm_bwd_partials(rows, d, dy.data_ptr(), dt(dy), lddy, x.data_ptr(), ldx, gamma.data_ptr(),
+                                      mean.data_ptr(), rstd.data_ptr(), dx.data_ptr(), lddx, int(accumulate),
+                                      part.data_ptr(), part.numel(), ctypes.addressof(np_), stream())
+        REDUCE_Q.add_reduce(part, np_.value, 2 * d, 2 * d, dgamma, accumulate=True)
+        return
     w, n = _ws(x.device, max(1 << 22, 1024 * d))
     lib.ea_layernorm_bwd(rows, d, dy.data_ptr(), dt(dy), lddy, x.data_ptr(), ldx, gamma.data_ptr(),
                          mean.data_ptr(), rstd.data_ptr(), dx.data_ptr(), lddx, int(accumulate),
                          dgamma.data_ptr(), dbeta.data_ptr(), 1, w, n, stream())
 
 
-def colsum(x, out, accumulate=True):
+def colsum(x, out, accumulate=True, defer=True):
+    """out (+)= column sums of x.  While the reduction queue is active the sum is deferred to
+    REDUCE_Q.flush(): pass defer=False when x is modified in place before the pass ends."""
+    if defer and REDUCE_Q.active and REDUCE_Q.add_colsum(x, out, accumulate):
+        return
     rows, n, ld = _rows(x)
     w, wn = _ws(x.device)
     lib.ea_colsum(rows, n, x.data_ptr(), dt(x), ld, out.data_ptr(), int(accumulate), w, wn, stream())

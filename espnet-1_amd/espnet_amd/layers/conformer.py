@@ -326,7 +326,8 @@ class ConformerBlockFn(torch.autograd.Function):
         dqv = empty(N, d, dtype=cd, device=dev)
         ops.gemm(dbd, pp, dqv, M=T, N=dk, K=P2, a_kmajor=1, b_kmajor=0, lda=ldbd, ldb=d, ldc=d,
                  batch=B, nh=H, sA=(T * ldbd, B * T * ldbd), sB=(0, dk), sC=(T * d, dk), splitk=False)
-        ops.colsum(dqkv[:, :d], b.g(A + "pos_bias_u", shape=(d,)))
+        # not deferred: dqkv[:, :d] receives dqv in place right below
+        ops.colsum(dqkv[:, :d], b.g(A + "pos_bias_u", shape=(d,)), defer=False)
         ops.colsum(dqv, b.g(A + "pos_bias_v", shape=(d,)))
         lib.ea_add_2d(N, d, dqv.data_ptr(), ops.dt(dqv), d, dqkv.data_ptr(), ops.dt(dqkv), 3 * d, 1.0,
                       ops.stream())

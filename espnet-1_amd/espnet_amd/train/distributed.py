@@ -126,15 +126,15 @@ class ArenaDataParallel:
         if not done:
             return  # the deferred GEMMs keep accumulating until a bucket needs them
         g = self.arena.grad
-        with hip_ops.wgrad(*hip_ops.WGRAD_Q.tensors()):
-            hip_ops.WGRAD_Q.flush()
+        with hip_ops.wgrad(*hip_ops.deferred_tensors()):
+            hip_ops.flush_deferred()
             for i in done:
                 self._works.append(dist.all_reduce(g[self.buckets[i]], async_op=True, group=self.group))
 
     def allreduce_grads(self):
         """Finish the step's gradient reduction (launch what the hooks did not, wait all)."""
         hip_ops.GRAD_READY = None
-        hip_ops.WGRAD_Q.flush()
+        hip_ops.flush_deferred()
         hip_ops.join_wgrad()
         g = self.arena.grad
         if self._pending is None:

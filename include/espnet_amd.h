@@ -173,6 +173,37 @@ int ea_reduce_partials(int nparts, int n, const float* part, long stride, float*
 int ea_colsum(int rows, int n, const void* x, int x_dtype, long ld, float* out, int accumulate,
               float* workspace, long ws_elems, void* stream);
 
+/* LayerNorm backward without the parameter-gradient reduction: dx as ea_layernorm_bwd, the
+ * per-row-block (dgamma | dbeta) partials written to part ([*nparts][2d]; part_elems sets the
+ * row-block size exactly as ea_layernorm_bwd's ws_elems does), to be summed by
+ * ea_reduce_grouped (deferred: one launch for a whole backward pass). */
+int ea_layernorm_bwd_partials(int rows, int d, const void* dy, int dy_dtype, long lddy, const float* x,
+                              long ldx, const float* gamma, const float* mean, const float* rstd,
+                              float* dx, long lddx, int accumulate, float* part, long part_elems,
+                              int* nparts, void* stream);
+
+/* Grouped reductions of a backward pass's parameter gradients (bias grads of every Linear:
+ * torch.nn.Linear bias.grad; LayerNorm weight/bias grads: torch.nn.LayerNorm in
+ * espnet/nets/pytorch_backend/transformer/layer_norm.py:12-42).  A column-sum problem writes
+ * the row-block partials part[ceil(rows/rpp)][n]; a reduce problem sums out[c] (+)=
+ * sum_p part[p*stride + c] in fixed order (f64).  ws: device workspace for the problem table
+ * (ea_grouped_table_bytes), untouched until the launch has run. */
+typedef struct ea_colsum_prob {
+  const void* x;
+  float* part;
+  long ld;
+  int rows, n, dtype, rpp;
+} ea_colsum_prob;
+typedef struct ea_reduce_prob {
+  const float* part;
+  float* out;
+  long stride;
+  int nparts, n, accumulate;
+} ea_reduce_prob;
+int ea_colsum_grouped(int n, const ea_colsum_prob* probs, void* ws, long ws_bytes, void* stream);
+int ea_reduce_grouped(int n, const ea_reduce_prob* probs, void* ws, long ws_bytes, void* stream);
+int ea_grouped_table_bytes(int n, long* colsum_bytes, long* reduce_bytes);
+
 /* BatchNorm1d (training: batch stats over ALL rows incl. padding, running stats update
  * with momentum and unbiased var, num_batches_tracked += 1; eval: given mean/rstd) fused
  * with the following activation: z = act(BN(y)).  y, z: (rows, C) channel-last.

@@ -63,3 +63,44 @@ def test_scale_dropout_colsum_matches_two_pass(rows, cols, dt):
     assert 0.08 < drop < 0.12
     torch.testing.assert_close(c1, c2, atol=1e-3, rtol=1e-5)
     torch.testing.assert_close(c1.double().cpu(), 1 + y2.double().sum(0).cpu(), atol=1e-3, rtol=1e-5)
+
+
+def test_grouped_reductions_match_per_call():
+    """Deferred parameter-gradient reductions (ReduceQueue: grouped column sums + grouped
+    ordered reductions, LayerNorm partials) equal the per-call ea_colsum / ea_layernorm_bwd
+    results bit for bit, including strided inputs, f32/bf16 and accumulate."""
+    from espnet_amd import hip_ops as ops
+    g = torch.Generator().manual_seed(4)
+    dev = "cuda"
+    xs = [torch.randn(7968, 2048, generator=g).to(dev).to(torch.bfloat16),
+          torch.randn(1312, 5000, generator=g).to(dev).to(torch.bfloat16),
+          torch.randn(300, 3 * 64, generator=g).to(dev)[:, :64],   # strided f32 view
+          torch.randn(33, 512, generator=g).to(dev)]
+    outs0 = [torch.randn(x.shape[1], generator=g).to(dev) for x in xs]
+    ref = [o.clone() for o in outs0]
+    for x, o in zip(xs, ref):
+        ops.colsum(x, o, accumulate=True)
+    # LayerNorm: d=512 rows 7968, bf16 dy
+    d, R = 512, 7968
+    x = torch.randn(R, d, generator=g).to(dev)
+    dy = torch.randn(R, d, generator=g).to(dev).to(torch.bfloat16)
+    gamma = torch.randn(d, generator=g).to(dev)
+    mean, rstd = x.mean(1), x.var(1, unbiased=False).add(1e-12).rsqrt()
+    gb_ref = torch.randn(2 * d, generator=g).to(dev)
+    gb_def = gb_ref.clone()
+    dx_ref = torch.zeros(R, d, device=dev)
+    dx_def = torch.zeros(R, d, device=dev)
+    ops.layernorm_bwd(dy, x, gamma, mean, rstd, dx_ref, gb_ref[:d], gb_ref[d:], accumulate=True)
+    outs = [o.clone() for o in outs0]
+    with ops.deferred_wgrad():
+        if ops.DEFER_REDUCE:
+            for x_, o in zip(xs, outs):
+                ops.colsum(x_, o, accumulate=True)
+            ops.layernorm_bwd(dy, x, gamma, mean, rstd, dx_def, gb_def[:d], gb_def[d:], accumulate=True)
+            assert len(ops.REDUCE_Q.colsums) == 4 and len(ops.REDUCE_Q.reduces) == 1
+    torch.cuda.synchronize()
+    if ops.DEFER_REDUCE:
+        for o, r in zip(outs, ref):
+            assert torch.equal(o, r)
+        assert torch.equal(dx_def, dx_ref)
+        assert torch.equal(gb_def, gb_ref)
