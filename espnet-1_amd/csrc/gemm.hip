@@ -543,80 +543,110 @@ EA_DEV bf16x8 frag_img(const char* img, int r, int ks, int lane) {
 // Epilogue of one wave's (MI*16) x (NJ*16) accumulator tile, in 64 x 64 chunks transposed
 // through the wave's private LDS region (64 x EPI_LDT floats); each lane then owns 4
 // consecutive columns of 16 rows per chunk.  The operand the epilogue kind reads (aux /
-// resid / C for beta != 0) is loaded for all of the chunk's row groups at once, right after
-// the transposition has freed the chunk's accumulator registers: one load round trip per
-// chunk instead of one per small batch; bias is read once per chunk.  With split-K (p.splitk > 1) the chunk goes to this slice's f32 slab.
+// resid / C for beta != 0) is loaded in batches of 8 row groups, all of a batch's loads in
+// flight together (one round trip per batch); bias is read once per batch.  With split-K (p.splitk > 1) the chunk goes to this slice's f32 slab.
 template <int KIND, int MI, int NJ>
 EA_DEV void epi_wave(const GemmP& p, const EpiK& k, char* smem, int z, int zb, int zh, int r0, int c0, int lane,
                      int w, const f32x4 (&acc)[MI][NJ]) {
   constexpr int RC = MI < 4 ? MI : 4;  // row blocks per chunk
   constexpr int NG = RC * 4;           // row groups (of 4 lanes' rows) per lane per chunk
+  constexpr int HB = NG < 8 ? NG : 8;  // row groups per operand-load batch
+  constexpr int NCH = (MI / RC) * (NJ / 4), NBC = NG / HB, NU = NCH * NBC;  // chunks, batches, units
   float* t = (float*)smem + w * (RC * 16) * EPI_LDT;
   const int rq = (lane >> 4) * 4, cc = lane & 15, lc = (lane & 15) * 4;
   float* slab = p.splitk > 1 ? p.ws + ((long)z * p.splitk + (blockIdx.z % p.splitk)) * (long)p.M * p.N : nullptr;
-  const bool reads = !slab && (KIND == EA_EPI_DACT || (KIND == EA_EPI_RESID && p.epi.resid) ||
-                               (KIND == EA_EPI_STORE && p.epi.beta != 0.f));
+  const bool reads = p.vec_c && !slab &&
+                     (KIND == EA_EPI_DACT || (KIND == EA_EPI_RESID && p.epi.resid) ||
+                      (KIND == EA_EPI_STORE && p.epi.beta != 0.f));
+  // the operand the kind reads (aux / resid / C for beta != 0), dtype dispatched once
+  const void* src = nullptr;
+  long sld = 0, sbase = 0;
+  int sdt = EA_F32;
+  if constexpr (KIND == EA_EPI_STORE) {
+    src = p.C; sld = p.ldc; sbase = zb * p.sCb + zh * p.sCh; sdt = p.c_dtype;
+  } else if constexpr (KIND == EA_EPI_RESID) {
+    src = p.epi.resid; sld = p.epi.ldr;
+  } else if constexpr (KIND == EA_EPI_DACT) {
+    src = p.epi.aux; sld = p.epi.ldaux; sdt = p.epi.aux_dtype;
+  }
+  auto ch_rb = [&](int ch) { return r0 + (ch / (NJ / 4)) * RC * 16; };
+  auto ch_col = [&](int ch) { return c0 + (ch % (NJ / 4)) * 64 + lc; };
+  // one batch of operand loads: unconditional, at clamped (in-range) indices, with the dtype
+  // branch outside the batch — a branch around each load makes hipcc drain vmcnt(0) after
+  // every one of them (out-of-range groups are never stored)
+  auto load_unit = [&](int u, float (&o)[HB][4]) {
+    if (!reads) return;
+    const int ch = u / NBC, h0 = (u % NBC) * HB;
+    const int rb = ch_rb(ch), cl = min(ch_col(ch), p.N - 4);
+    if (sdt == EA_BF16) {
 #pragma unroll
-  for (int ri = 0; ri < MI / RC; ++ri) {
+      for (int it = 0; it < HB; ++it)
+        vld4((const bf16*)src + sbase + (long)min(rb + (h0 + it) * 4 + (lane >> 4), p.M - 1) * sld + cl, o[it]);
+    } else {
 #pragma unroll
-    for (int cj = 0; cj < NJ / 4; ++cj) {
-      const int rb = r0 + ri * RC * 16, col = c0 + cj * 64 + lc;
-      if (ri + cj > 0) {
-        __builtin_amdgcn_wave_barrier();
-        asm volatile("" ::: "memory");
-      }
-#pragma unroll
-      for (int i = 0; i < RC; ++i)
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-#pragma unroll
-          for (int rr = 0; rr < 4; ++rr)
-            t[(i * 16 + rq + rr) * EPI_LDT + j * 16 + cc] = acc[ri * RC + i][cj * 4 + j][rr];
+      for (int it = 0; it < HB; ++it)
+        vld4((const float*)src + sbase + (long)min(rb + (h0 + it) * 4 + (lane >> 4), p.M - 1) * sld + cl, o[it]);
+    }
+  };
+  auto transpose = [&](int ch) {  // a chunk's accumulators -> the wave's LDS image
+    const int ri = ch / (NJ / 4), cj = ch % (NJ / 4);
+    if (ch > 0) {
       __builtin_amdgcn_wave_barrier();
       asm volatile("" ::: "memory");
-      if (!p.vec_c) {  // cold path: element-wise straight from the LDS image
+    }
+#pragma unroll
+    for (int i = 0; i < RC; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int rr = 0; rr < 4; ++rr)
+          t[(i * 16 + rq + rr) * EPI_LDT + j * 16 + cc] = acc[ri * RC + i][cj * 4 + j][rr];
+    __builtin_amdgcn_wave_barrier();
+    asm volatile("" ::: "memory");
+  };
+  if (!p.vec_c) {  // cold path (unaligned C / N % 4): element-wise straight from the LDS image
+#pragma unroll
+    for (int ch = 0; ch < NCH; ++ch) {
+      transpose(ch);
+      const int rb = ch_rb(ch), col = ch_col(ch);
 #pragma unroll 1
-        for (int it = 0; it < NG; ++it) {
-          const int lr = it * 4 + (lane >> 4), row = rb + lr;
-          if (row >= p.M) continue;
+      for (int it = 0; it < NG; ++it) {
+        const int lr = it * 4 + (lane >> 4), row = rb + lr;
+        if (row >= p.M) continue;
 #pragma unroll 1
-          for (int c = 0; c < 4; ++c) {
-            if (col + c >= p.N) break;
-            const float x = t[lr * EPI_LDT + lc + c];
-            if (slab) slab[(long)row * p.N + col + c] = x;
-            else epi_one<KIND>(p, z, zb, zh, row, col + c, x);
-          }
-        }
-        continue;
-      }
-      float bias[4] = {0.f, 0.f, 0.f, 0.f};
-      if (!slab && KIND != EA_EPI_DACT && p.epi.bias && col < p.N) {
-        const float4 bb = *(const float4*)(p.epi.bias + col);
-        bias[0] = bb.x; bias[1] = bb.y; bias[2] = bb.z; bias[3] = bb.w;
-      }
-      // the chunk's operand loads in flight HB row groups at a time (the chunk's accumulators
-      // are in LDS now, so their registers hold the operand)
-      constexpr int HB = NG < 8 ? NG : 8;
-#pragma unroll
-      for (int h0 = 0; h0 < NG; h0 += HB) {
-        float o[HB][4];
-        if (reads) {
-#pragma unroll
-          for (int it = 0; it < HB; ++it) {
-            const int row = rb + (h0 + it) * 4 + (lane >> 4);
-            if (row < p.M && col < p.N) epi_src<KIND>(p, zb, zh, row, col, o[it]);
-          }
-        }
-#pragma unroll
-        for (int it = 0; it < HB; ++it) {
-          const int lr = (h0 + it) * 4 + (lane >> 4), row = rb + lr;
-          const float4 f = *(const float4*)(t + lr * EPI_LDT + lc);
-          if (row >= p.M || col >= p.N) continue;
-          const float v[4] = {f.x, f.y, f.z, f.w};
-          if (slab) *(float4*)(slab + (long)row * p.N + col) = f;
-          else epi_four_pre<KIND>(p, k, z, zb, zh, row, col, v, bias, reads, o[it]);
+        for (int c = 0; c < 4; ++c) {
+          if (col + c >= p.N) break;
+          const float x = t[lr * EPI_LDT + lc + c];
+          if (slab) slab[(long)row * p.N + col + c] = x;
+          else epi_one<KIND>(p, z, zb, zh, row, col + c, x);
         }
       }
+    }
+    return;
+  }
+  // per chunk: transpose, then batches of HB row groups whose operand loads are all issued
+  // before any of them is used (software pipelining across batches measured slower: the
+  // second buffer of live operands costs more registers than the latency it hides)
+#pragma unroll
+  for (int u = 0; u < NU; ++u) {
+    const int ch = u / NBC, h0 = (u % NBC) * HB;
+    const int rb = ch_rb(ch), col = ch_col(ch);
+    if (u % NBC == 0) transpose(ch);
+    float ob[HB][4];
+    load_unit(u, ob);
+    float bias[4] = {0.f, 0.f, 0.f, 0.f};
+    if (!slab && KIND != EA_EPI_DACT && p.epi.bias && col < p.N) {
+      const float4 bb = *(const float4*)(p.epi.bias + col);
+      bias[0] = bb.x; bias[1] = bb.y; bias[2] = bb.z; bias[3] = bb.w;
+    }
+#pragma unroll
+    for (int it = 0; it < HB; ++it) {
+      const int lr = (h0 + it) * 4 + (lane >> 4), row = rb + lr;
+      const float4 f = *(const float4*)(t + lr * EPI_LDT + lc);
+      if (row >= p.M || col >= p.N) continue;
+      const float v[4] = {f.x, f.y, f.z, f.w};
+      if (slab) *(float4*)(slab + (long)row * p.N + col) = f;
+      else epi_four_pre<KIND>(p, k, z, zb, zh, row, col, v, bias, reads, ob[it]);
     }
   }
 }
