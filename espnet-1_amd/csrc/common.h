@@ -63,9 +63,11 @@ EA_DEV void store_from_f(void* p, long i, int dtype, float v) {
 // ------------------------------------------------------------------ dropout RNG
 // Counter-based: the keep decision of element `idx` under stream `seed` is a pure
 // function, so backward regenerates the forward mask with no mask tensor.  One 32-bit
-// hash (lowbias32 finaliser, two 32-bit multiplies) serves the element pair idx>>1, each
-// element using 16 of its bits; the 64-bit seed is folded into a 32-bit stream key that is
-// uniform across the launch (scalar unit, hoisted out of the loops).
+// hash serves the element pair idx>>1, each element using 16 of its bits; the 64-bit seed is
+// folded into a 32-bit stream key that is uniform across the launch (scalar unit, hoisted
+// out of the loops).  The per-pair mixer is Bob Jenkins' 6-shift integer hash (adds, shifts
+// and xors only): full-rate VALU on CDNA, where a 32-bit multiply is quarter rate — the
+// multiply-based mixer it replaces was half of a dropout-fused GEMM epilogue's cost.
 __host__ __device__ inline uint32_t ea_mix32(uint32_t x) {
   x ^= x >> 16; x *= 0x7feb352dU; x ^= x >> 15; x *= 0x846ca68bU; x ^= x >> 16;
   return x;
@@ -74,7 +76,14 @@ __host__ __device__ inline uint32_t ea_seed_key(uint64_t seed) {
   return ea_mix32((uint32_t)seed ^ ea_mix32((uint32_t)(seed >> 32) ^ 0x5bd1e995U));
 }
 EA_DEV uint32_t ea_pair_hash(uint32_t key, uint64_t pair) {
-  return ea_mix32(((uint32_t)pair ^ ((uint32_t)(pair >> 32) * 0x85ebca6bU)) * 0x9e3779b9U + key);
+  uint32_t a = (uint32_t)pair + key + __umul24((uint32_t)(pair >> 32), 0x9e3779u);
+  a = (a + 0x7ed55d16u) + (a << 12);
+  a = (a ^ 0xc761c23cu) ^ (a >> 19);
+  a = (a + 0x165667b1u) + (a << 5);
+  a = (a + 0xd3a2646cu) ^ (a << 9);
+  a = (a + 0xfd7046c5u) + (a << 3);
+  a = (a ^ 0xb55a4f09u) ^ (a >> 16);
+  return a;
 }
 // Per-step salt of every dropout stream (ea_set_rng_salt): launchers pass the process-wide
 // device pointer ea_g_rng_salt to their kernels, which mix *salt into the site seed.  The

@@ -37,6 +37,7 @@ struct GemmP {
   int tiles_m, tiles_n;
   int vec_a, vec_b;  // 16-B vector loads allowed (aligned base, ld and batch strides)
   int vec_c;         // 4-column vector epilogue allowed (aligned C/aux/resid/bias, N % 4 == 0)
+  int vec8;          // 8-column (16-B) epilogue allowed (N % 8 == 0, 16-B aligned rows of C/aux/resid)
   int lds;           // bf16 LDS-DMA kernel eligible (aligned operands < 4 GB)
   int bm, bn;        // output tile (LDS-DMA bf16 kernel: 64/128/256 x 128/256; else 128 x 128)
   const unsigned long long* salt;  // per-step dropout salt (device), see ea_set_rng_salt
@@ -313,6 +314,77 @@ EA_DEV void epi_four_pre(const GemmP& p, const EpiK& k, int z, int zb, int zh, i
 #pragma unroll
     for (int c = 0; c < 4; ++c) v[c] *= act_bwd(e.act, o[c]);
     st4(p.C, cidx, p.c_dtype, v);
+  }
+}
+
+// 8 consecutive columns (16-B bf16 / 2 x 16-B f32 accesses): the epilogue's stores are
+// issue-bound with 8-B bf16 stores (MI355X: ~7 B/cycle/CU), so bf16 outputs and operands
+// move 16 B per lane per instruction here
+EA_DEV void ld8(const void* p, long i, int dt, float (&v)[8]) {
+  if (dt == EA_BF16) {
+    const uint4 u = *(const uint4*)((const bf16*)p + i);
+    const bf16* b = (const bf16*)&u;
+#pragma unroll
+    for (int c = 0; c < 8; ++c) v[c] = (float)b[c];
+  } else {
+    const float4 f0 = *(const float4*)((const float*)p + i), f1 = *(const float4*)((const float*)p + i + 4);
+    v[0] = f0.x; v[1] = f0.y; v[2] = f0.z; v[3] = f0.w; v[4] = f1.x; v[5] = f1.y; v[6] = f1.z; v[7] = f1.w;
+  }
+}
+EA_DEV void st8(void* p, long i, int dt, const float (&v)[8]) {
+  if (dt == EA_BF16) {
+    union { uint4 u; bf16 b[8]; } t;
+#pragma unroll
+    for (int c = 0; c < 8; ++c) t.b[c] = (bf16)v[c];
+    *(uint4*)((bf16*)p + i) = t.u;
+  } else {
+    *(float4*)((float*)p + i) = make_float4(v[0], v[1], v[2], v[3]);
+    *(float4*)((float*)p + i + 4) = make_float4(v[4], v[5], v[6], v[7]);
+  }
+}
+EA_DEV void drop8k(const EpiK& k, uint64_t idx, float (&v)[8]) {  // idx even
+  if (!k.drop) return;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const uint32_t h = ea_pair_hash(k.key, (idx >> 1) + q);
+    v[2 * q] *= (h & 0xffffu) >= k.thr ? k.sc : 0.f;
+    v[2 * q + 1] *= (h >> 16) >= k.thr ? k.sc : 0.f;
+  }
+}
+template <int KIND>
+EA_DEV void epi_eight_pre(const GemmP& p, const EpiK& k, int z, int zb, int zh, int row, int col,
+                          const float (&acc)[8], const float (&bias)[8], bool has_o, const float (&o)[8]) {
+  const ea_epilogue& e = p.epi;
+  const long cidx = zb * p.sCb + zh * p.sCh + (long)row * p.ldc + col;
+  const uint64_t didx = ((uint64_t)z * p.M + row) * (uint64_t)p.N + col;
+  float v[8];
+#pragma unroll
+  for (int c = 0; c < 8; ++c) v[c] = e.alpha * acc[c] + (KIND != EA_EPI_DACT ? bias[c] : 0.f);
+  if constexpr (KIND == EA_EPI_STORE) {
+#pragma unroll
+    for (int c = 0; c < 8; ++c) v[c] *= e.post_scale;
+    drop8k(k, didx, v);
+    if (has_o) {
+#pragma unroll
+      for (int c = 0; c < 8; ++c) v[c] += e.beta * o[c];
+    }
+    st8(p.C, cidx, p.c_dtype, v);
+  } else if constexpr (KIND == EA_EPI_ACT) {
+    if (e.aux) st8(e.aux, (long)row * e.ldaux + col, e.aux_dtype, v);
+#pragma unroll
+    for (int c = 0; c < 8; ++c) v[c] = act_fwd(e.act, v[c]);
+    drop8k(k, didx, v);
+    st8(p.C, cidx, p.c_dtype, v);
+  } else if constexpr (KIND == EA_EPI_RESID) {
+    drop8k(k, didx, v);
+#pragma unroll
+    for (int c = 0; c < 8; ++c) v[c] = (has_o ? o[c] : 0.f) + e.rscale * v[c];
+    st8(p.C, cidx, EA_F32, v);
+  } else {
+    drop8k(k, didx, v);
+#pragma unroll
+    for (int c = 0; c < 8; ++c) v[c] *= act_bwd(e.act, o[c]);
+    st8(p.C, cidx, p.c_dtype, v);
   }
 }
 
@@ -619,6 +691,52 @@ EA_DEV void epi_wave(const GemmP& p, const EpiK& k, char* smem, int z, int zb, i
           const float x = t[lr * EPI_LDT + lc + c];
           if (slab) slab[(long)row * p.N + col + c] = x;
           else epi_one<KIND>(p, z, zb, zh, row, col + c, x);
+        }
+      }
+    }
+    return;
+  }
+  if (p.vec8) {  // 8 consecutive columns per lane: 16-B bf16 stores / operand loads
+    constexpr int NG8 = RC * 2;  // row groups of 8 rows per chunk
+    constexpr int HB8 = NG8 < 4 ? NG8 : 4;
+    const int lc8 = (lane & 7) * 8, rl = lane >> 3;
+#pragma unroll
+    for (int ch = 0; ch < NCH; ++ch) {
+      transpose(ch);
+      const int rb = ch_rb(ch), col = c0 + (ch % (NJ / 4)) * 64 + lc8;
+      float bias[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+      if (!slab && KIND != EA_EPI_DACT && p.epi.bias && col < p.N) {
+        const float4 b0 = *(const float4*)(p.epi.bias + col), b1 = *(const float4*)(p.epi.bias + col + 4);
+        bias[0] = b0.x; bias[1] = b0.y; bias[2] = b0.z; bias[3] = b0.w;
+        bias[4] = b1.x; bias[5] = b1.y; bias[6] = b1.z; bias[7] = b1.w;
+      }
+#pragma unroll
+      for (int h0 = 0; h0 < NG8; h0 += HB8) {
+        float o[HB8][8];
+        if (reads) {  // unconditional, clamped, dtype branch outside the batch (see load_unit)
+          const int cl = min(col, p.N - 8);
+          if (sdt == EA_BF16) {
+#pragma unroll
+            for (int it = 0; it < HB8; ++it)
+              ld8(src, sbase + (long)min(rb + (h0 + it) * 8 + rl, p.M - 1) * sld + cl, EA_BF16, o[it]);
+          } else {
+#pragma unroll
+            for (int it = 0; it < HB8; ++it)
+              ld8(src, sbase + (long)min(rb + (h0 + it) * 8 + rl, p.M - 1) * sld + cl, EA_F32, o[it]);
+          }
+        }
+#pragma unroll
+        for (int it = 0; it < HB8; ++it) {
+          const int lr = (h0 + it) * 8 + rl, row = rb + lr;
+          const float4 f0 = *(const float4*)(t + lr * EPI_LDT + lc8), f1 = *(const float4*)(t + lr * EPI_LDT + lc8 + 4);
+          if (row >= p.M || col >= p.N) continue;
+          if (slab) {
+            *(float4*)(slab + (long)row * p.N + col) = f0;
+            *(float4*)(slab + (long)row * p.N + col + 4) = f1;
+            continue;
+          }
+          const float v[8] = {f0.x, f0.y, f0.z, f0.w, f1.x, f1.y, f1.z, f1.w};
+          epi_eight_pre<KIND>(p, k, z, zb, zh, row, col, v, bias, reads, o[it]);
         }
       }
     }
@@ -1359,6 +1477,7 @@ __global__ __launch_bounds__(512, 1) void gemm_grouped(const GroupProbD* __restr
   p.epi.kind = EA_EPI_STORE; p.epi.alpha = 1.f; p.epi.beta = q.beta; p.epi.post_scale = 1.f;
   p.epi.rscale = 1.f;
   p.vec_c = 1;  // host-checked: N % 4 == 0, ldc % 4 == 0, 16-B aligned C
+  p.vec8 = q.N % 8 == 0 && q.ldc % 8 == 0;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int wm = (w >> 2) * 128, wn = (w & 3) * 64;
   f32x4 acc[8][4];
@@ -1602,6 +1721,10 @@ static int gemm_impl(int dtype, int a_kmajor, int b_kmajor, int M, int N, int K,
     if (epi->aux) vc = vc && epi->ldaux % 4 == 0 && ((uintptr_t)epi->aux % (4 * (epi->aux_dtype == EA_BF16 ? 2 : 4))) == 0;
     if (epi->resid) vc = vc && epi->ldr % 4 == 0 && ((uintptr_t)epi->resid % 16) == 0;
     p.vec_c = vc;
+    bool v8 = vc && N % 8 == 0 && ldc % 8 == 0 && sCb % 8 == 0 && sCh % 8 == 0 && ((uintptr_t)C % 16) == 0;
+    if (epi->aux) v8 = v8 && epi->ldaux % 8 == 0 && ((uintptr_t)epi->aux % 16) == 0;
+    if (epi->resid) v8 = v8 && epi->ldr % 8 == 0;
+    p.vec8 = v8;
   }
   p.bm = 128; p.bn = 128;
   // operand extent per batch slice (bytes) must fit the kernel's 32-bit source offsets
