@@ -1119,26 +1119,42 @@ EA_DEV bf16x8 frag32(const char* img, int r, int lane) {  // 16 rows/cols from r
   return out.v;
 }
 
-namespace pipe {
-constexpr int BMP = 256, BNP = 256, BK = 32, NSLOT = 4, NW = 8, NTT = 512;
-constexpr int A_BYTES = BMP * BK * 2, B_BYTES = BNP * BK * 2, SLOT = A_BYTES + B_BYTES;
-constexpr int RING = NSLOT * SLOT;
-constexpr int EPI_BYTES = NW * 64 * EPI_LDT * 4;
-constexpr int SMEM = RING > EPI_BYTES ? RING : EPI_BYTES;
-constexpr int ACH = A_BYTES / (NTT * 16), BCH = B_BYTES / (NTT * 16);  // 2 + 2 DMA per thread
-constexpr int G = ACH + BCH;
-}  // namespace pipe
+// Tile geometry of gemm_pipe: BT x BT output tiles, 8 waves in two ping-pong groups of 4.
+//  * BT = 256: each wave owns a 128 x 64 sub-tile (G0 rows 0-127, G1 rows 128-255), one
+//    block per CU (128 KiB ring).
+//  * BT = 128: each wave owns a 32 x 64 sub-tile (G0 rows 0-63 as 2 x 2 waves, G1 rows
+//    64-127), 64 KiB ring + 70 KiB epilogue staging -> two blocks per CU, so one block's
+//    epilogue overlaps the other's main loop (the N = 512 / short-K GEMMs of the step).
+template <int BT>
+struct PipeT {
+  static constexpr int BK = 32, NSLOT = 4, NW = 8, NTT = 512;
+  static constexpr int A_BYTES = BT * BK * 2, B_BYTES = BT * BK * 2, SLOT = A_BYTES + B_BYTES;
+  static constexpr int RING = NSLOT * SLOT;
+  static constexpr int MI = BT == 256 ? 8 : 2;  // 16-row fragments per wave
+  static constexpr int EPI_BYTES = NW * (MI < 4 ? MI : 4) * 16 * EPI_LDT * 4;
+  static constexpr int SMEM = RING > EPI_BYTES ? RING : EPI_BYTES;
+  static constexpr int ACH = A_BYTES / (NTT * 16), BCH = B_BYTES / (NTT * 16);  // DMA per thread
+  static constexpr int G = ACH + BCH;
+  static constexpr int OCC = BT == 256 ? 1 : 2;
+  static_assert(BT == 256 || BT == 128, "pipe tiles");
+  EA_DEV static int wm(int w) { return BT == 256 ? (w >> 2) * 128 : (w >> 2) * 64 + ((w >> 1) & 1) * 32; }
+  EA_DEV static int wn(int w) { return BT == 256 ? (w & 3) * 64 : (w & 1) * 64; }
+};
 
-// One 256x256 output tile over K range [kbeg, kend) into acc (the wave's 128 x 64 sub-tile);
+// One BT x BT output tile over K range [kbeg, kend) into acc (the wave's sub-tile, PipeT);
 // A / B point at this tile's batch slice.  Returns with every wave done reading smem.
-template <bool AK, bool BKM, int MODE = 0>
+template <bool AK, bool BKM, int MODE = 0, int BT = 256>
 EA_DEV void pipe_tile(const GemmP& p, char* smem, const bf16* A, const bf16* B, int m0, int n0, int kbeg,
-                      int kend, f32x4 (&acc)[8][4]) {
+                      int kend, f32x4 (&acc)[PipeT<BT>::MI][4]) {
   static_assert(MODE == 0 || (MODE == EA_CONV_FWD && AK && BKM) || (MODE == EA_CONV_DGRAD && AK && !BKM) ||
                 (MODE == EA_CONV_WGRAD && !AK && !BKM), "conv gather layouts");
-  using namespace pipe;
+  static_assert(MODE == 0 || BT == 256, "conv gathers run on 256-wide tiles");
+  using PC = PipeT<BT>;
+  constexpr int BK = PC::BK, NSLOT = PC::NSLOT, NW = PC::NW, NTT = PC::NTT, MI = PC::MI;
+  constexpr int A_BYTES = PC::A_BYTES, B_BYTES = PC::B_BYTES, SLOT = PC::SLOT;
+  constexpr int ACH = PC::ACH, BCH = PC::BCH, G = PC::G;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int wm = (w >> 2) * 128, wn = (w & 3) * 64;
+  const int wm = PC::wm(w), wn = PC::wn(w);
   const int nsl = max(0, (kend - kbeg) / BK);
   const bool tail = kbeg + nsl * BK < kend;
 
@@ -1274,10 +1290,10 @@ EA_DEV void pipe_tile(const GemmP& p, char* smem, const bf16* A, const bf16* B, 
 #pragma unroll
     for (int j = 0; j < 4; ++j) fb[j] = frag32<BKM>(lb, wn + j * 16, lane);
   };
-  auto rd_a = [&](int sl, bf16x8 (&fa)[8]) {
+  auto rd_a = [&](int sl, bf16x8 (&fa)[MI]) {
     const char* la = smem + (sl & (NSLOT - 1)) * SLOT;
 #pragma unroll
-    for (int i = 0; i < 8; ++i) fa[i] = frag32<AK>(la, wm + i * 16, lane);
+    for (int i = 0; i < MI; ++i) fa[i] = frag32<AK>(la, wm + i * 16, lane);
   };
 
   const int g1 = w >> 2;  // wave group: G1 runs one barrier behind G0
@@ -1289,7 +1305,7 @@ EA_DEV void pipe_tile(const GemmP& p, char* smem, const bf16* A, const bf16* B, 
   else wait_vmcnt<0>();
   lds_barrier();
   if (g1) lds_barrier();  // the stagger
-  bf16x8 fa[8], fb[4];
+  bf16x8 fa[MI], fb[4];
   for (int sl = 0; sl < nsl; ++sl) {
     // ---- LOAD(sl)
     __builtin_amdgcn_sched_barrier(0);
@@ -1308,7 +1324,7 @@ EA_DEV void pipe_tile(const GemmP& p, char* smem, const bf16* A, const bf16* B, 
       __builtin_amdgcn_sched_barrier(0);
     }
 #pragma unroll
-    for (int i = 0; i < 8; ++i) asm volatile("" ::"v"(fa[i]));
+    for (int i = 0; i < MI; ++i) asm volatile("" ::"v"(fa[i]));
 #pragma unroll
     for (int j = 0; j < 4; ++j) asm volatile("" ::"v"(fb[j]));
     __builtin_amdgcn_sched_barrier(0);
@@ -1316,7 +1332,7 @@ EA_DEV void pipe_tile(const GemmP& p, char* smem, const bf16* A, const bf16* B, 
     // ---- COMPUTE(sl)
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-    for (int i = 0; i < 8; ++i)
+    for (int i = 0; i < MI; ++i)
 #pragma unroll
       for (int j = 0; j < 4; ++j)
         acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
@@ -1364,7 +1380,7 @@ EA_DEV void pipe_tile(const GemmP& p, char* smem, const bf16* A, const bf16* B, 
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-    for (int i = 0; i < 8; ++i)
+    for (int i = 0; i < MI; ++i)
 #pragma unroll
       for (int j = 0; j < 4; ++j)
         acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
@@ -1373,10 +1389,11 @@ EA_DEV void pipe_tile(const GemmP& p, char* smem, const bf16* A, const bf16* B, 
   __syncthreads();  // every wave is done reading the ring
 }
 
-template <bool AK, bool BKM, int MODE = 0>
-__global__ __launch_bounds__(512, 1) void gemm_pipe(GemmP p) {
-  using namespace pipe;
-  __shared__ __attribute__((aligned(1024))) char smem[SMEM];
+template <bool AK, bool BKM, int MODE = 0, int BT = 256>
+__global__ __launch_bounds__(512, PipeT<BT>::OCC) void gemm_pipe(GemmP p) {
+  using PC = PipeT<BT>;
+  constexpr int MI = PC::MI;
+  __shared__ __attribute__((aligned(1024))) char smem[PC::SMEM];
   probe_start(p);
 
   const int nt = p.tiles_m * p.tiles_n;
@@ -1389,7 +1406,7 @@ __global__ __launch_bounds__(512, 1) void gemm_pipe(GemmP p) {
   const int gsz = min(GM, p.tiles_m - gm0);
   const int tm = gm0 + (t % (GM * p.tiles_n)) % gsz;
   const int tn = (t % (GM * p.tiles_n)) / gsz;
-  const int m0 = tm * BMP, n0 = tn * BNP;
+  const int m0 = tm * BT, n0 = tn * BT;
 
   const int z = blockIdx.z / p.splitk, sk = blockIdx.z % p.splitk;
   const int zb = z / p.nh, zh = z % p.nh;
@@ -1398,21 +1415,21 @@ __global__ __launch_bounds__(512, 1) void gemm_pipe(GemmP p) {
   const int kbeg = sk * p.kchunk;
   const int kend = min(p.K, kbeg + p.kchunk);
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int wm = (w >> 2) * 128, wn = (w & 3) * 64;
-  f32x4 acc[8][4];
+  const int wm = PC::wm(w), wn = PC::wn(w);
+  f32x4 acc[MI][4];
 #pragma unroll
-  for (int i = 0; i < 8; ++i)
+  for (int i = 0; i < MI; ++i)
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
   diag_stamp(p, 0);
-  pipe_tile<AK, BKM, MODE>(p, smem, A, B, m0, n0, kbeg, kend, acc);
+  pipe_tile<AK, BKM, MODE, BT>(p, smem, A, B, m0, n0, kbeg, kend, acc);
   diag_stamp(p, 1);
   const EpiK ek = make_epik(p);
   switch (p.splitk > 1 ? EA_EPI_STORE : p.epi.kind) {
-    case EA_EPI_STORE: epi_wave<EA_EPI_STORE, 8, 4>(p, ek, smem, z, zb, zh, m0 + wm, n0 + wn, lane, w, acc); break;
-    case EA_EPI_ACT: epi_wave<EA_EPI_ACT, 8, 4>(p, ek, smem, z, zb, zh, m0 + wm, n0 + wn, lane, w, acc); break;
-    case EA_EPI_RESID: epi_wave<EA_EPI_RESID, 8, 4>(p, ek, smem, z, zb, zh, m0 + wm, n0 + wn, lane, w, acc); break;
-    default: epi_wave<EA_EPI_DACT, 8, 4>(p, ek, smem, z, zb, zh, m0 + wm, n0 + wn, lane, w, acc); break;
+    case EA_EPI_STORE: epi_wave<EA_EPI_STORE, MI, 4>(p, ek, smem, z, zb, zh, m0 + wm, n0 + wn, lane, w, acc); break;
+    case EA_EPI_ACT: epi_wave<EA_EPI_ACT, MI, 4>(p, ek, smem, z, zb, zh, m0 + wm, n0 + wn, lane, w, acc); break;
+    case EA_EPI_RESID: epi_wave<EA_EPI_RESID, MI, 4>(p, ek, smem, z, zb, zh, m0 + wm, n0 + wn, lane, w, acc); break;
+    default: epi_wave<EA_EPI_DACT, MI, 4>(p, ek, smem, z, zb, zh, m0 + wm, n0 + wn, lane, w, acc); break;
   }
   if (p.diag) {
     __syncthreads();
@@ -1458,8 +1475,8 @@ __global__ void group_upload(GroupChunk c, GroupProbD* table, int* map) {
 template <bool AK, bool BKM>
 __global__ __launch_bounds__(512, 1) void gemm_grouped(const GroupProbD* __restrict__ table,
                                                        const int* __restrict__ map, int ntiles) {
-  using namespace pipe;
-  __shared__ __attribute__((aligned(1024))) char smem[SMEM];
+  using PC = PipeT<256>;
+  __shared__ __attribute__((aligned(1024))) char smem[PC::SMEM];
   const int nt = ntiles;
   const int bid = blockIdx.x;
   const int q8 = nt / 8, r8 = nt % 8, xcd = bid % 8;
@@ -1467,7 +1484,7 @@ __global__ __launch_bounds__(512, 1) void gemm_grouped(const GroupProbD* __restr
   const GroupProbD q = table[__builtin_amdgcn_readfirstlane(map[t])];
   const int lt = t - q.tile0;
   const int tm = lt / q.tiles_n, tn = lt - tm * q.tiles_n;  // neighbours share the A panel
-  const int m0 = tm * BMP, n0 = tn * BNP;
+  const int m0 = tm * 256, n0 = tn * 256;
   GemmP p{};
   p.M = q.M; p.N = q.N; p.K = q.K;
   p.A = q.A; p.lda = q.lda;
@@ -1479,7 +1496,7 @@ __global__ __launch_bounds__(512, 1) void gemm_grouped(const GroupProbD* __restr
   p.vec_c = 1;  // host-checked: N % 4 == 0, ldc % 4 == 0, 16-B aligned C
   p.vec8 = q.N % 8 == 0 && q.ldc % 8 == 0;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int wm = (w >> 2) * 128, wn = (w & 3) * 64;
+  const int wm = PC::wm(w), wn = PC::wn(w);
   f32x4 acc[8][4];
 #pragma unroll
   for (int i = 0; i < 8; ++i)
@@ -1526,7 +1543,7 @@ int g_gemm_stages = 2;
 unsigned long long* g_probe = nullptr;  // ea_gemm_set_probe
 unsigned long long* g_diag = nullptr;   // ea_gemm_set_diag
 int g_gemm_bm64 = 1;
-int g_gemm_pipe = 0;  // 256x256 dense tiles on gemm_pipe (ea_gemm_set_pipe)  // LDS ring depth of gemm_bf16_lds (2: 64 KiB, 2 blocks/CU; 3: 96 KiB)
+int g_gemm_pipe = 0;  // ea_gemm_set_pipe bits: 1 = 256x256 tiles on gemm_pipe, 2 = 128x128 tiles too
 
 int launch_lds(GemmP& p, int a_k, int b_k, int nz, hipStream_t st) {
   dim3 grid(p.tiles_m * p.tiles_n, 1, nz * p.splitk);
@@ -1572,6 +1589,11 @@ int launch_lds(GemmP& p, int a_k, int b_k, int nz, hipStream_t st) {
     } else {
       EA_GL4(256, 256, 2)
     }
+  } else if (g_gemm_pipe & 2) {
+    if (a_k && b_k) hipLaunchKernelGGL((gemm_pipe<true, true, 0, 128>), grid, dim3(512), 0, st, p);
+    else if (a_k) hipLaunchKernelGGL((gemm_pipe<true, false, 0, 128>), grid, dim3(512), 0, st, p);
+    else if (b_k) hipLaunchKernelGGL((gemm_pipe<false, true, 0, 128>), grid, dim3(512), 0, st, p);
+    else hipLaunchKernelGGL((gemm_pipe<false, false, 0, 128>), grid, dim3(512), 0, st, p);
   } else {
     EA_GL4(128, 128, 2)
   }

@@ -24,7 +24,6 @@ namespace {
 constexpr int DK = 64;     // head dim
 constexpr int QB = 64;     // forward: query rows per workgroup
 constexpr int KC = 64;     // forward: keys per chunk
-constexpr int BQ = 32;     // backward: query rows per tile
 constexpr int NWAVE = 4;
 
 // [rows][64] bf16 image, 128-B rows, 16-B chunk c stored at c ^ swz_k(row) (conflict-free
@@ -130,8 +129,19 @@ struct AttnP {
   bf16* dq; long lddq;
   bf16* dk; long lddk;
   bf16* dv; long lddv;
-  bf16* dbd; long lddbd;     // [h][b][i][lddbd] band gradient (rel-pos), pre-zeroed
+  bf16* dbd; long lddbd;     // [h][b][i][lddbd] band gradient (rel-pos), written in full
+  float* bias_part; long ldpart;  // [2][B*ceil(T1/64)][ldpart] column sums of dQ_u, dQ_v
+  bf16* qv_out; long ldqv;   // q + pos_bias_v (rel-pos), rows b*T1 + i, or null
+  int flags;                 // bit 0: dq includes the rel-pos term dBD.p
+  uint32_t* dmask; int ldm;  // dropout keep bits [z*T1 + i][ldm words], bit j&31 of word j>>5:
+                             // written by the forward, read by the backward (else rehashed)
 };
+
+// ldm >= 2 * ceil(T2 / 64): a 64-key chunk is the word pair (j0 >> 5, +1)
+EA_DEV bool keep_hash(uint32_t key, uint32_t thr, uint64_t idx) {
+  const uint32_t h = ea_pair_hash(key, idx >> 1);
+  return ((idx & 1) ? h >> 16 : h & 0xffffu) >= thr;
+}
 
 // ------------------------------------------------------------------------------ forward
 constexpr int F_K = 0, F_V = F_K + KC * 128, F_P = F_V + KC * 128;  // K, V chunk, P band (128 rows)
@@ -178,6 +188,9 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(AttnP a) {
   for (int r = 0; r < 4; ++r) { mrun[r] = -INFINITY; lrun[r] = 0.f; }
   const int ibase = i0 + 16 * w + 4 * g;  // query row of register rr: ibase + rr
   const int kend = a.causal ? min(kl, i0 + QB) : kl;
+  uint64_t rowbase[4];  // dropout element index of (row, key 0)
+#pragma unroll
+  for (int r = 0; r < 4; ++r) rowbase[r] = ((uint64_t)z * a.T1 + ibase + r) * a.T2;
 
   for (int j0 = 0; j0 < kend; j0 += KC) {
     km_stage(sm + F_K, a.k + (long)b * a.T2 * a.ldk + h * DK, a.ldk, j0, KC, a.T2, tid, 256);
@@ -242,18 +255,35 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(AttnP a) {
 #pragma unroll
       for (int t = 0; t < 4; ++t) oacc[t][r] *= alpha;
     }
-    // dropout, Pd -> bf16 image (16 rows x 64 keys) -> A fragments
+    // dropout (keep bits -> dmask for the backward), Pd -> bf16 image (16 rows x 64 keys)
+    if (a.p > 0.f) {
+      const uint32_t key = ea_seed_key(seed), thr = ea_drop_thr(a.p);
+      const float sc = 1.f / (1.f - a.p);
+      uint64_t bal[4][4];
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const bool kept = keep_hash(key, thr, rowbase[r] + (uint64_t)(j0 + 16 * t + lc));
+          pv[t][r] *= kept ? sc : 0.f;
+          bal[t][r] = __ballot(kept);
+        }
+      if (a.dmask && lc < 2) {  // lane lc = u writes word u of each of its group's 4 rows
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int i = ibase + r;
+          const uint64_t lo = lc ? bal[2][r] : bal[0][r], hi = lc ? bal[3][r] : bal[1][r];
+          const uint32_t word = (uint32_t)((lo >> (16 * g)) & 0xffffu) | ((uint32_t)((hi >> (16 * g)) & 0xffffu) << 16);
+          if (i < a.T1) a.dmask[((long)z * a.T1 + i) * a.ldm + (j0 >> 5) + lc] = word;
+        }
+      }
+    }
 #pragma unroll
     for (int t = 0; t < 4; ++t)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        float e = pv[t][r];
-        if (a.p > 0.f) {
-          const int i = ibase + r, j = j0 + 16 * t + lc;
-          e *= drop_scale(seed, ((uint64_t)z * a.T1 + i) * a.T2 + j, a.p);
-        }
         const int il = 4 * g + r, jl = 16 * t + lc;
-        *(bf16*)(pimg + km_off(il, jl >> 3) + (jl & 7) * 2) = (bf16)e;
+        *(bf16*)(pimg + km_off(il, jl >> 3) + (jl & 7) * 2) = (bf16)pv[t][r];
       }
     lds_fence();
 #pragma unroll
@@ -278,281 +308,551 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(AttnP a) {
 }
 
 // ------------------------------------------------------------------------------ backward
-constexpr int B_KV = 0;                                   // per wave: K_w, V_w images (8 KB each)
-constexpr int B_Q = B_KV + NWAVE * 2 * 64 * 128;          // Qu, Qv, dO tile images (32 rows)
-constexpr int B_D = B_Q + 3 * BQ * 128;                   // D_i, lse_i (32 each)
-constexpr int B_WS = B_D + 2 * BQ * 4;                    // per-wave scratch
-constexpr int B_BDLD = 97;                                // BDfull row stride (floats)
-constexpr int B_XSZ = BQ * B_BDLD * 4 > BQ * 64 * 4 ? BQ * B_BDLD * 4 : BQ * 64 * 4;  // BD gather | dQ partial
-constexpr int B_WSZ = ((B_XSZ + 15) / 16) * 16 + BQ * 128; // + dS image
-constexpr int B_BIAS = B_WS + NWAVE * B_WSZ;              // pos_bias_u, pos_bias_v of head h (f32)
-constexpr int B_LDS = B_BIAS + 2 * DK * 4;
+// Two launches of many workgroups each; no cross-workgroup sums, so results are
+// bit-reproducible.  Both recompute S (+ the rel-pos band), P = exp(S*scale - lse) from the
+// forward's row log-sum-exp, dP = dO.V^T and dS = P (dP keep - D) scale with D_i = dO_i.O_i;
+// dropout keep factors come from the forward's bit mask (or the counter hash without one).
+//  * attn_bwdq: one workgroup per (b, h, 64 queries), the forward kernel's layout (wave w owns
+//    16 query rows, keys in chunks of 64).  dQ = dS.K, plus (rel-pos) dS laid onto its band
+//    times the positional rows: d(q+v) = dBD.p, so the caller's band GEMM and add disappear.
+//    Emits the band gradient dBD rows in full (zeros off the band: no memset) for the
+//    linear_pos weight gradient, and per-workgroup column sums of both dQ terms
+//    (pos_bias_u / pos_bias_v gradients, reduced by the caller in fixed order).
+//  * attn_bwdkv: one workgroup per (b, h, 64 keys), wave w owns 16 keys; 32-query tiles are
+//    staged once per workgroup (next tile prefetched into registers during the MFMA work) and
+//    dV = Pd^T.dO, dK = dS^T.(Q+u) stay in registers.
+// Masked rows / keys give P = 0 and so dS = 0.
+constexpr int BQ = 32;  // attn_bwdkv query tile
+constexpr float LOG2E = 1.4426950408889634f;
+
+// dS^T image [64 keys][16 queries] bf16 (32-B rows), written 4 queries (8 B) at a time from
+// the C layout; read back as A fragments (16 queries x 32 keys) with transposed reads
+EA_DEV bf16x8 dst_frag(const char* img, int kb, int lane) {
+  const int i = lane & 15, q = i >> 2, p = i & 3, g = lane >> 4;
+  union { bf16x8 v; s16x4 h[2]; } out;
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const char* a = img + (kb + 8 * g + 4 * h + q) * 32 + p * 8;
+    out.h[h] = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(uintptr_t)a);
+  }
+  return out.v;
+}
+// dS band image [16 queries][96 band columns] bf16, 192-B rows, 16-B chunk c of row r at
+// c ^ ((r >> 2) & 3) (conflict-free b128 A-fragment reads)
+EA_DEV int band_off(int r, int c) { return r * 192 + ((((c >> 3) ^ ((r >> 2) & 3))) << 4) + (c & 7) * 2; }
+EA_DEV bf16x8 band_frag(const char* img, int ks, int lane) {
+  const int r = lane & 15, c = ks * 4 + (lane >> 4);
+  return *(const bf16x8*)(img + r * 192 + ((c ^ ((r >> 2) & 3)) << 4));
+}
+EA_DEV uint32_t pack_bf16x2(float lo, float hi) {
+  union { bf16 h[2]; uint32_t u; } x;
+  x.h[0] = (bf16)lo;
+  x.h[1] = (bf16)hi;
+  return x.u;
+}
+
+// attn_bwdq shared memory
+constexpr int Q_K = 0, Q_V = Q_K + KC * 128, Q_P = Q_V + KC * 128;  // K, V chunk, band (144 rows)
+constexpr int Q_D = Q_P + 144 * 128;                                // D_i, lse_i (64 each)
+constexpr int Q_WS = Q_D + 2 * QB * 4;                              // per-wave scratch
+constexpr int Q_XSZ = 16 * F_BDLD * 4;                              // BD gather | dS band image
+constexpr int Q_WSZ = Q_XSZ + 64 * 32;                              // + dS^T image
+constexpr int Q_RED = Q_WS + NWAVE * Q_WSZ;                         // column-sum exchange
+constexpr int Q_LDS = Q_RED + 2 * NWAVE * DK * 4;
+static_assert(Q_XSZ >= 16 * 192 && Q_XSZ % 16 == 0, "band image fits the gather scratch");
+static_assert(3 * QB * 128 <= Q_D, "setup images fit the chunk space");
+
+// rows [r0, r0+nrows) of (src + bias) into a km image, also written to out (if non-null)
+EA_DEV void km_stage_bias_out(char* img, const bf16* __restrict__ src, long ld, int r0, int nrows, int rlim,
+                              const float* __restrict__ bias, bf16* out, long ldout, int tid, int nthr) {
+  for (int c = tid; c < nrows * 8; c += nthr) {
+    const int row = c >> 3, ch = c & 7;
+    const int r = r0 + row;
+    union { uint4 u; bf16 e[8]; } t;
+    t.u = make_uint4(0u, 0u, 0u, 0u);
+    if (r >= 0 && r < rlim) {
+      t.u = *(const uint4*)(src + (long)r * ld + ch * 8);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) t.e[e] = (bf16)((float)t.e[e] + bias[ch * 8 + e]);
+      if (out) *(uint4*)(out + (long)r * ldout + ch * 8) = t.u;
+    }
+    *(uint4*)(img + km_off(row, ch)) = t.u;
+  }
+}
 
 template <bool REL>
-__global__ __launch_bounds__(256, 1) void attn_bwd_kernel(AttnP a) {
-  __shared__ __attribute__((aligned(16))) char sm[B_LDS];
-  const int z = blockIdx.x;
+__global__ __launch_bounds__(256, 2) void attn_bwdq_kernel(AttnP a) {
+  __shared__ __attribute__((aligned(16))) char sm[Q_LDS];
+  const int nqb = (a.T1 + QB - 1) / QB;
+  const int z = blockIdx.x / nqb, qb = blockIdx.x % nqb;
+  const int b = z / a.H, h = z % a.H;
+  const int i0 = qb * QB;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int g = lane >> 4, lc = lane & 15;
+  const int kl = a.klen ? (int)min((long long)a.T2, a.klen[b]) : a.T2;
+  const uint64_t seed = a.p > 0.f ? ea_salted(a.seed, a.salt) : 0;
+  const bool with_dqv = REL && (a.flags & 1);
+  char* ws = sm + Q_WS + w * Q_WSZ;
+  float* bds = (float*)ws;
+  char* band = ws;                // dS on its band (after the gather has read bds)
+  char* dst = ws + Q_XSZ;
+  float* Dv = (float*)(sm + Q_D);
+  float* Lv = Dv + QB;
+
+  // this wave's 16 rows of Q + u, Q + v and dO as A fragments; D_i and lse_i
+  bf16x8 qa[2], qv[2], doa[2];
+  {
+    const bf16* qsrc = a.q + (long)b * a.T1 * a.ldq + h * DK;
+    km_stage_bias(sm, qsrc, a.ldq, i0, QB, a.T1, a.bu ? a.bu + h * DK : nullptr, tid, 256);
+    if (REL)
+      km_stage_bias_out(sm + QB * 128, qsrc, a.ldq, i0, QB, a.T1, a.bv + h * DK,
+                        a.qv_out ? a.qv_out + (long)b * a.T1 * a.ldqv + h * DK : nullptr, a.ldqv, tid, 256);
+    km_stage(sm + 2 * QB * 128, a.dO + (long)b * a.T1 * a.lddo + h * DK, a.lddo, i0, QB, a.T1, tid, 256);
+    {  // D_i = dO_i . O_i: 4 threads per row, 16 columns each
+      const int row = tid >> 2, qd = tid & 3, i = i0 + row;
+      float d = 0.f;
+      if (i < a.T1) {
+        const bf16* dr = a.dO + ((long)b * a.T1 + i) * a.lddo + h * DK + qd * 16;
+        const bf16* orow = a.o + ((long)b * a.T1 + i) * a.ldo + h * DK + qd * 16;
+#pragma unroll
+        for (int hf = 0; hf < 2; ++hf) {
+          union { uint4 u; bf16 e[8]; } x, y;
+          x.u = *(const uint4*)(dr + hf * 8);
+          y.u = *(const uint4*)(orow + hf * 8);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) d += (float)x.e[e] * (float)y.e[e];
+        }
+      }
+      d += __shfl_xor(d, 1, 64);
+      d += __shfl_xor(d, 2, 64);
+      if (qd == 0) {
+        Dv[row] = d;
+        Lv[row] = i < a.T1 ? a.lse[(long)z * a.T1 + i] * LOG2E : INFINITY;
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      qa[ks] = km_frag(sm, 16 * w, ks, lane);
+      if (REL) qv[ks] = km_frag(sm + QB * 128, 16 * w, ks, lane);
+      doa[ks] = km_frag(sm + 2 * QB * 128, 16 * w, ks, lane);
+    }
+  }
+  const int ibase = i0 + 16 * w + 4 * g;  // query row of register r: ibase + r
+  float Dr[4], Lr[4];
+  int lim[4];  // key j of row r is valid iff j < lim[r]
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int i = ibase + r;
+    Dr[r] = Dv[16 * w + 4 * g + r];
+    Lr[r] = Lv[16 * w + 4 * g + r];
+    lim[r] = i < a.T1 ? (a.causal ? min(kl, i + 1) : kl) : 0;
+  }
+  const float sl2 = a.scale * LOG2E;
+  const int kend = a.causal ? min(kl, i0 + QB) : kl;
+  const int nch = (kend + KC - 1) / KC;
+  bf16* dbd_h = REL && a.dbd ? a.dbd + ((long)h * a.B + b) * a.T1 * a.lddbd : nullptr;
+  if (dbd_h) {  // zeros off the part of each row the chunk loop writes: r < T-1-i, r >= T-1-i+jcov
+    const int jcov = min(a.T2, nch * KC);
+    for (int il = 0; il < 16; ++il) {
+      const int i = i0 + 16 * w + il;
+      if (i >= a.T1) break;
+      bf16* drow = dbd_h + (long)i * a.lddbd;
+      const int lo = a.T1 - 1 - i, hi = lo + jcov;
+      for (int c = lane; c < a.lddbd; c += 64)
+        if (c < lo || c >= hi) drow[c] = (bf16)0.f;
+    }
+  }
+  const bool use_mask = a.p > 0.f && a.dmask != nullptr;
+  const uint32_t* mrow = a.dmask + ((long)z * a.T1 + ibase) * a.ldm;  // rows ibase + r (< T1)
+  const float dsc = a.p > 0.f ? 1.f / (1.f - a.p) : 1.f;
+
+  f32x4 dqu[4], dqv[4];
+#pragma unroll
+  for (int n = 0; n < 4; ++n) dqu[n] = dqv[n] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  const int pb = 48 - 16 * w;  // this wave's first band row in the chunk's band image
+  for (int j0 = 0; j0 < kend; j0 += KC) {
+    // keep words of rows ibase + r for keys j0 .. j0+63 (bit 16(t&1) + lc of word t>>1): the
+    // forward's mask, else rebuilt from the counter hash (this lane's bits only), else all kept
+    uint2 mw[4];
+    if (use_mask) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        mw[r] = ibase + r < a.T1 ? *(const uint2*)(mrow + (long)r * a.ldm + (j0 >> 5)) : make_uint2(0u, 0u);
+    } else if (a.p > 0.f) {
+      const uint32_t key = ea_seed_key(seed), thr = ea_drop_thr(a.p);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const uint64_t rowb = ((uint64_t)z * a.T1 + ibase + r) * a.T2 + j0 + lc;
+        uint32_t x = 0u, y = 0u;
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+          const uint32_t bit = (uint32_t)keep_hash(key, thr, rowb + 16 * t) << (16 * (t & 1) + lc);
+          if (t < 2) x |= bit; else y |= bit;
+        }
+        mw[r] = make_uint2(x, y);
+      }
+    } else {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) mw[r] = make_uint2(~0u, ~0u);
+    }
+    __syncthreads();  // the setup images / previous chunk's images are no longer read
+    km_stage(sm + Q_K, a.k + (long)b * a.T2 * a.ldk + h * DK, a.ldk, j0, KC, a.T2, tid, 256);
+    km_stage(sm + Q_V, a.v + (long)b * a.T2 * a.ldv + h * DK, a.ldv, j0, KC, a.T2, tid, 256);
+    const int rb = a.T1 - 1 - (i0 + QB - 1) + j0;  // first positional row of the block's band
+    if (REL) km_stage(sm + Q_P, a.pp + h * DK, a.ldp, rb, 144, 2 * a.T1 - 1, tid, 256);
+    __syncthreads();
+    f32x4 s[4], dp[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      s[t] = (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) s[t] = mfma(qa[ks], km_frag(sm + Q_K, 16 * t, ks, lane), s[t]);
+    }
+    if (REL) {
+#pragma unroll
+      for (int t = 0; t < 5; ++t) {
+        f32x4 bd = (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) bd = mfma(qv[ks], km_frag(sm + Q_P, pb + 16 * t, ks, lane), bd);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) bds[(4 * g + r) * F_BDLD + 16 * t + lc] = bd[r];
+      }
+      lds_fence();
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int il = 4 * g + r, jl = 16 * t + lc;
+          s[t][r] += bds[il * F_BDLD + 15 - il + jl];
+        }
+    }
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      dp[t] = (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) dp[t] = mfma(doa[ks], km_frag(sm + Q_V, 16 * t, ks, lane), dp[t]);
+    }
+    // dS (scaled), in place of s
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const int j = j0 + 16 * t + lc;
+        const float e = __builtin_amdgcn_exp2f(fmaf(s[t][r], sl2, -Lr[r]));
+        const float P = j < lim[r] ? e : 0.f;
+        const float kp = (((t < 2 ? mw[r].x : mw[r].y) >> (16 * (t & 1) + lc)) & 1u) ? dsc : 0.f;
+        s[t][r] = (P * a.scale) * fmaf(dp[t][r], kp, -Dr[r]);
+      }
+    // dS^T image (4 queries per 8-B write) and (rel-pos) the band image, column 15-il+jl
+    if (with_dqv) {
+      lds_fence();  // the gather above has read bds
+      const uint4 zero = make_uint4(0u, 0u, 0u, 0u);
+#pragma unroll
+      for (int c = 0; c < 3; ++c) *(uint4*)(band + (c * 64 + lane) * 16) = zero;
+      lds_fence();
+    }
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const uint2 v = make_uint2(pack_bf16x2(s[t][0], s[t][1]), pack_bf16x2(s[t][2], s[t][3]));
+      *(uint2*)(dst + (16 * t + lc) * 32 + g * 8) = v;
+      if (with_dqv) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int il = 4 * g + r;
+          *(bf16*)(band + band_off(il, 15 - il + 16 * t + lc)) = (bf16)s[t][r];
+        }
+      }
+    }
+    lds_fence();
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      const bf16x8 af = dst_frag(dst, 32 * ks, lane);
+#pragma unroll
+      for (int n = 0; n < 4; ++n) dqu[n] = mfma(af, km_frag_tr(sm + Q_K, 32 * ks, 16 * n, lane), dqu[n]);
+    }
+    if (with_dqv) {
+#pragma unroll
+      for (int ks = 0; ks < 3; ++ks) {
+        const bf16x8 af = band_frag(band, ks, lane);
+#pragma unroll
+        for (int n = 0; n < 4; ++n) dqv[n] = mfma(af, km_frag_tr(sm + Q_P, pb + 32 * ks, 16 * n, lane), dqv[n]);
+      }
+    }
+    if (dbd_h) {  // dBD_raw[h][b][i][T-1-i+j] = dS
+      const bool full = j0 + KC <= a.T2;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int i = ibase + r;
+        if (i >= a.T1) continue;
+        bf16* drow = dbd_h + (long)i * a.lddbd + (a.T1 - 1 - i) + j0 + lc;
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+          if (full || j0 + 16 * t + lc < a.T2) drow[16 * t] = (bf16)s[t][r];
+      }
+    }
+  }
+  // dQ (bf16) = dS.K (+ dBD.p); column sums of both terms over this block's rows
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int i = ibase + r;
+    if (i >= a.T1) continue;
+    bf16* qrow = a.dq + ((long)b * a.T1 + i) * a.lddq + h * DK;
+#pragma unroll
+    for (int n = 0; n < 4; ++n) qrow[16 * n + lc] = (bf16)(dqu[n][r] + (with_dqv ? dqv[n][r] : 0.f));
+  }
+  if (a.bias_part) {
+    float* red = (float*)(sm + Q_RED);  // [2][NWAVE][64]
+#pragma unroll
+    for (int n = 0; n < 4; ++n) {
+      float su = (dqu[n][0] + dqu[n][1]) + (dqu[n][2] + dqu[n][3]);
+      float sv = (dqv[n][0] + dqv[n][1]) + (dqv[n][2] + dqv[n][3]);
+      su += __shfl_xor(su, 16, 64);
+      sv += __shfl_xor(sv, 16, 64);
+      su += __shfl_xor(su, 32, 64);
+      sv += __shfl_xor(sv, 32, 64);
+      if (g == 0) {
+        red[w * DK + 16 * n + lc] = su;
+        red[(NWAVE + w) * DK + 16 * n + lc] = sv;
+      }
+    }
+    __syncthreads();
+    if (tid < 2 * DK) {
+      const int which = tid / DK, c = tid % DK;
+      const float* rr = red + which * NWAVE * DK;
+      const float v = (rr[c] + rr[DK + c]) + (rr[2 * DK + c] + rr[3 * DK + c]);
+      const long prow = (long)which * a.B * nqb + (long)b * nqb + qb;
+      if (which == 0 || REL) a.bias_part[prow * a.ldpart + h * DK + c] = v;
+    }
+  }
+}
+
+// attn_bwdkv shared memory
+constexpr int V_QU = 0, V_QV = V_QU + BQ * 128, V_DO = V_QV + BQ * 128, V_P = V_DO + BQ * 128;
+constexpr int V_D = V_P + 96 * 128;               // D_i, lse_i*log2e (32 each), keep words [2][32]
+constexpr int V_XLD = 97;                         // BDfull row stride (floats)
+constexpr int V_XS = V_D + 4 * BQ * 4;            // BDfull [32][97] f32, shared by the waves
+constexpr int V_LDS = V_XS + BQ * V_XLD * 4;
+
+template <bool REL>
+__global__ __launch_bounds__(256, 2) void attn_bwdkv_kernel(AttnP a) {
+  __shared__ __attribute__((aligned(16))) char sm[V_LDS];
+  const int nkb = (a.T2 + 63) / 64;
+  const int z = blockIdx.x / nkb, kb = blockIdx.x % nkb;
   const int b = z / a.H, h = z % a.H;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int g = lane >> 4, lc = lane & 15;
   const int kl = a.klen ? (int)min((long long)a.T2, a.klen[b]) : a.T2;
   const uint64_t seed = a.p > 0.f ? ea_salted(a.seed, a.salt) : 0;
-  char* kimg = sm + B_KV + w * 2 * 64 * 128;
-  char* vimg = kimg + 64 * 128;
-  char* quimg = sm + B_Q;
-  char* qvimg = quimg + BQ * 128;
-  char* doimg = qvimg + BQ * 128;
-  float* Dv = (float*)(sm + B_D);
+  const int j0 = 64 * kb, jw = j0 + 16 * w;
+  char* quimg = sm + V_QU;
+  char* qvimg = sm + V_QV;
+  char* doimg = sm + V_DO;
+  char* pimg = sm + V_P;
+  float* Dv = (float*)(sm + V_D);
   float* Lv = Dv + BQ;
-  char* ws = sm + B_WS + w * B_WSZ;
-  float* xs = (float*)ws;
-  char* dsimg = ws + ((B_XSZ + 15) / 16) * 16;
-  const int jw = 64 * w;  // this wave's keys [jw, jw+64)
-  const bool active = jw < kl;
+  uint32_t* Mw = (uint32_t*)(Lv + BQ);  // [word u][32 rows]
+  float* xs = (float*)(sm + V_XS);
 
-  km_stage(kimg, a.k + (long)b * a.T2 * a.ldk + h * DK, a.ldk, jw, 64, kl, lane, 64);
-  km_stage(vimg, a.v + (long)b * a.T2 * a.ldv + h * DK, a.ldv, jw, 64, kl, lane, 64);
-  f32x4 dka[4][4], dva[4][4];
+  f32x4 dka[4], dva[4];  // rows = keys jw + 4g + r, columns 16n + lc
 #pragma unroll
-  for (int m = 0; m < 4; ++m)
+  for (int n = 0; n < 4; ++n) dka[n] = dva[n] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  if (j0 < kl) {
+    // this wave's 16 keys as B fragments (key jw + lc, dims 32ks + 8g ..+7)
+    const int j = jw + lc;
+    bf16x8 kf[2], vf[2];
 #pragma unroll
-    for (int n = 0; n < 4; ++n) dka[m][n] = dva[m][n] = (f32x4){0.f, 0.f, 0.f, 0.f};
-
-  // The next query tile's inputs are fetched into registers while the current tile's MFMA
-  // work runs (one workgroup per CU, so global latency is otherwise exposed): thread tid
-  // owns row tid>>3, 16-B chunk tid&7 of the Q / dO / O tiles (BQ * 8 == 256 pieces).
-  static_assert(BQ * 8 == 256, "one 16-B piece per thread");
-  const bf16* qsrc = a.q + (long)b * a.T1 * a.ldq + h * DK;
-  const bf16* dosrc = a.dO + (long)b * a.T1 * a.lddo + h * DK;
-  const bf16* osrc = a.o + (long)b * a.T1 * a.ldo + h * DK;
-  const bf16* pbase = REL ? a.pp + h * DK : nullptr;
-  const int nqt = (a.T1 + BQ - 1) / BQ;
-  const int prow = tid >> 3, pch = tid & 7;
-  float* bias_s = (float*)(sm + B_BIAS);  // [u | v], read at each tile's staging
-  if (tid < DK) {
-    bias_s[tid] = a.bu ? a.bu[h * DK + tid] : 0.f;
-    bias_s[DK + tid] = REL ? a.bv[h * DK + tid] : 0.f;
-  }  // ordered before the first read by the loop's first __syncthreads
-  struct Pre { uint4 q, dO, o; float lse; };
-  auto fetch = [&](int i0n, Pre& pr) {
-    const int i = i0n + prow;
-    pr.q = pr.dO = pr.o = make_uint4(0u, 0u, 0u, 0u);
-    pr.lse = INFINITY;
-    if (i < a.T1) {
-      pr.q = *(const uint4*)(qsrc + (long)i * a.ldq + pch * 8);
-      pr.dO = *(const uint4*)(dosrc + (long)i * a.lddo + pch * 8);
-      pr.o = *(const uint4*)(osrc + (long)i * a.ldo + pch * 8);
-      pr.lse = a.lse[(long)z * a.T1 + i];
-    }
-  };
-  auto tile_on = [&](int i0n) { return active && !(a.causal && jw > i0n + BQ - 1); };
-  // BDfull B fragments: band rows rs + 16t + lc, rs = T-1-(i0+31)+jw (clamped rows only
-  // feed BDfull entries the diagonal gather never reads)
-  auto fetch_band = [&](int i0n, bf16x8 (&pf)[6][2]) {
-    const int rs = a.T1 - 1 - (i0n + BQ - 1) + jw;
-#pragma unroll
-    for (int t = 0; t < 6; ++t) {
-      const int r = min(max(rs + 16 * t + lc, 0), 2 * a.T1 - 2);
-#pragma unroll
-      for (int ks = 0; ks < 2; ++ks) pf[t][ks] = *(const bf16x8*)(pbase + (long)r * a.ldp + ks * 32 + g * 8);
-    }
-  };
-  Pre pre;
-  fetch(0, pre);
-  for (int qt = 0; qt < nqt; ++qt) {
-    const int i0 = qt * BQ;
-    __syncthreads();  // previous tile's readers of the shared images / exchange are done
-    {  // stage the Q + u, Q + v, dO images; D_i = dO_i . O_i (8 threads per row), lse_i
-      const bool ok = i0 + prow < a.T1;
-      union { uint4 u; bf16 e[8]; } x, y, qu, qv;
-      x.u = pre.q;
-      qu.u = qv.u = make_uint4(0u, 0u, 0u, 0u);
-      if (ok) {
-#pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          qu.e[e] = a.bu ? (bf16)((float)x.e[e] + bias_s[pch * 8 + e]) : x.e[e];
-          if (REL) qv.e[e] = (bf16)((float)x.e[e] + bias_s[DK + pch * 8 + e]);
-        }
-      }
-      *(uint4*)(quimg + km_off(prow, pch)) = qu.u;
-      if (REL) *(uint4*)(qvimg + km_off(prow, pch)) = qv.u;
-      *(uint4*)(doimg + km_off(prow, pch)) = pre.dO;
-      x.u = pre.dO;
-      y.u = pre.o;
-      float d = 0.f;
-#pragma unroll
-      for (int e = 0; e < 8; ++e) d += (float)x.e[e] * (float)y.e[e];
-#pragma unroll
-      for (int o = 1; o < 8; o <<= 1) d += __shfl_xor(d, o, 64);
-      if (pch == 0) {
-        Dv[prow] = d;
-        Lv[prow] = pre.lse;
+    for (int ks = 0; ks < 2; ++ks) {
+      kf[ks] = vf[ks] = (bf16x8){};
+      if (j < kl) {
+        kf[ks] = *(const bf16x8*)(a.k + ((long)b * a.T2 + j) * a.ldk + h * DK + 32 * ks + 8 * g);
+        vf[ks] = *(const bf16x8*)(a.v + ((long)b * a.T2 + j) * a.ldv + h * DK + 32 * ks + 8 * g);
       }
     }
-    __syncthreads();
-    if (qt + 1 < nqt) fetch(i0 + BQ, pre);
-    if (tile_on(i0)) {
-      // band fragments issued before the AC MFMAs so their latency hides under them
-      bf16x8 pfc[6][2];
-      if (REL) fetch_band(i0, pfc);
-      // scores (32 queries x 64 keys): s[mi][t], lane = key column 16t + lc, rows 16mi + 4g + r
-      f32x4 s[2][4];
+    const bf16* qsrc = a.q + (long)b * a.T1 * a.ldq + h * DK;
+    const bf16* dosrc = a.dO + (long)b * a.T1 * a.lddo + h * DK;
+    const bf16* osrc = a.o + (long)b * a.T1 * a.ldo + h * DK;
+    const int prow = tid >> 3, pch = tid & 7;
+    float bu8[8], bv8[8];  // this thread's 8 bias columns
 #pragma unroll
-      for (int mi = 0; mi < 2; ++mi)
-#pragma unroll
-        for (int t = 0; t < 4; ++t) {
-          s[mi][t] = (f32x4){0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-          for (int ks = 0; ks < 2; ++ks)
-            s[mi][t] = mfma(km_frag(quimg, 16 * mi, ks, lane), km_frag(kimg, 16 * t, ks, lane), s[mi][t]);
-        }
+    for (int e = 0; e < 8; ++e) {
+      bu8[e] = a.bu ? a.bu[h * DK + pch * 8 + e] : 0.f;
+      bv8[e] = REL ? a.bv[h * DK + pch * 8 + e] : 0.f;
+    }
+    const bool use_mask = a.p > 0.f && a.dmask != nullptr;
+    const float dsc = a.p > 0.f ? 1.f / (1.f - a.p) : 1.f;
+    const float sl2 = a.scale * LOG2E;
+    // thread tid owns row tid>>3, chunk tid&7 of the Q / dO / O tiles, band pieces tid + 256u
+    // (u < 3) of the 96 x 8 band image and (tid < 64) keep word tid>>5 of row tid&31
+    struct Pre { uint4 q, dO, o, p[3]; float lse; uint32_t mw; };
+    auto fetch = [&](int i0n, Pre& pr) {
+      const int i = i0n + prow;
+      pr.q = pr.dO = pr.o = make_uint4(0u, 0u, 0u, 0u);
+      pr.lse = INFINITY;
+      if (i < a.T1) {
+        pr.q = *(const uint4*)(qsrc + (long)i * a.ldq + pch * 8);
+        pr.dO = *(const uint4*)(dosrc + (long)i * a.lddo + pch * 8);
+        pr.o = *(const uint4*)(osrc + (long)i * a.ldo + pch * 8);
+        pr.lse = a.lse[(long)z * a.T1 + i];
+      }
+      if (use_mask && tid < 64) {
+        const int im = min(i0n + (tid & 31), a.T1 - 1);
+        pr.mw = a.dmask[((long)z * a.T1 + im) * a.ldm + (j0 >> 5) + (tid >> 5)];
+      }
       if (REL) {
-        // BDfull (32 x 96): band rows rs + [0, 96), B fragments prefetched into pfc
-        bf16x8 bq[2][2];
+        const int rs = a.T1 - 1 - (i0n + BQ - 1) + j0;
+#pragma unroll
+        for (int u = 0; u < 3; ++u) {
+          const int pc = tid + 256 * u, r = rs + (pc >> 3);
+          pr.p[u] = make_uint4(0u, 0u, 0u, 0u);
+          if (r >= 0 && r < 2 * a.T1 - 1) pr.p[u] = *(const uint4*)(a.pp + (long)r * a.ldp + h * DK + (pc & 7) * 8);
+        }
+      }
+    };
+    // queries before the key block see none of its keys under the causal mask
+    const int istart = a.causal ? (j0 / BQ) * BQ : 0;
+    const int imin = a.causal ? j : 0;  // rows i in [imin, T1) see key j (if j < kl)
+    const int bpos = 16 * (w & 1) + lc;  // this lane's bit in keep word w>>1
+    Pre pre;
+    fetch(istart, pre);
+    for (int i0 = istart; i0 < a.T1; i0 += BQ) {
+      __syncthreads();  // previous tile's readers of the images / BDfull are done
+      {
+        const bool ok = i0 + prow < a.T1;
+        union { uint4 u; bf16 e[8]; } x, y, qu, qv;
+        x.u = pre.q;
+        qu.u = qv.u = make_uint4(0u, 0u, 0u, 0u);
+        if (ok) {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            const float xf = (float)x.e[e];
+            qu.e[e] = (bf16)(xf + bu8[e]);
+            if (REL) qv.e[e] = (bf16)(xf + bv8[e]);
+          }
+        }
+        *(uint4*)(quimg + km_off(prow, pch)) = qu.u;
+        if (REL) *(uint4*)(qvimg + km_off(prow, pch)) = qv.u;
+        *(uint4*)(doimg + km_off(prow, pch)) = pre.dO;
+        if (REL) {
+#pragma unroll
+          for (int u = 0; u < 3; ++u) {
+            const int pc = tid + 256 * u;
+            *(uint4*)(pimg + km_off(pc >> 3, pc & 7)) = pre.p[u];
+          }
+        }
+        if (use_mask && tid < 64) Mw[(tid >> 5) * BQ + (tid & 31)] = pre.mw;
+        x.u = pre.dO;
+        y.u = pre.o;
+        float d = 0.f;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) d += (float)x.e[e] * (float)y.e[e];
+#pragma unroll
+        for (int o = 1; o < 8; o <<= 1) d += __shfl_xor(d, o, 64);
+        if (pch == 0) {
+          Dv[prow] = d;
+          Lv[prow] = pre.lse * LOG2E;
+        }
+      }
+      __syncthreads();
+      if (i0 + BQ < a.T1) fetch(i0 + BQ, pre);
+      // S (32 queries x this wave's 16 keys): s[mi] rows 16mi + 4g + r, key column jw + lc
+      f32x4 s[2], dp[2];
+#pragma unroll
+      for (int mi = 0; mi < 2; ++mi) {
+        s[mi] = (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) s[mi] = mfma(km_frag(quimg, 16 * mi, ks, lane), kf[ks], s[mi]);
+      }
+      if (REL) {
+        // BDfull (32 x 96) over band rows rs + [0, 96): the 12 (mi, t) tiles split over the waves
+#pragma unroll
+        for (int u = 0; u < 3; ++u) {
+          const int idx = w + 4 * u, mi = idx / 6, t = idx % 6;
+          f32x4 bd = (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+          for (int ks = 0; ks < 2; ++ks) bd = mfma(km_frag(qvimg, 16 * mi, ks, lane), km_frag(pimg, 16 * t, ks, lane), bd);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) xs[(16 * mi + 4 * g + r) * V_XLD + 16 * t + lc] = bd[r];
+        }
+        __syncthreads();
 #pragma unroll
         for (int mi = 0; mi < 2; ++mi)
 #pragma unroll
-          for (int ks = 0; ks < 2; ++ks) bq[mi][ks] = km_frag(qvimg, 16 * mi, ks, lane);
-#pragma unroll
-        for (int t = 0; t < 6; ++t) {
-#pragma unroll
-          for (int mi = 0; mi < 2; ++mi) {
-            f32x4 bd = (f32x4){0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-            for (int ks = 0; ks < 2; ++ks) bd = mfma(bq[mi][ks], pfc[t][ks], bd);
-#pragma unroll
-            for (int r2 = 0; r2 < 4; ++r2) xs[(16 * mi + 4 * g + r2) * B_BDLD + 16 * t + lc] = bd[r2];
+          for (int r = 0; r < 4; ++r) {
+            const int il = 16 * mi + 4 * g + r, jl = 16 * w + lc;
+            s[mi][r] += xs[il * V_XLD + (BQ - 1 - il) + jl];
           }
-        }
-        lds_fence();
-#pragma unroll
-        for (int mi = 0; mi < 2; ++mi)
-#pragma unroll
-          for (int t = 0; t < 4; ++t)
-#pragma unroll
-            for (int r2 = 0; r2 < 4; ++r2) {
-              const int il = 16 * mi + 4 * g + r2, jl = 16 * t + lc;
-              s[mi][t][r2] += xs[il * B_BDLD + (BQ - 1 - il) + jl];
-            }
-        lds_fence();
       }
-      // dPd = dO . V_w^T
-      f32x4 dp[2][4];
 #pragma unroll
-      for (int mi = 0; mi < 2; ++mi)
+      for (int mi = 0; mi < 2; ++mi) {
+        dp[mi] = (f32x4){0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-        for (int t = 0; t < 4; ++t) {
-          dp[mi][t] = (f32x4){0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-          for (int ks = 0; ks < 2; ++ks)
-            dp[mi][t] = mfma(km_frag(doimg, 16 * mi, ks, lane), km_frag(vimg, 16 * t, ks, lane), dp[mi][t]);
-        }
-      // P, Pd, dS (scaled): in place of s (-> dS) and dp (-> Pd)
-#pragma unroll
-      for (int mi = 0; mi < 2; ++mi)
-#pragma unroll
-        for (int r2 = 0; r2 < 4; ++r2) {
-          const int il = 16 * mi + 4 * g + r2, i = i0 + il;
-          const float L = Lv[il], D = Dv[il];
-#pragma unroll
-          for (int t = 0; t < 4; ++t) {
-            const int j = jw + 16 * t + lc;
-            const bool ok = i < a.T1 && j < kl && (!a.causal || j <= i);
-            const float P = ok ? __expf(s[mi][t][r2] * a.scale - L) : 0.f;
-            float keep = 1.f;
-            if (a.p > 0.f) keep = drop_scale(seed, ((uint64_t)z * a.T1 + i) * a.T2 + j, a.p);
-            const float dP = dp[mi][t][r2] * keep;
-            s[mi][t][r2] = P * (dP - D) * a.scale;  // d(raw score AC+BD)
-            dp[mi][t][r2] = P * keep;               // Pd
-          }
-        }
-      // dV_w += Pd^T dO, dK_w += dS^T Qu: A = the C-layout tile read as (key, 8 queries
-      // {4g..4g+3, 16+4g..16+4g+3}); B = dO / Qu rows in the same order (transposed reads)
-#pragma unroll
-      for (int t = 0; t < 4; ++t) {
-        union { bf16x8 v; bf16 e[8]; } ap, as;
-#pragma unroll
-        for (int r2 = 0; r2 < 4; ++r2) {
-          ap.e[r2] = (bf16)dp[0][t][r2];
-          ap.e[4 + r2] = (bf16)dp[1][t][r2];
-          as.e[r2] = (bf16)s[0][t][r2];
-          as.e[4 + r2] = (bf16)s[1][t][r2];
-        }
-#pragma unroll
-        for (int n = 0; n < 4; ++n) {
-          dva[t][n] = mfma(ap.v, km_frag_tr2(doimg, 4 * g, 16 + 4 * g, 16 * n, lane), dva[t][n]);
-          dka[t][n] = mfma(as.v, km_frag_tr2(quimg, 4 * g, 16 + 4 * g, 16 * n, lane), dka[t][n]);
-        }
+        for (int ks = 0; ks < 2; ++ks) dp[mi] = mfma(km_frag(doimg, 16 * mi, ks, lane), vf[ks], dp[mi]);
       }
-      // dS (bf16) image [32 queries][64 keys] -> dQ partial = dS . K_w
-#pragma unroll
-      for (int mi = 0; mi < 2; ++mi)
-#pragma unroll
-        for (int t = 0; t < 4; ++t)
-#pragma unroll
-          for (int r2 = 0; r2 < 4; ++r2) {
-            const int il = 16 * mi + 4 * g + r2, jl = 16 * t + lc;
-            *(bf16*)(dsimg + km_off(il, jl >> 3) + (jl & 7) * 2) = (bf16)s[mi][t][r2];
-          }
-      lds_fence();
-#pragma unroll
-      for (int n = 0; n < 4; ++n) {
-        const bf16x8 kb0 = km_frag_tr(kimg, 0, 16 * n, lane), kb1 = km_frag_tr(kimg, 32, 16 * n, lane);
+      // keep words of rows 16mi + 4g + r (this lane's bit bpos): staged mask, else rebuilt from
+      // the counter hash, else all kept
+      uint32_t mr[2][4];
+      if (use_mask) {
 #pragma unroll
         for (int mi = 0; mi < 2; ++mi) {
-          f32x4 dq = (f32x4){0.f, 0.f, 0.f, 0.f};
-          dq = mfma(km_frag(dsimg, 16 * mi, 0, lane), kb0, dq);
-          dq = mfma(km_frag(dsimg, 16 * mi, 1, lane), kb1, dq);
-#pragma unroll
-          for (int r2 = 0; r2 < 4; ++r2) xs[(16 * mi + 4 * g + r2) * 64 + 16 * n + lc] = dq[r2];
+          const uint4 m4 = *(const uint4*)(Mw + (w >> 1) * BQ + 16 * mi + 4 * g);
+          mr[mi][0] = m4.x; mr[mi][1] = m4.y; mr[mi][2] = m4.z; mr[mi][3] = m4.w;
         }
-      }
-      // rel-pos band gradient dBD_raw[h][b][i][T-1-i+j] = dS
-      if (REL) {
+      } else if (a.p > 0.f) {
+        const uint32_t key = ea_seed_key(seed), thr = ea_drop_thr(a.p);
 #pragma unroll
         for (int mi = 0; mi < 2; ++mi)
 #pragma unroll
-          for (int r2 = 0; r2 < 4; ++r2) {
-            const int i = i0 + 16 * mi + 4 * g + r2;
-            if (i >= a.T1) continue;
-            bf16* drow = a.dbd + (((long)h * a.B + b) * a.T1 + i) * a.lddbd + (a.T1 - 1 - i);
-#pragma unroll
-            for (int t = 0; t < 4; ++t) {
-              const int j = jw + 16 * t + lc;
-              if (j < kl) drow[j] = (bf16)s[mi][t][r2];
-            }
+          for (int r = 0; r < 4; ++r) {
+            const int i = i0 + 16 * mi + 4 * g + r;
+            mr[mi][r] = (uint32_t)keep_hash(key, thr, ((uint64_t)z * a.T1 + i) * a.T2 + j) << bpos;
           }
+      } else {
+#pragma unroll
+        for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) mr[mi][r] = ~0u;
       }
-    } else {
-      for (int e = lane; e < BQ * 64; e += 64) xs[e] = 0.f;
-    }
-    __syncthreads();
-    // dQ = sum over the waves' partials in fixed order
-    for (int e = tid; e < BQ * 64; e += 256) {
-      const int il = e >> 6, c = e & 63;
-      const int i = i0 + il;
-      float acc = 0.f;
+      union { bf16x8 v; bf16 e[8]; } ap, as;
 #pragma unroll
-      for (int v = 0; v < NWAVE; ++v) acc += ((const float*)(sm + B_WS + v * B_WSZ))[e];
-      if (i < a.T1) a.dq[((long)b * a.T1 + i) * a.lddq + h * DK + c] = (bf16)acc;
-    }
-  }
-  // dK_w, dV_w: rows = keys jw + 16t + 4g + r, columns 16n + lc
+      for (int mi = 0; mi < 2; ++mi) {
+        const float4 D4 = *(const float4*)(Dv + 16 * mi + 4 * g);
+        const float4 L4 = *(const float4*)(Lv + 16 * mi + 4 * g);
+        const float Dm[4] = {D4.x, D4.y, D4.z, D4.w}, Lm[4] = {L4.x, L4.y, L4.z, L4.w};
 #pragma unroll
-  for (int t = 0; t < 4; ++t)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int j = jw + 16 * t + 4 * g + r;
-      if (j >= a.T2) continue;
-      bf16* dkr = a.dk + ((long)b * a.T2 + j) * a.lddk + h * DK;
-      bf16* dvr = a.dv + ((long)b * a.T2 + j) * a.lddv + h * DK;
-      const bool ok = j < kl;
+        for (int r = 0; r < 4; ++r) {
+          const int i = i0 + 16 * mi + 4 * g + r;
+          const bool ok = j < kl && (unsigned)(i - imin) < (unsigned)(a.T1 - imin);
+          const float e = __builtin_amdgcn_exp2f(fmaf(s[mi][r], sl2, -Lm[r]));
+          const float P = ok ? e : 0.f;
+          const float kp = ((mr[mi][r] >> bpos) & 1u) ? dsc : 0.f;
+          as.e[4 * mi + r] = (bf16)((P * a.scale) * fmaf(dp[mi][r], kp, -Dm[r]));
+          ap.e[4 * mi + r] = (bf16)(P * kp);
+        }
+      }
+      // dV += Pd^T dO, dK += dS^T (Q+u): A = (key, 8 queries {4g..4g+3, 16+4g..16+4g+3}),
+      // B = dO / Q+u rows in the same order (transposed reads)
 #pragma unroll
       for (int n = 0; n < 4; ++n) {
-        dkr[16 * n + lc] = (bf16)(ok ? dka[t][n][r] : 0.f);
-        dvr[16 * n + lc] = (bf16)(ok ? dva[t][n][r] : 0.f);
+        dva[n] = mfma(ap.v, km_frag_tr2(doimg, 4 * g, 16 + 4 * g, 16 * n, lane), dva[n]);
+        dka[n] = mfma(as.v, km_frag_tr2(quimg, 4 * g, 16 + 4 * g, 16 * n, lane), dka[n]);
       }
     }
+  }
+  // dK, dV rows jw + 4g + r (zero for keys at or past klen)
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int j = jw + 4 * g + r;
+    if (j >= a.T2) continue;
+    bf16* dkr = a.dk + ((long)b * a.T2 + j) * a.lddk + h * DK;
+    bf16* dvr = a.dv + ((long)b * a.T2 + j) * a.lddv + h * DK;
+    const bool ok = j < kl;
+#pragma unroll
+    for (int n = 0; n < 4; ++n) {
+      dkr[16 * n + lc] = (bf16)(ok ? dka[n][r] : 0.f);
+      dvr[16 * n + lc] = (bf16)(ok ? dva[n][r] : 0.f);
+    }
+  }
 }
 
 AttnP make_p(int B, int H, int T1, int T2, const void* q, long ldq, const void* k, long ldk, const void* v, long ldv,
@@ -568,21 +868,73 @@ AttnP make_p(int B, int H, int T1, int T2, const void* q, long ldq, const void* 
 
 }  // namespace
 
-extern "C" int ea_attn_fused_fwd(int B, int H, int T1, int T2, int dk, const void* q, long ldq, const void* k,
-                                 long ldk, const void* v, long ldv, const float* bu, const float* bv,
-                                 const void* pp, long ldp, const long long* klen, int causal, float scale, float p,
-                                 unsigned long long seed, void* o, long ldo, float* lse, void* stream) {
+extern "C" int ea_attn_fused_fwd2(int B, int H, int T1, int T2, int dk, const void* q, long ldq, const void* k,
+                                  long ldk, const void* v, long ldv, const float* bu, const float* bv,
+                                  const void* pp, long ldp, const long long* klen, int causal, float scale, float p,
+                                  unsigned long long seed, void* o, long ldo, float* lse, unsigned* dmask, int ldm,
+                                  void* stream) {
   EA_ENTRY();
   EA_CHECK_ARG(dk == DK && B >= 1 && H >= 1 && T1 >= 1 && T2 >= 1);
   EA_CHECK_ARG(!pp || (T1 == T2 && bv != nullptr));
   EA_CHECK_ARG(ldq % 8 == 0 && ldk % 8 == 0 && ldv % 8 == 0 && (!pp || ldp % 8 == 0));
+  EA_CHECK_ARG(!dmask || ldm >= 2 * ((T2 + 63) / 64));
   AttnP a = make_p(B, H, T1, T2, q, ldq, k, ldk, v, ldv, bu, bv, pp, ldp, klen, causal, scale, p, seed);
   a.o = (bf16*)o; a.ldo = ldo; a.lse = lse;
+  a.dmask = (uint32_t*)dmask; a.ldm = ldm;
   dim3 grid(B * H * ((T1 + QB - 1) / QB));
   if (pp) hipLaunchKernelGGL(attn_fwd_kernel<true>, grid, dim3(256), 0, (hipStream_t)stream, a);
   else hipLaunchKernelGGL(attn_fwd_kernel<false>, grid, dim3(256), 0, (hipStream_t)stream, a);
   EA_LAUNCH_CHECK();
   return 0;
+}
+
+extern "C" int ea_attn_fused_fwd(int B, int H, int T1, int T2, int dk, const void* q, long ldq, const void* k,
+                                 long ldk, const void* v, long ldv, const float* bu, const float* bv,
+                                 const void* pp, long ldp, const long long* klen, int causal, float scale, float p,
+                                 unsigned long long seed, void* o, long ldo, float* lse, void* stream) {
+  return ea_attn_fused_fwd2(B, H, T1, T2, dk, q, ldq, k, ldk, v, ldv, bu, bv, pp, ldp, klen, causal, scale, p, seed,
+                            o, ldo, lse, nullptr, 0, stream);
+}
+
+static int attn_bwd_launch(AttnP& a, bool rel, hipStream_t st) {
+  const int nqb = (a.T1 + QB - 1) / QB, nkb = (a.T2 + 63) / 64;
+  const dim3 gq(a.B * a.H * nqb), gkv(a.B * a.H * nkb);
+  if (rel) {
+    hipLaunchKernelGGL(attn_bwdq_kernel<true>, gq, dim3(256), 0, st, a);
+    hipLaunchKernelGGL(attn_bwdkv_kernel<true>, gkv, dim3(256), 0, st, a);
+  } else {
+    hipLaunchKernelGGL(attn_bwdq_kernel<false>, gq, dim3(256), 0, st, a);
+    hipLaunchKernelGGL(attn_bwdkv_kernel<false>, gkv, dim3(256), 0, st, a);
+  }
+  EA_LAUNCH_CHECK();
+  return 0;
+}
+
+extern "C" int ea_attn_fused_bwd2(int B, int H, int T1, int T2, int dk, const void* q, long ldq, const void* k,
+                                  long ldk, const void* v, long ldv, const float* bu, const float* bv,
+                                  const void* pp, long ldp, const long long* klen, int causal, float scale, float p,
+                                  unsigned long long seed, const void* o, long ldo, const float* lse, const void* dO,
+                                  long lddo, void* dq, long lddq, void* dkout, long lddk, void* dvout, long lddv,
+                                  void* dbd, long lddbd, float* bias_part, long ldpart, void* qv_out, long ldqv,
+                                  const unsigned* dmask, int ldm, int flags, void* stream) {
+  EA_ENTRY();
+  EA_CHECK_ARG(dk == DK && B >= 1 && H >= 1 && T1 >= 1 && T2 >= 1);
+  EA_CHECK_ARG(!pp || (T1 == T2 && bv != nullptr && (dbd == nullptr || lddbd >= 2 * T1 - 1)));
+  EA_CHECK_ARG(ldq % 8 == 0 && ldk % 8 == 0 && ldv % 8 == 0 && ldo % 8 == 0 && lddo % 8 == 0 &&
+               (!pp || ldp % 8 == 0) && (!qv_out || (pp && ldqv % 8 == 0)));
+  EA_CHECK_ARG(!bias_part || ldpart >= (long)H * DK);
+  EA_CHECK_ARG(flags == 0 || (flags == 1 && pp));
+  EA_CHECK_ARG(!dmask || ldm >= 2 * ((T2 + 63) / 64));
+  AttnP a = make_p(B, H, T1, T2, q, ldq, k, ldk, v, ldv, bu, bv, pp, ldp, klen, causal, scale, p, seed);
+  a.o = (bf16*)o; a.ldo = ldo; a.lse = (float*)lse;
+  a.dO = (const bf16*)dO; a.lddo = lddo;
+  a.dq = (bf16*)dq; a.lddq = lddq; a.dk = (bf16*)dkout; a.lddk = lddk; a.dv = (bf16*)dvout; a.lddv = lddv;
+  a.dbd = (bf16*)dbd; a.lddbd = lddbd;
+  a.bias_part = bias_part; a.ldpart = ldpart;
+  a.qv_out = (bf16*)qv_out; a.ldqv = ldqv;
+  a.flags = flags;
+  a.dmask = (uint32_t*)dmask; a.ldm = ldm;
+  return attn_bwd_launch(a, pp != nullptr, (hipStream_t)stream);
 }
 
 extern "C" int ea_attn_fused_bwd(int B, int H, int T1, int T2, int dk, const void* q, long ldq, const void* k,
@@ -591,18 +943,8 @@ extern "C" int ea_attn_fused_bwd(int B, int H, int T1, int T2, int dk, const voi
                                  unsigned long long seed, const void* o, long ldo, const float* lse, const void* dO,
                                  long lddo, void* dq, long lddq, void* dkout, long lddk, void* dvout, long lddv,
                                  void* dbd, long lddbd, void* stream) {
-  EA_ENTRY();
-  EA_CHECK_ARG(dk == DK && B >= 1 && H >= 1 && T1 >= 1 && T2 >= 1 && T2 <= NWAVE * 64);
-  EA_CHECK_ARG(!pp || (T1 == T2 && bv != nullptr && dbd != nullptr && lddbd >= 2 * T1 - 1));
-  EA_CHECK_ARG(ldq % 8 == 0 && ldk % 8 == 0 && ldv % 8 == 0 && ldo % 8 == 0 && lddo % 8 == 0);
-  AttnP a = make_p(B, H, T1, T2, q, ldq, k, ldk, v, ldv, bu, bv, pp, ldp, klen, causal, scale, p, seed);
-  a.o = (bf16*)o; a.ldo = ldo; a.lse = (float*)lse;
-  a.dO = (const bf16*)dO; a.lddo = lddo;
-  a.dq = (bf16*)dq; a.lddq = lddq; a.dk = (bf16*)dkout; a.lddk = lddk; a.dv = (bf16*)dvout; a.lddv = lddv;
-  a.dbd = (bf16*)dbd; a.lddbd = lddbd;
-  dim3 grid(B * H);
-  if (pp) hipLaunchKernelGGL(attn_bwd_kernel<true>, grid, dim3(256), 0, (hipStream_t)stream, a);
-  else hipLaunchKernelGGL(attn_bwd_kernel<false>, grid, dim3(256), 0, (hipStream_t)stream, a);
-  EA_LAUNCH_CHECK();
-  return 0;
+  EA_CHECK_ARG(!pp || dbd != nullptr);
+  return ea_attn_fused_bwd2(B, H, T1, T2, dk, q, ldq, k, ldk, v, ldv, bu, bv, pp, ldp, klen, causal, scale, p, seed,
+                            o, ldo, lse, dO, lddo, dq, lddq, dkout, lddk, dvout, lddv, dbd, lddbd, nullptr, 0,
+                            nullptr, 0, nullptr, 0, 0, stream);
 }

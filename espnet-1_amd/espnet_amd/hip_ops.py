@@ -482,6 +482,15 @@ def layernorm_bwd(dy, x, gamma, mean, rstd, dx, dgamma, dbeta, accumulate=True):
                          dgamma.data_ptr(), dbeta.data_ptr(), 1, w, n, stream())
 
 
+def reduce_rows(part, nparts, n, stride, out, accumulate=True):
+    """out[c] (+)= sum_p part[p*stride + c], p in fixed order (deterministic); deferred with the
+    pass's other parameter-gradient reductions while the reduction queue is active."""
+    if REDUCE_Q.active:
+        REDUCE_Q.add_reduce(part, nparts, n, stride, out, accumulate)
+        return
+    lib.ea_reduce_partials(nparts, n, part.data_ptr(), stride, out.data_ptr(), int(accumulate), stream())
+
+
 def colsum(x, out, accumulate=True, defer=True):
     """out (+)= column sums of x.  While the reduction queue is active the sum is deferred to
     REDUCE_Q.flush(): pass defer=False when x is modified in place before the pass ends."""

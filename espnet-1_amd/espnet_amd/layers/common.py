@@ -18,7 +18,7 @@ from .._lib import (ACT_NONE, ACT_RELU, ACT_SWISH, EPI_ACT, EPI_DACT, EPI_RESID,
 
 __all__ = ["Bound", "rup", "empty", "ops", "lib", "EPI_ACT", "EPI_DACT", "EPI_RESID",
            "EPI_STORE", "ACT_NONE", "ACT_RELU", "ACT_SWISH", "site_seed", "attn_fwd", "attn_bwd",
-           "LayerNormFn", "ln_fwd", "ln_bwd", "math", "F32", "fused_attn_ok"]
+           "LayerNormFn", "ln_fwd", "ln_bwd", "math", "F32", "fused_attn_ok", "attn_dmask", "ptr"]
 
 F32 = torch.float32
 
@@ -37,9 +37,22 @@ FUSED_ATTN = os.environ.get("EA_FUSED_ATTN", "1") != "0"
 
 
 def fused_attn_ok(cd, dk, T1, T2) -> bool:
-    """The fused attention kernels (relattn.hip) take bf16 operands, head dim 64 and (for the
-    backward's key-per-wave split) at most 256 keys; other cases use the unfused path."""
-    return FUSED_ATTN and cd == torch.bfloat16 and dk == 64 and T2 <= 256 and T1 >= 1
+    """The fused attention kernels (relattn.hip) take bf16 operands and head dim 64 (any
+    lengths); other cases use the unfused path."""
+    return FUSED_ATTN and cd == torch.bfloat16 and dk == 64 and T1 >= 1 and T2 >= 1
+
+
+def ptr(t) -> int:
+    return 0 if t is None else t.data_ptr()
+
+
+def attn_dmask(rows, T2, p, device):
+    """Dropout keep-bit buffer of the fused attention (ea_attn_fused_fwd2 writes it, the
+    backward reads it instead of rehashing): rows x ldm uint32 words, or (None, 0) when p == 0."""
+    if p <= 0:
+        return None, 0
+    ldm = 2 * ((T2 + 63) // 64)
+    return torch.empty(rows * ldm, dtype=torch.int32, device=device), ldm
 
 
 def site_seed(base: int, layer: int, site: int) -> int:

@@ -15,8 +15,8 @@ from __future__ import annotations
 import torch
 from torch import nn
 
-from .common import (ACT_SWISH, EPI_ACT, EPI_DACT, EPI_RESID, EPI_STORE, F32, Bound, attn_bwd, fused_attn_ok,
-                     attn_fwd, empty, lib, ln_bwd, ln_fwd, math, ops, rup, site_seed)
+from .common import (ACT_SWISH, EPI_ACT, EPI_DACT, EPI_RESID, EPI_STORE, F32, Bound, attn_bwd, attn_dmask, fused_attn_ok,
+                     attn_fwd, empty, lib, ln_bwd, ln_fwd, math, ops, ptr, rup, site_seed)
 
 
 # ----------------------------------------------------------------------------- holders
@@ -191,12 +191,14 @@ class ConformerBlockFn(torch.autograd.Function):
             # one kernel: (q+u)k^T + rel_shift((q+v)p^T), mask, softmax, dropout, @v
             O = empty(N, d, dtype=cd, device=dev)
             lse = empty(B * H * T, device=dev)
-            lib.ea_attn_fused_fwd(B, H, T, T, dk, qkv.data_ptr(), 3 * d, qkv[:, d:].data_ptr(), 3 * d,
-                                  qkv[:, 2 * d:].data_ptr(), 3 * d, b.f(A + "pos_bias_u").data_ptr(),
-                                  b.f(A + "pos_bias_v").data_ptr(), pp.data_ptr(), d, olens.data_ptr(), 0,
-                                  scale, float(pa), sd(3), O.data_ptr(), d, lse.data_ptr(), ops.stream())
+            dmask, ldm = attn_dmask(B * H * T, T, pa, dev)
+            lib.ea_attn_fused_fwd2(B, H, T, T, dk, qkv.data_ptr(), 3 * d, qkv[:, d:].data_ptr(), 3 * d,
+                                   qkv[:, 2 * d:].data_ptr(), 3 * d, b.f(A + "pos_bias_u").data_ptr(),
+                                   b.f(A + "pos_bias_v").data_ptr(), pp.data_ptr(), d, olens.data_ptr(), 0,
+                                   scale, float(pa), sd(3), O.data_ptr(), d, lse.data_ptr(), ptr(dmask), ldm,
+                                   ops.stream())
             ldT = 0
-            s_core = ("fused", lse)
+            s_core = ("fused", lse, dmask, ldm)
         else:
             qu = empty(N, d, dtype=cd, device=dev)
             qv = empty(N, d, dtype=cd, device=dev)
@@ -303,18 +305,22 @@ class ConformerBlockFn(torch.autograd.Function):
         dqkv = empty(N, 3 * d, dtype=cd, device=dev)
         ldbd = rup(P2, 8)
         if s_core[0] == "fused":
-            lse = s_core[1]
-            dbd = torch.zeros(H * B * T * ldbd, dtype=cd, device=dev)
-            lib.ea_attn_fused_bwd(B, H, T, T, dk, qkv.data_ptr(), 3 * d, qkv[:, d:].data_ptr(), 3 * d,
-                                  qkv[:, 2 * d:].data_ptr(), 3 * d, b.f(A + "pos_bias_u").data_ptr(),
-                                  b.f(A + "pos_bias_v").data_ptr(), pp.data_ptr(), d, olens.data_ptr(), 0,
-                                  scale, float(pa), sd(3), O.data_ptr(), d, lse.data_ptr(), dO.data_ptr(), d,
-                                  dqkv.data_ptr(), 3 * d, dqkv[:, d:].data_ptr(), 3 * d, dqkv[:, 2 * d:].data_ptr(),
-                                  3 * d, dbd.data_ptr(), ldbd, ops.stream())
+            # dq includes the q+v path (dBD.p, in-kernel); dbd rows written in full; pos_bias_u /
+            # pos_bias_v gradients from per-block column sums of the two dq terms
+            _, lse, dmask, ldm = s_core
+            dbd = empty(H * B * T * ldbd, dtype=cd, device=dev)
             qv = empty(N, d, dtype=cd, device=dev)  # q + v, for the linear_pos weight gradient
-            lib.ea_add_pos_bias(N, H, dk, qkv.data_ptr(), 3 * d, b.f(A + "pos_bias_v").data_ptr(),
-                                b.f(A + "pos_bias_v").data_ptr(), qv.data_ptr(), qv.data_ptr(),
-                                ops.dt(qv), ops.stream())
+            nqb = (T + 63) // 64
+            part = empty(2 * B * nqb * d, device=dev)
+            lib.ea_attn_fused_bwd2(B, H, T, T, dk, qkv.data_ptr(), 3 * d, qkv[:, d:].data_ptr(), 3 * d,
+                                   qkv[:, 2 * d:].data_ptr(), 3 * d, b.f(A + "pos_bias_u").data_ptr(),
+                                   b.f(A + "pos_bias_v").data_ptr(), pp.data_ptr(), d, olens.data_ptr(), 0,
+                                   scale, float(pa), sd(3), O.data_ptr(), d, lse.data_ptr(), dO.data_ptr(), d,
+                                   dqkv.data_ptr(), 3 * d, dqkv[:, d:].data_ptr(), 3 * d,
+                                   dqkv[:, 2 * d:].data_ptr(), 3 * d, dbd.data_ptr(), ldbd, part.data_ptr(), d,
+                                   qv.data_ptr(), d, ptr(dmask), ldm, 1, ops.stream())
+            ops.reduce_rows(part[:B * nqb * d], B * nqb, d, d, b.g(A + "pos_bias_u", shape=(d,)))
+            ops.reduce_rows(part[B * nqb * d:], B * nqb, d, d, b.g(A + "pos_bias_v", shape=(d,)))
         else:
             _, qu, qv, P, Pd = s_core
             dbd = empty(H * B * T * ldbd, dtype=cd, device=dev)
@@ -322,15 +328,15 @@ class ConformerBlockFn(torch.autograd.Function):
                      ldq=d, ldk=3 * d, ldv=3 * d, scale=scale, p=pa, seed=sd(3), cd=cd,
                      dq=dqkv, lddq=3 * d, dk_=dqkv[:, d:], lddk=3 * d, dv=dqkv[:, 2 * d:], lddv=3 * d,
                      dbd=dbd, ldbd=ldbd)
-        # q_u = q + u: du = sum dq_u ; q_v = q + v path: dq_v = dBD . p_h, dv_bias = sum dq_v
-        dqv = empty(N, d, dtype=cd, device=dev)
-        ops.gemm(dbd, pp, dqv, M=T, N=dk, K=P2, a_kmajor=1, b_kmajor=0, lda=ldbd, ldb=d, ldc=d,
-                 batch=B, nh=H, sA=(T * ldbd, B * T * ldbd), sB=(0, dk), sC=(T * d, dk), splitk=False)
-        # not deferred: dqkv[:, :d] receives dqv in place right below
-        ops.colsum(dqkv[:, :d], b.g(A + "pos_bias_u", shape=(d,)), defer=False)
-        ops.colsum(dqv, b.g(A + "pos_bias_v", shape=(d,)))
-        lib.ea_add_2d(N, d, dqv.data_ptr(), ops.dt(dqv), d, dqkv.data_ptr(), ops.dt(dqkv), 3 * d, 1.0,
-                      ops.stream())
+            # q_u = q + u: du = sum dq_u ; q_v = q + v path: dq_v = dBD . p_h, dv_bias = sum dq_v
+            dqv = empty(N, d, dtype=cd, device=dev)
+            ops.gemm(dbd, pp, dqv, M=T, N=dk, K=P2, a_kmajor=1, b_kmajor=0, lda=ldbd, ldb=d, ldc=d,
+                     batch=B, nh=H, sA=(T * ldbd, B * T * ldbd), sB=(0, dk), sC=(T * d, dk), splitk=False)
+            # not deferred: dqkv[:, :d] receives dqv in place right below
+            ops.colsum(dqkv[:, :d], b.g(A + "pos_bias_u", shape=(d,)), defer=False)
+            ops.colsum(dqv, b.g(A + "pos_bias_v", shape=(d,)))
+            lib.ea_add_2d(N, d, dqv.data_ptr(), ops.dt(dqv), d, dqkv.data_ptr(), ops.dt(dqkv), 3 * d, 1.0,
+                          ops.stream())
         # linear_pos: dp[h] = sum_b dBD[h][b]^T qv[b, :, h]  (K = B*T), dWpos = dp^T pos
         with ops.wgrad(dbd, qv, pos):
             dpp = empty(P2, d, dtype=cd, device=dev)

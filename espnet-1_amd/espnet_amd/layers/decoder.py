@@ -16,7 +16,7 @@ import torch
 from torch import nn
 
 from .common import (ACT_RELU, EPI_ACT, EPI_DACT, EPI_RESID, EPI_STORE, F32, Bound, attn_bwd,
-                     attn_fwd, empty, fused_attn_ok, lib, ln_bwd, ln_fwd, ops, site_seed)
+                     attn_dmask, attn_fwd, empty, fused_attn_ok, lib, ln_bwd, ln_fwd, ops, ptr, site_seed)
 
 
 def _mha_fwd(q, k, v, *, B, H, T1, T2, dk, ldq, ldk, ldv, klen, causal, scale, p, seed, cd):
@@ -26,10 +26,11 @@ def _mha_fwd(q, k, v, *, B, H, T1, T2, dk, ldq, ldk, ldv, klen, causal, scale, p
     if fused_attn_ok(cd, dk, T1, T2):
         O = empty(B * T1, H * dk, dtype=cd, device=q.device)
         lse = empty(B * H * T1, device=q.device)
-        lib.ea_attn_fused_fwd(B, H, T1, T2, dk, q.data_ptr(), ldq, k.data_ptr(), ldk, v.data_ptr(), ldv,
-                              None, None, None, 0, klen.data_ptr(), int(causal), scale, float(p), seed,
-                              O.data_ptr(), H * dk, lse.data_ptr(), ops.stream())
-        return O, ("fused", O, lse)
+        dmask, ldm = attn_dmask(B * H * T1, T2, p, q.device)
+        lib.ea_attn_fused_fwd2(B, H, T1, T2, dk, q.data_ptr(), ldq, k.data_ptr(), ldk, v.data_ptr(), ldv,
+                               None, None, None, 0, klen.data_ptr(), int(causal), scale, float(p), seed,
+                               O.data_ptr(), H * dk, lse.data_ptr(), ptr(dmask), ldm, ops.stream())
+        return O, ("fused", O, lse, dmask, ldm)
     O, P, Pd, ldT = attn_fwd(q, k, v, B=B, H=H, T1=T1, T2=T2, dk=dk, ldq=ldq, ldk=ldk, ldv=ldv, klen=klen,
                              causal=causal, scale=scale, p=p, seed=seed, cd=cd)
     return O, ("unfused", P, Pd, ldT)
@@ -38,11 +39,12 @@ def _mha_fwd(q, k, v, *, B, H, T1, T2, dk, ldq, ldk, ldv, klen, causal, scale, p
 def _mha_bwd(st, dO, q, k, v, *, B, H, T1, T2, dk, ldq, ldk, ldv, klen, causal, scale, p, seed, cd,
              dq, lddq, dk_, lddk, dv, lddv):
     if st[0] == "fused":
-        _, O, lse = st
-        lib.ea_attn_fused_bwd(B, H, T1, T2, dk, q.data_ptr(), ldq, k.data_ptr(), ldk, v.data_ptr(), ldv,
-                              None, None, None, 0, klen.data_ptr(), int(causal), scale, float(p), seed,
-                              O.data_ptr(), H * dk, lse.data_ptr(), dO.data_ptr(), H * dk, dq.data_ptr(), lddq,
-                              dk_.data_ptr(), lddk, dv.data_ptr(), lddv, None, 0, ops.stream())
+        _, O, lse, dmask, ldm = st
+        lib.ea_attn_fused_bwd2(B, H, T1, T2, dk, q.data_ptr(), ldq, k.data_ptr(), ldk, v.data_ptr(), ldv,
+                               None, None, None, 0, klen.data_ptr(), int(causal), scale, float(p), seed,
+                               O.data_ptr(), H * dk, lse.data_ptr(), dO.data_ptr(), H * dk, dq.data_ptr(), lddq,
+                               dk_.data_ptr(), lddk, dv.data_ptr(), lddv, None, 0, None, 0, None, 0,
+                               ptr(dmask), ldm, 0, ops.stream())
         return
     _, P, Pd, ldT = st
     attn_bwd(dO, q, k, v, P, Pd, ldT, B=B, H=H, T1=T1, T2=T2, dk=dk, ldq=ldq, ldk=ldk, ldv=ldv, scale=scale,

@@ -24,7 +24,7 @@ lse = torch.empty(B * H * T, device=dev)
 dq, dk, dv = torch.empty_like(q), torch.empty_like(k), torch.empty_like(v)
 ldbd = (2 * T - 1 + 7) // 8 * 8
 dbd = torch.zeros(H * B * T * ldbd, dtype=bf, device=dev)
-scale, p, seed = 1.0 / math.sqrt(64), 0.1, 7
+scale, p, seed = 1.0 / math.sqrt(64), float(os.environ.get("ATTN_P", "0.1")), 7
 st = ops.stream()
 hs = torch.cuda.current_stream()  # ops.stream() launches on it
 

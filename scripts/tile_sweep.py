@@ -11,7 +11,7 @@ sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."
 import torch  # noqa: E402
 
 from espnet_amd import hip_ops as ops  # noqa: E402
-from espnet_amd._lib import ACT_RELU, ACT_SWISH, EPI_ACT, EPI_DACT, EPI_RESID, lib  # noqa: E402
+from espnet_amd._lib import GEMM_PIPE, ACT_RELU, ACT_SWISH, EPI_ACT, EPI_DACT, EPI_RESID, lib  # noqa: E402
 
 ROUNDS = int(sys.argv[1]) if len(sys.argv) > 1 else 3
 # M, N, K, a_k, b_k, epi, out dtype, calls per C3 step
@@ -31,8 +31,13 @@ SHAPES = [
     (1312, 512, 2048, 1, 0, None, torch.bfloat16, 6),
     (7968, 9728, 512, 1, 0, "dactrelu", torch.bfloat16, 1),
     (7968, 512, 9728, 1, 1, "resid", torch.float32, 1),
+    (1312, 512, 512, 1, 1, "resid", torch.float32, 12),
+    (1312, 2048, 512, 1, 1, "act", torch.bfloat16, 6),
+    (1312, 512, 2048, 1, 1, "resid", torch.float32, 6),
+    (497, 512, 512, 1, 1, None, torch.bfloat16, 12),
 ]
-TILES = [(64, 128, 0), (128, 128, 0), (256, 256, 0), (256, 256, 1), (0, 0, 1)]
+# (bm, bn, ea_gemm_set_pipe bits): 1 = 256x256 on gemm_pipe, 3 = 128x128 on gemm_pipe too
+TILES = [(64, 128, 1), (128, 128, 1), (128, 128, 3), (256, 256, 1), (0, 0, 1), (0, 0, 3)]
 
 
 def setup(M, N, K, a_k, b_k, epi, cdt):
@@ -82,7 +87,7 @@ for M, N, K, a_k, b_k, epi, cdt, calls in SHAPES:
             f()
             res[t].append(timed(f))
     lib.ea_gemm_set_tile(0, 0)
-    lib.ea_gemm_set_pipe(1)
+    lib.ea_gemm_set_pipe(GEMM_PIPE)
     med = {t: sorted(v)[len(v) // 2] for t, v in res.items() if v}
     best = min(med, key=med.get)
     for t in med:
@@ -91,8 +96,8 @@ for M, N, K, a_k, b_k, epi, cdt, calls in SHAPES:
     line = f"{M:6d} {N:5d} {K:5d} ({a_k},{b_k}) {str(epi):8s} x{calls:2d}:"
     for t in TILES:
         if t in med:
-            name = "auto" if t[0] == 0 else f"{t[0]}x{t[1]}{'p' if t[2] else ''}"
+            name = ("auto" if t[0] == 0 else f"{t[0]}x{t[1]}") + ("P" if t[2] == 3 else "")
             line += f"  {name} {med[t]:7.1f}"
     print(line + f"   best {best}", flush=True)
-print("per-step totals (ms):", {(f"{t[0]}x{t[1]}{'p' if t[2] else ''}" if t[0] else "auto"): round(v / 1e3, 3)
+print("per-step totals (ms):", {(("auto" if t[0] == 0 else f"{t[0]}x{t[1]}") + ("P" if t[2] == 3 else "")): round(v / 1e3, 3)
                                 for t, v in tot.items()}, "best-of:", round(best_tot / 1e3, 3))

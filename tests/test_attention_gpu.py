@@ -1,4 +1,4 @@
-"""Fused attention kernels (relattn.hip: ea_attn_fused_fwd / ea_attn_fused_bwd) against an fp32
+"""Fused attention kernels (relattn.hip: ea_attn_fused_fwd / ea_attn_fused_bwd / _bwd2) against an fp32
 PyTorch restatement of RelPositionMultiHeadedAttention / MultiHeadedAttention
 (espnet/nets/pytorch_backend/transformer/attention.py:15-111, 209-305; rel_shift :237-260)
 on the same bf16-rounded inputs, and against the unfused HIP path (same dropout masks)."""
@@ -67,7 +67,8 @@ def run_fused(q, k, v, u, vb, pp, klen, causal, H, dO, p=0.0, seed=0):
     dkk = torch.empty_like(k)
     dv = torch.empty_like(v)
     ldbd = (2 * T1 - 1 + 7) // 8 * 8
-    dbd = torch.zeros(H * B * T1 * ldbd, dtype=bf, device=DEV) if pp is not None else None
+    # NaN-filled: the kernel writes every band row in full (zeros off the band)
+    dbd = torch.full((H * B * T1 * ldbd,), float("nan"), dtype=bf, device=DEV) if pp is not None else None
     lib.ea_attn_fused_bwd(B, H, T1, T2, dk, q.data_ptr(), d, k.data_ptr(), d, v.data_ptr(), d, ptr(u), ptr(vb),
                           ptr(pp), d, klen.data_ptr(), int(causal), scale, p, seed, O.data_ptr(), d, lse.data_ptr(),
                           dO.data_ptr(), d, dq.data_ptr(), d, dkk.data_ptr(), d, dv.data_ptr(), d, ptr(dbd), ldbd,
@@ -94,6 +95,9 @@ def _inputs(B, H, T1, T2, rel, seed=0):
     (2, 2, 41, 41, False, True, [41, 30]),
     (2, 2, 41, 137, False, False, [137, 77]),
     (1, 1, 5, 5, True, False, [5]),
+    (1, 2, 300, 300, True, False, [300]),
+    (2, 1, 41, 300, False, False, [300, 131]),
+    (1, 2, 270, 270, False, True, [270]),
 ])
 def test_fused_attention_matches_fp32_reference(B, H, T1, T2, rel, causal, klens):
     q, k, v, u, vb, pp, dO = _inputs(B, H, T1, T2, rel)
@@ -164,3 +168,92 @@ def test_fused_matches_unfused_with_dropout():
     assert _rel(dv.view(N, d), dv2) < 2e-2
     band = dbd2.view(H, B, T, ldbd)[..., :P2]
     assert _rel(dbd.view(H, B, T, ldbd)[..., :P2], band) < 2e-2
+
+
+@pytest.mark.parametrize("B,H,T,klens,p", [
+    (2, 3, 137, [137, 100], 0.0),
+    (3, 2, 249, [249, 200, 64], 0.0),
+    (1, 2, 300, [300], 0.0),
+    (2, 2, 97, [97, 60], 0.1),
+])
+def test_fused_bwd2_rel_terms(B, H, T, klens, p):
+    """ea_attn_fused_bwd2 (flags=1): dq includes the (q+v) path, per-block column sums give
+    the pos_bias_u / pos_bias_v gradients, qv_out = bf16(q + v); dq, dk, dv, dbd otherwise
+    equal ea_attn_fused_bwd's."""
+    from espnet_amd import hip_ops as ops
+    from espnet_amd._lib import lib
+    q, k, v, u, vb, pp, dO = _inputs(B, H, T, T, True, seed=5)
+    klen = torch.tensor(klens, dtype=torch.long, device=DEV)
+    seed = 99
+    O, dq1, dk1, dv1, dbd1, ldbd = run_fused(q, k, v, u, vb, pp, klen, False, H, dO, p=p, seed=seed)
+    d = H * 64
+    lse = torch.empty(B * H * T, device=DEV)
+    O2 = torch.empty_like(O)
+    scale = 1 / 8
+    # forward with the dropout keep-bit mask; the backward reads it (bit-identical to rehashing)
+    ldm = 2 * ((T + 63) // 64)
+    dmask = torch.empty(B * H * T * ldm, dtype=torch.int32, device=DEV) if p > 0 else None
+    dmp = 0 if dmask is None else dmask.data_ptr()
+    lib.ea_attn_fused_fwd2(B, H, T, T, 64, q.data_ptr(), d, k.data_ptr(), d, v.data_ptr(), d, u.data_ptr(),
+                           vb.data_ptr(), pp.data_ptr(), d, klen.data_ptr(), 0, scale, p, seed, O2.data_ptr(), d,
+                           lse.data_ptr(), dmp, ldm, ops.stream())
+    dq, dk, dv = torch.empty_like(q), torch.empty_like(k), torch.empty_like(v)
+    dbd = torch.full((H * B * T * ldbd,), float("nan"), dtype=bf, device=DEV)
+    nqb = (T + 63) // 64
+    part = torch.full((2, B * nqb, d), float("nan"), device=DEV)
+    qv = torch.empty(B, T, d, dtype=bf, device=DEV)
+    rc = lib.ea_attn_fused_bwd2(B, H, T, T, 64, q.data_ptr(), d, k.data_ptr(), d, v.data_ptr(), d, u.data_ptr(),
+                                vb.data_ptr(), pp.data_ptr(), d, klen.data_ptr(), 0, scale, p, seed, O2.data_ptr(),
+                                d, lse.data_ptr(), dO.data_ptr(), d, dq.data_ptr(), d, dk.data_ptr(), d, dv.data_ptr(),
+                                d, dbd.data_ptr(), ldbd, part.data_ptr(), d, qv.data_ptr(), d, dmp, ldm, 1,
+                                ops.stream())
+    assert rc == 0
+    torch.cuda.synchronize()
+    assert torch.equal(O2, O) and torch.equal(dk, dk1) and torch.equal(dv, dv1) and torch.equal(dbd, dbd1)
+    assert torch.equal(qv, (q.float() + vb.view(1, 1, d)).to(bf))
+    # (q+v) path: dq - dq_u = dBD . pp_h on the same bf16 band
+    dbd4 = dbd.view(H, B, T, ldbd)[..., : 2 * T - 1].float()
+    pph = pp.float().view(2 * T - 1, H, 64).permute(1, 0, 2)
+    dq_v = torch.einsum("hbir,hrc->bihc", dbd4, pph).reshape(B, T, d)
+    assert _rel(dq.float(), dq1.float() + dq_v) < 1e-2
+    # bias partials: sums over each 64-query block of the two dq terms
+    du = part[0].sum(0)
+    dvb = part[1].sum(0)
+    assert _rel(du, dq1.float().sum((0, 1))) < 1e-2
+    assert _rel(dvb, dq_v.sum((0, 1))) < 1e-2
+    if p == 0.0:  # against the fp32 autograd reference
+        qf, kf, vf = (t.float().requires_grad_(True) for t in (q, k, v))
+        uf, vbf = u.clone().requires_grad_(True), vb.clone().requires_grad_(True)
+        ref = reference(qf, kf, vf, uf, vbf, pp.float(), klen, False, H)
+        ref.backward(dO.float())
+        assert _rel(dq, qf.grad) < 2e-2
+        assert _rel(du, uf.grad) < 2e-2
+        assert _rel(dvb, vbf.grad) < 2e-2
+
+
+@pytest.mark.parametrize("causal,T1,T2,klens", [(True, 45, 45, [45, 30]), (False, 45, 300, [300, 140])])
+def test_fused_dropout_mask_matches_rehash(causal, T1, T2, klens):
+    """Decoder shapes with dropout: ea_attn_fused_fwd2's keep bits read by ea_attn_fused_bwd2
+    give exactly the gradients of the rehashing legacy entry (ea_attn_fused_bwd)."""
+    from espnet_amd import hip_ops as ops
+    from espnet_amd._lib import lib
+    B, H, p, seed = 2, 2, 0.1, 4242
+    q, k, v, _, _, _, dO = _inputs(B, H, T1, T2, False, seed=7)
+    klen = torch.tensor(klens, dtype=torch.long, device=DEV)
+    O, dq1, dk1, dv1, _, _ = run_fused(q, k, v, None, None, None, klen, causal, H, dO, p=p, seed=seed)
+    d = H * 64
+    ldm = 2 * ((T2 + 63) // 64)
+    dmask = torch.empty(B * H * T1 * ldm, dtype=torch.int32, device=DEV)
+    O2 = torch.empty_like(O)
+    lse = torch.empty(B * H * T1, device=DEV)
+    lib.ea_attn_fused_fwd2(B, H, T1, T2, 64, q.data_ptr(), d, k.data_ptr(), d, v.data_ptr(), d, 0, 0, 0, 0,
+                           klen.data_ptr(), int(causal), 1 / 8, p, seed, O2.data_ptr(), d, lse.data_ptr(),
+                           dmask.data_ptr(), ldm, ops.stream())
+    dq, dk, dv = torch.empty_like(q), torch.empty_like(k), torch.empty_like(v)
+    lib.ea_attn_fused_bwd2(B, H, T1, T2, 64, q.data_ptr(), d, k.data_ptr(), d, v.data_ptr(), d, 0, 0, 0, 0,
+                           klen.data_ptr(), int(causal), 1 / 8, p, seed, O2.data_ptr(), d, lse.data_ptr(),
+                           dO.data_ptr(), d, dq.data_ptr(), d, dk.data_ptr(), d, dv.data_ptr(), d, 0, 0, 0, 0, 0, 0,
+                           dmask.data_ptr(), ldm, 0, ops.stream())
+    torch.cuda.synchronize()
+    assert torch.equal(O2, O)
+    assert torch.equal(dq, dq1) and torch.equal(dk, dk1) and torch.equal(dv, dv1)

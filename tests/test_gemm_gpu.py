@@ -169,7 +169,7 @@ def test_gemm_unaligned_leading_dims(dtype, a_k, b_k):
 
 # (bm, bn, pipe): pipe=1 routes the 256x256 tile to gemm_pipe (4-slot ring of 32-deep slices)
 from espnet_amd._lib import GEMM_PIPE as PIPE_DEFAULT  # noqa: E402  (restored after each test)
-TILES = [(64, 128, 0), (128, 128, 0), (256, 256, 0), (256, 256, 1)]
+TILES = [(64, 128, 0), (128, 128, 0), (128, 128, 3), (256, 256, 0), (256, 256, 1)]
 
 
 @pytest.fixture
@@ -183,7 +183,7 @@ def forced_tile(request):
     L.lib.ea_gemm_set_pipe(PIPE_DEFAULT)
 
 
-@pytest.mark.parametrize("forced_tile", TILES, indirect=True, ids=lambda t: f"{t[0]}x{t[1]}{'p' if t[2] else ''}")
+@pytest.mark.parametrize("forced_tile", TILES, indirect=True, ids=lambda t: f"{t[0]}x{t[1]}{'p' * t[2]}")
 @pytest.mark.parametrize("a_k,b_k", [(1, 1), (1, 0), (0, 1), (0, 0)])
 @pytest.mark.parametrize("MNK", [(300, 520, 200), (513, 257, 64), (40, 300, 130), (256, 256, 128),
                                  (600, 700, 1000), (260, 300, 32)])
@@ -203,7 +203,7 @@ def test_gemm_bf16_tiles(forced_tile, a_k, b_k, MNK):
     assert (C[:, N:] == 7.0).all(), "wrote outside ldc columns"
 
 
-@pytest.mark.parametrize("forced_tile", TILES, indirect=True, ids=lambda t: f"{t[0]}x{t[1]}{'p' if t[2] else ''}")
+@pytest.mark.parametrize("forced_tile", TILES, indirect=True, ids=lambda t: f"{t[0]}x{t[1]}{'p' * t[2]}")
 def test_gemm_bf16_tiles_epilogue_splitk(forced_tile):
     """Fused ACT epilogue and split-K dW under each tile shape."""
     ops, L = _ops()
