@@ -92,6 +92,27 @@ EA_DEV void km_stage_bias(char* img, const bf16* __restrict__ src, long ld, int 
   }
 }
 
+// Stage rows [r0, r0+NR) of a row-major bf16 matrix (64 columns) into a km image: thread tid
+// owns 16-B chunk tid&7 of rows (tid>>3) + 32u (a 256-thread block); rows outside [0, rlim)
+// are zero.  gsrc = this thread's element (row tid>>3, chunk tid&7) of the matrix at row 0, so
+// each piece costs one uniform row offset; km_off(row + 32u, c) = km_off(row, c) + 4096u.
+template <int NR>
+EA_DEV void stage_km(char* img, const bf16* gsrc, long ld, int r0, int rlim, int tid) {
+  constexpr int NU = (NR + 31) / 32;
+  const int row = tid >> 3;
+  const int lofs = km_off(row, tid & 7);
+  uint4 v[NU];
+#pragma unroll
+  for (int u = 0; u < NU; ++u) {
+    const int r = r0 + row + 32 * u;
+    v[u] = make_uint4(0u, 0u, 0u, 0u);
+    if ((NR % 32 == 0 || row + 32 * u < NR) && r >= 0 && r < rlim) v[u] = *(const uint4*)(gsrc + (long)(r0 + 32 * u) * ld);
+  }
+#pragma unroll
+  for (int u = 0; u < NU; ++u)
+    if (NR % 32 == 0 || row + 32 * u < NR) *(uint4*)(img + lofs + 4096 * u) = v[u];
+}
+
 EA_DEV f32x4 mfma(bf16x8 a, bf16x8 b, f32x4 c) { return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0); }
 EA_DEV float max16(float v) {  // max over the 16 lanes of a lane group (same lane>>4)
 #pragma unroll
@@ -133,6 +154,9 @@ struct AttnP {
   float* bias_part; long ldpart;  // [2][B*ceil(T1/64)][ldpart] column sums of dQ_u, dQ_v
   bf16* qv_out; long ldqv;   // q + pos_bias_v (rel-pos), rows b*T1 + i, or null
   int flags;                 // bit 0: dq includes the rel-pos term dBD.p
+  float* wsD;                // backward workspace: D_i = dO_i.O_i [z*T1 + i]
+  bf16* wsQu; long ldqu;     //   q + u rows (b*T1 + i, head columns), written by attn_bwdq
+  bf16* wsQv; long ldqvw;    //   q + v rows (rel-pos: qv_out when given, else workspace)
   uint32_t* dmask; int ldm;  // dropout keep bits [z*T1 + i][ldm words], bit j&31 of word j>>5:
                              // written by the forward, read by the backward (else rehashed)
 };
@@ -191,12 +215,16 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(AttnP a) {
   uint64_t rowbase[4];  // dropout element index of (row, key 0)
 #pragma unroll
   for (int r = 0; r < 4; ++r) rowbase[r] = ((uint64_t)z * a.T1 + ibase + r) * a.T2;
+  const long pofs = (long)(tid >> 3), cofs = h * DK + (tid & 7) * 8;  // stage_km thread bases
+  const bf16* gK = a.k + ((long)b * a.T2 + pofs) * a.ldk + cofs;
+  const bf16* gV = a.v + ((long)b * a.T2 + pofs) * a.ldv + cofs;
+  const bf16* gP = REL ? a.pp + pofs * a.ldp + cofs : nullptr;
 
   for (int j0 = 0; j0 < kend; j0 += KC) {
-    km_stage(sm + F_K, a.k + (long)b * a.T2 * a.ldk + h * DK, a.ldk, j0, KC, a.T2, tid, 256);
-    km_stage(sm + F_V, a.v + (long)b * a.T2 * a.ldv + h * DK, a.ldv, j0, KC, a.T2, tid, 256);
+    stage_km<KC>(sm + F_K, gK, a.ldk, j0, a.T2, tid);
+    stage_km<KC>(sm + F_V, gV, a.ldv, j0, a.T2, tid);
     const int rb = a.T1 - 1 - (i0 + QB - 1) + j0;  // first positional row of the block's band
-    if (REL) km_stage(sm + F_P, a.pp + h * DK, a.ldp, rb, 128, 2 * a.T1 - 1, tid, 256);
+    if (REL) stage_km<128>(sm + F_P, gP, a.ldp, rb, 2 * a.T1 - 1, tid);
     __syncthreads();
     f32x4 s[4];
 #pragma unroll
@@ -362,9 +390,9 @@ constexpr int Q_LDS = Q_RED + 2 * NWAVE * DK * 4;
 static_assert(Q_XSZ >= 16 * 192 && Q_XSZ % 16 == 0, "band image fits the gather scratch");
 static_assert(3 * QB * 128 <= Q_D, "setup images fit the chunk space");
 
-// rows [r0, r0+nrows) of (src + bias) into a km image, also written to out (if non-null)
-EA_DEV void km_stage_bias_out(char* img, const bf16* __restrict__ src, long ld, int r0, int nrows, int rlim,
-                              const float* __restrict__ bias, bf16* out, long ldout, int tid, int nthr) {
+// rows [r0, r0+nrows) of (src [+ bias]) into a km image, also written to out (if non-null)
+EA_DEV void km_stage_out(char* img, const bf16* __restrict__ src, long ld, int r0, int nrows, int rlim,
+                         const float* __restrict__ bias, bf16* out, long ldout, int tid, int nthr) {
   for (int c = tid; c < nrows * 8; c += nthr) {
     const int row = c >> 3, ch = c & 7;
     const int r = r0 + row;
@@ -372,8 +400,10 @@ EA_DEV void km_stage_bias_out(char* img, const bf16* __restrict__ src, long ld, 
     t.u = make_uint4(0u, 0u, 0u, 0u);
     if (r >= 0 && r < rlim) {
       t.u = *(const uint4*)(src + (long)r * ld + ch * 8);
+      if (bias) {
 #pragma unroll
-      for (int e = 0; e < 8; ++e) t.e[e] = (bf16)((float)t.e[e] + bias[ch * 8 + e]);
+        for (int e = 0; e < 8; ++e) t.e[e] = (bf16)((float)t.e[e] + bias[ch * 8 + e]);
+      }
       if (out) *(uint4*)(out + (long)r * ldout + ch * 8) = t.u;
     }
     *(uint4*)(img + km_off(row, ch)) = t.u;
@@ -402,11 +432,13 @@ __global__ __launch_bounds__(256, 2) void attn_bwdq_kernel(AttnP a) {
   // this wave's 16 rows of Q + u, Q + v and dO as A fragments; D_i and lse_i
   bf16x8 qa[2], qv[2], doa[2];
   {
+    // q + u, q + v also to the workspace / qv_out for attn_bwdkv (and the linear_pos gradient)
     const bf16* qsrc = a.q + (long)b * a.T1 * a.ldq + h * DK;
-    km_stage_bias(sm, qsrc, a.ldq, i0, QB, a.T1, a.bu ? a.bu + h * DK : nullptr, tid, 256);
+    km_stage_out(sm, qsrc, a.ldq, i0, QB, a.T1, a.bu ? a.bu + h * DK : nullptr,
+                 a.wsQu + (long)b * a.T1 * a.ldqu + h * DK, a.ldqu, tid, 256);
     if (REL)
-      km_stage_bias_out(sm + QB * 128, qsrc, a.ldq, i0, QB, a.T1, a.bv + h * DK,
-                        a.qv_out ? a.qv_out + (long)b * a.T1 * a.ldqv + h * DK : nullptr, a.ldqv, tid, 256);
+      km_stage_out(sm + QB * 128, qsrc, a.ldq, i0, QB, a.T1, a.bv + h * DK,
+                   a.wsQv + (long)b * a.T1 * a.ldqvw + h * DK, a.ldqvw, tid, 256);
     km_stage(sm + 2 * QB * 128, a.dO + (long)b * a.T1 * a.lddo + h * DK, a.lddo, i0, QB, a.T1, tid, 256);
     {  // D_i = dO_i . O_i: 4 threads per row, 16 columns each
       const int row = tid >> 2, qd = tid & 3, i = i0 + row;
@@ -428,6 +460,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwdq_kernel(AttnP a) {
       if (qd == 0) {
         Dv[row] = d;
         Lv[row] = i < a.T1 ? a.lse[(long)z * a.T1 + i] * LOG2E : INFINITY;
+        if (i < a.T1) a.wsD[(long)z * a.T1 + i] = d;
       }
     }
     __syncthreads();
@@ -454,19 +487,31 @@ __global__ __launch_bounds__(256, 2) void attn_bwdq_kernel(AttnP a) {
   bf16* dbd_h = REL && a.dbd ? a.dbd + ((long)h * a.B + b) * a.T1 * a.lddbd : nullptr;
   if (dbd_h) {  // zeros off the part of each row the chunk loop writes: r < T-1-i, r >= T-1-i+jcov
     const int jcov = min(a.T2, nch * KC);
-    for (int il = 0; il < 16; ++il) {
+    const uint4 zero = make_uint4(0u, 0u, 0u, 0u);
+    for (int il = 0; il < 16; ++il) {  // 8-column segments (lddbd % 8 == 0, 16-B aligned rows)
       const int i = i0 + 16 * w + il;
       if (i >= a.T1) break;
       bf16* drow = dbd_h + (long)i * a.lddbd;
       const int lo = a.T1 - 1 - i, hi = lo + jcov;
-      for (int c = lane; c < a.lddbd; c += 64)
-        if (c < lo || c >= hi) drow[c] = (bf16)0.f;
+      for (int c0 = 8 * lane; c0 < a.lddbd; c0 += 512) {
+        if (c0 + 8 <= lo || c0 >= hi) {
+          *(uint4*)(drow + c0) = zero;
+        } else if (c0 < lo || c0 + 8 > hi) {
+#pragma unroll
+          for (int e = 0; e < 8; ++e)
+            if (c0 + e < lo || c0 + e >= hi) drow[c0 + e] = (bf16)0.f;
+        }
+      }
     }
   }
   const bool use_mask = a.p > 0.f && a.dmask != nullptr;
   const uint32_t* mrow = a.dmask + ((long)z * a.T1 + ibase) * a.ldm;  // rows ibase + r (< T1)
   const float dsc = a.p > 0.f ? 1.f / (1.f - a.p) : 1.f;
 
+  const long pofs = (long)(tid >> 3), cofs = h * DK + (tid & 7) * 8;  // stage_km thread bases
+  const bf16* gK = a.k + ((long)b * a.T2 + pofs) * a.ldk + cofs;
+  const bf16* gV = a.v + ((long)b * a.T2 + pofs) * a.ldv + cofs;
+  const bf16* gP = REL ? a.pp + pofs * a.ldp + cofs : nullptr;
   f32x4 dqu[4], dqv[4];
 #pragma unroll
   for (int n = 0; n < 4; ++n) dqu[n] = dqv[n] = (f32x4){0.f, 0.f, 0.f, 0.f};
@@ -497,10 +542,10 @@ __global__ __launch_bounds__(256, 2) void attn_bwdq_kernel(AttnP a) {
       for (int r = 0; r < 4; ++r) mw[r] = make_uint2(~0u, ~0u);
     }
     __syncthreads();  // the setup images / previous chunk's images are no longer read
-    km_stage(sm + Q_K, a.k + (long)b * a.T2 * a.ldk + h * DK, a.ldk, j0, KC, a.T2, tid, 256);
-    km_stage(sm + Q_V, a.v + (long)b * a.T2 * a.ldv + h * DK, a.ldv, j0, KC, a.T2, tid, 256);
+    stage_km<KC>(sm + Q_K, gK, a.ldk, j0, a.T2, tid);
+    stage_km<KC>(sm + Q_V, gV, a.ldv, j0, a.T2, tid);
     const int rb = a.T1 - 1 - (i0 + QB - 1) + j0;  // first positional row of the block's band
-    if (REL) km_stage(sm + Q_P, a.pp + h * DK, a.ldp, rb, 144, 2 * a.T1 - 1, tid, 256);
+    if (REL) stage_km<144>(sm + Q_P, gP, a.ldp, rb, 2 * a.T1 - 1, tid);
     __syncthreads();
     f32x4 s[4], dp[4];
 #pragma unroll
@@ -669,31 +714,32 @@ __global__ __launch_bounds__(256, 2) void attn_bwdkv_kernel(AttnP a) {
         vf[ks] = *(const bf16x8*)(a.v + ((long)b * a.T2 + j) * a.ldv + h * DK + 32 * ks + 8 * g);
       }
     }
-    const bf16* qsrc = a.q + (long)b * a.T1 * a.ldq + h * DK;
-    const bf16* dosrc = a.dO + (long)b * a.T1 * a.lddo + h * DK;
-    const bf16* osrc = a.o + (long)b * a.T1 * a.ldo + h * DK;
     const int prow = tid >> 3, pch = tid & 7;
-    float bu8[8], bv8[8];  // this thread's 8 bias columns
-#pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      bu8[e] = a.bu ? a.bu[h * DK + pch * 8 + e] : 0.f;
-      bv8[e] = REL ? a.bv[h * DK + pch * 8 + e] : 0.f;
-    }
     const bool use_mask = a.p > 0.f && a.dmask != nullptr;
     const float dsc = a.p > 0.f ? 1.f / (1.f - a.p) : 1.f;
     const float sl2 = a.scale * LOG2E;
-    // thread tid owns row tid>>3, chunk tid&7 of the Q / dO / O tiles, band pieces tid + 256u
-    // (u < 3) of the 96 x 8 band image and (tid < 64) keep word tid>>5 of row tid&31
-    struct Pre { uint4 q, dO, o, p[3]; float lse; uint32_t mw; };
+    // thread tid owns row tid>>3, chunk tid&7 of the Q+u / Q+v / dO tiles, band rows
+    // (tid>>3) + 32u (u < 3) of the 96-row band image, (tid < 32) D / lse of row tid and
+    // (tid < 64) keep word tid>>5 of row tid&31; per-thread bases at row 0, uniform row offsets
+    const long cofs = h * DK + pch * 8;
+    const bf16* gQu = a.wsQu + ((long)b * a.T1 + prow) * a.ldqu + cofs;
+    const bf16* gQv = REL ? a.wsQv + ((long)b * a.T1 + prow) * a.ldqvw + cofs : nullptr;
+    const bf16* gdO = a.dO + ((long)b * a.T1 + prow) * a.lddo + cofs;
+    const bf16* gP = REL ? a.pp + (long)prow * a.ldp + cofs : nullptr;
+    const int lofs = km_off(prow, pch);
+    struct Pre { uint4 qu, qv, dO, p[3]; float D, L; uint32_t mw; };
     auto fetch = [&](int i0n, Pre& pr) {
       const int i = i0n + prow;
-      pr.q = pr.dO = pr.o = make_uint4(0u, 0u, 0u, 0u);
-      pr.lse = INFINITY;
+      pr.qu = pr.qv = pr.dO = make_uint4(0u, 0u, 0u, 0u);
       if (i < a.T1) {
-        pr.q = *(const uint4*)(qsrc + (long)i * a.ldq + pch * 8);
-        pr.dO = *(const uint4*)(dosrc + (long)i * a.lddo + pch * 8);
-        pr.o = *(const uint4*)(osrc + (long)i * a.ldo + pch * 8);
-        pr.lse = a.lse[(long)z * a.T1 + i];
+        pr.qu = *(const uint4*)(gQu + (long)i0n * a.ldqu);
+        if (REL) pr.qv = *(const uint4*)(gQv + (long)i0n * a.ldqvw);
+        pr.dO = *(const uint4*)(gdO + (long)i0n * a.lddo);
+      }
+      if (tid < BQ) {
+        const int ir = i0n + tid;
+        pr.D = ir < a.T1 ? a.wsD[(long)z * a.T1 + ir] : 0.f;
+        pr.L = ir < a.T1 ? a.lse[(long)z * a.T1 + ir] * LOG2E : INFINITY;
       }
       if (use_mask && tid < 64) {
         const int im = min(i0n + (tid & 31), a.T1 - 1);
@@ -703,9 +749,9 @@ __global__ __launch_bounds__(256, 2) void attn_bwdkv_kernel(AttnP a) {
         const int rs = a.T1 - 1 - (i0n + BQ - 1) + j0;
 #pragma unroll
         for (int u = 0; u < 3; ++u) {
-          const int pc = tid + 256 * u, r = rs + (pc >> 3);
+          const int r = rs + prow + 32 * u;
           pr.p[u] = make_uint4(0u, 0u, 0u, 0u);
-          if (r >= 0 && r < 2 * a.T1 - 1) pr.p[u] = *(const uint4*)(a.pp + (long)r * a.ldp + h * DK + (pc & 7) * 8);
+          if (r >= 0 && r < 2 * a.T1 - 1) pr.p[u] = *(const uint4*)(gP + (long)(rs + 32 * u) * a.ldp);
         }
       }
     };
@@ -717,42 +763,18 @@ __global__ __launch_bounds__(256, 2) void attn_bwdkv_kernel(AttnP a) {
     fetch(istart, pre);
     for (int i0 = istart; i0 < a.T1; i0 += BQ) {
       __syncthreads();  // previous tile's readers of the images / BDfull are done
-      {
-        const bool ok = i0 + prow < a.T1;
-        union { uint4 u; bf16 e[8]; } x, y, qu, qv;
-        x.u = pre.q;
-        qu.u = qv.u = make_uint4(0u, 0u, 0u, 0u);
-        if (ok) {
+      *(uint4*)(quimg + lofs) = pre.qu;
+      if (REL) *(uint4*)(qvimg + lofs) = pre.qv;
+      *(uint4*)(doimg + lofs) = pre.dO;
+      if (REL) {
 #pragma unroll
-          for (int e = 0; e < 8; ++e) {
-            const float xf = (float)x.e[e];
-            qu.e[e] = (bf16)(xf + bu8[e]);
-            if (REL) qv.e[e] = (bf16)(xf + bv8[e]);
-          }
-        }
-        *(uint4*)(quimg + km_off(prow, pch)) = qu.u;
-        if (REL) *(uint4*)(qvimg + km_off(prow, pch)) = qv.u;
-        *(uint4*)(doimg + km_off(prow, pch)) = pre.dO;
-        if (REL) {
-#pragma unroll
-          for (int u = 0; u < 3; ++u) {
-            const int pc = tid + 256 * u;
-            *(uint4*)(pimg + km_off(pc >> 3, pc & 7)) = pre.p[u];
-          }
-        }
-        if (use_mask && tid < 64) Mw[(tid >> 5) * BQ + (tid & 31)] = pre.mw;
-        x.u = pre.dO;
-        y.u = pre.o;
-        float d = 0.f;
-#pragma unroll
-        for (int e = 0; e < 8; ++e) d += (float)x.e[e] * (float)y.e[e];
-#pragma unroll
-        for (int o = 1; o < 8; o <<= 1) d += __shfl_xor(d, o, 64);
-        if (pch == 0) {
-          Dv[prow] = d;
-          Lv[prow] = pre.lse * LOG2E;
-        }
+        for (int u = 0; u < 3; ++u) *(uint4*)(pimg + lofs + 4096 * u) = pre.p[u];
       }
+      if (tid < BQ) {
+        Dv[tid] = pre.D;
+        Lv[tid] = pre.L;
+      }
+      if (use_mask && tid < 64) Mw[(tid >> 5) * BQ + (tid & 31)] = pre.mw;
       __syncthreads();
       if (i0 + BQ < a.T1) fetch(i0 + BQ, pre);
       // S (32 queries x this wave's 16 keys): s[mi] rows 16mi + 4g + r, key column jw + lc
@@ -910,41 +932,49 @@ static int attn_bwd_launch(AttnP& a, bool rel, hipStream_t st) {
   return 0;
 }
 
+static long attn_ws_layout(int B, int H, int T1, long* qu_off, long* qv_off) {
+  const long d = (long)B * H * T1 * 4, q = (long)B * T1 * H * DK * 2;
+  *qu_off = (d + 255) / 256 * 256;
+  *qv_off = *qu_off + (q + 255) / 256 * 256;
+  return *qv_off + q;
+}
+
+extern "C" int ea_attn_fused_bwd_ws_bytes(int B, int H, int T1, long* bytes) {
+  EA_CHECK_ARG(B >= 1 && H >= 1 && T1 >= 1 && bytes != nullptr);
+  long qu, qv;
+  *bytes = attn_ws_layout(B, H, T1, &qu, &qv);
+  return 0;
+}
+
 extern "C" int ea_attn_fused_bwd2(int B, int H, int T1, int T2, int dk, const void* q, long ldq, const void* k,
                                   long ldk, const void* v, long ldv, const float* bu, const float* bv,
                                   const void* pp, long ldp, const long long* klen, int causal, float scale, float p,
                                   unsigned long long seed, const void* o, long ldo, const float* lse, const void* dO,
                                   long lddo, void* dq, long lddq, void* dkout, long lddk, void* dvout, long lddv,
                                   void* dbd, long lddbd, float* bias_part, long ldpart, void* qv_out, long ldqv,
-                                  const unsigned* dmask, int ldm, int flags, void* stream) {
+                                  const unsigned* dmask, int ldm, void* ws, long ws_bytes, int flags, void* stream) {
   EA_ENTRY();
   EA_CHECK_ARG(dk == DK && B >= 1 && H >= 1 && T1 >= 1 && T2 >= 1);
-  EA_CHECK_ARG(!pp || (T1 == T2 && bv != nullptr && (dbd == nullptr || lddbd >= 2 * T1 - 1)));
+  EA_CHECK_ARG(!pp || (T1 == T2 && bv != nullptr));
+  EA_CHECK_ARG(!dbd || (pp && lddbd >= 2 * T1 - 1 && lddbd % 8 == 0 && (uintptr_t)dbd % 16 == 0));
   EA_CHECK_ARG(ldq % 8 == 0 && ldk % 8 == 0 && ldv % 8 == 0 && ldo % 8 == 0 && lddo % 8 == 0 &&
                (!pp || ldp % 8 == 0) && (!qv_out || (pp && ldqv % 8 == 0)));
   EA_CHECK_ARG(!bias_part || ldpart >= (long)H * DK);
   EA_CHECK_ARG(flags == 0 || (flags == 1 && pp));
   EA_CHECK_ARG(!dmask || ldm >= 2 * ((T2 + 63) / 64));
+  long qu_off, qv_off;
+  EA_CHECK_ARG(ws != nullptr && (uintptr_t)ws % 256 == 0 && ws_bytes >= attn_ws_layout(B, H, T1, &qu_off, &qv_off));
   AttnP a = make_p(B, H, T1, T2, q, ldq, k, ldk, v, ldv, bu, bv, pp, ldp, klen, causal, scale, p, seed);
   a.o = (bf16*)o; a.ldo = ldo; a.lse = (float*)lse;
   a.dO = (const bf16*)dO; a.lddo = lddo;
   a.dq = (bf16*)dq; a.lddq = lddq; a.dk = (bf16*)dkout; a.lddk = lddk; a.dv = (bf16*)dvout; a.lddv = lddv;
   a.dbd = (bf16*)dbd; a.lddbd = lddbd;
   a.bias_part = bias_part; a.ldpart = ldpart;
-  a.qv_out = (bf16*)qv_out; a.ldqv = ldqv;
   a.flags = flags;
   a.dmask = (uint32_t*)dmask; a.ldm = ldm;
+  a.wsD = (float*)ws;
+  a.wsQu = (bf16*)((char*)ws + qu_off); a.ldqu = (long)H * DK;
+  if (qv_out) { a.wsQv = (bf16*)qv_out; a.ldqvw = ldqv; }
+  else { a.wsQv = (bf16*)((char*)ws + qv_off); a.ldqvw = (long)H * DK; }
   return attn_bwd_launch(a, pp != nullptr, (hipStream_t)stream);
-}
-
-extern "C" int ea_attn_fused_bwd(int B, int H, int T1, int T2, int dk, const void* q, long ldq, const void* k,
-                                 long ldk, const void* v, long ldv, const float* bu, const float* bv,
-                                 const void* pp, long ldp, const long long* klen, int causal, float scale, float p,
-                                 unsigned long long seed, const void* o, long ldo, const float* lse, const void* dO,
-                                 long lddo, void* dq, long lddq, void* dkout, long lddk, void* dvout, long lddv,
-                                 void* dbd, long lddbd, void* stream) {
-  EA_CHECK_ARG(!pp || dbd != nullptr);
-  return ea_attn_fused_bwd2(B, H, T1, T2, dk, q, ldq, k, ldk, v, ldv, bu, bv, pp, ldp, klen, causal, scale, p, seed,
-                            o, ldo, lse, dO, lddo, dq, lddq, dkout, lddk, dvout, lddv, dbd, lddbd, nullptr, 0,
-                            nullptr, 0, nullptr, 0, 0, stream);
 }

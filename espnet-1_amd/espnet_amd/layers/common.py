@@ -7,6 +7,7 @@ Only activations flow through autograd, so a whole training step is ~25 autograd
 """
 from __future__ import annotations
 
+import ctypes
 import math
 import os
 
@@ -18,7 +19,8 @@ from .._lib import (ACT_NONE, ACT_RELU, ACT_SWISH, EPI_ACT, EPI_DACT, EPI_RESID,
 
 __all__ = ["Bound", "rup", "empty", "ops", "lib", "EPI_ACT", "EPI_DACT", "EPI_RESID",
            "EPI_STORE", "ACT_NONE", "ACT_RELU", "ACT_SWISH", "site_seed", "attn_fwd", "attn_bwd",
-           "LayerNormFn", "ln_fwd", "ln_bwd", "math", "F32", "fused_attn_ok", "attn_dmask", "ptr"]
+           "LayerNormFn", "ln_fwd", "ln_bwd", "math", "F32", "fused_attn_ok", "attn_dmask", "ptr",
+           "attn_fused_bwd"]
 
 F32 = torch.float32
 
@@ -53,6 +55,20 @@ def attn_dmask(rows, T2, p, device):
         return None, 0
     ldm = 2 * ((T2 + 63) // 64)
     return torch.empty(rows * ldm, dtype=torch.int32, device=device), ldm
+
+
+def attn_fused_bwd(*, B, H, T1, T2, q, ldq, k, ldk, v, ldv, bu, bv, pp, ldp, klen, causal, scale, p, seed,
+                   O, ldo, lse, dO, lddo, dq, lddq, dk, lddk, dv, lddv, dbd=None, ldbd=0, part=None,
+                   ldpart=0, qv_out=None, ldqv=0, dmask=None, ldm=0, flags=0):
+    """ea_attn_fused_bwd2 with its workspace (D_i, q+u, q+v handed between the two passes),
+    a stream-ordered allocation freed behind the launches."""
+    n = ctypes.c_long(0)
+    lib.ea_attn_fused_bwd_ws_bytes(B, H, T1, ctypes.addressof(n))
+    ws = torch.empty(n.value, dtype=torch.uint8, device=dO.device)
+    lib.ea_attn_fused_bwd2(B, H, T1, T2, 64, ptr(q), ldq, ptr(k), ldk, ptr(v), ldv, ptr(bu), ptr(bv), ptr(pp),
+                           ldp, ptr(klen), int(causal), float(scale), float(p), seed, ptr(O), ldo, ptr(lse),
+                           ptr(dO), lddo, ptr(dq), lddq, ptr(dk), lddk, ptr(dv), lddv, ptr(dbd), ldbd, ptr(part),
+                           ldpart, ptr(qv_out), ldqv, ptr(dmask), ldm, ws.data_ptr(), n.value, flags, ops.stream())
 
 
 def site_seed(base: int, layer: int, site: int) -> int:

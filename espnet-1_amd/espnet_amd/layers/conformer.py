@@ -15,8 +15,9 @@ from __future__ import annotations
 import torch
 from torch import nn
 
-from .common import (ACT_SWISH, EPI_ACT, EPI_DACT, EPI_RESID, EPI_STORE, F32, Bound, attn_bwd, attn_dmask, fused_attn_ok,
-                     attn_fwd, empty, lib, ln_bwd, ln_fwd, math, ops, ptr, rup, site_seed)
+from .common import (ACT_SWISH, EPI_ACT, EPI_DACT, EPI_RESID, EPI_STORE, F32, Bound, attn_bwd, attn_dmask,
+                     attn_fused_bwd, attn_fwd, empty, fused_attn_ok, lib, ln_bwd, ln_fwd, math, ops, ptr, rup,
+                     site_seed)
 
 
 # ----------------------------------------------------------------------------- holders
@@ -312,13 +313,12 @@ class ConformerBlockFn(torch.autograd.Function):
             qv = empty(N, d, dtype=cd, device=dev)  # q + v, for the linear_pos weight gradient
             nqb = (T + 63) // 64
             part = empty(2 * B * nqb * d, device=dev)
-            lib.ea_attn_fused_bwd2(B, H, T, T, dk, qkv.data_ptr(), 3 * d, qkv[:, d:].data_ptr(), 3 * d,
-                                   qkv[:, 2 * d:].data_ptr(), 3 * d, b.f(A + "pos_bias_u").data_ptr(),
-                                   b.f(A + "pos_bias_v").data_ptr(), pp.data_ptr(), d, olens.data_ptr(), 0,
-                                   scale, float(pa), sd(3), O.data_ptr(), d, lse.data_ptr(), dO.data_ptr(), d,
-                                   dqkv.data_ptr(), 3 * d, dqkv[:, d:].data_ptr(), 3 * d,
-                                   dqkv[:, 2 * d:].data_ptr(), 3 * d, dbd.data_ptr(), ldbd, part.data_ptr(), d,
-                                   qv.data_ptr(), d, ptr(dmask), ldm, 1, ops.stream())
+            attn_fused_bwd(B=B, H=H, T1=T, T2=T, q=qkv, ldq=3 * d, k=qkv[:, d:], ldk=3 * d, v=qkv[:, 2 * d:],
+                           ldv=3 * d, bu=b.f(A + "pos_bias_u"), bv=b.f(A + "pos_bias_v"), pp=pp, ldp=d,
+                           klen=olens, causal=False, scale=scale, p=pa, seed=sd(3), O=O, ldo=d, lse=lse, dO=dO,
+                           lddo=d, dq=dqkv, lddq=3 * d, dk=dqkv[:, d:], lddk=3 * d, dv=dqkv[:, 2 * d:],
+                           lddv=3 * d, dbd=dbd, ldbd=ldbd, part=part, ldpart=d, qv_out=qv, ldqv=d, dmask=dmask,
+                           ldm=ldm, flags=1)
             ops.reduce_rows(part[:B * nqb * d], B * nqb, d, d, b.g(A + "pos_bias_u", shape=(d,)))
             ops.reduce_rows(part[B * nqb * d:], B * nqb, d, d, b.g(A + "pos_bias_v", shape=(d,)))
         else:

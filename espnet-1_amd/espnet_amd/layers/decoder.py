@@ -16,7 +16,8 @@ import torch
 from torch import nn
 
 from .common import (ACT_RELU, EPI_ACT, EPI_DACT, EPI_RESID, EPI_STORE, F32, Bound, attn_bwd,
-                     attn_dmask, attn_fwd, empty, fused_attn_ok, lib, ln_bwd, ln_fwd, ops, ptr, site_seed)
+                     attn_dmask, attn_fused_bwd, attn_fwd, empty, fused_attn_ok, lib, ln_bwd, ln_fwd, ops, ptr,
+                     site_seed)
 
 
 def _mha_fwd(q, k, v, *, B, H, T1, T2, dk, ldq, ldk, ldv, klen, causal, scale, p, seed, cd):
@@ -40,11 +41,10 @@ def _mha_bwd(st, dO, q, k, v, *, B, H, T1, T2, dk, ldq, ldk, ldv, klen, causal, 
              dq, lddq, dk_, lddk, dv, lddv):
     if st[0] == "fused":
         _, O, lse, dmask, ldm = st
-        lib.ea_attn_fused_bwd2(B, H, T1, T2, dk, q.data_ptr(), ldq, k.data_ptr(), ldk, v.data_ptr(), ldv,
-                               None, None, None, 0, klen.data_ptr(), int(causal), scale, float(p), seed,
-                               O.data_ptr(), H * dk, lse.data_ptr(), dO.data_ptr(), H * dk, dq.data_ptr(), lddq,
-                               dk_.data_ptr(), lddk, dv.data_ptr(), lddv, None, 0, None, 0, None, 0,
-                               ptr(dmask), ldm, 0, ops.stream())
+        attn_fused_bwd(B=B, H=H, T1=T1, T2=T2, q=q, ldq=ldq, k=k, ldk=ldk, v=v, ldv=ldv, bu=None, bv=None, pp=None,
+                       ldp=0, klen=klen, causal=causal, scale=scale, p=p, seed=seed, O=O, ldo=H * dk, lse=lse,
+                       dO=dO, lddo=H * dk, dq=dq, lddq=lddq, dk=dk_, lddk=lddk, dv=dv, lddv=lddv, dmask=dmask,
+                       ldm=ldm)
         return
     _, P, Pd, ldT = st
     attn_bwd(dO, q, k, v, P, Pd, ldT, B=B, H=H, T1=T1, T2=T2, dk=dk, ldq=ldq, ldk=ldk, ldv=ldv, scale=scale,

@@ -366,20 +366,11 @@ int ea_attn_softmax_bwd(int B, int H, int T1, int T2, float scale, const float* 
  *   masked row: 0); O = dropout(P)·V (mask index (z*T1 + i)*T2 + j, z = b*H + h).
  * q rows b*T1 + i, k/v rows b*T2 + j, pp rows r < 2*T1-1, head h at column h*64 of each.
  * fwd writes O (bf16, rows b*T1 + i) and lse[z*T1 + i] (row log-sum-exp; +inf if masked).
- * bwd writes dq = d(q + bu) (the q_v path is NOT included: it leaves through dbd), dk, dv
- * (bf16) and, with pp, the band dbd[h][b][i][T-1-i+j] = gradient of the raw rel-pos term
- * (q_i + bv)·pp[r] (bf16, rows written in full: 0 off the band; lddbd >= 2*T1-1).
- * Nothing is materialised at (T1, T2) size; any T1, T2. */
+ * Nothing is materialised at (T1, T2) size; any T1, T2.  Backward: ea_attn_fused_bwd2. */
 int ea_attn_fused_fwd(int B, int H, int T1, int T2, int dk, const void* q, long ldq, const void* k,
                       long ldk, const void* v, long ldv, const float* bu, const float* bv,
                       const void* pp, long ldp, const long long* klen, int causal, float scale, float p,
                       unsigned long long seed, void* o, long ldo, float* lse, void* stream);
-int ea_attn_fused_bwd(int B, int H, int T1, int T2, int dk, const void* q, long ldq, const void* k,
-                      long ldk, const void* v, long ldv, const float* bu, const float* bv,
-                      const void* pp, long ldp, const long long* klen, int causal, float scale, float p,
-                      unsigned long long seed, const void* o, long ldo, const float* lse, const void* dO,
-                      long lddo, void* dq, long lddq, void* dkout, long lddk, void* dvout, long lddv,
-                      void* dbd, long lddbd, void* stream);
 /* ea_attn_fused_fwd that also writes the dropout keep decisions (p > 0) as bits for the
  * backward: dmask[(z*T1 + i)*ldm + (j >> 5)] bit (j & 31), ldm >= 2*ceil(T2/64) words (NULL:
  * none; words of key chunks past the row's last valid key are left unwritten). */
@@ -388,22 +379,27 @@ int ea_attn_fused_fwd2(int B, int H, int T1, int T2, int dk, const void* q, long
                        const void* pp, long ldp, const long long* klen, int causal, float scale, float p,
                        unsigned long long seed, void* o, long ldo, float* lse, unsigned* dmask, int ldm,
                        void* stream);
-/* ea_attn_fused_bwd plus the rel-pos terms the caller would otherwise compute from dbd:
- *   flags bit 0 (pp only): dq = d(q+bu) + d(q+bv), the second term dBD·pp computed in-kernel;
+/* Backward of ea_attn_fused_fwd(2): dq = d(q + bu) (flags bit 0, pp only: + d(q + bv), the
+ * rel-pos path dBD·pp computed in-kernel), dk, dv (bf16), and optionally:
+ *   dbd (pp only, or NULL): the band dbd[h][b][i][T-1-i+j] = gradient of the raw rel-pos term
+ *     (q_i + bv)·pp[r] (bf16, rows written in full: 0 off the band; lddbd >= 2*T1-1, lddbd % 8
+ *     == 0, 16-B aligned) — the linear_pos weight gradient's operand;
  *   bias_part (or NULL): [2][B*ceil(T1/64)][ldpart] f32, row (b*ceil(T1/64) + qb) holds the
  *     column sums over queries [64qb, 64qb+64) of d(q+bu) (plane 0) and, with pp, d(q+bv)
  *     (plane 1) at columns h*64 + c — reduce over rows for pos_bias_u / pos_bias_v gradients;
- *   qv_out (or NULL, pp only): q + bv (bf16, rows b*T1 + i, head columns), the B operand of
- *     the linear_pos weight gradient.  dbd may be NULL when its GEMM is not wanted;
+ *   qv_out (or NULL, pp only): q + bv (bf16, rows b*T1 + i, head columns);
  *   dmask (or NULL): the forward's keep bits (ea_attn_fused_fwd2, same p / seed), read
- *     instead of regenerating the dropout hash. */
+ *     instead of regenerating the dropout hash.
+ * ws: ea_attn_fused_bwd_ws_bytes() bytes of device scratch, 256-B aligned (D_i, q + bu, q + bv
+ * handed from the dQ pass to the dK/dV pass).  Two launches, any T1, T2, deterministic. */
+int ea_attn_fused_bwd_ws_bytes(int B, int H, int T1, long* bytes);
 int ea_attn_fused_bwd2(int B, int H, int T1, int T2, int dk, const void* q, long ldq, const void* k,
                        long ldk, const void* v, long ldv, const float* bu, const float* bv,
                        const void* pp, long ldp, const long long* klen, int causal, float scale, float p,
                        unsigned long long seed, const void* o, long ldo, const float* lse, const void* dO,
                        long lddo, void* dq, long lddq, void* dkout, long lddk, void* dvout, long lddv,
                        void* dbd, long lddbd, float* bias_part, long ldpart, void* qv_out, long ldqv,
-                       const unsigned* dmask, int ldm, int flags, void* stream);
+                       const unsigned* dmask, int ldm, void* ws, long ws_bytes, int flags, void* stream);
 
 /* ---------------------------------------------------------------- losses */
 

@@ -7,6 +7,7 @@ sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."
 import torch
 from espnet_amd import hip_ops as ops
 from espnet_amd._lib import lib
+from espnet_amd.layers.common import attn_fused_bwd
 
 dev = torch.device("cuda", 0)
 bf = torch.bfloat16
@@ -23,24 +24,29 @@ O = torch.empty(B, T, d, dtype=bf, device=dev)
 lse = torch.empty(B * H * T, device=dev)
 dq, dk, dv = torch.empty_like(q), torch.empty_like(k), torch.empty_like(v)
 ldbd = (2 * T - 1 + 7) // 8 * 8
-dbd = torch.zeros(H * B * T * ldbd, dtype=bf, device=dev)
+dbd = torch.empty(H * B * T * ldbd, dtype=bf, device=dev)  # written in full by the kernel
+ldm = 2 * ((T + 63) // 64)
+dmask = torch.empty(B * H * T * ldm, dtype=torch.int32, device=dev)
+nqb = (T + 63) // 64
+part = torch.empty(2 * B * nqb * d, device=dev)
+qv_out = torch.empty(B, T, d, dtype=bf, device=dev)
 scale, p, seed = 1.0 / math.sqrt(64), float(os.environ.get("ATTN_P", "0.1")), 7
 st = ops.stream()
 hs = torch.cuda.current_stream()  # ops.stream() launches on it
 
 
 def fwd():
-    lib.ea_attn_fused_fwd(B, H, T, T, 64, q.data_ptr(), d, k.data_ptr(), d, v.data_ptr(), d, u.data_ptr(),
-                          vb.data_ptr(), pp.data_ptr(), d, klen.data_ptr(), 0, scale, p, seed, O.data_ptr(), d,
-                          lse.data_ptr(), st)
+    lib.ea_attn_fused_fwd2(B, H, T, T, 64, q.data_ptr(), d, k.data_ptr(), d, v.data_ptr(), d, u.data_ptr(),
+                           vb.data_ptr(), pp.data_ptr(), d, klen.data_ptr(), 0, scale, p, seed, O.data_ptr(), d,
+                           lse.data_ptr(), dmask.data_ptr() if p > 0 else 0, ldm, st)
 
 
 def bwd():
-    lib.ea_attn_fused_bwd(B, H, T, T, 64, q.data_ptr(), d, k.data_ptr(), d, v.data_ptr(), d, u.data_ptr(),
-                          vb.data_ptr(), pp.data_ptr(), d, klen.data_ptr(), 0, scale, p, seed, O.data_ptr(), d,
-                          lse.data_ptr(), dO.data_ptr(), d, dq.data_ptr(), d, dk.data_ptr(), d, dv.data_ptr(), d,
-                          dbd.data_ptr(), ldbd, st)
-
+    # as the conformer layer calls it: dq with the rel-pos term, bias partials, q+v, keep bits
+    attn_fused_bwd(B=B, H=H, T1=T, T2=T, q=q, ldq=d, k=k, ldk=d, v=v, ldv=d, bu=u, bv=vb, pp=pp, ldp=d, klen=klen,
+                   causal=False, scale=scale, p=p, seed=seed, O=O, ldo=d, lse=lse, dO=dO, lddo=d, dq=dq, lddq=d,
+                   dk=dk, lddk=d, dv=dv, lddv=d, dbd=dbd, ldbd=ldbd, part=part, ldpart=d, qv_out=qv_out, ldqv=d,
+                   dmask=dmask if p > 0 else None, ldm=ldm, flags=1)
 
 for name, fn in (("fwd", fwd), ("bwd", bwd)):
     for _ in range(3):

@@ -1,4 +1,4 @@
-"""Fused attention kernels (relattn.hip: ea_attn_fused_fwd / ea_attn_fused_bwd / _bwd2) against an fp32
+"""Fused attention kernels (relattn.hip: ea_attn_fused_fwd(2) / ea_attn_fused_bwd2) against an fp32
 PyTorch restatement of RelPositionMultiHeadedAttention / MultiHeadedAttention
 (espnet/nets/pytorch_backend/transformer/attention.py:15-111, 209-305; rel_shift :237-260)
 on the same bf16-rounded inputs, and against the unfused HIP path (same dropout masks)."""
@@ -53,6 +53,7 @@ def _rel(a, b):
 def run_fused(q, k, v, u, vb, pp, klen, causal, H, dO, p=0.0, seed=0):
     from espnet_amd import hip_ops as ops
     from espnet_amd._lib import lib
+    from espnet_amd.layers.common import attn_fused_bwd
     B, T1, d = q.shape
     T2 = k.shape[1]
     dk = d // H
@@ -69,10 +70,10 @@ def run_fused(q, k, v, u, vb, pp, klen, causal, H, dO, p=0.0, seed=0):
     ldbd = (2 * T1 - 1 + 7) // 8 * 8
     # NaN-filled: the kernel writes every band row in full (zeros off the band)
     dbd = torch.full((H * B * T1 * ldbd,), float("nan"), dtype=bf, device=DEV) if pp is not None else None
-    lib.ea_attn_fused_bwd(B, H, T1, T2, dk, q.data_ptr(), d, k.data_ptr(), d, v.data_ptr(), d, ptr(u), ptr(vb),
-                          ptr(pp), d, klen.data_ptr(), int(causal), scale, p, seed, O.data_ptr(), d, lse.data_ptr(),
-                          dO.data_ptr(), d, dq.data_ptr(), d, dkk.data_ptr(), d, dv.data_ptr(), d, ptr(dbd), ldbd,
-                          ops.stream())
+    # the hash path (no keep-bit mask), dq without the rel-pos term (flags 0)
+    attn_fused_bwd(B=B, H=H, T1=T1, T2=T2, q=q, ldq=d, k=k, ldk=d, v=v, ldv=d, bu=u, bv=vb, pp=pp, ldp=d, klen=klen,
+                   causal=causal, scale=scale, p=p, seed=seed, O=O, ldo=d, lse=lse, dO=dO, lddo=d, dq=dq, lddq=d,
+                   dk=dkk, lddk=d, dv=dv, lddv=d, dbd=dbd, ldbd=ldbd)
     torch.cuda.synchronize()
     return O, dq, dkk, dv, dbd, ldbd
 
@@ -177,11 +178,12 @@ def test_fused_matches_unfused_with_dropout():
     (2, 2, 97, [97, 60], 0.1),
 ])
 def test_fused_bwd2_rel_terms(B, H, T, klens, p):
-    """ea_attn_fused_bwd2 (flags=1): dq includes the (q+v) path, per-block column sums give
-    the pos_bias_u / pos_bias_v gradients, qv_out = bf16(q + v); dq, dk, dv, dbd otherwise
-    equal ea_attn_fused_bwd's."""
+    """ea_attn_fused_bwd2 with flags=1 and the forward's keep bits: dq includes the (q+v)
+    path, per-block column sums give the pos_bias_u / pos_bias_v gradients, qv_out =
+    bf16(q + v); dk, dv, dbd equal the flags=0 / rehashing call's bit for bit."""
     from espnet_amd import hip_ops as ops
     from espnet_amd._lib import lib
+    from espnet_amd.layers.common import attn_fused_bwd
     q, k, v, u, vb, pp, dO = _inputs(B, H, T, T, True, seed=5)
     klen = torch.tensor(klens, dtype=torch.long, device=DEV)
     seed = 99
@@ -202,12 +204,10 @@ def test_fused_bwd2_rel_terms(B, H, T, klens, p):
     nqb = (T + 63) // 64
     part = torch.full((2, B * nqb, d), float("nan"), device=DEV)
     qv = torch.empty(B, T, d, dtype=bf, device=DEV)
-    rc = lib.ea_attn_fused_bwd2(B, H, T, T, 64, q.data_ptr(), d, k.data_ptr(), d, v.data_ptr(), d, u.data_ptr(),
-                                vb.data_ptr(), pp.data_ptr(), d, klen.data_ptr(), 0, scale, p, seed, O2.data_ptr(),
-                                d, lse.data_ptr(), dO.data_ptr(), d, dq.data_ptr(), d, dk.data_ptr(), d, dv.data_ptr(),
-                                d, dbd.data_ptr(), ldbd, part.data_ptr(), d, qv.data_ptr(), d, dmp, ldm, 1,
-                                ops.stream())
-    assert rc == 0
+    attn_fused_bwd(B=B, H=H, T1=T, T2=T, q=q, ldq=d, k=k, ldk=d, v=v, ldv=d, bu=u, bv=vb, pp=pp, ldp=d, klen=klen,
+                   causal=False, scale=scale, p=p, seed=seed, O=O2, ldo=d, lse=lse, dO=dO, lddo=d, dq=dq, lddq=d,
+                   dk=dk, lddk=d, dv=dv, lddv=d, dbd=dbd, ldbd=ldbd, part=part, ldpart=d, qv_out=qv, ldqv=d,
+                   dmask=dmask, ldm=ldm, flags=1)
     torch.cuda.synchronize()
     assert torch.equal(O2, O) and torch.equal(dk, dk1) and torch.equal(dv, dv1) and torch.equal(dbd, dbd1)
     assert torch.equal(qv, (q.float() + vb.view(1, 1, d)).to(bf))
@@ -234,9 +234,10 @@ def test_fused_bwd2_rel_terms(B, H, T, klens, p):
 @pytest.mark.parametrize("causal,T1,T2,klens", [(True, 45, 45, [45, 30]), (False, 45, 300, [300, 140])])
 def test_fused_dropout_mask_matches_rehash(causal, T1, T2, klens):
     """Decoder shapes with dropout: ea_attn_fused_fwd2's keep bits read by ea_attn_fused_bwd2
-    give exactly the gradients of the rehashing legacy entry (ea_attn_fused_bwd)."""
+    give exactly the gradients of its rehashing path (no mask)."""
     from espnet_amd import hip_ops as ops
     from espnet_amd._lib import lib
+    from espnet_amd.layers.common import attn_fused_bwd
     B, H, p, seed = 2, 2, 0.1, 4242
     q, k, v, _, _, _, dO = _inputs(B, H, T1, T2, False, seed=7)
     klen = torch.tensor(klens, dtype=torch.long, device=DEV)
@@ -250,10 +251,9 @@ def test_fused_dropout_mask_matches_rehash(causal, T1, T2, klens):
                            klen.data_ptr(), int(causal), 1 / 8, p, seed, O2.data_ptr(), d, lse.data_ptr(),
                            dmask.data_ptr(), ldm, ops.stream())
     dq, dk, dv = torch.empty_like(q), torch.empty_like(k), torch.empty_like(v)
-    lib.ea_attn_fused_bwd2(B, H, T1, T2, 64, q.data_ptr(), d, k.data_ptr(), d, v.data_ptr(), d, 0, 0, 0, 0,
-                           klen.data_ptr(), int(causal), 1 / 8, p, seed, O2.data_ptr(), d, lse.data_ptr(),
-                           dO.data_ptr(), d, dq.data_ptr(), d, dk.data_ptr(), d, dv.data_ptr(), d, 0, 0, 0, 0, 0, 0,
-                           dmask.data_ptr(), ldm, 0, ops.stream())
+    attn_fused_bwd(B=B, H=H, T1=T1, T2=T2, q=q, ldq=d, k=k, ldk=d, v=v, ldv=d, bu=None, bv=None, pp=None, ldp=0,
+                   klen=klen, causal=causal, scale=1 / 8, p=p, seed=seed, O=O2, ldo=d, lse=lse, dO=dO, lddo=d,
+                   dq=dq, lddq=d, dk=dk, lddk=d, dv=dv, lddv=d, dmask=dmask, ldm=ldm)
     torch.cuda.synchronize()
     assert torch.equal(O2, O)
     assert torch.equal(dq, dq1) and torch.equal(dk, dk1) and torch.equal(dv, dv1)
