@@ -485,23 +485,20 @@ __global__ __launch_bounds__(256, 2) void attn_bwdq_kernel(AttnP a) {
   const int kend = a.causal ? min(kl, i0 + QB) : kl;
   const int nch = (kend + KC - 1) / KC;
   bf16* dbd_h = REL && a.dbd ? a.dbd + ((long)h * a.B + b) * a.T1 * a.lddbd : nullptr;
-  if (dbd_h) {  // zeros off the part of each row the chunk loop writes: r < T-1-i, r >= T-1-i+jcov
+  if (dbd_h) {
+    // zeros off the part of each row the chunk loop writes (r < T-1-i, r >= T-1-i+jcov), in
+    // whole 8-column segments (lddbd % 8 == 0, 16-B aligned rows): a segment straddling the
+    // band edge is zeroed in full and its band columns are rewritten by this same wave's chunk
+    // stores, which the loop's first __syncthreads (vmcnt(0)) orders after these
     const int jcov = min(a.T2, nch * KC);
     const uint4 zero = make_uint4(0u, 0u, 0u, 0u);
-    for (int il = 0; il < 16; ++il) {  // 8-column segments (lddbd % 8 == 0, 16-B aligned rows)
+    for (int il = 0; il < 16; ++il) {
       const int i = i0 + 16 * w + il;
       if (i >= a.T1) break;
       bf16* drow = dbd_h + (long)i * a.lddbd;
       const int lo = a.T1 - 1 - i, hi = lo + jcov;
-      for (int c0 = 8 * lane; c0 < a.lddbd; c0 += 512) {
-        if (c0 + 8 <= lo || c0 >= hi) {
-          *(uint4*)(drow + c0) = zero;
-        } else if (c0 < lo || c0 + 8 > hi) {
-#pragma unroll
-          for (int e = 0; e < 8; ++e)
-            if (c0 + e < lo || c0 + e >= hi) drow[c0 + e] = (bf16)0.f;
-        }
-      }
+      for (int c0 = 8 * lane; c0 < a.lddbd; c0 += 512)
+        if (c0 < lo || c0 + 8 > hi) *(uint4*)(drow + c0) = zero;
     }
   }
   const bool use_mask = a.p > 0.f && a.dmask != nullptr;
