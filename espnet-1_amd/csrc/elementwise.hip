@@ -1034,3 +1034,12 @@ extern "C" int ea_conv1_wgrad(int B, int T, int F, int C, const float* x, const 
   if (rc) return rc;
   return ea_reduce_partials(nb, C, workspace + 9L * C, 10L * C, dbias, 1, stream);
 }
+
+extern "C" int ea_conv1_wgrad_reduce(int ntiles, int C, const float* part, float* dw, float* dbias, void* stream) {
+  EA_ENTRY();
+  EA_CHECK_ARG(ntiles >= 1 && C >= 1 && part && dw && dbias);
+  // weight: partial column t*C + c -> dw[c*9 + t]; bias: columns 9C .. 10C-1 (accumulating)
+  int rc = ea_reduce_partials_tr(ntiles, 9 * C, part, 10L * C, dw, 1, C, 9, stream);
+  if (rc) return rc;
+  return ea_reduce_partials(ntiles, C, part + 9L * C, 10L * C, dbias, 1, stream);
+}

@@ -44,6 +44,9 @@ struct GemmP {
   unsigned long long* stamp;       // kernel-span probe [first block start, last block end] or null
   ea_conv_geo g;                   // implicit-GEMM operand geometry (g.mode 0: dense operands)
   unsigned long long* diag;        // ea_gemm_set_diag: per-block [start, main loop done, end] s_memtime
+  const float* w1x;                // ea_gemm_conv_w1: conv1 input (B, w1T, w1F) f32, or null
+  float* w1part;                   //   per-M-tile conv1 weight / bias gradient partials
+  int w1T, w1F;
 };
 
 // Diagnostic timeline (ea_gemm_set_diag): thread 0 of each block stamps the shader clock at
@@ -1389,11 +1392,142 @@ EA_DEV void pipe_tile(const GemmP& p, char* smem, const bf16* A, const bf16* B, 
   __syncthreads();  // every wave is done reading the ring
 }
 
+// ---------------------------------------------------------------- conv1 weight gradient, fused
+// ea_gemm_conv_w1: the EA_CONV_DGRAD GEMM of Conv2dSubsampling's backward whose ReLU-masked
+// output g = d(conv1 pre-activation) (bf16-rounded, as the unfused path stores it) never goes
+// to HBM: each 256-row tile contributes its share of conv1's weight / bias gradient
+//   part[tm][t*C + c] = sum_{rows m of tile tm} g[m][c] * X[m][t],
+//   X[m][t] = x[b][2*t1 + t/3][2*f1 + t%3] (t < 9, pixel (b, t1, f1) of class-plane row m), 1 (t = 9)
+// as one more small MFMA product per wave: A = g^T (64 channels x 32 pixels, read from the
+// epilogue's f32 image), B = X (32 pixels x 16 taps) from an LDS image staged before the main
+// loop as bf16 hi + lo halves (x = hi + lo to 2^-16 relative).  The two wave groups' sums
+// are combined in fixed order; ea_conv1_wgrad_reduce sums the tiles.
+constexpr int W1_TS = 264;                              // X image tap row: 256 pixels + 8 (528 B)
+constexpr int W1_IMG = 16 * W1_TS * 2;                  // one half (hi or lo), bytes
+constexpr int W1_SMEM = PipeT<256>::SMEM + 2 * W1_IMG;  // 152 KiB
+
+EA_DEV void w1_stage_x(const GemmP& p, char* xs, int m0) {
+  bf16* hi = (bf16*)xs;
+  bf16* lo = (bf16*)(xs + W1_IMG);
+  const int tid = threadIdx.x;
+  const int row = tid >> 1, t0 = (tid & 1) * 5;  // 512 threads: 256 rows x 2 halves of taps 0..9
+  const int m = m0 + row;
+  float xv[5] = {0.f, 0.f, 0.f, 0.f, 0.f};
+  if (m < p.M) {
+    const int a = p.g.a, e = p.g.e, nI = p.g.nI[a], nJ = p.g.nJ[e];
+    const int bi = fdiv(m, nJ), j = m - bi * nJ;
+    const int b = fdiv(bi, nI), i = bi - b * nI;
+    const float* xp = p.w1x + ((long)b * p.w1T + 2 * (2 * i + a)) * p.w1F + 2 * (2 * j + e);
+#pragma unroll
+    for (int u = 0; u < 5; ++u) {
+      const int t = t0 + u;
+      xv[u] = t < 9 ? xp[(t / 3) * p.w1F + t % 3] : 1.f;
+    }
+  }
+#pragma unroll
+  for (int u = 0; u < 5; ++u) {
+    const bf16 h = (bf16)xv[u];
+    hi[(t0 + u) * W1_TS + row] = h;
+    lo[(t0 + u) * W1_TS + row] = (bf16)(xv[u] - (float)h);
+  }
+  for (int q = tid; q < 6 * 256; q += 512) {  // taps 10..15: zero
+    const int t = 10 + (q >> 8), r = q & 255;
+    hi[t * W1_TS + r] = (bf16)0.f;
+    lo[t * W1_TS + r] = (bf16)0.f;
+  }
+}
+
+// one wave's 128 x 64 (rows wm.., channels wn..) share; acc as pipe_tile leaves it
+EA_DEV void w1_epilogue(const GemmP& p, char* smem, int m0, int n0, int wm, int wn, int lane, int w, int tm,
+                        const f32x4 (&acc)[8][4]) {
+  float* t = (float*)smem + w * 64 * EPI_LDT;  // the wave's 64 x 64 f32 image
+  const char* xh = smem + PipeT<256>::SMEM;
+  const char* xl = xh + W1_IMG;
+  const int g = lane >> 4, lc = lane & 15, rq = g * 4;
+  const int lc8 = (lane & 7) * 8, rl = lane >> 3;
+  const bf16* aux = (const bf16*)p.epi.aux;
+  f32x4 out[4];
+#pragma unroll
+  for (int cb = 0; cb < 4; ++cb) out[cb] = (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int ch = 0; ch < 2; ++ch) {  // 64-row chunks
+    if (ch) {
+      __builtin_amdgcn_wave_barrier();
+      asm volatile("" ::: "memory");
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int rr = 0; rr < 4; ++rr) t[(i * 16 + rq + rr) * EPI_LDT + j * 16 + lc] = acc[ch * 4 + i][j][rr];
+    __builtin_amdgcn_wave_barrier();
+    asm volatile("" ::: "memory");
+    // ReLU mask (aux = conv1 output) and bf16 rounding, in place: lane = 8 columns of a row
+    const int rb = m0 + wm + ch * 64, col = n0 + wn + lc8;
+#pragma unroll
+    for (int h0 = 0; h0 < 8; h0 += 4) {
+      float o[4][8];
+#pragma unroll
+      for (int it = 0; it < 4; ++it)
+        ld8(aux, (long)min(rb + (h0 + it) * 8 + rl, p.M - 1) * p.epi.ldaux + col, EA_BF16, o[it]);
+#pragma unroll
+      for (int it = 0; it < 4; ++it) {
+        float* tr = t + ((h0 + it) * 8 + rl) * EPI_LDT + lc8;
+        float4 f0 = *(const float4*)tr, f1 = *(const float4*)(tr + 4);
+        float v[8] = {f0.x, f0.y, f0.z, f0.w, f1.x, f1.y, f1.z, f1.w};
+#pragma unroll
+        for (int c = 0; c < 8; ++c) v[c] = (float)(bf16)(o[it][c] > 0.f ? v[c] : 0.f);
+        *(float4*)tr = make_float4(v[0], v[1], v[2], v[3]);
+        *(float4*)(tr + 4) = make_float4(v[4], v[5], v[6], v[7]);
+      }
+    }
+    __builtin_amdgcn_wave_barrier();
+    asm volatile("" ::: "memory");
+    // out[cb][co, tap] += g^T . X over the chunk's 64 pixels (2 k-steps of 32)
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      const int pl = wm + ch * 64 + 32 * ks + 8 * g;  // tile-local pixel of k = 8g
+      const bf16x8 bh = *(const bf16x8*)(xh + (lc * W1_TS + pl) * 2);
+      const bf16x8 bl = *(const bf16x8*)(xl + (lc * W1_TS + pl) * 2);
+#pragma unroll
+      for (int cb = 0; cb < 4; ++cb) {
+        union { bf16x8 v; bf16 e[8]; } af;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) af.e[e] = (bf16)t[(32 * ks + 8 * g + e) * EPI_LDT + 16 * cb + lc];
+        out[cb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af.v, bh, out[cb], 0, 0, 0);
+        out[cb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af.v, bl, out[cb], 0, 0, 0);
+      }
+    }
+  }
+  // G1 (rows 128..255) hands its sums to G0 (same channels) through LDS; G0 writes the tile's
+  // partial: rows co = 16cb + 4g + r of the wave's 64 channels, column tap lc
+  __syncthreads();
+  float* cmb = (float*)smem;  // [4][64][16], over the (now free) epilogue images
+  if (w >= 4) {
+#pragma unroll
+    for (int cb = 0; cb < 4; ++cb)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) cmb[((w - 4) * 64 + 16 * cb + 4 * g + r) * 16 + lc] = out[cb][r];
+  }
+  __syncthreads();
+  if (w < 4 && lc < 10) {
+    float* prow = p.w1part + (long)tm * 10 * p.N + (long)lc * p.N;
+#pragma unroll
+    for (int cb = 0; cb < 4; ++cb)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int co = n0 + wn + 16 * cb + 4 * g + r;
+        if (co < p.N) prow[co] = out[cb][r] + cmb[(w * 64 + 16 * cb + 4 * g + r) * 16 + lc];
+      }
+  }
+}
+
 template <bool AK, bool BKM, int MODE = 0, int BT = 256>
 __global__ __launch_bounds__(512, PipeT<BT>::OCC) void gemm_pipe(GemmP p) {
   using PC = PipeT<BT>;
   constexpr int MI = PC::MI;
-  __shared__ __attribute__((aligned(1024))) char smem[PC::SMEM];
+  __shared__ __attribute__((aligned(1024))) char smem[MODE == EA_CONV_DGRAD ? W1_SMEM : PC::SMEM];
   probe_start(p);
 
   const int nt = p.tiles_m * p.tiles_n;
@@ -1422,8 +1556,18 @@ __global__ __launch_bounds__(512, PipeT<BT>::OCC) void gemm_pipe(GemmP p) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
   diag_stamp(p, 0);
+  if constexpr (MODE == EA_CONV_DGRAD) {
+    if (p.w1part) w1_stage_x(p, smem + PC::SMEM, m0);  // ordered by pipe_tile's first barrier
+  }
   pipe_tile<AK, BKM, MODE, BT>(p, smem, A, B, m0, n0, kbeg, kend, acc);
   diag_stamp(p, 1);
+  if constexpr (MODE == EA_CONV_DGRAD) {
+    if (p.w1part) {
+      w1_epilogue(p, smem, m0, n0, wm, wn, lane, w, tm, acc);
+      probe_end(p);
+      return;
+    }
+  }
   const EpiK ek = make_epik(p);
   switch (p.splitk > 1 ? EA_EPI_STORE : p.epi.kind) {
     case EA_EPI_STORE: epi_wave<EA_EPI_STORE, MI, 4>(p, ek, smem, z, zb, zh, m0 + wm, n0 + wn, lane, w, acc); break;
@@ -1713,7 +1857,8 @@ static int gemm_impl(int dtype, int a_kmajor, int b_kmajor, int M, int N, int K,
                      int batch, int nh,
                      void* C, int c_dtype, long ldc, long sCb, long sCh,
                      const ea_epilogue* epi, float* workspace, long ws_elems, void* stream,
-                     const ea_conv_geo* geo) {
+                     const ea_conv_geo* geo, const float* w1x = nullptr, int w1T = 0, int w1F = 0,
+                     float* w1part = nullptr) {
   EA_CHECK_ARG(epi != nullptr && M >= 0 && N >= 0 && K >= 0 && batch >= 1 && nh >= 1);
   EA_CHECK_ARG(dtype == EA_F32 || dtype == EA_BF16);
   if (M == 0 || N == 0) return 0;
@@ -1733,6 +1878,7 @@ static int gemm_impl(int dtype, int a_kmajor, int b_kmajor, int M, int N, int K,
   p.stamp = g_probe;
   p.diag = g_diag;
   p.g = geo ? *geo : ea_conv_geo{};
+  p.w1x = w1x; p.w1part = w1part; p.w1T = w1T; p.w1F = w1F;
   // unaligned operands (odd vocab / leading dims) take the element-wise load path
   p.vec_a = (lda % E == 0 && sAb % E == 0 && sAh % E == 0 && ((uintptr_t)A % 16) == 0);
   p.vec_b = (ldb % E == 0 && sBb % E == 0 && sBh % E == 0 && ((uintptr_t)B % 16) == 0);
@@ -1764,6 +1910,10 @@ static int gemm_impl(int dtype, int a_kmajor, int b_kmajor, int M, int N, int K,
     // weight gradient: few output tiles over a huge K (pixels) -> 256x256 tiles (the higher
     // per-CU MFMA rate) split over K to ~one block per CU (split rule below)
     if (geo->mode == EA_CONV_WGRAD && !g_force_bm) { p.bm = 256; p.bn = 256; }
+    if (w1part) {  // the fused conv1-gradient epilogue lives in the 256 x 256 ping-pong kernel
+      if (!g_gemm_pipe || !p.vec8) return EA_ERR_BAD_ARG;
+      p.bm = 256; p.bn = 256;
+    }
     if (p.bm != 256 || p.bn != 256) { p.bm = 128; p.bn = 128; }
   } else if (lds_path) {
     choose_tile(p, a_kmajor, (long)batch * nh);
@@ -1831,6 +1981,18 @@ extern "C" int ea_gemm_conv(const ea_conv_geo* geo, int a_kmajor, int b_kmajor, 
   EA_CHECK_ARG(geo != nullptr && geo->mode >= EA_CONV_FWD && geo->mode <= EA_CONV_WGRAD);
   return gemm_impl(EA_BF16, a_kmajor, b_kmajor, M, N, K, A, lda, 0, 0, B, ldb, 0, 0, 1, 1, C, c_dtype, ldc, 0, 0,
                    epi, workspace, ws_elems, stream, geo);
+}
+
+extern "C" int ea_gemm_conv_w1(const ea_conv_geo* geo, int M, int N, int K, const void* A, long lda, const void* B,
+                               long ldb, const ea_epilogue* epi, const float* x, int T, int Fin, float* part,
+                               void* stream) {
+  EA_ENTRY();
+  EA_CHECK_ARG(geo != nullptr && geo->mode == EA_CONV_DGRAD && x != nullptr && part != nullptr);
+  EA_CHECK_ARG(epi != nullptr && epi->kind == EA_EPI_DACT && epi->act == EA_ACT_RELU && epi->aux != nullptr &&
+               epi->aux_dtype == EA_BF16);
+  EA_CHECK_ARG(T >= 3 && Fin >= 3 && M < (1 << 24));
+  return gemm_impl(EA_BF16, 1, 0, M, N, K, A, lda, 0, 0, B, ldb, 0, 0, 1, 1, nullptr, EA_BF16, N, 0, 0, epi,
+                   nullptr, 0, stream, geo, x, T, Fin, part);
 }
 
 static long grouped_ws_bytes(int n, long ntiles) { return (long)n * (long)sizeof(GroupProbD) + 4 * ntiles + 256; }

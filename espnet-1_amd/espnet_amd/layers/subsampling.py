@@ -13,6 +13,7 @@ from __future__ import annotations
 
 import ctypes
 import math
+import os
 
 import torch
 from torch import nn
@@ -37,6 +38,10 @@ def phase_geo(B, T1, F1, T2, F2, C, mode, a=0, e=0, zero=0):
         off += rows[i]
     g.a, g.e, g.zero = a, e, zero
     return g, nI, nJ, rows
+
+
+# conv1's weight gradient fused into conv2's input-gradient epilogue (ea_gemm_conv_w1)
+FUSE_CONV1_WGRAD = os.environ.get("EA_FUSE_CONV1_WGRAD", "1") != "0"
 
 
 def _implicit_ok(cd, C):
@@ -228,11 +233,20 @@ class SubsampleFn(torch.autograd.Function):
                              ws_side.numel(), ops.stream())
             ops.permute3(dw2, b.g("conv.2.weight"), C, 9, C, accumulate=True)  # (Co,9,Ci) -> (Co,Ci,9)
         # input gradient per parity class (a, e): sub-pixel decomposition of the transposed
-        # conv, ReLU mask of conv1 fused (DACT with aux = x1p)
-        dx1p = empty(P1, C, dtype=cd, device=dev)
+        # conv, ReLU mask of conv1 fused (DACT with aux = x1p).  By default the masked gradient
+        # stays on chip: each tile's epilogue multiplies it by conv1's input patches
+        # (ea_gemm_conv_w1), so dx1 is never written and conv1's weight / bias gradients are
+        # the sum of per-tile partials
         ws = ops.workspace(ops._SPLITK_WS, dev)
         w2t = empty(9, C, C, dtype=cd, device=dev)  # tap-major: every tap's (co, ci) block dense
         ops.permute3(b.f("conv.2.weight"), w2t, 1, C * C, 9)  # (Co,Ci,9) -> (9,Co,Ci)
+        fuse = FUSE_CONV1_WGRAD
+        if fuse:
+            _, _, _, rows_all = phase_geo(B, T1, F1, T2, F2, C, CONV_DGRAD)
+            part = empty(sum((r + 255) // 256 for r in rows_all) * 10 * C, device=dev)
+            tile0 = 0
+        else:
+            dx1p = empty(P1, C, dtype=cd, device=dev)
         for a in (0, 1):
             for e in (0, 1):
                 geo, nI, nJ, rows = phase_geo(B, T1, F1, T2, F2, C, CONV_DGRAD, a=a, e=e, zero=P2 * C)
@@ -243,13 +257,23 @@ class SubsampleFn(torch.autograd.Function):
                 o = geo.plane[a * 2 + e] // C
                 aux = x1p[o:o + Mc]
                 epi = ops.make_epi(EPI_DACT, act=ACT_RELU, aux=aux)
-                lib.ea_gemm_conv(ctypes.byref(geo), 1, 0, Mc, C, ntaps * C, dx2.data_ptr(), C, w2t.data_ptr(),
-                                 C, dx1p[o:o + Mc].data_ptr(), ops.dt(dx1p), C, ctypes.byref(epi),
-                                 ws.data_ptr(), ws.numel(), ops.stream())
-        with ops.wgrad(dx1p, feats):
-            w, wn = ops._ws(dev, 1024 * 10 * C)
-            lib.ea_conv1_wgrad(B, T, Fin, C, feats.data_ptr(), dx1p.data_ptr(), ops.dt(dx1p),
-                               b.g("conv.0.weight").data_ptr(), b.g("conv.0.bias").data_ptr(), w, wn, ops.stream())
+                if fuse:
+                    lib.ea_gemm_conv_w1(ctypes.byref(geo), Mc, C, ntaps * C, dx2.data_ptr(), C, w2t.data_ptr(), C,
+                                        ctypes.byref(epi), feats.data_ptr(), T, Fin,
+                                        part.data_ptr() + 4 * tile0 * 10 * C, ops.stream())
+                    tile0 += (Mc + 255) // 256
+                else:
+                    lib.ea_gemm_conv(ctypes.byref(geo), 1, 0, Mc, C, ntaps * C, dx2.data_ptr(), C, w2t.data_ptr(),
+                                     C, dx1p[o:o + Mc].data_ptr(), ops.dt(dx1p), C, ctypes.byref(epi),
+                                     ws.data_ptr(), ws.numel(), ops.stream())
+        if fuse:
+            lib.ea_conv1_wgrad_reduce(tile0, C, part.data_ptr(), b.g("conv.0.weight").data_ptr(),
+                                      b.g("conv.0.bias").data_ptr(), ops.stream())
+        else:
+            with ops.wgrad(dx1p, feats):
+                w, wn = ops._ws(dev, 1024 * 10 * C)
+                lib.ea_conv1_wgrad(B, T, Fin, C, feats.data_ptr(), dx1p.data_ptr(), ops.dt(dx1p),
+                                   b.g("conv.0.weight").data_ptr(), b.g("conv.0.bias").data_ptr(), w, wn, ops.stream())
         ops.grad_ready(b)
         return None, None, None, None, None
 

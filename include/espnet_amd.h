@@ -96,6 +96,19 @@ typedef struct ea_conv_geo {
 int ea_gemm_conv(const ea_conv_geo* geo, int a_kmajor, int b_kmajor, int M, int N, int K,
                  const void* A, long lda, const void* B, long ldb, void* C, int c_dtype, long ldc,
                  const ea_epilogue* epi, float* workspace, long ws_elems, void* stream);
+/* The EA_CONV_DGRAD launch of one parity class fused with conv1's weight gradient: the
+ * ReLU-masked input gradient g (epi: EA_EPI_DACT, EA_ACT_RELU, aux = the class plane of x1p,
+ * bf16) is not stored; instead each 256-row tile tm writes
+ *   part[tm*10*N + t*N + c] = sum over its rows m of bf16(g[m][c]) * X[m][t],
+ *   X = x[b][2*t1 + t/3][2*f1 + t%3] (t < 9) for the pixel (b, t1, f1) of class-plane row m,
+ *   X = 1 (t = 9),
+ * x = the conv1 input (B, T, Fin) f32 — subsampling.py conv.0's weight / bias gradient
+ * (torch Conv2d backward) without the dx1 round trip through HBM.  part holds ceil(M/256)
+ * tiles; ea_conv1_wgrad_reduce sums any number of such tiles into dw [N][9] / dbias [N]. */
+int ea_gemm_conv_w1(const ea_conv_geo* geo, int M, int N, int K, const void* A, long lda, const void* B,
+                    long ldb, const ea_epilogue* epi, const float* x, int T, int Fin, float* part,
+                    void* stream);
+int ea_conv1_wgrad_reduce(int ntiles, int C, const float* part, float* dw, float* dbias, void* stream);
 
 /* Select the bf16 GEMM main loop: 2 = LDS-DMA (global_load_lds) 2-stage ring (default),
  * 0 = register-staged loop; 12 = same ring without 64-row tiles.

@@ -63,7 +63,10 @@ def test_implicit_pipe_kernel_matches_lds_kernel(C, B, T):
     gradient) on the ping-pong kernel (gemm_pipe) against gemm_bf16_lds, both on 256x256
     tiles: the same K order and the same split, so the results agree to the bit."""
     from espnet_amd._lib import GEMM_PIPE, lib
+    from espnet_amd.layers import subsampling as S
     lib.ea_gemm_set_tile(256, 256)
+    fuse = S.FUSE_CONV1_WGRAD
+    S.FUSE_CONV1_WGRAD = False  # the fused conv1 epilogue exists on the ping-pong kernel only
     try:
         lib.ea_gemm_set_pipe(0)
         y0, g0 = _run(C, B, T, True, torch.bfloat16)
@@ -72,6 +75,32 @@ def test_implicit_pipe_kernel_matches_lds_kernel(C, B, T):
     finally:
         lib.ea_gemm_set_tile(0, 0)
         lib.ea_gemm_set_pipe(GEMM_PIPE)
+        S.FUSE_CONV1_WGRAD = fuse
     assert torch.equal(y0, y1)
     for k in g0:
         assert torch.equal(g0[k], g1[k]), k
+
+
+@pytest.mark.parametrize("C,B,T", [(64, 3, 61), (512, 2, 131), (256, 4, 300)])
+def test_fused_conv1_wgrad_matches_unfused(C, B, T):
+    """ea_gemm_conv_w1: conv1's weight / bias gradient from the conv2 input-gradient tiles'
+    epilogues equals the unfused route (dx1 stored in bf16, then ea_conv1_wgrad) up to the
+    f32 summation order (the masked gradient is bf16-rounded in both; the input patches enter
+    the MFMA as bf16 hi + lo halves); every other output is bit-identical."""
+    from espnet_amd.layers import subsampling as S
+    fuse = S.FUSE_CONV1_WGRAD
+    try:
+        S.FUSE_CONV1_WGRAD = False
+        y0, g0 = _run(C, B, T, True, torch.bfloat16)
+        S.FUSE_CONV1_WGRAD = True
+        y1, g1 = _run(C, B, T, True, torch.bfloat16)
+    finally:
+        S.FUSE_CONV1_WGRAD = fuse
+    assert torch.equal(y0, y1)
+    for k in g0:
+        if k.startswith("conv.0."):
+            # two f32 summation orders over ~10^5 pixels whose products largely cancel
+            # (measured 3.3e-5 at C=512)
+            assert _rel(g1[k], g0[k]) < 2e-4, (k, _rel(g1[k], g0[k]))
+        else:
+            assert torch.equal(g0[k], g1[k]), k
