@@ -88,7 +88,8 @@ EA_DEV long phase_row(const PhaseGeo& g, int b, int t1, int f1) {
 template <typename TO>
 __global__ __launch_bounds__(256) void conv1_fwd_kernel(int B, int T, int F, PhaseGeo g, int C,
                                                         const float* __restrict__ x, const float* __restrict__ w,
-                                                        const float* __restrict__ bias, TO* __restrict__ y) {
+                                                        const float* __restrict__ bias, TO* __restrict__ y,
+                                                        uint8_t* __restrict__ pos) {
   const int groups = C / 8;
   const int cg = threadIdx.x % groups;  // blockDim.x is a multiple of C/8
   const int c0 = cg * 8;
@@ -119,10 +120,17 @@ __global__ __launch_bounds__(256) void conv1_fwd_kernel(int B, int T, int F, Pha
       for (int t = 0; t < 9; ++t) a = fmaf(wr[k][t], xv[t], a);
       o[k] = a > 0.f ? a : 0.f;
     }
-    TO* yp = y + phase_row(g, b, t1, f1) * C + c0;
+    const long prow = phase_row(g, b, t1, f1);
+    TO* yp = y + prow * C + c0;
     float lo[4] = {o[0], o[1], o[2], o[3]}, hi[4] = {o[4], o[5], o[6], o[7]};
     vst4(yp, lo);
     vst4(yp + 4, hi);
+    if (pos) {  // ReLU support bits of the stored (rounded) outputs: bit k = channel c0 + k > 0
+      uint32_t m = 0;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) m |= (uint32_t)((float)(TO)o[k] > 0.f) << k;
+      pos[prow * (C / 8) + cg] = (uint8_t)m;
+    }
   }
 }
 
@@ -992,8 +1000,8 @@ static PhaseGeo phase_geo(int B, int T1, int F1, int C) {
   return g;
 }
 
-extern "C" int ea_conv1_fwd(int B, int T, int F, int C, const float* x, const float* w, const float* bias,
-                            void* x1p, int dtype, void* stream) {
+extern "C" int ea_conv1_fwd2(int B, int T, int F, int C, const float* x, const float* w, const float* bias,
+                             void* x1p, int dtype, unsigned char* pos, void* stream) {
   EA_ENTRY();
   EA_CHECK_ARG(C % 8 == 0 && 256 % (C / 8) == 0 && T >= 3 && F >= 3);
   const int T1 = (T - 3) / 2 + 1, F1 = (F - 3) / 2 + 1;
@@ -1003,12 +1011,17 @@ extern "C" int ea_conv1_fwd(int B, int T, int F, int C, const float* x, const fl
   dim3 grid(ea_grid_cap(ea_cdiv(npix, ppb), 4096));
   if (dtype == EA_BF16)
     hipLaunchKernelGGL(conv1_fwd_kernel<bf16>, grid, dim3(256), 0, (hipStream_t)stream, B, T, F, g, C, x, w, bias,
-                       (bf16*)x1p);
+                       (bf16*)x1p, pos);
   else
     hipLaunchKernelGGL(conv1_fwd_kernel<float>, grid, dim3(256), 0, (hipStream_t)stream, B, T, F, g, C, x, w, bias,
-                       (float*)x1p);
+                       (float*)x1p, pos);
   EA_LAUNCH_CHECK();
   return 0;
+}
+
+extern "C" int ea_conv1_fwd(int B, int T, int F, int C, const float* x, const float* w, const float* bias,
+                            void* x1p, int dtype, void* stream) {
+  return ea_conv1_fwd2(B, T, F, C, x, w, bias, x1p, dtype, nullptr, stream);
 }
 
 extern "C" int ea_conv1_wgrad(int B, int T, int F, int C, const float* x, const void* dh, int dtype, float* dw,

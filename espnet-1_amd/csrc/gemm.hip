@@ -46,6 +46,7 @@ struct GemmP {
   unsigned long long* diag;        // ea_gemm_set_diag: per-block [start, main loop done, end] s_memtime
   const float* w1x;                // ea_gemm_conv_w1: conv1 input (B, w1T, w1F) f32, or null
   float* w1part;                   //   per-M-tile conv1 weight / bias gradient partials
+  const uint8_t* w1pos;            //   ReLU support bits (N/8 bytes per row) instead of aux, or null
   int w1T, w1F;
 };
 
@@ -1463,23 +1464,41 @@ EA_DEV void w1_epilogue(const GemmP& p, char* smem, int m0, int n0, int wm, int 
         for (int rr = 0; rr < 4; ++rr) t[(i * 16 + rq + rr) * EPI_LDT + j * 16 + lc] = acc[ch * 4 + i][j][rr];
     __builtin_amdgcn_wave_barrier();
     asm volatile("" ::: "memory");
-    // ReLU mask (aux = conv1 output) and bf16 rounding, in place: lane = 8 columns of a row
+    // ReLU mask (support bits, else aux = conv1 output) and bf16 rounding, in place: lane = 8
+    // columns of a row
     const int rb = m0 + wm + ch * 64, col = n0 + wn + lc8;
+    if (p.w1pos) {
+      uint32_t mb[8];
 #pragma unroll
-    for (int h0 = 0; h0 < 8; h0 += 4) {
-      float o[4][8];
+      for (int it = 0; it < 8; ++it)
+        mb[it] = p.w1pos[(long)min(rb + it * 8 + rl, p.M - 1) * (p.N >> 3) + min(col, p.N - 8) / 8];
 #pragma unroll
-      for (int it = 0; it < 4; ++it)
-        ld8(aux, (long)min(rb + (h0 + it) * 8 + rl, p.M - 1) * p.epi.ldaux + col, EA_BF16, o[it]);
-#pragma unroll
-      for (int it = 0; it < 4; ++it) {
-        float* tr = t + ((h0 + it) * 8 + rl) * EPI_LDT + lc8;
+      for (int it = 0; it < 8; ++it) {
+        float* tr = t + (it * 8 + rl) * EPI_LDT + lc8;
         float4 f0 = *(const float4*)tr, f1 = *(const float4*)(tr + 4);
         float v[8] = {f0.x, f0.y, f0.z, f0.w, f1.x, f1.y, f1.z, f1.w};
 #pragma unroll
-        for (int c = 0; c < 8; ++c) v[c] = (float)(bf16)(o[it][c] > 0.f ? v[c] : 0.f);
+        for (int c = 0; c < 8; ++c) v[c] = (float)(bf16)(((mb[it] >> c) & 1u) ? v[c] : 0.f);
         *(float4*)tr = make_float4(v[0], v[1], v[2], v[3]);
         *(float4*)(tr + 4) = make_float4(v[4], v[5], v[6], v[7]);
+      }
+    } else {
+#pragma unroll
+      for (int h0 = 0; h0 < 8; h0 += 4) {
+        float o[4][8];
+#pragma unroll
+        for (int it = 0; it < 4; ++it)
+          ld8(aux, (long)min(rb + (h0 + it) * 8 + rl, p.M - 1) * p.epi.ldaux + col, EA_BF16, o[it]);
+#pragma unroll
+        for (int it = 0; it < 4; ++it) {
+          float* tr = t + ((h0 + it) * 8 + rl) * EPI_LDT + lc8;
+          float4 f0 = *(const float4*)tr, f1 = *(const float4*)(tr + 4);
+          float v[8] = {f0.x, f0.y, f0.z, f0.w, f1.x, f1.y, f1.z, f1.w};
+#pragma unroll
+          for (int c = 0; c < 8; ++c) v[c] = (float)(bf16)(o[it][c] > 0.f ? v[c] : 0.f);
+          *(float4*)tr = make_float4(v[0], v[1], v[2], v[3]);
+          *(float4*)(tr + 4) = make_float4(v[4], v[5], v[6], v[7]);
+        }
       }
     }
     __builtin_amdgcn_wave_barrier();
@@ -1858,7 +1877,7 @@ static int gemm_impl(int dtype, int a_kmajor, int b_kmajor, int M, int N, int K,
                      void* C, int c_dtype, long ldc, long sCb, long sCh,
                      const ea_epilogue* epi, float* workspace, long ws_elems, void* stream,
                      const ea_conv_geo* geo, const float* w1x = nullptr, int w1T = 0, int w1F = 0,
-                     float* w1part = nullptr) {
+                     float* w1part = nullptr, const uint8_t* w1pos = nullptr) {
   EA_CHECK_ARG(epi != nullptr && M >= 0 && N >= 0 && K >= 0 && batch >= 1 && nh >= 1);
   EA_CHECK_ARG(dtype == EA_F32 || dtype == EA_BF16);
   if (M == 0 || N == 0) return 0;
@@ -1878,7 +1897,7 @@ static int gemm_impl(int dtype, int a_kmajor, int b_kmajor, int M, int N, int K,
   p.stamp = g_probe;
   p.diag = g_diag;
   p.g = geo ? *geo : ea_conv_geo{};
-  p.w1x = w1x; p.w1part = w1part; p.w1T = w1T; p.w1F = w1F;
+  p.w1x = w1x; p.w1part = w1part; p.w1pos = w1pos; p.w1T = w1T; p.w1F = w1F;
   // unaligned operands (odd vocab / leading dims) take the element-wise load path
   p.vec_a = (lda % E == 0 && sAb % E == 0 && sAh % E == 0 && ((uintptr_t)A % 16) == 0);
   p.vec_b = (ldb % E == 0 && sBb % E == 0 && sBh % E == 0 && ((uintptr_t)B % 16) == 0);
@@ -1993,6 +2012,17 @@ extern "C" int ea_gemm_conv_w1(const ea_conv_geo* geo, int M, int N, int K, cons
   EA_CHECK_ARG(T >= 3 && Fin >= 3 && M < (1 << 24));
   return gemm_impl(EA_BF16, 1, 0, M, N, K, A, lda, 0, 0, B, ldb, 0, 0, 1, 1, nullptr, EA_BF16, N, 0, 0, epi,
                    nullptr, 0, stream, geo, x, T, Fin, part);
+}
+
+extern "C" int ea_gemm_conv_w1b(const ea_conv_geo* geo, int M, int N, int K, const void* A, long lda, const void* B,
+                                long ldb, const ea_epilogue* epi, const float* x, int T, int Fin, float* part,
+                                const unsigned char* pos, void* stream) {
+  EA_ENTRY();
+  EA_CHECK_ARG(geo != nullptr && geo->mode == EA_CONV_DGRAD && x != nullptr && part != nullptr && pos != nullptr);
+  EA_CHECK_ARG(epi != nullptr && epi->kind == EA_EPI_DACT && epi->act == EA_ACT_RELU && N % 8 == 0);
+  EA_CHECK_ARG(T >= 3 && Fin >= 3 && M < (1 << 24));
+  return gemm_impl(EA_BF16, 1, 0, M, N, K, A, lda, 0, 0, B, ldb, 0, 0, 1, 1, nullptr, EA_BF16, N, 0, 0, epi,
+                   nullptr, 0, stream, geo, x, T, Fin, part, pos);
 }
 
 static long grouped_ws_bytes(int n, long ntiles) { return (long)n * (long)sizeof(GroupProbD) + 4 * ntiles + 256; }

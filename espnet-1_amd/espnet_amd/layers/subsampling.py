@@ -42,6 +42,8 @@ def phase_geo(B, T1, F1, T2, F2, C, mode, a=0, e=0, zero=0):
 
 # conv1's weight gradient fused into conv2's input-gradient epilogue (ea_gemm_conv_w1)
 FUSE_CONV1_WGRAD = os.environ.get("EA_FUSE_CONV1_WGRAD", "1") != "0"
+# ... with conv1's ReLU mask from support bits written by the forward (else the bf16 x1p rows)
+CONV1_POS_BITS = os.environ.get("EA_CONV1_POS_BITS", "1") != "0"
 
 
 def _implicit_ok(cd, C):
@@ -168,8 +170,12 @@ class SubsampleFn(torch.autograd.Function):
         P1, P2 = B * T1 * F1, B * T2 * F2
         x1p = empty(P1 + 64, C, dtype=cd, device=dev)  # + 64 zero rows (wgrad gather padding)
         x1p[P1:].zero_()
-        lib.ea_conv1_fwd(B, T, Fin, C, feats.data_ptr(), b.f("conv.0.weight").data_ptr(),
-                         b.f("conv.0.bias").data_ptr(), x1p.data_ptr(), ops.dt(x1p), ops.stream())
+        # ReLU support bits of x1p for the fused backward's mask (1/16 of x1p's bytes)
+        pos1 = (torch.empty(P1 * C // 8, dtype=torch.uint8, device=dev)
+                if training and FUSE_CONV1_WGRAD and CONV1_POS_BITS else None)
+        lib.ea_conv1_fwd2(B, T, Fin, C, feats.data_ptr(), b.f("conv.0.weight").data_ptr(),
+                          b.f("conv.0.bias").data_ptr(), x1p.data_ptr(), ops.dt(x1p),
+                          0 if pos1 is None else pos1.data_ptr(), ops.stream())
         w2 = empty(C, 9 * C, dtype=cd, device=dev)
         ops.permute3(b.f("conv.2.weight"), w2, C, C, 9)  # (Co,Ci,9) -> (Co,9,Ci)
         x2 = empty(P2, C, dtype=cd, device=dev)
@@ -192,7 +198,7 @@ class SubsampleFn(torch.autograd.Function):
         ctx.m = m
         ctx.implicit = True
         ctx.meta = (B, T, Fin, T1, F1, T2, F2, p, seed)
-        ctx.save = (feats, x1p, w2, x2, wl)
+        ctx.save = (feats, x1p, w2, x2, wl, pos1)
         return y.view(B, T2, C)
 
     @staticmethod
@@ -201,7 +207,7 @@ class SubsampleFn(torch.autograd.Function):
         b = m._b
         cd = b.cd
         B, T, Fin, T1, F1, T2, F2, p, seed = ctx.meta
-        feats, x1p, w2, x2, wl = ctx.save
+        feats, x1p, w2, x2, wl, pos1 = ctx.save
         ctx.save = None
         C = m.odim
         dev = dy.device
@@ -257,10 +263,16 @@ class SubsampleFn(torch.autograd.Function):
                 o = geo.plane[a * 2 + e] // C
                 aux = x1p[o:o + Mc]
                 epi = ops.make_epi(EPI_DACT, act=ACT_RELU, aux=aux)
-                if fuse:
+                if fuse and pos1 is None:
                     lib.ea_gemm_conv_w1(ctypes.byref(geo), Mc, C, ntaps * C, dx2.data_ptr(), C, w2t.data_ptr(), C,
                                         ctypes.byref(epi), feats.data_ptr(), T, Fin,
                                         part.data_ptr() + 4 * tile0 * 10 * C, ops.stream())
+                    tile0 += (Mc + 255) // 256
+                elif fuse:
+                    lib.ea_gemm_conv_w1b(ctypes.byref(geo), Mc, C, ntaps * C, dx2.data_ptr(), C, w2t.data_ptr(), C,
+                                         ctypes.byref(epi), feats.data_ptr(), T, Fin,
+                                         part.data_ptr() + 4 * tile0 * 10 * C, pos1.data_ptr() + o * (C // 8),
+                                         ops.stream())
                     tile0 += (Mc + 255) // 256
                 else:
                     lib.ea_gemm_conv(ctypes.byref(geo), 1, 0, Mc, C, ntaps * C, dx2.data_ptr(), C, w2t.data_ptr(),

@@ -108,6 +108,11 @@ int ea_gemm_conv(const ea_conv_geo* geo, int a_kmajor, int b_kmajor, int M, int 
 int ea_gemm_conv_w1(const ea_conv_geo* geo, int M, int N, int K, const void* A, long lda, const void* B,
                     long ldb, const ea_epilogue* epi, const float* x, int T, int Fin, float* part,
                     void* stream);
+/* ea_gemm_conv_w1 with the ReLU mask read from ea_conv1_fwd2's support bits of the class plane
+ * (pos = bits of the plane's first row, N/8 bytes per row) instead of the bf16 aux rows. */
+int ea_gemm_conv_w1b(const ea_conv_geo* geo, int M, int N, int K, const void* A, long lda, const void* B,
+                     long ldb, const ea_epilogue* epi, const float* x, int T, int Fin, float* part,
+                     const unsigned char* pos, void* stream);
 int ea_conv1_wgrad_reduce(int ntiles, int C, const float* part, float* dw, float* dbias, void* stream);
 
 /* Select the bf16 GEMM main loop: 2 = LDS-DMA (global_load_lds) 2-stage ring (default),
@@ -319,6 +324,11 @@ int ea_col2im_conv2(int B, int T1, int F1, int C, const void* dcol, int dcol_dty
  * workspace >= 10*C floats per block, up to 1024 blocks). */
 int ea_conv1_fwd(int B, int T, int F, int C, const float* x, const float* w, const float* bias,
                  void* x1p, int dtype, void* stream);
+/* ea_conv1_fwd that also writes the ReLU support of x1p as bits: pos[row*(C/8) + c/8] bit
+ * (c & 7) = (x1p[row][c] > 0), rows in x1p's phase-split order (the backward's ReLU mask at
+ * 1/16 of x1p's bytes; NULL: none). */
+int ea_conv1_fwd2(int B, int T, int F, int C, const float* x, const float* w, const float* bias,
+                  void* x1p, int dtype, unsigned char* pos, void* stream);
 int ea_conv1_wgrad(int B, int T, int F, int C, const float* x, const void* dh, int dtype, float* dw,
                    float* dbias, float* workspace, long ws_elems, void* stream);
 

@@ -88,15 +88,19 @@ def test_fused_conv1_wgrad_matches_unfused(C, B, T):
     f32 summation order (the masked gradient is bf16-rounded in both; the input patches enter
     the MFMA as bf16 hi + lo halves); every other output is bit-identical."""
     from espnet_amd.layers import subsampling as S
-    fuse = S.FUSE_CONV1_WGRAD
+    fuse, bits = S.FUSE_CONV1_WGRAD, S.CONV1_POS_BITS
     try:
         S.FUSE_CONV1_WGRAD = False
         y0, g0 = _run(C, B, T, True, torch.bfloat16)
-        S.FUSE_CONV1_WGRAD = True
+        S.FUSE_CONV1_WGRAD, S.CONV1_POS_BITS = True, False  # mask from the bf16 x1p rows
+        y2, g2 = _run(C, B, T, True, torch.bfloat16)
+        S.CONV1_POS_BITS = True  # mask from ea_conv1_fwd2's support bits
         y1, g1 = _run(C, B, T, True, torch.bfloat16)
     finally:
-        S.FUSE_CONV1_WGRAD = fuse
-    assert torch.equal(y0, y1)
+        S.FUSE_CONV1_WGRAD, S.CONV1_POS_BITS = fuse, bits
+    assert torch.equal(y0, y1) and torch.equal(y2, y1)
+    for k in g1:
+        assert torch.equal(g1[k], g2[k]), k  # same mask, same arithmetic
     for k in g0:
         if k.startswith("conv.0."):
             # two f32 summation orders over ~10^5 pixels whose products largely cancel
