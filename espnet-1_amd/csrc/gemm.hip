@@ -1333,13 +1333,15 @@ EA_DEV void pipe_tile(const GemmP& p, char* smem, const bf16* A, const bf16* B, 
     for (int j = 0; j < 4; ++j) asm volatile("" ::"v"(fb[j]));
     __builtin_amdgcn_sched_barrier(0);
     lds_barrier();
-    // ---- COMPUTE(sl)
+    // ---- COMPUTE(sl), at raised issue priority (the other group's LOAD waits for it)
     __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int i = 0; i < MI; ++i)
 #pragma unroll
       for (int j = 0; j < 4; ++j)
         acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
     __builtin_amdgcn_sched_barrier(0);
     lds_barrier();
   }
