@@ -70,7 +70,7 @@ __global__ __launch_bounds__(256) void softmax_fwd_kernel(SmP a) {
       if (j < a.T2) {
         const float pj = v[e] * inv;
         prow[j] = pj;
-        const float pd = a.p > 0.f ? pj * drop_scale(seed, base + j, a.p) : pj;
+        const float pd = a.p > 0.f ? pj * attn_drop_scale(seed, r, a.T2, j, a.p) : pj;
         store_from_f(a.Pd, r * a.ldPd + j, a.pd_dtype, pd);
       }
     }
@@ -109,7 +109,7 @@ __global__ __launch_bounds__(256) void softmax_bwd_kernel(SmBP a) {
       if (j < a.T2) {
         pv[e] = prow[j];
         float d = drow[j];
-        if (a.p > 0.f) d *= drop_scale(seed, base + j, a.p);
+        if (a.p > 0.f) d *= attn_drop_scale(seed, r, a.T2, j, a.p);
         dv[e] = d;
         dot += pv[e] * d;
       } else {

@@ -101,6 +101,19 @@ EA_DEV float drop_scale(uint64_t seed, uint64_t idx, float p) {
   const uint32_t bits = (idx & 1) ? h >> 16 : h & 0xffffu;
   return bits >= ea_drop_thr(p) ? 1.f / (1.f - p) : 0.f;
 }
+// Attention-score dropout stream: element (row, j) of a (rows x T2) score matrix, rows
+// z*T1 + i.  Keys 2m and 2m+1 of a row share one pair hash (its low / high 16 bits), so two
+// adjacent lanes draw a single hash for both; every path (fused kernels, unfused softmax,
+// forward and backward) uses this law.
+EA_DEV uint64_t attn_pair(uint64_t row, int T2, int j) { return row * (uint64_t)((T2 + 1) >> 1) + (uint64_t)(j >> 1); }
+EA_DEV bool attn_keep(uint32_t key, uint32_t thr, uint64_t row, int T2, int j) {
+  const uint32_t h = ea_pair_hash(key, attn_pair(row, T2, j));
+  return ((j & 1) ? h >> 16 : h & 0xffffu) >= thr;
+}
+EA_DEV float attn_drop_scale(uint64_t seed, uint64_t row, int T2, int j, float p) {
+  if (p <= 0.f) return 1.f;
+  return attn_keep(ea_seed_key(seed), ea_drop_thr(p), row, T2, j) ? 1.f / (1.f - p) : 0.f;
+}
 // four consecutive elements idx .. idx+3, idx even (two hashes); s[k] *= scale
 EA_DEV void drop_scale4(uint64_t seed, uint64_t idx, float p, float (&v)[4]) {
   if (p <= 0.f) return;

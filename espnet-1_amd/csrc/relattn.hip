@@ -114,15 +114,22 @@ EA_DEV void stage_km(char* img, const bf16* gsrc, long ld, int r0, int rlim, int
 }
 
 EA_DEV f32x4 mfma(bf16x8 a, bf16x8 b, f32x4 c) { return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0); }
-EA_DEV float max16(float v) {  // max over the 16 lanes of a lane group (same lane>>4)
-#pragma unroll
-  for (int o = 1; o < 16; o <<= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
-  return v;
+// 16-lane (lane >> 4 group) reductions with DPP: swap within pairs, within quads, then the
+// half-row and row mirrors; every lane ends with the same value (each step is a commutative
+// pairing)
+template <int CTRL>
+EA_DEV float dppf(float v) { return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), CTRL, 0xF, 0xF, false)); }
+EA_DEV float max16(float v) {
+  v = fmaxf(v, dppf<0xB1>(v));   // quad_perm [1,0,3,2]
+  v = fmaxf(v, dppf<0x4E>(v));   // quad_perm [2,3,0,1]
+  v = fmaxf(v, dppf<0x141>(v));  // row_half_mirror
+  return fmaxf(v, dppf<0x140>(v));  // row_mirror
 }
 EA_DEV float sum16(float v) {
-#pragma unroll
-  for (int o = 1; o < 16; o <<= 1) v += __shfl_xor(v, o, 64);
-  return v;
+  v += dppf<0xB1>(v);
+  v += dppf<0x4E>(v);
+  v += dppf<0x141>(v);
+  return v + dppf<0x140>(v);
 }
 EA_DEV void lds_fence() {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -160,12 +167,7 @@ struct AttnP {
   uint32_t* dmask; int ldm;  // dropout keep bits [z*T1 + i][ldm words], bit j&31 of word j>>5:
                              // written by the forward, read by the backward (else rehashed)
 };
-
 // ldm >= 2 * ceil(T2 / 64): a 64-key chunk is the word pair (j0 >> 5, +1)
-EA_DEV bool keep_hash(uint32_t key, uint32_t thr, uint64_t idx) {
-  const uint32_t h = ea_pair_hash(key, idx >> 1);
-  return ((idx & 1) ? h >> 16 : h & 0xffffu) >= thr;
-}
 
 // ------------------------------------------------------------------------------ forward
 constexpr int F_K = 0, F_V = F_K + KC * 128, F_P = F_V + KC * 128;  // K, V chunk, P band (128 rows)
@@ -212,9 +214,11 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(AttnP a) {
   for (int r = 0; r < 4; ++r) { mrun[r] = -INFINITY; lrun[r] = 0.f; }
   const int ibase = i0 + 16 * w + 4 * g;  // query row of register rr: ibase + rr
   const int kend = a.causal ? min(kl, i0 + QB) : kl;
-  uint64_t rowbase[4];  // dropout element index of (row, key 0)
-#pragma unroll
-  for (int r = 0; r < 4; ++r) rowbase[r] = ((uint64_t)z * a.T1 + ibase + r) * a.T2;
+  // dropout pair index of (row, key 0) for the two rows this lane hashes: the even lane of a
+  // pair hashes rows 0 and 2 of its group, the odd lane rows 1 and 3 (see attn_pair)
+  const int odd = lc & 1;
+  const uint64_t npair = (uint64_t)((a.T2 + 1) >> 1);
+  const uint64_t prA = ((uint64_t)z * a.T1 + ibase + odd) * npair, prB = prA + 2 * npair;
   const long pofs = (long)(tid >> 3), cofs = h * DK + (tid & 7) * 8;  // stage_km thread bases
   const bf16* gK = a.k + ((long)b * a.T2 + pofs) * a.ldk + cofs;
   const bf16* gV = a.v + ((long)b * a.T2 + pofs) * a.ldv + cofs;
@@ -289,13 +293,19 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(AttnP a) {
       const float sc = 1.f / (1.f - a.p);
       uint64_t bal[4][4];
 #pragma unroll
-      for (int t = 0; t < 4; ++t)
+      for (int t = 0; t < 4; ++t) {
+        const uint64_t jp = (uint64_t)((j0 + 16 * t + lc) >> 1);  // shared by the lane pair
+        const uint32_t hA = ea_pair_hash(key, prA + jp), hB = ea_pair_hash(key, prB + jp);
+        const uint32_t pA = (uint32_t)__builtin_amdgcn_mov_dpp((int)hA, 0xB1, 0xF, 0xF, false);
+        const uint32_t pB = (uint32_t)__builtin_amdgcn_mov_dpp((int)hB, 0xB1, 0xF, 0xF, false);
+        const uint32_t h[4] = {odd ? pA : hA, odd ? hA : pA, odd ? pB : hB, odd ? hB : pB};
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const bool kept = keep_hash(key, thr, rowbase[r] + (uint64_t)(j0 + 16 * t + lc));
+          const bool kept = (odd ? h[r] >> 16 : h[r] & 0xffffu) >= thr;  // key parity = lane parity
           pv[t][r] *= kept ? sc : 0.f;
           bal[t][r] = __ballot(kept);
         }
+      }
       if (a.dmask && lc < 2) {  // lane lc = u writes word u of each of its group's 4 rows
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
@@ -525,11 +535,11 @@ __global__ __launch_bounds__(256, 2) void attn_bwdq_kernel(AttnP a) {
       const uint32_t key = ea_seed_key(seed), thr = ea_drop_thr(a.p);
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const uint64_t rowb = ((uint64_t)z * a.T1 + ibase + r) * a.T2 + j0 + lc;
+        const uint64_t row = (uint64_t)z * a.T1 + ibase + r;
         uint32_t x = 0u, y = 0u;
 #pragma unroll
         for (int t = 0; t < 4; ++t) {
-          const uint32_t bit = (uint32_t)keep_hash(key, thr, rowb + 16 * t) << (16 * (t & 1) + lc);
+          const uint32_t bit = (uint32_t)attn_keep(key, thr, row, a.T2, j0 + 16 * t + lc) << (16 * (t & 1) + lc);
           if (t < 2) x |= bit; else y |= bit;
         }
         mw[r] = make_uint2(x, y);
@@ -824,7 +834,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwdkv_kernel(AttnP a) {
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
             const int i = i0 + 16 * mi + 4 * g + r;
-            mr[mi][r] = (uint32_t)keep_hash(key, thr, ((uint64_t)z * a.T1 + i) * a.T2 + j) << bpos;
+            mr[mi][r] = (uint32_t)attn_keep(key, thr, (uint64_t)z * a.T1 + i, a.T2, j) << bpos;
           }
       } else {
 #pragma unroll
