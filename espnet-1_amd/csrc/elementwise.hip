@@ -486,19 +486,26 @@ __global__ __launch_bounds__(256) void dwconv_bwd_kernel(int B, int T, int C, in
 }
 
 // Register-window variants for a compile-time kernel width: each thread owns one channel and
-// 8 consecutive time rows, holds the 8+K-1 input rows it touches in registers (one LDS read
-// per row instead of one per tap) and does the 8*K taps from registers.
-template <int K>
+// R consecutive time rows (a block: 64 channels x 4R rows), holds the R+K-1 input rows it
+// touches in registers (one LDS read per row instead of one per tap) and does the R*K taps
+// from registers; the block's taps are staged through LDS by one coalesced pass.
+constexpr int DW_R = 16;  // rows per thread (64-row tiles: the K-1 halo costs < 1.5x)
+template <int K, int R>
 __global__ __launch_bounds__(256) void dwconv_fwd_k_kernel(int B, int T, int C, const float* __restrict__ x,
                                                            const float* __restrict__ w,
                                                            const float* __restrict__ bias, float* __restrict__ y) {
-  constexpr int P = (K - 1) / 2, RL = DW_TT + K - 1, WIN = 8 + K - 1;
+  constexpr int P = (K - 1) / 2, TT = 4 * R, RL = TT + K - 1, WIN = R + K - 1;
   __shared__ float tile[RL * DW_CT];
-  const int ntt = ea_cdiv(T, DW_TT);
-  const int b = blockIdx.x / ntt, t0 = (blockIdx.x % ntt) * DW_TT;
+  __shared__ float wsm[K * DW_CT];  // [k][c]
+  const int ntt = ea_cdiv(T, TT);
+  const int b = blockIdx.x / ntt, t0 = (blockIdx.x % ntt) * TT;
   const int c0 = blockIdx.y * DW_CT;
   const int cc = threadIdx.x % DW_CT, tq = threadIdx.x / DW_CT;
   const int c = c0 + cc;
+  for (int i = threadIdx.x; i < DW_CT * K; i += 256) {  // w rows c0.. are one contiguous run
+    const int ci = i / K, k = i - ci * K;
+    wsm[k * DW_CT + ci] = c0 + ci < C ? w[(long)c0 * K + i] : 0.f;
+  }
   if (C % 4 == 0) {  // 16-B loads: 16 lanes cover one 64-channel row
     for (int i = threadIdx.x; i < RL * (DW_CT / 4); i += 256) {
       const int rr = i / (DW_CT / 4), c4 = (i % (DW_CT / 4)) * 4;
@@ -517,39 +524,44 @@ __global__ __launch_bounds__(256) void dwconv_fwd_k_kernel(int B, int T, int C, 
   if (c >= C) return;
   float win[WIN];
 #pragma unroll
-  for (int i = 0; i < WIN; ++i) win[i] = tile[(tq * 8 + i) * DW_CT + cc];
-  float acc[8];
+  for (int i = 0; i < WIN; ++i) win[i] = tile[(tq * R + i) * DW_CT + cc];
+  float acc[R];
   const float b0 = bias ? bias[c] : 0.f;
 #pragma unroll
-  for (int j = 0; j < 8; ++j) acc[j] = b0;
+  for (int j = 0; j < R; ++j) acc[j] = b0;
 #pragma unroll
   for (int k = 0; k < K; ++k) {
-    const float wk = w[c * K + k];
+    const float wk = wsm[k * DW_CT + cc];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) acc[j] += wk * win[j + k];
+    for (int j = 0; j < R; ++j) acc[j] += wk * win[j + k];
   }
 #pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    const int t = t0 + tq * 8 + j;
+  for (int j = 0; j < R; ++j) {
+    const int t = t0 + tq * R + j;
     if (t < T) y[((long)b * T + t) * C + c] = acc[j];
   }
 }
 
 // dx[t] = sum_k w[k] dy[t-k+P];  part[blk][k*C+c] = sum_t dy[t] x[t+k-P];  part[blk][K*C+c] = sum_t dy[t]
-template <int K>
+template <int K, int R>
 __global__ __launch_bounds__(256) void dwconv_bwd_k_kernel(int B, int T, int C, const float* __restrict__ x,
                                                            const float* __restrict__ w, const float* __restrict__ dy,
                                                            float* __restrict__ dx, float* __restrict__ part) {
-  constexpr int P = (K - 1) / 2, RL = DW_TT + K - 1, WIN = 8 + K - 1;
+  constexpr int P = (K - 1) / 2, TT = 4 * R, RL = TT + K - 1, WIN = R + K - 1;
   constexpr int SM = 2 * RL * DW_CT > 4 * (K + 1) * DW_CT ? 2 * RL * DW_CT : 4 * (K + 1) * DW_CT;
   __shared__ float sm[SM];
-  float* tdy = sm;                 // dy rows t0-(K-1-P) .. t0+DW_TT-1+P
-  float* tx = sm + RL * DW_CT;     // x rows  t0-P .. t0+DW_TT-1+(K-1-P)
-  const int ntt = ea_cdiv(T, DW_TT);
-  const int b = blockIdx.x / ntt, t0 = (blockIdx.x % ntt) * DW_TT;
+  __shared__ float wsm[K * DW_CT];  // [k][c]
+  float* tdy = sm;                 // dy rows t0-(K-1-P) .. t0+TT-1+P
+  float* tx = sm + RL * DW_CT;     // x rows  t0-P .. t0+TT-1+(K-1-P)
+  const int ntt = ea_cdiv(T, TT);
+  const int b = blockIdx.x / ntt, t0 = (blockIdx.x % ntt) * TT;
   const int c0 = blockIdx.y * DW_CT;
   const int cc = threadIdx.x % DW_CT, tq = threadIdx.x / DW_CT;
   const int c = c0 + cc;
+  for (int i = threadIdx.x; i < DW_CT * K; i += 256) {
+    const int ci = i / K, k = i - ci * K;
+    wsm[k * DW_CT + ci] = c0 + ci < C ? w[(long)c0 * K + i] : 0.f;
+  }
   if (C % 4 == 0) {
     for (int i = threadIdx.x; i < RL * (DW_CT / 4); i += 256) {
       const int rr = i / (DW_CT / 4), c4 = (i % (DW_CT / 4)) * 4;
@@ -574,31 +586,31 @@ __global__ __launch_bounds__(256) void dwconv_bwd_k_kernel(int B, int T, int C, 
   {
     float win[WIN];
 #pragma unroll
-    for (int i = 0; i < WIN; ++i) win[i] = tdy[(tq * 8 + i) * DW_CT + cc];
+    for (int i = 0; i < WIN; ++i) win[i] = tdy[(tq * R + i) * DW_CT + cc];
     if (c < C) {
-      float acc[8];
+      float acc[R];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) acc[j] = 0.f;
+      for (int j = 0; j < R; ++j) acc[j] = 0.f;
 #pragma unroll
       for (int k = 0; k < K; ++k) {
-        const float wk = w[c * K + k];
+        const float wk = wsm[k * DW_CT + cc];
 #pragma unroll
-        for (int j = 0; j < 8; ++j) acc[j] += wk * win[j - k + K - 1];
+        for (int j = 0; j < R; ++j) acc[j] += wk * win[j - k + K - 1];
       }
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const int t = t0 + tq * 8 + j;
+      for (int j = 0; j < R; ++j) {
+        const int t = t0 + tq * R + j;
         if (t < T) dx[((long)b * T + t) * C + c] = acc[j];
       }
     }
-    // dy[t0 + tq*8 + j] = win[j + K-1-P]  (rows past T are zero)
+    // dy[t0 + tq*R + j] = win[j + K-1-P]  (rows past T are zero)
     float xw[WIN];
 #pragma unroll
-    for (int i = 0; i < WIN; ++i) xw[i] = tx[(tq * 8 + i) * DW_CT + cc];
+    for (int i = 0; i < WIN; ++i) xw[i] = tx[(tq * R + i) * DW_CT + cc];
 #pragma unroll
     for (int k = 0; k <= K; ++k) aw[k] = 0.f;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
+    for (int j = 0; j < R; ++j) {
       const float d = win[j + K - 1 - P];
       aw[K] += d;
 #pragma unroll
@@ -901,9 +913,10 @@ extern "C" int ea_dwconv_fwd(int B, int T, int C, int K, const float* x, const f
   EA_ENTRY();
   EA_CHECK_ARG(K % 2 == 1);
   dim3 grid(B * ea_cdiv(T, DW_TT), ea_cdiv(C, DW_CT));
+  dim3 gridr(B * ea_cdiv(T, 4 * DW_R), ea_cdiv(C, DW_CT));
   hipStream_t st = (hipStream_t)stream;
   switch (K) {
-#define EA_DWF(KK) case KK: hipLaunchKernelGGL(dwconv_fwd_k_kernel<KK>, grid, dim3(256), 0, st, B, T, C, x, w, bias, y); break;
+#define EA_DWF(KK) case KK: hipLaunchKernelGGL((dwconv_fwd_k_kernel<KK, DW_R>), gridr, dim3(256), 0, st, B, T, C, x, w, bias, y); break;
     EA_DWF(3) EA_DWF(5) EA_DWF(7) EA_DWF(15) EA_DWF(31)
 #undef EA_DWF
     default: {
@@ -924,19 +937,21 @@ extern "C" int ea_dwconv_bwd(int B, int T, int C, int K, const float* x, const f
   dim3 grid(nblk, ea_cdiv(C, DW_CT));
   if (K == 3 || K == 5 || K == 7 || K == 15 || K == 31) {
     // one fused pass: dx, and per-block partials of dw and dbias
+    const int nblkr = B * ea_cdiv(T, 4 * DW_R);
+    dim3 gridr(nblkr, ea_cdiv(C, DW_CT));
     const long rowlen = (long)C * (K + 1);
-    EA_CHECK_ARG((long)nblk * rowlen <= ws_elems);
+    EA_CHECK_ARG((long)nblkr * rowlen <= ws_elems);
     hipStream_t st = (hipStream_t)stream;
     switch (K) {
-#define EA_DWB(KK) case KK: hipLaunchKernelGGL(dwconv_bwd_k_kernel<KK>, grid, dim3(256), 0, st, B, T, C, x, w, dy, dx, workspace); break;
+#define EA_DWB(KK) case KK: hipLaunchKernelGGL((dwconv_bwd_k_kernel<KK, DW_R>), gridr, dim3(256), 0, st, B, T, C, x, w, dy, dx, workspace); break;
       EA_DWB(3) EA_DWB(5) EA_DWB(7) EA_DWB(15) EA_DWB(31)
 #undef EA_DWB
     }
     EA_LAUNCH_CHECK();
     // partial columns are [k][c]; dw is (C, 1, K): the reduction writes it transposed
-    int rc = ea_reduce_partials_tr(nblk, C * K, workspace, rowlen, dw, accumulate_params, C, K, stream);
+    int rc = ea_reduce_partials_tr(nblkr, C * K, workspace, rowlen, dw, accumulate_params, C, K, stream);
     if (rc || !dbias) return rc;
-    return ea_reduce_partials(nblk, C, workspace + (long)C * K, rowlen, dbias, accumulate_params, stream);
+    return ea_reduce_partials(nblkr, C, workspace + (long)C * K, rowlen, dbias, accumulate_params, stream);
   }
   EA_CHECK_ARG((long)nblk * C * K <= ws_elems);
   const size_t sm = (size_t)(2 * (DW_TT + K - 1) + DW_TT) * DW_CT * sizeof(float);
