@@ -30,13 +30,17 @@ class CTC(nn.Module):
         self.zero_infinity = zero_infinity
         self._b = None
         self._seed = 0
+        self._overlap = False
 
     def bind(self, arena, prefix, cd):
         self._b = Bound(arena, prefix, cd)
 
-    def forward(self, hs_pad, hlens, ys_pad, ys_lens, seed: int = 0):
-        """ctc.py:72-97.  ys_pad (B, Lmax) padded with -1; returns sum_b loss_b / B."""
+    def forward(self, hs_pad, hlens, ys_pad, ys_lens, seed: int = 0, overlap: bool = False):
+        """ctc.py:72-97.  ys_pad (B, Lmax) padded with -1; returns sum_b loss_b / B.
+        overlap=True: the lattice runs on the auxiliary stream (hip_ops.aux) and the caller
+        must hip_ops.join_aux() before using the loss (ESPnetASRModel.forward does)."""
         self._seed = seed
+        self._overlap = overlap
         return CTCFn.apply(hs_pad.contiguous(), hlens, ys_pad.contiguous(), ys_lens, self,
                            int(ys_pad.shape[1]))
 

@@ -238,7 +238,7 @@ class ESPnetASRModel(AbsESPnetModel):
         loss_ctc = loss_att = acc_att = None
         if self.ctc_weight != 0.0:
             loss_ctc = self.ctc(encoder_out, encoder_out_lens, text.contiguous(), text_lengths,
-                                seed=site_seed(seed, 500, 1))
+                                seed=site_seed(seed, 500, 1), overlap=True)
             stats["loss_ctc"] = loss_ctc.detach()
             stats["cer_ctc"] = None
             if not self.training and self.error_calculator is not None:  # :571-575
@@ -258,6 +258,7 @@ class ESPnetASRModel(AbsESPnetModel):
             stats["acc"] = None
             stats["cer"] = None
             stats["wer"] = None
+        ops.join_aux()  # the CTC lattice ran on the auxiliary stream beside the decoder
         if self.ctc_weight == 0.0:
             loss = loss_att
         elif self.ctc_weight == 1.0:

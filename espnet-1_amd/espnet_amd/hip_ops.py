@@ -101,6 +101,53 @@ def join_wgrad(device=None):
         main.wait_stream(side)
 
 
+# latency-bound work that leaves most CUs idle (the CTC lattice: 2 workgroups per utterance)
+# overlaps independent work on an auxiliary stream (EA_OVERLAP_AUX=0: serial)
+OVERLAP_AUX = os.environ.get("EA_OVERLAP_AUX", "1") != "0"
+_AUX = {}
+
+
+class aux:
+    """Context: the enclosed launches run on the auxiliary stream, ordered after everything the
+    main stream has issued so far; `join_aux()` makes the main stream wait for them.  The
+    tensors it touches are record_stream()-ed for the caching allocator."""
+
+    def __init__(self, *tensors):
+        self.tensors = tensors
+
+    def __enter__(self):
+        if not OVERLAP_AUX or not torch.cuda.is_available():
+            self.ctx = None
+            return self
+        main = torch.cuda.current_stream()
+        dev = main.device
+        st = _AUX.get(dev)
+        if st is None:
+            st = _AUX[dev] = torch.cuda.Stream(device=dev)
+        st.wait_stream(main)
+        for t in self.tensors:
+            if t is not None:
+                t.record_stream(st)
+        self.ctx = torch.cuda.stream(st)
+        self.ctx.__enter__()
+        return self
+
+    def __exit__(self, *exc):
+        if self.ctx is not None:
+            self.ctx.__exit__(*exc)
+        return False
+
+
+def join_aux():
+    """Main stream waits for all auxiliary-stream work issued so far."""
+    if not _AUX:
+        return
+    main = torch.cuda.current_stream()
+    st = _AUX.get(main.device)
+    if st is not None:
+        main.wait_stream(st)
+
+
 GRAD_READY = None  # callable(prefix): a block's parameter gradients are final (DP overlap)
 
 

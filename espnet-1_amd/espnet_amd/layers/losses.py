@@ -4,6 +4,8 @@
 grad_output), so nothing here synchronises with the host."""
 from __future__ import annotations
 
+import contextlib
+
 import torch
 
 from .common import F32, empty, lib, ops
@@ -36,9 +38,14 @@ class CTCFn(torch.autograd.Function):
         nll = torch.empty(B, dtype=torch.float64, device=dev)
         loss_utt = empty(B, device=dev)
         loss = empty((), device=dev)
-        lib.ea_ctc_loss_fwd(B, T, V, logits.data_ptr(), V, hlens.data_ptr(), ys.data_ptr(), ys.stride(0),
-                            ylens.data_ptr(), Lmax, lse.data_ptr(), alpha.data_ptr(), beta.data_ptr(),
-                            nll.data_ptr(), loss_utt.data_ptr(), loss.data_ptr(), ops.stream())
+        # the lattice runs 2 workgroups per utterance for T' serial steps: on the auxiliary
+        # stream it overlaps the attention decoder's forward (ESPnetASRModel.forward joins
+        # before the losses are combined)
+        with (ops.aux(logits, hlens, ys, ylens, lse, alpha, beta, nll, loss_utt, loss) if ctc._overlap
+              else contextlib.nullcontext()):
+            lib.ea_ctc_loss_fwd(B, T, V, logits.data_ptr(), V, hlens.data_ptr(), ys.data_ptr(), ys.stride(0),
+                                ylens.data_ptr(), Lmax, lse.data_ptr(), alpha.data_ptr(), beta.data_ptr(),
+                                nll.data_ptr(), loss_utt.data_ptr(), loss.data_ptr(), ops.stream())
         ctx.ctc = ctc
         ctx.meta = (B, T, V, Lmax, d)
         ctx.save = (h, logits, lse, alpha, beta, nll, hlens, ys, ylens)
