@@ -240,22 +240,31 @@ __global__ void ctc_reduce_kernel(int B, const float* __restrict__ loss_utt, flo
 }
 
 // grad[b,t,v] = g_b * (softmax(x)[v] - sum_{s: l'(s)=v} exp(alpha+beta+nll-lp))
+// One block per (b, t) row.  The occupancies of the row's <= L+1 distinct labels go to a small
+// LDS table; one vectorized pass writes g*softmax for every column, then (after a barrier) the
+// label columns are rewritten with the same expression including their occupancy — the values
+// are those of a single pass with a V-wide occupancy array.
 template <typename TO>
 __global__ __launch_bounds__(256) void ctc_grad_kernel(CtcP p, const float* __restrict__ gscale, float coef,
                                                        TO* __restrict__ grad, long ldg) {
-  extern __shared__ float acc[];  // V
+  extern __shared__ float occ_tab[];  // [Lmax] label occupancy, then [Lmax] int label (or -1)
+  int* lab_tab = (int*)(occ_tab + p.Lmax);
   const long row = blockIdx.x;
   const int b = (int)(row / p.T), t = (int)(row % p.T);
   const int Tb = (int)min((long long)p.T, p.hlens[b]);
   const double nll = p.nll[b];
   TO* gr = grad + row * ldg;
+  const bool vec = (p.V % 4 == 0) && (p.ldt % 4 == 0) && (ldg % 4 == 0);
   if (t >= Tb || isinf(nll) || isnan(nll)) {
-    for (int v = threadIdx.x; v < p.V; v += blockDim.x) gr[v] = from_f<TO>(0.f);
+    if (vec) {
+      const float z4[4] = {0.f, 0.f, 0.f, 0.f};
+      for (int v = threadIdx.x * 4; v < p.V; v += blockDim.x * 4) vst4(gr + v, z4);
+    } else {
+      for (int v = threadIdx.x; v < p.V; v += blockDim.x) gr[v] = from_f<TO>(0.f);
+    }
     return;
   }
   __shared__ double red[16];
-  for (int v = threadIdx.x; v < p.V; v += blockDim.x) acc[v] = 0.f;
-  __syncthreads();
   const int L = (int)p.ylens[b];
   const int S = 2 * L + 1;
   const double* A = p.alpha + ((long)b * p.T + t) * p.Smax;
@@ -274,18 +283,32 @@ __global__ __launch_bounds__(256) void ctc_grad_kernel(CtcP p, const float* __re
     const int lab = ctc_label(p, b, s);
     bool first = true;
     for (int q = 1; q < s; q += 2) first = first && ctc_label(p, b, q) != lab;
-    if (!first) continue;
     double a = 0.0;
-    for (int q = s; q < S; q += 2)
-      if (ctc_label(p, b, q) == lab) a += occ(q, lab);
-    acc[lab] = (float)a;
+    if (first)
+      for (int q = s; q < S; q += 2)
+        if (ctc_label(p, b, q) == lab) a += occ(q, lab);
+    lab_tab[s >> 1] = first ? lab : -1;
+    occ_tab[s >> 1] = (float)a;
   }
-  if (threadIdx.x == 0) acc[0] = (float)bsum;
-  __syncthreads();
   const float g = gscale[0] * coef;
   const float* xr = p.logits + row * p.ldt;
   const float l = p.lse[row];
-  for (int v = threadIdx.x; v < p.V; v += blockDim.x) gr[v] = from_f<TO>(g * (__expf(xr[v] - l) - acc[v]));
+  if (vec) {
+    for (int v = threadIdx.x * 4; v < p.V; v += blockDim.x * 4) {
+      const float4 x4 = *(const float4*)(xr + v);
+      const float o[4] = {g * __expf(x4.x - l), g * __expf(x4.y - l), g * __expf(x4.z - l), g * __expf(x4.w - l)};
+      vst4(gr + v, o);
+    }
+  } else {
+    for (int v = threadIdx.x; v < p.V; v += blockDim.x) gr[v] = from_f<TO>(g * (__expf(xr[v] - l) - 0.f));
+  }
+  __syncthreads();  // the table is complete; this block's softmax writes are visible
+  for (int i = threadIdx.x; i <= L; i += blockDim.x) {
+    const int lab = i < L ? lab_tab[i] : 0;  // i == L: the blank
+    if (lab < 0) continue;
+    const float a = i < L ? occ_tab[i] : (float)bsum;
+    gr[lab] = from_f<TO>(g * (__expf(xr[lab] - l) - a));
+  }
 }
 
 // ---------------------------------------------------------------- label smoothing
@@ -414,7 +437,7 @@ extern "C" int ea_ctc_loss_bwd(int B, int T, int V, const float* logits, long ld
   CtcP p{B, T, V, Lmax, Smax, logits, ldt, lse, hlens, ys, ldys, ylens, (double*)alpha, (double*)beta,
          (double*)nll, nullptr};
   hipStream_t st = (hipStream_t)stream;
-  const size_t sm = (size_t)V * sizeof(float);
+  const size_t sm = (size_t)max(Lmax, 1) * (sizeof(float) + sizeof(int));
   if (grad_dtype == EA_BF16)
     hipLaunchKernelGGL(ctc_grad_kernel<bf16>, dim3((long)B * T), dim3(256), sm, st, p, gscale, coef, (bf16*)grad, ldg);
   else
