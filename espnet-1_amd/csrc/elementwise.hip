@@ -683,10 +683,31 @@ __global__ __launch_bounds__(256) void embed_bwd_kernel(int rows, int d, const l
   }
   __syncthreads();
   if (dup) return;
+  // the rows of this token, in increasing order (wave ballots + per-chunk offsets), then one
+  // pass per column over that list: the same summation order as scanning every row
+  __shared__ int list[EMBED_BWD_MAXROWS];
+  __shared__ int wcnt[4], nlist;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  if (threadIdx.x == 0) nlist = 0;
+  __syncthreads();
+  for (int base = r; base < rows; base += 256) {
+    const int q = base + threadIdx.x;
+    const bool hit = q < rows && stok[q] == (int)me;
+    const unsigned long long m = __ballot(hit);
+    if (lane == 0) wcnt[w] = __popcll(m);
+    __syncthreads();
+    int off = nlist;
+    for (int v = 0; v < w; ++v) off += wcnt[v];
+    if (hit) list[off + __popcll(m & ((1ull << lane) - 1ull))] = q;
+    __syncthreads();
+    if (threadIdx.x == 0) nlist += wcnt[0] + wcnt[1] + wcnt[2] + wcnt[3];
+    __syncthreads();
+  }
+  const int n = nlist;
   for (int c = threadIdx.x; c < d; c += blockDim.x) {
     float a = 0.f;
-    for (int q = r; q < rows; ++q) {
-      if (stok[q] != (int)me) continue;
+    for (int k = 0; k < n; ++k) {
+      const int q = list[k];
       const uint64_t i = (uint64_t)q * d + c;
       float v = dy[i] * xscale;
       if (p > 0.f) v *= drop_scale(seed, i, p);
