@@ -37,6 +37,53 @@ __global__ void mvn_kernel(int B, int T, int F, const float* __restrict__ x, con
   }
 }
 
+// Same op over a (row chunk, utterance) grid: the one-block-per-utterance kernel above
+// leaves most CUs idle and walks T/ny rows serially per thread.  Pass 1 writes each chunk's
+// f64 column sums over its valid rows to ws[b][chunk][F]; pass 2 sums an utterance's chunk
+// partials in chunk order, then writes its own chunk of y.
+constexpr int MVN_TC = 32;  // rows per chunk
+
+__global__ __launch_bounds__(512) void mvn_part_kernel(int T, int F, const float* __restrict__ x,
+                                                       const long long* __restrict__ lens, double* __restrict__ ws) {
+  const int c = blockIdx.x, b = blockIdx.y, nch = gridDim.x;
+  const int f = threadIdx.x, ty = threadIdx.y, ny = blockDim.y;
+  __shared__ double red[512];
+  const long long L = lens[b];
+  const int t1 = (int)min((long long)min(T, (c + 1) * MVN_TC), L);
+  double s = 0.0;
+  if (f < F)
+    for (int t = c * MVN_TC + ty; t < t1; t += ny) s += x[((long)b * T + t) * F + f];
+  red[ty * blockDim.x + f] = s;
+  __syncthreads();
+  if (ty == 0 && f < F) {
+    double a = 0.0;
+    for (int k = 0; k < ny; ++k) a += red[k * blockDim.x + f];
+    ws[((long)b * nch + c) * F + f] = a;
+  }
+}
+
+__global__ __launch_bounds__(512) void mvn_apply_kernel(int T, int F, const float* __restrict__ x,
+                                                        const long long* __restrict__ lens,
+                                                        const double* __restrict__ ws, float* __restrict__ y) {
+  const int c = blockIdx.x, b = blockIdx.y, nch = gridDim.x;
+  const int f = threadIdx.x, ty = threadIdx.y, ny = blockDim.y;
+  __shared__ float mean_s[256];
+  const long long L = lens[b];
+  if (ty == 0 && f < F) {
+    double a = 0.0;
+    for (int k = 0; k < nch; ++k) a += ws[((long)b * nch + k) * F + f];
+    mean_s[f] = (float)a / (float)L;  // f32 mean like the reference (sum / len)
+  }
+  __syncthreads();
+  if (f >= F) return;
+  const float mean = mean_s[f];
+  const int t1 = min(T, (c + 1) * MVN_TC);
+  for (int t = c * MVN_TC + ty; t < t1; t += ny) {
+    const long i = ((long)b * T + t) * F + f;
+    y[i] = (t < L ? x[i] : 0.f) - mean;
+  }
+}
+
 // lengths after Conv2dSubsampling as the reference derives them from the sliced mask
 // x_mask[:, :, :-2:2][:, :, :-2:2] (subsampling.py:91): l -> ceil(min(l, T-2)/2) twice.
 __global__ void subsample_lens_kernel(int B, int T, const long long* __restrict__ ilens, long long* __restrict__ olens) {
@@ -130,6 +177,65 @@ __global__ __launch_bounds__(256) void conv1_fwd_kernel(int B, int T, int F, Pha
 #pragma unroll
       for (int k = 0; k < 8; ++k) m |= (uint32_t)((float)(TO)o[k] > 0.f) << k;
       pos[prow * (C / 8) + cg] = (uint8_t)m;
+    }
+  }
+}
+
+// Same conv as conv1_fwd_kernel for C a multiple of 512 (one wave = one pixel's 512
+// channels, 8 per lane): blocks stride over output rows (b, t1), so the index arithmetic is
+// per row and wave-uniform (scalar), the 9 taps of a pixel are wave-uniform loads, and the
+// per-pixel vector work is the 72 FMAs, ReLU, bf16 packing and the support byte.
+template <typename TO>
+__global__ __launch_bounds__(256) void conv1_fwd_rows_kernel(int B, int T, int F, PhaseGeo g, int C,
+                                                             const float* __restrict__ x, const float* __restrict__ w,
+                                                             const float* __restrict__ bias, TO* __restrict__ y,
+                                                             uint8_t* __restrict__ pos) {
+  const int lane = threadIdx.x & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int nwc = C >> 9;                 // waves per pixel
+  const int wc = wv % nwc, pw = wv / nwc;  // channel slice, pixel slot of this wave
+  const int ppb = 4 / nwc;                // pixels per block per step (C <= 2048)
+  const int cg = wc * 64 + lane, c0 = cg * 8;
+  float wr[8][9], br[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    br[k] = bias[c0 + k];
+#pragma unroll
+    for (int t = 0; t < 9; ++t) wr[k][t] = w[(c0 + k) * 9 + t];
+  }
+  const int rows = B * g.T1;
+  for (int row = blockIdx.x; row < rows; row += gridDim.x) {
+    const int b = row / g.T1, t1 = row - b * g.T1;
+    const int a = t1 & 1;
+    const int nI = a ? g.nI1 : g.nI0;
+    const float* xr = x + ((long)b * T + 2 * t1) * F;
+    for (int f1 = pw; f1 < g.F1; f1 += ppb) {
+      const float* xp = xr + 2 * f1;
+      float xv[9];
+#pragma unroll
+      for (int kh = 0; kh < 3; ++kh)
+#pragma unroll
+        for (int kw = 0; kw < 3; ++kw) xv[kh * 3 + kw] = xp[kh * F + kw];
+      const int e = f1 & 1;
+      const long prow = g.plane[a * 2 + e] + ((long)(b * nI + (t1 >> 1)) * (e ? g.nJ1 : g.nJ0) + (f1 >> 1));
+      float o[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        float s = br[k];
+#pragma unroll
+        for (int t = 0; t < 9; ++t) s = fmaf(wr[k][t], xv[t], s);
+        o[k] = s > 0.f ? s : 0.f;
+      }
+      TO* yp = y + prow * C + c0;
+      float lo[4] = {o[0], o[1], o[2], o[3]}, hi[4] = {o[4], o[5], o[6], o[7]};
+      vst4(yp, lo);
+      vst4(yp + 4, hi);
+      if (pos) {
+        uint32_t m = 0;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) m |= (uint32_t)((float)(TO)o[k] > 0.f) << k;
+        pos[prow * (C / 8) + cg] = (uint8_t)m;
+      }
     }
   }
 }
@@ -752,6 +858,30 @@ extern "C" int ea_utterance_mvn(int B, int T, int F, const float* x, const long 
   return 0;
 }
 
+extern "C" int ea_utterance_mvn_ws_bytes(int B, int T, int F, long* bytes) {
+  EA_ENTRY();
+  EA_CHECK_ARG(bytes != nullptr && B >= 0 && T >= 0 && F > 0);
+  *bytes = (long)B * ea_cdiv(T, MVN_TC) * F * (long)sizeof(double);
+  return 0;
+}
+
+extern "C" int ea_utterance_mvn2(int B, int T, int F, const float* x, const long long* lens, float* y, void* ws,
+                                 long ws_bytes, void* stream) {
+  EA_ENTRY();
+  EA_CHECK_ARG(F <= 256 && F > 0 && ws != nullptr);
+  const int nch = ea_cdiv(T, MVN_TC);
+  EA_CHECK_ARG(ws_bytes >= (long)B * nch * F * (long)sizeof(double));
+  if (B == 0 || T == 0) return 0;
+  const int bx = F <= 64 ? 64 : (F <= 128 ? 128 : 256);
+  const int by = 512 / bx;
+  hipStream_t st = (hipStream_t)stream;
+  hipLaunchKernelGGL(mvn_part_kernel, dim3(nch, B), dim3(bx, by), 0, st, T, F, x, lens, (double*)ws);
+  EA_LAUNCH_CHECK();
+  hipLaunchKernelGGL(mvn_apply_kernel, dim3(nch, B), dim3(bx, by), 0, st, T, F, x, lens, (const double*)ws, y);
+  EA_LAUNCH_CHECK();
+  return 0;
+}
+
 extern "C" int ea_subsample_lens(int B, int T, const long long* ilens, long long* olens, void* stream) {
   EA_ENTRY();
   hipLaunchKernelGGL(subsample_lens_kernel, dim3(ea_cdiv(B, 64)), dim3(64), 0, (hipStream_t)stream, B, T, ilens, olens);
@@ -1043,6 +1173,19 @@ extern "C" int ea_conv1_fwd2(int B, int T, int F, int C, const float* x, const f
   const int T1 = (T - 3) / 2 + 1, F1 = (F - 3) / 2 + 1;
   const PhaseGeo g = phase_geo(B, T1, F1, C);
   const long npix = (long)B * T1 * F1;
+  static const bool pix_kernel = std::getenv("EA_CONV1_FWD_PIX") != nullptr;  // A/B switch
+  if ((C == 512 || C == 1024 || C == 2048) && (long)B * T1 < (1L << 31) && !pix_kernel) {
+    // 2048 blocks: each loads its 80 weights per lane once and walks ~B*T1/2048 rows
+    dim3 grid((unsigned)std::min<long>((long)B * T1, 2048));
+    if (dtype == EA_BF16)
+      hipLaunchKernelGGL(conv1_fwd_rows_kernel<bf16>, grid, dim3(256), 0, (hipStream_t)stream, B, T, F, g, C, x, w,
+                         bias, (bf16*)x1p, pos);
+    else
+      hipLaunchKernelGGL(conv1_fwd_rows_kernel<float>, grid, dim3(256), 0, (hipStream_t)stream, B, T, F, g, C, x, w,
+                         bias, (float*)x1p, pos);
+    EA_LAUNCH_CHECK();
+    return 0;
+  }
   const int ppb = 256 / (C / 8);
   dim3 grid(ea_grid_cap(ea_cdiv(npix, ppb), 4096));
   if (dtype == EA_BF16)

@@ -11,20 +11,66 @@
 
 namespace {
 
-// ---------------------------------------------------------------- row log-sum-exp
+// ---------------------------------------------------------------- row reductions
+// One 256-thread block per logits row (V ~ 5000 f32 = 20 KB): the max (and, for the
+// label-smoothing loss, its first index and the f64 row sum), then the f64 sum of
+// exp(x - max).  16-B loads when the row is 16-B aligned; the second pass re-reads the
+// row from L2.  Partial results combine in a fixed order (deterministic).
+struct RowRed { float mx; int am; double sx, se; };
+
+template <bool LSM>
+EA_DEV RowRed row_reduce(const float* __restrict__ xr, int V) {
+  __shared__ float s_m[4];
+  __shared__ int s_i[4];
+  __shared__ double s_x[4], s_e[4];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int V4 = ((uintptr_t)xr & 15) == 0 ? V >> 2 : 0;
+  const float4* x4 = (const float4*)xr;
+  float mx = -INFINITY;
+  int am = 0x7fffffff;
+  double sx = 0.0;
+  auto take = [&](float t, int v) {
+    if (t > mx || (t == mx && v < am)) { mx = t; am = v; }
+    if (LSM) sx += (double)t;
+  };
+  for (int i = tid; i < V4; i += 256) {
+    const float4 q = x4[i];
+    take(q.x, 4 * i); take(q.y, 4 * i + 1); take(q.z, 4 * i + 2); take(q.w, 4 * i + 3);
+  }
+  for (int v = 4 * V4 + tid; v < V; v += 256) take(xr[v], v);
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const float om = __shfl_xor(mx, o, 64);
+    const int oi = __shfl_xor(am, o, 64);
+    if (om > mx || (om == mx && oi < am)) { mx = om; am = oi; }
+  }
+  if (LSM) sx = wave_sum_d(sx);
+  if (lane == 0) { s_m[w] = mx; s_i[w] = am; s_x[w] = sx; }
+  __syncthreads();
+  RowRed r{s_m[0], s_i[0], s_x[0], 0.0};
+#pragma unroll
+  for (int k = 1; k < 4; ++k) {
+    if (s_m[k] > r.mx || (s_m[k] == r.mx && s_i[k] < r.am)) { r.mx = s_m[k]; r.am = s_i[k]; }
+    r.sx += s_x[k];
+  }
+  double se = 0.0;
+  for (int i = tid; i < V4; i += 256) {
+    const float4 q = x4[i];
+    se += (double)(__expf(q.x - r.mx) + __expf(q.y - r.mx)) + (double)(__expf(q.z - r.mx) + __expf(q.w - r.mx));
+  }
+  for (int v = 4 * V4 + tid; v < V; v += 256) se += (double)__expf(xr[v] - r.mx);
+  se = wave_sum_d(se);
+  if (lane == 0) s_e[w] = se;
+  __syncthreads();
+  r.se = (s_e[0] + s_e[1]) + (s_e[2] + s_e[3]);
+  return r;
+}
+
 __global__ __launch_bounds__(256) void lse_rows_kernel(long rows, int V, const float* __restrict__ x, long ld,
                                                        float* __restrict__ lse) {
-  const int lane = threadIdx.x & 63;
-  const long r = blockIdx.x * 4L + (threadIdx.x >> 6);
-  if (r >= rows) return;
-  const float* xr = x + r * ld;
-  float mx = -INFINITY;
-  for (int v = lane; v < V; v += 64) mx = fmaxf(mx, xr[v]);
-  mx = wave_max(mx);
-  double s = 0.0;
-  for (int v = lane; v < V; v += 64) s += (double)__expf(xr[v] - mx);
-  s = wave_sum_d(s);
-  if (lane == 0) lse[r] = mx + (float)log(s);
+  const long r = blockIdx.x;
+  const RowRed s = row_reduce<false>(x + r * ld, V);
+  if (threadIdx.x == 0) lse[r] = s.mx + (float)log(s.se);
 }
 
 EA_DEV double lae(double a, double b) {  // log(exp a + exp b)
@@ -323,30 +369,13 @@ struct LsmP {
 };
 
 __global__ __launch_bounds__(256) void lsm_fwd_kernel(LsmP p) {
-  const int lane = threadIdx.x & 63;
-  const long r = blockIdx.x * 4L + (threadIdx.x >> 6);
-  if (r >= p.rows) return;
+  const long r = blockIdx.x;
   const float* xr = p.x + r * p.ldx;
-  float mx = -INFINITY;
-  int am = 0x7fffffff;
-  double sx = 0.0;
-  for (int v = lane; v < p.V; v += 64) {
-    const float t = xr[v];
-    if (t > mx || (t == mx && v < am)) { mx = t; am = v; }
-    sx += t;
-  }
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {
-    const float om = __shfl_xor(mx, o, 64);
-    const int oi = __shfl_xor(am, o, 64);
-    if (om > mx || (om == mx && oi < am)) { mx = om; am = oi; }
-  }
-  sx = wave_sum_d(sx);
-  double se = 0.0;
-  for (int v = lane; v < p.V; v += 64) se += (double)__expf(xr[v] - mx);
-  se = wave_sum_d(se);
-  if (lane != 0) return;
-  const double lse = (double)mx + log(se);
+  const RowRed s = row_reduce<true>(xr, p.V);
+  if (threadIdx.x != 0) return;
+  const int am = s.am;
+  const double sx = s.sx;
+  const double lse = (double)s.mx + log(s.se);
   p.lse[r] = (float)lse;
   const long long t = p.tgt[r];
   if (t == p.ignore_id) { p.loss_row[r] = 0.0; return; }
@@ -409,7 +438,7 @@ extern "C" int ea_ctc_loss_fwd(int B, int T, int V, const float* logits, long ld
   EA_ENTRY();
   hipStream_t st = (hipStream_t)stream;
   const long rows = (long)B * T;
-  hipLaunchKernelGGL(lse_rows_kernel, dim3(ea_cdiv(rows, 4)), dim3(256), 0, st, rows, V, logits, ldt, lse);
+  hipLaunchKernelGGL(lse_rows_kernel, dim3(rows), dim3(256), 0, st, rows, V, logits, ldt, lse);
   EA_LAUNCH_CHECK();
   const int Smax = 2 * Lmax + 1;
   CtcP p{B, T, V, Lmax, Smax, logits, ldt, lse, hlens, ys, ldys, ylens, alpha, beta, nll, loss_utt};
@@ -453,7 +482,7 @@ extern "C" int ea_lsm_loss_fwd(long rows, int V, const float* x, long ldx, const
   hipStream_t st = (hipStream_t)stream;
   hipMemsetAsync(stat, 0, 2 * sizeof(int), st);
   LsmP p{rows, V, x, ldx, tgt, smoothing, ignore_id, lse, loss_row, stat};
-  hipLaunchKernelGGL(lsm_fwd_kernel, dim3(ea_cdiv(rows, 4)), dim3(256), 0, st, p);
+  hipLaunchKernelGGL(lsm_fwd_kernel, dim3(rows), dim3(256), 0, st, p);
   EA_LAUNCH_CHECK();
   hipLaunchKernelGGL(lsm_finalize_kernel, dim3(1), dim3(256), 0, st, rows, loss_row, stat, normalize_length, batch, loss, acc, inv_denom);
   EA_LAUNCH_CHECK();

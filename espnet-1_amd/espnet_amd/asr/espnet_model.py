@@ -8,6 +8,7 @@ force_gatherable shapes).  Runtime: call `prepare(device, amp)` once after const
 """
 from __future__ import annotations
 
+import ctypes
 import logging
 from typing import Dict, List, Optional, Tuple, Union
 
@@ -41,7 +42,11 @@ class UtteranceMVN(nn.Module):
     def forward(self, x, ilens):
         B, T, F = x.shape
         y = torch.empty_like(x)
-        lib.ea_utterance_mvn(B, T, F, x.data_ptr(), ilens.data_ptr(), y.data_ptr(), ops.stream())
+        n = ctypes.c_long(0)
+        lib.ea_utterance_mvn_ws_bytes(B, T, F, ctypes.addressof(n))
+        ws = torch.empty(max(n.value, 8), dtype=torch.uint8, device=x.device)
+        lib.ea_utterance_mvn2(B, T, F, x.data_ptr(), ilens.data_ptr(), y.data_ptr(), ws.data_ptr(), ws.numel(),
+                              ops.stream())
         return y, ilens
 
 

@@ -242,6 +242,11 @@ int ea_batchnorm_bwd(int rows, int C, const void* dz, int dz_dtype, const float*
 /* utterance_mvn(norm_means=True, norm_vars=False), espnet2/layers/utterance_mvn.py:45-88:
  * x (B,T,F) f32 -> y = (x masked to valid frames) - per-utterance mean. F <= 256. */
 int ea_utterance_mvn(int B, int T, int F, const float* x, const long long* lens, float* y, void* stream);
+/* Same op over a (32-row chunk, utterance) grid in two launches (chunk column sums in f64,
+ * then mean + write); ws holds ea_utterance_mvn_ws_bytes(B, T, F) bytes (any alignment of 8). */
+int ea_utterance_mvn_ws_bytes(int B, int T, int F, long* bytes);
+int ea_utterance_mvn2(int B, int T, int F, const float* x, const long long* lens, float* y, void* ws,
+                      long ws_bytes, void* stream);
 
 /* Raw-waveform frontend (espnet2/asr/frontend/default.py:17-140), four launches around two
  * f32 GEMMs (ea_gemm, exact-f32 MFMA):
