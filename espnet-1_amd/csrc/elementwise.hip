@@ -3,6 +3,9 @@
 // All grid-stride, coalesced along the contiguous (channel) dimension.
 #include "common.h"
 
+#include <cstdlib>
+#include <cstring>
+
 namespace {
 
 // ---------------------------------------------------------------- input prep
@@ -185,7 +188,7 @@ __global__ __launch_bounds__(256) void conv1_fwd_kernel(int B, int T, int F, Pha
 // channels, 8 per lane): blocks stride over output rows (b, t1), so the index arithmetic is
 // per row and wave-uniform (scalar), the 9 taps of a pixel are wave-uniform loads, and the
 // per-pixel vector work is the 72 FMAs, ReLU, bf16 packing and the support byte.
-template <typename TO>
+template <typename TO, bool NT>
 __global__ __launch_bounds__(256) void conv1_fwd_rows_kernel(int B, int T, int F, PhaseGeo g, int C,
                                                              const float* __restrict__ x, const float* __restrict__ w,
                                                              const float* __restrict__ bias, TO* __restrict__ y,
@@ -209,32 +212,52 @@ __global__ __launch_bounds__(256) void conv1_fwd_rows_kernel(int B, int T, int F
     const int a = t1 & 1;
     const int nI = a ? g.nI1 : g.nI0;
     const float* xr = x + ((long)b * T + 2 * t1) * F;
-    for (int f1 = pw; f1 < g.F1; f1 += ppb) {
-      const float* xp = xr + 2 * f1;
-      float xv[9];
+    const long rbase = (long)(b * nI + (t1 >> 1));
+    // two pixels per step: both pixels' taps are in flight before either is computed
+    for (int f0 = pw; f0 < g.F1; f0 += 2 * ppb) {
+      const int fb = f0 + ppb < g.F1 ? f0 + ppb : f0;  // odd tail: recompute f0 (same values)
+      float xv[2][9];
 #pragma unroll
-      for (int kh = 0; kh < 3; ++kh)
+      for (int u = 0; u < 2; ++u) {
+        const float* xp = xr + 2 * (u ? fb : f0);
 #pragma unroll
-        for (int kw = 0; kw < 3; ++kw) xv[kh * 3 + kw] = xp[kh * F + kw];
-      const int e = f1 & 1;
-      const long prow = g.plane[a * 2 + e] + ((long)(b * nI + (t1 >> 1)) * (e ? g.nJ1 : g.nJ0) + (f1 >> 1));
-      float o[8];
+        for (int kh = 0; kh < 3; ++kh)
 #pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        float s = br[k];
-#pragma unroll
-        for (int t = 0; t < 9; ++t) s = fmaf(wr[k][t], xv[t], s);
-        o[k] = s > 0.f ? s : 0.f;
+          for (int kw = 0; kw < 3; ++kw) xv[u][kh * 3 + kw] = xp[kh * F + kw];
       }
-      TO* yp = y + prow * C + c0;
-      float lo[4] = {o[0], o[1], o[2], o[3]}, hi[4] = {o[4], o[5], o[6], o[7]};
-      vst4(yp, lo);
-      vst4(yp + 4, hi);
-      if (pos) {
-        uint32_t m = 0;
 #pragma unroll
-        for (int k = 0; k < 8; ++k) m |= (uint32_t)((float)(TO)o[k] > 0.f) << k;
-        pos[prow * (C / 8) + cg] = (uint8_t)m;
+      for (int u = 0; u < 2; ++u) {
+        const int f1 = u ? fb : f0;
+        const int e = f1 & 1;
+        const long prow = g.plane[a * 2 + e] + rbase * (e ? g.nJ1 : g.nJ0) + (f1 >> 1);
+        float o[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          float s = br[k];
+#pragma unroll
+          for (int t = 0; t < 9; ++t) s = fmaf(wr[k][t], xv[u][t], s);
+          o[k] = s > 0.f ? s : 0.f;
+        }
+        TO* yp = y + prow * C + c0;
+        if constexpr (sizeof(TO) == 2) {  // one 16-B store per lane
+          typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+          union { u32x4 u; TO h[8]; } pk;
+#pragma unroll
+          for (int k = 0; k < 8; ++k) pk.h[k] = (TO)o[k];
+          if (NT) __builtin_nontemporal_store(pk.u, (u32x4*)yp);
+          else *(u32x4*)yp = pk.u;
+        } else {
+          float lo[4] = {o[0], o[1], o[2], o[3]}, hi[4] = {o[4], o[5], o[6], o[7]};
+          vst4(yp, lo);
+          vst4(yp + 4, hi);
+        }
+        if (pos) {
+          uint32_t m = 0;
+#pragma unroll
+          for (int k = 0; k < 8; ++k) m |= (uint32_t)((float)(TO)o[k] > 0.f) << k;
+          if (NT) __builtin_nontemporal_store((uint8_t)m, pos + prow * (C / 8) + cg);
+          else pos[prow * (C / 8) + cg] = (uint8_t)m;
+        }
       }
     }
   }
@@ -1154,6 +1177,11 @@ extern "C" int ea_argmax_rows(long rows, int V, const float* x, long ld, long lo
   return 0;
 }
 
+static bool getenv_is(const char* name, const char* v) {
+  const char* e = std::getenv(name);
+  return e != nullptr && std::strcmp(e, v) == 0;
+}
+
 static PhaseGeo phase_geo(int B, int T1, int F1, int C) {
   PhaseGeo g;
   g.T1 = T1; g.F1 = F1;
@@ -1175,13 +1203,26 @@ extern "C" int ea_conv1_fwd2(int B, int T, int F, int C, const float* x, const f
   const long npix = (long)B * T1 * F1;
   static const bool pix_kernel = std::getenv("EA_CONV1_FWD_PIX") != nullptr;  // A/B switch
   if ((C == 512 || C == 1024 || C == 2048) && (long)B * T1 < (1L << 31) && !pix_kernel) {
-    // 2048 blocks: each loads its 80 weights per lane once and walks ~B*T1/2048 rows
-    dim3 grid((unsigned)std::min<long>((long)B * T1, 2048));
-    if (dtype == EA_BF16)
-      hipLaunchKernelGGL(conv1_fwd_rows_kernel<bf16>, grid, dim3(256), 0, (hipStream_t)stream, B, T, F, g, C, x, w,
-                         bias, (bf16*)x1p, pos);
+    // one resident wave of blocks: each loads its 80 weights per lane once and walks rows
+    static int resident = 0;
+    if (!resident) {
+      int per_cu = 0, dev = 0, ncu = 0;
+      (void)hipGetDevice(&dev);
+      (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+      (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, conv1_fwd_rows_kernel<bf16, false>, 256, 0);
+      resident = std::max(1, per_cu) * std::max(1, ncu);
+    }
+    dim3 grid((unsigned)std::min<long>((long)B * T1, resident));
+    // streaming stores (the 0.6 GB output exceeds L2 + MALL): 210 -> 168 us at the C3 shape
+    static const bool nt = !getenv_is("EA_CONV1_FWD_NT", "0");
+    if (dtype == EA_BF16 && nt)
+      hipLaunchKernelGGL((conv1_fwd_rows_kernel<bf16, true>), grid, dim3(256), 0, (hipStream_t)stream, B, T, F, g, C,
+                         x, w, bias, (bf16*)x1p, pos);
+    else if (dtype == EA_BF16)
+      hipLaunchKernelGGL((conv1_fwd_rows_kernel<bf16, false>), grid, dim3(256), 0, (hipStream_t)stream, B, T, F, g, C,
+                         x, w, bias, (bf16*)x1p, pos);
     else
-      hipLaunchKernelGGL(conv1_fwd_rows_kernel<float>, grid, dim3(256), 0, (hipStream_t)stream, B, T, F, g, C, x, w,
+      hipLaunchKernelGGL((conv1_fwd_rows_kernel<float, false>), grid, dim3(256), 0, (hipStream_t)stream, B, T, F, g, C, x, w,
                          bias, (float*)x1p, pos);
     EA_LAUNCH_CHECK();
     return 0;
