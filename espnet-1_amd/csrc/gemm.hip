@@ -3,6 +3,8 @@
 // the LDS-DMA kernels of gemm_kern.h (instantiated in gemm_pipe*.hip and gemm_lds*.hip).
 
 #include "gemm_kern.h"
+#include <cstdio>
+#include <cstdlib>
 
 namespace {
 // split-K combine: C = epi(sum_s slab[s]) (any epilogue kind), 4 columns per thread
@@ -257,6 +259,10 @@ static int gemm_impl(int dtype, int a_kmajor, int b_kmajor, int M, int N, int K,
   }
   p.splitk = splitk;
   p.kchunk = kchunk;
+  static const bool trace = std::getenv("EA_GEMM_TRACE") != nullptr;  // shape census (diagnostics)
+  if (trace)
+    std::fprintf(stderr, "[ea_gemm] M=%d N=%d K=%d ak=%d bk=%d nz=%d tile=%dx%d splitk=%d epi=%d geo=%d lds=%d\n", M,
+                 N, K, a_kmajor, b_kmajor, nz, p.bm, p.bn, splitk, (int)epi->kind, geo ? geo->mode : 0, (int)p.lds);
   hipStream_t st = (hipStream_t)stream;
   int rc = dtype == EA_BF16 ? launch<bf16>(p, a_kmajor, b_kmajor, nz, st)
                             : launch<float>(p, a_kmajor, b_kmajor, nz, st);

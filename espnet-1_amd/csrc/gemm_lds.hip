@@ -1,6 +1,8 @@
 // Dense GEMM launches on the 2-stage LDS-DMA kernel (gemm_kern.h: gemm_bf16_lds).
 #include "gemm_kern.h"
 
+#include <cstdlib>
+
 namespace eag {
 int launch_lds_dense(GemmP& p, int a_k, int b_k, dim3 grid, hipStream_t st) {
 #define EA_GL(BMV, BNV, AKV, BKV, S) \
@@ -10,9 +12,18 @@ int launch_lds_dense(GemmP& p, int a_k, int b_k, dim3 grid, hipStream_t st) {
   else if (a_k) EA_GL(BMV, BNV, true, false, S);       \
   else if (b_k) EA_GL(BMV, BNV, false, true, S);       \
   else EA_GL(BMV, BNV, false, false, S);
+  static const int s64 = [] { const char* e = std::getenv("EA_LDS64_STAGES"); return e ? std::atoi(e) : 2; }();
   if (p.bm == 64) {
-    if (b_k) EA_GL(64, 128, true, true, 2);
-    else EA_GL(64, 128, true, false, 2);
+    if (s64 == 3) {
+      if (b_k) EA_GL(64, 128, true, true, 3);
+      else EA_GL(64, 128, true, false, 3);
+    } else if (s64 == 4) {
+      if (b_k) EA_GL(64, 128, true, true, 4);
+      else EA_GL(64, 128, true, false, 4);
+    } else {
+      if (b_k) EA_GL(64, 128, true, true, 2);
+      else EA_GL(64, 128, true, false, 2);
+    }
   } else if (p.bm == 256 && p.bn == 256) {
     EA_GL4(256, 256, 2)
   } else {

@@ -390,15 +390,21 @@ __global__ __launch_bounds__(256) void ln_fwd_vec_kernel(int rows, int d, const 
 // dx (+)= rstd*(dxh - mean(dxh) - xh*mean(dxh*xh)) with dxh = dy*gamma, and this block's
 // partial dgamma = sum dy*xh, dbeta = sum dy over its rows (part[blk][0:d], part[blk][d:2d];
 // the 4 waves' sums combined in fixed order), all from one read of dy and x.
-template <int NJ, typename TI>
+// DROP: also y = dropout(yscale * dx_new) in bf16 (element index r*d + c, the law and salt
+// of ea_scale_dropout): the next residual site's dropout backward, without re-reading dx.
+struct LnDrop {
+  bf16* y; long ldy; float scale, p; uint64_t seed; const unsigned long long* salt;
+};
+template <int NJ, typename TI, bool DROP = false>
 __global__ __launch_bounds__(256) void ln_bwd_vec_kernel(int rows, int d, const TI* __restrict__ dy, long lddy,
                                                          const float* __restrict__ x, long ldx,
                                                          const float* __restrict__ g, const float* __restrict__ mean,
                                                          const float* __restrict__ rstd, float* __restrict__ dx,
                                                          long lddx, int accumulate, int rows_per_blk,
-                                                         float* __restrict__ part) {
+                                                         float* __restrict__ part, LnDrop dr = LnDrop{}) {
   __shared__ float red[4][2][512 * NJ];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  if (DROP && dr.p > 0.f) dr.seed = ea_salted(dr.seed, dr.salt);
   float gg[NJ][8], pg[NJ][8], pb[NJ][8];
 #pragma unroll
   for (int j = 0; j < NJ; ++j) {
@@ -445,6 +451,17 @@ __global__ __launch_bounds__(256) void ln_bwd_vec_kernel(int rows, int d, const 
 #pragma unroll
       for (int i = 0; i < 8; ++i) v[i] = rs * (dg[j][i] - s1 - xh[j][i] * s2) + (accumulate ? prev[i] : 0.f);
       st8(o, v);
+      if constexpr (DROP) {
+        float lo[4], hi[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) { lo[i] = v[i] * dr.scale; hi[i] = v[i + 4] * dr.scale; }
+        const uint64_t e = (uint64_t)r * d + c;
+        drop_scale4(dr.seed, e, dr.p, lo);
+        drop_scale4(dr.seed, e + 4, dr.p, hi);
+        bf16* yo = dr.y + (long)r * dr.ldy + c;
+        vst4(yo, lo);
+        vst4(yo + 4, hi);
+      }
     }
   }
 #pragma unroll
@@ -810,9 +827,11 @@ extern "C" int ea_layernorm_fwd(int rows, int d, const float* x, long ldx, const
 static int ln_bwd_impl(int rows, int d, const void* dy, int dy_dtype, long lddy, const float* x, long ldx,
                        const float* gamma, const float* mean, const float* rstd, float* dx, long lddx, int accumulate,
                        float* dgamma, int accumulate_params, float* workspace, long ws_elems, int* nparts_out,
-                       hipStream_t st) {
+                       hipStream_t st, const LnDrop* drop = nullptr) {
   if (nparts_out) *nparts_out = 0;
   if (rows == 0) return 0;
+  // the dropout output in-kernel: vectorized path, bf16 dy and y, 16-B aligned y rows
+  const bool kdrop = drop && dy_dtype == EA_BF16 && drop->ldy % 8 == 0 && ((uintptr_t)drop->y % 16) == 0;
   const bool vec = d % 4 == 0 && lddy % 4 == 0 && ldx % 4 == 0 && ((uintptr_t)x % 16) == 0 &&
                    ((uintptr_t)dy % (dy_dtype == EA_BF16 ? 8 : 16)) == 0;
   if (!vec) {  // generic fused path (row kernel + per-block partials)
@@ -838,7 +857,10 @@ static int ln_bwd_impl(int rows, int d, const void* dy, int dy_dtype, long lddy,
     const int nb = ea_cdiv(rows, rpb);
     EA_CHECK_ARG(ws_elems >= (long)nb * 2 * d);
 #define EA_LNB(NJ)                                                                                        \
-  if (dy_dtype == EA_BF16)                                                                                \
+  if (kdrop)                                                                                              \
+    hipLaunchKernelGGL((ln_bwd_vec_kernel<NJ, bf16, true>), dim3(nb), dim3(256), 0, st, rows, d, (const bf16*)dy, lddy, \
+                       x, ldx, gamma, mean, rstd, dx, lddx, accumulate, rpb, workspace, *drop);            \
+  else if (dy_dtype == EA_BF16)                                                                           \
     hipLaunchKernelGGL((ln_bwd_vec_kernel<NJ, bf16>), dim3(nb), dim3(256), 0, st, rows, d, (const bf16*)dy, lddy, x, ldx, \
                        gamma, mean, rstd, dx, lddx, accumulate, rpb, workspace);                           \
   else                                                                                                    \
@@ -873,6 +895,47 @@ static int ln_bwd_impl(int rows, int d, const void* dy, int dy_dtype, long lddy,
                      workspace, (long)2 * d, dgamma, accumulate_params);
   EA_LAUNCH_CHECK();
   return 0;
+}
+
+// ln_bwd_impl + the dropout output: in the LN kernel when it can (kdrop above, vectorized
+// rows), otherwise as an ea_scale_dropout pass over the finished dx.
+static int ln_bwd_drop_impl(int rows, int d, const void* dy, int dy_dtype, long lddy, const float* x, long ldx,
+                            const float* gamma, const float* mean, const float* rstd, float* dx, long lddx,
+                            int accumulate, float* dgamma, int accumulate_params, float* workspace, long ws_elems,
+                            int* nparts_out, void* y, int y_dtype, long ldy, float yscale, float p,
+                            unsigned long long seed, hipStream_t st) {
+  const LnDrop dr{(bf16*)y, ldy, yscale, p, (uint64_t)seed, ea_g_rng_salt};
+  const bool vec8 = d % 8 == 0 && d <= 1024 && lddy % 8 == 0 && ldx % 4 == 0 && lddx % 4 == 0 &&
+                    ((uintptr_t)x % 16) == 0 && ((uintptr_t)dy % 16) == 0 && ((uintptr_t)dx % 16) == 0 &&
+                    ((uintptr_t)gamma % 16) == 0;
+  const bool in_kernel = vec8 && y_dtype == EA_BF16 && dy_dtype == EA_BF16 && ldy % 8 == 0 && ((uintptr_t)y % 16) == 0;
+  int rc = ln_bwd_impl(rows, d, dy, dy_dtype, lddy, x, ldx, gamma, mean, rstd, dx, lddx, accumulate, dgamma,
+                       accumulate_params, workspace, ws_elems, nparts_out, st, in_kernel ? &dr : nullptr);
+  if (rc || in_kernel || rows == 0) return rc;
+  return ea_scale_dropout(rows, d, dx, EA_F32, lddx, y, y_dtype, ldy, yscale, p, seed, st);
+}
+
+extern "C" int ea_layernorm_bwd_drop(int rows, int d, const void* dy, int dy_dtype, long lddy, const float* x,
+                                     long ldx, const float* gamma, const float* mean, const float* rstd, float* dx,
+                                     long lddx, int accumulate, float* dgamma, float* dbeta, int accumulate_params,
+                                     float* workspace, long ws_elems, void* y, int y_dtype, long ldy, float yscale,
+                                     float p, unsigned long long seed, void* stream) {
+  EA_ENTRY();
+  EA_CHECK_ARG(dgamma != nullptr && dbeta == dgamma + d && y != nullptr && (y_dtype == EA_BF16 || y_dtype == EA_F32));
+  return ln_bwd_drop_impl(rows, d, dy, dy_dtype, lddy, x, ldx, gamma, mean, rstd, dx, lddx, accumulate, dgamma,
+                          accumulate_params, workspace, ws_elems, nullptr, y, y_dtype, ldy, yscale, p, seed,
+                          (hipStream_t)stream);
+}
+
+extern "C" int ea_layernorm_bwd_partials_drop(int rows, int d, const void* dy, int dy_dtype, long lddy,
+                                              const float* x, long ldx, const float* gamma, const float* mean,
+                                              const float* rstd, float* dx, long lddx, int accumulate, float* part,
+                                              long part_elems, int* nparts, void* y, int y_dtype, long ldy,
+                                              float yscale, float p, unsigned long long seed, void* stream) {
+  EA_ENTRY();
+  EA_CHECK_ARG(part != nullptr && nparts != nullptr && y != nullptr && (y_dtype == EA_BF16 || y_dtype == EA_F32));
+  return ln_bwd_drop_impl(rows, d, dy, dy_dtype, lddy, x, ldx, gamma, mean, rstd, dx, lddx, accumulate, nullptr, 0,
+                          part, part_elems, nparts, y, y_dtype, ldy, yscale, p, seed, (hipStream_t)stream);
 }
 
 extern "C" int ea_layernorm_bwd(int rows, int d, const void* dy, int dy_dtype, long lddy, const float* x,

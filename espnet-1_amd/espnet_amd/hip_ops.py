@@ -508,22 +508,39 @@ def layernorm_fwd(x, gamma, beta, y, mean, rstd, eps=1e-12):
                          mean.data_ptr(), rstd.data_ptr(), stream())
 
 
-def layernorm_bwd(dy, x, gamma, mean, rstd, dx, dgamma, dbeta, accumulate=True):
+def layernorm_bwd(dy, x, gamma, mean, rstd, dx, dgamma, dbeta, accumulate=True, drop=None):
+    """drop=(y, scale, p, seed): also y = dropout(scale * dx) once dx is final (the next residual
+    site's dropout backward, ea_layernorm_bwd_drop), instead of an ea_scale_dropout pass."""
     rows, d, ldx = _rows(x)
     _, _, lddy = _rows(dy)
     _, _, lddx = _rows(dx)
+    if drop is not None:
+        y, ysc, yp, yseed = drop
+        _, _, ldy = _rows(y)
+        dargs = (y.data_ptr(), dt(y), ldy, float(ysc), float(yp), yseed & 0xFFFFFFFFFFFFFFFF)
     if REDUCE_Q.active and rows > 0 and dbeta.data_ptr() == dgamma.data_ptr() + 4 * d:
         # dx now; the (dgamma | dbeta) row-block partials go to a buffer of their own and are
         # summed with the pass's other parameter-gradient reductions (REDUCE_Q.flush)
         nparts_max = max((rows + 15) // 16, 128)
         part = torch.empty(nparts_max * 2 * d, dtype=torch.float32, device=x.device)
         np_ = ctypes.c_int(0)
-        lib.ea_layernorm_bwd_partials(rows, d, dy.data_ptr(), dt(dy), lddy, x.data_ptr(), ldx, gamma.data_ptr(),
-                                      mean.data_ptr(), rstd.data_ptr(), dx.data_ptr(), lddx, int(accumulate),
-                                      part.data_ptr(), part.numel(), ctypes.addressof(np_), stream())
+        if drop is not None:
+            lib.ea_layernorm_bwd_partials_drop(rows, d, dy.data_ptr(), dt(dy), lddy, x.data_ptr(), ldx,
+                                               gamma.data_ptr(), mean.data_ptr(), rstd.data_ptr(), dx.data_ptr(),
+                                               lddx, int(accumulate), part.data_ptr(), part.numel(),
+                                               ctypes.addressof(np_), *dargs, stream())
+        else:
+            lib.ea_layernorm_bwd_partials(rows, d, dy.data_ptr(), dt(dy), lddy, x.data_ptr(), ldx, gamma.data_ptr(),
+                                          mean.data_ptr(), rstd.data_ptr(), dx.data_ptr(), lddx, int(accumulate),
+                                          part.data_ptr(), part.numel(), ctypes.addressof(np_), stream())
         REDUCE_Q.add_reduce(part, np_.value, 2 * d, 2 * d, dgamma, accumulate=True)
         return
     w, n = _ws(x.device, max(1 << 22, 1024 * d))
+    if drop is not None:
+        lib.ea_layernorm_bwd_drop(rows, d, dy.data_ptr(), dt(dy), lddy, x.data_ptr(), ldx, gamma.data_ptr(),
+                                  mean.data_ptr(), rstd.data_ptr(), dx.data_ptr(), lddx, int(accumulate),
+                                  dgamma.data_ptr(), dbeta.data_ptr(), 1, w, n, *dargs, stream())
+        return
     lib.ea_layernorm_bwd(rows, d, dy.data_ptr(), dt(dy), lddy, x.data_ptr(), ldx, gamma.data_ptr(),
                          mean.data_ptr(), rstd.data_ptr(), dx.data_ptr(), lddx, int(accumulate),
                          dgamma.data_ptr(), dbeta.data_ptr(), 1, w, n, stream())

@@ -20,7 +20,7 @@ from .._lib import (ACT_NONE, ACT_RELU, ACT_SWISH, EPI_ACT, EPI_DACT, EPI_RESID,
 __all__ = ["Bound", "rup", "empty", "ops", "lib", "EPI_ACT", "EPI_DACT", "EPI_RESID",
            "EPI_STORE", "ACT_NONE", "ACT_RELU", "ACT_SWISH", "site_seed", "attn_fwd", "attn_bwd",
            "LayerNormFn", "ln_fwd", "ln_bwd", "math", "F32", "fused_attn_ok", "attn_dmask", "ptr",
-           "attn_fused_bwd"]
+           "attn_fused_bwd", "dv_buf", "drop_arg", "site_dv"]
 
 F32 = torch.float32
 
@@ -118,9 +118,38 @@ def ln_fwd(x2d, b: Bound, name: str, out_dtype):
     return y, mu, rs
 
 
-def ln_bwd(dy, x2d, b: Bound, name: str, mu, rs, dx, accumulate=True):
+def ln_bwd(dy, x2d, b: Bound, name: str, mu, rs, dx, accumulate=True, drop=None):
     ops.layernorm_bwd(dy, x2d, b.f(_n(name, "weight")), mu, rs, dx, b.g(_n(name, "weight")),
-                      b.g(_n(name, "bias")), accumulate=accumulate)
+                      b.g(_n(name, "bias")), accumulate=accumulate, drop=drop)
+
+
+# Every norm_* backward of a Conformer / Transformer block is followed by a residual dropout
+# backward (the next sub-block's output dropout, walking backward): with FUSE_LN_DROP the
+# LayerNorm kernel writes that site's dv = dropout(scale * dx) from the dx it has just finished
+# (ea_layernorm_bwd_drop), and the site keeps only the bias column sum.
+FUSE_LN_DROP = os.environ.get("EA_FUSE_LN_DROP", "1") != "0"
+
+
+def dv_buf(N, d, cd, dev):
+    """Pre-allocated dv of the next site when the LayerNorm backward writes it, else None."""
+    return empty(N, d, dtype=cd, device=dev) if FUSE_LN_DROP and cd == torch.bfloat16 else None
+
+
+def drop_arg(dv, scale, p, seed):
+    return None if dv is None else (dv, scale, p, seed)
+
+
+def site_dv(dx, dv, bias_g, scale, p, seed, cd):
+    """dv = dropout(scale * dx) (+ bias column sum) of a residual site; dv already written by
+    the preceding LayerNorm backward when given."""
+    if dv is not None:
+        with ops.wgrad(dv):
+            ops.colsum(dv, bias_g)
+        return dv
+    N, d = dx.shape
+    dv = empty(N, d, dtype=cd, device=dx.device)
+    ops.scale_dropout_colsum(dx, dv, bias_g, scale=scale, p=p, seed=seed)
+    return dv
 
 
 class LayerNormFn(torch.autograd.Function):

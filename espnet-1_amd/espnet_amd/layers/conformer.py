@@ -17,7 +17,7 @@ from torch import nn
 
 from .common import (ACT_SWISH, EPI_ACT, EPI_DACT, EPI_RESID, EPI_STORE, F32, Bound, attn_bwd, attn_dmask,
                      attn_fused_bwd, attn_fwd, empty, fused_attn_ok, lib, ln_bwd, ln_fwd, math, ops, ptr, rup,
-                     site_seed)
+                     site_seed, dv_buf, drop_arg, site_dv)
 
 
 # ----------------------------------------------------------------------------- holders
@@ -139,13 +139,14 @@ def _ffn_fwd(L, b, x_in, pre, ln_name, p, seed_in, seed_out):
     return x_out, (xn, mu, rs, h, a)
 
 
-def _ffn_bwd(L, b, dx, x_in, saved, pre, ln_name, p, seed_in, seed_out):
-    """dx: f32 (N,d) grad of the sub-block output; updated in place to grad of x_in."""
+def _ffn_bwd(L, b, dx, x_in, saved, pre, ln_name, p, seed_in, seed_out, dv_in=None, next_drop=None):
+    """dx: f32 (N,d) grad of the sub-block output; updated in place to grad of x_in.  dv_in: this
+    site's dv when already written; next_drop: the following site's (dv, scale, p, seed) for the
+    LayerNorm backward to write."""
     cd = b.cd
     xn, mu, rs, h, a = saved
     N, d = dx.shape
-    dv = empty(N, d, dtype=cd, device=dx.device)
-    ops.scale_dropout_colsum(dx, dv, b.g(pre + ".w_2.bias"), scale=L.ff_scale, p=p, seed=seed_out)
+    dv = site_dv(dx, dv_in, b.g(pre + ".w_2.bias"), L.ff_scale, p, seed_out, cd)
     with ops.wgrad(dv, a):
         ops.linear_dw(dv, a, b.g(pre + ".w_2.weight"), accumulate=True)
     dh = empty(*h.shape, dtype=cd, device=dx.device)
@@ -156,7 +157,7 @@ def _ffn_bwd(L, b, dx, x_in, saved, pre, ln_name, p, seed_in, seed_out):
         ops.linear_dw(dh, xn, b.g(pre + ".w_1.weight"), accumulate=True)
     dxn = empty(N, d, dtype=cd, device=dx.device)
     ops.linear_dx(dh, b.w(pre + ".w_1.weight"), dxn)
-    ln_bwd(dxn, x_in, b, ln_name, mu, rs, dx, accumulate=True)
+    ln_bwd(dxn, x_in, b, ln_name, mu, rs, dx, accumulate=True, drop=next_drop)
 
 
 class ConformerBlockFn(torch.autograd.Function):
@@ -265,15 +266,18 @@ class ConformerBlockFn(torch.autograd.Function):
         dev = dout.device
         P2 = 2 * T - 1
         dx = empty(N, d, device=dev)
-        ln_bwd(dout.reshape(N, d).contiguous(), x4, b, "norm_final", mu5, rs5, dx, accumulate=False)
+        dv_ff2 = dv_buf(N, d, cd, dev)
+        ln_bwd(dout.reshape(N, d).contiguous(), x4, b, "norm_final", mu5, rs5, dx, accumulate=False,
+               drop=drop_arg(dv_ff2, L.ff_scale, p, sd(7)))
         # ---- FFN
-        _ffn_bwd(L, b, dx, x3, s_ff2, "feed_forward", "norm_ff", p, sd(6), sd(7))
+        dv_conv = dv_buf(N, d, cd, dev)
+        _ffn_bwd(L, b, dx, x3, s_ff2, "feed_forward", "norm_ff", p, sd(6), sd(7), dv_in=dv_ff2,
+                 next_drop=drop_arg(dv_conv, 1.0, p, sd(5)))
         # ---- conv module
         C = "conv_module."
         K = L.conv_module.kernel_size
         xn3, mu3, rs3, g2, glu, y, z, bn_mean, bn_rstd = s_conv
-        dv = empty(N, d, dtype=cd, device=dev)
-        ops.scale_dropout_colsum(dx, dv, b.g(C + "pointwise_conv2.bias"), p=p, seed=sd(5))
+        dv = site_dv(dx, dv_conv, b.g(C + "pointwise_conv2.bias"), 1.0, p, sd(5), cd)
         with ops.wgrad(dv, z):
             ops.linear_dw(dv, z, b.g(C + "pointwise_conv2.weight", shape=(d, d)), accumulate=True)
         dz = empty(N, d, dtype=cd, device=dev)
@@ -293,12 +297,12 @@ class ConformerBlockFn(torch.autograd.Function):
             ops.linear_dw(dg2, xn3, b.g(C + "pointwise_conv1.weight", shape=(2 * d, d)), accumulate=True)
         dxn3 = empty(N, d, dtype=cd, device=dev)
         ops.linear_dx(dg2, b.w(C + "pointwise_conv1.weight", shape=(2 * d, d)), dxn3)
-        ln_bwd(dxn3, x2, b, "norm_conv", mu3, rs3, dx, accumulate=True)
+        dv_att = dv_buf(N, d, cd, dev)
+        ln_bwd(dxn3, x2, b, "norm_conv", mu3, rs3, dx, accumulate=True, drop=drop_arg(dv_att, 1.0, p, sd(4)))
         # ---- rel-pos MHSA
         A = "self_attn."
         xn2, mu2, rs2, qkv, pp, O, s_core = s_att
-        dv = empty(N, d, dtype=cd, device=dev)
-        ops.scale_dropout_colsum(dx, dv, b.g(A + "linear_out.bias"), p=p, seed=sd(4))
+        dv = site_dv(dx, dv_att, b.g(A + "linear_out.bias"), 1.0, p, sd(4), cd)
         with ops.wgrad(dv, O):
             ops.linear_dw(dv, O, b.g(A + "linear_out.weight"), accumulate=True)
         dO = empty(N, d, dtype=cd, device=dev)
@@ -351,8 +355,9 @@ class ConformerBlockFn(torch.autograd.Function):
                                           shape=(3 * d, d)), accumulate=True)
         dxn2 = empty(N, d, dtype=cd, device=dev)
         ops.linear_dx(dqkv, qkv_w, dxn2)
-        ln_bwd(dxn2, x1, b, "norm_mha", mu2, rs2, dx, accumulate=True)
+        dv_ff1 = dv_buf(N, d, cd, dev)
+        ln_bwd(dxn2, x1, b, "norm_mha", mu2, rs2, dx, accumulate=True, drop=drop_arg(dv_ff1, L.ff_scale, p, sd(2)))
         # ---- macaron FFN
-        _ffn_bwd(L, b, dx, x0, s_ff1, "feed_forward_macaron", "norm_ff_macaron", p, sd(1), sd(2))
+        _ffn_bwd(L, b, dx, x0, s_ff1, "feed_forward_macaron", "norm_ff_macaron", p, sd(1), sd(2), dv_in=dv_ff1)
         ops.grad_ready(b)
         return dx.view(B, T, d), None, None, None, None, None

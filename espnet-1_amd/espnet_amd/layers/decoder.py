@@ -17,7 +17,7 @@ from torch import nn
 
 from .common import (ACT_RELU, EPI_ACT, EPI_DACT, EPI_RESID, EPI_STORE, F32, Bound, attn_bwd,
                      attn_dmask, attn_fused_bwd, attn_fwd, empty, fused_attn_ok, lib, ln_bwd, ln_fwd, ops, ptr,
-                     site_seed)
+                     site_seed, dv_buf, drop_arg, site_dv)
 
 
 def _mha_fwd(q, k, v, *, B, H, T1, T2, dk, ldq, ldk, ldv, klen, causal, scale, p, seed, cd):
@@ -222,7 +222,9 @@ class DecoderFn(torch.autograd.Function):
         dxf = empty(N, d, dtype=cd, device=dev)
         ops.linear_dx(dlog, b.w("output_layer.weight"), dxf)
         dx = empty(N, d, device=dev)
-        ln_bwd(dxf, xlast, b, "after_norm", muf, rsf, dx, accumulate=False)
+        # each norm backward also writes the dropout backward of the site below it (dv_buf)
+        dv_ff = dv_buf(N, d, cd, dev) if nb > 0 else None
+        ln_bwd(dxf, xlast, b, "after_norm", muf, rsf, dx, accumulate=False, drop=drop_arg(dv_ff, 1.0, p, sd(nb - 1, 6)))
         ldkv = 2 * d * nb
         dkv = empty(Nm, ldkv, dtype=cd, device=dev)
         for l in reversed(range(nb)):
@@ -231,8 +233,7 @@ class DecoderFn(torch.autograd.Function):
             x0, x1, x2, s1, s2, s3 = saved[l]
             # feed-forward
             xn3, mu3, rs3, h, a = s3
-            dv = empty(N, d, dtype=cd, device=dev)
-            ops.scale_dropout_colsum(dx, dv, b.g(ff + "w_2.bias"), p=p, seed=sd(l, 6))
+            dv = site_dv(dx, dv_ff, b.g(ff + "w_2.bias"), 1.0, p, sd(l, 6), cd)
             with ops.wgrad(dv, a):
                 ops.linear_dw(dv, a, b.g(ff + "w_2.weight"), accumulate=True)
             dh = empty(*h.shape, dtype=cd, device=dev)
@@ -243,11 +244,11 @@ class DecoderFn(torch.autograd.Function):
                 ops.linear_dw(dh, xn3, b.g(ff + "w_1.weight"), accumulate=True)
             dxn = empty(N, d, dtype=cd, device=dev)
             ops.linear_dx(dh, b.w(ff + "w_1.weight"), dxn)
-            ln_bwd(dxn, x2, b, n + "norm3", mu3, rs3, dx, accumulate=True)
+            dv_src = dv_buf(N, d, cd, dev)
+            ln_bwd(dxn, x2, b, n + "norm3", mu3, rs3, dx, accumulate=True, drop=drop_arg(dv_src, 1.0, p, sd(l, 4)))
             # source attention
             xn2, mu2, rs2, q2, O2, st2 = s2
-            dv = empty(N, d, dtype=cd, device=dev)
-            ops.scale_dropout_colsum(dx, dv, b.g(xa + "linear_out.bias"), p=p, seed=sd(l, 4))
+            dv = site_dv(dx, dv_src, b.g(xa + "linear_out.bias"), 1.0, p, sd(l, 4), cd)
             with ops.wgrad(dv, O2):
                 ops.linear_dw(dv, O2, b.g(xa + "linear_out.weight"), accumulate=True)
             dO = empty(N, d, dtype=cd, device=dev)
@@ -262,11 +263,11 @@ class DecoderFn(torch.autograd.Function):
                 ops.linear_dw(dq, xn2, b.g(xa + "linear_q.weight"), accumulate=True)
             dxn = empty(N, d, dtype=cd, device=dev)
             ops.linear_dx(dq, b.w(xa + "linear_q.weight"), dxn)
-            ln_bwd(dxn, x1, b, n + "norm2", mu2, rs2, dx, accumulate=True)
+            dv_self = dv_buf(N, d, cd, dev)
+            ln_bwd(dxn, x1, b, n + "norm2", mu2, rs2, dx, accumulate=True, drop=drop_arg(dv_self, 1.0, p, sd(l, 2)))
             # self attention
             xn1, mu1, rs1, qkv, O1, st1 = s1
-            dv = empty(N, d, dtype=cd, device=dev)
-            ops.scale_dropout_colsum(dx, dv, b.g(sa + "linear_out.bias"), p=p, seed=sd(l, 2))
+            dv = site_dv(dx, dv_self, b.g(sa + "linear_out.bias"), 1.0, p, sd(l, 2), cd)
             with ops.wgrad(dv, O1):
                 ops.linear_dw(dv, O1, b.g(sa + "linear_out.weight"), accumulate=True)
             dO = empty(N, d, dtype=cd, device=dev)
@@ -283,7 +284,8 @@ class DecoderFn(torch.autograd.Function):
                 ops.linear_dw(dqkv, xn1, b.g(*wn, shape=(3 * d, d)), accumulate=True)
             dxn = empty(N, d, dtype=cd, device=dev)
             ops.linear_dx(dqkv, b.w(*wn, shape=(3 * d, d)), dxn)
-            ln_bwd(dxn, x0, b, n + "norm1", mu1, rs1, dx, accumulate=True)
+            dv_ff = dv_buf(N, d, cd, dev) if l > 0 else None  # layer l-1's feed-forward site
+            ln_bwd(dxn, x0, b, n + "norm1", mu1, rs1, dx, accumulate=True, drop=drop_arg(dv_ff, 1.0, p, sd(l - 1, 6)))
         pe = dec.embed[1]
         lib.ea_embed_bwd(N, d, ys_in.data_ptr(), dx.data_ptr(), pe.xscale, p_pos, sd(0, 0),
                          b.g("embed.0.weight").data_ptr(), ops.stream())

@@ -200,6 +200,22 @@ int ea_layernorm_bwd_partials(int rows, int d, const void* dy, int dy_dtype, lon
                               float* dx, long lddx, int accumulate, float* part, long part_elems,
                               int* nparts, void* stream);
 
+/* The two entries above plus the next residual site's dropout backward: y = dropout(yscale *
+ * dx) after dx is final (ea_scale_dropout's mask law, index r*d + c), written by the LayerNorm
+ * kernel itself when dy and y are bf16 (vectorized rows), else by an ea_scale_dropout pass.
+ * Saves the f32 dx re-read of the Conformer block's backward (encoder_layer.py:115-171:
+ * every norm_* backward is followed by a dropout backward). */
+int ea_layernorm_bwd_drop(int rows, int d, const void* dy, int dy_dtype, long lddy, const float* x,
+                          long ldx, const float* gamma, const float* mean, const float* rstd, float* dx,
+                          long lddx, int accumulate, float* dgamma, float* dbeta, int accumulate_params,
+                          float* workspace, long ws_elems, void* y, int y_dtype, long ldy, float yscale,
+                          float p, unsigned long long seed, void* stream);
+int ea_layernorm_bwd_partials_drop(int rows, int d, const void* dy, int dy_dtype, long lddy,
+                                   const float* x, long ldx, const float* gamma, const float* mean,
+                                   const float* rstd, float* dx, long lddx, int accumulate, float* part,
+                                   long part_elems, int* nparts, void* y, int y_dtype, long ldy,
+                                   float yscale, float p, unsigned long long seed, void* stream);
+
 /* Grouped reductions of a backward pass's parameter gradients (bias grads of every Linear:
  * torch.nn.Linear bias.grad; LayerNorm weight/bias grads: torch.nn.LayerNorm in
  * espnet/nets/pytorch_backend/transformer/layer_norm.py:12-42).  A column-sum problem writes

@@ -20,7 +20,7 @@ SHAPES = [  # name, M, N, K, a_k, b_k, out dtype
     ("conv2 dcol", 151392, 4608, 512, 1, 0, torch.bfloat16),
     ("dec ffn fwd", 1280, 2048, 512, 1, 1, torch.bfloat16),
 ]
-TILES = [(0, 0), (64, 128), (128, 128), (256, 128), (256, 256)]
+TILES = [(0, 0), (64, 128), (128, 128), (256, 256)]
 
 
 def t(M, N, K, ak, bk, cdt, iters):

@@ -104,3 +104,60 @@ def test_grouped_reductions_match_per_call():
             assert torch.equal(o, r)
         assert torch.equal(dx_def, dx_ref)
         assert torch.equal(gb_def, gb_ref)
+
+
+@pytest.mark.parametrize("rows,d,ydt", [(7968, 512, torch.bfloat16), (1312, 1024, torch.bfloat16),
+                                        (100, 80, torch.bfloat16), (257, 256, torch.float32)])
+@pytest.mark.parametrize("partials", [False, True])
+def test_layernorm_bwd_drop_matches_two_pass(rows, d, ydt, partials):
+    """ea_layernorm_bwd_drop / _partials_drop (dx plus the next site's y = dropout(scale*dx)) vs
+    ea_layernorm_bwd / _partials then ea_scale_dropout, in-kernel (bf16 y, vector rows) and
+    pass fallback: y bit-identical to the dropout of the launch's own dx."""
+    import ctypes
+    from espnet_amd import hip_ops as ops
+    from espnet_amd._lib import lib
+    lib.ea_set_rng_salt(None)
+    g = torch.Generator().manual_seed(rows * d)
+    x = (torch.randn(rows, d, generator=g) * 2 + 1).cuda()
+    gamma = (torch.rand(d, generator=g) + 0.5).cuda()
+    beta = torch.randn(d, generator=g).cuda()
+    dy = torch.randn(rows, d, generator=g).to(torch.bfloat16).cuda()
+    yln = torch.empty(rows, d, dtype=torch.bfloat16, device="cuda")
+    mu = torch.empty(rows, device="cuda")
+    rs = torch.empty(rows, device="cuda")
+    ops.layernorm_fwd(x, gamma, beta, yln, mu, rs)
+    dx0 = torch.randn(rows, d, generator=g).cuda()
+    res = []
+    for fused in (False, True):
+        dx = dx0.clone()
+        y = torch.empty(rows, d, dtype=ydt, device="cuda")
+        par = torch.zeros(2 * d, device="cuda")
+        if partials:
+            part = torch.empty(max((rows + 15) // 16, 128) * 2 * d, device="cuda")
+            npart = ctypes.c_int(0)
+            args = (rows, d, dy.data_ptr(), ops.dt(dy), d, x.data_ptr(), d, gamma.data_ptr(), mu.data_ptr(),
+                    rs.data_ptr(), dx.data_ptr(), d, 1, part.data_ptr(), part.numel(), ctypes.addressof(npart))
+            if fused:
+                lib.ea_layernorm_bwd_partials_drop(*args, y.data_ptr(), ops.dt(y), d, 0.5, 0.1, 99, ops.stream())
+            else:
+                lib.ea_layernorm_bwd_partials(*args, ops.stream())
+            ops.reduce_rows(part, npart.value, 2 * d, 2 * d, par)
+        else:
+            ops.layernorm_bwd(dy, x, gamma, mu, rs, dx, par[:d], par[d:], accumulate=True,
+                              drop=(y, 0.5, 0.1, 99) if fused else None)
+        if not fused:
+            ops.scale_dropout(dx, y, scale=0.5, p=0.1, seed=99)
+        torch.cuda.synchronize()
+        res.append((dx, y, par))
+    (dx1, y1, p1), (dx2, y2, p2) = res
+    # y is exactly the site's dropout of the dx this launch wrote; dx and the parameter sums
+    # match the plain kernel to f32 rounding (the compiler may contract the variants' FMAs
+    # differently)
+    y3 = torch.empty_like(y2)
+    ops.scale_dropout(dx2, y3, scale=0.5, p=0.1, seed=99)
+    torch.cuda.synchronize()
+    assert torch.equal(y2, y3)
+    torch.testing.assert_close(dx2, dx1, atol=1e-5, rtol=1e-5)
+    torch.testing.assert_close(p2, p1, atol=1e-4, rtol=1e-5)
+    torch.testing.assert_close(y2.float(), y1.float(), atol=1e-2, rtol=1e-2)
+    assert 0.08 < (y2 == 0).float().mean().item() < 0.12
