@@ -391,9 +391,12 @@ __global__ __launch_bounds__(256) void ln_fwd_vec_kernel(int rows, int d, const 
 // partial dgamma = sum dy*xh, dbeta = sum dy over its rows (part[blk][0:d], part[blk][d:2d];
 // the 4 waves' sums combined in fixed order), all from one read of dy and x.
 // DROP: also y = dropout(yscale * dx_new) in bf16 (element index r*d + c, the law and salt
-// of ea_scale_dropout): the next residual site's dropout backward, without re-reading dx.
+// of ea_scale_dropout): the next residual site's dropout backward, without re-reading dx;
+// with ypart, the block's column sums of the stored y (that site's bias gradient) go to
+// ypart[blk][0:d] the same way.
 struct LnDrop {
-  bf16* y; long ldy; float scale, p; uint64_t seed; const unsigned long long* salt;
+  bf16* y; long ldy; float scale, p; uint64_t seed; const unsigned long long* salt; float* ypart;
+  bool want_ycol; float* ycol;  // host side: column sums requested; their final target (direct mode)
 };
 template <int NJ, typename TI, bool DROP = false>
 __global__ __launch_bounds__(256) void ln_bwd_vec_kernel(int rows, int d, const TI* __restrict__ dy, long lddy,
@@ -402,10 +405,11 @@ __global__ __launch_bounds__(256) void ln_bwd_vec_kernel(int rows, int d, const 
                                                          const float* __restrict__ rstd, float* __restrict__ dx,
                                                          long lddx, int accumulate, int rows_per_blk,
                                                          float* __restrict__ part, LnDrop dr = LnDrop{}) {
-  __shared__ float red[4][2][512 * NJ];
+  constexpr int NS = DROP ? 3 : 2;
+  __shared__ float red[4][NS][512 * NJ];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   if (DROP && dr.p > 0.f) dr.seed = ea_salted(dr.seed, dr.salt);
-  float gg[NJ][8], pg[NJ][8], pb[NJ][8];
+  float gg[NJ][8], pg[NJ][8], pb[NJ][8], py[DROP ? NJ : 1][8];
 #pragma unroll
   for (int j = 0; j < NJ; ++j) {
     const int c = (lane + 64 * j) * 8;
@@ -413,26 +417,50 @@ __global__ __launch_bounds__(256) void ln_bwd_vec_kernel(int rows, int d, const 
 #pragma unroll
     for (int i = 0; i < 8; ++i) pg[j][i] = pb[j][i] = 0.f;
   }
+#pragma unroll
+  for (int j = 0; j < (DROP ? NJ : 1); ++j)
+#pragma unroll
+    for (int i = 0; i < 8; ++i) py[j][i] = 0.f;
   const int r0 = blockIdx.x * rows_per_blk, r1 = min(rows, r0 + rows_per_blk);
-  for (int r = r0 + w; r < r1; r += 4) {
-    const float mu = mean[r], rs = rstd[r];
+  // U rows per wave step (rows rb and rb + 4): every load of both rows is issued before
+  // either row is computed (the grid is ~2 waves per SIMD: latency, not bandwidth, bounds a
+  // one-row step).  Rows are still folded into the partials in order rb, rb + 4.
+  constexpr int U = NJ == 1 ? 2 : 1;
+  for (int rb = r0 + w; rb < r1; rb += 4 * U) {
+    float xv[U][NJ][8], dv[U][NJ][8], pv[U][NJ][8], mu[U], rs[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int r = rb + 4 * u < r1 ? rb + 4 * u : rb;  // no second row: reload the first (unused)
+      mu[u] = mean[r];
+      rs[u] = rstd[r];
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) {
+        const int c = (lane + 64 * j) * 8;
+        if (c < d) {
+          ld8(x + (long)r * ldx + c, xv[u][j]);
+          ld8(dy + (long)r * lddy + c, dv[u][j]);
+          if (accumulate) ld8(dx + (long)r * lddx + c, pv[u][j]);
+        }
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+    const int r = rb + 4 * u;
+    if (r >= r1) break;
     float xh[NJ][8], dg[NJ][8];
     float s1 = 0.f, s2 = 0.f;
 #pragma unroll
     for (int j = 0; j < NJ; ++j) {
       const int c = (lane + 64 * j) * 8;
       if (c < d) {
-        float xv[8], dv[8];
-        ld8(x + (long)r * ldx + c, xv);
-        ld8(dy + (long)r * lddy + c, dv);
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
-          xh[j][i] = (xv[i] - mu) * rs;
-          dg[j][i] = dv[i] * gg[j][i];
+          xh[j][i] = (xv[u][j][i] - mu[u]) * rs[u];
+          dg[j][i] = dv[u][j][i] * gg[j][i];
           s1 += dg[j][i];
           s2 += dg[j][i] * xh[j][i];
-          pg[j][i] += dv[i] * xh[j][i];
-          pb[j][i] += dv[i];
+          pg[j][i] += dv[u][j][i] * xh[j][i];
+          pb[j][i] += dv[u][j][i];
         }
       } else {
 #pragma unroll
@@ -446,10 +474,9 @@ __global__ __launch_bounds__(256) void ln_bwd_vec_kernel(int rows, int d, const 
       const int c = (lane + 64 * j) * 8;
       if (c >= d) continue;
       float* o = dx + (long)r * lddx + c;
-      float v[8], prev[8];
-      if (accumulate) ld8(o, prev);
+      float v[8];
 #pragma unroll
-      for (int i = 0; i < 8; ++i) v[i] = rs * (dg[j][i] - s1 - xh[j][i] * s2) + (accumulate ? prev[i] : 0.f);
+      for (int i = 0; i < 8; ++i) v[i] = rs[u] * (dg[j][i] - s1 - xh[j][i] * s2) + (accumulate ? pv[u][j][i] : 0.f);
       st8(o, v);
       if constexpr (DROP) {
         float lo[4], hi[4];
@@ -461,7 +488,13 @@ __global__ __launch_bounds__(256) void ln_bwd_vec_kernel(int rows, int d, const 
         bf16* yo = dr.y + (long)r * dr.ldy + c;
         vst4(yo, lo);
         vst4(yo + 4, hi);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {  // sums of the stored (rounded) values
+          py[DROP ? j : 0][i] += (float)(bf16)lo[i];
+          py[DROP ? j : 0][i + 4] += (float)(bf16)hi[i];
+        }
       }
+    }
     }
   }
 #pragma unroll
@@ -472,6 +505,7 @@ __global__ __launch_bounds__(256) void ln_bwd_vec_kernel(int rows, int d, const 
       if (c + i < 512 * NJ) {
         red[w][0][c + i] = pg[j][i];
         red[w][1][c + i] = pb[j][i];
+        if constexpr (DROP) red[w][NS - 1][c + i] = py[DROP ? j : 0][i];
       }
     }
   }
@@ -479,6 +513,8 @@ __global__ __launch_bounds__(256) void ln_bwd_vec_kernel(int rows, int d, const 
   for (int c = threadIdx.x; c < d; c += blockDim.x) {
     part[(long)blockIdx.x * 2 * d + c] = (red[0][0][c] + red[1][0][c]) + (red[2][0][c] + red[3][0][c]);
     part[(long)blockIdx.x * 2 * d + d + c] = (red[0][1][c] + red[1][1][c]) + (red[2][1][c] + red[3][1][c]);
+    if (DROP && dr.ypart)
+      dr.ypart[(long)blockIdx.x * d + c] = (red[0][NS - 1][c] + red[1][NS - 1][c]) + (red[2][NS - 1][c] + red[3][NS - 1][c]);
   }
 }
 
@@ -831,7 +867,7 @@ static int ln_bwd_impl(int rows, int d, const void* dy, int dy_dtype, long lddy,
   if (nparts_out) *nparts_out = 0;
   if (rows == 0) return 0;
   // the dropout output in-kernel: vectorized path, bf16 dy and y, 16-B aligned y rows
-  const bool kdrop = drop && dy_dtype == EA_BF16 && drop->ldy % 8 == 0 && ((uintptr_t)drop->y % 16) == 0;
+  const bool kdrop = drop && drop->ldy % 8 == 0 && ((uintptr_t)drop->y % 16) == 0;
   const bool vec = d % 4 == 0 && lddy % 4 == 0 && ldx % 4 == 0 && ((uintptr_t)x % 16) == 0 &&
                    ((uintptr_t)dy % (dy_dtype == EA_BF16 ? 8 : 16)) == 0;
   if (!vec) {  // generic fused path (row kernel + per-block partials)
@@ -853,13 +889,21 @@ static int ln_bwd_impl(int rows, int d, const void* dy, int dy_dtype, long lddy,
                     ((uintptr_t)x % 16) == 0 && ((uintptr_t)dy % 16) == 0 && ((uintptr_t)dx % 16) == 0 &&
                     ((uintptr_t)gamma % 16) == 0;
   if (vec8) {  // one pass: dx + per-block dgamma/dbeta partials, then the ordered reducer
-    const int rpb = max(16, ea_cdiv(rows, (int)max(1L, ws_elems / (2L * d))));
+    // with the dropout output's column sums: [nb][d] y partials after the [nb][2d] LN partials
+    const bool ycs = kdrop && drop->want_ycol;
+    const long per = ycs ? 3L * d : 2L * d;
+    const int rpb = max(16, ea_cdiv(rows, (int)max(1L, ws_elems / per)));
     const int nb = ea_cdiv(rows, rpb);
-    EA_CHECK_ARG(ws_elems >= (long)nb * 2 * d);
+    EA_CHECK_ARG(ws_elems >= (long)nb * per);
+    LnDrop dd = kdrop ? *drop : LnDrop{};
+    dd.ypart = ycs ? workspace + (long)nb * 2 * d : nullptr;
 #define EA_LNB(NJ)                                                                                        \
-  if (kdrop)                                                                                              \
+  if (kdrop && dy_dtype == EA_BF16)                                                                       \
     hipLaunchKernelGGL((ln_bwd_vec_kernel<NJ, bf16, true>), dim3(nb), dim3(256), 0, st, rows, d, (const bf16*)dy, lddy, \
-                       x, ldx, gamma, mean, rstd, dx, lddx, accumulate, rpb, workspace, *drop);            \
+                       x, ldx, gamma, mean, rstd, dx, lddx, accumulate, rpb, workspace, dd);               \
+  else if (kdrop)                                                                                         \
+    hipLaunchKernelGGL((ln_bwd_vec_kernel<NJ, float, true>), dim3(nb), dim3(256), 0, st, rows, d, (const float*)dy, lddy, \
+                       x, ldx, gamma, mean, rstd, dx, lddx, accumulate, rpb, workspace, dd);               \
   else if (dy_dtype == EA_BF16)                                                                           \
     hipLaunchKernelGGL((ln_bwd_vec_kernel<NJ, bf16>), dim3(nb), dim3(256), 0, st, rows, d, (const bf16*)dy, lddy, x, ldx, \
                        gamma, mean, rstd, dx, lddx, accumulate, rpb, workspace);                           \
@@ -873,6 +917,11 @@ static int ln_bwd_impl(int rows, int d, const void* dy, int dy_dtype, long lddy,
     hipLaunchKernelGGL(reduce_partials_kernel, dim3(ea_cdiv(2 * d, RP_CW)), dim3(256), 0, st, nb, 2 * d,
                        workspace, (long)2 * d, dgamma, accumulate_params);
     EA_LAUNCH_CHECK();
+    if (ycs) {
+      hipLaunchKernelGGL(reduce_partials_kernel, dim3(ea_cdiv(d, RP_CW)), dim3(256), 0, st, nb, d, dd.ypart, (long)d,
+                         drop->ycol, 1);
+      EA_LAUNCH_CHECK();
+    }
     return 0;
   }
   dim3 g1(ea_cdiv(rows, 4)), blk(256);
@@ -898,44 +947,59 @@ static int ln_bwd_impl(int rows, int d, const void* dy, int dy_dtype, long lddy,
 }
 
 // ln_bwd_impl + the dropout output: in the LN kernel when it can (kdrop above, vectorized
-// rows), otherwise as an ea_scale_dropout pass over the finished dx.
+// rows), otherwise as an ea_scale_dropout pass over the finished dx.  ycol (optional): its
+// column sums added into ycol, from the LN kernel's own partials when in-kernel (direct mode:
+// reduced here; partials mode: left after the LN partials, *ycol_parts = 1, for the caller),
+// else by ea_colsum (*ycol_parts = 0).
 static int ln_bwd_drop_impl(int rows, int d, const void* dy, int dy_dtype, long lddy, const float* x, long ldx,
                             const float* gamma, const float* mean, const float* rstd, float* dx, long lddx,
                             int accumulate, float* dgamma, int accumulate_params, float* workspace, long ws_elems,
                             int* nparts_out, void* y, int y_dtype, long ldy, float yscale, float p,
-                            unsigned long long seed, hipStream_t st) {
-  const LnDrop dr{(bf16*)y, ldy, yscale, p, (uint64_t)seed, ea_g_rng_salt};
+                            unsigned long long seed, float* ycol, int* ycol_parts, hipStream_t st) {
+  if (ycol_parts) *ycol_parts = 0;
+  const LnDrop dr{(bf16*)y, ldy, yscale, p, (uint64_t)seed, ea_g_rng_salt, nullptr, ycol != nullptr, ycol};
   const bool vec8 = d % 8 == 0 && d <= 1024 && lddy % 8 == 0 && ldx % 4 == 0 && lddx % 4 == 0 &&
                     ((uintptr_t)x % 16) == 0 && ((uintptr_t)dy % 16) == 0 && ((uintptr_t)dx % 16) == 0 &&
                     ((uintptr_t)gamma % 16) == 0;
-  const bool in_kernel = vec8 && y_dtype == EA_BF16 && dy_dtype == EA_BF16 && ldy % 8 == 0 && ((uintptr_t)y % 16) == 0;
+  const bool in_kernel = vec8 && y_dtype == EA_BF16 && ldy % 8 == 0 && ((uintptr_t)y % 16) == 0;
   int rc = ln_bwd_impl(rows, d, dy, dy_dtype, lddy, x, ldx, gamma, mean, rstd, dx, lddx, accumulate, dgamma,
                        accumulate_params, workspace, ws_elems, nparts_out, st, in_kernel ? &dr : nullptr);
-  if (rc || in_kernel || rows == 0) return rc;
-  return ea_scale_dropout(rows, d, dx, EA_F32, lddx, y, y_dtype, ldy, yscale, p, seed, st);
+  if (rc || rows == 0) return rc;
+  if (in_kernel) {
+    if (ycol && ycol_parts) *ycol_parts = 1;
+    return 0;
+  }
+  rc = ea_scale_dropout(rows, d, dx, EA_F32, lddx, y, y_dtype, ldy, yscale, p, seed, st);
+  if (rc || !ycol) return rc;
+  // column sums through ea_colsum on the workspace left after the LN partials
+  const long used = nparts_out ? (long)*nparts_out * 2 * d : 0;
+  return ea_colsum(rows, d, y, y_dtype, ldy, ycol, 1, workspace + used, ws_elems - used, st);
 }
 
 extern "C" int ea_layernorm_bwd_drop(int rows, int d, const void* dy, int dy_dtype, long lddy, const float* x,
                                      long ldx, const float* gamma, const float* mean, const float* rstd, float* dx,
                                      long lddx, int accumulate, float* dgamma, float* dbeta, int accumulate_params,
                                      float* workspace, long ws_elems, void* y, int y_dtype, long ldy, float yscale,
-                                     float p, unsigned long long seed, void* stream) {
+                                     float p, unsigned long long seed, float* ycol, void* stream) {
   EA_ENTRY();
   EA_CHECK_ARG(dgamma != nullptr && dbeta == dgamma + d && y != nullptr && (y_dtype == EA_BF16 || y_dtype == EA_F32));
   return ln_bwd_drop_impl(rows, d, dy, dy_dtype, lddy, x, ldx, gamma, mean, rstd, dx, lddx, accumulate, dgamma,
-                          accumulate_params, workspace, ws_elems, nullptr, y, y_dtype, ldy, yscale, p, seed,
-                          (hipStream_t)stream);
+                          accumulate_params, workspace, ws_elems, nullptr, y, y_dtype, ldy, yscale, p, seed, ycol,
+                          nullptr, (hipStream_t)stream);
 }
 
 extern "C" int ea_layernorm_bwd_partials_drop(int rows, int d, const void* dy, int dy_dtype, long lddy,
                                               const float* x, long ldx, const float* gamma, const float* mean,
                                               const float* rstd, float* dx, long lddx, int accumulate, float* part,
                                               long part_elems, int* nparts, void* y, int y_dtype, long ldy,
-                                              float yscale, float p, unsigned long long seed, void* stream) {
+                                              float yscale, float p, unsigned long long seed, float* ycol,
+                                              int* ycol_parts, void* stream) {
   EA_ENTRY();
   EA_CHECK_ARG(part != nullptr && nparts != nullptr && y != nullptr && (y_dtype == EA_BF16 || y_dtype == EA_F32));
+  EA_CHECK_ARG(ycol == nullptr || ycol_parts != nullptr);
   return ln_bwd_drop_impl(rows, d, dy, dy_dtype, lddy, x, ldx, gamma, mean, rstd, dx, lddx, accumulate, nullptr, 0,
-                          part, part_elems, nparts, y, y_dtype, ldy, yscale, p, seed, (hipStream_t)stream);
+                          part, part_elems, nparts, y, y_dtype, ldy, yscale, p, seed, ycol, ycol_parts,
+                          (hipStream_t)stream);
 }
 
 extern "C" int ea_layernorm_bwd(int rows, int d, const void* dy, int dy_dtype, long lddy, const float* x,

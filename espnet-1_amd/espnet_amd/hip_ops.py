@@ -509,26 +509,33 @@ def layernorm_fwd(x, gamma, beta, y, mean, rstd, eps=1e-12):
 
 
 def layernorm_bwd(dy, x, gamma, mean, rstd, dx, dgamma, dbeta, accumulate=True, drop=None):
-    """drop=(y, scale, p, seed): also y = dropout(scale * dx) once dx is final (the next residual
-    site's dropout backward, ea_layernorm_bwd_drop), instead of an ea_scale_dropout pass."""
+    """drop=(y, scale, p, seed[, ycol]): also y = dropout(scale * dx) once dx is final (the next
+    residual site's dropout backward, ea_layernorm_bwd_drop), instead of an ea_scale_dropout
+    pass; ycol (+)= column sums of y (that site's bias gradient) from the same kernel."""
     rows, d, ldx = _rows(x)
     _, _, lddy = _rows(dy)
     _, _, lddx = _rows(dx)
     if drop is not None:
-        y, ysc, yp, yseed = drop
+        y, ysc, yp, yseed = drop[:4]
+        ycol = drop[4] if len(drop) > 4 else None
         _, _, ldy = _rows(y)
-        dargs = (y.data_ptr(), dt(y), ldy, float(ysc), float(yp), yseed & 0xFFFFFFFFFFFFFFFF)
+        dargs = (y.data_ptr(), dt(y), ldy, float(ysc), float(yp), yseed & 0xFFFFFFFFFFFFFFFF,
+                 0 if ycol is None else ycol.data_ptr())
     if REDUCE_Q.active and rows > 0 and dbeta.data_ptr() == dgamma.data_ptr() + 4 * d:
         # dx now; the (dgamma | dbeta) row-block partials go to a buffer of their own and are
         # summed with the pass's other parameter-gradient reductions (REDUCE_Q.flush)
         nparts_max = max((rows + 15) // 16, 128)
-        part = torch.empty(nparts_max * 2 * d, dtype=torch.float32, device=x.device)
+        part = torch.empty(nparts_max * (3 if drop is not None else 2) * d, dtype=torch.float32, device=x.device)
         np_ = ctypes.c_int(0)
         if drop is not None:
+            yparts = ctypes.c_int(0)
             lib.ea_layernorm_bwd_partials_drop(rows, d, dy.data_ptr(), dt(dy), lddy, x.data_ptr(), ldx,
                                                gamma.data_ptr(), mean.data_ptr(), rstd.data_ptr(), dx.data_ptr(),
                                                lddx, int(accumulate), part.data_ptr(), part.numel(),
-                                               ctypes.addressof(np_), *dargs, stream())
+                                               ctypes.addressof(np_), *dargs, ctypes.addressof(yparts), stream())
+            if yparts.value:
+                npv = np_.value
+                REDUCE_Q.add_reduce(part[npv * 2 * d:], npv, d, d, ycol, accumulate=True)
         else:
             lib.ea_layernorm_bwd_partials(rows, d, dy.data_ptr(), dt(dy), lddy, x.data_ptr(), ldx, gamma.data_ptr(),
                                           mean.data_ptr(), rstd.data_ptr(), dx.data_ptr(), lddx, int(accumulate),

@@ -135,16 +135,15 @@ def dv_buf(N, d, cd, dev):
     return empty(N, d, dtype=cd, device=dev) if FUSE_LN_DROP and cd == torch.bfloat16 else None
 
 
-def drop_arg(dv, scale, p, seed):
-    return None if dv is None else (dv, scale, p, seed)
+def drop_arg(dv, scale, p, seed, bias_g):
+    """The LayerNorm backward's drop= argument: write dv and add its column sums to bias_g."""
+    return None if dv is None else (dv, scale, p, seed, bias_g)
 
 
 def site_dv(dx, dv, bias_g, scale, p, seed, cd):
-    """dv = dropout(scale * dx) (+ bias column sum) of a residual site; dv already written by
-    the preceding LayerNorm backward when given."""
+    """dv = dropout(scale * dx) and bias_g += its column sums at a residual site; both already
+    done by the preceding LayerNorm backward when dv is given."""
     if dv is not None:
-        with ops.wgrad(dv):
-            ops.colsum(dv, bias_g)
         return dv
     N, d = dx.shape
     dv = empty(N, d, dtype=cd, device=dx.device)

@@ -268,11 +268,11 @@ class ConformerBlockFn(torch.autograd.Function):
         dx = empty(N, d, device=dev)
         dv_ff2 = dv_buf(N, d, cd, dev)
         ln_bwd(dout.reshape(N, d).contiguous(), x4, b, "norm_final", mu5, rs5, dx, accumulate=False,
-               drop=drop_arg(dv_ff2, L.ff_scale, p, sd(7)))
+               drop=drop_arg(dv_ff2, L.ff_scale, p, sd(7), b.g("feed_forward.w_2.bias")))
         # ---- FFN
         dv_conv = dv_buf(N, d, cd, dev)
         _ffn_bwd(L, b, dx, x3, s_ff2, "feed_forward", "norm_ff", p, sd(6), sd(7), dv_in=dv_ff2,
-                 next_drop=drop_arg(dv_conv, 1.0, p, sd(5)))
+                 next_drop=drop_arg(dv_conv, 1.0, p, sd(5), b.g("conv_module.pointwise_conv2.bias")))
         # ---- conv module
         C = "conv_module."
         K = L.conv_module.kernel_size
@@ -298,7 +298,8 @@ class ConformerBlockFn(torch.autograd.Function):
         dxn3 = empty(N, d, dtype=cd, device=dev)
         ops.linear_dx(dg2, b.w(C + "pointwise_conv1.weight", shape=(2 * d, d)), dxn3)
         dv_att = dv_buf(N, d, cd, dev)
-        ln_bwd(dxn3, x2, b, "norm_conv", mu3, rs3, dx, accumulate=True, drop=drop_arg(dv_att, 1.0, p, sd(4)))
+        ln_bwd(dxn3, x2, b, "norm_conv", mu3, rs3, dx, accumulate=True,
+               drop=drop_arg(dv_att, 1.0, p, sd(4), b.g("self_attn.linear_out.bias")))
         # ---- rel-pos MHSA
         A = "self_attn."
         xn2, mu2, rs2, qkv, pp, O, s_core = s_att
@@ -356,7 +357,8 @@ class ConformerBlockFn(torch.autograd.Function):
         dxn2 = empty(N, d, dtype=cd, device=dev)
         ops.linear_dx(dqkv, qkv_w, dxn2)
         dv_ff1 = dv_buf(N, d, cd, dev)
-        ln_bwd(dxn2, x1, b, "norm_mha", mu2, rs2, dx, accumulate=True, drop=drop_arg(dv_ff1, L.ff_scale, p, sd(2)))
+        ln_bwd(dxn2, x1, b, "norm_mha", mu2, rs2, dx, accumulate=True,
+               drop=drop_arg(dv_ff1, L.ff_scale, p, sd(2), b.g("feed_forward_macaron.w_2.bias")))
         # ---- macaron FFN
         _ffn_bwd(L, b, dx, x0, s_ff1, "feed_forward_macaron", "norm_ff_macaron", p, sd(1), sd(2), dv_in=dv_ff1)
         ops.grad_ready(b)

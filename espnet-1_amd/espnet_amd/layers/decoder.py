@@ -224,7 +224,9 @@ class DecoderFn(torch.autograd.Function):
         dx = empty(N, d, device=dev)
         # each norm backward also writes the dropout backward of the site below it (dv_buf)
         dv_ff = dv_buf(N, d, cd, dev) if nb > 0 else None
-        ln_bwd(dxf, xlast, b, "after_norm", muf, rsf, dx, accumulate=False, drop=drop_arg(dv_ff, 1.0, p, sd(nb - 1, 6)))
+        ln_bwd(dxf, xlast, b, "after_norm", muf, rsf, dx, accumulate=False,
+               drop=None if dv_ff is None else
+               drop_arg(dv_ff, 1.0, p, sd(nb - 1, 6), b.g(f"decoders.{nb - 1}.feed_forward.w_2.bias")))
         ldkv = 2 * d * nb
         dkv = empty(Nm, ldkv, dtype=cd, device=dev)
         for l in reversed(range(nb)):
@@ -245,7 +247,8 @@ class DecoderFn(torch.autograd.Function):
             dxn = empty(N, d, dtype=cd, device=dev)
             ops.linear_dx(dh, b.w(ff + "w_1.weight"), dxn)
             dv_src = dv_buf(N, d, cd, dev)
-            ln_bwd(dxn, x2, b, n + "norm3", mu3, rs3, dx, accumulate=True, drop=drop_arg(dv_src, 1.0, p, sd(l, 4)))
+            ln_bwd(dxn, x2, b, n + "norm3", mu3, rs3, dx, accumulate=True,
+                   drop=drop_arg(dv_src, 1.0, p, sd(l, 4), b.g(xa + "linear_out.bias")))
             # source attention
             xn2, mu2, rs2, q2, O2, st2 = s2
             dv = site_dv(dx, dv_src, b.g(xa + "linear_out.bias"), 1.0, p, sd(l, 4), cd)
@@ -264,7 +267,8 @@ class DecoderFn(torch.autograd.Function):
             dxn = empty(N, d, dtype=cd, device=dev)
             ops.linear_dx(dq, b.w(xa + "linear_q.weight"), dxn)
             dv_self = dv_buf(N, d, cd, dev)
-            ln_bwd(dxn, x1, b, n + "norm2", mu2, rs2, dx, accumulate=True, drop=drop_arg(dv_self, 1.0, p, sd(l, 2)))
+            ln_bwd(dxn, x1, b, n + "norm2", mu2, rs2, dx, accumulate=True,
+                   drop=drop_arg(dv_self, 1.0, p, sd(l, 2), b.g(sa + "linear_out.bias")))
             # self attention
             xn1, mu1, rs1, qkv, O1, st1 = s1
             dv = site_dv(dx, dv_self, b.g(sa + "linear_out.bias"), 1.0, p, sd(l, 2), cd)
@@ -285,7 +289,9 @@ class DecoderFn(torch.autograd.Function):
             dxn = empty(N, d, dtype=cd, device=dev)
             ops.linear_dx(dqkv, b.w(*wn, shape=(3 * d, d)), dxn)
             dv_ff = dv_buf(N, d, cd, dev) if l > 0 else None  # layer l-1's feed-forward site
-            ln_bwd(dxn, x0, b, n + "norm1", mu1, rs1, dx, accumulate=True, drop=drop_arg(dv_ff, 1.0, p, sd(l - 1, 6)))
+            ln_bwd(dxn, x0, b, n + "norm1", mu1, rs1, dx, accumulate=True,
+                   drop=None if dv_ff is None else
+                   drop_arg(dv_ff, 1.0, p, sd(l - 1, 6), b.g(f"decoders.{l - 1}.feed_forward.w_2.bias")))
         pe = dec.embed[1]
         lib.ea_embed_bwd(N, d, ys_in.data_ptr(), dx.data_ptr(), pe.xscale, p_pos, sd(0, 0),
                          b.g("embed.0.weight").data_ptr(), ops.stream())

@@ -203,18 +203,23 @@ int ea_layernorm_bwd_partials(int rows, int d, const void* dy, int dy_dtype, lon
 /* The two entries above plus the next residual site's dropout backward: y = dropout(yscale *
  * dx) after dx is final (ea_scale_dropout's mask law, index r*d + c), written by the LayerNorm
  * kernel itself when dy and y are bf16 (vectorized rows), else by an ea_scale_dropout pass.
- * Saves the f32 dx re-read of the Conformer block's backward (encoder_layer.py:115-171:
- * every norm_* backward is followed by a dropout backward). */
+ * ycol (optional): ycol += column sums of the stored y (that site's bias gradient) -- from the
+ * LayerNorm kernel's own per-block partials when in-kernel.  In partials mode those y partials
+ * ([*nparts][d], right after the [*nparts][2d] LayerNorm partials in part; part_elems must hold
+ * 3d per row block) are left to the caller when *ycol_parts = 1; *ycol_parts = 0 means ycol was
+ * already accumulated.  Saves the f32 dx and bf16 y re-reads of the Conformer block's backward
+ * (encoder_layer.py:115-171: every norm_* backward is followed by a dropout backward). */
 int ea_layernorm_bwd_drop(int rows, int d, const void* dy, int dy_dtype, long lddy, const float* x,
                           long ldx, const float* gamma, const float* mean, const float* rstd, float* dx,
                           long lddx, int accumulate, float* dgamma, float* dbeta, int accumulate_params,
                           float* workspace, long ws_elems, void* y, int y_dtype, long ldy, float yscale,
-                          float p, unsigned long long seed, void* stream);
+                          float p, unsigned long long seed, float* ycol, void* stream);
 int ea_layernorm_bwd_partials_drop(int rows, int d, const void* dy, int dy_dtype, long lddy,
                                    const float* x, long ldx, const float* gamma, const float* mean,
                                    const float* rstd, float* dx, long lddx, int accumulate, float* part,
                                    long part_elems, int* nparts, void* y, int y_dtype, long ldy,
-                                   float yscale, float p, unsigned long long seed, void* stream);
+                                   float yscale, float p, unsigned long long seed, float* ycol,
+                                   int* ycol_parts, void* stream);
 
 /* Grouped reductions of a backward pass's parameter gradients (bias grads of every Linear:
  * torch.nn.Linear bias.grad; LayerNorm weight/bias grads: torch.nn.LayerNorm in

@@ -109,10 +109,12 @@ def test_grouped_reductions_match_per_call():
 @pytest.mark.parametrize("rows,d,ydt", [(7968, 512, torch.bfloat16), (1312, 1024, torch.bfloat16),
                                         (100, 80, torch.bfloat16), (257, 256, torch.float32)])
 @pytest.mark.parametrize("partials", [False, True])
-def test_layernorm_bwd_drop_matches_two_pass(rows, d, ydt, partials):
-    """ea_layernorm_bwd_drop / _partials_drop (dx plus the next site's y = dropout(scale*dx)) vs
-    ea_layernorm_bwd / _partials then ea_scale_dropout, in-kernel (bf16 y, vector rows) and
-    pass fallback: y bit-identical to the dropout of the launch's own dx."""
+@pytest.mark.parametrize("dyt", [torch.bfloat16, torch.float32])
+def test_layernorm_bwd_drop_matches_two_pass(rows, d, ydt, partials, dyt):
+    """ea_layernorm_bwd_drop / _partials_drop (dx, the next site's y = dropout(scale*dx) and its
+    column sums) vs ea_layernorm_bwd / _partials then ea_scale_dropout, in-kernel (bf16 y,
+    vector rows) and pass fallback: y bit-identical to the dropout of the launch's own dx,
+    column sums = f64 sums of the stored y."""
     import ctypes
     from espnet_amd import hip_ops as ops
     from espnet_amd._lib import lib
@@ -121,35 +123,42 @@ def test_layernorm_bwd_drop_matches_two_pass(rows, d, ydt, partials):
     x = (torch.randn(rows, d, generator=g) * 2 + 1).cuda()
     gamma = (torch.rand(d, generator=g) + 0.5).cuda()
     beta = torch.randn(d, generator=g).cuda()
-    dy = torch.randn(rows, d, generator=g).to(torch.bfloat16).cuda()
+    dy = torch.randn(rows, d, generator=g).to(dyt).cuda()
     yln = torch.empty(rows, d, dtype=torch.bfloat16, device="cuda")
     mu = torch.empty(rows, device="cuda")
     rs = torch.empty(rows, device="cuda")
     ops.layernorm_fwd(x, gamma, beta, yln, mu, rs)
     dx0 = torch.randn(rows, d, generator=g).cuda()
+    ycol0 = torch.randn(d, generator=g).cuda()
     res = []
     for fused in (False, True):
         dx = dx0.clone()
         y = torch.empty(rows, d, dtype=ydt, device="cuda")
         par = torch.zeros(2 * d, device="cuda")
+        ycol = ycol0.clone()
         if partials:
-            part = torch.empty(max((rows + 15) // 16, 128) * 2 * d, device="cuda")
-            npart = ctypes.c_int(0)
+            part = torch.empty(max((rows + 15) // 16, 128) * 3 * d, device="cuda")
+            npart, yparts = ctypes.c_int(0), ctypes.c_int(0)
             args = (rows, d, dy.data_ptr(), ops.dt(dy), d, x.data_ptr(), d, gamma.data_ptr(), mu.data_ptr(),
                     rs.data_ptr(), dx.data_ptr(), d, 1, part.data_ptr(), part.numel(), ctypes.addressof(npart))
             if fused:
-                lib.ea_layernorm_bwd_partials_drop(*args, y.data_ptr(), ops.dt(y), d, 0.5, 0.1, 99, ops.stream())
+                lib.ea_layernorm_bwd_partials_drop(*args, y.data_ptr(), ops.dt(y), d, 0.5, 0.1, 99, ycol.data_ptr(),
+                                                   ctypes.addressof(yparts), ops.stream())
             else:
                 lib.ea_layernorm_bwd_partials(*args, ops.stream())
-            ops.reduce_rows(part, npart.value, 2 * d, 2 * d, par)
+            n = npart.value
+            ops.reduce_rows(part, n, 2 * d, 2 * d, par)
+            if yparts.value:
+                ops.reduce_rows(part[n * 2 * d:], n, d, d, ycol)
+            assert yparts.value == int(fused and ydt == torch.bfloat16 and d % 8 == 0)
         else:
             ops.layernorm_bwd(dy, x, gamma, mu, rs, dx, par[:d], par[d:], accumulate=True,
-                              drop=(y, 0.5, 0.1, 99) if fused else None)
+                              drop=(y, 0.5, 0.1, 99, ycol) if fused else None)
         if not fused:
             ops.scale_dropout(dx, y, scale=0.5, p=0.1, seed=99)
         torch.cuda.synchronize()
-        res.append((dx, y, par))
-    (dx1, y1, p1), (dx2, y2, p2) = res
+        res.append((dx, y, par, ycol))
+    (dx1, y1, p1, _), (dx2, y2, p2, c2) = res
     # y is exactly the site's dropout of the dx this launch wrote; dx and the parameter sums
     # match the plain kernel to f32 rounding (the compiler may contract the variants' FMAs
     # differently)
@@ -160,4 +169,6 @@ def test_layernorm_bwd_drop_matches_two_pass(rows, d, ydt, partials):
     torch.testing.assert_close(dx2, dx1, atol=1e-5, rtol=1e-5)
     torch.testing.assert_close(p2, p1, atol=1e-4, rtol=1e-5)
     torch.testing.assert_close(y2.float(), y1.float(), atol=1e-2, rtol=1e-2)
+    torch.testing.assert_close(c2.double().cpu(), ycol0.double().cpu() + y2.double().sum(0).cpu(), atol=2e-3,
+                               rtol=1e-5)
     assert 0.08 < (y2 == 0).float().mean().item() < 0.12
