@@ -123,7 +123,8 @@ def synthetic_batch(cfg, seed):
 
 
 PMC_FILE = os.path.join(ROOT, "profiles", "pmc_conv2_fwd.json")
-GEMM_SOURCES = [os.path.join(ROOT, "espnet-1_amd", "csrc", f) for f in ("gemm.hip", "common.h")]
+GEMM_SOURCES = [os.path.join(ROOT, "espnet-1_amd", "csrc", f)
+                for f in ("gemm.hip", "gemm_kern.h", "gemm_pipe_conv.hip", "common.h")]
 
 
 def gemm_src_sha():
