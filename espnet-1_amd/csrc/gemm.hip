@@ -45,13 +45,14 @@ unsigned long long* g_diag = nullptr;   // ea_gemm_set_diag
 int g_gemm_bm64 = 1;
 int g_gemm_pipe = 0;  // ea_gemm_set_pipe bits: 1 = 256x256 tiles on gemm_pipe, 2 = 128x128 tiles too
 
-int launch_lds(GemmP& p, int a_k, int b_k, int nz, hipStream_t st) {
+int launch_lds(GemmP& p, int a_k, int b_k, int nz, hipStream_t st, bool pipe128 = false) {
   dim3 grid(p.tiles_m * p.tiles_n, 1, nz * p.splitk);
   if (p.g.mode != 0) {  // implicit-GEMM conv2 modes: fixed layouts, 128x128 or 256x256 tiles
     if (p.bm == 256 && g_gemm_pipe) return launch_pipe_conv(p, grid, st);
     return launch_lds_conv(p, grid, st);
   }
-  if ((p.bm == 256 && p.bn == 256 && (g_gemm_pipe & 1)) || (p.bm == 128 && p.bn == 128 && (g_gemm_pipe & 2)))
+  if ((p.bm == 256 && p.bn == 256 && (g_gemm_pipe & 1)) ||
+      (p.bm == 128 && p.bn == 128 && ((g_gemm_pipe & 2) || pipe128)))
     return launch_pipe(p, a_k, b_k, grid, st);
   return launch_lds_dense(p, a_k, b_k, grid, st);
 }
@@ -83,8 +84,8 @@ void choose_tile(GemmP& p, int a_k, long nz) {
 }
 
 template <typename T>
-int launch(GemmP& p, int a_k, int b_k, int nz, hipStream_t st) {
-  if (sizeof(T) == 2 && p.lds) return launch_lds(p, a_k, b_k, nz, st);
+int launch(GemmP& p, int a_k, int b_k, int nz, hipStream_t st, bool pipe128 = false) {
+  if (sizeof(T) == 2 && p.lds) return launch_lds(p, a_k, b_k, nz, st, pipe128);
   if (p.bm != 128 || p.bn != 128) return EA_ERR_BAD_ARG;
   dim3 grid(p.tiles_m * p.tiles_n, 1, nz * p.splitk);
 #define EA_GEMM_CASE(AKV, BKV)                                                      \
@@ -210,6 +211,7 @@ static int gemm_impl(int dtype, int a_kmajor, int b_kmajor, int M, int N, int K,
   const bool lds_path = dtype == EA_BF16 && p.vec_a && p.vec_b && g_gemm_stages > 0 &&
                         a_ext < 4.0e9 && b_ext < 4.0e9;
   p.lds = lds_path;
+  bool pipe128 = false;
   if (geo && geo->mode != 0) {
     // gather modes: LDS-DMA path only, K a whole number of 64-deep tiles within taps
     if (!lds_path || K % 64 != 0 || geo->C % 64 != 0 || batch * nh != 1) return EA_ERR_BAD_ARG;
@@ -226,6 +228,17 @@ static int gemm_impl(int dtype, int a_kmajor, int b_kmajor, int M, int N, int K,
     if (p.bm != 256 || p.bn != 256) { p.bm = 128; p.bn = 128; }
   } else if (lds_path) {
     choose_tile(p, a_kmajor, (long)batch * nh);
+    // One-round 256x256 grids serialise each CU's main loop and its epilogue; 128x128
+    // tiles two per CU let one block's epilogue stores overlap the other's main loop.
+    // EA_EPI128 bits: 1 = switch such grids when the epilogue stores an activation pair
+    // (ACT / DACT), 2 = on the ping-pong kernel, 4 = whatever the epilogue.
+    static const int epi128 = [] { const char* e = std::getenv("EA_EPI128"); return e ? std::atoi(e) : 0; }();
+    if ((epi128 & 1) && !g_force_bm && p.bm == 256 && p.bn == 256 &&
+        ((epi128 & 4) || epi->kind == EA_EPI_ACT || epi->kind == EA_EPI_DACT) &&
+        (long)ea_cdiv(M, 256) * ea_cdiv(N, 256) * batch * nh <= 256) {
+      p.bm = 128; p.bn = 128;
+      pipe128 = (epi128 & 2) != 0;
+    }
   }
   if (p.bm == 64 && !a_kmajor) return EA_ERR_BAD_ARG;
   p.tiles_m = ea_cdiv(M, p.bm);
@@ -264,7 +277,7 @@ static int gemm_impl(int dtype, int a_kmajor, int b_kmajor, int M, int N, int K,
     std::fprintf(stderr, "[ea_gemm] M=%d N=%d K=%d ak=%d bk=%d nz=%d tile=%dx%d splitk=%d epi=%d geo=%d lds=%d\n", M,
                  N, K, a_kmajor, b_kmajor, nz, p.bm, p.bn, splitk, (int)epi->kind, geo ? geo->mode : 0, (int)p.lds);
   hipStream_t st = (hipStream_t)stream;
-  int rc = dtype == EA_BF16 ? launch<bf16>(p, a_kmajor, b_kmajor, nz, st)
+  int rc = dtype == EA_BF16 ? launch<bf16>(p, a_kmajor, b_kmajor, nz, st, pipe128)
                             : launch<float>(p, a_kmajor, b_kmajor, nz, st);
   if (rc) return rc;
   if (splitk > 1) {

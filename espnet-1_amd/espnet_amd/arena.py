@@ -28,17 +28,27 @@ class ParamArena:
         named = dict(model.named_parameters())
         seen = set()
         chunks: List[List[str]] = []  # each chunk is packed back to back, chunk starts aligned
-        # explicit adjacency groups first (in the given order), then the rest one by one in
-        # registration order
+        # registration order, except that an adjacency group is laid out in full where its
+        # first-registered member would go: every module's parameters stay in one region of
+        # the arena, so a data-parallel bucket (a byte range) is final as soon as the modules
+        # in it are, and the front of the arena is the first-registered module (the
+        # subsampling front end, whose backward is the last of the step)
+        group_of: Dict[str, List[str]] = {}
         for group in order:
-            g = [n for n in group if n in named and n not in seen]
-            seen.update(g)
-            if g:
-                chunks.append(g)
+            g = [n for n in group if n in named]
+            if not g:
+                continue
+            first = min(g, key=list(named).index)
+            group_of.setdefault(first, [])
+            group_of[first] += [n for n in g if n not in group_of[first]]
         for n in named:
-            if n not in seen:
-                chunks.append([n])
-                seen.add(n)
+            if n in seen:
+                continue
+            g = [m for m in group_of.get(n, [n]) if m not in seen]
+            if n not in g:
+                g.insert(0, n)
+            seen.update(g)
+            chunks.append(g)
         self.offsets: Dict[str, int] = {}
         layout: List[str] = []
         off = 0

@@ -34,15 +34,7 @@ class ArenaDataParallel:
         self.arena = arena
         n = arena.numel
         per = max(int(bucket_mb * 1024 * 1024 / 4) // 64 * 64, 64)
-        # buckets back-to-front: the tail of the arena (decoder / CTC head, whose grads
-        # are final first in backward) is reduced first
-        self.buckets: List[slice] = []
-        end = n
-        while end > 0:
-            start = max(0, end - per)
-            self.buckets.append(slice(start, end))
-            end = start
-        # module prefix -> buckets it overlaps (prefixes = the block-level autograd nodes)
+        # module prefix -> arena span (prefixes = the block-level autograd nodes)
         self.prefixes = sorted({getattr(m, "_b").prefix for m in model.modules()
                                 if getattr(m, "_b", None) is not None}, key=len, reverse=True)
         span = {}
@@ -53,6 +45,25 @@ class ArenaDataParallel:
             o = arena.offsets[name]
             lo, hi = span.get(pre, (o, o))
             span[pre] = (min(lo, o), max(hi, o + arena._params[name].numel()))
+        # buckets back-to-front: the tail of the arena (decoder / CTC head, whose grads
+        # are final first in backward) is reduced first.  The front module (the subsampling
+        # front end: its backward is the last of the step) gets a bucket of its own, so the
+        # blocks above it are reduced while its backward runs and only its own bytes are
+        # exposed after the backward ends.
+        front_end = 0
+        if span:
+            front = min(span, key=lambda p: span[p][0])
+            front_end = min(n, (span[front][1] + 63) // 64 * 64)
+            if front_end >= n:
+                front_end = 0
+        self.buckets: List[slice] = []
+        end = n
+        while end > 0:
+            start = max(0, end - per)
+            if start < front_end < end:
+                start = front_end
+            self.buckets.append(slice(start, end))
+            end = start
         self._bucket_mods = []
         for b in self.buckets:
             self._bucket_mods.append({p for p, (lo, hi) in span.items() if lo < b.stop and hi > b.start})
