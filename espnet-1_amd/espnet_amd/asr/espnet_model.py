@@ -269,6 +269,7 @@ class ESPnetASRModel(AbsESPnetModel):
         elif self.ctc_weight == 1.0:
             loss = loss_ctc
         else:
+            ops.take_aux_fork()  # drop a fork point left by an earlier backward, if any
             loss = CombineFn.apply(loss_ctc, loss_att, float(self.ctc_weight))
         stats["loss"] = loss.detach()
         # force_gatherable (device_funcs.py:36-71): 0-d -> (1,), int weight -> int64 tensor

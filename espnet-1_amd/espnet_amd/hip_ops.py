@@ -109,11 +109,13 @@ _AUX = {}
 
 class aux:
     """Context: the enclosed launches run on the auxiliary stream, ordered after everything the
-    main stream has issued so far; `join_aux()` makes the main stream wait for them.  The
-    tensors it touches are record_stream()-ed for the caching allocator."""
+    main stream has issued so far (or, with `after=event`, only after that event); `join_aux()`
+    makes the main stream wait for them.  The tensors it touches are record_stream()-ed for
+    the caching allocator."""
 
-    def __init__(self, *tensors):
+    def __init__(self, *tensors, after=None):
         self.tensors = tensors
+        self.after = after
 
     def __enter__(self):
         if not OVERLAP_AUX or not torch.cuda.is_available():
@@ -124,7 +126,10 @@ class aux:
         st = _AUX.get(dev)
         if st is None:
             st = _AUX[dev] = torch.cuda.Stream(device=dev)
-        st.wait_stream(main)
+        if self.after is not None:
+            st.wait_event(self.after)
+        else:
+            st.wait_stream(main)
         for t in self.tensors:
             if t is not None:
                 t.record_stream(st)
@@ -136,6 +141,30 @@ class aux:
         if self.ctx is not None:
             self.ctx.__exit__(*exc)
         return False
+
+
+# the CTC head's backward (gradient kernel + ctc_lo input gradient) overlaps the attention
+# decoder's backward on the auxiliary stream (EA_OVERLAP_CTC_BWD=0: serial)
+OVERLAP_CTC_BWD = os.environ.get("EA_OVERLAP_CTC_BWD", "1") != "0"
+_AUX_FORK = {}
+
+
+def mark_aux_fork():
+    """Record where the loss gradients exist on the main stream (the hybrid combination's
+    backward): a backward issued later on the host can fork from this point onto the
+    auxiliary stream instead of queueing behind everything issued in between."""
+    if not (OVERLAP_AUX and OVERLAP_CTC_BWD) or not torch.cuda.is_available():
+        return
+    ev = torch.cuda.Event()
+    ev.record(torch.cuda.current_stream())
+    _AUX_FORK[torch.cuda.current_device()] = ev
+
+
+def take_aux_fork():
+    """The event mark_aux_fork() recorded on this device (consumed), or None."""
+    if not _AUX_FORK or not torch.cuda.is_available():
+        return None
+    return _AUX_FORK.pop(torch.cuda.current_device(), None)
 
 
 def join_aux():

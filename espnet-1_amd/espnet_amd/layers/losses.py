@@ -62,18 +62,31 @@ class CTCFn(torch.autograd.Function):
         ctx.save = None
         N = B * T
         dev = gl.device
-        dl = empty(N, V, dtype=cd, device=dev)
-        lib.ea_ctc_loss_bwd(B, T, V, logits.data_ptr(), V, hlens.data_ptr(), ys.data_ptr(), ys.stride(0),
-                            ylens.data_ptr(), Lmax, lse.data_ptr(), alpha.data_ptr(), beta.data_ptr(),
-                            nll.data_ptr(), _g(gl).data_ptr(), 1.0 / B, dl.data_ptr(), ops.dt(dl), V,
-                            ops.stream())
-        with ops.wgrad(dl, h):
-            ops.colsum(dl, b.g("ctc_lo.bias"))
-            ops.linear_dw(dl, h, b.g("ctc_lo.weight"), accumulate=True)
-        dh = empty(N, d, device=dev)
-        ops.linear_dx(dl, b.w("ctc_lo.weight"), dh)
-        if ctc.dropout_rate > 0:
-            ops.scale_dropout(dh, dh, p=ctc.dropout_rate, seed=ctc._seed)
+        gl = _g(gl)
+        # hybrid loss: the autograd engine issues this node after the whole attention decoder
+        # backward; forked from the point where the loss gradients exist (CombineFn.backward)
+        # onto the auxiliary stream, its kernels fill the CUs the latency-bound decoder
+        # backward leaves idle, and the main stream joins before it consumes dh.  dl / dh come
+        # from the auxiliary stream's pool: a main-stream block could still be in use by the
+        # decoder kernels queued after the fork point.
+        fork = ops.take_aux_fork() if ctc._overlap else None
+        with (ops.aux(gl, logits, hlens, ys, ylens, lse, alpha, beta, nll, h, after=fork)
+              if fork is not None else contextlib.nullcontext()):
+            dl = empty(N, V, dtype=cd, device=dev)
+            dh = empty(N, d, device=dev)
+            lib.ea_ctc_loss_bwd(B, T, V, logits.data_ptr(), V, hlens.data_ptr(), ys.data_ptr(), ys.stride(0),
+                                ylens.data_ptr(), Lmax, lse.data_ptr(), alpha.data_ptr(), beta.data_ptr(),
+                                nll.data_ptr(), gl.data_ptr(), 1.0 / B, dl.data_ptr(), ops.dt(dl), V,
+                                ops.stream())
+            with ops.wgrad(dl, h):
+                ops.colsum(dl, b.g("ctc_lo.bias"))
+                ops.linear_dw(dl, h, b.g("ctc_lo.weight"), accumulate=True)
+            ops.linear_dx(dl, b.w("ctc_lo.weight"), dh)
+            if ctc.dropout_rate > 0:
+                ops.scale_dropout(dh, dh, p=ctc.dropout_rate, seed=ctc._seed)
+        if fork is not None:
+            ops.join_aux()
+            dh.record_stream(torch.cuda.current_stream())  # consumed on the main stream
         ops.grad_ready(b)
         return dh.view(B, T, d), None, None, None, None, None
 
@@ -131,4 +144,5 @@ class CombineFn(torch.autograd.Function):
         gb = empty((), device=g.device)
         lib.ea_axpby_scalar(g.data_ptr(), ctx.w, 0, 0.0, ga.data_ptr(), ops.stream())
         lib.ea_axpby_scalar(g.data_ptr(), 1.0 - ctx.w, 0, 0.0, gb.data_ptr(), ops.stream())
+        ops.mark_aux_fork()  # the CTC head's backward forks from here (CTCFn.backward)
         return ga, gb, None

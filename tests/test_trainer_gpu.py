@@ -124,3 +124,40 @@ def test_nonfinite_grad_norm_skips_update_and_schedule():
     for k, v in before.items():
         assert torch.equal(m.state_dict()[k], v), k
     assert float(m.arena.grad.abs().max()) == 0.0  # zero_grad still ran
+
+
+def test_ctc_backward_fork_is_bit_exact_at_c3():
+    """The CTC head's backward forked onto the auxiliary stream beside the decoder backward
+    (hip_ops.OVERLAP_CTC_BWD) gives bit-identical losses and parameters to the serial order
+    over several captured C3 steps (bf16, dropout on): no buffer is shared across the
+    streams while both run."""
+    import bench
+    from espnet_amd import hip_ops as ops
+    from espnet_amd.optim.adam import ArenaAdam
+    from espnet_amd.schedulers.warmup_lr import WarmupLR
+    from espnet_amd.train.graph import CapturedTrainStep
+
+    cfg = bench.c3_config()
+    host = bench.synthetic_batch(cfg, 1)
+    runs = []
+    saved = ops.OVERLAP_CTC_BWD
+    try:
+        for fork in (True, False):
+            ops.OVERLAP_CTC_BWD = fork
+            m = bench.build(cfg)
+            m.prepare("cuda:0", amp=True, seed=1234)
+            m.train()
+            opt = ArenaAdam(m, lr=cfg["optim"]["lr"], weight_decay=cfg["optim"]["weight_decay"])
+            sched = WarmupLR(opt, warmup_steps=cfg["warmup_steps"])
+            batch = {k: v.to("cuda:0") for k, v in host.items()}
+            step = CapturedTrainStep(m, opt, sched, grad_clip=5.0, warmup=2)
+            losses = [float(step(batch, (cfg["T"], cfg["L"]))[0].item()) for _ in range(6)]
+            torch.cuda.synchronize()
+            runs.append((losses, m.arena.data.double().sum().item(), m.arena.data[:4096].clone().cpu()))
+            del m, opt, sched, step
+            torch.cuda.empty_cache()
+    finally:
+        ops.OVERLAP_CTC_BWD = saved
+    assert runs[0][0] == runs[1][0]
+    assert runs[0][1] == runs[1][1]
+    assert torch.equal(runs[0][2], runs[1][2])
