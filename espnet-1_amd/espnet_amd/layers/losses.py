@@ -5,6 +5,7 @@ grad_output), so nothing here synchronises with the host."""
 from __future__ import annotations
 
 import contextlib
+import os
 
 import torch
 
@@ -18,6 +19,10 @@ def _g(t):
     return t
 
 
+# EA_CTC_HEAD_AUX=0: only the lattice on the auxiliary stream (A/B switch)
+CTC_HEAD_AUX = os.environ.get("EA_CTC_HEAD_AUX", "1") != "0"
+
+
 class CTCFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, hs, hlens, ys, ylens, ctc, Lmax):
@@ -28,9 +33,7 @@ class CTCFn(torch.autograd.Function):
         dev = hs.device
         N = B * T
         h = empty(N, d, dtype=cd, device=dev)
-        ops.scale_dropout(hs.reshape(N, d), h, p=ctc.dropout_rate, seed=ctc._seed)
         logits = empty(N, V, device=dev)
-        ops.linear(h, b.w("ctc_lo.weight"), logits, epi=ops.make_epi(bias=b.f("ctc_lo.bias")))
         S = 2 * Lmax + 1
         lse = empty(N, device=dev)
         alpha = torch.empty(B * T * S, dtype=torch.float64, device=dev)
@@ -38,11 +41,19 @@ class CTCFn(torch.autograd.Function):
         nll = torch.empty(B, dtype=torch.float64, device=dev)
         loss_utt = empty(B, device=dev)
         loss = empty((), device=dev)
-        # the lattice runs 2 workgroups per utterance for T' serial steps: on the auxiliary
-        # stream it overlaps the attention decoder's forward (ESPnetASRModel.forward joins
-        # before the losses are combined)
-        with (ops.aux(logits, hlens, ys, ylens, lse, alpha, beta, nll, loss_utt, loss) if ctc._overlap
+        # the whole head (ctc_lo GEMM, log-sum-exp rows, and the lattice: 2 workgroups per
+        # utterance for T' serial steps) runs on the auxiliary stream beside the attention
+        # decoder's forward (ESPnetASRModel.forward joins before the losses are combined)
+        def head():
+            ops.scale_dropout(hs.reshape(N, d), h, p=ctc.dropout_rate, seed=ctc._seed)
+            ops.linear(h, b.w("ctc_lo.weight"), logits, epi=ops.make_epi(bias=b.f("ctc_lo.bias")))
+
+        if not CTC_HEAD_AUX:
+            head()
+        with (ops.aux(hs, h, logits, hlens, ys, ylens, lse, alpha, beta, nll, loss_utt, loss) if ctc._overlap
               else contextlib.nullcontext()):
+            if CTC_HEAD_AUX:
+                head()
             lib.ea_ctc_loss_fwd(B, T, V, logits.data_ptr(), V, hlens.data_ptr(), ys.data_ptr(), ys.stride(0),
                                 ylens.data_ptr(), Lmax, lse.data_ptr(), alpha.data_ptr(), beta.data_ptr(),
                                 nll.data_ptr(), loss_utt.data_ptr(), loss.data_ptr(), ops.stream())
