@@ -25,11 +25,16 @@ from .. import hip_ops
 
 
 class ArenaDataParallel:
-    def __init__(self, model, bucket_mb: float = 64.0, group=None, overlap: bool = True):
+    def __init__(self, model, bucket_mb: float = 64.0, group=None, overlap: bool = True,
+                 force_collectives: bool = False):
         self.model = model
         self.group = group
         self.world_size = dist.get_world_size(group) if dist.is_initialized() else 1
         self.rank = dist.get_rank(group) if dist.is_initialized() else 0
+        # `active`: the step issues its collectives.  Always for world_size > 1; with
+        # force_collectives also at world_size 1 (a world-1 RCCL group exercises the same
+        # code path on a one-GPU box: capture of the all-reduces, bucket hooks, packing)
+        self.active = self.world_size > 1 or (force_collectives and dist.is_initialized())
         arena = model.arena
         self.arena = arena
         n = arena.numel
@@ -70,14 +75,14 @@ class ArenaDataParallel:
         self.overlap = overlap
         self._pending = None
         self._works = []
-        if self.world_size > 1:
+        if self.active:
             dist.broadcast(arena.data, 0, group=group)
             arena.refresh_shadow()
             self.broadcast_buffers()
 
     # ------------------------------------------------------------------ per step
     def broadcast_buffers(self):
-        if self.world_size > 1:
+        if self.active:
             for b in (self.arena.buf_f32, self.arena.buf_i64):
                 if b.numel():
                     dist.broadcast(b, 0, group=self.group)
@@ -116,7 +121,7 @@ class ArenaDataParallel:
         """Arm the grad-ready hooks for one backward pass."""
         self._pending = [set(m) for m in self._bucket_mods]
         self._works = []
-        if self.overlap and self.world_size > 1:
+        if self.overlap and self.active:
             hip_ops.GRAD_READY = self.grad_ready
 
     def grad_ready(self, prefix: str):

@@ -28,13 +28,13 @@ class Trainer:
     @staticmethod
     def train_one_step(model, batch: Dict[str, torch.Tensor], optimizer: ArenaAdam, scheduler=None, *,
                        grad_clip: float = 5.0, accum_grad: int = 1, iiter: int = 1, dp=None, maxlens=None):
-        if dp is not None and dp.world_size > 1:
+        if dp is not None and dp.active:
             dp.broadcast_buffers()
         if maxlens is not None:
             loss, stats, weight = model(**batch, _maxlens=maxlens)
         else:
             loss, stats, weight = model(**batch)
-        if dp is not None and dp.world_size > 1:
+        if dp is not None and dp.active:
             # every rank packs the model's full (fixed) key set, None entries flagged, so
             # the one stats all-reduce has the same size on every rank
             present = {k for k, v in stats.items() if v is not None}
@@ -43,13 +43,13 @@ class Trainer:
         else:
             stats = {k: v for k, v in stats.items() if v is not None}  # trainer.py:604
         loss = loss / accum_grad if accum_grad > 1 else loss
-        if dp is not None and dp.world_size > 1:
+        if dp is not None and dp.active:
             dp.begin_backward()
         # the Linear weight gradients of the pass are queued and run as grouped GEMMs (at the
         # end of the pass, or per bucket from the DP hooks)
         with ops.deferred_wgrad():
             loss.backward()
-        if dp is not None and dp.world_size > 1:
+        if dp is not None and dp.active:
             dp.allreduce_grads()
         grad_norm = None
         if iiter % accum_grad == 0:
@@ -71,7 +71,7 @@ class Trainer:
         `device` holds the stop flag: "cuda" for RCCL, "cpu" for gloo."""
         was_training = model.training
         model.eval()
-        distributed = dp is not None and dp.world_size > 1
+        distributed = dp is not None and dp.active
         group = dp.group if distributed else None
         stop = torch.zeros((), dtype=torch.long, device=device)
         sums: Dict[str, float] = {}

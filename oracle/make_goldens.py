@@ -113,7 +113,7 @@ def np32(t):
     t = t.detach().cpu()
     if t.dtype in (torch.float64, torch.float16, torch.bfloat16):
         t = t.float()
-    return t.numpy()
+    return t.numpy().copy()  # a snapshot: buffers (BN running stats) are updated in place later
 
 
 # --------------------------------------------------------------------------------------
@@ -573,6 +573,119 @@ def capture_avg_nbest(name="avg_nbest"):
     print(f"{name}: {files} -> {path}")
 
 
+# --------------------------------------------------------------------------------------
+# BASELINE-sized goldens (weights regenerated from the seed, not stored)
+# --------------------------------------------------------------------------------------
+SIZED = {
+    # BASELINE.json configs[2] (C3): Conformer-L 12x512 + 6-layer decoder, V=5000, T=1000,
+    # L=40, at B=2 with one ragged utterance (multi-tile T'=249, 12-layer depth)
+    "c3_b2": dict(
+        encoder="conformer", input_size=80, vocab_size=5000,
+        encoder_conf=conformer_conf(512, 8, 2048, 12), decoder="transformer",
+        decoder_conf=decoder_conf(8, 2048, 6),
+        model_conf=dict(ctc_weight=0.3, lsm_weight=0.1, length_normalized_loss=False),
+        speech_lengths=[1000, 871], text_lengths=[40, 33], seed=0,
+    ),
+    # BASELINE.json configs[1] (C2): Conformer-S 6x256, CTC only, T=500, L=20, at B=2
+    "c2_b2": dict(
+        encoder="conformer", input_size=80, vocab_size=5000,
+        encoder_conf=conformer_conf(256, 4, 1024, 6), decoder="transformer",
+        decoder_conf=decoder_conf(4, 2048, 6),
+        model_conf=dict(ctc_weight=1.0, lsm_weight=0.0, length_normalized_loss=False),
+        speech_lengths=[500, 437], text_lengths=[20, 14], seed=0,
+    ),
+    # AMP check: d_k = 64, 2+2 blocks, T' = 99 (two 64-query tiles), ragged
+    "amp_hybrid": dict(
+        encoder="conformer", input_size=80, vocab_size=300,
+        encoder_conf=conformer_conf(256, 4, 1024, 2), decoder="transformer",
+        decoder_conf=decoder_conf(4, 1024, 2),
+        model_conf=dict(ctc_weight=0.3, lsm_weight=0.1, length_normalized_loss=False),
+        speech_lengths=[400, 360, 287], text_lengths=[20, 17, 9], seed=0,
+    ),
+}
+
+
+def _rel_l2(a, b):
+    a, b = a.double(), b.double()
+    den = float(b.norm())
+    return float((a - b).norm()) / den if den > 0 else float((a - b).norm())
+
+
+def capture_sized(name):
+    """A BASELINE-sized model in fp32 AND under torch.autocast("cpu", bfloat16).
+    Weights come from torch.manual_seed(seed) + perturb_norms(Generator(1000 + seed)) —
+    the build's modules initialise bit-identically under the same seed
+    (tests/test_model_build.py) — and only per-tensor sums are stored to check the
+    regeneration.  fp32: loss/stats/encoder output/CTC argmax, per-parameter gradient norm,
+    sum and 256-element head, BN running stats.  bf16: loss/stats and, per parameter, the
+    relative L2 distance of the autocast gradient from the fp32 one (the reference's own
+    bf16 rounding error, the yardstick for the build's AMP path)."""
+    cfg = SIZED[name]
+    seed = cfg["seed"]
+    torch.manual_seed(seed)
+    model = build_reference_model(cfg)
+    perturb_norms(model, torch.Generator().manual_seed(1000 + seed))
+    batch = make_batch(cfg, torch.Generator().manual_seed(1))
+    model.train()
+    sd0 = {k: v.clone() for k, v in model.state_dict().items()}
+    rec = {"cfg": np.array(json.dumps({k: v for k, v in cfg.items()}))}
+    for k, v in sd0.items():
+        rec["wsum." + k] = np.array(v.double().sum().item())
+    for k, v in batch.items():
+        rec["in." + k] = v.numpy()
+    enc_out = {}
+
+    def enc_hook(mod, inp, out):
+        enc_out["x"], enc_out["lens"] = out[0], out[1]
+
+    h = model.encoder.register_forward_hook(enc_hook)
+    loss, stats, weight = model(**{k: v.clone() for k, v in batch.items()})
+    loss.backward()
+    h.remove()
+    rec["out.loss"] = np32(loss)
+    rec["out.weight"] = weight.numpy()
+    for k, v in stats.items():
+        if v is not None:
+            rec["stat." + k] = np32(v)
+    rec["out.encoder_out"] = np32(enc_out["x"])
+    rec["out.encoder_out_lens"] = enc_out["lens"].numpy()
+    with torch.no_grad():
+        logits = model.ctc.ctc_lo(enc_out["x"])
+        rec["out.ctc_argmax"] = logits.argmax(-1).numpy()
+        top2 = logits.topk(2, dim=-1).values
+        rec["out.ctc_top2_gap"] = np32(top2[..., 0] - top2[..., 1])
+    g32 = {}
+    for k, p in model.named_parameters():
+        if p.grad is None:
+            continue
+        g = p.grad.detach().clone()
+        g32[k] = g
+        rec["gn." + k] = np.array(g.double().norm().item())
+        rec["gs." + k] = np.array(g.double().sum().item())
+        rec["gh." + k] = np32(g.reshape(-1)[:256])
+    for k, v in model.state_dict().items():
+        if "running" in k or "num_batches" in k:
+            rec["buf_after." + k] = np32(v)
+    # the same step under CPU autocast (bf16), from the same initial state
+    model.load_state_dict(sd0)
+    model.zero_grad()
+    with torch.autocast("cpu", dtype=torch.bfloat16):
+        aloss, astats, _ = model(**{k: v.clone() for k, v in batch.items()})
+    aloss.backward()
+    rec["amp.loss"] = np32(aloss)
+    for k, v in astats.items():
+        if v is not None:
+            rec["ampstat." + k] = np32(v)
+    for k, p in model.named_parameters():
+        if k in g32:
+            rec["ampdev." + k] = np.array(_rel_l2(p.grad.detach(), g32[k]))
+    path = os.path.join(OUT, f"{name}.npz")
+    np.savez_compressed(path, **rec)
+    devs = sorted(float(rec[k]) for k in rec if k.startswith("ampdev."))
+    print(f"{name}: loss={loss.item():.6f} amp={aloss.item():.6f} ampdev median {devs[len(devs) // 2]:.2e} "
+          f"max {devs[-1]:.2e} -> {path} ({os.path.getsize(path) / 1e6:.2f} MB)")
+
+
 # (beam, length_bonus weight, maxlenratio[, ctc_weight])
 BEAM_CASES = [(3, 0.0, 0.0), (4, 0.5, 0.0), (3, 0.0, 0.5), (3, 0.0, 0.0, 0.3), (4, 0.5, 0.0, 0.5),
               (3, 0.0, 0.5, 0.3)]
@@ -645,3 +758,6 @@ if __name__ == "__main__":
         capture_frontend()
     if "beam" in which:
         capture_beam()
+    for n in SIZED:
+        if n in which or "sized" in which:
+            capture_sized(n)

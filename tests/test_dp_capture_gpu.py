@@ -1,0 +1,179 @@
+"""Data-parallel training steps on the GPU box.
+
+1. RCCL: a world-1 `nccl` process group (RCCL is the nccl backend on ROCm) with
+   ArenaDataParallel(force_collectives=True), so the step issues exactly the collectives
+   of an N-GPU step (BN-buffer broadcasts, the packed stats/weight all-reduce, bucketed
+   gradient all-reduces launched from the backward's grad-ready hooks on the
+   weight-gradient stream).  The step is captured as a hipGraph WITH those collectives
+   and replayed; the replayed steps must be bit-identical to eager DP steps and to the
+   plain single-process step (a one-rank SUM is the identity), dropout on, bf16.
+   Reference: espnet2/train/trainer.py:229-244 (DDP wrap), :604-632.
+2. gloo, 2 ranks on cuda:0: the overlapped path (deferred bf16 weight-gradient GEMMs and
+   bias/LayerNorm reductions flushed per completed bucket on the side stream, all-reduce
+   started from that stream) against overlap=False, under Trainer.train_one_step with
+   amp=True: identical reduced gradients and stats, with a None stat on one rank.
+"""
+import os
+import tempfile
+
+import numpy as np
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+pytestmark = pytest.mark.gpu
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+def _paths():
+    import sys
+    for p in (HERE, os.path.dirname(HERE), os.path.join(os.path.dirname(HERE), "espnet-1_amd")):
+        if p not in sys.path:
+            sys.path.insert(0, p)
+
+
+def _setup(amp=True, dropout=0.1):
+    from goldens import load, section
+    from test_model_build import build
+    from espnet_amd.optim.adam import ArenaAdam
+    from espnet_amd.schedulers.warmup_lr import WarmupLR
+    meta, d = load("train2")
+    cfg, _ = load(meta["cfg_name"])
+    cfg = dict(cfg)
+    cfg["encoder_conf"] = dict(cfg["encoder_conf"], dropout_rate=dropout, positional_dropout_rate=dropout,
+                               attention_dropout_rate=dropout)
+    cfg["decoder_conf"] = dict(cfg["decoder_conf"], dropout_rate=dropout, positional_dropout_rate=dropout,
+                               self_attention_dropout_rate=dropout, src_attention_dropout_rate=dropout)
+    torch.manual_seed(0)
+    m = build(cfg)
+    m.load_state_dict({k: torch.from_numpy(v) for k, v in section(d, "w").items()})
+    m.prepare("cuda:0", amp=amp, seed=77)
+    m.train()
+    opt = ArenaAdam(m, lr=meta["lr"], weight_decay=meta["weight_decay"])
+    sched = WarmupLR(opt, warmup_steps=meta["warmup_steps"])
+    return d, m, opt, sched
+
+
+def _batches(d, n):
+    from goldens import section
+    base = {k: torch.from_numpy(v) for k, v in section(d, "in0").items()}
+    g = torch.Generator().manual_seed(5)
+    out = []
+    for _ in range(n):
+        b = dict(base)
+        b["speech"] = torch.randn(base["speech"].shape, generator=g)
+        b["text"] = torch.where(base["text"] >= 0, torch.randint(2, 48, base["text"].shape, generator=g),
+                                base["text"])
+        out.append(b)
+    return out
+
+
+def _rccl_worker(init, q):
+    _paths()
+    import torch.distributed as dist
+    from espnet_amd.train.distributed import ArenaDataParallel
+    from espnet_amd.train.graph import CapturedTrainStep
+    from espnet_amd.train.trainer import Trainer
+    torch.cuda.set_device(0)
+    dist.init_process_group("nccl", init_method=f"file://{init}", rank=0, world_size=1,
+                            device_id=torch.device("cuda", 0))
+    try:
+        d, _, _, _ = _setup()
+        batches = _batches(d, 5)
+        res = {}
+        # plain single-process eager steps (no DP)
+        _, m0, o0, s0 = _setup()
+        res["plain"] = [float(Trainer.train_one_step(m0, b, o0, s0, grad_clip=5.0)[0]) for b in batches]
+        res["plain_w"] = m0.arena.data.cpu().clone()
+        # eager DP steps with every collective issued over RCCL
+        _, m1, o1, s1 = _setup()
+        dp1 = ArenaDataParallel(m1, bucket_mb=0.25, force_collectives=True)
+        assert dp1.active and len(dp1.buckets) > 1
+        res["eager"] = [float(Trainer.train_one_step(m1, b, o1, s1, grad_clip=5.0, dp=dp1)[0]) for b in batches]
+        res["eager_w"] = m1.arena.data.cpu().clone()
+        # the same DP step captured (RCCL collectives inside the hipGraph) and replayed
+        _, m2, o2, s2 = _setup()
+        dp2 = ArenaDataParallel(m2, bucket_mb=0.25, force_collectives=True)
+        run = CapturedTrainStep(m2, o2, s2, grad_clip=5.0, dp=dp2, warmup=1)
+        res["graph"] = [float(run(b)[0]) for b in batches]
+        res["graph_w"] = m2.arena.data.cpu().clone()
+        res["n_graphs"] = len(run.graphs)
+        torch.cuda.synchronize()
+        q.put(res)
+    except Exception as e:  # surface the worker's failure in the test
+        import traceback
+        q.put({"error": traceback.format_exc()})
+        raise
+    finally:
+        dist.destroy_process_group()
+
+
+def test_rccl_world1_captured_dp_step_bit_exact():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    init = tempfile.mktemp(prefix="ea_rccl_")
+    p = ctx.Process(target=_rccl_worker, args=(init, q))
+    p.start()
+    res = q.get(timeout=300)
+    p.join(60)
+    assert "error" not in res, res.get("error")
+    assert res["n_graphs"] == 1
+    assert res["eager"] == res["graph"], (res["eager"], res["graph"])
+    assert torch.equal(res["eager_w"], res["graph_w"])
+    assert res["plain"] == res["eager"], (res["plain"], res["eager"])
+    assert torch.equal(res["plain_w"], res["eager_w"])
+    assert len(set(res["graph"])) == len(res["graph"])  # fresh dropout masks every replay
+
+
+def _gloo_worker(rank, world, init, q):
+    _paths()
+    import torch.distributed as dist
+    from goldens import section
+    from espnet_amd.train.distributed import ArenaDataParallel
+    from espnet_amd.train.trainer import Trainer
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", init_method=f"file://{init}", rank=rank, world_size=world)
+    out = {}
+    for overlap in (True, False):
+        d, m, opt, sched = _setup(amp=True, dropout=0.1)
+        dp = ArenaDataParallel(m, bucket_mb=0.25, overlap=overlap)
+        full = {k: torch.from_numpy(v) for k, v in section(d, "in0").items()}
+        batch = {k: v[rank::world] for k, v in full.items()}
+        # accum_grad=2, iiter=1: no optimizer step, the reduced gradients stay in the arena
+        loss, stats, weight, gn = Trainer.train_one_step(m, batch, opt, sched, grad_clip=5.0, dp=dp,
+                                                         accum_grad=2, iiter=1)
+        torch.cuda.synchronize()
+        out[overlap] = dict(loss=float(loss), stats={k: float(v) for k, v in stats.items()},
+                            weight=int(weight), grad=m.arena.grad.cpu().clone())
+    # a stat that is None on one rank only: averaged over the ranks that have it
+    stats = {"a": torch.tensor([2.0 + rank], device="cuda:0"), "b": None if rank == 1 else torch.tensor([5.0],
+                                                                                                      device="cuda:0")}
+    _, st, w = dp.weighted_average(torch.ones(1, device="cuda:0"), stats,
+                                   torch.tensor([1 + rank], device="cuda:0"))
+    out["none_case"] = ({k: float(v) for k, v in st.items()}, int(w))
+    if rank == 0:
+        q.put(out)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_gloo_two_ranks_overlap_amp_matches_serial():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    init = tempfile.mktemp(prefix="ea_ovl_")
+    ps = [ctx.Process(target=_gloo_worker, args=(r, 2, init, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    out = q.get(timeout=300)
+    for p in ps:
+        p.join(120)
+    a, b = out[True], out[False]
+    assert a["loss"] == b["loss"] and a["weight"] == b["weight"]
+    assert a["stats"] == b["stats"]
+    assert torch.equal(a["grad"], b["grad"]), float((a["grad"] - b["grad"]).abs().max())
+    assert float(a["grad"].abs().sum()) > 0
+    st, w = out["none_case"]
+    assert w == 3
+    np.testing.assert_allclose(st["a"], (2.0 * 1 + 3.0 * 2) / 3)
+    np.testing.assert_allclose(st["b"], 5.0)  # only rank 0 had it

@@ -145,3 +145,34 @@ def test_oracle_ddp_gloo_two_ranks(tmp_path):
     np.testing.assert_allclose(loss, d["out.loss_scaled"], rtol=2e-6)
     assert err < 2e-5, err
     assert bufs < 1e-5, bufs
+
+
+@pytest.mark.parametrize("name", ["c2_b2", "amp_hybrid", "c3_b2"])
+def test_oracle_sized_goldens(name):
+    """The oracle at BASELINE sizes (C3 / C2 architectures, B=2, ragged) against the
+    reference's fp32 capture: loss, stats, encoder output, CTC argmax, every parameter's
+    gradient norm / sum / 256-element head, BatchNorm running stats."""
+    from goldens import assert_grad_close, is_null_grad, regenerate_sized, sibling_weight
+    from test_model_build import build
+    cfg, d, m = regenerate_sized(name, build)
+    torch.set_num_threads(8)
+    ora = OracleASR(cfg, {k: v.detach() for k, v in m.state_dict().items()})
+    inp = {k: torch.from_numpy(v) for k, v in section(d, "in").items()}
+    loss, stats, _ = ora(**inp)
+    loss.backward()
+    np.testing.assert_allclose(loss.item(), d["out.loss"], rtol=2e-6, atol=1e-4)
+    for k, v in section(d, "stat").items():
+        np.testing.assert_allclose(float(stats[k]), v, rtol=2e-6, atol=1e-4, err_msg=k)
+    np.testing.assert_allclose(ora.encoder_out.detach().numpy(), d["out.encoder_out"], atol=1e-4, rtol=1e-4)
+    np.testing.assert_array_equal(ora.encoder_out_lens.numpy(), d["out.encoder_out_lens"])
+    np.testing.assert_array_equal(ora.ctc_logits.detach().argmax(-1).numpy(), d["out.ctc_argmax"])
+    gn_all = section(d, "gn")
+    for k, gn in gn_all.items():
+        g = ora.params[k].grad.double()
+        if is_null_grad(k):  # exact gradient 0: rounding noise, small against the weight's
+            assert g.norm().item() <= 1e-3 * gn_all[sibling_weight(k)], k
+            continue
+        np.testing.assert_allclose(g.norm().item(), gn, rtol=5e-4, err_msg=k)
+        assert_grad_close(g.reshape(-1)[:256].numpy(), d["gh." + k], k)
+    for k, v in section(d, "buf_after").items():
+        np.testing.assert_allclose(ora.bufs[k].numpy(), v, atol=1e-5, rtol=1e-5, err_msg=k)

@@ -53,6 +53,7 @@ def test_validate_weighted_average_single_process():
 class _DP:
     def __init__(self, model):
         self.world_size = dist.get_world_size()
+        self.active = self.world_size > 1
         self.group = None
         self.arena = model  # buf_f32 / buf_i64
 
