@@ -201,8 +201,8 @@ def conv2d_subsampling(P, name, x, cfg, training):
         pe = rel_pos_table(max(5000, t), d)
         c0 = pe.shape[0] // 2
         pos = pe[c0 - t + 1: c0 + t].unsqueeze(0)
-        return drop(x, pdp, training), drop(pos, pdp, training)
-    x = x + sinusoid_table(t, d).unsqueeze(0)
+        return drop(x, pdp, training), drop(pos.to(x.dtype), pdp, training)
+    x = x + sinusoid_table(t, d).to(x.dtype).unsqueeze(0)
     return drop(x, pdp, training), None
 
 
@@ -242,7 +242,7 @@ def transformer_decoder(P, hs, hlens, ys_in, ys_in_lens, cfg, training):
     tgt_mask = (~pad_mask(ys_in_lens, L))[:, None, :] & torch.tril(torch.ones(L, L, dtype=torch.bool))[None]
     mem_mask = (~pad_mask(hlens, hs.shape[1]))[:, None, :]
     x = F.embedding(ys_in, P["decoder.embed.0.weight"])
-    x = x * math.sqrt(d) + sinusoid_table(L, d).unsqueeze(0)
+    x = x * math.sqrt(d) + sinusoid_table(L, d).to(x.dtype).unsqueeze(0)
     x = drop(x, cfg["positional_dropout_rate"], training)
     for i in range(cfg["num_blocks"]):
         n = f"decoder.decoders.{i}"
@@ -308,8 +308,11 @@ class OracleASR:
     """ESPnetASRModel.forward (espnet2/asr/espnet_model.py:188-338) with encoder=conformer,
     decoder=transformer, normalize=utterance_mvn, frontend/specaug None."""
 
-    def __init__(self, cfg: dict, state: Dict[str, Tensor]):
+    def __init__(self, cfg: dict, state: Dict[str, Tensor], dtype=torch.float32):
+        """dtype=torch.float64 gives the exact-arithmetic yardstick the fp32 results (the
+        reference's and the build's) are both measured against."""
         self.cfg = cfg
+        self.dtype = dtype
         self.V = cfg["vocab_size"]
         self.ctc_weight = cfg["model_conf"].get("ctc_weight", 0.5)
         self.lsm = cfg["model_conf"].get("lsm_weight", 0.0)
@@ -319,12 +322,14 @@ class OracleASR:
         self.bufs = {}
         for k, v in state.items():
             t = torch.as_tensor(v).clone()
-            if "running" in k or "num_batches" in k:
+            if "running" in k:
+                self.bufs[k] = t.to(dtype)
+            elif "num_batches" in k:
                 self.bufs[k] = t
             elif self.ctc_weight == 1.0 and k.startswith("decoder."):
                 continue  # decoder dropped when ctc_weight == 1 (espnet_model.py:147-155)
             else:
-                self.params[k] = t.float().requires_grad_(True)
+                self.params[k] = t.to(dtype).requires_grad_(True)
         self.training = True
 
     def forward(self, speech, speech_lengths, text, text_lengths):
@@ -332,7 +337,7 @@ class OracleASR:
         P = self.params
         text = text.clone()
         text = text[:, : int(text_lengths.max())]
-        speech = speech[:, : int(speech_lengths.max())]
+        speech = speech[:, : int(speech_lengths.max())].to(self.dtype)
         feats = utterance_mvn(speech, speech_lengths)
         enc, olens = conformer_encoder(P, feats, speech_lengths, cfg["encoder_conf"], self.bufs,
                                        self.training)
