@@ -791,6 +791,21 @@ __global__ void embed_fwd_kernel(long rows, int d, int L, const long long* __res
     y[i] = v;
   }
 }
+// y[r] = dropout(y[r] + pe[r % L]) in place: the absolute PositionalEncoding after the
+// subsampling Linear (embedding.py:81-92; the Linear's epilogue already applied x*xscale).
+// Same per-element dropout index r*d + c as ea_scale_dropout, so the backward is an
+// ea_scale_dropout(_colsum) with scale xscale.
+__global__ void add_pe_dropout_kernel(long n, int d, int L, const float* __restrict__ pe, float p, uint64_t seed,
+                                      const unsigned long long* salt, float* __restrict__ y) {
+  if (p > 0.f) seed = ea_salted(seed, salt);
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+    const long r = i / d;
+    const int c = (int)(i % d);
+    float v = y[i] + pe[(r % L) * d + c];
+    if (p > 0.f) v *= drop_scale(seed, (uint64_t)i, p);
+    y[i] = v;
+  }
+}
 // dE[tok[r]] += xscale * dropout_mask * dy[r], deterministic: one block per row r; the
 // block of a token's FIRST row sums all of that token's rows in increasing order and owns
 // the update of dE[tok] (no atomics, bit-reproducible).  tok staged in LDS (rows <= 4096).
@@ -1155,6 +1170,17 @@ extern "C" int ea_embed_fwd(long rows, int d, int L, const long long* tok, const
   EA_ENTRY();
   const long n = rows * d;
   hipLaunchKernelGGL(embed_fwd_kernel, EA_GRID(n), rows, d, L, tok, E, xscale, pe, p, (uint64_t)seed, ea_g_rng_salt, y);
+  EA_LAUNCH_CHECK();
+  return 0;
+}
+
+extern "C" int ea_add_pe_dropout(long rows, int d, int L, const float* pe, float p, unsigned long long seed,
+                                 float* y, void* stream) {
+  EA_ENTRY();
+  EA_CHECK_ARG(rows >= 0 && d > 0 && L > 0);
+  const long n = rows * d;
+  if (n == 0) return 0;
+  hipLaunchKernelGGL(add_pe_dropout_kernel, EA_GRID(n), n, d, L, pe, p, (uint64_t)seed, ea_g_rng_salt, y);
   EA_LAUNCH_CHECK();
   return 0;
 }

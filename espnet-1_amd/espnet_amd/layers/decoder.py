@@ -63,6 +63,11 @@ def sinusoid_table(n, d):
 
 
 class PositionalEncoding(nn.Module):
+    """embedding.py:35-92: x * sqrt(d) + pe[t], dropout (the table is a constant, not in
+    the state_dict)."""
+
+    absolute = True
+
     def __init__(self, d_model, dropout_rate, max_len=5000):
         super().__init__()
         self.d_model = d_model

@@ -111,6 +111,21 @@ class Conv2dSubsampling(nn.Module):
         return SubsampleFn.apply(feats, self._anchor, self, seed, self.training)
 
 
+def _out_linear(x2r, wl, b, pe, p, seed, B, T2, C):
+    """out.0 Linear on (t, f*C + c) rows, then x*sqrt(d) and dropout (embedding.py:326 for
+    RelPositionalEncoding); with the absolute PositionalEncoding (TransformerEncoder) the
+    table row is added before the dropout (embedding.py:91-92).  Both apply the dropout
+    with ea_scale_dropout's index law, so the backward is the same scale-dropout."""
+    y = empty(B * T2, C, device=x2r.device)
+    if getattr(pe, "absolute", False):
+        ops.linear(x2r, wl, y, epi=ops.make_epi(bias=b.f("out.0.bias"), post_scale=pe.xscale))
+        lib.ea_add_pe_dropout(B * T2, C, T2, pe.table(T2, y.device).data_ptr(), float(p), seed, y.data_ptr(),
+                              ops.stream())
+    else:
+        ops.linear(x2r, wl, y, epi=ops.make_epi(bias=b.f("out.0.bias"), post_scale=pe.xscale, drop_p=p, seed=seed))
+    return y
+
+
 class SubsampleFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, feats, anchor, m: Conv2dSubsampling, seed, training):
@@ -150,10 +165,8 @@ class SubsampleFn(torch.autograd.Function):
         # out.0 Linear on (t, f*C + c) rows, * sqrt(d), dropout (embedding.py:326)
         wl = empty(C, F2 * C, dtype=cd, device=dev)
         ops.permute3(b.f("out.0.weight"), wl, C, C, F2)  # (d, C, F2) -> (d, F2, C)
-        y = empty(B * T2, C, device=dev)
         p = pe.dropout_rate if training else 0.0
-        ops.linear(x2.view(B * T2, F2 * C), wl, y,
-                   epi=ops.make_epi(bias=b.f("out.0.bias"), post_scale=pe.xscale, drop_p=p, seed=seed))
+        y = _out_linear(x2.view(B * T2, F2 * C), wl, b, pe, p, seed, B, T2, C)
         ctx.m = m
         ctx.meta = (B, T, Fin, T1, F1, T2, F2, p, seed)
         ctx.save = (col1, x1, col2, w2, x2, wl)
@@ -191,10 +204,8 @@ class SubsampleFn(torch.autograd.Function):
             probe.end("conv2_gemm")
         wl = empty(C, F2 * C, dtype=cd, device=dev)
         ops.permute3(b.f("out.0.weight"), wl, C, C, F2)  # (d, C, F2) -> (d, F2, C)
-        y = empty(B * T2, C, device=dev)
         p = pe.dropout_rate if training else 0.0
-        ops.linear(x2.view(B * T2, F2 * C), wl, y,
-                   epi=ops.make_epi(bias=b.f("out.0.bias"), post_scale=pe.xscale, drop_p=p, seed=seed))
+        y = _out_linear(x2.view(B * T2, F2 * C), wl, b, pe, p, seed, B, T2, C)
         ctx.m = m
         ctx.implicit = True
         ctx.meta = (B, T, Fin, T1, F1, T2, F2, p, seed)

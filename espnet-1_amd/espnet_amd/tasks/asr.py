@@ -13,7 +13,8 @@ from typing import Any, Dict
 
 from ..asr.ctc import CTC
 from ..asr.decoder.transformer_decoder import TransformerDecoder
-from ..asr.encoder.conformer_encoder import ConformerEncoder
+from ..asr.encoder.conformer_encoder import AbsEncoder, ConformerEncoder
+from ..asr.encoder.transformer_encoder import TransformerEncoder
 from ..asr.espnet_model import ESPnetASRModel, UtteranceMVN
 from ..asr.frontend.default import DefaultFrontend, GlobalMVN
 from ..asr.specaug import SpecAug
@@ -40,7 +41,8 @@ class ClassChoices:
         return self.classes[key]
 
 
-encoder_choices = ClassChoices("encoder", dict(conformer=ConformerEncoder), default="rnn")
+encoder_choices = ClassChoices("encoder", dict(conformer=ConformerEncoder, transformer=TransformerEncoder),
+                                default="rnn")
 decoder_choices = ClassChoices("decoder", dict(transformer=TransformerDecoder), default=None,
                                optional=True)
 normalize_choices = ClassChoices("normalize", dict(utterance_mvn=UtteranceMVN, global_mvn=GlobalMVN),

@@ -378,6 +378,13 @@ int ea_add_pos_bias(long N, int H, int dk, const void* q, long ldq, const float*
  * backward adds into the embedding gradient in a fixed order (no atomics; rows <= 4096). */
 int ea_embed_fwd(long rows, int d, int L, const long long* tok, const float* E, float xscale,
                  const float* pe, float p, unsigned long long seed, float* y, void* stream);
+/* y = dropout(y + pe[r % L]) in place over rows x d (f32): the absolute PositionalEncoding
+ * added after Conv2dSubsampling's Linear for encoder: transformer (TransformerEncoder,
+ * espnet2/asr/encoder/transformer_encoder.py:94 -> subsampling.py:66-69 + embedding.py:81-92;
+ * the Linear epilogue applies the x*sqrt(d) scale).  Dropout index r*d + c (ea_scale_dropout's
+ * law), so the backward is ea_scale_dropout_colsum with scale sqrt(d). */
+int ea_add_pe_dropout(long rows, int d, int L, const float* pe, float p, unsigned long long seed, float* y,
+                      void* stream);
 int ea_embed_bwd(long rows, int d, const long long* tok, const float* dy, float xscale, float p,
                  unsigned long long seed, float* dE, void* stream);
 

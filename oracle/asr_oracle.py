@@ -231,6 +231,32 @@ def conformer_encoder(P, x, ilens, cfg, bufs, training):
     return x, olens
 
 
+def transformer_encoder(P, x, ilens, cfg, training):
+    """TransformerEncoder.forward, espnet2/asr/encoder/transformer_encoder.py:184-232 with
+    Conv2dSubsampling + PositionalEncoding(odim, dropout_rate) (the encoder passes its
+    dropout_rate, not positional_dropout_rate: transformer_encoder.py:94,
+    subsampling.py:66-69) and EncoderLayer (transformer/encoder_layer.py:79-130,
+    normalize_before=True): x += drop(MHA(LN1(x))); x += drop(FFN_relu(LN2(x)))."""
+    if x.shape[1] < 7:
+        raise ValueError("TooShortUttError: needs more than 7 frames")
+    T = x.shape[1]
+    sub_cfg = dict(cfg, pos_enc_layer_type="abs_pos", positional_dropout_rate=cfg["dropout_rate"])
+    x, _ = conv2d_subsampling(P, "encoder.embed", x, sub_cfg, training)
+    Tp = x.shape[1]
+    olens = subsample_lens(ilens, T)
+    mask = (~pad_mask(olens, Tp))[:, None, :]
+    pd = cfg["dropout_rate"]
+    for i in range(cfg["num_blocks"]):
+        n = f"encoder.encoders.{i}"
+        y = layer_norm(P, n + ".norm1", x)
+        x = x + drop(std_mha(P, n + ".self_attn", y, y, mask, cfg["attention_heads"], cfg["attention_dropout_rate"],
+                             training), pd, training)
+        y = layer_norm(P, n + ".norm2", x)
+        x = x + drop(ffn(P, n + ".feed_forward", y, F.relu, pd, training), pd, training)
+    x = layer_norm(P, "encoder.after_norm", x)
+    return x, olens
+
+
 # ---------------------------------------------------------------------------- decoder
 def transformer_decoder(P, hs, hlens, ys_in, ys_in_lens, cfg, training):
     """BaseTransformerDecoder.forward, espnet2/asr/decoder/transformer_decoder.py:92-145,
@@ -305,8 +331,8 @@ def add_sos_eos(ys_pad, ys_lens, sos, eos, ignore_id=-1):
 
 # ---------------------------------------------------------------------------- model
 class OracleASR:
-    """ESPnetASRModel.forward (espnet2/asr/espnet_model.py:188-338) with encoder=conformer,
-    decoder=transformer, normalize=utterance_mvn, frontend/specaug None."""
+    """ESPnetASRModel.forward (espnet2/asr/espnet_model.py:188-338) with encoder=conformer
+    or transformer, decoder=transformer, normalize=utterance_mvn, frontend/specaug None."""
 
     def __init__(self, cfg: dict, state: Dict[str, Tensor], dtype=torch.float32):
         """dtype=torch.float64 gives the exact-arithmetic yardstick the fp32 results (the
@@ -339,8 +365,11 @@ class OracleASR:
         text = text[:, : int(text_lengths.max())]
         speech = speech[:, : int(speech_lengths.max())].to(self.dtype)
         feats = utterance_mvn(speech, speech_lengths)
-        enc, olens = conformer_encoder(P, feats, speech_lengths, cfg["encoder_conf"], self.bufs,
-                                       self.training)
+        if cfg.get("encoder", "conformer") == "transformer":
+            enc, olens = transformer_encoder(P, feats, speech_lengths, cfg["encoder_conf"], self.training)
+        else:
+            enc, olens = conformer_encoder(P, feats, speech_lengths, cfg["encoder_conf"], self.bufs,
+                                           self.training)
         stats = {}
         loss_ctc = loss_att = acc = None
         if self.ctc_weight != 0.0:

@@ -155,6 +155,17 @@ CONFIGS = {
         model_conf=dict(ctc_weight=1.0, lsm_weight=0.0, length_normalized_loss=False),
         speech_lengths=[100, 100, 81], text_lengths=[10, 4, 8],
     ),
+    # BASELINE.json configs[0] (C1): Transformer-tiny (2x64 encoder/decoder), mini_an4-shaped
+    # batch of 2 (utterance lengths from the 8 mini_an4 recordings), V=30 characters
+    "c1_tiny": dict(
+        encoder="transformer", input_size=80, vocab_size=30,
+        encoder_conf=dict(output_size=64, attention_heads=4, linear_units=256, num_blocks=2,
+                          dropout_rate=0.0, positional_dropout_rate=0.0, attention_dropout_rate=0.0,
+                          input_layer="conv2d", normalize_before=True),
+        decoder="transformer", decoder_conf=decoder_conf(4, 256, 2),
+        model_conf=dict(ctc_weight=0.3, lsm_weight=0.1, length_normalized_loss=False),
+        speech_lengths=[290, 220], text_lengths=[14, 9],
+    ),
     # realistic widths (d=256, h=4, ff=1024, d_k=64), one block each, equal lengths
     "medium_hybrid": dict(
         encoder="conformer", input_size=80, vocab_size=300,
@@ -738,8 +749,8 @@ def capture_beam(name="beam", cfg_name="tiny_hybrid"):
 if __name__ == "__main__":
     os.makedirs(OUT, exist_ok=True)
     which = sys.argv[1:] or ["models", "train", "ops", "ddp"]
-    if "models" in which:
-        for n, c in CONFIGS.items():
+    for n, c in CONFIGS.items():
+        if "models" in which or n in which:
             capture_model(n, c, light=n.startswith("medium"))
     if "train" in which:
         capture_train_steps()

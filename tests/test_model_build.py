@@ -17,7 +17,7 @@ def build(cfg):
     return build_model(args)
 
 
-@pytest.mark.parametrize("name", ["tiny_hybrid", "tiny_ctc", "medium_hybrid"])
+@pytest.mark.parametrize("name", ["tiny_hybrid", "tiny_ctc", "medium_hybrid", "c1_tiny"])
 def test_state_dict_layout_and_init(name):
     cfg, d = load(name)
     torch.manual_seed(0)

@@ -29,7 +29,7 @@ def run(name, amp=False):
     return cfg, d, m, loss, stats, weight
 
 
-@pytest.mark.parametrize("name", ["tiny_hybrid", "tiny_ctc", "medium_hybrid"])
+@pytest.mark.parametrize("name", ["tiny_hybrid", "tiny_ctc", "medium_hybrid", "c1_tiny"])
 def test_model_fp32_parity(name):
     cfg, d, m, loss, stats, weight = run(name)
     # fp32 atol 1e-4 on loss/logits (BASELINE.json north_star); + a relative term for
@@ -61,18 +61,27 @@ def test_model_fp32_parity(name):
         np.testing.assert_allclose(sd[k].cpu().numpy(), v, atol=1e-5, rtol=1e-5, err_msg=k)
 
 
-@pytest.mark.parametrize("name", ["tiny_hybrid", "medium_hybrid"])
+@pytest.mark.parametrize("name", ["tiny_hybrid", "medium_hybrid", "c1_tiny"])
 def test_model_bf16_amp_close(name):
-    """AMP (bf16 MFMA operands, f32 accumulation/normalisation/losses) stays close."""
+    """AMP (bf16 MFMA operands, f32 accumulation/normalisation/losses) stays close, per
+    parameter tensor: relative L2 distance of each gradient from the reference's fp32
+    gradient <= 6e-2 (bf16 keeps 8 significant bits; the BASELINE-sized goldens bound it
+    against the reference's own bf16 run, tests/test_model_sized_gpu.py)."""
+    from goldens import is_null_grad
     cfg, d, m, loss, stats, weight = run(name, amp=True)
     np.testing.assert_allclose(loss.item(), d["out.loss"], rtol=2e-2)
     params = dict(m.named_parameters())
-    num = den = 0.0
+    worst = []
     for k, g in section(d, "g").items():
+        if is_null_grad(k):
+            continue
         mine = params[k].grad.double().cpu()
-        num += float(((mine - torch.from_numpy(g).double()) ** 2).sum())
-        den += float((torch.from_numpy(g).double() ** 2).sum())
-    assert (num / den) ** 0.5 < 5e-2, (num / den) ** 0.5
+        ref = torch.from_numpy(g).double()
+        e = float((mine - ref).norm() / ref.norm().clamp_min(1e-30))
+        worst.append((e, k))
+    worst.sort(reverse=True)
+    print(name, "worst per-tensor bf16 rel L2:", worst[:4])
+    assert worst[0][0] < 6e-2, worst[:5]
 
 
 def test_model_with_specaug_matches_oracle():

@@ -17,7 +17,7 @@ def run_oracle(name):
     return cfg, d, model, loss, stats
 
 
-@pytest.mark.parametrize("name", ["tiny_hybrid", "tiny_ctc", "medium_hybrid"])
+@pytest.mark.parametrize("name", ["tiny_hybrid", "tiny_ctc", "medium_hybrid", "c1_tiny"])
 def test_oracle_model_forward_backward(name):
     cfg, d, model, loss, stats = run_oracle(name)
     np.testing.assert_allclose(loss.item(), d["out.loss"], rtol=2e-6, atol=1e-4)
