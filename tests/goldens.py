@@ -36,7 +36,7 @@ def sibling_weight(name):
     return name[: -len("bias")] + "weight"
 
 
-def assert_grad_close(mine, ref, name, rtol=2e-4, scale_tol=1e-3):
+def assert_grad_close(mine, ref, name, rtol=2e-4, scale_tol=1e-3, atol=0.0):
     """fp32 gradient parity: |mine - ref| <= rtol*|ref| + scale_tol*max|ref| element-wise.
     The scale term is the fp32 summation-order noise of a deep backward (reduction over
     B*T' rows in a different order than ATen's): relative to the tensor's largest entry,
@@ -45,7 +45,7 @@ def assert_grad_close(mine, ref, name, rtol=2e-4, scale_tol=1e-3):
     mine = np.asarray(mine, dtype=np.float64)
     ref = np.asarray(ref, dtype=np.float64)
     scale = float(np.abs(ref).max()) if ref.size else 0.0
-    np.testing.assert_allclose(mine, ref, rtol=rtol, atol=scale_tol * scale + 1e-12, err_msg=name)
+    np.testing.assert_allclose(mine, ref, rtol=rtol, atol=max(atol, scale_tol * scale) + 1e-12, err_msg=name)
 
 
 def perturb_norms(model, gen):

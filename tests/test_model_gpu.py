@@ -49,8 +49,11 @@ def test_model_fp32_parity(name):
         np.testing.assert_allclose(m._last_decoder_out.detach().cpu().numpy(), d["out.decoder_out"],
                                    atol=1e-4, rtol=1e-4)
     params = dict(m.named_parameters())
+    from goldens import assert_grad_close
     for k, g in section(d, "g").items():
-        np.testing.assert_allclose(params[k].grad.cpu().numpy(), g, atol=2e-5, rtol=2e-4, err_msg=k)
+        # atol 2e-5, or 1e-5 of the tensor's largest entry when that is larger (the
+        # reference's own fp32 summation noise on O(10) gradients, tests/goldens.py)
+        assert_grad_close(params[k].grad.cpu().numpy(), g, k, rtol=2e-4, scale_tol=1e-5, atol=2e-5)
     for k, gn in section(d, "gn").items():
         mine = params[k].grad.double().cpu()
         np.testing.assert_allclose(mine.norm().item(), gn, rtol=1e-4, err_msg=k)
