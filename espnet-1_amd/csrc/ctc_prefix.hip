@@ -25,8 +25,9 @@ EA_DEV float np_logaddexpf(float x, float y) {
 
 // logp[t][v] = log_softmax(logits[t]) (one block per frame), then (block 0, thread 0)
 // r0[t] = (logzero, cumulative blank log-prob)  — initial_state(), :289-301
-__global__ __launch_bounds__(256) void ctc_logsoftmax_kernel(int V, const float* __restrict__ logits, long ldl,
-                                                             float* __restrict__ logp) {
+template <bool LOG>
+__global__ __launch_bounds__(256) void ctc_softmax_rows_kernel(int V, const float* __restrict__ logits, long ldl,
+                                                               float* __restrict__ out) {
   __shared__ float red[256];
   const int t = blockIdx.x;
   const float* row = logits + (long)t * ldl;
@@ -49,7 +50,7 @@ __global__ __launch_bounds__(256) void ctc_logsoftmax_kernel(int V, const float*
     __syncthreads();
   }
   const float lz = m + logf(red[0]);
-  for (int v = threadIdx.x; v < V; v += 256) logp[(long)t * V + v] = row[v] - lz;
+  for (int v = threadIdx.x; v < V; v += 256) out[(long)t * V + v] = LOG ? row[v] - lz : expf(row[v] - lz);
 }
 
 __global__ void ctc_prefix_init_kernel(int T, int V, int blank, const float* __restrict__ logp, float* __restrict__ r0) {
@@ -126,9 +127,23 @@ extern "C" int ea_ctc_prefix_init(int T, int V, const float* logits, long ld_log
   EA_ENTRY();
   EA_CHECK_ARG(T >= 1 && V >= 1 && blank >= 0 && blank < V && ld_logits >= V);
   hipStream_t st = (hipStream_t)stream;
-  hipLaunchKernelGGL(ctc_logsoftmax_kernel, dim3(T), dim3(256), 0, st, V, logits, ld_logits, logp);
+  hipLaunchKernelGGL(ctc_softmax_rows_kernel<true>, dim3(T), dim3(256), 0, st, V, logits, ld_logits, logp);
   EA_LAUNCH_CHECK();
   hipLaunchKernelGGL(ctc_prefix_init_kernel, dim3(1), dim3(1), 0, st, T, V, blank, logp, r0);
+  EA_LAUNCH_CHECK();
+  return 0;
+}
+
+extern "C" int ea_softmax_rows(long rows, int V, const float* logits, long ld, float* out, int log, void* stream) {
+  EA_ENTRY();
+  EA_CHECK_ARG(rows >= 0 && rows < (1L << 31) && V >= 1 && ld >= V);
+  if (rows == 0) return 0;
+  if (log)
+    hipLaunchKernelGGL(ctc_softmax_rows_kernel<true>, dim3((unsigned)rows), dim3(256), 0, (hipStream_t)stream, V,
+                       logits, ld, out);
+  else
+    hipLaunchKernelGGL(ctc_softmax_rows_kernel<false>, dim3((unsigned)rows), dim3(256), 0, (hipStream_t)stream, V,
+                       logits, ld, out);
   EA_LAUNCH_CHECK();
   return 0;
 }

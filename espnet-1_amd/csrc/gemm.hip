@@ -118,6 +118,34 @@ __global__ void probe_end_kernel(unsigned long long* s) {
 }
 }  // namespace
 
+// Step phase timer (ea_phase_stamp): st = {last stamp, step counter}; ring[slot][4] =
+// {forward, backward, optimizer seconds, extra}.  Stream-ordered single-thread kernels: a
+// stamp runs after everything issued before it on the stream, so the differences are the
+// device durations of the phases, and a captured step re-measures itself on every replay.
+namespace {
+__global__ void phase_stamp_kernel(unsigned long long* st, float* ring, int cap, int phase, const float* extra) {
+  const unsigned long long now = __builtin_amdgcn_s_memrealtime();
+  if (phase > 0) {
+    const long slot = (long)(st[1] % (unsigned long long)cap);
+    ring[slot * 4 + phase - 1] = (float)((double)(now - st[0]) * 1e-8);  // 100 MHz clock
+    if (phase == 3) {
+      ring[slot * 4 + 3] = extra ? extra[0] : 0.f;
+      st[1] = st[1] + 1ull;
+    }
+  }
+  st[0] = now;
+}
+}  // namespace
+
+extern "C" int ea_phase_stamp(unsigned long long* state, float* ring, int cap, int phase, const float* extra,
+                              void* stream) {
+  EA_ENTRY();
+  EA_CHECK_ARG(state != nullptr && ring != nullptr && cap > 0 && phase >= 0 && phase <= 3);
+  hipLaunchKernelGGL(phase_stamp_kernel, dim3(1), dim3(1), 0, (hipStream_t)stream, state, ring, cap, phase, extra);
+  EA_LAUNCH_CHECK();
+  return 0;
+}
+
 extern "C" int ea_gemm_set_diag(unsigned long long* buf) {
   EA_ENTRY();
   g_diag = buf;

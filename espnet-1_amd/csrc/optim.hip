@@ -48,19 +48,24 @@ __global__ void adam_prep_kernel(ea_opt_state* st, ea_lr_schedule sc, float b1, 
                                  float max_norm) {
   const float nrm = norm ? norm[0] : 0.f;
   st->last_norm = nrm;
+  auto lr_at = [&](long long t) {  // espnet2/schedulers/warmup_lr.py:40-50, s = t
+    double lr = sc.base_lr;
+    if (sc.kind == EA_SCHED_WARMUP) {
+      const double s = (double)t, w = sc.warmup_steps;
+      lr = sc.base_lr * sqrt(w) * fmin(1.0 / sqrt(s), s * pow(w, -1.5));
+    }
+    return lr;
+  };
   if (norm && !isfinite(nrm)) {
     st->skip = 1;
+    st->next_lr = (float)lr_at(st->step + 1);
     return;
   }
   st->skip = 0;
   const long long t = st->step + 1;
   st->step = t;
-  double lr = sc.base_lr;
-  if (sc.kind == EA_SCHED_WARMUP) {  // espnet2/schedulers/warmup_lr.py:40-50, s = t
-    const double s = (double)t, w = sc.warmup_steps;
-    lr = sc.base_lr * sqrt(w) * fmin(1.0 / sqrt(s), s * pow(w, -1.5));
-  }
-  st->lr = (float)lr;
+  st->lr = (float)lr_at(t);
+  st->next_lr = (float)lr_at(t + 1);
   st->bc1 = (float)(1.0 - pow((double)b1, (double)t));
   st->bc2_sqrt = (float)sqrt(1.0 - pow((double)b2, (double)t));
   st->coef = (norm && max_norm > 0.f) ? fminf(max_norm / (nrm + 1e-6f), 1.f) : 1.f;

@@ -74,8 +74,10 @@ class LrSchedule(ctypes.Structure):
     _fields_ = [("kind", ctypes.c_int), ("warmup_steps", ctypes.c_float), ("base_lr", ctypes.c_double)]
 
 
-# ea_opt_state (device memory, 32 B): step i64 | lr bc1 bc2_sqrt coef last_norm f32 | skip i32
-OPT_STATE_BYTES = 32
+# ea_opt_state (device memory, 40 B): step i64 | lr bc1 bc2_sqrt coef last_norm f32 | skip i32 |
+# next_lr f32 | pad
+OPT_STATE_BYTES = 40
+OPT_STATE_NEXT_LR = 8  # float index of next_lr
 
 
 _CTYPES = {

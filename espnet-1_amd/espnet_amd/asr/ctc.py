@@ -54,6 +54,24 @@ class CTC(nn.Module):
         return out.view(B, T, -1)
 
     @torch.no_grad()
+    def _softmax(self, hs_pad, log):
+        lg = self.logits(hs_pad)
+        B, T, V = lg.shape
+        out = torch.empty_like(lg)
+        lib.ea_softmax_rows(B * T, V, lg.data_ptr(), V, out.data_ptr(), int(log), ops.stream())
+        return out
+
+    def softmax(self, hs_pad):
+        """ctc.py:99-107: softmax(ctc_lo(hs_pad), dim=2) -> (B, T, V).  An inference helper
+        here (no autograd; the interCTC conditioning that differentiates it is not built)."""
+        return self._softmax(hs_pad, False)
+
+    def log_softmax(self, hs_pad):
+        """ctc.py:109-117: log_softmax(ctc_lo(hs_pad), dim=2) -> (B, T, V) (decoding's CTC
+        prefix scorer input); no autograd."""
+        return self._softmax(hs_pad, True)
+
+    @torch.no_grad()
     def argmax(self, hs_pad):
         """ctc.py:119-127: argmax over the vocabulary of ctc_lo(hs_pad) -> (B, T) int64."""
         lg = self.logits(hs_pad)

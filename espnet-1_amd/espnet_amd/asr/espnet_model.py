@@ -22,13 +22,14 @@ from ..layers.common import site_seed
 from ..layers.losses import CombineFn, LabelSmoothingLossFn
 from .ctc import CTC
 from .error_calculator import ErrorCalculator
+from .abs_modules import AbsNormalize
 
 
 class AbsESPnetModel(nn.Module):
     pass
 
 
-class UtteranceMVN(nn.Module):
+class UtteranceMVN(AbsNormalize):
     """espnet2/layers/utterance_mvn.py:10-43 (norm_means=True, norm_vars=False)."""
 
     def __init__(self, norm_means: bool = True, norm_vars: bool = False, eps: float = 1.0e-20):

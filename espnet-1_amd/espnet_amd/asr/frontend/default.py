@@ -25,6 +25,7 @@ from torch import nn
 
 from ... import hip_ops as ops
 from ..._lib import lib
+from ..abs_modules import AbsFrontend, AbsNormalize
 
 
 # ----------------------------------------------------------------------------- librosa mel
@@ -159,7 +160,7 @@ class LogMel(nn.Module):
         self.register_buffer("melmat", torch.from_numpy(mel_filterbank(**self.mel_options).T).float())
 
 
-class DefaultFrontend(nn.Module):
+class DefaultFrontend(AbsFrontend):
     """frontend/default.py:17-140 with frontend_conf's WPE / beamformer off (their defaults)."""
 
     def __init__(self, fs: Union[int, str] = 16000, n_fft: int = 512, win_length: int = None,
@@ -204,7 +205,7 @@ class DefaultFrontend(nn.Module):
         return feats, olens
 
 
-class GlobalMVN(nn.Module):
+class GlobalMVN(AbsNormalize):
     """layers/global_mvn.py:13-104: mean/std buffers from a stats file (.npy array or .npz
     with count/sum/sum_square), loaded with numpy's default allow_pickle=False."""
 

@@ -19,6 +19,7 @@ from torch import nn
 
 from .. import hip_ops as ops
 from .._lib import lib
+from .abs_modules import AbsSpecAug
 
 
 def _width_range(r, name):
@@ -113,7 +114,7 @@ def _draw_spans(B, D, width_range, num_mask):
     return torch.stack([pos, length], dim=-1).to(torch.int32)
 
 
-class SpecAug(nn.Module):
+class SpecAug(AbsSpecAug):
     """specaug.py:9-102 with the same constructor arguments and ValueErrors."""
 
     def __init__(self, apply_time_warp: bool = True, time_warp_window: int = 5,

@@ -25,47 +25,10 @@ from typing import Collection, Dict, Optional, Sequence, Tuple, Union
 import torch
 
 
-class EpochReporter:
-    """reporter.py: stats[epoch][phase][key] = value; epoch = the current epoch."""
+from .reporter import Reporter
 
-    def __init__(self, epoch: int = 0):
-        self.epoch = epoch
-        self.stats: Dict[int, Dict[str, Dict[str, float]]] = {}
-
-    def set_epoch(self, epoch: int):
-        self.epoch = epoch
-
-    def get_epoch(self) -> int:
-        return self.epoch
-
-    def register(self, phase: str, values: Dict[str, float], epoch: int = None):
-        e = self.epoch if epoch is None else epoch
-        self.stats.setdefault(e, {}).setdefault(phase, {}).update({k: float(v) for k, v in values.items()})
-
-    def has(self, key: str, key2: str, epoch: int = None) -> bool:
-        epoch = self.get_epoch() if epoch is None else epoch
-        return epoch in self.stats and key in self.stats[epoch] and key2 in self.stats[epoch][key]
-
-    def sort_epochs_and_values(self, key: str, key2: str, mode: str):
-        if mode not in ("min", "max"):
-            raise ValueError(f"mode must min or max: {mode}")
-        if not self.has(key, key2):
-            raise KeyError(f"{key}.{key2} is not found")
-        values = [(e, self.stats[e][key][key2]) for e in self.stats]
-        return sorted(values, key=(lambda x: x[1]) if mode == "min" else (lambda x: -x[1]))
-
-    def sort_epochs(self, key, key2, mode):
-        return [e for e, _ in self.sort_epochs_and_values(key, key2, mode)]
-
-    def get_best_epoch(self, key, key2, mode, nbest: int = 0) -> int:
-        return self.sort_epochs(key, key2, mode)[nbest]
-
-    def state_dict(self):
-        return {"stats": self.stats, "epoch": self.epoch}
-
-    def load_state_dict(self, state_dict):
-        self.epoch = state_dict["epoch"]
-        self.stats = state_dict["stats"]
+# the per-epoch reporter the checkpoint / averaging code reads (train/reporter.py)
+EpochReporter = Reporter
 
 
 def _load(path, map_location="cpu"):
@@ -112,52 +75,67 @@ def resume(checkpoint, model, reporter, optimizers: Sequence, schedulers: Sequen
     logging.info(f"The training was resumed using {checkpoint}")
 
 
+def _relink(link: Path, target: str):
+    if link.is_symlink() or link.exists():
+        link.unlink()
+    link.symlink_to(target)
+
+
+def _sum_into(running: Dict[str, torch.Tensor], other: Dict[str, torch.Tensor]):
+    for key in running:
+        running[key] = running[key] + other[key]
+
+
+def _divide_floats(running: Dict[str, torch.Tensor], n: int):
+    """Float entries become means; integer ones (BatchNorm num_batches_tracked) stay sums."""
+    for key, v in running.items():
+        if v.dtype.is_floating_point or v.dtype.is_complex:
+            running[key] = v / n
+
+
 @torch.no_grad()
 def average_nbest_models(output_dir, reporter, best_model_criterion: Sequence[Sequence[str]],
                          nbest: Union[Collection[int], int], suffix: Optional[str] = None) -> None:
-    """average_nbest_models.py:13-108, including its reuse of the first loaded epoch's dict
-    as the accumulator (so with several nbest values a later average starts from the
-    earlier sum, exactly as the reference does)."""
+    """main_funcs/average_nbest_models.py:13-108: for each criterion with values, link
+    {phase}.{key}.ave_1best to the best epoch file, write {phase}.{key}.ave_{n}best as the
+    mean of the n best epoch files (integer tensors summed), and link {phase}.{key}.ave to
+    the largest average.
+
+    Observable detail kept from the reference: the state dicts read from disk are cached per
+    epoch and an average is accumulated INTO the cached dict of its best epoch, so a later
+    (larger-n) average of the same criterion, or of another criterion whose list contains
+    that epoch, starts from that already-averaged dict.  The files written are therefore
+    bit-identical to the reference's (tests/test_checkpoint.py against its output)."""
     output_dir = Path(output_dir)
-    nbests = [nbest] if isinstance(nbest, int) else list(nbest)
-    if len(nbests) == 0:
+    sizes = [nbest] if isinstance(nbest, int) else list(nbest)
+    if not sizes:
         warnings.warn("At least 1 nbest values are required")
-        nbests = [1]
-    suffix = suffix + "." if suffix is not None else ""
-    nbest_epochs = [(ph, k, reporter.sort_epochs_and_values(ph, k, m)[: max(nbests)])
-                    for ph, k, m in best_model_criterion if reporter.has(ph, k)]
-    _loaded = {}
-    for ph, cr, epoch_and_values in nbest_epochs:
-        _nbests = [i for i in nbests if i <= len(epoch_and_values)] or [1]
-        for n in _nbests:
+        sizes = [1]
+    tag = "" if suffix is None else suffix + "."
+    cache: Dict[int, Dict[str, torch.Tensor]] = {}
+
+    def state_of(epoch: int) -> Dict[str, torch.Tensor]:
+        if epoch not in cache:
+            cache[epoch] = _load(output_dir / f"{epoch}epoch.pth")
+        return cache[epoch]
+
+    for phase, key, mode in best_model_criterion:
+        if not reporter.has(phase, key):
+            continue
+        ranked = [e for e, _ in reporter.sort_epochs_and_values(phase, key, mode)[: max(sizes)]]
+        usable = [n for n in sizes if n <= len(ranked)] or [1]
+        stem = f"{phase}.{key}"
+        for n in usable:
             if n == 0:
                 continue
             if n == 1:
-                e, _ = epoch_and_values[0]
-                op = output_dir / f"{e}epoch.pth"
-                sym_op = output_dir / f"{ph}.{cr}.ave_1best.{suffix}pth"
-                if sym_op.is_symlink() or sym_op.exists():
-                    sym_op.unlink()
-                sym_op.symlink_to(op.name)
-            else:
-                op = output_dir / f"{ph}.{cr}.ave_{n}best.{suffix}pth"
-                logging.info(f'Averaging {n}best models: criterion="{ph}.{cr}": {op}')
-                avg = None
-                for e, _ in epoch_and_values[:n]:
-                    if e not in _loaded:
-                        _loaded[e] = _load(output_dir / f"{e}epoch.pth")
-                    states = _loaded[e]
-                    if avg is None:
-                        avg = states
-                    else:
-                        for k in avg:
-                            avg[k] = avg[k] + states[k]
-                for k in avg:
-                    if not str(avg[k].dtype).startswith("torch.int"):
-                        avg[k] = avg[k] / n
-                torch.save(avg, op)
-        op = output_dir / f"{ph}.{cr}.ave_{max(_nbests)}best.{suffix}pth"
-        sym_op = output_dir / f"{ph}.{cr}.ave.{suffix}pth"
-        if sym_op.is_symlink() or sym_op.exists():
-            sym_op.unlink()
-        sym_op.symlink_to(op.name)
+                _relink(output_dir / f"{stem}.ave_1best.{tag}pth", f"{ranked[0]}epoch.pth")
+                continue
+            out = output_dir / f"{stem}.ave_{n}best.{tag}pth"
+            logging.info(f'Averaging {n}best models: criterion="{stem}": {out}')
+            running = state_of(ranked[0])
+            for e in ranked[1:n]:
+                _sum_into(running, state_of(e))
+            _divide_floats(running, n)
+            torch.save(running, out)
+        _relink(output_dir / f"{stem}.ave.{tag}pth", f"{stem}.ave_{max(usable)}best.{tag}pth")

@@ -145,8 +145,15 @@ class SubReporter:
         end = self.count if end is None else end
         if self.count == 0 or start == end:
             return ""
-        parts = [_fmt(k, s.aggregate(start, end)) for k, s in self.stats.items()]
-        return f"{self.epoch}epoch:{self.key}:{start + 1}-{end}batch: " + ", ".join(parts)
+        msg = f"{self.epoch}epoch:{self.key}:{start + 1}-{end}batch: "
+        for idx, (k, s) in enumerate(self.stats.items()):
+            # the reference separates keys with ", " except before key number `count` (it
+            # compares the key index with the number of steps, reporter.py:190) - kept, so the
+            # log lines are byte-identical
+            if idx != 0 and idx != self.count:
+                msg += ", "
+            msg += _fmt(k, s.aggregate(start, end))
+        return msg
 
     def finished(self) -> None:
         self._finished = True

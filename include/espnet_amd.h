@@ -163,6 +163,12 @@ int ea_gemm_set_probe(unsigned long long* slots);
  * buf[4b..4b+3] = {shader clock at start, after the main loop, at the end, 100 MHz clock at start}.
  * buf must hold 4 * blocks entries. */
 int ea_gemm_set_diag(unsigned long long* buf);
+/* Device-side step phase timer (Reporter forward_time / backward_time / optim_step_time,
+ * espnet2/train/trainer.py:566,623,682): phase 0 marks the step start, phases 1..3 write the
+ * seconds since the previous stamp into ring[slot*4 + phase-1] (slot = step counter % cap),
+ * phase 3 also copies *extra (e.g. the optimizer's device lr; NULL: 0) into ring[slot*4+3]
+ * and advances the counter.  state = {last stamp, step counter} (2 x u64, zeroed). */
+int ea_phase_stamp(unsigned long long* state, float* ring, int cap, int phase, const float* extra, void* stream);
 int ea_probe_begin(unsigned long long* slots, void* stream);
 int ea_probe_end(unsigned long long* slots, void* stream);
 
@@ -509,13 +515,16 @@ typedef struct ea_lr_schedule {
   float warmup_steps;
   double base_lr;
 } ea_lr_schedule;
-typedef struct ea_opt_state {  /* device memory, zero-initialised; 32 bytes */
+typedef struct ea_opt_state {  /* device memory, zero-initialised; 40 bytes */
   long long step;      /* applied updates so far */
   float lr;            /* lr of the last applied update */
   float bc1, bc2_sqrt; /* 1-b1^t, sqrt(1-b2^t) */
   float coef;          /* clip coefficient min(1, max_norm/(norm+1e-6)) */
   float last_norm;     /* grad norm seen by the last call */
   int skip;            /* 1: the last call skipped the update (non-finite norm) */
+  float next_lr;       /* lr(step + 1): the optimizer's lr after scheduler.step(), what the
+                          reference reports as optim0_lr0 (trainer.py:705-712) */
+  int pad;
 } ea_opt_state;
 int ea_adam_step_dev(long n, float* params, const float* grads, float* exp_avg, float* exp_avg_sq,
                      void* params_bf16, const ea_lr_schedule* sched, float beta1, float beta2, float eps,
@@ -530,6 +539,10 @@ int ea_axpby_scalar(const float* a, float wa, const float* b, float wb, float* o
 
 
 /* ---------------------------------------------------------------- joint CTC/attention decoding */
+
+/* out[r][v] = softmax or (log=1) log_softmax over the V entries of logits row r (rows*ld f32,
+ * out dense rows x V): CTC.softmax / CTC.log_softmax, espnet2/asr/ctc.py:99-117. */
+int ea_softmax_rows(long rows, int V, const float* logits, long ld, float* out, int log, void* stream);
 
 /* CTCPrefixScorer.init_state (espnet/nets/scorers/ctc.py:25-37 + ctc_prefix_score.py:289-301):
  * logp[t][v] = log_softmax(logits[t]) (T x V f32, dense) and the initial forward variables

@@ -486,6 +486,41 @@ def capture_sampler(name="sampler"):
     out = {"cfg": np.array(json.dumps({k: {kk: (vv if kk != "shape_files" else len(vv)) for kk, vv in v.items()}
                                        for k, v in settings.items()})),
            "T": Ts.astype(np.int64)}
+    from espnet2.samplers.build_batch_sampler import build_batch_sampler
+    # the other batch types, through build_batch_sampler (build_batch_sampler.py:72-162)
+    cat = os.path.join(d, "utt2category")
+    with open(cat, "w") as f:
+        for i in range(n):
+            f.write(f"utt{i:03d} {'a' if i % 3 else 'b'}\n")
+    built = {
+        "b_unsorted": dict(type="unsorted", batch_size=7, batch_bins=0, shape_files=[sp]),
+        "b_unsorted_dl": dict(type="unsorted", batch_size=7, batch_bins=0, shape_files=[sp], drop_last=True),
+        "b_sorted": dict(type="sorted", batch_size=7, batch_bins=0, shape_files=[sp]),
+        "b_sorted_desc": dict(type="sorted", batch_size=8, batch_bins=0, shape_files=[sp], sort_batch="descending"),
+        "b_folded": dict(type="folded", batch_size=12, batch_bins=0, shape_files=[sp, tx], fold_lengths=[800, 150]),
+        "b_folded_min": dict(type="folded", batch_size=12, batch_bins=0, shape_files=[sp], fold_lengths=[500],
+                             min_batch_size=3, sort_batch="descending", sort_in_batch="ascending"),
+        "b_folded_cat": dict(type="folded", batch_size=10, batch_bins=0, shape_files=[sp], fold_lengths=[700],
+                             utt2category_file=cat),
+        "b_length": dict(type="length", batch_size=0, batch_bins=9000, shape_files=[sp, tx]),
+        "b_length_min": dict(type="length", batch_size=0, batch_bins=20000, shape_files=[sp], min_batch_size=4),
+        "b_length_nopad": dict(type="length", batch_size=0, batch_bins=7000, shape_files=[sp], padding=False,
+                               drop_last=True),
+        "b_numel": dict(type="numel", batch_size=0, batch_bins=600000, shape_files=[sp, tx], sort_batch="descending"),
+    }
+    for key, kw in built.items():
+        s = build_batch_sampler(**kw)
+        flat, sizes = [], []
+        for b in s:
+            flat += [int(k[3:]) for k in b]
+            sizes.append(len(b))
+        out[f"{key}.flat"] = np.array(flat, np.int64)
+        out[f"{key}.sizes"] = np.array(sizes, np.int64)
+    meta = json.loads(str(out["cfg"]))
+    meta["built"] = {k: {kk: (vv if kk not in ("shape_files", "utt2category_file") else
+                              (len(vv) if kk == "shape_files" else "utt2category"))
+                         for kk, vv in v.items()} for k, v in built.items()}
+    out["cfg"] = np.array(json.dumps(meta))
     for key, kw in settings.items():
         s = NumElementsBatchSampler(**kw)
         flat, sizes = [], []
@@ -697,6 +732,134 @@ def capture_sized(name):
           f"max {devs[-1]:.2e} -> {path} ({os.path.getsize(path) / 1e6:.2f} MB)")
 
 
+def capture_epoch(name="epoch_accum2", cfg_name="tiny_hybrid"):
+    """Trainer.train_one_epoch (espnet2/train/trainer.py:472-731) itself, on the CPU, over a
+    fixed 4-batch iterator with accum_grad=2 (the conformer8 recipe uses 4): loss / accum,
+    two backwards per update, clip_grad_norm_(5), Adam + WarmupLR after every 2nd batch;
+    then the reporter's per-epoch aggregates (reporter.py) and the parameters after."""
+    import argparse
+
+    from espnet2.schedulers.warmup_lr import WarmupLR
+    from espnet2.train.reporter import Reporter
+    from espnet2.train.trainer import Trainer, TrainerOptions
+    from espnet2.train.distributed_utils import DistributedOption
+
+    cfg = CONFIGS[cfg_name]
+    torch.manual_seed(0)
+    model = build_reference_model(cfg)
+    perturb_norms(model, torch.Generator().manual_seed(1000))
+    sd0 = {k: v.clone() for k, v in model.state_dict().items()}
+    opt = torch.optim.Adam(model.parameters(), lr=0.002, weight_decay=1e-6)
+    sched = WarmupLR(opt, warmup_steps=10)
+    batches = [make_batch(cfg, torch.Generator().manual_seed(11 + s)) for s in range(4)]
+    rec = {"cfg": np.array(json.dumps(dict(cfg_name=cfg_name, lr=0.002, weight_decay=1e-6, warmup_steps=10,
+                                           grad_clip=5.0, accum_grad=2, n_batches=4)))}
+    for k, v in sd0.items():
+        rec["w." + k] = np32(v)
+    for s, b in enumerate(batches):
+        for k, v in b.items():
+            rec[f"in{s}." + k] = v.clone().numpy()
+    args = argparse.Namespace(ngpu=0, resume=False, use_amp=False, train_dtype="float32", grad_noise=False,
+                              accum_grad=2, grad_clip=5.0, grad_clip_type=2.0, log_interval=None,
+                              no_forward_run=False, use_matplotlib=False, use_tensorboard=False, use_wandb=False,
+                              output_dir="/tmp", max_epoch=1, seed=0, sharded_ddp=False, patience=None,
+                              keep_nbest_models=[1], nbest_averaging_interval=0,
+                              early_stopping_criterion=("valid", "loss", "min"),
+                              best_model_criterion=[("train", "loss", "min")],
+                              val_scheduler_criterion=("valid", "loss"), unused_parameters=False,
+                              wandb_model_log_interval=-1, create_graph_in_tensorboard=False)
+    options = TrainerOptions(**{f: getattr(args, f) for f in TrainerOptions.__dataclass_fields__})
+    reporter = Reporter()
+    reporter.set_epoch(1)
+    iterator = [([f"u{s}_{i}" for i in range(len(b["speech"]))], {k: v.clone() for k, v in b.items()})
+                for s, b in enumerate(batches)]
+    with reporter.observe("train") as sub:
+        invalid = Trainer.train_one_epoch(model=model, iterator=iterator, optimizers=[opt], schedulers=[sched],
+                                          scaler=None, reporter=sub, summary_writer=None, options=options,
+                                          distributed_option=DistributedOption(distributed=False))
+    stats = reporter.stats[1]["train"]
+    keys = [k for k, v in stats.items() if isinstance(v, float) and not k.endswith("_time")]
+    rec["stats_keys"] = np.array(json.dumps(keys))
+    for k in keys:
+        rec["stat." + k] = np.array(stats[k], dtype=np.float64)
+    rec["all_invalid"] = np.array(bool(invalid))
+    rec["total_count"] = np.array(stats["total_count"])
+    rec["time_keys"] = np.array(json.dumps(sorted(k for k in stats if k.endswith("_time"))))
+    for k, v in model.state_dict().items():
+        rec["w_after." + k] = np32(v)
+    path = os.path.join(OUT, f"{name}.npz")
+    np.savez_compressed(path, **rec)
+    print(f"{name}: stats {({k: stats[k] for k in keys})} -> {path}")
+
+
+def capture_reporter(name="reporter"):
+    """espnet2/train/reporter.py: SubReporter aggregation (WeightedAverage with NaN / inf
+    values and zero weights, Average, keys registered late or skipped in a step), its
+    log_message, and Reporter epoch bookkeeping (sort / best / early stopping)."""
+    from espnet2.train.reporter import Reporter
+    rep = Reporter()
+    seq = [  # (weighted stats, weight, unweighted stats)
+        ({"loss": 3.0, "acc": 0.5}, 4, {"lr": 0.1}),
+        ({"loss": float("nan"), "acc": 0.25}, 2, {"lr": 0.2}),
+        ({"loss": 1.0, "acc": None}, 3, {}),
+        ({"loss": 2.0, "acc": 0.75, "late": 9.0}, 1, {"lr": 0.4}),
+        ({"loss": float("inf"), "acc": 1.0, "late": 1.0}, 5, {"lr": 0.5}),
+    ]
+    out = {}
+    msgs = []
+    for e in (1, 2, 3):
+        rep.set_epoch(e)
+        with rep.observe("train") as sub:
+            for st, w, un in seq:
+                sub.register({k: (None if v is None else v * e) for k, v in st.items()}, w)
+                if un:
+                    sub.register(un)
+                sub.next()
+                msgs.append(sub.log_message(-2))
+        with rep.observe("valid") as sub:
+            sub.register({"loss": float(4 - e) if e != 2 else 5.0, "acc": 0.1 * e}, 2)
+            sub.next()
+    for e in (1, 2, 3):
+        for key in ("train", "valid"):
+            for k2, v in rep.stats[e][key].items():
+                if isinstance(v, float):
+                    out[f"e{e}.{key}.{k2}"] = np.array(v, dtype=np.float64)
+    out["msgs"] = np.array(json.dumps(msgs))
+    out["sort_valid_loss_min"] = np.array(rep.sort_epochs("valid", "loss", "min"))
+    out["best_train_acc_max"] = np.array(rep.get_best_epoch("train", "acc", "max"))
+    out["early_stop_p0"] = np.array(rep.check_early_stopping(0, "valid", "loss", "min"))
+    out["early_stop_p1"] = np.array(rep.check_early_stopping(1, "valid", "loss", "min"))
+    path = os.path.join(OUT, f"{name}.npz")
+    np.savez_compressed(path, **out)
+    print(f"{name}: {len(out)} entries -> {path}")
+
+
+def capture_iter_factory(name="iterfactory"):
+    """SequenceIterFactory batch orders (espnet2/iterators/sequence_iter_factory.py:72-135)
+    for shuffle on/off and num_iters_per_epoch below / above the number of batches."""
+    from espnet2.iterators.sequence_iter_factory import SequenceIterFactory
+    batches = [tuple(f"u{i}_{j}" for j in range(i % 3 + 1)) for i in range(7)]
+    out = {}
+    cases = {"plain": dict(), "shuffle": dict(shuffle=True), "n3": dict(shuffle=True, num_iters_per_epoch=3),
+             "n10": dict(shuffle=True, num_iters_per_epoch=10), "n3_noshuf": dict(num_iters_per_epoch=3)}
+    for key, kw in cases.items():
+        f = SequenceIterFactory(dataset=None, batches=list(batches), seed=5, **kw)
+        for epoch in range(1, 6):
+            import espnet2.iterators.sequence_iter_factory as m
+            orig = m.DataLoader
+            got = {}
+            m.DataLoader = lambda dataset, batch_sampler, **k: got.setdefault("b", batch_sampler)
+            try:
+                f.build_iter(epoch)
+            finally:
+                m.DataLoader = orig
+            out[f"{key}.e{epoch}"] = np.array(json.dumps([list(b) for b in got["b"]]))
+    out["cfg"] = np.array(json.dumps({"batches": [list(b) for b in batches], "cases": cases, "seed": 5}))
+    path = os.path.join(OUT, f"{name}.npz")
+    np.savez_compressed(path, **out)
+    print(f"{name}: {len(out)} entries -> {path}")
+
+
 # (beam, length_bonus weight, maxlenratio[, ctc_weight])
 BEAM_CASES = [(3, 0.0, 0.0), (4, 0.5, 0.0), (3, 0.0, 0.5), (3, 0.0, 0.0, 0.3), (4, 0.5, 0.0, 0.5),
               (3, 0.0, 0.5, 0.3)]
@@ -769,6 +932,12 @@ if __name__ == "__main__":
         capture_frontend()
     if "beam" in which:
         capture_beam()
+    if "epoch" in which:
+        capture_epoch()
+    if "reporter" in which:
+        capture_reporter()
+    if "iterfactory" in which:
+        capture_iter_factory()
     for n in SIZED:
         if n in which or "sized" in which:
             capture_sized(n)

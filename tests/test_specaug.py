@@ -72,6 +72,7 @@ def test_sampler_matches_reference(tmp_path):
     sp, tx = tmp_path / "speech_shape", tmp_path / "text_shape"
     sp.write_text("".join(f"utt{i:03d} {t},80\n" for i, t in enumerate(Ts)))
     tx.write_text("".join(f"utt{i:03d} {max(1, round(t / 25))}\n" for i, t in enumerate(Ts)))
+    built = cfg.pop("built")
     for key, kw in cfg.items():
         kw = dict(kw)
         kw["shape_files"] = [str(sp), str(tx)][: kw["shape_files"]]
@@ -80,6 +81,19 @@ def test_sampler_matches_reference(tmp_path):
         sizes = [len(b) for b in s]
         assert flat == d[f"{key}.flat"].tolist(), key
         assert sizes == d[f"{key}.sizes"].tolist(), key
+    # every batch type through build_batch_sampler (incl. a category file)
+    from espnet_amd.samplers.batch_samplers import build_batch_sampler
+    cat = tmp_path / "utt2category"
+    cat.write_text("".join(f"utt{i:03d} {'a' if i % 3 else 'b'}\n" for i in range(len(Ts))))
+    for key, kw in built.items():
+        kw = dict(kw)
+        kw["shape_files"] = [str(sp), str(tx)][: kw["shape_files"]]
+        if "utt2category_file" in kw:
+            kw["utt2category_file"] = str(cat)
+        s = build_batch_sampler(**kw)
+        assert [int(k[3:]) for b in s for k in b] == d[f"{key}.flat"].tolist(), key
+        assert [len(b) for b in s] == d[f"{key}.sizes"].tolist(), key
+        assert s.generate(0) == list(s)
     # in-memory shapes give the same batches as the shape files
     mem = NumElementsBatchSampler(400000, utt2shapes=[{f"utt{i:03d}": [int(t), 80] for i, t in enumerate(Ts)}])
     assert [int(k[3:]) for b in mem for k in b] == d["default.flat"].tolist()
