@@ -121,3 +121,22 @@ def test_ctc_prefix_kernel_matches_numpy_restatement():
         ol = len(y) - 1
         lo = max(ol, 1) - 1  # rows below the start are never read by the reference
         np.testing.assert_allclose(rn.cpu().numpy()[:, lo:], r_ref[:, lo:], rtol=1e-5, atol=1e-4)
+
+
+def test_ctc_softmax_log_softmax_api():
+    """CTC.softmax / CTC.log_softmax / CTC.argmax (espnet2/asr/ctc.py:99-127) on the HIP
+    path against torch fp32 of the same ctc_lo logits."""
+    from goldens import load, section
+    from test_model_build import build
+    cfg, d = load("tiny_hybrid")
+    torch.manual_seed(0)
+    m = build(cfg)
+    m.load_state_dict({k: torch.from_numpy(v) for k, v in section(d, "w").items()})
+    m.prepare("cuda:0", amp=False)
+    hs = torch.from_numpy(d["out.encoder_out"]).cuda()
+    lg = m.ctc.logits(hs).double().cpu()
+    sm = m.ctc.softmax(hs).double().cpu()
+    lsm = m.ctc.log_softmax(hs).double().cpu()
+    torch.testing.assert_close(sm, torch.softmax(lg, dim=2), atol=1e-6, rtol=1e-5)
+    torch.testing.assert_close(lsm, torch.log_softmax(lg, dim=2), atol=1e-5, rtol=1e-6)
+    assert torch.equal(m.ctc.argmax(hs).cpu(), lg.argmax(2))
