@@ -8,7 +8,7 @@ from typing import Tuple
 import torch
 from torch import nn
 
-from ...layers.common import Bound
+from ...layers.common import Bound, multisequential_draw
 from ...layers.conformer import LayerNorm, MultiHeadedAttention, PositionwiseFeedForward
 from ...layers.decoder import DecoderFn, DecoderLayer, PositionalEncoding, decoder_arena_groups
 
@@ -68,6 +68,7 @@ class TransformerDecoder(AbsDecoder):
 
     def forward(self, hs_pad: torch.Tensor, hlens: torch.Tensor, ys_in_pad: torch.Tensor,
                 ys_in_lens: torch.Tensor, seed: int = 0) -> Tuple[torch.Tensor, torch.Tensor]:
+        multisequential_draw(len(self.decoders))
         x = DecoderFn.apply(hs_pad.contiguous(), hlens, ys_in_pad.contiguous(), ys_in_lens, self,
                             seed, self.training)
         return x, ys_in_lens

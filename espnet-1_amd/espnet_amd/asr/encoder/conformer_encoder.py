@@ -13,7 +13,7 @@ from typing import List, Optional, Tuple, Union
 import torch
 from torch import nn
 
-from ...layers.common import LayerNormFn, site_seed
+from ...layers.common import LayerNormFn, multisequential_draw, site_seed
 from ...layers.conformer import (ConvolutionModule, EncoderLayer, LayerNorm,
                                  PositionwiseFeedForward, RelPositionMultiHeadedAttention)
 from ...layers.subsampling import Conv2dSubsampling, RelPositionalEncoding
@@ -158,6 +158,7 @@ class ConformerEncoder(AbsEncoder):
         olens = torch.empty(B, dtype=torch.long, device=xs_pad.device)
         lib.ea_subsample_lens(B, T, ilens.data_ptr(), olens.data_ptr(), ops.stream())
         x = self.embed(xs_pad, seed)
+        multisequential_draw(len(self.encoders))
         T2 = x.shape[1]
         pos = self.embed.out[1].pos_emb(T2, x.device, self._cd, self.training, site_seed(seed, 0, 9))
         for layer in self.encoders:

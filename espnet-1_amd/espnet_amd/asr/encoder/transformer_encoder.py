@@ -18,7 +18,7 @@ from torch import nn
 
 from ... import hip_ops as ops
 from ..._lib import lib
-from ...layers.common import LayerNormFn
+from ...layers.common import LayerNormFn, multisequential_draw
 from ...layers.conformer import MultiHeadedAttention, PositionwiseFeedForward
 from ...layers.decoder import PositionalEncoding
 from ...layers.subsampling import Conv2dSubsampling
@@ -113,6 +113,7 @@ class TransformerEncoder(AbsEncoder):
         olens = torch.empty(B, dtype=torch.long, device=xs_pad.device)
         lib.ea_subsample_lens(B, T, ilens.data_ptr(), olens.data_ptr(), ops.stream())
         x = self.embed(xs_pad, seed)
+        multisequential_draw(len(self.encoders))
         for layer in self.encoders:
             x = layer(x, olens, seed)
         x = LayerNormFn.apply(x, self.after_norm)

@@ -20,7 +20,7 @@ from .._lib import (ACT_NONE, ACT_RELU, ACT_SWISH, EPI_ACT, EPI_DACT, EPI_RESID,
 __all__ = ["Bound", "rup", "empty", "ops", "lib", "EPI_ACT", "EPI_DACT", "EPI_RESID",
            "EPI_STORE", "ACT_NONE", "ACT_RELU", "ACT_SWISH", "site_seed", "attn_fwd", "attn_bwd",
            "LayerNormFn", "ln_fwd", "ln_bwd", "math", "F32", "fused_attn_ok", "attn_dmask", "ptr",
-           "attn_fused_bwd", "dv_buf", "drop_arg", "site_dv"]
+           "attn_fused_bwd", "dv_buf", "drop_arg", "site_dv", "multisequential_draw"]
 
 F32 = torch.float32
 
@@ -69,6 +69,15 @@ def attn_fused_bwd(*, B, H, T1, T2, q, ldq, k, ldk, v, ldv, bu, bv, pp, ldp, kle
                            ldp, ptr(klen), int(causal), float(scale), float(p), seed, ptr(O), ldo, ptr(lse),
                            ptr(dO), lddo, ptr(dq), lddq, ptr(dk), lddk, ptr(dv), lddv, ptr(dbd), ldbd, ptr(part),
                            ldpart, ptr(qv_out), ldqv, ptr(dmask), ldm, ws.data_ptr(), n.value, flags, ops.stream())
+
+
+def multisequential_draw(n: int):
+    """MultiSequential.forward (espnet/nets/pytorch_backend/transformer/repeat.py:27) draws
+    `torch.empty(len(self)).uniform_()` from torch's default CPU generator on every forward,
+    training or not (its layer-drop decisions; rate 0 in the recipes).  The build draws the
+    same numbers at the same point so the host RNG stream the reference's SpecAug / TimeWarp
+    read next step stays aligned."""
+    torch.empty(n).uniform_()
 
 
 def site_seed(base: int, layer: int, site: int) -> int:

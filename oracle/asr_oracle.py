@@ -225,6 +225,7 @@ def conformer_encoder(P, x, ilens, cfg, bufs, training):
     Tp = x.shape[1]
     olens = subsample_lens(ilens, T)
     mask = (~pad_mask(olens, Tp))[:, None, :]
+    torch.empty(cfg["num_blocks"]).uniform_()  # MultiSequential's layer-drop draw, repeat.py:27
     for i in range(cfg["num_blocks"]):
         x = conformer_layer(P, f"encoder.encoders.{i}", x, pos, mask, cfg, bufs, training)
     x = layer_norm(P, "encoder.after_norm", x)
@@ -246,6 +247,7 @@ def transformer_encoder(P, x, ilens, cfg, training):
     olens = subsample_lens(ilens, T)
     mask = (~pad_mask(olens, Tp))[:, None, :]
     pd = cfg["dropout_rate"]
+    torch.empty(cfg["num_blocks"]).uniform_()  # repeat.py:27
     for i in range(cfg["num_blocks"]):
         n = f"encoder.encoders.{i}"
         y = layer_norm(P, n + ".norm1", x)
@@ -270,6 +272,7 @@ def transformer_decoder(P, hs, hlens, ys_in, ys_in_lens, cfg, training):
     x = F.embedding(ys_in, P["decoder.embed.0.weight"])
     x = x * math.sqrt(d) + sinusoid_table(L, d).to(x.dtype).unsqueeze(0)
     x = drop(x, cfg["positional_dropout_rate"], training)
+    torch.empty(cfg["num_blocks"]).uniform_()  # repeat.py:27
     for i in range(cfg["num_blocks"]):
         n = f"decoder.decoders.{i}"
         y = layer_norm(P, n + ".norm1", x)
@@ -364,6 +367,8 @@ class OracleASR:
         text = text.clone()
         text = text[:, : int(text_lengths.max())]
         speech = speech[:, : int(speech_lengths.max())].to(self.dtype)
+        if self.training and cfg.get("specaug_conf") is not None:  # espnet_model.py:365-366
+            speech = specaug(speech, speech_lengths, cfg["specaug_conf"])
         feats = utterance_mvn(speech, speech_lengths)
         if cfg.get("encoder", "conformer") == "transformer":
             enc, olens = transformer_encoder(P, feats, speech_lengths, cfg["encoder_conf"], self.training)

@@ -300,6 +300,47 @@ def capture_train_steps(name="train2", cfg_name="tiny_hybrid", steps=2):
     print(f"{name}: -> {path} ({os.path.getsize(path)/1e6:.2f} MB)")
 
 
+def capture_train_specaug(name="train3_specaug", cfg_name="tiny_hybrid", steps=3):
+    """Three Trainer steps with SpecAug (conformer8 options) under one torch.manual_seed:
+    the TimeWarp / mask draws of step k+1 come after step k's MultiSequential layer-drop
+    draws (repeat.py:27: 2 encoder + 2 decoder uniforms per forward), so the parameters
+    after step 3 pin the whole host RNG stream of the step, not only SpecAug's."""
+    from espnet2.asr.specaug.specaug import SpecAug
+    from espnet2.schedulers.warmup_lr import WarmupLR
+
+    cfg = CONFIGS[cfg_name]
+    torch.manual_seed(0)
+    model = build_reference_model(cfg)
+    perturb_norms(model, torch.Generator().manual_seed(1000))
+    model.specaug = SpecAug(**SPECAUG_CONFS["conformer8"])
+    sd0 = {k: v.clone() for k, v in model.state_dict().items()}
+    opt = torch.optim.Adam(model.parameters(), lr=0.002, weight_decay=1e-6)
+    sched = WarmupLR(opt, warmup_steps=10)
+    model.train()
+    rec = {"cfg": np.array(json.dumps(dict(cfg_name=cfg_name, lr=0.002, weight_decay=1e-6, warmup_steps=10,
+                                           grad_clip=5.0, steps=steps, seed=123,
+                                           specaug=SPECAUG_CONFS["conformer8"])))}
+    for k, v in sd0.items():
+        rec["w." + k] = np32(v)
+    batches = [make_batch(cfg, torch.Generator().manual_seed(21 + s)) for s in range(steps)]
+    torch.manual_seed(123)
+    for s, batch in enumerate(batches):
+        for k, v in batch.items():
+            rec[f"in{s}." + k] = v.clone().numpy()
+        loss, stats, weight = model(**{k: v.clone() for k, v in batch.items()})
+        loss.backward()
+        torch.nn.utils.clip_grad_norm_(model.parameters(), max_norm=5.0, norm_type=2.0)
+        opt.step()
+        sched.step()
+        opt.zero_grad()
+        rec[f"out{s}.loss"] = np32(loss)
+    for k, v in model.state_dict().items():
+        rec["w_after." + k] = np32(v)
+    path = os.path.join(OUT, f"{name}.npz")
+    np.savez_compressed(path, **rec)
+    print(f"{name}: losses {[float(rec[f'out{s}.loss']) for s in range(steps)]} -> {path}")
+
+
 def capture_ctc_op(name="ctc_op"):
     """Raw CTC (espnet2/asr/ctc.py:52-63 builtin path) on random logits, incl. repeated
     labels, a zero-length target and an infeasible target (zero_infinity=True -> 0)."""
@@ -932,6 +973,8 @@ if __name__ == "__main__":
         capture_frontend()
     if "beam" in which:
         capture_beam()
+    if "train_specaug" in which:
+        capture_train_specaug()
     if "epoch" in which:
         capture_epoch()
     if "reporter" in which:

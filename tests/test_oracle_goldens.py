@@ -176,3 +176,23 @@ def test_oracle_sized_goldens(name):
         assert_grad_close(g.reshape(-1)[:256].numpy(), d["gh." + k], k)
     for k, v in section(d, "buf_after").items():
         np.testing.assert_allclose(ora.bufs[k].numpy(), v, atol=1e-5, rtol=1e-5, err_msg=k)
+
+
+def test_oracle_three_specaug_steps():
+    """Host RNG stream of a training step (SpecAug's draws, then MultiSequential's
+    layer-drop draws, repeat.py:27) against the reference's 3-step SpecAug trainer run."""
+    from oracle.asr_oracle import OracleTrainer
+    meta, d = load("train3_specaug")
+    cfg, _ = load(meta["cfg_name"])
+    cfg = dict(cfg, specaug_conf=meta["specaug"])
+    ora = OracleASR(cfg, section(d, "w"))
+    tr = OracleTrainer(ora, meta["lr"], meta["weight_decay"], meta["warmup_steps"], meta["grad_clip"])
+    torch.manual_seed(meta["seed"])
+    for s in range(meta["steps"]):
+        batch = {k: torch.from_numpy(v) for k, v in section(d, f"in{s}").items()}
+        loss, _, _ = tr.step(batch)
+        np.testing.assert_allclose(loss.item(), d[f"out{s}.loss"], rtol=2e-6, atol=1e-4)
+    for k, v in section(d, "w_after").items():
+        if k in ora.params:
+            tol = 6e-4 if k.endswith("depthwise_conv.bias") else 5e-5
+            np.testing.assert_allclose(ora.params[k].detach().numpy(), v, atol=tol, rtol=1e-5, err_msg=k)

@@ -161,3 +161,35 @@ def test_ctc_backward_fork_is_bit_exact_at_c3():
     assert runs[0][0] == runs[1][0]
     assert runs[0][1] == runs[1][1]
     assert torch.equal(runs[0][2], runs[1][2])
+
+
+def test_three_specaug_steps_follow_reference_rng_stream():
+    """Three eager training steps with SpecAug under one torch.manual_seed against the
+    reference's own 3-step run (tests/golden/train3_specaug.npz): the host draws of step k+1
+    (TimeWarp / masks) come after step k's MultiSequential draws (repeat.py:27), which the
+    build replicates, so every step sees the reference's augmentation.  Tolerances: the
+    HIP bicubic warp differs from ATen's by <= 5e-5 (tests/test_specaug.py)."""
+    from test_model_build import build
+    from espnet_amd.asr.specaug import SpecAug
+    from espnet_amd.optim.adam import ArenaAdam
+    from espnet_amd.schedulers.warmup_lr import WarmupLR
+    from espnet_amd.train.trainer import Trainer
+    meta, d = load("train3_specaug")
+    cfg, _ = load(meta["cfg_name"])
+    torch.manual_seed(0)
+    m = build(cfg)
+    m.load_state_dict({k: torch.from_numpy(v) for k, v in section(d, "w").items()})
+    m.specaug = SpecAug(**meta["specaug"])
+    m.prepare("cuda:0", amp=False)
+    m.train()
+    opt = ArenaAdam(m, lr=meta["lr"], weight_decay=meta["weight_decay"])
+    sched = WarmupLR(opt, warmup_steps=meta["warmup_steps"])
+    torch.manual_seed(meta["seed"])
+    for s in range(meta["steps"]):
+        batch = {k: torch.from_numpy(v) for k, v in section(d, f"in{s}").items()}
+        loss, _, _, _ = Trainer.train_one_step(m, batch, opt, sched, grad_clip=meta["grad_clip"])
+        np.testing.assert_allclose(float(loss), d[f"out{s}.loss"], rtol=2e-5, atol=1e-4)
+    sd = m.state_dict()
+    for k, v in section(d, "w_after").items():
+        tol = 1e-3 if k.endswith("depthwise_conv.bias") else 1e-4
+        np.testing.assert_allclose(sd[k].cpu().float().numpy(), v, atol=tol, rtol=1e-4, err_msg=k)
