@@ -159,18 +159,46 @@ class SpecAug(AbsSpecAug):
         tm = self.time_mask.draw(B, T) if self.time_mask is not None else None
         return (torch.tensor(warp, dtype=torch.int32).reshape(B, 2), per_utt, fm, tm)
 
+    # ------------------------------------------------------------------ captured steps
+    def predraw(self, B: int, T: int, F: int, lens_host, device):
+        """Draw this step's parameters now (host RNG, the reference's order) into a static
+        device buffer for the shape (B, T, F): a hipGraph-captured step then reads them
+        from there on every replay (train/graph.py), so SpecAug steps capture.  The next
+        forward of that shape uses the buffer instead of drawing."""
+        warp, per_utt, fm, tm = self.draw(B, T, F, lens_host)
+        nf = 0 if fm is None else fm.shape[1]
+        nt = 0 if tm is None else tm.shape[1]
+        # the per-utterance warp over each utterance's own length equals the batch warp when
+        # all lengths equal T (time_warp.py:73-86), so a captured kernel always runs per-utterance
+        host = torch.cat([warp.reshape(-1)] + [a.reshape(-1) for a in (fm, tm) if a is not None]).pin_memory()
+        key = (B, T, F)
+        static = getattr(self, "_static", None)
+        if static is None:
+            static = self._static = {}
+        buf = static.get(key)
+        if buf is None or buf[0].numel() != host.numel():
+            buf = static[key] = (torch.empty(host.numel(), dtype=torch.int32, device=device), nf, nt)
+        buf[0].copy_(host, non_blocking=True)
+        self._pending = key
+
     def forward(self, x: torch.Tensor, x_lengths: torch.Tensor = None, lens_host=None):
         """x (B, T, F) f32 on the device -> (augmented copy, x_lengths).  `lens_host` (list of
         ints) spares the device->host read of x_lengths that the equal-length test needs."""
         B, T, F = x.shape
-        if lens_host is None and x_lengths is not None:
-            lens_host = [int(v) for v in x_lengths.tolist()]
-        warp, per_utt, fm, tm = self.draw(B, T, F, lens_host)
         dev = x.device
-        nf = 0 if fm is None else fm.shape[1]
-        nt = 0 if tm is None else tm.shape[1]
-        params = torch.cat([warp.reshape(-1)] + [a.reshape(-1) for a in (fm, tm) if a is not None])
-        params = params.pin_memory().to(dev, non_blocking=True) if x.is_cuda else params
+        pending = getattr(self, "_pending", None)
+        if pending == (B, T, F):
+            self._pending = None
+            params, nf, nt = self._static[pending]
+            per_utt = 1
+        else:
+            if lens_host is None and x_lengths is not None:
+                lens_host = [int(v) for v in x_lengths.tolist()]
+            warp, per_utt, fm, tm = self.draw(B, T, F, lens_host)
+            nf = 0 if fm is None else fm.shape[1]
+            nt = 0 if tm is None else tm.shape[1]
+            params = torch.cat([warp.reshape(-1)] + [a.reshape(-1) for a in (fm, tm) if a is not None])
+            params = params.pin_memory().to(dev, non_blocking=True) if x.is_cuda else params
         warp_d = params[: 2 * B]
         fm_d = params[2 * B: 2 * B + 2 * B * nf]
         tm_d = params[2 * B + 2 * B * nf:]

@@ -76,8 +76,13 @@ def multisequential_draw(n: int):
     `torch.empty(len(self)).uniform_()` from torch's default CPU generator on every forward,
     training or not (its layer-drop decisions; rate 0 in the recipes).  The build draws the
     same numbers at the same point so the host RNG stream the reference's SpecAug / TimeWarp
-    read next step stays aligned."""
-    torch.empty(n).uniform_()
+    read next step stays aligned.  A captured step makes its draws before the replay
+    (train/graph.py) and suppresses these with SKIP_LAYERDROP_DRAWS."""
+    if not SKIP_LAYERDROP_DRAWS:
+        torch.empty(n).uniform_()
+
+
+SKIP_LAYERDROP_DRAWS = False
 
 
 def site_seed(base: int, layer: int, site: int) -> int:

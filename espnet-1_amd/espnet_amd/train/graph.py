@@ -16,7 +16,10 @@ Semantics per call are exactly one training step on the given batch:
   * the next call captures the step (capture executes nothing) and replays it once;
   * later calls copy the batch into the graph's static input buffers and replay.
 Shapes (B, T_max, F, L_max) key the graphs; lengths below the maxima vary freely since the
-kernels read them from device memory.  Outputs (loss, stats, weight, grad_norm) are views
+kernels read them from device memory.  The step's host RNG draws (SpecAug's warp and mask
+parameters, MultiSequential's layer-drop uniforms) are made before each call in the
+reference's order; SpecAug's land in a static device buffer the captured kernel reads, so
+SpecAug (C5) steps are captured too.  Outputs (loss, stats, weight, grad_norm) are views
 of graph memory, overwritten by the next replay of the same graph.
 """
 from __future__ import annotations
@@ -25,6 +28,8 @@ from typing import Dict, Optional
 
 import torch
 
+from ..layers import common
+from ..layers.common import multisequential_draw as layerdrop_draw
 from .trainer import Trainer
 
 
@@ -35,10 +40,6 @@ class _Captured:
 class CapturedTrainStep:
     def __init__(self, model, optimizer, scheduler=None, *, grad_clip: float = 5.0, dp=None,
                  warmup: int = 2, enabled: bool = True):
-        if enabled and getattr(model, "specaug", None) is not None:
-            # SpecAug draws its warp/mask parameters on the host per step (the reference's
-            # torch.randint calls), which a replayed graph would freeze: run such steps eagerly
-            raise ValueError("CapturedTrainStep: a model with SpecAug trains eagerly (enabled=False)")
         self.model = model
         self.optimizer = optimizer
         self.scheduler = scheduler
@@ -68,34 +69,65 @@ class CapturedTrainStep:
     def _maxlens(batch):
         return int(batch["speech_lengths"].max()), int(batch["text_lengths"].max())
 
+    # ------------------------------------------------------------------ host draws
+    def _host_draws(self, batch, maxlens, lens_host):
+        """The step's host RNG draws, in the reference's order, made before the step runs
+        (a replay executes no Python): SpecAug's warp / mask parameters into its static
+        device buffer (SpecAug.predraw), then MultiSequential's layer-drop uniforms of the
+        encoder and decoder (repeat.py:27).  The forward then skips its own draws."""
+        m = self.model
+        if not m.training:
+            return
+        if m.specaug is not None:
+            B, _, F = batch["speech"].shape
+            T = maxlens[0]
+            if lens_host is None:
+                sl = batch["speech_lengths"]
+                lens_host = [int(v) for v in sl.tolist()]  # a device read if the lengths live there
+            if m.frontend is not None:  # sample counts -> feature frames
+                T = int(m.frontend.stft.frames_lens(T))
+                F = m.frontend.output_size()
+                lens_host = [int(m.frontend.stft.frames_lens(int(v))) for v in lens_host]
+            m.specaug.predraw(B, T, F, lens_host, m._device)
+        layerdrop_draw(len(m.encoder.encoders))
+        if m.decoder is not None:
+            layerdrop_draw(len(m.decoder.decoders))
+
     # ------------------------------------------------------------------ step
-    def __call__(self, batch: Dict[str, torch.Tensor], maxlens: Optional[tuple] = None):
-        """One training step on `batch`; returns (loss, stats, weight, grad_norm)."""
+    def __call__(self, batch: Dict[str, torch.Tensor], maxlens: Optional[tuple] = None, lens_host=None):
+        """One training step on `batch`; returns (loss, stats, weight, grad_norm).
+        `lens_host`: the speech lengths as host ints when the batch's live on the device
+        (SpecAug's per-utterance warp draws need them)."""
         if maxlens is None:
             maxlens = self._maxlens(batch)
         if not self.enabled:
             return self._eager(batch, maxlens)
         B, _, F = batch["speech"].shape
         key = (B, maxlens[0], F, maxlens[1])
-        cap = self.graphs.get(key)
-        if cap is not None:
-            for k, v in cap.inputs.items():
-                v.copy_(batch[k][:, :v.shape[1]] if v.dim() > 1 else batch[k], non_blocking=True)
-            cap.graph.replay()
-            return cap.outputs
-        n = self._seen.get(key, 0)
-        self._seen[key] = n + 1
-        dbatch = self._device_batch(batch, maxlens)
-        if n < self.warmup:
-            if self._side is None:
-                self._side = torch.cuda.Stream(device=self.model._device)
-            main = torch.cuda.current_stream()
-            self._side.wait_stream(main)
-            with torch.cuda.stream(self._side):
-                out = self._eager(dbatch, maxlens)
-            main.wait_stream(self._side)
-            return out
-        return self._capture(key, dbatch, maxlens)
+        self._host_draws(batch, maxlens, lens_host)
+        common.SKIP_LAYERDROP_DRAWS = True
+        try:
+            cap = self.graphs.get(key)
+            if cap is not None:
+                for k, v in cap.inputs.items():
+                    v.copy_(batch[k][:, :v.shape[1]] if v.dim() > 1 else batch[k], non_blocking=True)
+                cap.graph.replay()
+                return cap.outputs
+            n = self._seen.get(key, 0)
+            self._seen[key] = n + 1
+            dbatch = self._device_batch(batch, maxlens)
+            if n < self.warmup:
+                if self._side is None:
+                    self._side = torch.cuda.Stream(device=self.model._device)
+                main = torch.cuda.current_stream()
+                self._side.wait_stream(main)
+                with torch.cuda.stream(self._side):
+                    out = self._eager(dbatch, maxlens)
+                main.wait_stream(self._side)
+                return out
+            return self._capture(key, dbatch, maxlens)
+        finally:
+            common.SKIP_LAYERDROP_DRAWS = False
 
     def _capture(self, key, dbatch, maxlens):
         cap = _Captured()

@@ -201,11 +201,12 @@ class Trainer:
                 # the padded maxima from the host copy of the lengths (no device read)
                 maxlens = (int(batch["speech_lengths"].max()), int(batch["text_lengths"].max())) \
                     if "speech_lengths" in batch and "text_lengths" in batch else None
+                lens_host = batch["speech_lengths"].tolist() if "speech_lengths" in batch else None
                 batch = {k: v.to(device, non_blocking=True) if isinstance(v, torch.Tensor) else v
                          for k, v in batch.items()}
                 update = iiter % accum_grad == 0
                 if step_runner is not None and accum_grad == 1:
-                    loss, stats, weight, gn = step_runner(batch, maxlens)
+                    loss, stats, weight, gn = step_runner(batch, maxlens, lens_host=lens_host)
                 else:
                     loss, stats, weight, gn = cls.train_one_step(model, batch, optimizer, scheduler,
                                                                  grad_clip=options.grad_clip, accum_grad=accum_grad,
@@ -318,7 +319,7 @@ class Trainer:
             logging.warning(f"The training has already reached at max_epoch: {start_epoch}")
         dp = ArenaDataParallel(model) if distributed else None
         runner = None
-        if opts.accum_grad == 1 and getattr(model, "specaug", None) is None:
+        if opts.accum_grad == 1:
             runner = CapturedTrainStep(model, optimizers[0], schedulers[0] if schedulers else None,
                                        grad_clip=opts.grad_clip, dp=dp, warmup=2)
         all_invalid = False

@@ -193,3 +193,50 @@ def test_three_specaug_steps_follow_reference_rng_stream():
     for k, v in section(d, "w_after").items():
         tol = 1e-3 if k.endswith("depthwise_conv.bias") else 1e-4
         np.testing.assert_allclose(sd[k].cpu().float().numpy(), v, atol=tol, rtol=1e-4, err_msg=k)
+
+
+@pytest.mark.parametrize("equal_lengths", [False, True])
+def test_captured_specaug_steps_equal_eager(equal_lengths):
+    """SpecAug steps captured as a hipGraph (draws made on the host before each replay into
+    SpecAug's static device buffer, MultiSequential's draws before the replay too) give
+    bit-identical losses and parameters to eager SpecAug steps under the same torch seed;
+    with equal lengths this also checks that the captured per-utterance warp equals the
+    reference's batch warp (time_warp.py:73-86)."""
+    from test_model_build import build
+    from espnet_amd.asr.specaug import SpecAug
+    from espnet_amd.optim.adam import ArenaAdam
+    from espnet_amd.schedulers.warmup_lr import WarmupLR
+    from espnet_amd.train.graph import CapturedTrainStep
+    from espnet_amd.train.trainer import Trainer
+    meta, d = load("train3_specaug")
+    cfg, _ = load(meta["cfg_name"])
+    base = {k: torch.from_numpy(v) for k, v in section(d, "in0").items()}
+    if equal_lengths:
+        T = int(base["speech_lengths"].max())
+        base["speech_lengths"] = torch.full_like(base["speech_lengths"], T)
+    g = torch.Generator().manual_seed(3)
+    batches = [dict(base, speech=torch.randn(base["speech"].shape, generator=g)) for _ in range(4)]
+
+    def setup():
+        torch.manual_seed(0)
+        m = build(cfg)
+        m.load_state_dict({k: torch.from_numpy(v) for k, v in section(d, "w").items()})
+        m.specaug = SpecAug(**meta["specaug"])
+        m.prepare("cuda:0", amp=True, seed=5)
+        m.train()
+        opt = ArenaAdam(m, lr=meta["lr"], weight_decay=meta["weight_decay"])
+        return m, opt, WarmupLR(opt, warmup_steps=meta["warmup_steps"])
+
+    m1, o1, s1 = setup()
+    torch.manual_seed(99)
+    eager = [float(Trainer.train_one_step(m1, b, o1, s1, grad_clip=5.0)[0]) for b in batches]
+    rng_eager = torch.get_rng_state()
+    m2, o2, s2 = setup()
+    run = CapturedTrainStep(m2, o2, s2, grad_clip=5.0, warmup=1)
+    torch.manual_seed(99)
+    graph = [float(run(b)[0]) for b in batches]
+    assert len(run.graphs) == 1
+    assert eager == graph
+    assert torch.equal(rng_eager, torch.get_rng_state())  # the same host draws, in the same order
+    for (k, p1), p2 in zip(m1.state_dict().items(), m2.state_dict().values()):
+        assert torch.equal(p1, p2), k
