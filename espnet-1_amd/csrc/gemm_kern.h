@@ -632,6 +632,31 @@ EA_DEV bf16x8 frag_img(const char* img, int r, int ks, int lane) {
   return frag_bf16<false>(img + (r >> 7) * 16384, r & 127, ks, lane);
 }
 
+// Block -> (output tile, batch slice z, K split sk).  Work items w = (z, sk)-major over the
+// grid's nt tiles; each XCD (blocks dispatched round-robin over the linear block id, so XCD =
+// id % 8 — a speed assumption only) takes a contiguous range of w, so the blocks sharing a
+// slice's A / B panels (every tile of one split, or of one batch slice) share one L2; inside a
+// slice, GM-row groups keep the N-tiles of one M panel together.
+struct TileIdx { int tm, tn, z, sk; };
+EA_DEV TileIdx tile_index(const GemmP& p) {
+  const int nt = p.tiles_m * p.tiles_n;
+  const int total = gridDim.x * gridDim.z;
+  const int bid = blockIdx.x + gridDim.x * blockIdx.z;
+  const int q = total / 8, r = total % 8, xcd = bid % 8;
+  const int w = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + bid / 8;
+  const int zz = w / nt, t = w - zz * nt;
+  const int GM = 8;
+  const int grp = t / (GM * p.tiles_n);
+  const int gm0 = grp * GM;
+  const int gsz = min(GM, p.tiles_m - gm0);
+  TileIdx ti;
+  ti.tm = gm0 + (t % (GM * p.tiles_n)) % gsz;
+  ti.tn = (t % (GM * p.tiles_n)) / gsz;
+  ti.z = zz / p.splitk;
+  ti.sk = zz % p.splitk;
+  return ti;
+}
+
 // Epilogue of one wave's (MI*16) x (NJ*16) accumulator tile, in 64 x 64 chunks transposed
 // through the wave's private LDS region (64 x EPI_LDT floats); each lane then owns 4
 // consecutive columns of 16 rows per chunk.  The operand the epilogue kind reads (aux /
@@ -639,14 +664,14 @@ EA_DEV bf16x8 frag_img(const char* img, int r, int ks, int lane) {
 // flight together (one round trip per batch); bias is read once per batch.  With split-K (p.splitk > 1) the chunk goes to this slice's f32 slab.
 template <int KIND, int MI, int NJ>
 EA_DEV void epi_wave(const GemmP& p, const EpiK& k, char* smem, int z, int zb, int zh, int r0, int c0, int lane,
-                     int w, const f32x4 (&acc)[MI][NJ]) {
+                     int w, const f32x4 (&acc)[MI][NJ], int sk = 0) {
   constexpr int RC = MI < 4 ? MI : 4;  // row blocks per chunk
   constexpr int NG = RC * 4;           // row groups (of 4 lanes' rows) per lane per chunk
   constexpr int HB = NG < 8 ? NG : 8;  // row groups per operand-load batch
   constexpr int NCH = (MI / RC) * (NJ / 4), NBC = NG / HB, NU = NCH * NBC;  // chunks, batches, units
   float* t = (float*)smem + w * (RC * 16) * EPI_LDT;
   const int rq = (lane >> 4) * 4, cc = lane & 15, lc = (lane & 15) * 4;
-  float* slab = p.splitk > 1 ? p.ws + ((long)z * p.splitk + (blockIdx.z % p.splitk)) * (long)p.M * p.N : nullptr;
+  float* slab = p.splitk > 1 ? p.ws + ((long)z * p.splitk + sk) * (long)p.M * p.N : nullptr;
   const bool reads = p.vec_c && !slab &&
                      (KIND == EA_EPI_DACT || (KIND == EA_EPI_RESID && p.epi.resid) ||
                       (KIND == EA_EPI_STORE && p.epi.beta != 0.f));
@@ -834,19 +859,9 @@ __global__ __launch_bounds__(128 * WN, 1) void gemm_bf16_lds(GemmP p) {
   __shared__ __attribute__((aligned(1024))) char smem[SMEM];
   probe_start(p);
 
-  const int nt = p.tiles_m * p.tiles_n;
-  const int bid = blockIdx.x;
-  const int q = nt / 8, r = nt % 8, xcd = bid % 8;
-  const int t = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + bid / 8;
-  const int GM = 8;
-  const int grp = t / (GM * p.tiles_n);
-  const int gm0 = grp * GM;
-  const int gsz = min(GM, p.tiles_m - gm0);
-  const int tm = gm0 + (t % (GM * p.tiles_n)) % gsz;
-  const int tn = (t % (GM * p.tiles_n)) / gsz;
-  const int m0 = tm * BM_, n0 = tn * BN_;
-
-  const int z = blockIdx.z / p.splitk, sk = blockIdx.z % p.splitk;
+  const TileIdx ti = tile_index(p);
+  const int tm = ti.tm, m0 = ti.tm * BM_, n0 = ti.tn * BN_;
+  const int z = ti.z, sk = ti.sk;
   const int zb = z / p.nh, zh = z % p.nh;
   const bf16* A = (const bf16*)p.A + zb * p.sAb + zh * p.sAh;
   const bf16* B = (const bf16*)p.B + zb * p.sBb + zh * p.sBh;
@@ -948,8 +963,12 @@ __global__ __launch_bounds__(128 * WN, 1) void gemm_bf16_lds(GemmP p) {
     const char* ak = abase + kt * astep;
     const char* bk = bbase + kt * bstep;
     if constexpr (MODE == EA_CONV_FWD || MODE == EA_CONV_DGRAD) {
-      const int ktg = ktg0 + kt, q = ktg / CT, c0 = (ktg - q * CT) * BK;
-      if (c0 == 0 || kt == 0) a_tap(q);
+      // FWD: k = (64-channel block, tap, channel) — one tap per K-tile, the 9 taps of a block
+      // back to back; DGRAD: k = (tap of the class, channel)
+      const int ktg = ktg0 + kt;
+      const int q = MODE == EA_CONV_FWD ? ktg % 9 : ktg / CT;
+      const int c0 = MODE == EA_CONV_FWD ? (ktg / 9) * BK : (ktg - q * CT) * BK;
+      if (MODE == EA_CONV_FWD || c0 == 0 || kt == 0) a_tap(q);
 #pragma unroll
       for (int i = 0; i < ACH; ++i)
         __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)((const char*)A + (long)(cur[i] + c0) * 2),
@@ -1062,10 +1081,10 @@ __global__ __launch_bounds__(128 * WN, 1) void gemm_bf16_lds(GemmP p) {
   __syncthreads();  // every wave is done reading the operand ring: reuse it for the epilogue
   const EpiK ek = make_epik(p);
   switch (p.splitk > 1 ? EA_EPI_STORE : p.epi.kind) {
-    case EA_EPI_STORE: epi_wave<EA_EPI_STORE, MI, NJ>(p, ek, smem, z, zb, zh, m0 + wm, n0 + wn, lane, w, acc); break;
-    case EA_EPI_ACT: epi_wave<EA_EPI_ACT, MI, NJ>(p, ek, smem, z, zb, zh, m0 + wm, n0 + wn, lane, w, acc); break;
-    case EA_EPI_RESID: epi_wave<EA_EPI_RESID, MI, NJ>(p, ek, smem, z, zb, zh, m0 + wm, n0 + wn, lane, w, acc); break;
-    default: epi_wave<EA_EPI_DACT, MI, NJ>(p, ek, smem, z, zb, zh, m0 + wm, n0 + wn, lane, w, acc); break;
+    case EA_EPI_STORE: epi_wave<EA_EPI_STORE, MI, NJ>(p, ek, smem, z, zb, zh, m0 + wm, n0 + wn, lane, w, acc, sk); break;
+    case EA_EPI_ACT: epi_wave<EA_EPI_ACT, MI, NJ>(p, ek, smem, z, zb, zh, m0 + wm, n0 + wn, lane, w, acc, sk); break;
+    case EA_EPI_RESID: epi_wave<EA_EPI_RESID, MI, NJ>(p, ek, smem, z, zb, zh, m0 + wm, n0 + wn, lane, w, acc, sk); break;
+    default: epi_wave<EA_EPI_DACT, MI, NJ>(p, ek, smem, z, zb, zh, m0 + wm, n0 + wn, lane, w, acc, sk); break;
   }
   probe_end(p);
 }
@@ -1265,8 +1284,23 @@ EA_DEV void pipe_tile(const GemmP& p, char* smem, const bf16* A, const bf16* B, 
     const char* ak = abase + sl * astep;
     const char* bk = bbase + sl * bstep;
     if constexpr (MODE == EA_CONV_FWD || MODE == EA_CONV_DGRAD) {
-      const int ks = ksl0 + sl, q = ks / CS, c0 = (ks - q * CS) * BK;
-      if (c0 == 0 || sl == 0) a_tap(q);
+      // FWD: k = (64-channel block, tap, channel): 2 slices per tap, the 9 taps of a block back
+      // to back, so a tile's x1p footprint for one block stays in cache across its taps;
+      // DGRAD: k = (tap of the class, channel)
+      const int ks = ksl0 + sl;
+      int q, c0;
+      bool newtap;
+      if constexpr (MODE == EA_CONV_FWD) {
+        const int cb = ks / 18, r = ks - 18 * cb;
+        q = r >> 1;
+        c0 = cb * 64 + (r & 1) * BK;
+        newtap = (r & 1) == 0;
+      } else {
+        q = ks / CS;
+        c0 = (ks - q * CS) * BK;
+        newtap = c0 == 0;
+      }
+      if (newtap || sl == 0) a_tap(q);
 #pragma unroll
       for (int i = 0; i < ACH; ++i)
         __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)((const char*)A + (long)(cur[i] + c0) * 2),
@@ -1425,13 +1459,15 @@ constexpr int W1_TS = 264;                              // X image tap row: 256 
 constexpr int W1_IMG = 16 * W1_TS * 2;                  // one half (hi or lo), bytes
 constexpr int W1_SMEM = PipeT<256>::SMEM + 2 * W1_IMG;  // 152 KiB
 
-EA_DEV void w1_stage_x(const GemmP& p, char* xs, int m0) {
-  bf16* hi = (bf16*)xs;
-  bf16* lo = (bf16*)(xs + W1_IMG);
+// The conv1 input patches of the tile's 256 pixels: loaded into registers before the main
+// loop (w1_load_x; the loads land while it runs) and written to the LDS image after it
+// (w1_stage_x), so their latency is off the tile's critical path.
+EA_DEV void w1_load_x(const GemmP& p, int m0, float (&xv)[5]) {
   const int tid = threadIdx.x;
   const int row = tid >> 1, t0 = (tid & 1) * 5;  // 512 threads: 256 rows x 2 halves of taps 0..9
   const int m = m0 + row;
-  float xv[5] = {0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int u = 0; u < 5; ++u) xv[u] = 0.f;
   if (m < p.M) {
     const int a = p.g.a, e = p.g.e, nI = p.g.nI[a], nJ = p.g.nJ[e];
     const int bi = fdiv(m, nJ), j = m - bi * nJ;
@@ -1443,6 +1479,12 @@ EA_DEV void w1_stage_x(const GemmP& p, char* xs, int m0) {
       xv[u] = t < 9 ? xp[(t / 3) * p.w1F + t % 3] : 1.f;
     }
   }
+}
+EA_DEV void w1_stage_x(char* xs, const float (&xv)[5]) {
+  bf16* hi = (bf16*)xs;
+  bf16* lo = (bf16*)(xs + W1_IMG);
+  const int tid = threadIdx.x;
+  const int row = tid >> 1, t0 = (tid & 1) * 5;
 #pragma unroll
   for (int u = 0; u < 5; ++u) {
     const bf16 h = (bf16)xv[u];
@@ -1567,19 +1609,9 @@ __global__ __launch_bounds__(512, PipeT<BT>::OCC) void gemm_pipe(GemmP p) {
   __shared__ __attribute__((aligned(1024))) char smem[MODE == EA_CONV_DGRAD ? W1_SMEM : PC::SMEM];
   probe_start(p);
 
-  const int nt = p.tiles_m * p.tiles_n;
-  const int bid = blockIdx.x;
-  const int q8 = nt / 8, r8 = nt % 8, xcd = bid % 8;
-  const int t = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + bid / 8;
-  const int GM = 8;
-  const int grp = t / (GM * p.tiles_n);
-  const int gm0 = grp * GM;
-  const int gsz = min(GM, p.tiles_m - gm0);
-  const int tm = gm0 + (t % (GM * p.tiles_n)) % gsz;
-  const int tn = (t % (GM * p.tiles_n)) / gsz;
-  const int m0 = tm * BT, n0 = tn * BT;
-
-  const int z = blockIdx.z / p.splitk, sk = blockIdx.z % p.splitk;
+  const TileIdx ti = tile_index(p);
+  const int tm = ti.tm, m0 = ti.tm * BT, n0 = ti.tn * BT;
+  const int z = ti.z, sk = ti.sk;
   const int zb = z / p.nh, zh = z % p.nh;
   const bf16* A = (const bf16*)p.A + zb * p.sAb + zh * p.sAh;
   const bf16* B = (const bf16*)p.B + zb * p.sBb + zh * p.sBh;
@@ -1593,13 +1625,16 @@ __global__ __launch_bounds__(512, PipeT<BT>::OCC) void gemm_pipe(GemmP p) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
   diag_stamp(p, 0);
+  float w1x[5];
   if constexpr (MODE == EA_CONV_DGRAD) {
-    if (p.w1part) w1_stage_x(p, smem + PC::SMEM, m0);  // ordered by pipe_tile's first barrier
+    if (p.w1part) w1_load_x(p, m0, w1x);
   }
   pipe_tile<AK, BKM, MODE, BT>(p, smem, A, B, m0, n0, kbeg, kend, acc);
   diag_stamp(p, 1);
   if constexpr (MODE == EA_CONV_DGRAD) {
     if (p.w1part) {
+      w1_stage_x(smem + PC::SMEM, w1x);  // its own region: read across waves by w1_epilogue
+      __syncthreads();
       w1_epilogue(p, smem, m0, n0, wm, wn, lane, w, tm, acc);
       probe_end(p);
       return;
@@ -1607,10 +1642,10 @@ __global__ __launch_bounds__(512, PipeT<BT>::OCC) void gemm_pipe(GemmP p) {
   }
   const EpiK ek = make_epik(p);
   switch (p.splitk > 1 ? EA_EPI_STORE : p.epi.kind) {
-    case EA_EPI_STORE: epi_wave<EA_EPI_STORE, MI, 4>(p, ek, smem, z, zb, zh, m0 + wm, n0 + wn, lane, w, acc); break;
-    case EA_EPI_ACT: epi_wave<EA_EPI_ACT, MI, 4>(p, ek, smem, z, zb, zh, m0 + wm, n0 + wn, lane, w, acc); break;
-    case EA_EPI_RESID: epi_wave<EA_EPI_RESID, MI, 4>(p, ek, smem, z, zb, zh, m0 + wm, n0 + wn, lane, w, acc); break;
-    default: epi_wave<EA_EPI_DACT, MI, 4>(p, ek, smem, z, zb, zh, m0 + wm, n0 + wn, lane, w, acc); break;
+    case EA_EPI_STORE: epi_wave<EA_EPI_STORE, MI, 4>(p, ek, smem, z, zb, zh, m0 + wm, n0 + wn, lane, w, acc, sk); break;
+    case EA_EPI_ACT: epi_wave<EA_EPI_ACT, MI, 4>(p, ek, smem, z, zb, zh, m0 + wm, n0 + wn, lane, w, acc, sk); break;
+    case EA_EPI_RESID: epi_wave<EA_EPI_RESID, MI, 4>(p, ek, smem, z, zb, zh, m0 + wm, n0 + wn, lane, w, acc, sk); break;
+    default: epi_wave<EA_EPI_DACT, MI, 4>(p, ek, smem, z, zb, zh, m0 + wm, n0 + wn, lane, w, acc, sk); break;
   }
   if (p.diag) {
     __syncthreads();

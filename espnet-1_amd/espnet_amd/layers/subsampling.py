@@ -189,8 +189,9 @@ class SubsampleFn(torch.autograd.Function):
         lib.ea_conv1_fwd2(B, T, Fin, C, feats.data_ptr(), b.f("conv.0.weight").data_ptr(),
                           b.f("conv.0.bias").data_ptr(), x1p.data_ptr(), ops.dt(x1p),
                           0 if pos1 is None else pos1.data_ptr(), ops.stream())
+        # K order (64-channel block, tap, channel): (Co, Ci/64, 64, 9) -> (Co, Ci/64, 9, 64)
         w2 = empty(C, 9 * C, dtype=cd, device=dev)
-        ops.permute3(b.f("conv.2.weight"), w2, C, C, 9)  # (Co,Ci,9) -> (Co,9,Ci)
+        ops.permute3(b.f("conv.2.weight"), w2, C * C // 64, 64, 9)
         x2 = empty(P2, C, dtype=cd, device=dev)
         geo, _, _, _ = phase_geo(B, T1, F1, T2, F2, C, CONV_FWD)
         probe = ops.PROBE

@@ -71,8 +71,9 @@ int ea_gemm(int dtype, int a_kmajor, int b_kmajor, int M, int N, int K,
  * f1 = 2j+e stored dense as [b][i][j][C] (dims nI[a] x nJ[e]) at element offset
  * plane[a*2+e].  Every tap of every conv2 pixel is then one contiguous C-row, gathered by
  * the LDS-DMA loader (no im2col buffer):
- *  EA_CONV_FWD  : A[m = (b,t2,f2)][k = (kh,kw,c)] = x1p row; B = W2p [Co][9*C] K-major
- *                 (a_kmajor = b_kmajor = 1); out (P, Co).
+ *  EA_CONV_FWD  : A[m = (b,t2,f2)][k = (cb,kh,kw,c)] = x1p row (64-channel blocks cb, the 9
+ *                 taps of a block consecutive in k, c < 64 within the block); B = W2p
+ *                 [Co][C/64][9][64] K-major (a_kmajor = b_kmajor = 1); out (P, Co).
  *  EA_CONV_DGRAD: input gradient for one parity class (a, e) (sub-pixel decomposition of the
  *                 transposed conv): A[m = (b,i,j)][k = (tap of class, co)] = dY2 row of
  *                 (t2, f2) = ((2i+a-kh)/2, (2j+e-kw)/2), or one of 64 zero rows at `zero`
@@ -443,9 +444,11 @@ int ea_attn_fused_fwd2(int B, int H, int T1, int T2, int dk, const void* q, long
                        void* stream);
 /* Backward of ea_attn_fused_fwd(2): dq = d(q + bu) (flags bit 0, pp only: + d(q + bv), the
  * rel-pos path dBD·pp computed in-kernel), dk, dv (bf16), and optionally:
- *   dbd (pp only, or NULL): the band dbd[h][b][i][T-1-i+j] = gradient of the raw rel-pos term
- *     (q_i + bv)·pp[r] (bf16, rows written in full: 0 off the band; lddbd >= 2*T1-1, lddbd % 8
- *     == 0, 16-B aligned) — the linear_pos weight gradient's operand;
+ *   dbd (pp only, or NULL): the band dbd[h][b][i][bs + T1-1-i+j] = gradient of the raw rel-pos
+ *     term (q_i + bv)·pp[r], shifted by bs = (-T1) & 7 columns so that every workgroup's band
+ *     window starts on a 16-B boundary (bf16, rows written in full with 128-B segments: 0 off
+ *     the band and in columns [0, bs); lddbd >= 2*T1-1+bs, lddbd % 8 == 0, 16-B aligned) — the
+ *     linear_pos weight gradient's operand (a GEMM over columns [0, bs + 2*T1-1));
  *   bias_part (or NULL): [2][B*ceil(T1/64)][ldpart] f32, row (b*ceil(T1/64) + qb) holds the
  *     column sums over queries [64qb, 64qb+64) of d(q+bu) (plane 0) and, with pp, d(q+bv)
  *     (plane 1) at columns h*64 + c — reduce over rows for pos_bias_u / pos_bias_v gradients;
