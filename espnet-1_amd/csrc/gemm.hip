@@ -43,6 +43,7 @@ int g_gemm_stages = 2;
 unsigned long long* g_probe = nullptr;  // ea_gemm_set_probe
 unsigned long long* g_diag = nullptr;   // ea_gemm_set_diag
 int g_gemm_bm64 = 1;
+int g_gemm_bm32 = [] { const char* e = std::getenv("EA_GEMM_BM32"); return e ? std::atoi(e) : 1; }();
 int g_gemm_pipe = 0;  // ea_gemm_set_pipe bits: 1 = 256x256 tiles on gemm_pipe, 2 = 128x128 tiles too
 
 int launch_lds(GemmP& p, int a_k, int b_k, int nz, hipStream_t st, bool pipe128 = false) {
@@ -65,16 +66,17 @@ int g_force_bm = 0, g_force_bn = 0;
 void choose_tile(GemmP& p, int a_k, long nz) {
   struct Cfg { int bm, bn, occ; double t0, rcu; bool ak_only; };
   static const Cfg cfgs[] = {{256, 256, 1, 12.4, 4.49, false}, {128, 128, 2, 8.3, 2.9, false},
-                             {64, 128, 3, 6.8, 2.8, true}};
+                             {64, 128, 3, 6.8, 2.8, true}, {32, 128, 2, 6.0, 2.0, true}};
   p.bm = 128; p.bn = 128;
   if (g_force_bm) {
-    if (g_force_bm == 64 && !a_k) return;  // 64-row tiles need K-major A: keep 128 x 128
+    if (g_force_bm <= 64 && !a_k) return;  // 32/64-row tiles need K-major A: keep 128 x 128
     p.bm = g_force_bm; p.bn = g_force_bn;
     return;
   }
   double best = 1e300;
   for (const Cfg& c : cfgs) {
     if (c.ak_only && (!a_k || !g_gemm_bm64)) continue;
+    if (c.bm == 32 && !g_gemm_bm32) continue;
     const long tiles = (long)ea_cdiv(p.M, c.bm) * ea_cdiv(p.N, c.bn) * nz;
     const double rounds = (double)((tiles + 256L * c.occ - 1) / (256L * c.occ));
     const double per_cu = (double)((tiles + 255) / 256) * 2.0 * c.bm * c.bn * (double)p.K * 1e-6;
@@ -182,8 +184,8 @@ extern "C" int ea_gemm_set_pipe(int on) {
 
 extern "C" int ea_gemm_set_tile(int bm, int bn) {
   EA_ENTRY();
-  EA_CHECK_ARG((bm == 0 && bn == 0) || (bm == 64 && bn == 128) || (bm == 128 && bn == 128) ||
-               (bm == 256 && bn == 256));
+  EA_CHECK_ARG((bm == 0 && bn == 0) || (bm == 32 && bn == 128) || (bm == 64 && bn == 128) ||
+               (bm == 128 && bn == 128) || (bm == 256 && bn == 256));
   g_force_bm = bm;
   g_force_bn = bn;
   return 0;
@@ -268,7 +270,7 @@ static int gemm_impl(int dtype, int a_kmajor, int b_kmajor, int M, int N, int K,
       pipe128 = (epi128 & 2) != 0;
     }
   }
-  if (p.bm == 64 && !a_kmajor) return EA_ERR_BAD_ARG;
+  if (p.bm <= 64 && !a_kmajor) return EA_ERR_BAD_ARG;
   p.tiles_m = ea_cdiv(M, p.bm);
   p.tiles_n = ea_cdiv(N, p.bn);
   const int KT = dtype == EA_BF16 ? KCfg<bf16>::KT : KCfg<float>::KT;
@@ -286,7 +288,9 @@ static int gemm_impl(int dtype, int a_kmajor, int b_kmajor, int M, int N, int K,
       while (splitk > 1 && (long)splitk * M * N > ws_elems) --splitk;
       splitk = max(splitk, 1);
     }
-  } else if (workspace && tiles < 200 && K >= 16 * KT && K >= 1024) {
+  } else if (workspace && tiles < 200 && K >= 16 * KT && K >= 1024 && (long)p.tiles_m * p.tiles_n * nz < 128) {
+    // (a grid already covering half the CUs — e.g. 32-row tiles of a decoder GEMM — runs
+    // unsplit: the partial slabs and the combine pass cost more than the extra blocks gain)
     splitk = (int)((384 + tiles - 1) / tiles);
     splitk = min(splitk, K / (4 * KT));
     splitk = min(splitk, 16);

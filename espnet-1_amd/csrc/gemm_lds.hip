@@ -15,7 +15,10 @@ int launch_lds_dense(GemmP& p, int a_k, int b_k, dim3 grid, hipStream_t st) {
   else if (b_k) EA_GL(BMV, BNV, false, true, S);       \
   else EA_GL(BMV, BNV, false, false, S);
   static const int s64 = [] { const char* e = std::getenv("EA_LDS64_STAGES"); return e ? std::atoi(e) : 3; }();
-  if (p.bm == 64) {
+  if (p.bm == 32) {  // small-M GEMMs (decoder tokens, positional rows): twice the blocks of 64x128
+    if (b_k) EA_GL(32, 128, true, true, 3);
+    else EA_GL(32, 128, true, false, 3);
+  } else if (p.bm == 64) {
     if (s64 == 3) {
       if (b_k) EA_GL(64, 128, true, true, 3);
       else EA_GL(64, 128, true, false, 3);

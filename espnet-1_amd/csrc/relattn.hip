@@ -396,6 +396,13 @@ EA_DEV bf16x8 dst_frag(const char* img, int kb, int lane) {
   }
   return out.v;
 }
+// dS band image [16 queries][96 band columns] bf16, 192-B rows, 16-B chunk c of row r at
+// c ^ ((r >> 2) & 3) (conflict-free b128 A-fragment reads)
+EA_DEV int band_off(int r, int c) { return r * 192 + ((((c >> 3) ^ ((r >> 2) & 3))) << 4) + (c & 7) * 2; }
+EA_DEV bf16x8 band_frag(const char* img, int ks, int lane) {
+  const int r = lane & 15, c = ks * 4 + (lane >> 4);
+  return *(const bf16x8*)(img + r * 192 + ((c ^ ((r >> 2) & 3)) << 4));
+}
 EA_DEV uint32_t pack_bf16x2(float lo, float hi) {
   union { bf16 h[2]; uint32_t u; } x;
   x.h[0] = (bf16)lo;
@@ -407,13 +414,11 @@ EA_DEV uint32_t pack_bf16x2(float lo, float hi) {
 constexpr int Q_K = 0, Q_V = Q_K + KC * 128, Q_P = Q_V + KC * 128;  // K, V chunk, band (144 rows)
 constexpr int Q_D = Q_P + 144 * 128;                                // D_i, lse_i (64 each)
 constexpr int Q_WS = Q_D + 2 * QB * 4;                              // per-wave scratch
-constexpr int Q_XSZ = 16 * F_BDLD * 4;                              // BD gather
-constexpr int Q_RING = Q_XSZ + 64 * 32;                             // after the dS^T image:
-constexpr int Q_WSZ = Q_RING + 2 * 16 * 128;                        //   the band ring, 2 km halves
-constexpr int Q_RED = Q_WS;                                         // column-sum exchange (after the loop)
-constexpr int Q_LDS = Q_WS + NWAVE * Q_WSZ;
-static_assert(Q_XSZ % 16 == 0 && 2 * NWAVE * DK * 4 <= Q_XSZ, "column sums fit wave 0's gather scratch");
-static_assert(2 * Q_LDS <= 160 * 1024, "two workgroups per CU");
+constexpr int Q_XSZ = 16 * F_BDLD * 4;                              // BD gather | dS band image
+constexpr int Q_WSZ = Q_XSZ + 64 * 32;                              // + dS^T image
+constexpr int Q_RED = Q_WS + NWAVE * Q_WSZ;                         // column-sum exchange
+constexpr int Q_LDS = Q_RED + 2 * NWAVE * DK * 4;
+static_assert(Q_XSZ >= 16 * 192 && Q_XSZ % 16 == 0, "band image fits the gather scratch");
 static_assert(3 * QB * 128 <= Q_D, "setup images fit the chunk space");
 
 // rows [r0, r0+nrows) of (src [+ bias]) into a km image, also written to out (if non-null)
@@ -450,8 +455,8 @@ __global__ __launch_bounds__(256, 2) void attn_bwdq_kernel(AttnP a) {
   const bool with_dqv = REL && (a.flags & 1);
   char* ws = sm + Q_WS + w * Q_WSZ;
   float* bds = (float*)ws;
+  char* band = ws;                // dS on its band (after the gather has read bds)
   char* dst = ws + Q_XSZ;
-  char* ring = ws + Q_RING;
   float* Dv = (float*)(sm + Q_D);
   float* Lv = Dv + QB;
 
@@ -510,40 +515,22 @@ __global__ __launch_bounds__(256, 2) void attn_bwdq_kernel(AttnP a) {
   const float sl2 = a.scale * LOG2E;
   const int kend = a.causal ? min(kl, i0 + QB) : kl;
   const int nch = (kend + KC - 1) / KC;
-  // The band ring (rel-pos): dS of row il, key jl of chunk j0 sits at dbd column
-  // e + 15 - il + jl, e = ebase + j0 the chunk's window start (the same for the wave's 16 rows,
-  // a multiple of 8 thanks to the band shift bs).  The ring holds window columns [e, e+128) as
-  // two 16 x 64 km halves: after chunk j0 the low half [e, e+64) is complete (later chunks
-  // start at column e + 64 + 15 - il >= e + 64), so it feeds the d(q+v) MFMA once, goes to
-  // HBM as whole 128-B row segments and is cleared to become the next chunk's high half.
-  const bool use_ring = REL && (with_dqv || a.dbd != nullptr);
-  bf16* dbd_w = REL && a.dbd ? a.dbd + (((long)h * a.B + b) * a.T1 + i0 + 16 * w) * a.lddbd : nullptr;
-  const int bs = (-a.T1) & 7;                         // band shift (include/espnet_amd.h)
-  const int ebase = a.T1 - 16 - i0 - 16 * w + bs;     // window start of chunk 0
-  const int rowv = min(16, a.T1 - (i0 + 16 * w));     // valid rows of the wave (<= 0: none)
-  const uint4 zero4 = make_uint4(0u, 0u, 0u, 0u);
-  // 16 x 8 chunks of a half: lane's pieces q = lane + 64u -> row q >> 3, chunk q & 7
-  auto emit = [&](const char* half, int e) {
-    if (!dbd_w) return;
-#pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      const int q = lane + 64 * u, row = q >> 3, col = e + 8 * (q & 7);
-      const uint4 v = *(const uint4*)(half + km_off(row, q & 7));
-      if (row < rowv && col >= 0 && col < a.lddbd) *(uint4*)(dbd_w + (long)row * a.lddbd + col) = v;
+  bf16* dbd_h = REL && a.dbd ? a.dbd + ((long)h * a.B + b) * a.T1 * a.lddbd : nullptr;
+  if (dbd_h) {
+    // zeros off the part of each row the chunk loop writes (r < T-1-i, r >= T-1-i+jcov), in
+    // whole 8-column segments (lddbd % 8 == 0, 16-B aligned rows): a segment straddling the
+    // band edge is zeroed in full and its band columns are rewritten by this same wave's chunk
+    // stores, which the loop's first __syncthreads (vmcnt(0)) orders after these
+    const int jcov = min(a.T2, nch * KC);
+    const uint4 zero = make_uint4(0u, 0u, 0u, 0u);
+    for (int il = 0; il < 16; ++il) {
+      const int i = i0 + 16 * w + il;
+      if (i >= a.T1) break;
+      bf16* drow = dbd_h + (long)i * a.lddbd;
+      const int lo = a.T1 - 1 - i, hi = lo + jcov;
+      for (int c0 = 8 * lane; c0 < a.lddbd; c0 += 512)
+        if (c0 < lo || c0 + 8 > hi) *(uint4*)(drow + c0) = zero;
     }
-  };
-  auto zero_cols = [&](int c0, int c1) {  // columns [c0, c1) of the valid rows, 8 at a time
-    if (!dbd_w || c1 <= c0 || rowv <= 0) return;
-    const int nc = (c1 - c0) >> 3;
-    for (int q = lane; q < rowv * nc; q += 64) {
-      const int row = q / nc;
-      *(uint4*)(dbd_w + (long)row * a.lddbd + c0 + 8 * (q - row * nc)) = zero4;
-    }
-  };
-  if (use_ring) {
-#pragma unroll
-    for (int u = 0; u < 4; ++u) *(uint4*)(ring + (lane + 64 * u) * 16) = zero4;
-    zero_cols(0, max(0, ebase));
   }
   const bool use_mask = a.p > 0.f && a.dmask != nullptr;
   const uint32_t* mrow = a.dmask + ((long)z * a.T1 + ibase) * a.ldm;  // rows ibase + r (< T1)
@@ -630,18 +617,23 @@ __global__ __launch_bounds__(256, 2) void attn_bwdq_kernel(AttnP a) {
         const float kp = (((t < 2 ? mw[r].x : mw[r].y) >> (16 * (t & 1) + lc)) & 1u) ? dsc : 0.f;
         s[t][r] = (P * a.scale) * fmaf(dp[t][r], kp, -Dr[r]);
       }
-    // dS^T image (4 queries per 8-B write) and (rel-pos) the ring, window column 15-il+jl
-    char* rlo = ring + ((j0 / KC) & 1) * 2048;  // window columns [0, 64) of this chunk
-    char* rhi = ring + (((j0 / KC) & 1) ^ 1) * 2048;
+    // dS^T image (4 queries per 8-B write) and (rel-pos) the band image, column 15-il+jl
+    if (with_dqv) {
+      lds_fence();  // the gather above has read bds
+      const uint4 zero = make_uint4(0u, 0u, 0u, 0u);
+#pragma unroll
+      for (int c = 0; c < 3; ++c) *(uint4*)(band + (c * 64 + lane) * 16) = zero;
+      lds_fence();
+    }
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
       const uint2 v = make_uint2(pack_bf16x2(s[t][0], s[t][1]), pack_bf16x2(s[t][2], s[t][3]));
       *(uint2*)(dst + (16 * t + lc) * 32 + g * 8) = v;
-      if (use_ring) {
+      if (with_dqv) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const int il = 4 * g + r, c = 15 - il + 16 * t + lc;
-          *(bf16*)((c < 64 ? rlo : rhi) + km_off(il, (c & 63) >> 3) + (c & 7) * 2) = (bf16)s[t][r];
+          const int il = 4 * g + r;
+          *(bf16*)(band + band_off(il, 15 - il + 16 * t + lc)) = (bf16)s[t][r];
         }
       }
     }
@@ -652,36 +644,26 @@ __global__ __launch_bounds__(256, 2) void attn_bwdq_kernel(AttnP a) {
 #pragma unroll
       for (int n = 0; n < 4; ++n) dqu[n] = mfma(af, km_frag_tr(sm + Q_K, 32 * ks, 16 * n, lane), dqu[n]);
     }
-    if (use_ring) {
-      // the complete low half: d(q+v) += band . p (positional rows pb + [0, 64) of this chunk's
-      // staging), then to HBM, then cleared
-      if (with_dqv) {
+    if (with_dqv) {
 #pragma unroll
-        for (int ks = 0; ks < 2; ++ks) {
-          const bf16x8 af = km_frag(rlo, 0, ks, lane);
+      for (int ks = 0; ks < 3; ++ks) {
+        const bf16x8 af = band_frag(band, ks, lane);
 #pragma unroll
-          for (int n = 0; n < 4; ++n) dqv[n] = mfma(af, km_frag_tr(sm + Q_P, pb + 32 * ks, 16 * n, lane), dqv[n]);
-        }
+        for (int n = 0; n < 4; ++n) dqv[n] = mfma(af, km_frag_tr(sm + Q_P, pb + 32 * ks, 16 * n, lane), dqv[n]);
       }
-      emit(rlo, ebase + j0);
-      lds_fence();  // the reads above before the clear
-#pragma unroll
-      for (int u = 0; u < 2; ++u) *(uint4*)(rlo + (lane + 64 * u) * 16) = zero4;
     }
-  }
-  if (use_ring) {
-    // the last chunk's tail (window columns [64, 79-il) of it = [0, 15) of the next): its
-    // positional rows pb + 64 + [0, 32) are still staged; then zeros to the end of the rows
-    char* rlo = ring + (nch & 1) * 2048;
-    lds_fence();
-    if (with_dqv && nch > 0) {
-      const bf16x8 af = km_frag(rlo, 0, 0, lane);
+    if (dbd_h) {  // dBD_raw[h][b][i][T-1-i+j] = dS
+      const bool full = j0 + KC <= a.T2;
 #pragma unroll
-      for (int n = 0; n < 4; ++n) dqv[n] = mfma(af, km_frag_tr(sm + Q_P, pb + 64, 16 * n, lane), dqv[n]);
+      for (int r = 0; r < 4; ++r) {
+        const int i = ibase + r;
+        if (i >= a.T1) continue;
+        bf16* drow = dbd_h + (long)i * a.lddbd + (a.T1 - 1 - i) + j0 + lc;
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+          if (full || j0 + 16 * t + lc < a.T2) drow[16 * t] = (bf16)s[t][r];
+      }
     }
-    const int efin = ebase + nch * KC;
-    emit(rlo, efin);
-    zero_cols(max(0, efin + 64), (int)a.lddbd);
   }
   // dQ (bf16) = dS.K (+ dBD.p); column sums of both terms over this block's rows
 #pragma unroll
@@ -693,8 +675,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwdq_kernel(AttnP a) {
     for (int n = 0; n < 4; ++n) qrow[16 * n + lc] = (bf16)(dqu[n][r] + (with_dqv ? dqv[n][r] : 0.f));
   }
   if (a.bias_part) {
-    float* red = (float*)(sm + Q_RED);  // [2][NWAVE][64], over wave 0's gather scratch
-    __syncthreads();                    // every wave is past its chunk loop
+    float* red = (float*)(sm + Q_RED);  // [2][NWAVE][64]
 #pragma unroll
     for (int n = 0; n < 4; ++n) {
       float su = (dqu[n][0] + dqu[n][1]) + (dqu[n][2] + dqu[n][3]);
@@ -1003,7 +984,7 @@ extern "C" int ea_attn_fused_bwd2(int B, int H, int T1, int T2, int dk, const vo
   EA_ENTRY();
   EA_CHECK_ARG(dk == DK && B >= 1 && H >= 1 && T1 >= 1 && T2 >= 1);
   EA_CHECK_ARG(!pp || (T1 == T2 && bv != nullptr));
-  EA_CHECK_ARG(!dbd || (pp && lddbd >= 2 * T1 - 1 + ((-T1) & 7) && lddbd % 8 == 0 && (uintptr_t)dbd % 16 == 0));
+  EA_CHECK_ARG(!dbd || (pp && lddbd >= 2 * T1 - 1 && lddbd % 8 == 0 && (uintptr_t)dbd % 16 == 0));
   EA_CHECK_ARG(ldq % 8 == 0 && ldk % 8 == 0 && ldv % 8 == 0 && ldo % 8 == 0 && lddo % 8 == 0 &&
                (!pp || ldp % 8 == 0) && (!qv_out || (pp && ldqv % 8 == 0)));
   EA_CHECK_ARG(!bias_part || ldpart >= (long)H * DK);

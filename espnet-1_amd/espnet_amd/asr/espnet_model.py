@@ -140,13 +140,26 @@ class ESPnetASRModel(AbsESPnetModel):
         self.seed = 0
         self._step = 0
         # loading weights into a prepared model writes the f32 arena (the Parameters are its
-        # views); under AMP the GEMMs read the bf16 shadow, so refresh it after every load
-        self.register_load_state_dict_post_hook(ESPnetASRModel._refresh_shadow_after_load)
+        # views); under AMP the GEMMs read the bf16 shadow, so it is refreshed after every load
+        # — of the whole model or of any submodule (model.encoder.load_state_dict, as the
+        # reference's init_param / load_pretrained_model do; prepare() hooks every module).
+        # torch runs the loaded module's pre-hook first and its post-hook last (after its
+        # children's), so the shadow is refreshed once per load_state_dict call.  In-place
+        # edits of parameters (e.g. under torch.no_grad()) are seen by no hook: call
+        # arena.refresh_shadow() after them.
+        self.__dict__["_load_root"] = None  # not a submodule attribute
+        self.register_load_state_dict_pre_hook(self._load_pre_hook)
+        self.register_load_state_dict_post_hook(self._load_post_hook)
 
-    @staticmethod
-    def _refresh_shadow_after_load(module, incompatible_keys):
-        if module.arena is not None:
-            module.arena.refresh_shadow()
+    def _load_pre_hook(self, module, *args, **kwargs):
+        if self.__dict__.get("_load_root") is None:
+            self.__dict__["_load_root"] = module
+
+    def _load_post_hook(self, module, incompatible_keys):
+        if module is self.__dict__.get("_load_root"):
+            self.__dict__["_load_root"] = None
+            if self.arena is not None:
+                self.arena.refresh_shadow()
 
     # ------------------------------------------------------------------ runtime
     def arena_groups(self):
@@ -171,6 +184,12 @@ class ESPnetASRModel(AbsESPnetModel):
                     m._buffers[k] = v.to(device)
         self.arena = ParamArena(self, device, self.arena_groups(), shadow_dtype=cd)
         self.compute_dtype = cd
+        if not self.__dict__.get("_sub_hooks", False):
+            for m in self.modules():
+                if m is not self:
+                    m.register_load_state_dict_pre_hook(self._load_pre_hook)
+                    m.register_load_state_dict_post_hook(self._load_post_hook)
+            self.__dict__["_sub_hooks"] = True
         self._anchor = torch.zeros(1, device=device, requires_grad=True)
         self.encoder.bind(self.arena, "encoder.", cd, self._anchor)
         if self.decoder is not None:

@@ -178,17 +178,34 @@ def join_aux():
 
 
 GRAD_READY = None  # callable(prefix): a block's parameter gradients are final (DP overlap)
+# single process, EA_STREAM_WGRAD=N > 0: every N finished blocks, the deferred weight
+# gradients / reductions queued so far are launched on the weight-gradient side stream (one
+# grouped GEMM per flush) to overlap the backward of the blocks below.  Measured slower on the
+# C3 step (1599-1605 utt/s at N=1, 1588 at N=2, vs 1616-1618 with one flush at the end:
+# profiles/r3_stream_wgrad_ab.txt — the grouped tiles take whole CUs from the main stream's
+# chip-filling kernels), so the default (0) flushes once at the end of the pass
+STREAM_WGRAD = int(os.environ.get("EA_STREAM_WGRAD", "0"))
+_STREAM_COUNT = [0]
 
 
 def grad_ready(bound):
-    """A block's backward is done.  Single process: its parameter gradients (some written on
-    the side stream) are final once the main stream has joined the side stream.  Data
-    parallel (GRAD_READY set): the hook flushes the deferred weight gradients and issues the
-    bucket all-reduces from the side stream, so the main stream goes on with the backward."""
+    """A block's backward is done.  Data parallel (GRAD_READY set): the hook flushes the
+    deferred weight gradients and issues the bucket all-reduces from the side stream, so the
+    main stream goes on with the backward.  Single process: the deferred queues are flushed
+    onto the side stream every STREAM_WGRAD blocks (deferred_wgrad's exit joins the side
+    stream before anything reads the gradients); with nothing deferred, the main stream
+    joins the side stream here."""
     if GRAD_READY is not None:
         GRAD_READY(bound.prefix)
-    else:
-        join_wgrad()
+        return
+    if STREAM_WGRAD > 0 and OVERLAP_WGRAD and (WGRAD_Q.active or REDUCE_Q.active) and torch.cuda.is_available():
+        _STREAM_COUNT[0] += 1
+        if _STREAM_COUNT[0] >= STREAM_WGRAD:
+            _STREAM_COUNT[0] = 0
+            with wgrad(*deferred_tensors()):
+                flush_deferred()
+        return
+    join_wgrad()
 
 
 def dt(t: torch.Tensor) -> int:
@@ -318,7 +335,15 @@ def linear_dw(dy, x, dw, *, accumulate=False, post=None):
 
 # ----------------------------------------------------------------------------- deferred weight gradients
 DEFER_WGRAD = os.environ.get("EA_DEFER_WGRAD", "1") != "0"
+# bytes the deferred queues may keep alive (queued operands / partial buffers) before they
+# flush early: a pass whose queued dY / X / LayerNorm partials exceed it launches what it has
+# and continues (C3 queues ~3.5 GB per backward, under the default)
+DEFER_BUDGET = int(float(os.environ.get("EA_DEFER_BUDGET_MB", "8192")) * 2 ** 20)
 _GWS = {}
+
+
+def _nbytes(t):
+    return t.numel() * t.element_size()
 
 
 class WgradQueue:
@@ -334,6 +359,7 @@ class WgradQueue:
         self.active = False
         self.items = []
         self.posts = []
+        self.pending = 0  # bytes of queued dY / X kept alive
 
     def add(self, dy, x, dw, *, M, N, K, lda, ldb, ldc, beta, post=None) -> bool:
         if not (dy.dtype == torch.bfloat16 and x.dtype == torch.bfloat16 and dw.dtype == torch.float32):
@@ -350,6 +376,9 @@ class WgradQueue:
         self.items.append((K, dy, x, dw, M, N, lda, ldb, ldc, beta, lo, hi))
         if post is not None:
             self.posts.append(post)
+        self.pending += _nbytes(dy) + _nbytes(x)
+        if self.pending > DEFER_BUDGET:
+            self.flush()
         return True
 
     def flush(self):
@@ -360,6 +389,7 @@ class WgradQueue:
         posts = self.posts
         self.items = []
         self.posts = []
+        self.pending = 0
         n = len(items)
         cur = torch.cuda.current_stream()
         for it in items:  # operands may come from another stream's pool: keep them until this launch ran
@@ -416,6 +446,12 @@ class ReduceQueue:
         self.colsums = []
         self.reduces = []
         self.spans = []
+        self.pending = 0  # bytes of queued inputs / partial buffers kept alive
+
+    def _account(self, t):
+        self.pending += _nbytes(t)
+        if self.pending > DEFER_BUDGET:
+            self.flush()
 
     def _claim(self, out, n):
         lo = out.data_ptr()
@@ -432,11 +468,13 @@ class ReduceQueue:
             return False
         self._claim(out, n)
         self.colsums.append((x, rows, n, ld, out, accumulate))
+        self._account(x)
         return True
 
     def add_reduce(self, part, nparts, n, stride, out, accumulate=True):
         self._claim(out, n)
         self.reduces.append((part, nparts, n, stride, out, accumulate))
+        self._account(part)
 
     def tensors(self):
         return [c[0] for c in self.colsums] + [r[0] for r in self.reduces]
@@ -446,6 +484,7 @@ class ReduceQueue:
             return
         colsums, reduces = self.colsums, list(self.reduces)
         self.colsums, self.reduces, self.spans = [], [], []
+        self.pending = 0
         cur = torch.cuda.current_stream()
         for t in [c[0] for c in colsums] + [r[0] for r in reduces]:
             t.record_stream(cur)
@@ -501,8 +540,11 @@ class deferred_wgrad:
 
     def __exit__(self, *exc):
         WGRAD_Q.active, REDUCE_Q.active = self.prev
+        _STREAM_COUNT[0] = 0
         if exc[0] is None:
             flush_deferred()
+            if GRAD_READY is None:
+                join_wgrad()  # gradients flushed onto the side stream during the pass are final
         else:
             WGRAD_Q.items, WGRAD_Q.posts = [], []
             REDUCE_Q.colsums, REDUCE_Q.reduces, REDUCE_Q.spans = [], [], []
@@ -553,7 +595,12 @@ def layernorm_bwd(dy, x, gamma, mean, rstd, dx, dgamma, dbeta, accumulate=True, 
     if REDUCE_Q.active and rows > 0 and dbeta.data_ptr() == dgamma.data_ptr() + 4 * d:
         # dx now; the (dgamma | dbeta) row-block partials go to a buffer of their own and are
         # summed with the pass's other parameter-gradient reductions (REDUCE_Q.flush)
-        nparts_max = max((rows + 15) // 16, 128)
+        # the vectorized kernel's block count (16-row blocks; ln_bwd_impl), the generic paths'
+        # at most 128 blocks
+        vec8 = (d % 8 == 0 and d <= 1024 and lddy % 8 == 0 and ldx % 4 == 0 and lddx % 4 == 0
+                and x.data_ptr() % 16 == 0 and dy.data_ptr() % 16 == 0 and dx.data_ptr() % 16 == 0
+                and gamma.data_ptr() % 16 == 0)
+        nparts_max = (rows + 15) // 16 if vec8 else max((rows + 15) // 16, 128)
         part = torch.empty(nparts_max * (3 if drop is not None else 2) * d, dtype=torch.float32, device=x.device)
         np_ = ctypes.c_int(0)
         if drop is not None:

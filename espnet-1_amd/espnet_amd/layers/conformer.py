@@ -310,13 +310,10 @@ class ConformerBlockFn(torch.autograd.Function):
         ops.linear_dx(dv, b.w(A + "linear_out.weight"), dO)
         dqkv = empty(N, 3 * d, dtype=cd, device=dev)
         ldbd = rup(P2, 8)
-        bs = 0  # band shift: the fused kernel's band starts at column bs = (-T) & 7
         if s_core[0] == "fused":
             # dq includes the q+v path (dBD.p, in-kernel); dbd rows written in full; pos_bias_u /
             # pos_bias_v gradients from per-block column sums of the two dq terms
             _, lse, dmask, ldm = s_core
-            bs = (-T) & 7
-            ldbd = rup(P2 + bs, 8)
             dbd = empty(H * B * T * ldbd, dtype=cd, device=dev)
             qv = empty(N, d, dtype=cd, device=dev)  # q + v, for the linear_pos weight gradient
             nqb = (T + 63) // 64
@@ -345,14 +342,12 @@ class ConformerBlockFn(torch.autograd.Function):
             ops.colsum(dqv, b.g(A + "pos_bias_v", shape=(d,)))
             lib.ea_add_2d(N, d, dqv.data_ptr(), ops.dt(dqv), d, dqkv.data_ptr(), ops.dt(dqkv), 3 * d, 1.0,
                           ops.stream())
-        # linear_pos: dp[h] = sum_b dBD[h][b]^T qv[b, :, h]  (K = B*T), dWpos = dp^T pos.  The
-        # GEMM runs over band columns [0, bs + P2); rows [0, bs) of its output (all-zero band
-        # columns ahead of the shifted band) are dropped
+        # linear_pos: dp[h] = sum_b dBD[h][b]^T qv[b, :, h]  (K = B*T), dWpos = dp^T pos
         with ops.wgrad(dbd, qv, pos):
-            dpp = empty(P2 + bs, d, dtype=cd, device=dev)
-            ops.gemm(dbd, qv, dpp, M=P2 + bs, N=dk, K=B * T, a_kmajor=0, b_kmajor=0, lda=ldbd, ldb=d, ldc=d,
+            dpp = empty(P2, d, dtype=cd, device=dev)
+            ops.gemm(dbd, qv, dpp, M=P2, N=dk, K=B * T, a_kmajor=0, b_kmajor=0, lda=ldbd, ldb=d, ldc=d,
                      batch=1, nh=H, sA=(0, B * T * ldbd), sB=(0, dk), sC=(0, dk))
-            ops.linear_dw(dpp[bs:], pos, b.g(A + "linear_pos.weight"), accumulate=True)
+            ops.linear_dw(dpp, pos, b.g(A + "linear_pos.weight"), accumulate=True)
         del dbd
         qkv_w = b.w(A + "linear_q.weight", A + "linear_k.weight", A + "linear_v.weight", shape=(3 * d, d))
         with ops.wgrad(dqkv, xn2):

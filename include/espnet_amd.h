@@ -121,7 +121,7 @@ int ea_conv1_wgrad_reduce(int ntiles, int C, const float* part, float* dw, float
  * Process-wide; for A/B measurements. */
 int ea_gemm_set_pipeline(int stages);
 
-/* Pin the bf16 LDS-DMA GEMM output tile (bm x bn in {64x128, 128x128, 256x256});
+/* Pin the bf16 LDS-DMA GEMM output tile (bm x bn in {32x128, 64x128, 128x128, 256x256});
  * 0,0 = automatic choice by grid size.  Process-wide; for tests and tuning. */
 int ea_gemm_set_tile(int bm, int bn);
 /* Route 256x256-tile bf16 GEMMs to the pipelined kernel (gemm_pipe: 4-slot ring of 32-deep
@@ -444,11 +444,9 @@ int ea_attn_fused_fwd2(int B, int H, int T1, int T2, int dk, const void* q, long
                        void* stream);
 /* Backward of ea_attn_fused_fwd(2): dq = d(q + bu) (flags bit 0, pp only: + d(q + bv), the
  * rel-pos path dBD·pp computed in-kernel), dk, dv (bf16), and optionally:
- *   dbd (pp only, or NULL): the band dbd[h][b][i][bs + T1-1-i+j] = gradient of the raw rel-pos
- *     term (q_i + bv)·pp[r], shifted by bs = (-T1) & 7 columns so that every workgroup's band
- *     window starts on a 16-B boundary (bf16, rows written in full with 128-B segments: 0 off
- *     the band and in columns [0, bs); lddbd >= 2*T1-1+bs, lddbd % 8 == 0, 16-B aligned) — the
- *     linear_pos weight gradient's operand (a GEMM over columns [0, bs + 2*T1-1));
+ *   dbd (pp only, or NULL): the band dbd[h][b][i][T-1-i+j] = gradient of the raw rel-pos term
+ *     (q_i + bv)·pp[r] (bf16, rows written in full: 0 off the band; lddbd >= 2*T1-1, lddbd % 8
+ *     == 0, 16-B aligned) — the linear_pos weight gradient's operand;
  *   bias_part (or NULL): [2][B*ceil(T1/64)][ldpart] f32, row (b*ceil(T1/64) + qb) holds the
  *     column sums over queries [64qb, 64qb+64) of d(q+bu) (plane 0) and, with pp, d(q+bv)
  *     (plane 1) at columns h*64 + c — reduce over rows for pos_bias_u / pos_bias_v gradients;

@@ -23,7 +23,7 @@ klen = torch.full((B,), T, dtype=torch.long, device=dev)
 O = torch.empty(B, T, d, dtype=bf, device=dev)
 lse = torch.empty(B * H * T, device=dev)
 dq, dk, dv = torch.empty_like(q), torch.empty_like(k), torch.empty_like(v)
-ldbd = (2 * T - 1 + ((-T) & 7) + 7) // 8 * 8
+ldbd = (2 * T - 1 + 7) // 8 * 8
 dbd = torch.empty(H * B * T * ldbd, dtype=bf, device=dev)  # written in full by the kernel
 ldm = 2 * ((T + 63) // 64)
 dmask = torch.empty(B * H * T * ldm, dtype=torch.int32, device=dev)

@@ -67,7 +67,7 @@ def run_fused(q, k, v, u, vb, pp, klen, causal, H, dO, p=0.0, seed=0):
     dq = torch.empty_like(q)
     dkk = torch.empty_like(k)
     dv = torch.empty_like(v)
-    ldbd = (2 * T1 - 1 + ((-T1) & 7) + 7) // 8 * 8
+    ldbd = (2 * T1 - 1 + 7) // 8 * 8
     # NaN-filled: the kernel writes every band row in full (zeros off the band)
     dbd = torch.full((H * B * T1 * ldbd,), float("nan"), dtype=bf, device=DEV) if pp is not None else None
     # the hash path (no keep-bit mask), dq without the rel-pos term (flags 0)
@@ -76,16 +76,6 @@ def run_fused(q, k, v, u, vb, pp, klen, causal, H, dO, p=0.0, seed=0):
                    dk=dkk, lddk=d, dv=dv, lddv=d, dbd=dbd, ldbd=ldbd)
     torch.cuda.synchronize()
     return O, dq, dkk, dv, dbd, ldbd
-
-
-def fused_band(dbd, H, B, T, ldbd):
-    """The fused kernel's band rows dBD[h][b][i][r], r < 2T-1: columns bs + r of its output,
-    bs = (-T) & 7 (include/espnet_amd.h); the bs leading columns must be written zeros."""
-    bs = (-T) & 7
-    rows = dbd.view(H, B, T, ldbd)
-    assert bs == 0 or float(rows[..., :bs].float().abs().max()) == 0.0
-    assert not torch.isnan(rows.float()).any()
-    return rows[..., bs: bs + 2 * T - 1]
 
 
 def _inputs(B, H, T1, T2, rel, seed=0):
@@ -129,7 +119,7 @@ def test_fused_attention_matches_fp32_reference(B, H, T1, T2, rel, causal, klens
     # rel-pos: dq from the kernel is the (q+u) path; the (q+v) path leaves through dbd:
     # dq_total = dq + dBD . pp_h, d pp_h = dBD^T . (q+v)
     d = H * 64
-    dbd4 = fused_band(dbd, H, B, T1, ldbd).float()
+    dbd4 = dbd.view(H, B, T1, ldbd)[..., : 2 * T1 - 1].float()
     pph = pp.float().view(2 * T1 - 1, H, 64).permute(1, 0, 2)  # (H, R, 64)
     dq_v = torch.einsum("hbir,hrc->bihc", dbd4, pph).reshape(B, T1, d)
     assert _rel(dq.float() + dq_v, qf.grad) < 2e-2
@@ -178,7 +168,7 @@ def test_fused_matches_unfused_with_dropout():
     assert _rel(dk.view(N, d), dk2) < 2e-2
     assert _rel(dv.view(N, d), dv2) < 2e-2
     band = dbd2.view(H, B, T, ldbd)[..., :P2]
-    assert _rel(fused_band(dbd, H, B, T, ldbd), band) < 2e-2
+    assert _rel(dbd.view(H, B, T, ldbd)[..., :P2], band) < 2e-2
 
 
 @pytest.mark.parametrize("B,H,T,klens,p", [
@@ -222,7 +212,7 @@ def test_fused_bwd2_rel_terms(B, H, T, klens, p):
     assert torch.equal(O2, O) and torch.equal(dk, dk1) and torch.equal(dv, dv1) and torch.equal(dbd, dbd1)
     assert torch.equal(qv, (q.float() + vb.view(1, 1, d)).to(bf))
     # (q+v) path: dq - dq_u = dBD . pp_h on the same bf16 band
-    dbd4 = fused_band(dbd, H, B, T, ldbd).float()
+    dbd4 = dbd.view(H, B, T, ldbd)[..., : 2 * T - 1].float()
     pph = pp.float().view(2 * T - 1, H, 64).permute(1, 0, 2)
     dq_v = torch.einsum("hbir,hrc->bihc", dbd4, pph).reshape(B, T, d)
     assert _rel(dq.float(), dq1.float() + dq_v) < 1e-2

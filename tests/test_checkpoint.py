@@ -171,3 +171,30 @@ def test_amp_resume_into_prepared_model_uses_loaded_weights(tmp_path):
     l2, _, _ = m2(**batch(0))
     l3, _, _ = m3(**batch(0))
     np.testing.assert_allclose(l2.item(), l3.item(), rtol=1e-6)
+
+
+@pytest.mark.gpu
+def test_amp_submodule_load_refreshes_shadow():
+    """Loading into a submodule of a prepared AMP model (model.encoder.load_state_dict, as the
+    reference's init_param / load_pretrained_model do) refreshes the bf16 weight shadow the
+    GEMMs read; a whole-model load refreshes it once."""
+    from test_model_build import build
+
+    tc, d = load("train2")
+    cfg, _ = load(tc["cfg_name"])
+    w0 = {k: torch.from_numpy(v) for k, v in section(d, "w").items()}
+    torch.manual_seed(7)
+    m = build(cfg)
+    m.prepare("cuda", amp=True)
+    calls = []
+    real = m.arena.refresh_shadow
+    m.arena.refresh_shadow = lambda: (calls.append(1), real())[1]
+    enc = {k[len("encoder."):]: v for k, v in w0.items() if k.startswith("encoder.")}
+    m.encoder.load_state_dict(enc)
+    assert len(calls) == 1
+    torch.cuda.synchronize()
+    assert torch.equal(m.arena.shadow, m.arena.data.to(torch.bfloat16))
+    m.load_state_dict(w0)
+    assert len(calls) == 2  # once for the whole-model load, not once per submodule
+    torch.cuda.synchronize()
+    assert torch.equal(m.arena.shadow, m.arena.data.to(torch.bfloat16))

@@ -60,7 +60,7 @@ def test_ddp_two_ranks_matches_reference_golden():
     ps = [ctx.Process(target=_worker, args=(r, 2, init, q)) for r in range(2)]
     for p in ps:
         p.start()
-    out = q.get(timeout=300)
+    out = q.get(timeout=140)
     for p in ps:
         p.join(120)
     np.testing.assert_allclose(out["loss"], d["out.loss_scaled"], rtol=2e-6, atol=1e-4)

@@ -115,7 +115,7 @@ def test_rccl_world1_captured_dp_step_bit_exact():
     init = tempfile.mktemp(prefix="ea_rccl_")
     p = ctx.Process(target=_rccl_worker, args=(init, q))
     p.start()
-    res = q.get(timeout=300)
+    res = q.get(timeout=140)
     p.join(60)
     assert "error" not in res, res.get("error")
     assert res["n_graphs"] == 1
@@ -165,7 +165,7 @@ def test_gloo_two_ranks_overlap_amp_matches_serial():
     ps = [ctx.Process(target=_gloo_worker, args=(r, 2, init, q)) for r in range(2)]
     for p in ps:
         p.start()
-    out = q.get(timeout=300)
+    out = q.get(timeout=140)
     for p in ps:
         p.join(120)
     a, b = out[True], out[False]
