@@ -189,15 +189,17 @@ def cpu_baseline(cfg, seconds_budget=25.0):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=50)   # median over >= 50 steps
+    ap.add_argument("--warmup", type=int, default=10)  # after 10 warm-up steps
     ap.add_argument("--config", default="c3", choices=["c3", "c2", "c5"])
     ap.add_argument("--fp32", action="store_true", help="exact-f32 MFMA instead of bf16 AMP")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--profile-steps", type=int, default=0)
     ap.add_argument("--graph-dp", action="store_true",
-                    help="with N > 1, capture the step incl. its RCCL all-reduces as a hipGraph too "
-                         "(default for N > 1: eager steps, see DESIGN.md section 5)")
+                    help="(kept for old command lines) with N > 1 the step incl. its RCCL all-reduces "
+                         "is captured as a hipGraph by default")
+    ap.add_argument("--eager-dp", action="store_true",
+                    help="with N > 1, launch every kernel and collective eagerly instead")
     ap.add_argument("--eager", action="store_true", help="launch every kernel from Python each step "
                     "(default: the step is captured once as a hipGraph and replayed)")
     args = ap.parse_args()
@@ -238,9 +240,10 @@ def main():
     host = synthetic_batch(cfg, 1 + rank)  # abs_task.py:1566-1575: each rank its own shard
     batch = {k: v.to(dev) for k, v in host.items()}  # resident in HBM before timing
     maxlens = (cfg["T"], cfg["L"])
-    # multi-GPU steps run eagerly unless --graph-dp: hipGraph capture of the RCCL collectives
-    # has not been exercised on a multi-GPU node yet
-    eager = args.eager or (world > 1 and not args.graph_dp)
+    # multi-GPU steps are captured with their RCCL collectives too (tests/test_dp_capture_gpu.py:
+    # bit-identical to eager DP); CapturedTrainStep falls back to eager steps if a node's stack
+    # cannot capture them
+    eager = args.eager or (world > 1 and args.eager_dp)
     runner = CapturedTrainStep(model, opt, sched, grad_clip=5.0, dp=dp, warmup=2, enabled=not eager)
 
     def step():
@@ -257,14 +260,19 @@ def main():
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
+    # per-step HIP events on the step's stream (median step time)
+    evs = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps + 1)]
     t0 = time.perf_counter()
-    for _ in range(args.steps):
+    evs[0].record()
+    for i in range(args.steps):
         loss, stats, weight, gn = step()
+        evs[i + 1].record()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     t1 = time.perf_counter()
     hip_ops.PROBE = None
+    step_ms = sorted(evs[i].elapsed_time(evs[i + 1]) for i in range(args.steps))
     elapsed = t1 - t0
     if world > 1:
         t = torch.tensor([elapsed], device=dev)
@@ -273,6 +281,18 @@ def main():
     ms = elapsed / args.steps * 1e3
     utt = cfg["B"] * world * args.steps / elapsed
     conv_ms, n_conv = probe.mean_ms("conv2_gemm")
+    # the same launch timed with HIP events on its stream: eager forwards of the subsampling
+    # block after the timed region (events cannot sit inside the captured graph)
+    ev_probe = hip_ops.EventProbe(["conv2_gemm"])
+    hip_ops.PROBE = ev_probe
+    with torch.no_grad():
+        for i in range(6):
+            if i == 1:
+                ev_probe.reset()  # first launch warms the eager path
+            model.encoder.embed(batch["speech"], 0)
+    conv_ev_ms, n_ev = ev_probe.mean_ms("conv2_gemm")
+    hip_ops.PROBE = None
+    med_ms = step_ms[len(step_ms) // 2]
     B, T = cfg["B"], cfg["T"]
     T1, F1 = (T - 3) // 2 + 1, (80 - 3) // 2 + 1
     T2, F2 = (T1 - 3) // 2 + 1, (F1 - 3) // 2 + 1
@@ -302,7 +322,15 @@ def main():
                          "traffic_unit": "bytes/launch (HBM, PMC)", "traffic_source": traffic_src,
                          "traffic_measured_on_this_build": traffic_same,
                          "algorithmic_bytes": int(2 * (B * T1 * F1 * C + C * 9 * C + B * T2 * F2 * C)),
-                         "launch_ms": round(conv_ms, 4), "launches": n_conv},
+                         "launch_ms": round(conv_ms, 4), "launches": n_conv,
+                         "timing": "achieved/frac from the in-kernel probe (first-block start to "
+                                   "last-block end, every timed replay); frac_events from HIP "
+                                   "events around eager launches on the launch stream",
+                         "launch_ms_events": round(conv_ev_ms, 4), "launches_events": n_ev,
+                         "frac_events": round(conv_flop / (conv_ev_ms * 1e-3) / 1e12 / PEAK[dtype], 4)},
+            "step_ms_median": round(med_ms, 3),
+            "step_ms_p10_p90": [round(step_ms[len(step_ms) // 10], 3), round(step_ms[(9 * len(step_ms)) // 10], 3)],
+            "value_median": round(cfg["B"] * world / (med_ms * 1e-3), 3),
             "loss": round(loss_v, 4),
         }
         if world == 1 and not args.no_cpu_baseline:

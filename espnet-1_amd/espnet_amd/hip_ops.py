@@ -52,6 +52,38 @@ class KernelProbe:
         return (tot / cnt * self.TICK_MS if cnt else float("nan")), cnt
 
 
+class EventProbe:
+    """The same begin/end interface as KernelProbe, timed with HIP events recorded on the
+    launch stream around the named launch (eager launches only: not inside a graph capture).
+    bench.py reports it beside the in-kernel probe and the rocprof average."""
+
+    def __init__(self, names):
+        self.names = set(names)
+        self.pairs = {n: [] for n in names}
+        self.active = True
+
+    def begin(self, name):
+        if self.active and name in self.names:
+            ev = torch.cuda.Event(enable_timing=True)
+            ev.record(torch.cuda.current_stream())
+            self.pairs[name].append([ev, None])
+
+    def end(self, name):
+        if self.active and name in self.names:
+            ev = torch.cuda.Event(enable_timing=True)
+            ev.record(torch.cuda.current_stream())
+            self.pairs[name][-1][1] = ev
+
+    def reset(self):
+        for v in self.pairs.values():
+            v.clear()
+
+    def mean_ms(self, name):
+        torch.cuda.synchronize()
+        ts = [a.elapsed_time(b) for a, b in self.pairs[name] if b is not None]
+        return (sum(ts) / len(ts) if ts else float("nan")), len(ts)
+
+
 PROBE = None
 # run weight-gradient GEMMs / bias reductions on a side stream (EA_OVERLAP_WGRAD=0: serial, for profiling)
 OVERLAP_WGRAD = os.environ.get("EA_OVERLAP_WGRAD", "1") != "0"

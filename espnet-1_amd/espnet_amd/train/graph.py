@@ -125,7 +125,18 @@ class CapturedTrainStep:
                     out = self._eager(dbatch, maxlens)
                 main.wait_stream(self._side)
                 return out
-            return self._capture(key, dbatch, maxlens)
+            try:
+                return self._capture(key, dbatch, maxlens)
+            except RuntimeError as e:
+                # a stack that cannot capture this step (e.g. a collective library without
+                # graph support on some node): warn once and run every step eagerly.  Capture
+                # executes nothing, so the step is simply run now.
+                import warnings
+                warnings.warn(f"hipGraph capture of the training step failed ({e}); running eager steps")
+                torch.cuda.synchronize()
+                self.enabled = False
+                self.graphs.pop(key, None)
+                return self._eager(dbatch, maxlens)
         finally:
             common.SKIP_LAYERDROP_DRAWS = False
 
