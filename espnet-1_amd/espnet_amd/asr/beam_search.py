@@ -7,9 +7,10 @@ Same constructor arguments, scorer/weight dictionaries, hypothesis record, searc
 sorted, beam-pruned pool) and end conditions (<eos> forced at maxlen, end detection for
 maxlenratio 0, retry with a smaller minlenratio when nothing ended).  MI355X layout: at every
 step ALL running hypotheses (they share a length) are scored in ONE batched call per scorer
-(the decoder's `batch_score`, HIP kernels over an (n_hyps, T, d) memory); only the
-(n_hyps, vocab) score matrix comes back to the host for the selection, which is done in f32
-exactly as the reference does it.
+(the decoder's `batch_score`: one incremental step over a device key/value cache, the
+surviving hypotheses' cache rows gathered once per step); only the (n_hyps, vocab) score
+matrix comes back to the host for the selection, which is done in f32 exactly as the
+reference does it.
 
 Partial scorers (CTCPrefixScorer, scorers/ctc.py) score only the pre-beam candidates of
 each hypothesis; every (hypothesis, candidate) pair of a step is scored by ONE launch of the
@@ -182,17 +183,19 @@ class BeamSearch(torch.nn.Module):
     def append_token(xs: torch.Tensor, x: int) -> torch.Tensor:
         return torch.cat((xs, torch.tensor([x], dtype=xs.dtype, device=xs.device)))
 
-    def _score_all(self, running: List[Hypothesis], x: torch.Tensor) -> Dict[str, torch.Tensor]:
+    def _score_all(self, running: List[Hypothesis], x: torch.Tensor):
         """Every full scorer on every running hypothesis in one batched call:
-        {name: (n_hyps, n_vocab) f32 on the host}."""
+        ({name: (n_hyps, n_vocab) f32 on the host}, {name: per-hypothesis states after the
+        call, or None}) — the decoder's state is its row of the step's key/value cache."""
         n = len(running)
         ys = torch.stack([h.yseq for h in running]).to(x.device)
         xs = x.unsqueeze(0).expand(n, *x.shape)
-        out = {}
+        out, states = {}, {}
         for k, d in self.full_scorers.items():
-            sc, _ = d.batch_score(ys, [h.states[k] for h in running], xs)
+            sc, st = d.batch_score(ys, [h.states[k] for h in running], xs)
             out[k] = sc.float().cpu()
-        return out
+            states[k] = st
+        return out, states
 
     def beam(self, weighted_scores: torch.Tensor, ids: torch.Tensor):
         """beam_search.py:209-237: top-k full ids and the matching pre-beam (local) ids."""
@@ -213,7 +216,7 @@ class BeamSearch(torch.nn.Module):
         incremental sort-and-prune is one stable descending sort of the n_hyps x beam
         candidates in hypothesis order (it keeps the same beam, ties included)."""
         n, V = len(running_hyps), self.n_vocab
-        allsc = self._score_all(running_hyps, x)
+        allsc, allst = self._score_all(running_hyps, x)
         W = torch.zeros(n, V, dtype=torch.float32)
         for k in self.full_scorers:
             W += self.weights[k] * allsc[k]
@@ -246,7 +249,8 @@ class BeamSearch(torch.nn.Module):
             j, pj = int(top[hi, r]), int(local[hi, r])
             new_scores = {k: hyp.scores[k] + allsc[k][hi, j] for k in self.full_scorers}
             new_scores.update({k: hyp.scores[k] + part[k][0][hi][pj] for k in self.part_scorers})
-            new_states = {k: hyp.states[k] for k in self.full_scorers}
+            # beam_search.py:330 merge_states: a full scorer's state after scoring hyp
+            new_states = {k: (hyp.states[k] if allst[k] is None else allst[k][hi]) for k in self.full_scorers}
             new_states.update({k: d.select_state(part[k][1][hi], pj) for k, d in self.part_scorers.items()})
             best_hyps.append(Hypothesis(score=W[hi, j], yseq=self.append_token(hyp.yseq, j), scores=new_scores,
                                         states=new_states))
@@ -291,3 +295,11 @@ class BeamSearch(torch.nn.Module):
         if len(nbest) == 0:
             return [] if minlenratio < 0.1 else self.forward(x, maxlenratio, max(0.0, minlenratio - 0.1))
         return nbest
+
+
+class BatchBeamSearch(BeamSearch):
+    """espnet/nets/batch_beam_search.py:26 (BatchBeamSearch: every running hypothesis scored
+    in one batched call per scorer, states kept batched).  BeamSearch above already runs that
+    way — batched full scorers over the decoder's key/value cache, one CTC prefix launch per
+    step — so this is the same search under the reference's class name."""
+

@@ -1,16 +1,61 @@
 """TransformerDecoder — drop-in for espnet2/asr/decoder/transformer_decoder.py:232-281
 (training forward :92-145).  Same constructor, state_dict keys and init order; the
-forward is one HIP autograd node (layers/decoder.py: DecoderFn)."""
+forward is one HIP autograd node (layers/decoder.py: DecoderFn).
+
+Inference (transformer_decoder.py:146-229: forward_one_step / score / batch_score): an
+incremental decoder over a device key/value cache (DecoderKVCache) — each step computes only
+the new position of every hypothesis: its self-attention keys/values are appended to the
+cache, the encoder memory's cross-attention keys/values are projected once per memory (one
+GEMM for all layers), and the next-token log-softmax is one row kernel (ea_softmax_rows).
+The reference's cache holds each layer's outputs for the prefix and re-projects the prefix's
+keys/values every step; the scores are the same (a causal decoder's prefix rows do not
+depend on later tokens)."""
 from __future__ import annotations
 
+import math
 from typing import Tuple
 
 import torch
 from torch import nn
 
-from ...layers.common import Bound, multisequential_draw
+from ... import hip_ops as ops
+from ..._lib import lib
+from ...layers.common import (ACT_RELU, EPI_ACT, EPI_RESID, Bound, empty, ln_fwd, multisequential_draw)
 from ...layers.conformer import LayerNorm, MultiHeadedAttention, PositionwiseFeedForward
-from ...layers.decoder import DecoderFn, DecoderLayer, PositionalEncoding, decoder_arena_groups
+from ...layers.decoder import (DecoderFn, DecoderLayer, PositionalEncoding, _kv_names, _mha_fwd,
+                               decoder_arena_groups)
+
+
+class DecoderKVCache:
+    """Incremental-decoding state of n hypotheses after L prefix positions.
+
+    kv: (num_blocks, n, L, 2d) in the compute dtype — every layer's self-attention [key |
+    value] rows of every prefix position (one row per (hypothesis, position), so the new
+    position's key/value projection is ONE GEMM writing both halves, and the attention reads
+    keys at column 0 and values at column d with row stride 2d).  mem: the cross-attention
+    keys/values of the encoder memory for all layers, (n*T, 2*d*num_blocks), with the memory
+    lengths; shared by every step over that memory (MemoryKV)."""
+
+    __slots__ = ("kv", "L", "mem")
+
+    def __init__(self, kv, L, mem):
+        self.kv, self.L, self.mem = kv, L, mem
+
+    def select(self, rows):
+        """The caches of hypotheses `rows` (device or host indices), in that order."""
+        idx = torch.as_tensor(rows, dtype=torch.long, device=self.kv.device)
+        return DecoderKVCache(self.kv.index_select(1, idx), self.L, self.mem)
+
+
+class MemoryKV:
+    """Cross-attention keys/values of one encoder memory for all decoder layers (the training
+    forward's single K/V GEMM, layers/decoder.py), kept per hypothesis count n."""
+
+    __slots__ = ("memory", "by_n")
+
+    def __init__(self, memory):
+        self.memory = memory
+        self.by_n = {}
 
 
 class AbsDecoder(nn.Module):
@@ -76,26 +121,145 @@ class TransformerDecoder(AbsDecoder):
     # ------------------------------------------------------------------ inference scorer
     @torch.no_grad()
     def forward_one_step(self, tgt: torch.Tensor, tgt_mask: torch.Tensor, memory: torch.Tensor,
-                         cache=None):
-        """transformer_decoder.py:146-184: log-softmax of the next token after each prefix
-        in tgt (B, L) over memory (B, T, d), no memory mask.  The prefix is recomputed with
-        the fused kernels instead of extending per-layer caches (a causal decoder's prefix
-        outputs do not depend on later tokens, so the scores are the reference's); the
-        returned `cache` is the per-layer placeholder list the reference's API passes on."""
+                         memory_mask=None, *, cache=None, return_hs=False):
+        """transformer_decoder.py:146-184: log-softmax of the next token after each prefix in
+        tgt (B, L) over memory (B, T, d) (no memory mask; tgt_mask is the causal mask the
+        reference builds, implied here).  `cache`: the DecoderKVCache this method returned
+        for tgt[:, :-1] (rows in tgt's order) — then only the last position is computed;
+        None (or a cache of another length) builds it from the prefix first.  Returns
+        (logp (B, V) f32, the cache of tgt)."""
+        if memory_mask is not None:
+            raise NotImplementedError("memory_mask is not used by the ASR scorers")
         B, L = tgt.shape
         dev = memory.device
-        hlens = torch.full((B,), memory.shape[1], dtype=torch.long, device=dev)
-        ylens = torch.full((B,), L, dtype=torch.long, device=dev)
-        logits = DecoderFn.apply(memory.contiguous(), hlens, tgt.to(dev).contiguous(), ylens, self, 0, False)
-        y = torch.log_softmax(logits[:, -1].float(), dim=-1)
-        return y, [None] * len(self.decoders)
+        tgt = tgt.to(dev)
+        if not isinstance(cache, DecoderKVCache) or cache.L != L - 1 or cache.kv.shape[1] != B:
+            cache = self._empty_cache(memory)
+            for pos in range(L - 1):  # prefill: the prefix one position at a time
+                _, cache = self._step(tgt[:, pos], pos, cache)
+        logp, hs, cache = self._step(tgt[:, -1], L - 1, cache, want_hs=True)
+        if return_hs:
+            return (logp, hs), cache
+        return logp, cache
+
+    def _empty_cache(self, memory):
+        b = self._b
+        B = memory.shape[0]
+        d = memory.shape[2]
+        kv = torch.empty(len(self.decoders), B, 0, 2 * d, dtype=b.cd, device=memory.device)
+        return DecoderKVCache(kv, 0, MemoryKV(memory))
+
+    def _memory_kv(self, mem: MemoryKV, n: int):
+        """(n*T, 2*d*nb) cross-attention K/V rows and lengths of n hypotheses over the memory:
+        one GEMM (all layers' src_attn.linear_k/linear_v are adjacent in the arena)."""
+        got = mem.by_n.get(n)
+        if got is not None:
+            return got
+        b = self._b
+        m = mem.memory
+        Bm, T, d = m.shape
+        nb = len(self.decoders)
+        if Bm == n:
+            rows = m.reshape(n * T, d)
+        elif Bm == 1 or m.stride(0) == 0:  # one memory shared by every hypothesis
+            rows = m[:1].expand(n, T, d).reshape(n * T, d)
+        else:
+            raise ValueError(f"memory batch {Bm} does not match {n} hypotheses")
+        kvw, kvb = _kv_names(nb)
+        kv = empty(n * T, 2 * d * nb, dtype=b.cd, device=m.device)
+        ops.linear(ops.cast(rows.contiguous(), b.cd), b.w(*kvw, shape=(2 * d * nb, d)), kv,
+                   epi=ops.make_epi(bias=b.f(*kvb, shape=(2 * d * nb,))))
+        hlens = torch.full((n,), T, dtype=torch.long, device=m.device)
+        mem.by_n[n] = (kv, hlens, T)
+        return mem.by_n[n]
+
+    def _step(self, tok, pos, cache: DecoderKVCache, want_hs=False):
+        """One position (index pos) for every hypothesis: tok (n,) the token at pos; cache
+        holds positions [0, pos).  Returns (logp (n, V) f32, new cache) (+ the after_norm
+        output when want_hs)."""
+        b = self._b
+        cd = b.cd
+        nb = len(self.decoders)
+        n = tok.shape[0]
+        d = self.output_layer.in_features
+        H = self.decoders[0].self_attn.h
+        dk = d // H
+        V = self.output_layer.out_features
+        dev = tok.device
+        scale = 1.0 / math.sqrt(dk)
+        mkv, hlens, Tm = self._memory_kv(cache.mem, n)
+        ldm = 2 * d * nb
+        L1 = pos + 1
+        kv = torch.empty(nb, n, L1, 2 * d, dtype=cd, device=dev)
+        if pos:
+            kv[:, :, :pos].copy_(cache.kv)
+        klen = torch.full((n,), L1, dtype=torch.long, device=dev)
+        pe = self.embed[1]
+        x = empty(n, d, device=dev)
+        tok = tok.reshape(n).to(torch.long).contiguous()
+        table = pe.table(L1, dev)
+        lib.ea_embed_fwd(n, d, 1, tok.data_ptr(), b.f("embed.0.weight").data_ptr(), pe.xscale,
+                         table[pos:].data_ptr(), 0.0, 0, x.data_ptr(), ops.stream())
+        for l in range(nb):
+            nm = f"decoders.{l}."
+            sa, xa, ff = nm + "self_attn.", nm + "src_attn.", nm + "feed_forward."
+            xn1, _, _ = ln_fwd(x, b, nm + "norm1", cd)
+            q = empty(n, d, dtype=cd, device=dev)
+            ops.linear(xn1, b.w(sa + "linear_q.weight"), q, epi=ops.make_epi(bias=b.f(sa + "linear_q.bias")))
+            kvl = kv[l]  # (n, L1, 2d): this position's [k | v] row written in place
+            ops.linear(xn1, b.w(sa + "linear_k.weight", sa + "linear_v.weight", shape=(2 * d, d)), kvl[:, pos],
+                       epi=ops.make_epi(bias=b.f(sa + "linear_k.bias", sa + "linear_v.bias", shape=(2 * d,))))
+            O1, _ = _mha_fwd(q, kvl, kvl[:, :, d:], B=n, H=H, T1=1, T2=L1, dk=dk, ldq=d, ldk=2 * d, ldv=2 * d,
+                             klen=klen, causal=False, scale=scale, p=0.0, seed=0, cd=cd)
+            x1 = empty(n, d, device=dev)
+            ops.linear(O1, b.w(sa + "linear_out.weight"), x1,
+                       epi=ops.make_epi(EPI_RESID, bias=b.f(sa + "linear_out.bias"), resid=x))
+            xn2, _, _ = ln_fwd(x1, b, nm + "norm2", cd)
+            q2 = empty(n, d, dtype=cd, device=dev)
+            ops.linear(xn2, b.w(xa + "linear_q.weight"), q2, epi=ops.make_epi(bias=b.f(xa + "linear_q.bias")))
+            O2, _ = _mha_fwd(q2, mkv[:, 2 * d * l:], mkv[:, 2 * d * l + d:], B=n, H=H, T1=1, T2=Tm, dk=dk,
+                             ldq=d, ldk=ldm, ldv=ldm, klen=hlens, causal=False, scale=scale, p=0.0, seed=0, cd=cd)
+            x2 = empty(n, d, device=dev)
+            ops.linear(O2, b.w(xa + "linear_out.weight"), x2,
+                       epi=ops.make_epi(EPI_RESID, bias=b.f(xa + "linear_out.bias"), resid=x1))
+            xn3, _, _ = ln_fwd(x2, b, nm + "norm3", cd)
+            Fh = self.decoders[l].feed_forward.w_1.out_features
+            h = empty(n, Fh, dtype=cd, device=dev)
+            a = empty(n, Fh, dtype=cd, device=dev)
+            ops.linear(xn3, b.w(ff + "w_1.weight"), a,
+                       epi=ops.make_epi(EPI_ACT, bias=b.f(ff + "w_1.bias"), act=ACT_RELU, aux=h))
+            x3 = empty(n, d, device=dev)
+            ops.linear(a, b.w(ff + "w_2.weight"), x3,
+                       epi=ops.make_epi(EPI_RESID, bias=b.f(ff + "w_2.bias"), resid=x2))
+            x = x3
+        xf, _, _ = ln_fwd(x, b, "after_norm", cd)
+        logits = empty(n, V, device=dev)
+        ops.linear(xf, b.w("output_layer.weight"), logits, epi=ops.make_epi(bias=b.f("output_layer.bias")))
+        logp = empty(n, V, device=dev)
+        lib.ea_softmax_rows(n, V, logits.data_ptr(), V, logp.data_ptr(), 1, ops.stream())
+        new = DecoderKVCache(kv, L1, cache.mem)
+        if want_hs:
+            return logp, xf, new
+        return logp, new
 
     def score(self, ys, state, x):
-        """transformer_decoder.py:186-192 (one hypothesis)."""
-        logp, state = self.forward_one_step(ys.unsqueeze(0), None, x.unsqueeze(0), cache=state)
-        return logp.squeeze(0), state
+        """transformer_decoder.py:186-192 (one hypothesis); state = (DecoderKVCache, row)."""
+        cache = state[0].select([state[1]]) if isinstance(state, tuple) else None
+        logp, cache = self.forward_one_step(ys.unsqueeze(0), None, x.unsqueeze(0), cache=cache)
+        return logp.squeeze(0), (cache, 0)
 
     def batch_score(self, ys: torch.Tensor, states, xs: torch.Tensor):
-        """transformer_decoder.py:194-229: scores of the next token for a batch of prefixes."""
-        logp, st = self.forward_one_step(ys, None, xs, cache=None)
-        return logp, [[None] * len(self.decoders) for _ in range(len(ys))]
+        """transformer_decoder.py:194-229 (BatchScorerInterface): next-token scores of n
+        prefixes (n, L) over xs (n, T, d).  A hypothesis's state is (cache, row) — its row of
+        the batched DecoderKVCache its parent was scored with; the step gathers the surviving
+        rows once and computes only the new position."""
+        n = ys.shape[0]
+        cache = None
+        if states and all(isinstance(s, tuple) for s in states):
+            src = states[0][0]
+            if all(s[0] is src for s in states) and src.L == ys.shape[1] - 1:
+                cache = src.select([s[1] for s in states])
+                if cache.mem.memory.shape[1:] != xs.shape[1:]:
+                    cache = None
+        logp, new = self.forward_one_step(ys, None, xs, cache=cache)
+        return logp, [(new, i) for i in range(n)]

@@ -65,9 +65,10 @@ def attention_greedy(model, speech: torch.Tensor, speech_lengths: torch.Tensor, 
                 maxlen = max(1, int(maxlenratio * T))
             yseq = [sos]
             score = 0.0
+            st = [None]  # the decoder's key/value cache row, carried from step to step
             for i in range(maxlen):
                 ys = torch.tensor([yseq], dtype=torch.long, device=enc.device)
-                logp, _ = model.decoder.batch_score(ys, [None], enc)
+                logp, st = model.decoder.batch_score(ys, st, enc)
                 tok = int(torch.argmax(logp[0]))
                 score += float(logp[0, tok])
                 yseq.append(tok)
