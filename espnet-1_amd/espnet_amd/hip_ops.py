@@ -217,6 +217,8 @@ GRAD_READY = None  # callable(prefix): a block's parameter gradients are final (
 # profiles/r3_stream_wgrad_ab.txt — the grouped tiles take whole CUs from the main stream's
 # chip-filling kernels), so the default (0) flushes once at the end of the pass
 STREAM_WGRAD = int(os.environ.get("EA_STREAM_WGRAD", "0"))
+# the end-of-pass reduction flush on the side stream beside the grouped GEMM (EA_REDUCE_SIDE=0: serial)
+REDUCE_SIDE = os.environ.get("EA_REDUCE_SIDE", "1") != "0"
 _STREAM_COUNT = [0]
 
 
@@ -574,9 +576,17 @@ class deferred_wgrad:
         WGRAD_Q.active, REDUCE_Q.active = self.prev
         _STREAM_COUNT[0] = 0
         if exc[0] is None:
-            flush_deferred()
+            if GRAD_READY is None and OVERLAP_WGRAD and REDUCE_SIDE and torch.cuda.is_available():
+                # the pass's reductions (bias column sums, LayerNorm parameter sums: bandwidth-
+                # bound) on the side stream beside the grouped weight-gradient GEMM (MFMA-bound)
+                # on this one; disjoint outputs (bias / norm vs weight gradients)
+                with wgrad(*REDUCE_Q.tensors()):
+                    REDUCE_Q.flush()
+                WGRAD_Q.flush()
+            else:
+                flush_deferred()
             if GRAD_READY is None:
-                join_wgrad()  # gradients flushed onto the side stream during the pass are final
+                join_wgrad()  # gradients written on the side stream during the pass are final
         else:
             WGRAD_Q.items, WGRAD_Q.posts = [], []
             REDUCE_Q.colsums, REDUCE_Q.reduces, REDUCE_Q.spans = [], [], []
