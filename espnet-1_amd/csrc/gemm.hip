@@ -6,6 +6,10 @@
 #include <cstdio>
 #include <cstdlib>
 
+namespace eag {
+int g_pipe_slots = [] { const char* e = std::getenv("EA_PIPE_SLOTS"); return e ? std::atoi(e) : 4; }();
+}  // namespace eag
+
 namespace {
 // split-K combine: C = epi(sum_s slab[s]) (any epilogue kind), 4 columns per thread
 __global__ void splitk_reduce(GemmP p) {

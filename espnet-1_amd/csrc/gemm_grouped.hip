@@ -37,10 +37,10 @@ __global__ void group_upload(GroupChunk c, GroupProbD* table, int* map) {
   }
 }
 
-template <bool AK, bool BKM>
+template <bool AK, bool BKM, int NS = 4>
 __global__ __launch_bounds__(512, 1) void gemm_grouped(const GroupProbD* __restrict__ table,
                                                        const int* __restrict__ map, int ntiles) {
-  using PC = PipeT<256>;
+  using PC = PipeT<256, NS>;
   __shared__ __attribute__((aligned(1024))) char smem[PC::SMEM];
   const int nt = ntiles;
   const int bid = blockIdx.x;
@@ -67,7 +67,7 @@ __global__ __launch_bounds__(512, 1) void gemm_grouped(const GroupProbD* __restr
   for (int i = 0; i < 8; ++i)
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
-  pipe_tile<AK, BKM>(p, smem, q.A, q.B, m0, n0, 0, q.K, acc);
+  pipe_tile<AK, BKM, 0, 256, NS>(p, smem, q.A, q.B, m0, n0, 0, q.K, acc);
   const EpiK ek = make_epik(p);
   epi_wave<EA_EPI_STORE, 8, 4>(p, ek, smem, 0, 0, 0, m0 + wm, n0 + wn, lane, w, acc);
 }
@@ -125,10 +125,17 @@ extern "C" int ea_gemm_grouped(int a_kmajor, int b_kmajor, int n, const ea_group
     }
   }
   const dim3 grid((unsigned)ntiles), block(512);
-  if (a_kmajor && b_kmajor) hipLaunchKernelGGL((gemm_grouped<true, true>), grid, block, 0, st, table, map, (int)ntiles);
-  else if (a_kmajor) hipLaunchKernelGGL((gemm_grouped<true, false>), grid, block, 0, st, table, map, (int)ntiles);
-  else if (b_kmajor) hipLaunchKernelGGL((gemm_grouped<false, true>), grid, block, 0, st, table, map, (int)ntiles);
-  else hipLaunchKernelGGL((gemm_grouped<false, false>), grid, block, 0, st, table, map, (int)ntiles);
+  if (eag::g_pipe_slots == 5) {
+    if (a_kmajor && b_kmajor) hipLaunchKernelGGL((gemm_grouped<true, true, 5>), grid, block, 0, st, table, map, (int)ntiles);
+    else if (a_kmajor) hipLaunchKernelGGL((gemm_grouped<true, false, 5>), grid, block, 0, st, table, map, (int)ntiles);
+    else if (b_kmajor) hipLaunchKernelGGL((gemm_grouped<false, true, 5>), grid, block, 0, st, table, map, (int)ntiles);
+    else hipLaunchKernelGGL((gemm_grouped<false, false, 5>), grid, block, 0, st, table, map, (int)ntiles);
+  } else {
+    if (a_kmajor && b_kmajor) hipLaunchKernelGGL((gemm_grouped<true, true>), grid, block, 0, st, table, map, (int)ntiles);
+    else if (a_kmajor) hipLaunchKernelGGL((gemm_grouped<true, false>), grid, block, 0, st, table, map, (int)ntiles);
+    else if (b_kmajor) hipLaunchKernelGGL((gemm_grouped<false, true>), grid, block, 0, st, table, map, (int)ntiles);
+    else hipLaunchKernelGGL((gemm_grouped<false, false>), grid, block, 0, st, table, map, (int)ntiles);
+  }
   EA_LAUNCH_CHECK();
   return 0;
 }

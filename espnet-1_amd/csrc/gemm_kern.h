@@ -61,6 +61,8 @@ int launch_pipe(GemmP& p, int a_k, int b_k, dim3 grid, hipStream_t st);  // gemm
 int launch_pipe_conv(GemmP& p, dim3 grid, hipStream_t st);               // gemm_pipe_conv.hip: conv2 modes
 int launch_lds_dense(GemmP& p, int a_k, int b_k, dim3 grid, hipStream_t st);  // gemm_lds.hip
 int launch_lds_conv(GemmP& p, dim3 grid, hipStream_t st);                     // gemm_lds_conv.hip
+// ring depth of the 256x256 ping-pong kernel: 4 slots, or 5 (EA_PIPE_SLOTS; gemm.hip)
+extern int g_pipe_slots;
 }  // namespace eag
 
 namespace {
@@ -1164,9 +1166,9 @@ EA_DEV bf16x8 frag32(const char* img, int r, int lane) {  // 16 rows/cols from r
 //  * BT = 128: each wave owns a 32 x 64 sub-tile (G0 rows 0-63 as 2 x 2 waves, G1 rows
 //    64-127), 64 KiB ring + 70 KiB epilogue staging -> two blocks per CU, so one block's
 //    epilogue overlaps the other's main loop (the N = 512 / short-K GEMMs of the step).
-template <int BT>
+template <int BT, int NS = 4>
 struct PipeT {
-  static constexpr int BK = 32, NSLOT = 4, NW = 8, NTT = 512;
+  static constexpr int BK = 32, NSLOT = NS, NW = 8, NTT = 512;
   static constexpr int A_BYTES = BT * BK * 2, B_BYTES = BT * BK * 2, SLOT = A_BYTES + B_BYTES;
   static constexpr int RING = NSLOT * SLOT;
   static constexpr int MI = BT == 256 ? 8 : 2;  // 16-row fragments per wave
@@ -1176,19 +1178,20 @@ struct PipeT {
   static constexpr int G = ACH + BCH;
   static constexpr int OCC = BT == 256 ? 1 : 2;
   static_assert(BT == 256 || BT == 128, "pipe tiles");
+  static_assert(NS == 4 || NS == 5, "ring depth: 4 slots, or 5 (256x256: the whole 160 KiB LDS)");
   EA_DEV static int wm(int w) { return BT == 256 ? (w >> 2) * 128 : (w >> 2) * 64 + ((w >> 1) & 1) * 32; }
   EA_DEV static int wn(int w) { return BT == 256 ? (w & 3) * 64 : (w & 1) * 64; }
 };
 
 // One BT x BT output tile over K range [kbeg, kend) into acc (the wave's sub-tile, PipeT);
 // A / B point at this tile's batch slice.  Returns with every wave done reading smem.
-template <bool AK, bool BKM, int MODE = 0, int BT = 256>
+template <bool AK, bool BKM, int MODE = 0, int BT = 256, int NS = 4>
 EA_DEV void pipe_tile(const GemmP& p, char* smem, const bf16* A, const bf16* B, int m0, int n0, int kbeg,
-                      int kend, f32x4 (&acc)[PipeT<BT>::MI][4]) {
+                      int kend, f32x4 (&acc)[PipeT<BT, NS>::MI][4]) {
   static_assert(MODE == 0 || (MODE == EA_CONV_FWD && AK && BKM) || (MODE == EA_CONV_DGRAD && AK && !BKM) ||
                 (MODE == EA_CONV_WGRAD && !AK && !BKM), "conv gather layouts");
   static_assert(MODE == 0 || BT == 256, "conv gathers run on 256-wide tiles");
-  using PC = PipeT<BT>;
+  using PC = PipeT<BT, NS>;
   constexpr int BK = PC::BK, NSLOT = PC::NSLOT, NW = PC::NW, NTT = PC::NTT, MI = PC::MI;
   constexpr int A_BYTES = PC::A_BYTES, B_BYTES = PC::B_BYTES, SLOT = PC::SLOT;
   constexpr int ACH = PC::ACH, BCH = PC::BCH, G = PC::G;
@@ -1280,7 +1283,7 @@ EA_DEV void pipe_tile(const GemmP& p, char* smem, const bf16* A, const bf16* B, 
   const int dF = BK % max(p.g.F2, 1), dT = BK / max(p.g.F2, 1);
 
   auto issue = [&](int sl) {  // called for sl = 0, 1, 2, ... in order (gather state advances)
-    char* base = smem + (sl & (NSLOT - 1)) * SLOT;
+    char* base = smem + (sl % NSLOT) * SLOT;
     const char* ak = abase + sl * astep;
     const char* bk = bbase + sl * bstep;
     if constexpr (MODE == EA_CONV_FWD || MODE == EA_CONV_DGRAD) {
@@ -1340,12 +1343,12 @@ EA_DEV void pipe_tile(const GemmP& p, char* smem, const bf16* A, const bf16* B, 
   };
 
   auto rd_b = [&](int sl, bf16x8 (&fb)[4]) {
-    const char* lb = smem + (sl & (NSLOT - 1)) * SLOT + A_BYTES;
+    const char* lb = smem + (sl % NSLOT) * SLOT + A_BYTES;
 #pragma unroll
     for (int j = 0; j < 4; ++j) fb[j] = frag32<BKM>(lb, wn + j * 16, lane);
   };
   auto rd_a = [&](int sl, bf16x8 (&fa)[MI]) {
-    const char* la = smem + (sl & (NSLOT - 1)) * SLOT;
+    const char* la = smem + (sl % NSLOT) * SLOT;
 #pragma unroll
     for (int i = 0; i < MI; ++i) fa[i] = frag32<AK>(la, wm + i * 16, lane);
   };
@@ -1353,8 +1356,9 @@ EA_DEV void pipe_tile(const GemmP& p, char* smem, const bf16* A, const bf16* B, 
   const int g1 = w >> 2;  // wave group: G1 runs one barrier behind G0
   const int npre = min(NSLOT - 1, nsl);
   for (int sl = 0; sl < npre; ++sl) issue(sl);
-  // own share of slice 0 landed (slices 1, 2 may stay in flight), then everyone's
-  if (npre >= 3) wait_vmcnt<2 * G>();
+  // own share of slice 0 landed (slices 1 .. npre-1 may stay in flight), then everyone's
+  if (NSLOT == 5 && npre >= 4) wait_vmcnt<(NSLOT == 5 ? 3 : 2) * G>();
+  else if (npre >= 3) wait_vmcnt<2 * G>();
   else if (npre == 2) wait_vmcnt<G>();
   else wait_vmcnt<0>();
   lds_barrier();
@@ -1366,9 +1370,11 @@ EA_DEV void pipe_tile(const GemmP& p, char* smem, const bf16* A, const bf16* B, 
     rd_b(sl, fb);
     rd_a(sl, fa);
     if (sl + NSLOT - 1 < nsl) issue(sl + NSLOT - 1);
-    // own share of slice sl+1 landed: the groups issued after it (sl+2, sl+3) may stay in flight
-    const int newer = min(2, nsl - 2 - sl);
-    if (newer >= 2) wait_vmcnt<2 * G>();
+    // own share of slice sl+1 landed: the groups issued after it (sl+2 .. sl+NSLOT-1) may stay
+    // in flight
+    const int newer = min(NSLOT - 2, nsl - 2 - sl);
+    if (NSLOT == 5 && newer >= 3) wait_vmcnt<(NSLOT == 5 ? 3 : 2) * G>();
+    else if (newer >= 2) wait_vmcnt<2 * G>();
     else if (newer == 1) wait_vmcnt<G>();
     else wait_vmcnt<0>();
     // fragments in registers before the barrier: the COMPUTE segment never waits on LDS, and
@@ -1602,9 +1608,9 @@ EA_DEV void w1_epilogue(const GemmP& p, char* smem, int m0, int n0, int wm, int 
   }
 }
 
-template <bool AK, bool BKM, int MODE = 0, int BT = 256>
-__global__ __launch_bounds__(512, PipeT<BT>::OCC) void gemm_pipe(GemmP p) {
-  using PC = PipeT<BT>;
+template <bool AK, bool BKM, int MODE = 0, int BT = 256, int NS = 4>
+__global__ __launch_bounds__(512, (PipeT<BT, NS>::OCC)) void gemm_pipe(GemmP p) {
+  using PC = PipeT<BT, NS>;
   constexpr int MI = PC::MI;
   __shared__ __attribute__((aligned(1024))) char smem[MODE == EA_CONV_DGRAD ? W1_SMEM : PC::SMEM];
   probe_start(p);
@@ -1629,7 +1635,7 @@ __global__ __launch_bounds__(512, PipeT<BT>::OCC) void gemm_pipe(GemmP p) {
   if constexpr (MODE == EA_CONV_DGRAD) {
     if (p.w1part) w1_load_x(p, m0, w1x);
   }
-  pipe_tile<AK, BKM, MODE, BT>(p, smem, A, B, m0, n0, kbeg, kend, acc);
+  pipe_tile<AK, BKM, MODE, BT, NS>(p, smem, A, B, m0, n0, kbeg, kend, acc);
   diag_stamp(p, 1);
   if constexpr (MODE == EA_CONV_DGRAD) {
     if (p.w1part) {

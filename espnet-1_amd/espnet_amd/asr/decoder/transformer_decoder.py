@@ -13,6 +13,7 @@ depend on later tokens)."""
 from __future__ import annotations
 
 import math
+import os
 from typing import Tuple
 
 import torch
@@ -45,6 +46,141 @@ class DecoderKVCache:
         """The caches of hypotheses `rows` (device or host indices), in that order."""
         idx = torch.as_tensor(rows, dtype=torch.long, device=self.kv.device)
         return DecoderKVCache(self.kv.index_select(1, idx), self.L, self.mem)
+
+
+class GraphStepKV:
+    """Decoder state of n hypotheses inside a captured decoding run (DecodeGraphs): which of
+    the run's two static key/value buffers holds positions [0, L), and the step it was
+    written at (a state older than the previous step is stale: its buffer was reused)."""
+
+    __slots__ = ("run", "n", "buf", "L", "step")
+
+    def __init__(self, run, n, buf, L, step):
+        self.run, self.n, self.buf, self.L, self.step = run, n, buf, L, step
+
+
+class DecodeGraphs:
+    """Captured incremental decoder steps over one encoder memory (inference, §8(f) row 4).
+
+    Decoding is launch-bound: a step is ~80 small launches for ~10 hypotheses.  Here each
+    hypothesis count n gets two hipGraphs of ONE step (one per direction between two static
+    (num_blocks, n, Lcap, 2d) key/value buffers), captured once with static-shape inputs: the
+    token ids and the position live in device buffers, the positional-encoding row is gathered
+    by the position on the device, the new key/value row is written at the position with an
+    index copy, and self-attention runs over Lcap keys masked to pos + 1 (the fused kernel
+    stops at that length).  A step = one packed host->device copy, one row gather of the
+    surviving hypotheses' caches (outside the graph: n may change between steps) and a replay."""
+
+    def __init__(self, dec, memory: "MemoryKV", lcap: int):
+        self.dec, self.mem, self.lcap = dec, memory, lcap
+        self.per_n = {}
+        self.nstep = 0  # steps run so far (a state from an older step is stale)
+
+    def _setup(self, n):
+        dec = self.dec
+        b = dec._b
+        dev = self.mem.memory.device
+        nb = len(dec.decoders)
+        d = dec.output_layer.in_features
+        V = dec.output_layer.out_features
+        st = dict(kv=[torch.zeros(nb, n, self.lcap, 2 * d, dtype=b.cd, device=dev) for _ in range(2)],
+                  inp=torch.zeros(n + 1, dtype=torch.long, device=dev),   # [tokens | position]
+                  host=torch.zeros(n + 1, dtype=torch.long).pin_memory(),
+                  graphs=[None, None], out=[None, None], pool=None)
+        self.per_n[n] = st
+        dec._memory_kv(self.mem, n)  # cross-attention K/V before capture
+        return st
+
+    def _body(self, st, n, buf):
+        """The step the graph captures: reads st['inp'], writes st['kv'][buf] row pos and the
+        returned (n, V) log-probabilities."""
+        dec = self.dec
+        b = dec._b
+        cd = b.cd
+        nb = len(dec.decoders)
+        d = dec.output_layer.in_features
+        H = dec.decoders[0].self_attn.h
+        dk = d // H
+        V = dec.output_layer.out_features
+        dev = st["inp"].device
+        scale = 1.0 / math.sqrt(dk)
+        mkv, hlens, Tm = dec._memory_kv(self.mem, n)
+        ldm = 2 * d * nb
+        tok = st["inp"][:n]
+        pos = st["inp"][n:]
+        kv = st["kv"][buf]
+        klen = (pos + 1).expand(n).contiguous()
+        pe = dec.embed[1]
+        pe_row = pe.table(self.lcap, dev).index_select(0, pos)
+        x = empty(n, d, device=dev)
+        lib.ea_embed_fwd(n, d, 1, tok.data_ptr(), b.f("embed.0.weight").data_ptr(), pe.xscale, pe_row.data_ptr(),
+                         0.0, 0, x.data_ptr(), ops.stream())
+        for l in range(nb):
+            nm = f"decoders.{l}."
+            sa, xa, ff = nm + "self_attn.", nm + "src_attn.", nm + "feed_forward."
+            xn1, _, _ = ln_fwd(x, b, nm + "norm1", cd)
+            q = empty(n, d, dtype=cd, device=dev)
+            ops.linear(xn1, b.w(sa + "linear_q.weight"), q, epi=ops.make_epi(bias=b.f(sa + "linear_q.bias")))
+            row = empty(n, 2 * d, dtype=cd, device=dev)
+            ops.linear(xn1, b.w(sa + "linear_k.weight", sa + "linear_v.weight", shape=(2 * d, d)), row,
+                       epi=ops.make_epi(bias=b.f(sa + "linear_k.bias", sa + "linear_v.bias", shape=(2 * d,))))
+            kvl = kv[l]
+            kvl.index_copy_(1, pos, row.view(n, 1, 2 * d))
+            O1, _ = _mha_fwd(q, kvl, kvl[:, :, d:], B=n, H=H, T1=1, T2=self.lcap, dk=dk, ldq=d, ldk=2 * d,
+                             ldv=2 * d, klen=klen, causal=False, scale=scale, p=0.0, seed=0, cd=cd)
+            x1 = empty(n, d, device=dev)
+            ops.linear(O1, b.w(sa + "linear_out.weight"), x1,
+                       epi=ops.make_epi(EPI_RESID, bias=b.f(sa + "linear_out.bias"), resid=x))
+            xn2, _, _ = ln_fwd(x1, b, nm + "norm2", cd)
+            q2 = empty(n, d, dtype=cd, device=dev)
+            ops.linear(xn2, b.w(xa + "linear_q.weight"), q2, epi=ops.make_epi(bias=b.f(xa + "linear_q.bias")))
+            O2, _ = _mha_fwd(q2, mkv[:, 2 * d * l:], mkv[:, 2 * d * l + d:], B=n, H=H, T1=1, T2=Tm, dk=dk,
+                             ldq=d, ldk=ldm, ldv=ldm, klen=hlens, causal=False, scale=scale, p=0.0, seed=0, cd=cd)
+            x2 = empty(n, d, device=dev)
+            ops.linear(O2, b.w(xa + "linear_out.weight"), x2,
+                       epi=ops.make_epi(EPI_RESID, bias=b.f(xa + "linear_out.bias"), resid=x1))
+            xn3, _, _ = ln_fwd(x2, b, nm + "norm3", cd)
+            Fh = dec.decoders[l].feed_forward.w_1.out_features
+            h = empty(n, Fh, dtype=cd, device=dev)
+            a = empty(n, Fh, dtype=cd, device=dev)
+            ops.linear(xn3, b.w(ff + "w_1.weight"), a,
+                       epi=ops.make_epi(EPI_ACT, bias=b.f(ff + "w_1.bias"), act=ACT_RELU, aux=h))
+            x3 = empty(n, d, device=dev)
+            ops.linear(a, b.w(ff + "w_2.weight"), x3,
+                       epi=ops.make_epi(EPI_RESID, bias=b.f(ff + "w_2.bias"), resid=x2))
+            x = x3
+        xf, _, _ = ln_fwd(x, b, "after_norm", cd)
+        logits = empty(n, V, device=dev)
+        ops.linear(xf, b.w("output_layer.weight"), logits, epi=ops.make_epi(bias=b.f("output_layer.bias")))
+        logp = empty(n, V, device=dev)
+        lib.ea_softmax_rows(n, V, logits.data_ptr(), V, logp.data_ptr(), 1, ops.stream())
+        return logp
+
+    def step(self, tok, pos, prev: "GraphStepKV", rows):
+        """Score position pos (tok: host ints, n of them) for hypotheses whose caches are rows
+        `rows` of prev (None at pos 0).  Returns (logp (n, V) — a static buffer, valid until
+        the next step — and the new GraphStepKV)."""
+        n = len(tok)
+        st = self.per_n.get(n) or self._setup(n)
+        buf = 0 if prev is None else 1 - prev.buf
+        if prev is not None:
+            src = self.per_n[prev.n]["kv"][prev.buf]
+            idx = torch.as_tensor(rows, dtype=torch.long).to(src.device, non_blocking=True)
+            torch.index_select(src, 1, idx, out=st["kv"][buf])
+        st["host"][:n] = torch.as_tensor(tok, dtype=torch.long)
+        st["host"][n] = pos
+        st["inp"].copy_(st["host"], non_blocking=True)
+        if st["graphs"][buf] is None:
+            self._body(st, n, buf)  # eager warm-up (lazy workspaces), then capture
+            torch.cuda.synchronize()
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g, pool=st["pool"]):
+                st["out"][buf] = self._body(st, n, buf)
+            st["pool"] = g.pool()
+            st["graphs"][buf] = g
+        st["graphs"][buf].replay()
+        self.nstep += 1
+        return st["out"][buf], GraphStepKV(self, n, buf, pos + 1, self.nstep)
 
 
 class MemoryKV:
@@ -248,12 +384,46 @@ class TransformerDecoder(AbsDecoder):
         logp, cache = self.forward_one_step(ys.unsqueeze(0), None, x.unsqueeze(0), cache=cache)
         return logp.squeeze(0), (cache, 0)
 
+    # captured decoding steps (DecodeGraphs): on by default on the GPU; EA_DECODE_GRAPH=0 runs
+    # the eager incremental step.  graph_lcap: key/value capacity (positions) of a captured run.
+    decode_graph = os.environ.get("EA_DECODE_GRAPH", "1") != "0"
+    graph_lcap = 512
+
+    def _graph_batch_score(self, ys, states, xs):
+        """batch_score on a captured run, or None when this call cannot use one (a prefix
+        longer than the capacity, states of another run / a stale step, a new memory)."""
+        n, L = ys.shape
+        pos = L - 1
+        if pos >= self.graph_lcap:
+            return None
+        prev, rows = None, None
+        if pos > 0:
+            if not (states and all(isinstance(s, tuple) and isinstance(s[0], GraphStepKV) for s in states)):
+                return None
+            prev = states[0][0]
+            run = prev.run
+            if any(s[0].run is not run or s[0].step != prev.step or s[0].L != pos for s in states) \
+                    or prev.step != run.nstep or run.mem.memory.shape[1:] != xs.shape[1:]:
+                return None
+            rows = [s[1] for s in states]  # the parents' rows of the previous step's buffer
+        else:
+            mem = xs[:1] if (xs.shape[0] == 1 or xs.stride(0) == 0) else xs
+            run = DecodeGraphs(self, MemoryKV(mem), self.graph_lcap)
+        tok = ys[:, -1].tolist()
+        logp, kv = run.step(tok, pos, prev, rows)
+        return logp, [(kv, i) for i in range(n)]
+
     def batch_score(self, ys: torch.Tensor, states, xs: torch.Tensor):
         """transformer_decoder.py:194-229 (BatchScorerInterface): next-token scores of n
         prefixes (n, L) over xs (n, T, d).  A hypothesis's state is (cache, row) — its row of
-        the batched DecoderKVCache its parent was scored with; the step gathers the surviving
-        rows once and computes only the new position."""
+        the batched key/value cache its parent was scored with; the step gathers the surviving
+        rows once and computes only the new position (on a captured run, DecodeGraphs, when
+        it can: a search that starts from the <sos> prefix)."""
         n = ys.shape[0]
+        if self.decode_graph and not self.training and torch.cuda.is_available():
+            got = self._graph_batch_score(ys, states, xs)
+            if got is not None:
+                return got
         cache = None
         if states and all(isinstance(s, tuple) for s in states):
             src = states[0][0]

@@ -65,14 +65,18 @@ def test_decoder_batch_score_matches_full_forward():
     assert cache.L == 5 and tuple(cache.kv.shape) == (len(m.decoder.decoders), 3, 5, 2 * xs.shape[2])
 
 
+@pytest.mark.parametrize("graph", [False, True])
 @pytest.mark.parametrize("amp", [False, True])
-def test_decoder_kv_cache_steps_match_full_forward(amp):
+def test_decoder_kv_cache_steps_match_full_forward(amp, graph, monkeypatch):
     """Incremental decoding (transformer_decoder.py:146-229 with its cache): every step's
     batch_score over the previous step's cache rows — gathered in a shuffled order, as a beam
     reorders its hypotheses — equals the full decoder forward of the same prefixes at their
     last position (fp32: 2e-5; bf16: the step and the full pass round the same bf16 operands in
-    different GEMM shapes, 2e-2 on the log-probabilities)."""
+    different GEMM shapes, 2e-2 on the log-probabilities).  graph=True: the captured steps
+    (DecodeGraphs: static key/value buffers, position and tokens in device memory)."""
     from test_model_build import build
+    from espnet_amd.asr.decoder.transformer_decoder import TransformerDecoder
+    monkeypatch.setattr(TransformerDecoder, "decode_graph", graph)
     cfg, d = load("tiny_hybrid")
     torch.manual_seed(0)
     m = build(cfg)
@@ -99,6 +103,7 @@ def test_decoder_kv_cache_steps_match_full_forward(amp):
             ys = torch.cat([ys[parents], torch.randint(2, V - 1, (n, 1), generator=g)], dim=1)
             states = [st[int(p)] for p in parents]
         assert st[0][0].L == 7
+        assert (type(st[0][0]).__name__ == "GraphStepKV") == graph
     m.train()
 
 
