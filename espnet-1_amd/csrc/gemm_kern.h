@@ -885,7 +885,7 @@ __global__ __launch_bounds__(128 * WN, 1) void gemm_bf16_lds(GemmP p) {
       return (uint32_t)(((long)min(mn0 + row, MN - 1) * ld + c * 8) * 2);
     }
     const int pnl = ci >> 10, cj = ci & 1023, k = cj >> 4, c = (cj & 15) ^ swz_mn_bf16(k);
-    return (uint32_t)(((long)k * ld + min((long)(mn0 + pnl * 128 + c * 8), ld - 8)) * 2);
+    return (uint32_t)(((long)k * ld + min((long)(mn0 + pnl * 128 + c * 8), (long)((MN - 1) & ~7))) * 2);
   };
   const char* abase = (const char*)(A + (AK ? (long)kbeg : (long)kbeg * p.lda));
   const char* bbase = (const char*)(B + (BKM ? (long)kbeg : (long)kbeg * p.ldb));
@@ -1209,7 +1209,7 @@ EA_DEV void pipe_tile(const GemmP& p, char* smem, const bf16* A, const bf16* B, 
       return (uint32_t)(((long)min(mn0 + row, MN - 1) * ld + c * 8) * 2);
     }
     const int pnl = ci >> 9, cj = ci & 511, k = cj >> 4, c = (cj & 15) ^ swz_mn_bf16(k);
-    return (uint32_t)(((long)k * ld + min((long)(mn0 + pnl * 128 + c * 8), ld - 8)) * 2);
+    return (uint32_t)(((long)k * ld + min((long)(mn0 + pnl * 128 + c * 8), (long)((MN - 1) & ~7))) * 2);
   };
   const char* abase = (const char*)(A + (AK ? (long)kbeg : (long)kbeg * p.lda));
   const char* bbase = (const char*)(B + (BKM ? (long)kbeg : (long)kbeg * p.ldb));
