@@ -28,7 +28,7 @@ for r in csv.DictReader(open(f"{o}/g_kernel_trace.csv")):
     if "gemm_" not in n and "splitk" not in n:
         continue
     wg = int(r["Workgroup_Size_X"])
-    key = (n.split("(eag")[0].split("(anonymous")[0].replace("void (anonymous namespace)::", "")[:48],
+    key = (n.replace("void (anonymous namespace)::", "").replace("(anonymous namespace)::", "").split("(")[0][:48],
            int(r["Grid_Size_X"]) // wg, int(r["Grid_Size_Z"]))
     disp[key].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
 
