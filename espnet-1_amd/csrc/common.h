@@ -142,6 +142,33 @@ EA_DEV float act_bwd(int act, float h) {  // derivative wrt pre-activation h
   return 1.f;
 }
 
+// N elements at once: the activation branch (uniform) taken once outside the element loop, so
+// the N independent exp -> rcp chains share one basic block and interleave (a branch per
+// element serialises each chain's latency)
+template <int N>
+EA_DEV void act_fwd_n(int act, float (&v)[N]) {
+  if (act == EA_ACT_SWISH) {
+#pragma unroll
+    for (int c = 0; c < N; ++c) v[c] = v[c] * sigmoidf_(v[c]);
+  } else if (act == EA_ACT_RELU) {
+#pragma unroll
+    for (int c = 0; c < N; ++c) v[c] = v[c] > 0.f ? v[c] : 0.f;
+  }
+}
+template <int N>
+EA_DEV void act_bwd_mul_n(int act, float (&v)[N], const float (&h)[N]) {  // v *= act'(h)
+  if (act == EA_ACT_SWISH) {
+#pragma unroll
+    for (int c = 0; c < N; ++c) {
+      const float s = sigmoidf_(h[c]);
+      v[c] *= s * (1.f + h[c] * (1.f - s));
+    }
+  } else if (act == EA_ACT_RELU) {
+#pragma unroll
+    for (int c = 0; c < N; ++c) v[c] *= h[c] > 0.f ? 1.f : 0.f;
+  }
+}
+
 // ------------------------------------------------------------------ reductions (wave64)
 EA_DEV float wave_sum(float v) {
 #pragma unroll

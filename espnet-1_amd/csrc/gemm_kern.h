@@ -322,8 +322,7 @@ EA_DEV void epi_four_pre(const GemmP& p, const EpiK& k, int z, int zb, int zh, i
     st4(p.C, cidx, p.c_dtype, v);
   } else if constexpr (KIND == EA_EPI_ACT) {
     if (e.aux) st4(e.aux, (long)row * e.ldaux + col, e.aux_dtype, v);
-#pragma unroll
-    for (int c = 0; c < 4; ++c) v[c] = act_fwd(e.act, v[c]);
+    act_fwd_n<4>(e.act, v);
     drop4k(k, didx, v);
     st4(p.C, cidx, p.c_dtype, v);
   } else if constexpr (KIND == EA_EPI_RESID) {
@@ -333,8 +332,7 @@ EA_DEV void epi_four_pre(const GemmP& p, const EpiK& k, int z, int zb, int zh, i
     st4(p.C, cidx, EA_F32, v);
   } else {
     drop4k(k, didx, v);
-#pragma unroll
-    for (int c = 0; c < 4; ++c) v[c] *= act_bwd(e.act, o[c]);
+    act_bwd_mul_n<4>(e.act, v, o);
     st4(p.C, cidx, p.c_dtype, v);
   }
 }
@@ -393,8 +391,7 @@ EA_DEV void epi_eight_pre(const GemmP& p, const EpiK& k, int z, int zb, int zh, 
     st8(p.C, cidx, p.c_dtype, v);
   } else if constexpr (KIND == EA_EPI_ACT) {
     if (e.aux) st8(e.aux, (long)row * e.ldaux + col, e.aux_dtype, v);
-#pragma unroll
-    for (int c = 0; c < 8; ++c) v[c] = act_fwd(e.act, v[c]);
+    act_fwd_n<8>(e.act, v);
     drop8k(k, didx, v);
     st8(p.C, cidx, p.c_dtype, v);
   } else if constexpr (KIND == EA_EPI_RESID) {
@@ -404,8 +401,7 @@ EA_DEV void epi_eight_pre(const GemmP& p, const EpiK& k, int z, int zb, int zh, 
     st8(p.C, cidx, EA_F32, v);
   } else {
     drop8k(k, didx, v);
-#pragma unroll
-    for (int c = 0; c < 8; ++c) v[c] *= act_bwd(e.act, o[c]);
+    act_bwd_mul_n<8>(e.act, v, o);
     st8(p.C, cidx, p.c_dtype, v);
   }
 }

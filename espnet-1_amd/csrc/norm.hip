@@ -724,10 +724,11 @@ __global__ __launch_bounds__(256) void bn_apply_act_vec_kernel(int rows, int C, 
     const float4 mu = *(const float4*)(mean + c), rs = *(const float4*)(rstd + c);
     const float4 gg = *(const float4*)(g + c), bb = *(const float4*)(b + c);
     float o[4];
-    o[0] = act_fwd(act, (v.x - mu.x) * rs.x * gg.x + bb.x);
-    o[1] = act_fwd(act, (v.y - mu.y) * rs.y * gg.y + bb.y);
-    o[2] = act_fwd(act, (v.z - mu.z) * rs.z * gg.z + bb.z);
-    o[3] = act_fwd(act, (v.w - mu.w) * rs.w * gg.w + bb.w);
+    o[0] = (v.x - mu.x) * rs.x * gg.x + bb.x;
+    o[1] = (v.y - mu.y) * rs.y * gg.y + bb.y;
+    o[2] = (v.z - mu.z) * rs.z * gg.z + bb.z;
+    o[3] = (v.w - mu.w) * rs.w * gg.w + bb.w;
+    act_fwd_n<4>(act, o);
     vst4(z + i * 4, o);
   }
 }
@@ -749,12 +750,18 @@ __global__ __launch_bounds__(256) void bn_bwd_partial_vec_kernel(int rows, int C
     float mu[4], rs[4], gg[4], bb[4];
     vld4(mean + c, mu); vld4(rstd + c, rs); vld4(g + c, gg); vld4(b + c, bb);
     auto accum = [&](const float (&yv)[4], const float (&dv)[4]) {
+      float xh[4], h[4], dh[4];
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
-        const float xh = (yv[k] - mu[k]) * rs[k];
-        const float dh = dv[k] * act_bwd(act, xh * gg[k] + bb[k]);
-        s1[k] += dh * xh;
-        s2[k] += dh;
+        xh[k] = (yv[k] - mu[k]) * rs[k];
+        h[k] = xh[k] * gg[k] + bb[k];
+        dh[k] = dv[k];
+      }
+      act_bwd_mul_n<4>(act, dh, h);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        s1[k] += dh[k] * xh[k];
+        s2[k] += dh[k];
       }
     };
     int r = r0 + w;
@@ -805,12 +812,16 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_vec_kernel(int rows, int C, 
     vld4(y + i * 4, yv); vld4(dz + i * 4, dv);
     vld4(mean + c, mu); vld4(rstd + c, rs); vld4(g + c, gg); vld4(b + c, bb);
     vld4(dgamma + c, dg); vld4(dbeta + c, db);
+    float xh[4], h[4], dh[4];
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
-      const float xh = (yv[k] - mu[k]) * rs[k];
-      const float dh = dv[k] * act_bwd(act, xh * gg[k] + bb[k]);
-      o[k] = gg[k] * rs[k] * (dh - db[k] * invn - xh * dg[k] * invn);
+      xh[k] = (yv[k] - mu[k]) * rs[k];
+      h[k] = xh[k] * gg[k] + bb[k];
+      dh[k] = dv[k];
     }
+    act_bwd_mul_n<4>(act, dh, h);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) o[k] = gg[k] * rs[k] * (dh[k] - db[k] * invn - xh[k] * dg[k] * invn);
     vst4(dy + i * 4, o);
   }
 }
