@@ -150,7 +150,7 @@ def pmc_traffic():
             d = json.load(f)
         from espnet_amd._lib import GEMM_PIPE
         # measured on these sources AND on the kernel this build reports as the roofline kernel
-        kernel = "gemm_pipe<true, true, 1, 256>" if GEMM_PIPE else "gemm_bf16_lds<256, 256"
+        kernel = "gemm_pipe<true, true, 1, 256" if GEMM_PIPE else "gemm_bf16_lds<256, 256"
         same = d.get("gemm_src_sha") == gemm_src_sha() and kernel in d.get("kernel", "")
         return int(d["traffic_bytes_per_launch"]), os.path.relpath(PMC_FILE, ROOT), same
     except (OSError, KeyError, ValueError):
