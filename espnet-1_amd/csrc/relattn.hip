@@ -19,6 +19,12 @@
 // (z*T1 + i)*T2 + j), regenerated in backward.
 #include "common.h"
 
+// timing experiments only (scripts/build_def.py): bit 1 no dBD stores, 2 no d(q+v) term, 4 K/V/band
+// staged for the first chunk only, 8 no BD gather in attn_bwdq
+#ifndef ATTN_EXP
+#define ATTN_EXP 0
+#endif
+
 namespace {
 
 constexpr int DK = 64;     // head dim
@@ -452,7 +458,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwdq_kernel(AttnP a) {
   const int g = lane >> 4, lc = lane & 15;
   const int kl = a.klen ? (int)min((long long)a.T2, a.klen[b]) : a.T2;
   const uint64_t seed = a.p > 0.f ? ea_salted(a.seed, a.salt) : 0;
-  const bool with_dqv = REL && (a.flags & 1);
+  const bool with_dqv = REL && (a.flags & 1) && !(ATTN_EXP & 2);
   char* ws = sm + Q_WS + w * Q_WSZ;
   float* bds = (float*)ws;
   char* band = ws;                // dS on its band (after the gather has read bds)
@@ -515,7 +521,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwdq_kernel(AttnP a) {
   const float sl2 = a.scale * LOG2E;
   const int kend = a.causal ? min(kl, i0 + QB) : kl;
   const int nch = (kend + KC - 1) / KC;
-  bf16* dbd_h = REL && a.dbd ? a.dbd + ((long)h * a.B + b) * a.T1 * a.lddbd : nullptr;
+  bf16* dbd_h = REL && a.dbd && !(ATTN_EXP & 1) ? a.dbd + ((long)h * a.B + b) * a.T1 * a.lddbd : nullptr;
   if (dbd_h) {
     // zeros off the part of each row the chunk loop writes (r < T-1-i, r >= T-1-i+jcov), in
     // whole 8-column segments (lddbd % 8 == 0, 16-B aligned rows): a segment straddling the
@@ -570,10 +576,12 @@ __global__ __launch_bounds__(256, 2) void attn_bwdq_kernel(AttnP a) {
       for (int r = 0; r < 4; ++r) mw[r] = make_uint2(~0u, ~0u);
     }
     __syncthreads();  // the setup images / previous chunk's images are no longer read
+    if (!(ATTN_EXP & 4) || j0 == 0) {
     stage_km<KC>(sm + Q_K, gK, a.ldk, j0, a.T2, tid);
     stage_km<KC>(sm + Q_V, gV, a.ldv, j0, a.T2, tid);
     const int rb = a.T1 - 1 - (i0 + QB - 1) + j0;  // first positional row of the block's band
     if (REL) stage_km<144>(sm + Q_P, gP, a.ldp, rb, 2 * a.T1 - 1, tid);
+    }
     __syncthreads();
     f32x4 s[4], dp[4];
 #pragma unroll
@@ -582,7 +590,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwdq_kernel(AttnP a) {
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks) s[t] = mfma(qa[ks], km_frag(sm + Q_K, 16 * t, ks, lane), s[t]);
     }
-    if (REL) {
+    if (REL && !(ATTN_EXP & 8)) {
 #pragma unroll
       for (int t = 0; t < 5; ++t) {
         f32x4 bd = (f32x4){0.f, 0.f, 0.f, 0.f};
