@@ -184,8 +184,15 @@ struct AttnP {
   bf16* wsQv; long ldqvw;    //   q + v rows (rel-pos: qv_out when given, else workspace)
   uint32_t* dmask; int ldm;  // dropout keep bits [z*T1 + i][ldm words], bit j&31 of word j>>5:
                              // written by the forward, read by the backward (else rehashed)
+  char* wsDummy;             // 1 KiB sink for the pipelined dQ pass's out-of-range dbd stores
 };
 // ldm >= 2 * ceil(T2 / 64): a 64-key chunk is the word pair (j0 >> 5, +1)
+
+// Shifted dbd layout of the pipelined dQ pass (flags bit 1): logical column r of every row at
+// physical column r + shift, shift >= 15 with (T1 + shift) % 8 == 0, so that the band window of
+// any 16-row wave starts on a 16-B boundary; row stride ea_attn_dbd_ld(T1) (multiple of 8).
+__host__ __device__ inline int ea_attn_dbd_shift_dev(int T1) { return 15 + ((8 - (T1 + 15) % 8) % 8); }
+__host__ __device__ inline long ea_attn_dbd_ld(int T1) { return (2L * T1 - 1 + ea_attn_dbd_shift_dev(T1) + 7) / 8 * 8; }
 
 // ------------------------------------------------------------------------------ forward
 constexpr int F_K = 0, F_V = F_K + KC * 128, F_P = F_V + KC * 128;  // K, V chunk, P band (128 rows)
@@ -708,6 +715,511 @@ __global__ __launch_bounds__(256, 2) void attn_bwdq_kernel(AttnP a) {
   }
 }
 
+// ------------------------------------------------------------- attn_bwdq, pipelined (v2)
+// The dQ pass of attn_bwdq_kernel restructured around the latency it paid per key chunk:
+//  * K and V chunks are double-buffered and the positional rows live in a 208-row ring (a
+//    chunk's band is 144 rows, the next chunk adds 64); every image is filled by LDS-DMA one
+//    chunk ahead, so a chunk costs one barrier and no staging registers;
+//  * the BD diagonal gather is a ds_bpermute per (band tile, register) instead of an LDS
+//    image written and re-read;
+//  * dS is laid onto a per-wave band window whose column c is positional row Rw + c for all
+//    16 rows of the wave, so d(q+v) = window . p needs K = 64 per chunk (the window's last 16
+//    columns carry into the next window) and the first 64 columns are final: they leave as
+//    16-B stores into dbd rows shifted by ea_attn_dbd_shift(T1) columns (flags bit 1), with
+//    the shift chosen so that every window starts on a 16-B boundary.
+// Dropout keep words come from the forward's bit mask (prefetched a chunk ahead), else from
+// the counter hash.  Summation order differs from attn_bwdq_kernel only in d(q+v) (64-column
+// windows instead of 96), so dq / bias partials agree to f32 rounding, dbd bit for bit.
+constexpr int RING = 208;  // band ring rows (13 x 16)
+template <bool REL>
+struct Q2 {
+  static constexpr int K = 0, V = K + 2 * KC * 128;                 // [2][64 rows] each
+  static constexpr int P = V + 2 * KC * 128;                        // ring [208 rows]
+  static constexpr int WS = P + (REL ? RING * 128 : 0);             // per wave: window + dS^T
+  static constexpr int WIN = REL ? 16 * 192 : 0;                    // [16][96] bf16 window
+  static constexpr int WSZ = WIN + 64 * 32;
+  static constexpr int D = WS + NWAVE * WSZ;                        // D_i, lse_i (64 each)
+  static constexpr int LDS = D + 2 * QB * 4;
+};
+static_assert(Q2<true>::LDS <= 80 * 1024 + 512, "two workgroups per CU");
+
+// ds_read_b64_tr_b16 as inline asm (the builtin makes hipcc drain vmcnt while an LDS-DMA is in
+// flight); the caller waits lgkmcnt(0) before using the result
+EA_DEV s16x4 tr_asm(const char* p) {
+  s16x4 v;
+  const uint32_t a = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) char*)p;
+  asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(v) : "v"(a) : "memory");
+  return v;
+}
+// LDS reads as inline asm too: hipcc cannot tell an image being read from the one an LDS-DMA is
+// filling and would drain vmcnt in front of every compiler-visible LDS read
+EA_DEV bf16x8 ld128_asm(const char* p) {
+  bf16x8 v;
+  const uint32_t a = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) char*)p;
+  asm volatile("ds_read_b128 %0, %1" : "=v"(v) : "v"(a) : "memory");
+  return v;
+}
+EA_DEV uint2 ld64_asm(const char* p) {
+  __attribute__((ext_vector_type(2))) unsigned v;
+  const uint32_t a = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) char*)p;
+  asm volatile("ds_read_b64 %0, %1" : "=v"(v) : "v"(a) : "memory");
+  return make_uint2(v.x, v.y);
+}
+EA_DEV uint32_t lds_addr(const char* p) { return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) char*)p; }
+EA_DEV void st16_asm(char* p, bf16 x) {
+  const uint32_t v = (uint32_t)__builtin_bit_cast(unsigned short, x);
+  asm volatile("ds_write_b16 %0, %1" ::"v"(lds_addr(p)), "v"(v) : "memory");
+}
+typedef __attribute__((ext_vector_type(2))) unsigned u32x2;
+typedef __attribute__((ext_vector_type(4))) unsigned u32x4;
+EA_DEV void st64_asm(char* p, uint2 v) {
+  const u32x2 x = {v.x, v.y};
+  asm volatile("ds_write_b64 %0, %1" ::"v"(lds_addr(p)), "v"(x) : "memory");
+}
+EA_DEV void st128_asm(char* p, uint4 v) {
+  const u32x4 x = {v.x, v.y, v.z, v.w};
+  asm volatile("ds_write_b128 %0, %1" ::"v"(lds_addr(p)), "v"(x) : "memory");
+}
+EA_DEV bf16x8 km_frag_asm(const char* img, int r0, int ks, int lane) {
+  return ld128_asm(img + km_off(r0 + (lane & 15), ks * 4 + (lane >> 4)));
+}
+EA_DEV bf16x8 band_frag_asm(const char* img, int ks, int lane) {
+  const int r = lane & 15, c = ks * 4 + (lane >> 4);
+  return ld128_asm(img + r * 192 + ((c ^ ((r >> 2) & 3)) << 4));
+}
+// wait for the asm LDS reads; the sched_barrier keeps their consumers (MFMAs the compiler sees
+// no memory dependence for) from being scheduled above the wait
+EA_DEV void lgkm0() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+}
+EA_DEV uint2 gld64_asm(const void* p) {  // untracked global load: the caller waits vmcnt itself
+  __attribute__((ext_vector_type(2))) unsigned v;
+  asm volatile("global_load_dwordx2 %0, %1, off" : "=v"(v) : "v"(p) : "memory");
+  return make_uint2(v.x, v.y);
+}
+template <int N>
+EA_DEV void vmcnt_le() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+  __builtin_amdgcn_sched_barrier(0);
+}
+EA_DEV void vmcnt_le_rt(int n) {  // n in {0, 2, 4, 6}
+  if (n >= 6) vmcnt_le<6>();
+  else if (n >= 4) vmcnt_le<4>();
+  else if (n >= 2) vmcnt_le<2>();
+  else vmcnt_le<0>();
+}
+EA_DEV void bar() {
+  lgkm0();
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+// km_frag_tr over image rows {k0 + 8(g&1) + 4h + q : g < 2} and {k1 + ... : g >= 2} (two 16-row
+// groups that need not be adjacent: ring wrap)
+EA_DEV bf16x8 km_tr_rows(const char* img, int k0, int k1, int n0, int lane) {
+  const int i = lane & 15, q = i >> 2, p = i & 3, g = lane >> 4;
+  const int col = n0 + 4 * p;
+  const int kb = (g >> 1) ? k1 : k0;
+  union { bf16x8 v; s16x4 h[2]; } out;
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int row = kb + 8 * (g & 1) + 4 * h + q;
+    out.h[h] = tr_asm(img + km_off(row, col >> 3) + (col & 7) * 2);
+  }
+  return out.v;
+}
+EA_DEV bf16x8 dst_frag_asm(const char* img, int kb, int lane) {
+  const int i = lane & 15, q = i >> 2, p = i & 3, g = lane >> 4;
+  union { bf16x8 v; s16x4 h[2]; } out;
+#pragma unroll
+  for (int h = 0; h < 2; ++h) out.h[h] = tr_asm(img + (kb + 8 * g + 4 * h + q) * 32 + p * 8);
+  return out.v;
+}
+// LDS-DMA of km-image rows [ir, ir+8) (ir % 8 == 0) from global rows src + (r0 + 0..7)*ld (64
+// bf16 columns), rows clamped into [0, rlim): one instruction per wave, lane L fills row
+// ir + (L >> 3), 16-B slot L & 7 (= logical chunk (L & 7) ^ km_swz(row))
+EA_DEV void km_dma8(char* img, int ir, const bf16* src, long ld, int r0, int rlim, int lane) {
+  const int rr = lane >> 3, ch = (lane & 7) ^ km_swz(ir + rr);
+  const int r = min(max(r0 + rr, 0), rlim - 1);
+  __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)(src + (long)r * ld + ch * 8),
+                                   (__attribute__((address_space(3))) void*)(img + ir * 128), 16, 0, 0);
+}
+
+// MM: dropout keep decisions — 0 none (p = 0), 1 the forward's bit mask, 2 the counter hash
+template <bool REL, int MM>
+__global__ __launch_bounds__(256, 2) void attn_bwdq2_kernel(AttnP a) {
+  using L = Q2<REL>;
+  __shared__ __attribute__((aligned(16))) char sm[L::LDS];
+  const int nqb = (a.T1 + QB - 1) / QB;
+  const int z = blockIdx.x / nqb, qb = blockIdx.x % nqb;
+  const int b = z / a.H, h = z % a.H;
+  const int i0 = qb * QB;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int g = lane >> 4, lc = lane & 15;
+  const int kl = a.klen ? (int)min((long long)a.T2, a.klen[b]) : a.T2;
+  const uint64_t seed = a.p > 0.f ? ea_salted(a.seed, a.salt) : 0;
+  const bool with_dqv = REL && (a.flags & 1);
+  char* win = sm + L::WS + w * L::WSZ;  // band window (REL)
+  char* dst = win + L::WIN;
+  float* Dv = (float*)(sm + L::D);
+  float* Lv = Dv + QB;
+  const int kend = a.causal ? min(kl, i0 + QB) : kl;
+  const int nch = (kend + KC - 1) / KC;
+  const int rlimP = 2 * a.T1 - 1;
+  const int rb0 = a.T1 - 1 - (i0 + QB - 1);  // chunk 0's first positional row (ring position 0)
+  const bf16* kh_ = a.k + (long)b * a.T2 * a.ldk + h * DK;
+  const bf16* vh_ = a.v + (long)b * a.T2 * a.ldv + h * DK;
+  const bf16* ph_ = REL ? a.pp + h * DK : nullptr;
+  // chunk c's K / V rows into buffer c & 1; ring rows [x0, x0 + 8n) (relative to rb0) by groups
+  auto dma_kv = [&](int c) {
+    char* kb = sm + L::K + (c & 1) * KC * 128;
+    char* vb = sm + L::V + (c & 1) * KC * 128;
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int gi = w + 4 * u;
+      km_dma8(kb, 8 * gi, kh_, a.ldk, 64 * c + 8 * gi, a.T2, lane);
+      km_dma8(vb, 8 * gi, vh_, a.ldv, 64 * c + 8 * gi, a.T2, lane);
+    }
+  };
+  auto dma_ring = [&](int x0, int ngrp) {  // groups gi = w, w+4, ... < ngrp
+    for (int gi = w; gi < ngrp; gi += 4) {
+      const int x = x0 + 8 * gi;
+      km_dma8(sm + L::P, x % RING, ph_, a.ldp, rb0 + x, rlimP, lane);
+    }
+  };
+  if (nch > 0) {
+    dma_kv(0);
+    if (REL) dma_ring(0, 18);
+  }
+
+  // this wave's 16 rows of Q + u, Q + v and dO as A fragments; D_i and lse_i.  Setup images in
+  // the second K / V buffers and the window area (free until chunk 1's DMA / chunk 0's window)
+  char* img_qu = sm + L::K + KC * 128;
+  char* img_qv = sm + L::V + KC * 128;
+  char* img_do = sm + L::WS;  // the per-wave areas: 4 x 5 KiB (rel-pos) or 4 x 2 KiB
+  static_assert(NWAVE * L::WSZ >= QB * 128, "dO image fits the per-wave areas");
+  bf16x8 qa[2], qv[2], doa[2];
+  {
+    const bf16* qsrc = a.q + (long)b * a.T1 * a.ldq + h * DK;
+    km_stage_out(img_qu, qsrc, a.ldq, i0, QB, a.T1, a.bu ? a.bu + h * DK : nullptr,
+                 a.wsQu + (long)b * a.T1 * a.ldqu + h * DK, a.ldqu, tid, 256);
+    if (REL)
+      km_stage_out(img_qv, qsrc, a.ldq, i0, QB, a.T1, a.bv + h * DK,
+                   a.wsQv + (long)b * a.T1 * a.ldqvw + h * DK, a.ldqvw, tid, 256);
+    km_stage(img_do, a.dO + (long)b * a.T1 * a.lddo + h * DK, a.lddo, i0, QB, a.T1, tid, 256);
+    {  // D_i = dO_i . O_i: 4 threads per row, 16 columns each
+      const int row = tid >> 2, qd = tid & 3, i = i0 + row;
+      float d = 0.f;
+      if (i < a.T1) {
+        const bf16* dr = a.dO + ((long)b * a.T1 + i) * a.lddo + h * DK + qd * 16;
+        const bf16* orow = a.o + ((long)b * a.T1 + i) * a.ldo + h * DK + qd * 16;
+#pragma unroll
+        for (int hf = 0; hf < 2; ++hf) {
+          union { uint4 u; bf16 e[8]; } x, y;
+          x.u = *(const uint4*)(dr + hf * 8);
+          y.u = *(const uint4*)(orow + hf * 8);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) d += (float)x.e[e] * (float)y.e[e];
+        }
+      }
+      d += __shfl_xor(d, 1, 64);
+      d += __shfl_xor(d, 2, 64);
+      if (qd == 0) {
+        Dv[row] = d;
+        Lv[row] = i < a.T1 ? a.lse[(long)z * a.T1 + i] * LOG2E : INFINITY;
+        if (i < a.T1) a.wsD[(long)z * a.T1 + i] = d;
+      }
+    }
+    bar();
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      qa[ks] = km_frag(img_qu, 16 * w, ks, lane);
+      if (REL) qv[ks] = km_frag(img_qv, 16 * w, ks, lane);
+      doa[ks] = km_frag(img_do, 16 * w, ks, lane);
+    }
+  }
+  const int ibase = i0 + 16 * w + 4 * g;  // query row of register r: ibase + r
+  float Dr[4], Lr[4];
+  int lim[4];  // key j of row r is valid iff j < lim[r]
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int i = ibase + r;
+    Dr[r] = Dv[16 * w + 4 * g + r];
+    Lr[r] = Lv[16 * w + 4 * g + r];
+    lim[r] = i < a.T1 ? (a.causal ? min(kl, i + 1) : kl) : 0;
+  }
+  bar();  // setup images read: the window area and the second buffers are free
+  if (REL) {  // zero this wave's window
+    const uint4 zero = make_uint4(0u, 0u, 0u, 0u);
+#pragma unroll
+    for (int c = 0; c < 3; ++c) *(uint4*)(win + (c * 64 + lane) * 16) = zero;
+  }
+  const float sl2 = a.scale * LOG2E;
+  bf16* dbd_h = REL && a.dbd ? a.dbd + ((long)h * a.B + b) * a.T1 * a.lddbd : nullptr;
+  // window start (physical dbd column) of chunk 0 for this wave's rows: Rw + shift, 8-aligned
+  const int shift = REL ? ea_attn_dbd_shift_dev(a.T1) : 0;
+  const int W0 = a.T1 - 16 - (i0 + 16 * w) + shift;
+  const float dsc = MM ? 1.f / (1.f - a.p) : 1.f;
+  // keep words of rows ibase + r (clamped to the last row: always four loads per chunk)
+  const uint32_t* mrow = a.dmask + ((long)z * a.T1 + min(ibase, a.T1 - 1)) * a.ldm;
+  // dbd stores per chunk: two 16-B pieces per lane (out-of-range rows to the dummy sink)
+  const int nst = dbd_h ? 2 : 0;
+
+  f32x4 dqu[4], dqv[4];
+#pragma unroll
+  for (int n = 0; n < 4; ++n) dqu[n] = dqv[n] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  const int pb = 48 - 16 * w;  // this wave's first band row relative to the chunk's band start
+  for (int c = 0; c < nch; ++c) {
+    const int j0 = c * KC;
+    // this chunk's images landed (older than the mask loads of this chunk and the previous
+    // chunk's dbd stores), all waves done with the previous chunk
+    // this chunk's images landed (only the previous chunk's dbd stores are younger), all waves
+    // done with the previous chunk
+    vmcnt_le_rt(c == 0 ? 0 : nst);
+    bar();
+    uint2 mw[4];
+    if (MM == 1) {  // issued before the prefetch: the dS phase waits for these four only
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int ro = ibase + r < a.T1 ? r * a.ldm : (a.T1 - 1 - min(ibase, a.T1 - 1)) * a.ldm;
+        mw[r] = gld64_asm(mrow + ro + (j0 >> 5));
+      }
+    }
+    const int ndma = c + 1 < nch ? (REL ? 6 : 4) : 0;  // LDS-DMA issued after the mask loads
+    if (c + 1 < nch) {
+      dma_kv(c + 1);
+      if (REL) dma_ring(64 * c + 144, 8);
+    }
+    if (MM == 2) {
+      const uint32_t key = ea_seed_key(seed), thr = ea_drop_thr(a.p);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const uint64_t row = (uint64_t)z * a.T1 + ibase + r;
+        uint32_t x = 0u, y = 0u;
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+          const uint32_t bit = (uint32_t)attn_keep(key, thr, row, a.T2, j0 + 16 * t + lc) << (16 * (t & 1) + lc);
+          if (t < 2) x |= bit; else y |= bit;
+        }
+        mw[r] = make_uint2(x, y);
+      }
+    }
+    const char* kimg = sm + L::K + (c & 1) * KC * 128;
+    const char* vimg = sm + L::V + (c & 1) * KC * 128;
+    const char* ring = sm + L::P;
+    f32x4 s[4], dp[4];
+    {
+      bf16x8 kf[4][2];
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) kf[t][ks] = km_frag_asm(kimg, 16 * t, ks, lane);
+      lgkm0();
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        s[t] = (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) s[t] = mfma(qa[ks], kf[t][ks], s[t]);
+      }
+    }
+    if (REL) {
+      // BDfull (16 x 80) over ring rows 64c + pb + [0, 80), gathered onto the diagonal
+      f32x4 bd[5];
+      {
+        bf16x8 pf[5][2];
+#pragma unroll
+        for (int t = 0; t < 5; ++t) {
+          const int rp = (64 * c + pb + 16 * t) % RING;
+#pragma unroll
+          for (int ks = 0; ks < 2; ++ks) pf[t][ks] = km_frag_asm(ring, rp, ks, lane);
+        }
+        lgkm0();
+#pragma unroll
+        for (int t = 0; t < 5; ++t) {
+          bd[t] = (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+          for (int ks = 0; ks < 2; ++ks) bd[t] = mfma(qv[ks], pf[t][ks], bd[t]);
+        }
+      }
+      // (one bpermute per band tile and register: the two calls of neighbouring t are the same
+      // expression; no array of gathered values, which hipcc turned into a scratch-indexed load)
+      // output (il = 4g + r, jl = 16t + lc) reads BDfull column 16t + lc + 15 - il: tile t (or
+      // t + 1 past a tile edge) of lane 16g + ((lc + 15 - il) & 15)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int sft = lc + 15 - 4 * g - r;
+        const int src = (16 * g + (sft & 15)) * 4;
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+          const float lo = __int_as_float(__builtin_amdgcn_ds_bpermute(src, __float_as_int(bd[t][r])));
+          const float hi = __int_as_float(__builtin_amdgcn_ds_bpermute(src, __float_as_int(bd[t + 1][r])));
+          s[t][r] += sft >= 16 ? hi : lo;
+        }
+      }
+    }
+    {
+      bf16x8 vf[4][2];
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) vf[t][ks] = km_frag_asm(vimg, 16 * t, ks, lane);
+      lgkm0();
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        dp[t] = (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) dp[t] = mfma(doa[ks], vf[t][ks], dp[t]);
+      }
+    }
+    // dS (scaled), in place of s
+    if (MM == 1) vmcnt_le_rt(ndma);  // the mask words (older than this chunk's prefetch)
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const int j = j0 + 16 * t + lc;
+        const float e = __builtin_amdgcn_exp2f(fmaf(s[t][r], sl2, -Lr[r]));
+        const float P = j < lim[r] ? e : 0.f;
+        float kp = 1.f;
+        if (MM) kp = (((t < 2 ? mw[r].x : mw[r].y) >> (16 * (t & 1) + lc)) & 1u) ? dsc : 0.f;
+        s[t][r] = (P * a.scale) * fmaf(dp[t][r], kp, -Dr[r]);
+      }
+    // dS^T image (4 queries per 8-B write); (rel-pos) dS onto the window, column 15 - il + jl
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const uint2 v = make_uint2(pack_bf16x2(s[t][0], s[t][1]), pack_bf16x2(s[t][2], s[t][3]));
+      st64_asm(dst + (16 * t + lc) * 32 + g * 8, v);
+      if (REL && (with_dqv || dbd_h)) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int il = 4 * g + r;
+          st16_asm(win + band_off(il, 15 - il + 16 * t + lc), (bf16)s[t][r]);
+        }
+      }
+    }
+    // dQu += dS . K
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      const bf16x8 af = dst_frag_asm(dst, 32 * ks, lane);
+      bf16x8 bf[4];
+#pragma unroll
+      for (int n = 0; n < 4; ++n) bf[n] = km_tr_rows(kimg, 32 * ks, 32 * ks + 16, 16 * n, lane);
+      lgkm0();
+#pragma unroll
+      for (int n = 0; n < 4; ++n) dqu[n] = mfma(af, bf[n], dqu[n]);
+    }
+    if (REL && (with_dqv || dbd_h)) {
+      if (with_dqv) {  // dQv += window[:, 0:64] . p[ring rows 64c + pb + 0..63]
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) {
+          const bf16x8 af = band_frag_asm(win, ks, lane);
+          const int r0 = (64 * c + pb + 32 * ks) % RING, r1 = (64 * c + pb + 32 * ks + 16) % RING;
+          bf16x8 bf[4];
+#pragma unroll
+          for (int n = 0; n < 4; ++n) bf[n] = km_tr_rows(ring, r0, r1, 16 * n, lane);
+          lgkm0();
+#pragma unroll
+          for (int n = 0; n < 4; ++n) dqv[n] = mfma(af, bf[n], dqv[n]);
+        }
+      }
+      if (dbd_h) {  // the window's first 64 columns are final: rows i0 + 16w + (q >> 3)
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+          const int q = lane + 64 * u, row = q >> 3, ch = q & 7;
+          const bf16x8 vb = ld128_asm(win + row * 192 + ((ch ^ ((row >> 2) & 3)) << 4));
+          lgkm0();
+          const uint4 v = *(const uint4*)&vb;
+          const int i = i0 + 16 * w + row, col = W0 + j0 + 8 * ch;
+          bf16* dstp = (i < a.T1 && col < a.lddbd) ? dbd_h + (long)i * a.lddbd + col
+                                                  : (bf16*)((char*)a.wsDummy + lane * 16);
+          *(uint4*)dstp = v;
+        }
+      }
+      // carry columns [64, 80) to [0, 16), zero [16, 96)
+      {
+        const int row = lane >> 2, cq = 4 * (lane & 3);
+        const uint2 tail = ld64_asm(win + band_off(row, 64 + cq));
+        lgkm0();
+        const uint4 zero = make_uint4(0u, 0u, 0u, 0u);
+#pragma unroll
+        for (int u = 0; u < 3; ++u) {
+          const int q = lane + 64 * u;
+          if (u < 2 || q < 160) {
+            const int zr = q / 10, zc = 2 + q % 10;
+            st128_asm(win + zr * 192 + ((zc ^ ((zr >> 2) & 3)) << 4), zero);
+          }
+        }
+        st64_asm(win + band_off(row, cq), tail);
+      }
+    }
+  }
+  if (REL && nch > 0 && (with_dqv || dbd_h)) {
+    // the last window's carried tail: columns [0, 16) = positional rows of virtual chunk nch
+    if (with_dqv) {
+      const bf16x8 af = band_frag(win, 0, lane);
+      const int r0 = (64 * nch + pb) % RING, r1 = (64 * nch + pb + 16) % RING;
+      bf16x8 bf[4];
+#pragma unroll
+      for (int n = 0; n < 4; ++n) bf[n] = km_tr_rows(sm + L::P, r0, r1, 16 * n, lane);
+      lgkm0();
+#pragma unroll
+      for (int n = 0; n < 4; ++n) dqv[n] = mfma(af, bf[n], dqv[n]);
+    }
+    if (dbd_h && lane < 32) {
+      const int row = lane >> 1, ch = lane & 1;
+      const uint4 v = *(const uint4*)(win + row * 192 + ((ch ^ ((row >> 2) & 3)) << 4));
+      const int i = i0 + 16 * w + row, col = W0 + nch * KC + 8 * ch;
+      if (i < a.T1 && col < a.lddbd) *(uint4*)(dbd_h + (long)i * a.lddbd + col) = v;
+    }
+  }
+  if (dbd_h) {
+    // zeros outside the windows written above: columns [0, W0) and [W0 + 64 nch + 16, lddbd)
+    const int lo = W0, hi = W0 + nch * KC + (nch > 0 ? 16 : 0);
+    const uint4 zero = make_uint4(0u, 0u, 0u, 0u);
+    for (int il = 0; il < 16; ++il) {
+      const int i = i0 + 16 * w + il;
+      if (i >= a.T1) break;
+      bf16* drow = dbd_h + (long)i * a.lddbd;
+      for (int c0 = 8 * lane; c0 < a.lddbd; c0 += 512)
+        if (c0 < lo || c0 >= hi) *(uint4*)(drow + c0) = zero;
+    }
+  }
+  // dQ (bf16) = dS.K (+ dBD.p); column sums of both terms over this block's rows
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int i = ibase + r;
+    if (i >= a.T1) continue;
+    bf16* qrow = a.dq + ((long)b * a.T1 + i) * a.lddq + h * DK;
+#pragma unroll
+    for (int n = 0; n < 4; ++n) qrow[16 * n + lc] = (bf16)(dqu[n][r] + (with_dqv ? dqv[n][r] : 0.f));
+  }
+  if (a.bias_part) {
+    bar();  // chunk images no longer read: the column-sum exchange reuses the K buffers
+    float* red = (float*)(sm + L::K);  // [2][NWAVE][64]
+#pragma unroll
+    for (int n = 0; n < 4; ++n) {
+      float su = (dqu[n][0] + dqu[n][1]) + (dqu[n][2] + dqu[n][3]);
+      float sv = (dqv[n][0] + dqv[n][1]) + (dqv[n][2] + dqv[n][3]);
+      su += __shfl_xor(su, 16, 64);
+      sv += __shfl_xor(sv, 16, 64);
+      su += __shfl_xor(su, 32, 64);
+      sv += __shfl_xor(sv, 32, 64);
+      if (g == 0) {
+        red[w * DK + 16 * n + lc] = su;
+        red[(NWAVE + w) * DK + 16 * n + lc] = sv;
+      }
+    }
+    bar();
+    if (tid < 2 * DK) {
+      const int which = tid / DK, c = tid % DK;
+      const float* rr = red + which * NWAVE * DK;
+      const float v = (rr[c] + rr[DK + c]) + (rr[2 * DK + c] + rr[3 * DK + c]);
+      const long prow = (long)which * a.B * nqb + (long)b * nqb + qb;
+      if (which == 0 || REL) a.bias_part[prow * a.ldpart + h * DK + c] = v;
+    }
+  }
+}
+
 // attn_bwdkv shared memory
 constexpr int V_QU = 0, V_QV = V_QU + BQ * 128, V_DO = V_QV + BQ * 128, V_P = V_DO + BQ * 128;
 constexpr int V_D = V_P + 96 * 128;               // D_i, lse_i*log2e (32 each), keep words [2][32]
@@ -954,25 +1466,34 @@ extern "C" int ea_attn_fused_fwd(int B, int H, int T1, int T2, int dk, const voi
                             o, ldo, lse, nullptr, 0, stream);
 }
 
-static int attn_bwd_launch(AttnP& a, bool rel, hipStream_t st) {
+static int attn_bwd_launch(AttnP& a, bool rel, bool v2, hipStream_t st) {
   const int nqb = (a.T1 + QB - 1) / QB, nkb = (a.T2 + 63) / 64;
   const dim3 gq(a.B * a.H * nqb), gkv(a.B * a.H * nkb);
+  const int mm = a.p > 0.f ? (a.dmask ? 1 : 2) : 0;
   if (rel) {
-    hipLaunchKernelGGL(attn_bwdq_kernel<true>, gq, dim3(256), 0, st, a);
+    if (v2 && mm == 0) hipLaunchKernelGGL((attn_bwdq2_kernel<true, 0>), gq, dim3(256), 0, st, a);
+    else if (v2 && mm == 1) hipLaunchKernelGGL((attn_bwdq2_kernel<true, 1>), gq, dim3(256), 0, st, a);
+    else if (v2) hipLaunchKernelGGL((attn_bwdq2_kernel<true, 2>), gq, dim3(256), 0, st, a);
+    else hipLaunchKernelGGL(attn_bwdq_kernel<true>, gq, dim3(256), 0, st, a);
     hipLaunchKernelGGL(attn_bwdkv_kernel<true>, gkv, dim3(256), 0, st, a);
   } else {
-    hipLaunchKernelGGL(attn_bwdq_kernel<false>, gq, dim3(256), 0, st, a);
+    if (v2 && mm == 0) hipLaunchKernelGGL((attn_bwdq2_kernel<false, 0>), gq, dim3(256), 0, st, a);
+    else if (v2 && mm == 1) hipLaunchKernelGGL((attn_bwdq2_kernel<false, 1>), gq, dim3(256), 0, st, a);
+    else if (v2) hipLaunchKernelGGL((attn_bwdq2_kernel<false, 2>), gq, dim3(256), 0, st, a);
+    else hipLaunchKernelGGL(attn_bwdq_kernel<false>, gq, dim3(256), 0, st, a);
     hipLaunchKernelGGL(attn_bwdkv_kernel<false>, gkv, dim3(256), 0, st, a);
   }
   EA_LAUNCH_CHECK();
   return 0;
 }
 
-static long attn_ws_layout(int B, int H, int T1, long* qu_off, long* qv_off) {
+static long attn_ws_layout(int B, int H, int T1, long* qu_off, long* qv_off, long* dummy_off = nullptr) {
   const long d = (long)B * H * T1 * 4, q = (long)B * T1 * H * DK * 2;
   *qu_off = (d + 255) / 256 * 256;
   *qv_off = *qu_off + (q + 255) / 256 * 256;
-  return *qv_off + q;
+  const long du = *qv_off + (q + 255) / 256 * 256;
+  if (dummy_off) *dummy_off = du;
+  return du + 1024;
 }
 
 extern "C" int ea_attn_fused_bwd_ws_bytes(int B, int H, int T1, long* bytes) {
@@ -992,14 +1513,20 @@ extern "C" int ea_attn_fused_bwd2(int B, int H, int T1, int T2, int dk, const vo
   EA_ENTRY();
   EA_CHECK_ARG(dk == DK && B >= 1 && H >= 1 && T1 >= 1 && T2 >= 1);
   EA_CHECK_ARG(!pp || (T1 == T2 && bv != nullptr));
-  EA_CHECK_ARG(!dbd || (pp && lddbd >= 2 * T1 - 1 && lddbd % 8 == 0 && (uintptr_t)dbd % 16 == 0));
+  EA_CHECK_ARG(flags >= 0 && flags <= 7 && !((flags & 2) && (flags & 4)));
+  // flags bit 1: pipelined dQ pass, dbd in the shifted layout; bit 2: the original dQ pass
+  // (A/B); neither: the original pass when dbd is given (unshifted layout), else the pipelined
+  const bool v2 = (flags & 2) || (!(flags & 4) && !dbd);
+  const long ldmin = (flags & 2) ? ea_attn_dbd_ld(T1) : 2L * T1 - 1;
+  EA_CHECK_ARG(!dbd || (pp && lddbd >= ldmin && lddbd % 8 == 0 && (uintptr_t)dbd % 16 == 0));
   EA_CHECK_ARG(ldq % 8 == 0 && ldk % 8 == 0 && ldv % 8 == 0 && ldo % 8 == 0 && lddo % 8 == 0 &&
                (!pp || ldp % 8 == 0) && (!qv_out || (pp && ldqv % 8 == 0)));
   EA_CHECK_ARG(!bias_part || ldpart >= (long)H * DK);
-  EA_CHECK_ARG(flags == 0 || (flags == 1 && pp));
+  EA_CHECK_ARG(!(flags & 1) || pp);
   EA_CHECK_ARG(!dmask || ldm >= 2 * ((T2 + 63) / 64));
-  long qu_off, qv_off;
-  EA_CHECK_ARG(ws != nullptr && (uintptr_t)ws % 256 == 0 && ws_bytes >= attn_ws_layout(B, H, T1, &qu_off, &qv_off));
+  long qu_off, qv_off, du_off;
+  EA_CHECK_ARG(ws != nullptr && (uintptr_t)ws % 256 == 0 &&
+               ws_bytes >= attn_ws_layout(B, H, T1, &qu_off, &qv_off, &du_off));
   AttnP a = make_p(B, H, T1, T2, q, ldq, k, ldk, v, ldv, bu, bv, pp, ldp, klen, causal, scale, p, seed);
   a.o = (bf16*)o; a.ldo = ldo; a.lse = (float*)lse;
   a.dO = (const bf16*)dO; a.lddo = lddo;
@@ -1009,8 +1536,16 @@ extern "C" int ea_attn_fused_bwd2(int B, int H, int T1, int T2, int dk, const vo
   a.flags = flags;
   a.dmask = (uint32_t*)dmask; a.ldm = ldm;
   a.wsD = (float*)ws;
+  a.wsDummy = (char*)ws + du_off;
   a.wsQu = (bf16*)((char*)ws + qu_off); a.ldqu = (long)H * DK;
   if (qv_out) { a.wsQv = (bf16*)qv_out; a.ldqvw = ldqv; }
   else { a.wsQv = (bf16*)((char*)ws + qv_off); a.ldqvw = (long)H * DK; }
-  return attn_bwd_launch(a, pp != nullptr, (hipStream_t)stream);
+  return attn_bwd_launch(a, pp != nullptr, v2, (hipStream_t)stream);
+}
+
+extern "C" int ea_attn_dbd_layout(int T1, int* shift, long* lddbd) {
+  EA_CHECK_ARG(T1 >= 1 && shift != nullptr && lddbd != nullptr);
+  *shift = ea_attn_dbd_shift_dev(T1);
+  *lddbd = ea_attn_dbd_ld(T1);
+  return 0;
 }

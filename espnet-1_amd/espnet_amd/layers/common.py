@@ -57,6 +57,16 @@ def attn_dmask(rows, T2, p, device):
     return torch.empty(rows * ldm, dtype=torch.int32, device=device), ldm
 
 
+def dbd_layout(T1: int):
+    """(shift, row stride) of the band gradient written by the pipelined dQ pass
+    (ea_attn_dbd_layout: logical column r at physical r + shift, 16-B aligned band windows)."""
+    sh, ld = ctypes.c_int(0), ctypes.c_long(0)
+    rc = lib.ea_attn_dbd_layout(int(T1), ctypes.addressof(sh), ctypes.addressof(ld))
+    if rc != 0:
+        raise RuntimeError(f"ea_attn_dbd_layout({T1}) failed: {rc}")
+    return sh.value, ld.value
+
+
 def attn_fused_bwd(*, B, H, T1, T2, q, ldq, k, ldk, v, ldv, bu, bv, pp, ldp, klen, causal, scale, p, seed,
                    O, ldo, lse, dO, lddo, dq, lddq, dk, lddk, dv, lddv, dbd=None, ldbd=0, part=None,
                    ldpart=0, qv_out=None, ldqv=0, dmask=None, ldm=0, flags=0):

@@ -15,7 +15,7 @@ from __future__ import annotations
 import torch
 from torch import nn
 
-from .common import (ACT_SWISH, EPI_ACT, EPI_DACT, EPI_RESID, EPI_STORE, F32, Bound, attn_bwd, attn_dmask,
+from .common import (ACT_SWISH, EPI_ACT, EPI_DACT, EPI_RESID, EPI_STORE, F32, Bound, attn_bwd, attn_dmask, dbd_layout,
                      attn_fused_bwd, attn_fwd, empty, fused_attn_ok, lib, ln_bwd, ln_fwd, math, ops, ptr, rup,
                      site_seed, dv_buf, drop_arg, site_dv)
 
@@ -309,11 +309,13 @@ class ConformerBlockFn(torch.autograd.Function):
         dO = empty(N, d, dtype=cd, device=dev)
         ops.linear_dx(dv, b.w(A + "linear_out.weight"), dO)
         dqkv = empty(N, 3 * d, dtype=cd, device=dev)
-        ldbd = rup(P2, 8)
+        ldbd, shift = rup(P2, 8), 0
         if s_core[0] == "fused":
-            # dq includes the q+v path (dBD.p, in-kernel); dbd rows written in full; pos_bias_u /
+            # dq includes the q+v path (dBD.p, in-kernel); dbd rows written in full, in the
+            # pipelined dQ pass's shifted layout (logical column r at r + shift); pos_bias_u /
             # pos_bias_v gradients from per-block column sums of the two dq terms
             _, lse, dmask, ldm = s_core
+            shift, ldbd = dbd_layout(T)
             dbd = empty(H * B * T * ldbd, dtype=cd, device=dev)
             qv = empty(N, d, dtype=cd, device=dev)  # q + v, for the linear_pos weight gradient
             nqb = (T + 63) // 64
@@ -323,7 +325,7 @@ class ConformerBlockFn(torch.autograd.Function):
                            klen=olens, causal=False, scale=scale, p=pa, seed=sd(3), O=O, ldo=d, lse=lse, dO=dO,
                            lddo=d, dq=dqkv, lddq=3 * d, dk=dqkv[:, d:], lddk=3 * d, dv=dqkv[:, 2 * d:],
                            lddv=3 * d, dbd=dbd, ldbd=ldbd, part=part, ldpart=d, qv_out=qv, ldqv=d, dmask=dmask,
-                           ldm=ldm, flags=1)
+                           ldm=ldm, flags=1 | 2)
             ops.reduce_rows(part[:B * nqb * d], B * nqb, d, d, b.g(A + "pos_bias_u", shape=(d,)))
             ops.reduce_rows(part[B * nqb * d:], B * nqb, d, d, b.g(A + "pos_bias_v", shape=(d,)))
         else:
@@ -342,12 +344,15 @@ class ConformerBlockFn(torch.autograd.Function):
             ops.colsum(dqv, b.g(A + "pos_bias_v", shape=(d,)))
             lib.ea_add_2d(N, d, dqv.data_ptr(), ops.dt(dqv), d, dqkv.data_ptr(), ops.dt(dqkv), 3 * d, 1.0,
                           ops.stream())
-        # linear_pos: dp[h] = sum_b dBD[h][b]^T qv[b, :, h]  (K = B*T), dWpos = dp^T pos
+        # linear_pos: dp[h] = sum_b dBD[h][b]^T qv[b, :, h]  (K = B*T), dWpos = dp^T pos; with the
+        # shifted layout the GEMM runs over every physical column and rows [shift, shift + P2) of
+        # its output are dp
         with ops.wgrad(dbd, qv, pos):
-            dpp = empty(P2, d, dtype=cd, device=dev)
-            ops.gemm(dbd, qv, dpp, M=P2, N=dk, K=B * T, a_kmajor=0, b_kmajor=0, lda=ldbd, ldb=d, ldc=d,
+            Mp = P2 + shift if shift else P2
+            dpp_full = empty(Mp, d, dtype=cd, device=dev)
+            ops.gemm(dbd, qv, dpp_full, M=Mp, N=dk, K=B * T, a_kmajor=0, b_kmajor=0, lda=ldbd, ldb=d, ldc=d,
                      batch=1, nh=H, sA=(0, B * T * ldbd), sB=(0, dk), sC=(0, dk))
-            ops.linear_dw(dpp, pos, b.g(A + "linear_pos.weight"), accumulate=True)
+            ops.linear_dw(dpp_full[shift:], pos, b.g(A + "linear_pos.weight"), accumulate=True)
         del dbd
         qkv_w = b.w(A + "linear_q.weight", A + "linear_k.weight", A + "linear_v.weight", shape=(3 * d, d))
         with ops.wgrad(dqkv, xn2):

@@ -454,8 +454,16 @@ int ea_attn_fused_fwd2(int B, int H, int T1, int T2, int dk, const void* q, long
  *   dmask (or NULL): the forward's keep bits (ea_attn_fused_fwd2, same p / seed), read
  *     instead of regenerating the dropout hash.
  * ws: ea_attn_fused_bwd_ws_bytes() bytes of device scratch, 256-B aligned (D_i, q + bu, q + bv
- * handed from the dQ pass to the dK/dV pass).  Two launches, any T1, T2, deterministic. */
+ * handed from the dQ pass to the dK/dV pass).  Two launches, any T1, T2, deterministic.
+ * flags bit 1 (2): the pipelined dQ pass (LDS-DMA one key chunk ahead, 16-B band stores); dbd
+ *   is then in the SHIFTED layout of ea_attn_dbd_layout: logical column r at r + shift, row
+ *   stride lddbd >= the returned minimum.  Without dbd the pipelined pass is the default.
+ * flags bit 2 (4): force the original dQ pass (A/B measurements; unshifted dbd). */
 int ea_attn_fused_bwd_ws_bytes(int B, int H, int T1, long* bytes);
+/* Shifted dbd layout of ea_attn_fused_bwd2 flags bit 1: shift >= 15 with (T1 + shift) % 8 == 0,
+ * minimum row stride lddbd = roundup8(2*T1 - 1 + shift); columns outside [shift, shift + 2*T1-1)
+ * are written as zeros. */
+int ea_attn_dbd_layout(int T1, int* shift, long* lddbd);
 int ea_attn_fused_bwd2(int B, int H, int T1, int T2, int dk, const void* q, long ldq, const void* k,
                        long ldk, const void* v, long ldv, const float* bu, const float* bv,
                        const void* pp, long ldp, const long long* klen, int causal, float scale, float p,

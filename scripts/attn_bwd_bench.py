@@ -23,7 +23,12 @@ klen = torch.full((B,), T, dtype=torch.long, device=dev)
 O = torch.empty(B, T, d, dtype=bf, device=dev)
 lse = torch.empty(B * H * T, device=dev)
 dq, dk, dv = torch.empty_like(q), torch.empty_like(k), torch.empty_like(v)
-ldbd = (2 * T - 1 + 7) // 8 * 8
+V1 = os.environ.get("ATTN_V1", "0") == "1"  # the original dQ pass (unshifted dbd) for A/B
+if V1:
+    ldbd = (2 * T - 1 + 7) // 8 * 8
+else:
+    from espnet_amd.layers.common import dbd_layout
+    _, ldbd = dbd_layout(T)
 dbd = torch.empty(H * B * T * ldbd, dtype=bf, device=dev)  # written in full by the kernel
 ldm = 2 * ((T + 63) // 64)
 dmask = torch.empty(B * H * T * ldm, dtype=torch.int32, device=dev)
@@ -46,7 +51,7 @@ def bwd():
     attn_fused_bwd(B=B, H=H, T1=T, T2=T, q=q, ldq=d, k=k, ldk=d, v=v, ldv=d, bu=u, bv=vb, pp=pp, ldp=d, klen=klen,
                    causal=False, scale=scale, p=p, seed=seed, O=O, ldo=d, lse=lse, dO=dO, lddo=d, dq=dq, lddq=d,
                    dk=dk, lddk=d, dv=dv, lddv=d, dbd=dbd, ldbd=ldbd, part=part, ldpart=d, qv_out=qv_out, ldqv=d,
-                   dmask=dmask if p > 0 else None, ldm=ldm, flags=1)
+                   dmask=dmask if p > 0 else None, ldm=ldm, flags=1 | (4 if V1 else 2))
 
 for name, fn in (("fwd", fwd), ("bwd", bwd)):
     for _ in range(3):

@@ -50,7 +50,30 @@ def _rel(a, b):
     return float((a.float() - b.float()).norm() / b.float().norm().clamp_min(1e-30))
 
 
-def run_fused(q, k, v, u, vb, pp, klen, causal, H, dO, p=0.0, seed=0):
+def dbd_layout(T1, v2):
+    """(shift, row stride) of the band gradient: v2 = the pipelined dQ pass's shifted layout
+    (ea_attn_dbd_layout), else logical columns at 0."""
+    import ctypes
+    from espnet_amd._lib import lib
+    if not v2:
+        return 0, (2 * T1 - 1 + 7) // 8 * 8
+    sh, ld = ctypes.c_int(0), ctypes.c_long(0)
+    assert lib.ea_attn_dbd_layout(T1, ctypes.addressof(sh), ctypes.addressof(ld)) == 0
+    assert sh.value >= 15 and (T1 + sh.value) % 8 == 0 and ld.value % 8 == 0
+    return sh.value, ld.value
+
+
+def band_view(dbd, H, B, T1, v2):
+    """dbd as (H, B, T1, 2*T1-1) logical columns, plus the physical columns outside them."""
+    sh, ld = dbd_layout(T1, v2)
+    full = dbd.view(H, B, T1, ld)
+    outside = torch.cat([full[..., :sh], full[..., sh + 2 * T1 - 1:]], dim=-1)
+    return full[..., sh: sh + 2 * T1 - 1], outside
+
+
+def run_fused(q, k, v, u, vb, pp, klen, causal, H, dO, p=0.0, seed=0, v2=False):
+    """Forward + backward through the C ABI; v2 = the pipelined dQ pass (flags bit 1, shifted
+    dbd), else the original pass (flags bit 2)."""
     from espnet_amd import hip_ops as ops
     from espnet_amd._lib import lib
     from espnet_amd.layers.common import attn_fused_bwd
@@ -67,13 +90,13 @@ def run_fused(q, k, v, u, vb, pp, klen, causal, H, dO, p=0.0, seed=0):
     dq = torch.empty_like(q)
     dkk = torch.empty_like(k)
     dv = torch.empty_like(v)
-    ldbd = (2 * T1 - 1 + 7) // 8 * 8
+    _, ldbd = dbd_layout(T1, v2)
     # NaN-filled: the kernel writes every band row in full (zeros off the band)
     dbd = torch.full((H * B * T1 * ldbd,), float("nan"), dtype=bf, device=DEV) if pp is not None else None
-    # the hash path (no keep-bit mask), dq without the rel-pos term (flags 0)
+    # the hash path (no keep-bit mask), dq without the rel-pos term (flag bit 0 clear)
     attn_fused_bwd(B=B, H=H, T1=T1, T2=T2, q=q, ldq=d, k=k, ldk=d, v=v, ldv=d, bu=u, bv=vb, pp=pp, ldp=d, klen=klen,
                    causal=causal, scale=scale, p=p, seed=seed, O=O, ldo=d, lse=lse, dO=dO, lddo=d, dq=dq, lddq=d,
-                   dk=dkk, lddk=d, dv=dv, lddv=d, dbd=dbd, ldbd=ldbd)
+                   dk=dkk, lddk=d, dv=dv, lddv=d, dbd=dbd, ldbd=ldbd, flags=2 if v2 else 4)
     torch.cuda.synchronize()
     return O, dq, dkk, dv, dbd, ldbd
 
@@ -90,6 +113,7 @@ def _inputs(B, H, T1, T2, rel, seed=0):
     return q, k, v, u, vb, pp, dO
 
 
+@pytest.mark.parametrize("v2", [False, True])
 @pytest.mark.parametrize("B,H,T1,T2,rel,causal,klens", [
     (2, 3, 137, 137, True, False, [137, 100]),
     (3, 2, 249, 249, True, False, [249, 200, 64]),
@@ -99,11 +123,13 @@ def _inputs(B, H, T1, T2, rel, seed=0):
     (1, 2, 300, 300, True, False, [300]),
     (2, 1, 41, 300, False, False, [300, 131]),
     (1, 2, 270, 270, False, True, [270]),
+    (2, 1, 64, 64, True, False, [64, 1]),
+    (1, 1, 130, 130, True, False, [130]),
 ])
-def test_fused_attention_matches_fp32_reference(B, H, T1, T2, rel, causal, klens):
+def test_fused_attention_matches_fp32_reference(B, H, T1, T2, rel, causal, klens, v2):
     q, k, v, u, vb, pp, dO = _inputs(B, H, T1, T2, rel)
     klen = torch.tensor(klens, dtype=torch.long, device=DEV)
-    O, dq, dk, dv, dbd, ldbd = run_fused(q, k, v, u, vb, pp, klen, causal, H, dO)
+    O, dq, dk, dv, dbd, ldbd = run_fused(q, k, v, u, vb, pp, klen, causal, H, dO, v2=v2)
     # fp32 reference on the same (bf16-rounded) inputs; q+u / q+v rounded to bf16 like the kernel
     qf, kf, vf = (t.float().requires_grad_(True) for t in (q, k, v))
     ppf = pp.float().requires_grad_(True) if rel else None
@@ -119,7 +145,9 @@ def test_fused_attention_matches_fp32_reference(B, H, T1, T2, rel, causal, klens
     # rel-pos: dq from the kernel is the (q+u) path; the (q+v) path leaves through dbd:
     # dq_total = dq + dBD . pp_h, d pp_h = dBD^T . (q+v)
     d = H * 64
-    dbd4 = dbd.view(H, B, T1, ldbd)[..., : 2 * T1 - 1].float()
+    dbd4, off_band = band_view(dbd, H, B, T1, v2)
+    dbd4 = dbd4.float()
+    assert off_band.numel() == 0 or float(off_band.float().abs().max()) == 0.0  # zeros, no NaN left
     pph = pp.float().view(2 * T1 - 1, H, 64).permute(1, 0, 2)  # (H, R, 64)
     dq_v = torch.einsum("hbir,hrc->bihc", dbd4, pph).reshape(B, T1, d)
     assert _rel(dq.float() + dq_v, qf.grad) < 2e-2
@@ -257,3 +285,54 @@ def test_fused_dropout_mask_matches_rehash(causal, T1, T2, klens):
     torch.cuda.synchronize()
     assert torch.equal(O2, O)
     assert torch.equal(dq, dq1) and torch.equal(dk, dk1) and torch.equal(dv, dv1)
+
+
+@pytest.mark.parametrize("B,H,T,klens,p,mask", [
+    (2, 3, 137, [137, 100], 0.0, False),
+    (3, 2, 249, [249, 200, 64], 0.1, True),
+    (2, 2, 249, [249, 249], 0.1, False),
+    (1, 2, 300, [300], 0.1, True),
+    (2, 1, 97, [97, 1], 0.0, False),
+    (2, 2, 45, [45, 30], 0.1, True),
+])
+def test_bwdq_pipelined_matches_original(B, H, T, klens, p, mask):
+    """The pipelined dQ pass (flags bit 1: LDS-DMA one chunk ahead, bpermute gather, 64-column
+    band windows, shifted 16-B dbd stores) against the original pass on the same inputs: dk,
+    dv, dbd (logical columns) and the pos_bias_u partials bit for bit; dq and the pos_bias_v
+    partials (d(q+v) summed over 64- instead of 96-column windows) to f32 rounding."""
+    from espnet_amd import hip_ops as ops
+    from espnet_amd._lib import lib
+    from espnet_amd.layers.common import attn_fused_bwd
+    q, k, v, u, vb, pp, dO = _inputs(B, H, T, T, True, seed=11)
+    klen = torch.tensor(klens, dtype=torch.long, device=DEV)
+    d, seed, scale = H * 64, 77, 1 / 8
+    ldm = 2 * ((T + 63) // 64)
+    dmask = torch.empty(B * H * T * ldm, dtype=torch.int32, device=DEV) if mask else None
+    O = torch.empty(B, T, d, dtype=bf, device=DEV)
+    lse = torch.empty(B * H * T, device=DEV)
+    lib.ea_attn_fused_fwd2(B, H, T, T, 64, q.data_ptr(), d, k.data_ptr(), d, v.data_ptr(), d, u.data_ptr(),
+                           vb.data_ptr(), pp.data_ptr(), d, klen.data_ptr(), 0, scale, p, seed, O.data_ptr(), d,
+                           lse.data_ptr(), 0 if dmask is None else dmask.data_ptr(), ldm, ops.stream())
+    nqb = (T + 63) // 64
+    out = {}
+    for v2 in (False, True):
+        sh, ld = dbd_layout(T, v2)
+        dq, dk, dv = torch.empty_like(q), torch.empty_like(k), torch.empty_like(v)
+        dbd = torch.full((H * B * T * ld,), float("nan"), dtype=bf, device=DEV)
+        part = torch.full((2, B * nqb, d), float("nan"), device=DEV)
+        qv = torch.empty(B, T, d, dtype=bf, device=DEV)
+        attn_fused_bwd(B=B, H=H, T1=T, T2=T, q=q, ldq=d, k=k, ldk=d, v=v, ldv=d, bu=u, bv=vb, pp=pp, ldp=d,
+                       klen=klen, causal=False, scale=scale, p=p, seed=seed, O=O, ldo=d, lse=lse, dO=dO, lddo=d,
+                       dq=dq, lddq=d, dk=dk, lddk=d, dv=dv, lddv=d, dbd=dbd, ldbd=ld, part=part, ldpart=d,
+                       qv_out=qv, ldqv=d, dmask=dmask, ldm=ldm, flags=1 | (2 if v2 else 4))
+        torch.cuda.synchronize()
+        band, outside = band_view(dbd, H, B, T, v2)
+        out[v2] = (dq, dk, dv, band, outside, part, qv)
+    (dq1, dk1, dv1, b1, o1, p1, qv1), (dq2, dk2, dv2, b2, o2, p2, qv2) = out[False], out[True]
+    assert torch.equal(dk1, dk2) and torch.equal(dv1, dv2) and torch.equal(qv1, qv2)
+    assert torch.equal(b1, b2)
+    assert o2.numel() == 0 or float(o2.float().abs().max()) == 0.0
+    assert torch.equal(p1[0], p2[0])
+    assert _rel(dq2, dq1) < 2e-3
+    assert float((dq2.float() - dq1.float()).abs().max()) <= 2e-2 * float(dq1.float().abs().max())
+    assert _rel(p2[1], p1[1]) < 1e-4
