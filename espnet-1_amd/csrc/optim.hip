@@ -202,3 +202,56 @@ extern "C" int ea_axpby_scalar(const float* a, float wa, const float* b, float w
   EA_LAUNCH_CHECK();
   return 0;
 }
+
+// ----------------------------------------------------------------- transposed weight shadow
+// bf16 W^T copies of the shadow weights whose Linear input gradient (dX = dY . W, N = K_in) runs
+// on narrow-N tiles: read K-major there, the weight panel is one LDS-DMA stream instead of
+// 128-wide MN-major panels (about a third of those launches' time).  Problem p: dst[c*R + r] =
+// src[off + r*C + c] for an R x C row-major weight; one workgroup per 64 x 64 tile, the tiles
+// listed as (problem, tile row, tile col); R, C multiples of 8.
+namespace {
+struct TrProb {
+  long long src_off;
+  bf16* dst;
+  int R, C;
+};
+__global__ __launch_bounds__(256) void transpose_grouped_kernel(const int4* __restrict__ tiles,
+                                                                const TrProb* __restrict__ probs,
+                                                                const bf16* __restrict__ src) {
+  __shared__ __attribute__((aligned(16))) bf16 t[64][72];  // 144-B rows
+  const int4 tl = tiles[blockIdx.x];
+  const TrProb p = probs[tl.x];
+  const int r0 = tl.y * 64, c0 = tl.z * 64, tid = threadIdx.x;
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const int q = tid + 256 * u, rr = q >> 3, ch = q & 7;
+    const int r = r0 + rr, c = c0 + ch * 8;
+    uint4 v = make_uint4(0u, 0u, 0u, 0u);
+    if (r < p.R && c < p.C) v = *(const uint4*)(src + p.src_off + (long)r * p.C + c);
+    *(uint4*)&t[rr][ch * 8] = v;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const int q = tid + 256 * u, cc = q >> 3, ch = q & 7;
+    const int c = c0 + cc, r = r0 + ch * 8;
+    if (c < p.C && r < p.R) {
+      union { uint4 u4; bf16 e[8]; } o;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) o.e[e] = t[ch * 8 + e][cc];
+      *(uint4*)(p.dst + (long)c * p.R + r) = o.u4;
+    }
+  }
+}
+}  // namespace
+
+extern "C" int ea_transpose_bf16_grouped(int ntiles, const int* tiles, const void* probs, const void* src,
+                                         void* stream) {
+  EA_ENTRY();
+  EA_CHECK_ARG(ntiles >= 0 && (ntiles == 0 || (tiles && probs && src)));
+  if (ntiles == 0) return 0;
+  hipLaunchKernelGGL(transpose_grouped_kernel, dim3(ntiles), dim3(256), 0, (hipStream_t)stream,
+                     (const int4*)tiles, (const TrProb*)probs, (const bf16*)src);
+  EA_LAUNCH_CHECK();
+  return 0;
+}

@@ -67,6 +67,8 @@ class ParamArena:
             self.shadow = torch.zeros(self.numel, dtype=shadow_dtype, device=self.device)
         self.names = layout
         self._params = named
+        from . import hip_ops  # transposed bf16 copies for the Linear input-gradient GEMMs
+        self.tshadow = hip_ops.attach_transposed_shadow(self.shadow)
         self._flatten_buffers(model)
         with torch.no_grad():
             for n in layout:
@@ -130,6 +132,8 @@ class ParamArena:
             from ._lib import lib
             lib.ea_cast_f32_bf16(self.numel, self.data.data_ptr(), self.shadow.data_ptr(),
                                  hip_ops.stream())
+            if self.tshadow is not None:
+                self.tshadow.refresh()
 
     def rebind(self):
         """Re-point Parameters at the arena (after an external .data / .grad reassignment)."""

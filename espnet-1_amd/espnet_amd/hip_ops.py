@@ -7,6 +7,7 @@ from __future__ import annotations
 
 import ctypes
 import os
+import weakref
 
 import torch
 
@@ -338,11 +339,86 @@ def linear(x, w, out, *, epi: Epilogue = None):
                 ldc=ldc, epi=epi)
 
 
+# ----------------------------------------------------------------------------- transposed shadow
+# The Linear input gradient dX = dY . W has N = K_in: for K_in <= 512 it runs on the narrow
+# 64x128 / 32x128 tiles, where W read MN-major (128-wide panels, transposed LDS reads) costs
+# about a third of the launch.  A bf16 W^T copy per such weight, rewritten by one grouped
+# transpose after every optimizer step (and shadow refresh), lets those GEMMs read both
+# operands K-major.  EA_WT_SHADOW=0 turns it off (A/B).
+WT_SHADOW = os.environ.get("EA_WT_SHADOW", "1") != "0"
+WT_MAX_KIN = 512
+TSHADOWS = {}  # arena shadow storage pointer -> weakref(TransposedShadow) (the arena owns it)
+
+
+class TransposedShadow:
+    def __init__(self, shadow):
+        self.shadow = shadow  # the arena's bf16 weight shadow (flat)
+        self.items = {}  # (element offset, R, C) -> (C, R) bf16 tensor
+        self.tiles = self.probs = None
+        self.ntiles = 0
+
+    def _rebuild(self):
+        probs, tiles = [], []
+        for pi, ((off, R, C), dst) in enumerate(self.items.items()):
+            probs.append((off, dst.data_ptr(), R | (C << 32)))
+            tiles += [(pi, tr, tc, 0) for tr in range((R + 63) // 64) for tc in range((C + 63) // 64)]
+        dev = self.shadow.device
+        self.probs = torch.tensor(probs, dtype=torch.int64).to(dev)
+        self.tiles = torch.tensor(tiles, dtype=torch.int32).to(dev)
+        self.ntiles = len(tiles)
+
+    def get(self, w):
+        """W^T (C x R, row-major) of a contiguous (R x C) view of the shadow, created (and
+        transposed from the current shadow) on first use."""
+        off = (w.data_ptr() - self.shadow.data_ptr()) // w.element_size()
+        key = (off, int(w.shape[0]), int(w.shape[1]))
+        wt = self.items.get(key)
+        if wt is None:
+            if torch.cuda.is_current_stream_capturing():
+                return None  # registration happens in the eager warm-up steps
+            wt = torch.empty(key[2], key[1], dtype=w.dtype, device=w.device)
+            self.items[key] = wt
+            self._rebuild()
+            self.refresh()
+        return wt
+
+    def refresh(self):
+        if self.ntiles:
+            lib.ea_transpose_bf16_grouped(self.ntiles, self.tiles.data_ptr(), self.probs.data_ptr(),
+                                          self.shadow.data_ptr(), stream())
+
+
+def attach_transposed_shadow(shadow):
+    """Register an arena's bf16 shadow for transposed copies (returns the registry, or None)."""
+    if not WT_SHADOW or shadow is None or shadow.dtype != torch.bfloat16:
+        return None
+    ts = TransposedShadow(shadow)
+    TSHADOWS[shadow.untyped_storage().data_ptr()] = weakref.ref(ts)
+    return ts
+
+
+def _transposed(w):
+    if not TSHADOWS or w.dtype != torch.bfloat16 or w.dim() != 2 or w.shape[1] > WT_MAX_KIN:
+        return None
+    if w.stride(1) != 1 or w.stride(0) != w.shape[1] or w.shape[0] % 8 or w.shape[1] % 8:
+        return None
+    ref = TSHADOWS.get(w.untyped_storage().data_ptr())
+    ts = None if ref is None else ref()
+    if ts is None or ts.shadow.untyped_storage().data_ptr() != w.untyped_storage().data_ptr():
+        return None
+    return ts.get(w)
+
+
 def linear_dx(dy, w, out, *, epi: Epilogue = None):
-    """out[r, k] = epi(sum_n dy[r, n] * w[n, k]) — Linear input gradient."""
+    """out[r, k] = epi(sum_n dy[r, n] * w[n, k]) — Linear input gradient (W^T K-major from the
+    transposed shadow when the arena keeps one for w)."""
     M, N, lda = _rows(dy)
     K = w.shape[1]
     _, _, ldc = _rows(out)
+    wt = _transposed(w)
+    if wt is not None:
+        return gemm(dy, wt, out, M=M, N=K, K=N, a_kmajor=1, b_kmajor=1, lda=lda, ldb=wt.stride(0),
+                    ldc=ldc, epi=epi)
     return gemm(dy, w, out, M=M, N=K, K=N, a_kmajor=1, b_kmajor=0, lda=lda, ldb=w.stride(0),
                 ldc=ldc, epi=epi)
 

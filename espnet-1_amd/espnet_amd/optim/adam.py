@@ -77,6 +77,8 @@ class ArenaAdam(torch.optim.Optimizer):
                              self.exp_avg_sq.data_ptr(), ops.ptr(a.shadow), ctypes.byref(self.schedule),
                              b1, b2, float(g["eps"]), float(g["weight_decay"]), self.state_dev.data_ptr(),
                              ops.ptr(grad_norm), float(max_norm), ops.stream())
+        if getattr(a, "tshadow", None) is not None:  # W^T copies follow the new bf16 shadow
+            a.tshadow.refresh()
 
     def zero_grad(self, set_to_none: bool = False):
         self.arena.grad.zero_()

@@ -541,6 +541,11 @@ int ea_adam_step_dev(long n, float* params, const float* grads, float* exp_avg, 
                      void* stream);
 
 int ea_cast_f32_bf16(long n, const float* x, void* y, void* stream);
+/* Transposed bf16 weight copies for the Linear input-gradient GEMMs (read K-major): problem
+ * table probs[] of {int64 src_off; bf16* dst; int32 R, C} (24 B each, device memory), tile table
+ * tiles[] of int32x4 {problem, tile row, tile col, 0} (64 x 64 tiles); dst[c*R + r] =
+ * src[src_off + r*C + c].  R, C multiples of 8. */
+int ea_transpose_bf16_grouped(int ntiles, const int* tiles, const void* probs, const void* src, void* stream);
 /* x *= s[0]*c (device scalar) */
 int ea_scale_by_scalar(long n, float* x, const float* s, float c, void* stream);
 /* out[0] = wa*a[0] + wb*b[0] (b may be NULL) — loss = w*ctc + (1-w)*att, espnet_model.py:325 */
