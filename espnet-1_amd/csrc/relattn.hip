@@ -18,6 +18,7 @@
 // GEMMs.  Dropout masks use the same counter hash as the unfused path (index
 // (z*T1 + i)*T2 + j), regenerated in backward.
 #include "common.h"
+#include <stdlib.h>
 
 // timing experiments only (scripts/build_def.py): bit 1 no dBD stores, 2 no d(q+v) term, 4 K/V/band
 // staged for the first chunk only, 8 no BD gather in attn_bwdq
@@ -1220,6 +1221,234 @@ __global__ __launch_bounds__(256, 2) void attn_bwdq2_kernel(AttnP a) {
   }
 }
 
+// ---------------------------------------------------------- attn forward, pipelined (v2)
+// attn_fwd_kernel with the dQ pass's pipelining: K / V chunks double-buffered and the
+// positional band (128 rows per chunk) in a 192-row ring, all filled by LDS-DMA one chunk
+// ahead (one barrier per chunk, no staging registers); the BD diagonal gather by ds_bpermute;
+// Pd written as a [64 keys][16 queries] image with one 8-B store per key tile (4 queries of a
+// lane) instead of 16 two-byte stores, read back as the PV MFMA's A operand with transposed
+// reads.  Same arithmetic in the same order as attn_fwd_kernel: O, lse and the keep bits are
+// bit-identical.  MM: 0 no dropout, 1 dropout + keep bits to dmask, 2 dropout only.
+template <bool REL>
+struct F2 {
+  static constexpr int RINGF = 192;
+  static constexpr int K = 0, V = K + 2 * KC * 128, P = V + 2 * KC * 128;
+  static constexpr int PT = P + (REL ? RINGF * 128 : 0);  // per wave: Pd^T image [64][16] bf16
+  static constexpr int LDS = PT + NWAVE * 64 * 32;
+};
+static_assert(F2<true>::LDS <= 80 * 1024, "two workgroups per CU");
+
+template <bool REL, int MM>
+__global__ __launch_bounds__(256, 2) void attn_fwd2_kernel(AttnP a) {
+  using L = F2<REL>;
+  constexpr int RF = L::RINGF;
+  __shared__ __attribute__((aligned(16))) char sm[L::LDS];
+  const int nqb = (a.T1 + QB - 1) / QB;
+  const int z = blockIdx.x / nqb, qb = blockIdx.x % nqb;
+  const int b = z / a.H, h = z % a.H;
+  const int i0 = qb * QB;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int g = lane >> 4, lc = lane & 15;
+  const int kl = a.klen ? (int)min((long long)a.T2, a.klen[b]) : a.T2;
+  const uint64_t seed = MM ? ea_salted(a.seed, a.salt) : 0;
+  char* pt = sm + L::PT + w * 64 * 32;
+  const int kend = a.causal ? min(kl, i0 + QB) : kl;
+  const int nch = (kend + KC - 1) / KC;
+  const int rlimP = 2 * a.T1 - 1;
+  const int rb0 = a.T1 - 1 - (i0 + QB - 1);  // chunk 0's first positional row (ring position 0)
+  const bf16* kh_ = a.k + (long)b * a.T2 * a.ldk + h * DK;
+  const bf16* vh_ = a.v + (long)b * a.T2 * a.ldv + h * DK;
+  const bf16* ph_ = REL ? a.pp + h * DK : nullptr;
+  auto dma_kv = [&](int c) {
+    char* kb = sm + L::K + (c & 1) * KC * 128;
+    char* vb = sm + L::V + (c & 1) * KC * 128;
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int gi = w + 4 * u;
+      km_dma8(kb, 8 * gi, kh_, a.ldk, 64 * c + 8 * gi, a.T2, lane);
+      km_dma8(vb, 8 * gi, vh_, a.ldv, 64 * c + 8 * gi, a.T2, lane);
+    }
+  };
+  auto dma_ring = [&](int x0, int ngrp) {
+    for (int gi = w; gi < ngrp; gi += 4) {
+      const int x = x0 + 8 * gi;
+      km_dma8(sm + L::P, x % RF, ph_, a.ldp, rb0 + x, rlimP, lane);
+    }
+  };
+  if (nch > 0) {
+    dma_kv(0);
+    if (REL) dma_ring(0, 16);
+  }
+  // this wave's 16 query rows as A fragments (q + u, q + v), from images in the second buffers
+  bf16x8 qa[2], qv[2];
+  {
+    char* img_qu = sm + L::K + KC * 128;
+    char* img_qv = sm + L::V + KC * 128;
+    const bf16* qsrc = a.q + (long)b * a.T1 * a.ldq + h * DK;
+    km_stage_bias(img_qu, qsrc, a.ldq, i0, QB, a.T1, a.bu ? a.bu + h * DK : nullptr, tid, 256);
+    if (REL) km_stage_bias(img_qv, qsrc, a.ldq, i0, QB, a.T1, a.bv + h * DK, tid, 256);
+    bar();
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      qa[ks] = km_frag(img_qu, 16 * w, ks, lane);
+      if (REL) qv[ks] = km_frag(img_qv, 16 * w, ks, lane);
+    }
+  }
+  f32x4 oacc[4];
+#pragma unroll
+  for (int t = 0; t < 4; ++t) oacc[t] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  float mrun[4], lrun[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) { mrun[r] = -INFINITY; lrun[r] = 0.f; }
+  const int ibase = i0 + 16 * w + 4 * g;  // query row of register rr: ibase + rr
+  const int odd = lc & 1;
+  const uint64_t npair = (uint64_t)((a.T2 + 1) >> 1);
+  const uint64_t prA = ((uint64_t)z * a.T1 + ibase + odd) * npair, prB = prA + 2 * npair;
+  const int pb = 48 - 16 * w;
+  for (int c = 0; c < nch; ++c) {
+    const int j0 = c * KC;
+    vmcnt_le<0>();  // this chunk's images (and the previous chunk's keep-bit stores) landed
+    bar();          // all waves done with the previous chunk (and, at c = 0, the setup images)
+    if (c + 1 < nch) {
+      dma_kv(c + 1);
+      if (REL) dma_ring(64 * c + 128, 8);
+    }
+    const char* kimg = sm + L::K + (c & 1) * KC * 128;
+    const char* vimg = sm + L::V + (c & 1) * KC * 128;
+    f32x4 s[4];
+    {
+      bf16x8 kf[4][2];
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) kf[t][ks] = km_frag_asm(kimg, 16 * t, ks, lane);
+      lgkm0();
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        s[t] = (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) s[t] = mfma(qa[ks], kf[t][ks], s[t]);
+      }
+    }
+    if (REL) {
+      // BDfull (16 x 80) over ring rows 64c + pb + [0, 80), gathered onto the diagonal
+      f32x4 bd[5];
+      {
+        bf16x8 pf[5][2];
+#pragma unroll
+        for (int t = 0; t < 5; ++t) {
+          const int rp = (64 * c + pb + 16 * t) % RF;
+#pragma unroll
+          for (int ks = 0; ks < 2; ++ks) pf[t][ks] = km_frag_asm(sm + L::P, rp, ks, lane);
+        }
+        lgkm0();
+#pragma unroll
+        for (int t = 0; t < 5; ++t) {
+          bd[t] = (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+          for (int ks = 0; ks < 2; ++ks) bd[t] = mfma(qv[ks], pf[t][ks], bd[t]);
+        }
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int sft = lc + 15 - 4 * g - r;
+        const int src = (16 * g + (sft & 15)) * 4;
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+          const float lo = __int_as_float(__builtin_amdgcn_ds_bpermute(src, __float_as_int(bd[t][r])));
+          const float hi = __int_as_float(__builtin_amdgcn_ds_bpermute(src, __float_as_int(bd[t + 1][r])));
+          s[t][r] += sft >= 16 ? hi : lo;
+        }
+      }
+    }
+    // mask, online softmax
+    float pv[4][4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int i = ibase + r;
+      float mx = -INFINITY;
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const int j = j0 + 16 * t + lc;
+        const bool ok = j < kl && (!a.causal || j <= i);
+        const float x = ok ? s[t][r] * a.scale : -INFINITY;
+        pv[t][r] = x;
+        mx = fmaxf(mx, x);
+      }
+      mx = max16(mx);
+      const float mnew = fmaxf(mrun[r], mx);
+      const float alpha = mnew == -INFINITY ? 1.f : __expf(mrun[r] - mnew);
+      float sum = 0.f;
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const float e = pv[t][r] == -INFINITY ? 0.f : __expf(pv[t][r] - mnew);
+        pv[t][r] = e;
+        sum += e;
+      }
+      sum = sum16(sum);
+      lrun[r] = lrun[r] * alpha + sum;
+      mrun[r] = mnew;
+#pragma unroll
+      for (int t = 0; t < 4; ++t) oacc[t][r] *= alpha;
+    }
+    // dropout (keep bits -> dmask for the backward)
+    if (MM) {
+      const uint32_t key = ea_seed_key(seed), thr = ea_drop_thr(a.p);
+      const float sc = 1.f / (1.f - a.p);
+      uint64_t bal[4][4];
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const uint64_t jp = (uint64_t)((j0 + 16 * t + lc) >> 1);  // shared by the lane pair
+        const uint32_t hA = ea_pair_hash(key, prA + jp), hB = ea_pair_hash(key, prB + jp);
+        const uint32_t pA = (uint32_t)__builtin_amdgcn_mov_dpp((int)hA, 0xB1, 0xF, 0xF, false);
+        const uint32_t pB = (uint32_t)__builtin_amdgcn_mov_dpp((int)hB, 0xB1, 0xF, 0xF, false);
+        const uint32_t hh[4] = {odd ? pA : hA, odd ? hA : pA, odd ? pB : hB, odd ? hB : pB};
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const bool kept = (odd ? hh[r] >> 16 : hh[r] & 0xffffu) >= thr;  // key parity = lane parity
+          pv[t][r] *= kept ? sc : 0.f;
+          bal[t][r] = __ballot(kept);
+        }
+      }
+      if (MM == 1 && lc < 2) {  // lane lc = u writes word u of each of its group's 4 rows
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int i = ibase + r;
+          const uint64_t lo = lc ? bal[2][r] : bal[0][r], hi = lc ? bal[3][r] : bal[1][r];
+          const uint32_t word = (uint32_t)((lo >> (16 * g)) & 0xffffu) | ((uint32_t)((hi >> (16 * g)) & 0xffffu) << 16);
+          if (i < a.T1) a.dmask[((long)z * a.T1 + i) * a.ldm + (j0 >> 5) + lc] = word;
+        }
+      }
+    }
+    // Pd^T image: key 16t + lc, queries 4g .. 4g+3 in one 8-B store
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+      st64_asm(pt + (16 * t + lc) * 32 + g * 8,
+               make_uint2(pack_bf16x2(pv[t][0], pv[t][1]), pack_bf16x2(pv[t][2], pv[t][3])));
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      const bf16x8 pa = dst_frag_asm(pt, 32 * ks, lane);
+      bf16x8 vf[4];
+#pragma unroll
+      for (int t = 0; t < 4; ++t) vf[t] = km_tr_rows(vimg, 32 * ks, 32 * ks + 16, 16 * t, lane);
+      lgkm0();
+#pragma unroll
+      for (int t = 0; t < 4; ++t) oacc[t] = mfma(pa, vf[t], oacc[t]);
+    }
+  }
+  // normalise, store O (bf16) and the row log-sum-exp
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int i = ibase + r;
+    if (i >= a.T1) continue;
+    const float inv = lrun[r] > 0.f ? 1.f / lrun[r] : 0.f;
+    bf16* orow = a.o + ((long)b * a.T1 + i) * a.ldo + h * DK;
+#pragma unroll
+    for (int t = 0; t < 4; ++t) orow[16 * t + lc] = (bf16)(oacc[t][r] * inv);
+    if (lc == 0) a.lse[(long)z * a.T1 + i] = lrun[r] > 0.f ? mrun[r] + __logf(lrun[r]) : INFINITY;
+  }
+}
+
 // attn_bwdkv shared memory
 constexpr int V_QU = 0, V_QV = V_QU + BQ * 128, V_DO = V_QV + BQ * 128, V_P = V_DO + BQ * 128;
 constexpr int V_D = V_P + 96 * 128;               // D_i, lse_i*log2e (32 each), keep words [2][32]
@@ -1425,6 +1654,252 @@ __global__ __launch_bounds__(256, 2) void attn_bwdkv_kernel(AttnP a) {
   }
 }
 
+// ------------------------------------------------------------ attn_bwdkv, pipelined (v2)
+// attn_bwdkv_kernel with the same treatment: the 32-query tiles (q + u, q + v, dO images), their
+// D_i / lse_i / keep words and the positional rows (a 128-row ring: a tile's band is 96 rows,
+// the next tile's 32 new rows lie below it) are filled by LDS-DMA one tile ahead, so a tile
+// costs one barrier; each wave computes the three BD tiles its 16 keys read and gathers them by
+// ds_bpermute (no shared BDfull image, no second barrier).  dK, dV stay in registers.
+constexpr int RINGK = 128;
+template <bool REL>
+struct KV2 {
+  static constexpr int IMG = BQ * 128;                          // one 32-row km image
+  static constexpr int QU = 0, QV = QU + 2 * IMG, DO = QV + (REL ? 2 * IMG : 0), P = DO + 2 * IMG;
+  static constexpr int SM = P + (REL ? RINGK * 128 : 0);        // [2][D 32 | L 32 | mask 2 x 32]
+  static constexpr int LDS = SM + 2 * 128 * 4;
+};
+static_assert(KV2<true>::LDS <= 80 * 1024, "two workgroups per CU");
+
+// km_frag_tr2 via asm (rows k0 + q for half 0, k1 + q for half 1)
+EA_DEV bf16x8 km_tr2_asm(const char* img, int k0, int k1, int n0, int lane) {
+  const int i = lane & 15, q = i >> 2, p = i & 3;
+  const int col = n0 + 4 * p;
+  union { bf16x8 v; s16x4 h[2]; } out;
+  out.h[0] = tr_asm(img + km_off(k0 + q, col >> 3) + (col & 7) * 2);
+  out.h[1] = tr_asm(img + km_off(k1 + q, col >> 3) + (col & 7) * 2);
+  return out.v;
+}
+EA_DEV void dma_dword(char* lds, const void* src) {  // lane L writes lds + 4L
+  __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)src,
+                                   (__attribute__((address_space(3))) void*)lds, 4, 0, 0);
+}
+
+template <bool REL, int MM>
+__global__ __launch_bounds__(256, 2) void attn_bwdkv2_kernel(AttnP a) {
+  using L = KV2<REL>;
+  __shared__ __attribute__((aligned(16))) char sm[L::LDS];
+  const int nkb = (a.T2 + 63) / 64;
+  const int z = blockIdx.x / nkb, kb = blockIdx.x % nkb;
+  const int b = z / a.H, h = z % a.H;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int g = lane >> 4, lc = lane & 15;
+  const int kl = a.klen ? (int)min((long long)a.T2, a.klen[b]) : a.T2;
+  const uint64_t seed = MM == 2 ? ea_salted(a.seed, a.salt) : 0;
+  const int j0 = 64 * kb, jw = j0 + 16 * w;
+  f32x4 dka[4], dva[4];  // rows = keys jw + 4g + r, columns 16n + lc
+#pragma unroll
+  for (int n = 0; n < 4; ++n) dka[n] = dva[n] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  if (j0 < kl) {
+    const int j = jw + lc;
+    bf16x8 kf[2], vf[2];
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      kf[ks] = vf[ks] = (bf16x8){};
+      if (j < kl) {
+        kf[ks] = *(const bf16x8*)(a.k + ((long)b * a.T2 + j) * a.ldk + h * DK + 32 * ks + 8 * g);
+        vf[ks] = *(const bf16x8*)(a.v + ((long)b * a.T2 + j) * a.ldv + h * DK + 32 * ks + 8 * g);
+      }
+    }
+    const float dsc = MM ? 1.f / (1.f - a.p) : 1.f;
+    const float sl2 = a.scale * LOG2E;
+    const int istart = a.causal ? (j0 / BQ) * BQ : 0;
+    const int imin = a.causal ? j : 0;  // rows i in [imin, T1) see key j (if j < kl)
+    const int bpos = 16 * (w & 1) + lc;  // this lane's bit in keep word w>>1
+    const int ntile = (a.T1 - istart + BQ - 1) / BQ;
+    const int rs0 = a.T1 - 1 - (istart + BQ - 1) + j0;  // first tile's first band row
+    const bf16* quh = a.wsQu + (long)b * a.T1 * a.ldqu + h * DK;
+    const bf16* qvh = REL ? a.wsQv + (long)b * a.T1 * a.ldqvw + h * DK : nullptr;
+    const bf16* doh = a.dO + (long)b * a.T1 * a.lddo + h * DK;
+    const bf16* ph_ = REL ? a.pp + h * DK : nullptr;
+    // tile m: images at buffer m & 1; ring rows rs0 - 32m + [0, 96) at positions
+    // (row - rs0) mod 128; small arrays: D, lse (log2 scaled at use), keep words of 32 rows
+    auto dma_tile = [&](int m, bool first) {
+      const int i0 = istart + BQ * m;
+      const int buf = m & 1;
+      km_dma8(sm + L::QU + buf * L::IMG, 8 * w, quh, a.ldqu, i0 + 8 * w, a.T1, lane);
+      if (REL) km_dma8(sm + L::QV + buf * L::IMG, 8 * w, qvh, a.ldqvw, i0 + 8 * w, a.T1, lane);
+      km_dma8(sm + L::DO + buf * L::IMG, 8 * w, doh, a.lddo, i0 + 8 * w, a.T1, lane);
+      if (REL) {
+        // first tile: all 96 rows (12 groups); later: the 32 new rows below the previous band
+        const int x0 = first ? 0 : -32 * m, ng = first ? 12 : 4;
+        for (int gi = w; gi < ng; gi += 4) {
+          const int x = x0 + 8 * gi;  // relative to rs0; position x mod 128
+          km_dma8(sm + L::P, ((x % RINGK) + RINGK) % RINGK, ph_, a.ldp, rs0 + x, 2 * a.T1 - 1, lane);
+        }
+      }
+      if (w == 0) {
+        char* s = sm + L::SM + buf * 512;
+        const int ir = min(i0 + (lane & 31), a.T1 - 1);
+        const float* src = lane < 32 ? a.wsD + (long)z * a.T1 + ir : a.lse + (long)z * a.T1 + ir;
+        dma_dword(s, src);
+        if (MM == 1) dma_dword(s + 256, a.dmask + ((long)z * a.T1 + ir) * a.ldm + (j0 >> 5) + (lane >> 5));
+      }
+    };
+    if (ntile > 0) dma_tile(0, true);
+    for (int m = 0; m < ntile; ++m) {
+      const int i0 = istart + BQ * m;
+      vmcnt_le<0>();
+      bar();
+      if (m + 1 < ntile) dma_tile(m + 1, false);
+      const int buf = m & 1;
+      const char* quimg = sm + L::QU + buf * L::IMG;
+      const char* qvimg = sm + L::QV + buf * L::IMG;
+      const char* doimg = sm + L::DO + buf * L::IMG;
+      const char* smv = sm + L::SM + buf * 512;
+      // S (32 queries x this wave's 16 keys): s[mi] rows 16mi + 4g + r, key column jw + lc
+      f32x4 s[2], dp[2];
+      {
+        bf16x8 qf[2][2], df[2][2];
+#pragma unroll
+        for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+          for (int ks = 0; ks < 2; ++ks) {
+            qf[mi][ks] = km_frag_asm(quimg, 16 * mi, ks, lane);
+            df[mi][ks] = km_frag_asm(doimg, 16 * mi, ks, lane);
+          }
+        lgkm0();
+#pragma unroll
+        for (int mi = 0; mi < 2; ++mi) {
+          s[mi] = dp[mi] = (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+          for (int ks = 0; ks < 2; ++ks) {
+            s[mi] = mfma(qf[mi][ks], kf[ks], s[mi]);
+            dp[mi] = mfma(df[mi][ks], vf[ks], dp[mi]);
+          }
+        }
+      }
+      if (REL) {
+        // BDfull tiles (mi, t) for t in {w, w+1, w+2}: band rows rs + 16t + [0, 16) with
+        // rs = rs0 - 32m (ring position (16t - 32m) mod 128)
+        f32x4 bd[2][3];
+        {
+          bf16x8 vq[2][2], pf[3][2];
+#pragma unroll
+          for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+            for (int ks = 0; ks < 2; ++ks) vq[mi][ks] = km_frag_asm(qvimg, 16 * mi, ks, lane);
+#pragma unroll
+          for (int u = 0; u < 3; ++u) {
+            const int rp = (((16 * (w + u) - 32 * m) % RINGK) + RINGK) % RINGK;
+#pragma unroll
+            for (int ks = 0; ks < 2; ++ks) pf[u][ks] = km_frag_asm(sm + L::P, rp, ks, lane);
+          }
+          lgkm0();
+#pragma unroll
+          for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+            for (int u = 0; u < 3; ++u) {
+              bd[mi][u] = (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+              for (int ks = 0; ks < 2; ++ks) bd[mi][u] = mfma(vq[mi][ks], pf[u][ks], bd[mi][u]);
+            }
+        }
+        // (il = 16mi + 4g + r, jl = 16w + lc) reads BDfull column 31 - il + jl = 16(w + u) +
+        // ((lc + 31 - 16mi - 4g - r) & 15), u = (lc + 31 - 16mi - 4g - r) >> 4
+#pragma unroll
+        for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int sft = lc + 31 - 16 * mi - 4 * g - r;
+            const int src = (16 * g + (sft & 15)) * 4;
+            const float x0 = __int_as_float(__builtin_amdgcn_ds_bpermute(src, __float_as_int(bd[mi][0][r])));
+            const float x1 = __int_as_float(__builtin_amdgcn_ds_bpermute(src, __float_as_int(bd[mi][1][r])));
+            const float x2 = __int_as_float(__builtin_amdgcn_ds_bpermute(src, __float_as_int(bd[mi][2][r])));
+            const int u = sft >> 4;
+            s[mi][r] += u == 0 ? x0 : (u == 1 ? x1 : x2);
+          }
+      }
+      // keep words of rows 16mi + 4g + r (this lane's bit bpos), D_i, lse_i
+      float Dm[2][4], Lm[2][4];
+      uint32_t mr[2][4];
+      {
+        bf16x8 dv[2], lv[2], mv[2];
+#pragma unroll
+        for (int mi = 0; mi < 2; ++mi) {
+          dv[mi] = ld128_asm(smv + (16 * mi + 4 * g) * 4);
+          lv[mi] = ld128_asm(smv + 128 + (16 * mi + 4 * g) * 4);
+          if (MM == 1) mv[mi] = ld128_asm(smv + 256 + (w >> 1) * 128 + (16 * mi + 4 * g) * 4);
+        }
+        lgkm0();
+#pragma unroll
+        for (int mi = 0; mi < 2; ++mi) {
+          const float4 D4 = __builtin_bit_cast(float4, dv[mi]);
+          const float4 L4 = __builtin_bit_cast(float4, lv[mi]);
+          Dm[mi][0] = D4.x; Dm[mi][1] = D4.y; Dm[mi][2] = D4.z; Dm[mi][3] = D4.w;
+          Lm[mi][0] = L4.x * LOG2E; Lm[mi][1] = L4.y * LOG2E; Lm[mi][2] = L4.z * LOG2E; Lm[mi][3] = L4.w * LOG2E;
+          if (MM == 1) {
+            const uint4 m4 = __builtin_bit_cast(uint4, mv[mi]);
+            mr[mi][0] = m4.x; mr[mi][1] = m4.y; mr[mi][2] = m4.z; mr[mi][3] = m4.w;
+          }
+        }
+      }
+      if (MM == 2) {
+        const uint32_t key = ea_seed_key(seed), thr = ea_drop_thr(a.p);
+#pragma unroll
+        for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int i = i0 + 16 * mi + 4 * g + r;
+            mr[mi][r] = (uint32_t)attn_keep(key, thr, (uint64_t)z * a.T1 + i, a.T2, j) << bpos;
+          }
+      }
+      union { bf16x8 v; bf16 e[8]; } ap, as;
+#pragma unroll
+      for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int i = i0 + 16 * mi + 4 * g + r;
+          const bool ok = j < kl && (unsigned)(i - imin) < (unsigned)(a.T1 - imin);
+          const float e = __builtin_amdgcn_exp2f(fmaf(s[mi][r], sl2, -Lm[mi][r]));
+          const float P = ok ? e : 0.f;
+          const float kp = MM ? (((mr[mi][r] >> bpos) & 1u) ? dsc : 0.f) : 1.f;
+          as.e[4 * mi + r] = (bf16)((P * a.scale) * fmaf(dp[mi][r], kp, -Dm[mi][r]));
+          ap.e[4 * mi + r] = (bf16)(P * kp);
+        }
+      // dV += Pd^T dO, dK += dS^T (Q+u): A = (key, 8 queries {4g..4g+3, 16+4g..16+4g+3}),
+      // B = dO / Q+u rows in the same order (transposed reads)
+      {
+        bf16x8 bo[4], bu[4];
+#pragma unroll
+        for (int n = 0; n < 4; ++n) {
+          bo[n] = km_tr2_asm(doimg, 4 * g, 16 + 4 * g, 16 * n, lane);
+          bu[n] = km_tr2_asm(quimg, 4 * g, 16 + 4 * g, 16 * n, lane);
+        }
+        lgkm0();
+#pragma unroll
+        for (int n = 0; n < 4; ++n) {
+          dva[n] = mfma(ap.v, bo[n], dva[n]);
+          dka[n] = mfma(as.v, bu[n], dka[n]);
+        }
+      }
+    }
+  }
+  // dK, dV rows jw + 4g + r (zero for keys at or past klen)
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int j = jw + 4 * g + r;
+    if (j >= a.T2) continue;
+    bf16* dkr = a.dk + ((long)b * a.T2 + j) * a.lddk + h * DK;
+    bf16* dvr = a.dv + ((long)b * a.T2 + j) * a.lddv + h * DK;
+    const bool ok = j < kl;
+#pragma unroll
+    for (int n = 0; n < 4; ++n) {
+      dkr[16 * n + lc] = (bf16)(ok ? dka[n][r] : 0.f);
+      dvr[16 * n + lc] = (bf16)(ok ? dva[n][r] : 0.f);
+    }
+  }
+}
+
 AttnP make_p(int B, int H, int T1, int T2, const void* q, long ldq, const void* k, long ldk, const void* v, long ldv,
              const float* bu, const float* bv, const void* pp, long ldp, const long long* klen, int causal, float scale,
              float p, unsigned long long seed) {
@@ -1452,8 +1927,22 @@ extern "C" int ea_attn_fused_fwd2(int B, int H, int T1, int T2, int dk, const vo
   a.o = (bf16*)o; a.ldo = ldo; a.lse = lse;
   a.dmask = (uint32_t*)dmask; a.ldm = ldm;
   dim3 grid(B * H * ((T1 + QB - 1) / QB));
-  if (pp) hipLaunchKernelGGL(attn_fwd_kernel<true>, grid, dim3(256), 0, (hipStream_t)stream, a);
-  else hipLaunchKernelGGL(attn_fwd_kernel<false>, grid, dim3(256), 0, (hipStream_t)stream, a);
+  const hipStream_t st = (hipStream_t)stream;
+  const char* ev = getenv("EA_ATTN_FWD_V1");  // A/B: the original forward kernel
+  const bool v1 = ev && ev[0] == '1';
+  const int mm = p > 0.f ? (dmask ? 1 : 2) : 0;
+  if (v1) {
+    if (pp) hipLaunchKernelGGL(attn_fwd_kernel<true>, grid, dim3(256), 0, st, a);
+    else hipLaunchKernelGGL(attn_fwd_kernel<false>, grid, dim3(256), 0, st, a);
+  } else if (pp) {
+    if (mm == 0) hipLaunchKernelGGL((attn_fwd2_kernel<true, 0>), grid, dim3(256), 0, st, a);
+    else if (mm == 1) hipLaunchKernelGGL((attn_fwd2_kernel<true, 1>), grid, dim3(256), 0, st, a);
+    else hipLaunchKernelGGL((attn_fwd2_kernel<true, 2>), grid, dim3(256), 0, st, a);
+  } else {
+    if (mm == 0) hipLaunchKernelGGL((attn_fwd2_kernel<false, 0>), grid, dim3(256), 0, st, a);
+    else if (mm == 1) hipLaunchKernelGGL((attn_fwd2_kernel<false, 1>), grid, dim3(256), 0, st, a);
+    else hipLaunchKernelGGL((attn_fwd2_kernel<false, 2>), grid, dim3(256), 0, st, a);
+  }
   EA_LAUNCH_CHECK();
   return 0;
 }
@@ -1470,18 +1959,26 @@ static int attn_bwd_launch(AttnP& a, bool rel, bool v2, hipStream_t st) {
   const int nqb = (a.T1 + QB - 1) / QB, nkb = (a.T2 + 63) / 64;
   const dim3 gq(a.B * a.H * nqb), gkv(a.B * a.H * nkb);
   const int mm = a.p > 0.f ? (a.dmask ? 1 : 2) : 0;
+  const char* ev = getenv("EA_ATTN_BWDKV_V1");  // A/B: the original dK/dV pass
+  const bool kv1 = ev && ev[0] == '1';
   if (rel) {
     if (v2 && mm == 0) hipLaunchKernelGGL((attn_bwdq2_kernel<true, 0>), gq, dim3(256), 0, st, a);
     else if (v2 && mm == 1) hipLaunchKernelGGL((attn_bwdq2_kernel<true, 1>), gq, dim3(256), 0, st, a);
     else if (v2) hipLaunchKernelGGL((attn_bwdq2_kernel<true, 2>), gq, dim3(256), 0, st, a);
     else hipLaunchKernelGGL(attn_bwdq_kernel<true>, gq, dim3(256), 0, st, a);
-    hipLaunchKernelGGL(attn_bwdkv_kernel<true>, gkv, dim3(256), 0, st, a);
+    if (kv1) hipLaunchKernelGGL(attn_bwdkv_kernel<true>, gkv, dim3(256), 0, st, a);
+    else if (mm == 0) hipLaunchKernelGGL((attn_bwdkv2_kernel<true, 0>), gkv, dim3(256), 0, st, a);
+    else if (mm == 1) hipLaunchKernelGGL((attn_bwdkv2_kernel<true, 1>), gkv, dim3(256), 0, st, a);
+    else hipLaunchKernelGGL((attn_bwdkv2_kernel<true, 2>), gkv, dim3(256), 0, st, a);
   } else {
     if (v2 && mm == 0) hipLaunchKernelGGL((attn_bwdq2_kernel<false, 0>), gq, dim3(256), 0, st, a);
     else if (v2 && mm == 1) hipLaunchKernelGGL((attn_bwdq2_kernel<false, 1>), gq, dim3(256), 0, st, a);
     else if (v2) hipLaunchKernelGGL((attn_bwdq2_kernel<false, 2>), gq, dim3(256), 0, st, a);
     else hipLaunchKernelGGL(attn_bwdq_kernel<false>, gq, dim3(256), 0, st, a);
-    hipLaunchKernelGGL(attn_bwdkv_kernel<false>, gkv, dim3(256), 0, st, a);
+    if (kv1) hipLaunchKernelGGL(attn_bwdkv_kernel<false>, gkv, dim3(256), 0, st, a);
+    else if (mm == 0) hipLaunchKernelGGL((attn_bwdkv2_kernel<false, 0>), gkv, dim3(256), 0, st, a);
+    else if (mm == 1) hipLaunchKernelGGL((attn_bwdkv2_kernel<false, 1>), gkv, dim3(256), 0, st, a);
+    else hipLaunchKernelGGL((attn_bwdkv2_kernel<false, 2>), gkv, dim3(256), 0, st, a);
   }
   EA_LAUNCH_CHECK();
   return 0;

@@ -336,3 +336,74 @@ def test_bwdq_pipelined_matches_original(B, H, T, klens, p, mask):
     assert _rel(dq2, dq1) < 2e-3
     assert float((dq2.float() - dq1.float()).abs().max()) <= 2e-2 * float(dq1.float().abs().max())
     assert _rel(p2[1], p1[1]) < 1e-4
+
+
+@pytest.mark.parametrize("B,H,T1,T2,rel,causal,klens,p", [
+    (3, 2, 249, 249, True, False, [249, 200, 64], 0.1),
+    (2, 3, 137, 137, True, False, [137, 100], 0.0),
+    (1, 2, 300, 300, True, False, [300], 0.1),
+    (2, 2, 45, 45, False, True, [45, 30], 0.1),
+    (2, 1, 41, 300, False, False, [300, 131], 0.0),
+    (1, 1, 5, 5, True, False, [5], 0.1),
+])
+def test_fwd_pipelined_matches_original(B, H, T1, T2, rel, causal, klens, p, monkeypatch):
+    """The pipelined forward (LDS-DMA one chunk ahead, bpermute BD gather, Pd^T image) is the
+    original forward's arithmetic in the same order: O, lse and the keep bits bit for bit."""
+    from espnet_amd import hip_ops as ops
+    from espnet_amd._lib import lib
+    q, k, v, u, vb, pp, _ = _inputs(B, H, T1, T2, rel, seed=21)
+    klen = torch.tensor(klens, dtype=torch.long, device=DEV)
+    d = H * 64
+    ldm = 2 * ((T2 + 63) // 64)
+    ptr = lambda t: 0 if t is None else t.data_ptr()  # noqa: E731
+    out = []
+    for v1 in ("1", "0"):
+        monkeypatch.setenv("EA_ATTN_FWD_V1", v1)
+        O = torch.empty(B, T1, d, dtype=bf, device=DEV)
+        lse = torch.empty(B * H * T1, device=DEV)
+        dmask = torch.zeros(B * H * T1 * ldm, dtype=torch.int32, device=DEV)
+        lib.ea_attn_fused_fwd2(B, H, T1, T2, 64, q.data_ptr(), d, k.data_ptr(), d, v.data_ptr(), d, ptr(u),
+                               ptr(vb), ptr(pp), d, klen.data_ptr(), int(causal), 1 / 8, p, 5, O.data_ptr(), d,
+                               lse.data_ptr(), dmask.data_ptr() if p > 0 else 0, ldm, ops.stream())
+        torch.cuda.synchronize()
+        out.append((O, lse, dmask))
+    (O1, l1, m1), (O2, l2, m2) = out
+    assert torch.equal(O1, O2) and torch.equal(l1, l2) and torch.equal(m1, m2)
+
+
+@pytest.mark.parametrize("B,H,T1,T2,rel,causal,klens,p,mask", [
+    (3, 2, 249, 249, True, False, [249, 200, 64], 0.1, True),
+    (2, 3, 137, 137, True, False, [137, 100], 0.0, False),
+    (1, 2, 300, 300, True, False, [300], 0.1, False),
+    (2, 2, 45, 45, False, True, [45, 30], 0.1, True),
+    (2, 1, 41, 300, False, False, [300, 131], 0.0, False),
+    (1, 1, 5, 5, True, False, [5], 0.1, True),
+])
+def test_bwdkv_pipelined_matches_original(B, H, T1, T2, rel, causal, klens, p, mask, monkeypatch):
+    """The pipelined dK/dV pass (LDS-DMA one query tile ahead, per-wave BD tiles gathered by
+    bpermute) recomputes the same values in the same MFMA order: dK, dV bit for bit."""
+    from espnet_amd import hip_ops as ops
+    from espnet_amd._lib import lib
+    from espnet_amd.layers.common import attn_fused_bwd
+    q, k, v, u, vb, pp, dO = _inputs(B, H, T1, T2, rel, seed=31)
+    klen = torch.tensor(klens, dtype=torch.long, device=DEV)
+    d = H * 64
+    ldm = 2 * ((T2 + 63) // 64)
+    ptr = lambda t: 0 if t is None else t.data_ptr()  # noqa: E731
+    O = torch.empty(B, T1, d, dtype=bf, device=DEV)
+    lse = torch.empty(B * H * T1, device=DEV)
+    dmask = torch.zeros(B * H * T1 * ldm, dtype=torch.int32, device=DEV) if mask else None
+    lib.ea_attn_fused_fwd2(B, H, T1, T2, 64, q.data_ptr(), d, k.data_ptr(), d, v.data_ptr(), d, ptr(u), ptr(vb),
+                           ptr(pp), d, klen.data_ptr(), int(causal), 1 / 8, p, 9, O.data_ptr(), d, lse.data_ptr(),
+                           ptr(dmask), ldm, ops.stream())
+    out = []
+    for v1 in ("1", "0"):
+        monkeypatch.setenv("EA_ATTN_BWDKV_V1", v1)
+        dq, dk, dv = torch.empty_like(q), torch.empty_like(k), torch.empty_like(v)
+        attn_fused_bwd(B=B, H=H, T1=T1, T2=T2, q=q, ldq=d, k=k, ldk=d, v=v, ldv=d, bu=u, bv=vb, pp=pp, ldp=d,
+                       klen=klen, causal=causal, scale=1 / 8, p=p, seed=9, O=O, ldo=d, lse=lse, dO=dO, lddo=d,
+                       dq=dq, lddq=d, dk=dk, lddk=d, dv=dv, lddv=d, dmask=dmask, ldm=ldm)
+        torch.cuda.synchronize()
+        out.append((dq, dk, dv))
+    (dq1, dk1, dv1), (dq2, dk2, dv2) = out
+    assert torch.equal(dq1, dq2) and torch.equal(dk1, dk2) and torch.equal(dv1, dv2)
