@@ -27,6 +27,9 @@ from .. import hip_ops as ops
 from .._lib import lib
 
 
+LOGZERO = -10000000000.0  # ctc_prefix_score.py:33
+
+
 class Hypothesis(NamedTuple):
     """beam_search.py:17-29."""
 
@@ -94,8 +97,26 @@ class CTCPrefixScorer:
 
     @staticmethod
     def select_state(state, i, new_id=None):
+        if len(state) == 5:  # a CTCPrefixScoreTH state (batch_score_partial), ctc.py:40-63
+            r_new, log_psi, f_min, f_max, cand = state
+            row = cand[i].tolist()
+            pos = row.index(int(new_id)) if int(new_id) in row else 0
+            return r_new[0][i, pos], log_psi[i, int(new_id)].expand(log_psi.size(1)), f_min, f_max
         sc, st = state
         return sc[i], st[i]
+
+    def batch_init_state(self, x: torch.Tensor):
+        """ctc.py:87-99: the vectorised scorer over this utterance's log-posteriors."""
+        from .ctc_prefix_score import CTCPrefixScoreTH
+        logp = self.ctc.log_softmax(x.unsqueeze(0)).float()
+        self.impl = CTCPrefixScoreTH(logp, torch.tensor([logp.size(1)]), 0, self.eos)
+        return None
+
+    def batch_score_partial(self, y, ids, state, x):
+        """ctc.py:101-126: score the pre-beam ids of every hypothesis in one call."""
+        batch_state = (([s[0] for s in state], torch.stack([s[1] for s in state]), state[0][2], state[0][3])
+                       if state[0] is not None else None)
+        return self.impl(y, batch_state, ids)
 
     def final_score(self, state):
         return 0.0
@@ -298,8 +319,61 @@ class BeamSearch(torch.nn.Module):
 
 
 class BatchBeamSearch(BeamSearch):
-    """espnet/nets/batch_beam_search.py:26 (BatchBeamSearch: every running hypothesis scored
-    in one batched call per scorer, states kept batched).  BeamSearch above already runs that
-    way — batched full scorers over the decoder's key/value cache, one CTC prefix launch per
-    step — so this is the same search under the reference's class name."""
+    """espnet/nets/batch_beam_search.py:26-348 (BatchBeamSearch).  The scoring is batched as in
+    BeamSearch above (decoder over its key/value cache, one CTC prefix launch per step); what
+    differs is the reference's selection rule, reproduced here:
+      * partial scores are full-vocabulary rows as CTCPrefixScoreTH returns them: the pre-beam
+        ids scored, <eos> ALWAYS scored with the full-sequence probability (TH sets it for every
+        hypothesis, ctc_prefix_score.py:178-179), blank and everything else logzero - prefix;
+      * the new beam is the global top-k over the flattened (n_hyps x vocab) weighted scores
+        (batch_beam, :81-101), in topk order, with no final-score step in post_process."""
+
+    def search(self, running_hyps: List[Hypothesis], x: torch.Tensor) -> List[Hypothesis]:
+        n, V = len(running_hyps), self.n_vocab
+        allsc, allst = self._score_all(running_hyps, x)
+        W = torch.zeros(n, V, dtype=torch.float32)
+        for k in self.full_scorers:
+            W += self.weights[k] * allsc[k]
+        if self.do_pre_beam:
+            pre = W if self.pre_beam_score_key == "full" else allsc[self.pre_beam_score_key]
+            ids = torch.topk(pre, self.pre_beam_size, dim=1)[1]
+        else:
+            ids = torch.arange(V).expand(n, V)
+        if ids.shape[1] < V:  # <eos> scored for every hypothesis (a duplicate column if pre-beamed)
+            ids = torch.cat([ids, torch.full((n, 1), self.eos, dtype=ids.dtype)], dim=1)
+        part, pos = {}, {}
+        for k, d in self.part_scorers.items():
+            sc, st = d.score_partial_multi([h.yseq for h in running_hyps], list(ids),
+                                           [h.states[k] for h in running_hyps])
+            full = torch.full((n, V), LOGZERO, dtype=torch.float32)
+            full -= torch.stack([torch.as_tensor(h.states[k][0], dtype=torch.float32) for h in running_hyps]).view(n, 1)
+            full.scatter_(1, ids, torch.stack(sc))
+            part[k] = (full, st)
+            W += self.weights[k] * full
+        W += torch.stack([torch.as_tensor(h.score, dtype=torch.float32) for h in running_hyps]).view(n, 1)
+        top = W.view(-1).topk(self.beam_size)[1]
+        best_hyps = []
+        for t in top.tolist():
+            hi, j = divmod(t, V)
+            hyp = running_hyps[hi]
+            new_scores = {k: hyp.scores[k] + allsc[k][hi, j] for k in self.full_scorers}
+            new_scores.update({k: hyp.scores[k] + part[k][0][hi, j] for k in self.part_scorers})
+            new_states = {k: (hyp.states[k] if allst[k] is None else allst[k][hi]) for k in self.full_scorers}
+            row = ids[hi].tolist()
+            pj = row.index(j) if j in row else 0  # TH's scoring_idmap fallback
+            new_states.update({k: d.select_state(part[k][1][hi], pj) for k, d in self.part_scorers.items()})
+            best_hyps.append(Hypothesis(score=W[hi, j], yseq=self.append_token(hyp.yseq, j), scores=new_scores,
+                                        states=new_states))
+        return best_hyps
+
+    def post_process(self, i: int, maxlen: int, maxlenratio: float, running_hyps: List[Hypothesis],
+                     ended_hyps: List[Hypothesis]) -> List[Hypothesis]:
+        """batch_beam_search.py:303-348: <eos> forced at maxlen, ended hypotheses moved out (no
+        final-score step)."""
+        if i == maxlen - 1:
+            running_hyps = [h._replace(yseq=self.append_token(h.yseq, self.eos)) for h in running_hyps]
+        remained = []
+        for hyp in running_hyps:
+            (ended_hyps if int(hyp.yseq[-1]) == self.eos else remained).append(hyp)
+        return remained
 

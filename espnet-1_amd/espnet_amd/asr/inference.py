@@ -85,12 +85,14 @@ def attention_greedy(model, speech: torch.Tensor, speech_lengths: torch.Tensor, 
 @torch.no_grad()
 def attention_beam_search(model, speech: torch.Tensor, speech_lengths: torch.Tensor, beam_size: int,
                           length_bonus: float = 0.0, maxlenratio: float = 0.0, minlenratio: float = 0.0,
-                          ctc_weight: float = 0.0):
+                          ctc_weight: float = 0.0, batch: bool = False):
     """Speech2Text-style decoding (espnet2/bin/asr_inference.py:140-175) with BeamSearch
     (espnet/nets/beam_search.py) over the decoder (weight 1 - ctc_weight), the CTC prefix
     scorer (ctc_weight, pre-beam "full") and LengthBonus (length_bonus): per utterance the
     n-best list of Hypothesis records (yseq with <sos>/<eos>, score, per-scorer scores)."""
-    from .beam_search import BeamSearch, CTCPrefixScorer, LengthBonus
+    from .beam_search import BatchBeamSearch, BeamSearch, CTCPrefixScorer, LengthBonus
+    if batch:  # espnet/nets/batch_beam_search.py under its own name (the same batched search)
+        BeamSearch = BatchBeamSearch  # noqa: N806
     was = model.training
     model.eval()
     try:

@@ -950,6 +950,89 @@ def capture_beam(name="beam", cfg_name="tiny_hybrid"):
     print(f"{name}: {len(meta)} searches -> {path}")
 
 
+def capture_ctc_th(name="ctc_th"):
+    """espnet/nets/ctc_prefix_score.py CTCPrefixScoreTH (the vectorised prefix scorer the
+    reference's BatchBeamSearch uses through CTCPrefixScorer.batch_score_partial) on seeded
+    log-posteriors of two utterances of different lengths: three steps (full vocabulary, a
+    pre-beam subset, full again) with index_select_state between them, including a selected
+    label outside the scored subset (its state falls back to candidate 0, as the reference
+    does).  Records every step's local scores."""
+    from espnet.nets.ctc_prefix_score import CTCPrefixScoreTH
+    g = torch.Generator().manual_seed(5)
+    B, T, O, W = 2, 23, 9, 3
+    eos = O - 1
+    x = torch.log_softmax(torch.randn(B, T, O, generator=g) * 2.0, dim=-1)
+    xlens = torch.tensor([23, 17])
+    out = {"x": np32(x), "xlens": xlens.numpy().astype(np.int64)}
+    impl = CTCPrefixScoreTH(x.clone(), xlens, 0, eos)
+    n_bh = B * W
+    y = [torch.tensor([eos]) for _ in range(n_bh)]
+    state = None
+    plan = [None, torch.tensor([[1, 2, 3, 8], [2, 4, 5, 6], [1, 3, 5, 7], [2, 3, 4, 5], [1, 6, 7, 8],
+                                [3, 4, 6, 7]]), None]
+    best_plan = [torch.tensor([[1, 9 + 2, 18 + 3], [4, 9 + 5, 18 + 7]]),
+                 torch.tensor([[2, 9 + 4, 18 + 6], [3 + 9, 18 + 7, 8]]),
+                 None]
+    for step, sids in enumerate(plan):
+        sc, st = impl(y, state, sids)
+        out[f"s{step}.scores"] = np32(sc)
+        out[f"s{step}.y"] = np.stack([yy.numpy() for yy in y]).astype(np.int64)
+        if sids is not None:
+            out[f"s{step}.ids"] = sids.numpy().astype(np.int64)
+        best = best_plan[step]
+        if best is None:
+            break
+        out[f"s{step}.best"] = best.numpy().astype(np.int64)
+        state = impl.index_select_state(st, best)
+        hyp = (best // O + (torch.arange(B) * W).view(-1, 1)).view(-1)
+        lab = torch.fmod(best, O).view(-1)
+        y = [torch.cat([y[int(h)], lab[i:i + 1]]) for i, h in enumerate(hyp)]
+    out["cfg"] = np.array(json.dumps({"B": B, "T": T, "O": O, "W": W, "eos": eos, "blank": 0}))
+    path = os.path.join(OUT, f"{name}.npz")
+    np.savez_compressed(path, **out)
+    print(f"{name} -> {path}")
+
+
+def capture_beam_batch(name="beam_batch", cfg_name="tiny_hybrid"):
+    """espnet/nets/batch_beam_search.py BatchBeamSearch (decoder batch_score, CTCPrefixScorer
+    batch_score_partial over CTCPrefixScoreTH, LengthBonus) on the tiny hybrid model, the
+    BEAM_CASES of capture_beam with CTC weight > 0."""
+    from espnet.nets.batch_beam_search import BatchBeamSearch
+    from espnet.nets.scorers.ctc import CTCPrefixScorer
+    from espnet.nets.scorers.length_bonus import LengthBonus
+    z = np.load(os.path.join(OUT, cfg_name + ".npz"))
+    cfg = json.loads(str(z["cfg"]))
+    model = build_reference_model(cfg)
+    model.load_state_dict({k[2:]: torch.from_numpy(z[k]) for k in z.files if k.startswith("w.")})
+    model.eval()
+    speech = torch.from_numpy(z["in.speech"])
+    lens = torch.from_numpy(z["in.speech_lengths"])
+    V = model.vocab_size
+    cases = [c for c in BEAM_CASES if len(c) > 3] + [(3, 0.0, 0.0, 1.0)]
+    out, meta = {}, []
+    with torch.no_grad():
+        for ci, case in enumerate(cases):
+            beam, lb, mlr, cw = case
+            bs = BatchBeamSearch(scorers={"decoder": model.decoder, "ctc": CTCPrefixScorer(model.ctc, model.eos),
+                                          "length_bonus": LengthBonus(V)},
+                                 weights={"decoder": 1.0 - cw, "ctc": cw, "length_bonus": lb}, beam_size=beam,
+                                 vocab_size=V, sos=model.sos, eos=model.eos, token_list=None,
+                                 pre_beam_score_key="full")
+            for u in range(speech.shape[0]):
+                le = int(lens[u])
+                enc, _ = model.encode(speech[u:u + 1, :le], lens[u:u + 1])
+                nbest = bs(x=enc[0], maxlenratio=mlr, minlenratio=0.0)
+                for r, h in enumerate(nbest):
+                    key = f"c{ci}.u{u}.h{r}"
+                    out[key + ".yseq"] = h.yseq.numpy().astype(np.int64)
+                    out[key + ".score"] = np.float64(float(h.score))
+                meta.append({"case": ci, "utt": u, "n": len(nbest)})
+    out["cfg"] = np.array(json.dumps({"cases": cases, "nbest": meta, "model": cfg_name}))
+    path = os.path.join(OUT, f"{name}.npz")
+    np.savez_compressed(path, **out)
+    print(f"{name}: {len(meta)} searches -> {path}")
+
+
 if __name__ == "__main__":
     os.makedirs(OUT, exist_ok=True)
     which = sys.argv[1:] or ["models", "train", "ops", "ddp"]
@@ -973,6 +1056,10 @@ if __name__ == "__main__":
         capture_frontend()
     if "beam" in which:
         capture_beam()
+    if "ctc_th" in which:
+        capture_ctc_th()
+    if "beam_batch" in which:
+        capture_beam_batch()
     if "train_specaug" in which:
         capture_train_specaug()
     if "epoch" in which:
