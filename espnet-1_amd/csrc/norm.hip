@@ -425,7 +425,10 @@ __global__ __launch_bounds__(256) void ln_bwd_vec_kernel(int rows, int d, const 
   // U rows per wave step (rows rb and rb + 4): every load of both rows is issued before
   // either row is computed (the grid is ~2 waves per SIMD: latency, not bandwidth, bounds a
   // one-row step).  Rows are still folded into the partials in order rb, rb + 4.
-  constexpr int U = NJ == 1 ? 2 : 1;
+#ifndef EA_LN_BWD_U
+#define EA_LN_BWD_U 2
+#endif
+  constexpr int U = NJ == 1 ? EA_LN_BWD_U : 1;
   for (int rb = r0 + w; rb < r1; rb += 4 * U) {
     float xv[U][NJ][8], dv[U][NJ][8], pv[U][NJ][8], mu[U], rs[U];
 #pragma unroll
