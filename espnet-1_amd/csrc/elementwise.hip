@@ -1302,3 +1302,28 @@ extern "C" int ea_conv1_wgrad_reduce(int ntiles, int C, const float* part, float
   if (rc) return rc;
   return ea_reduce_partials(ntiles, C, part + 9L * C, 10L * C, dbias, 1, stream);
 }
+
+// ------------------------------------------------------------------ ReLU (f32, in place)
+// The ReLU of the legacy Encoder's "linear" input layer (Linear -> LayerNorm -> Dropout -> ReLU,
+// espnet/nets/pytorch_backend/transformer/encoder.py:120-127) used by TransformerLM.
+namespace {
+__global__ void relu_inplace_kernel(long n, float* __restrict__ x) {
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n / 4; i += (long)gridDim.x * blockDim.x) {
+    float4 v = ((float4*)x)[i];
+    v.x = fmaxf(v.x, 0.f); v.y = fmaxf(v.y, 0.f); v.z = fmaxf(v.z, 0.f); v.w = fmaxf(v.w, 0.f);
+    ((float4*)x)[i] = v;
+  }
+  for (long i = (n / 4) * 4 + blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x)
+    x[i] = fmaxf(x[i], 0.f);
+}
+}  // namespace
+
+extern "C" int ea_relu_f32_inplace(long n, float* x, void* stream) {
+  EA_ENTRY();
+  EA_CHECK_ARG(n >= 0 && (n == 0 || (x && (uintptr_t)x % 16 == 0)));
+  if (n == 0) return 0;
+  hipLaunchKernelGGL(relu_inplace_kernel, dim3(ea_grid_cap(ea_cdiv(n / 4 + 1, 256), 4096)), dim3(256), 0,
+                     (hipStream_t)stream, n, x);
+  EA_LAUNCH_CHECK();
+  return 0;
+}

@@ -85,7 +85,7 @@ def attention_greedy(model, speech: torch.Tensor, speech_lengths: torch.Tensor, 
 @torch.no_grad()
 def attention_beam_search(model, speech: torch.Tensor, speech_lengths: torch.Tensor, beam_size: int,
                           length_bonus: float = 0.0, maxlenratio: float = 0.0, minlenratio: float = 0.0,
-                          ctc_weight: float = 0.0, batch: bool = False):
+                          ctc_weight: float = 0.0, batch: bool = False, lm=None, lm_weight: float = 1.0):
     """Speech2Text-style decoding (espnet2/bin/asr_inference.py:140-175) with BeamSearch
     (espnet/nets/beam_search.py) over the decoder (weight 1 - ctc_weight), the CTC prefix
     scorer (ctc_weight, pre-beam "full") and LengthBonus (length_bonus): per utterance the
@@ -97,9 +97,12 @@ def attention_beam_search(model, speech: torch.Tensor, speech_lengths: torch.Ten
     model.eval()
     try:
         V = model.vocab_size
-        bs = BeamSearch(scorers={"decoder": model.decoder, "ctc": CTCPrefixScorer(model.ctc, model.eos),
-                                 "length_bonus": LengthBonus(V)},
-                        weights={"decoder": 1.0 - ctc_weight, "ctc": ctc_weight, "length_bonus": length_bonus},
+        scorers = {"decoder": model.decoder, "ctc": CTCPrefixScorer(model.ctc, model.eos),
+                   "length_bonus": LengthBonus(V)}
+        weights = {"decoder": 1.0 - ctc_weight, "ctc": ctc_weight, "length_bonus": length_bonus}
+        if lm is not None:  # shallow fusion (asr_inference.py:149-183: scorers["lm"], lm_weight)
+            scorers["lm"], weights["lm"] = lm, lm_weight
+        bs = BeamSearch(scorers=scorers, weights=weights,
                         beam_size=beam_size, vocab_size=V, sos=model.sos, eos=model.eos, pre_beam_score_key="full")
         res = []
         for b in range(speech.shape[0]):

@@ -79,7 +79,7 @@ class TransformerBlockFn(torch.autograd.Function):
         qkv = empty(N, 3 * d, dtype=cd, device=dev)
         ops.linear(xn1, b.w(*_QKV_W, shape=(3 * d, d)), qkv, epi=ops.make_epi(bias=b.f(*_QKV_B, shape=(3 * d,))))
         O, st = _mha_fwd(qkv, qkv[:, d:], qkv[:, 2 * d:], B=B, H=H, T1=T, T2=T, dk=dk, ldq=3 * d, ldk=3 * d,
-                         ldv=3 * d, klen=olens, causal=False, scale=scale, p=pa, seed=sd(1), cd=cd)
+                         ldv=3 * d, klen=olens, causal=getattr(L, "causal", False), scale=scale, p=pa, seed=sd(1), cd=cd)
         x1 = empty(N, d, device=dev)
         ops.linear(O, b.w("self_attn.linear_out.weight"), x1,
                    epi=ops.make_epi(EPI_RESID, bias=b.f("self_attn.linear_out.bias"), resid=x0, drop_p=p,
@@ -135,7 +135,7 @@ class TransformerBlockFn(torch.autograd.Function):
         ops.linear_dx(dv, b.w("self_attn.linear_out.weight"), dO)
         dqkv = empty(N, 3 * d, dtype=cd, device=dev)
         _mha_bwd(st, dO, qkv, qkv[:, d:], qkv[:, 2 * d:], B=B, H=H, T1=T, T2=T, dk=dk, ldq=3 * d, ldk=3 * d,
-                 ldv=3 * d, klen=olens, causal=False, scale=scale, p=pa, seed=sd(1), cd=cd, dq=dqkv, lddq=3 * d,
+                 ldv=3 * d, klen=olens, causal=getattr(L, "causal", False), scale=scale, p=pa, seed=sd(1), cd=cd, dq=dqkv, lddq=3 * d,
                  dk_=dqkv[:, d:], lddk=3 * d, dv=dqkv[:, 2 * d:], lddv=3 * d)
         with ops.wgrad(dqkv, xn1):
             ops.colsum(dqkv, b.g(*_QKV_B, shape=(3 * d,)))

@@ -541,6 +541,9 @@ int ea_adam_step_dev(long n, float* params, const float* grads, float* exp_avg, 
                      void* stream);
 
 int ea_cast_f32_bf16(long n, const float* x, void* y, void* stream);
+/* x = max(x, 0) in place (f32, 16-B aligned): the ReLU of the legacy Encoder's "linear" input
+ * layer (transformer/encoder.py:120-127), used by TransformerLM (espnet2/lm/transformer_lm.py). */
+int ea_relu_f32_inplace(long n, float* x, void* stream);
 /* Transposed bf16 weight copies for the Linear input-gradient GEMMs (read K-major): problem
  * table probs[] of {int64 src_off; bf16* dst; int32 R, C} (24 B each, device memory), tile table
  * tiles[] of int32x4 {problem, tile row, tile col, 0} (64 x 64 tiles); dst[c*R + r] =

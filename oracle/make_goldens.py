@@ -1033,6 +1033,68 @@ def capture_beam_batch(name="beam_batch", cfg_name="tiny_hybrid"):
     print(f"{name}: {len(meta)} searches -> {path}")
 
 
+def capture_lm(name="lm_tiny", cfg_name="tiny_hybrid"):
+    """espnet2/lm/transformer_lm.py TransformerLM (pos_enc None as in the librispeech lm_conf,
+    2 layers, att_unit 128 / 2 heads so d_k = 64) over the tiny hybrid model's vocabulary:
+    forward logits, batch_score on prefixes, and BeamSearch with LM shallow fusion
+    (scorers decoder + ctc + lm + length_bonus, asr_inference.py:140-183)."""
+    from espnet.nets.beam_search import BeamSearch
+    from espnet.nets.scorers.ctc import CTCPrefixScorer
+    from espnet.nets.scorers.length_bonus import LengthBonus
+    from espnet2.lm.transformer_lm import TransformerLM
+    z = np.load(os.path.join(OUT, cfg_name + ".npz"))
+    cfg = json.loads(str(z["cfg"]))
+    model = build_reference_model(cfg)
+    model.load_state_dict({k[2:]: torch.from_numpy(z[k]) for k in z.files if k.startswith("w.")})
+    model.eval()
+    V = model.vocab_size
+    torch.manual_seed(3)
+    lm_conf = dict(vocab_size=V, pos_enc=None, embed_unit=32, att_unit=128, head=2, unit=256, layer=2,
+                   dropout_rate=0.0)
+    lm = TransformerLM(**lm_conf)
+    gen = torch.Generator().manual_seed(4)
+    with torch.no_grad():
+        for n, p_ in lm.named_parameters():  # non-trivial norms
+            if "norm" in n or "embed.1" in n:
+                p_.add_(torch.randn(p_.shape, generator=gen) * 0.1)
+    lm.eval()
+    out = {f"w.{k}": np32(v) for k, v in lm.state_dict().items()}
+    ids = torch.randint(2, V - 1, (3, 7), generator=gen)
+    ys = torch.cat([torch.full((4, 1), model.sos), torch.randint(2, V - 1, (4, 4), generator=gen)], dim=1)
+    with torch.no_grad():
+        logits, _ = lm(ids, None)
+        logp, _ = lm.batch_score(ys, [None] * 4, None)
+    out["in.ids"] = ids.numpy().astype(np.int64)
+    out["in.ys"] = ys.numpy().astype(np.int64)
+    out["out.logits"] = np32(logits)
+    out["out.bs_logp"] = np32(logp)
+    speech = torch.from_numpy(z["in.speech"])
+    lens = torch.from_numpy(z["in.speech_lengths"])
+    cases = [(3, 0.0, 0.0, 0.3, 0.3), (4, 0.5, 0.0, 0.5, 0.5)]
+    meta = []
+    with torch.no_grad():
+        for ci, (beam, lb, mlr, cw, lw) in enumerate(cases):
+            bs = BeamSearch(scorers={"decoder": model.decoder, "ctc": CTCPrefixScorer(model.ctc, model.eos),
+                                     "lm": lm, "length_bonus": LengthBonus(V)},
+                            weights={"decoder": 1.0 - cw, "ctc": cw, "lm": lw, "length_bonus": lb},
+                            beam_size=beam, vocab_size=V, sos=model.sos, eos=model.eos, token_list=None,
+                            pre_beam_score_key="full")
+            for u in range(speech.shape[0]):
+                le = int(lens[u])
+                enc, _ = model.encode(speech[u:u + 1, :le], lens[u:u + 1])
+                nbest = bs(x=enc[0], maxlenratio=mlr, minlenratio=0.0)
+                for r, h in enumerate(nbest):
+                    key = f"c{ci}.u{u}.h{r}"
+                    out[key + ".yseq"] = h.yseq.numpy().astype(np.int64)
+                    out[key + ".score"] = np.float64(float(h.score))
+                    out[key + ".lm"] = np.float64(float(h.scores["lm"]))
+                meta.append({"case": ci, "utt": u, "n": len(nbest)})
+    out["cfg"] = np.array(json.dumps({"lm_conf": lm_conf, "cases": cases, "nbest": meta, "model": cfg_name}))
+    path = os.path.join(OUT, f"{name}.npz")
+    np.savez_compressed(path, **out)
+    print(f"{name}: {len(meta)} searches -> {path}")
+
+
 if __name__ == "__main__":
     os.makedirs(OUT, exist_ok=True)
     which = sys.argv[1:] or ["models", "train", "ops", "ddp"]
@@ -1060,6 +1122,8 @@ if __name__ == "__main__":
         capture_ctc_th()
     if "beam_batch" in which:
         capture_beam_batch()
+    if "lm" in which:
+        capture_lm()
     if "train_specaug" in which:
         capture_train_specaug()
     if "epoch" in which:
