@@ -672,7 +672,9 @@ __global__ __launch_bounds__(256) void dwconv_fwd_k_kernel(int B, int T, int C, 
 }
 
 // dx[t] = sum_k w[k] dy[t-k+P];  part[blk][k*C+c] = sum_t dy[t] x[t+k-P];  part[blk][K*C+c] = sum_t dy[t]
-template <int K, int R>
+// CK: partials laid out as the parameters are — [c][k] (dw is (C, 1, K)) then [c] (dbias) — so
+// their sums are plain row reductions the host can defer into the pass's grouped reduce
+template <int K, int R, bool CK = false>
 __global__ __launch_bounds__(256) void dwconv_bwd_k_kernel(int B, int T, int C, const float* __restrict__ x,
                                                            const float* __restrict__ w, const float* __restrict__ dy,
                                                            float* __restrict__ dx, float* __restrict__ part) {
@@ -752,11 +754,15 @@ __global__ __launch_bounds__(256) void dwconv_bwd_k_kernel(int B, int T, int C, 
   __syncthreads();
   const long blk = (long)blockIdx.x;
   for (int i = threadIdx.x; i < (K + 1) * DW_CT; i += blockDim.x) {
-    const int k = i / DW_CT, ci = i % DW_CT, cg = c0 + ci;
+    // [k][c]: k = i / DW_CT (coalesced over c); CK: (c, k) with k fastest over the dw block
+    const int k = CK ? (i < K * DW_CT ? i % K : K) : i / DW_CT;
+    const int ci = CK ? (i < K * DW_CT ? i / K : i - K * DW_CT) : i % DW_CT;
+    const int cg = c0 + ci;
     if (cg >= C) continue;
     const float v = (sm[(0 * (K + 1) + k) * DW_CT + ci] + sm[(1 * (K + 1) + k) * DW_CT + ci]) +
                     (sm[(2 * (K + 1) + k) * DW_CT + ci] + sm[(3 * (K + 1) + k) * DW_CT + ci]);
-    part[blk * (long)C * (K + 1) + (long)k * C + cg] = v;  // [k][c] (coalesced); k == K: dbias
+    const long o = CK ? (k < K ? (long)cg * K + k : (long)C * K + cg) : (long)k * C + cg;
+    part[blk * (long)C * (K + 1) + o] = v;  // k == K: dbias
   }
 }
 
@@ -1150,6 +1156,24 @@ extern "C" int ea_dwconv_bwd(int B, int T, int C, int K, const float* x, const f
   int rc = ea_reduce_partials(nblk, C * K, workspace, (long)C * K, dw, accumulate_params, stream);
   if (rc) return rc;
   if (dbias) return ea_colsum(B * T, C, dy, EA_F32, C, dbias, accumulate_params, workspace, ws_elems, stream);
+  return 0;
+}
+
+extern "C" int ea_dwconv_bwd_partials(int B, int T, int C, int K, const float* x, const float* w, const float* dy,
+                                      float* dx, float* part, long part_elems, int* nparts, void* stream) {
+  EA_ENTRY();
+  EA_CHECK_ARG((K == 3 || K == 5 || K == 7 || K == 15 || K == 31) && part && nparts);
+  const int nblkr = B * ea_cdiv(T, 4 * DW_R);
+  EA_CHECK_ARG((long)nblkr * C * (K + 1) <= part_elems);
+  dim3 gridr(nblkr, ea_cdiv(C, DW_CT));
+  hipStream_t st = (hipStream_t)stream;
+  switch (K) {
+#define EA_DWB(KK) case KK: hipLaunchKernelGGL((dwconv_bwd_k_kernel<KK, DW_R, true>), gridr, dim3(256), 0, st, B, T, C, x, w, dy, dx, part); break;
+    EA_DWB(3) EA_DWB(5) EA_DWB(7) EA_DWB(15) EA_DWB(31)
+#undef EA_DWB
+  }
+  EA_LAUNCH_CHECK();
+  *nparts = nblkr;
   return 0;
 }
 

@@ -12,6 +12,9 @@ column blocks so attention reads q/k/v with strides, no transposes.
 """
 from __future__ import annotations
 
+import ctypes
+import os
+
 import torch
 from torch import nn
 
@@ -21,6 +24,10 @@ from .common import (ACT_SWISH, EPI_ACT, EPI_DACT, EPI_RESID, EPI_STORE, F32, Bo
 
 
 # ----------------------------------------------------------------------------- holders
+
+# depthwise-conv dw / dbias partials deferred into the grouped reduce (EA_DWCONV_DEFER=1; per call by default until measured)
+DWCONV_DEFER = os.environ.get("EA_DWCONV_DEFER", "0") == "1"
+
 class PositionwiseFeedForward(nn.Module):
     """positionwise_feed_forward.py:12-32 (w_2(dropout(act(w_1 x))))."""
 
@@ -286,10 +293,21 @@ class ConformerBlockFn(torch.autograd.Function):
         ops.batchnorm_bwd(dz, y, bn_mean, bn_rstd, b.f(C + "norm.weight"), b.f(C + "norm.bias"),
                           ACT_SWISH, dy, b.g(C + "norm.weight"), b.g(C + "norm.bias"))
         dglu = empty(N, d, device=dev)
-        w, wn = ops._ws(dev, B * ((T + 31) // 32) * d * (K + 1) + 1024)
-        lib.ea_dwconv_bwd(B, T, d, K, glu.data_ptr(), b.f(C + "depthwise_conv.weight").data_ptr(),
-                          dy.data_ptr(), dglu.data_ptr(), b.g(C + "depthwise_conv.weight").data_ptr(),
-                          b.g(C + "depthwise_conv.bias").data_ptr(), 1, w, wn, ops.stream())
+        if DWCONV_DEFER and ops.REDUCE_Q.active and K in (3, 5, 7, 15, 31):
+            # dw / dbias partials summed with the pass's other parameter-gradient reductions
+            part = empty(B * ((T + 31) // 32) * d * (K + 1), device=dev)
+            npart = ctypes.c_int(0)
+            lib.ea_dwconv_bwd_partials(B, T, d, K, glu.data_ptr(), b.f(C + "depthwise_conv.weight").data_ptr(),
+                                       dy.data_ptr(), dglu.data_ptr(), part.data_ptr(), part.numel(),
+                                       ctypes.addressof(npart), ops.stream())
+            rl = d * (K + 1)
+            ops.REDUCE_Q.add_reduce(part, npart.value, d * K, rl, b.g(C + "depthwise_conv.weight").view(-1))
+            ops.REDUCE_Q.add_reduce(part[d * K:], npart.value, d, rl, b.g(C + "depthwise_conv.bias"))
+        else:
+            w, wn = ops._ws(dev, B * ((T + 31) // 32) * d * (K + 1) + 1024)
+            lib.ea_dwconv_bwd(B, T, d, K, glu.data_ptr(), b.f(C + "depthwise_conv.weight").data_ptr(),
+                              dy.data_ptr(), dglu.data_ptr(), b.g(C + "depthwise_conv.weight").data_ptr(),
+                              b.g(C + "depthwise_conv.bias").data_ptr(), 1, w, wn, ops.stream())
         dg2 = empty(N, 2 * d, dtype=cd, device=dev)
         lib.ea_glu_bwd(N, d, g2.data_ptr(), ops.dt(g2), dglu.data_ptr(), dg2.data_ptr(), ops.stream())
         with ops.wgrad(dg2, xn3):

@@ -376,6 +376,11 @@ int ea_dwconv_fwd(int B, int T, int C, int K, const float* x, const float* w, co
 int ea_dwconv_bwd(int B, int T, int C, int K, const float* x, const float* w, const float* dy,
                   float* dx, float* dw, float* dbias, int accumulate_params, float* workspace,
                   long ws_elems, void* stream);
+/* ea_dwconv_bwd without the parameter reductions (K in {3,5,7,15,31}): dx, and per-block
+ * partials part[p][0 : C*K] of dw in its (C, 1, K) layout and part[p][C*K : C*(K+1)] of dbias,
+ * p < *nparts (row stride C*(K+1)) — plain row sums the caller may defer and group. */
+int ea_dwconv_bwd_partials(int B, int T, int C, int K, const float* x, const float* w, const float* dy,
+                           float* dx, float* part, long part_elems, int* nparts, void* stream);
 
 /* q + pos_bias_u / q + pos_bias_v (attention.py:287-290) for the fused qkv rows. */
 int ea_add_pos_bias(long N, int H, int dk, const void* q, long ldq, const float* u, const float* v,
