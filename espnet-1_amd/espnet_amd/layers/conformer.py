@@ -25,7 +25,7 @@ from .common import (ACT_SWISH, EPI_ACT, EPI_DACT, EPI_RESID, EPI_STORE, F32, Bo
 
 # ----------------------------------------------------------------------------- holders
 
-# depthwise-conv dw / dbias partials deferred into the grouped reduce (EA_DWCONV_DEFER=1; per call by default until measured)
+# depthwise-conv dw / dbias partials deferred into the grouped reduce (EA_DWCONV_DEFER=1; measured neutral, off)
 DWCONV_DEFER = os.environ.get("EA_DWCONV_DEFER", "0") == "1"
 
 class PositionwiseFeedForward(nn.Module):
