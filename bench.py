@@ -202,6 +202,10 @@ def main():
                     help="with N > 1, launch every kernel and collective eagerly instead")
     ap.add_argument("--eager", action="store_true", help="launch every kernel from Python each step "
                     "(default: the step is captured once as a hipGraph and replayed)")
+    ap.add_argument("--no-dp-rehearsal", action="store_true",
+                    help="at N=1, skip the second timing of the step as one rank of a DP job (a "
+                         "world-1 RCCL group with every collective of an N-GPU step)")
+    ap.add_argument("--dp-rehearsal-steps", type=int, default=20)
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -249,6 +253,30 @@ def main():
     def step():
         return runner(batch, maxlens)
 
+    def timed(step_fn, steps):
+        """Barrier + synchronize on both sides of exactly `steps` steps; per-step HIP events
+        on the step's stream.  -> (wall seconds, max over ranks; sorted per-step ms; the last
+        step's outputs)."""
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        evs = [torch.cuda.Event(enable_timing=True) for _ in range(steps + 1)]
+        t0 = time.perf_counter()
+        evs[0].record()
+        last = None
+        for i in range(steps):
+            last = step_fn()
+            evs[i + 1].record()
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        el = time.perf_counter() - t0
+        if world > 1:
+            t = torch.tensor([el], device=dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            el = float(t.item())
+        return el, sorted(evs[i].elapsed_time(evs[i + 1]) for i in range(steps)), last
+
     # in-kernel span probe of the dominant GEMM; captured into the graph, so it measures
     # every replay; reset after warmup so only the timed region counts
     probe = hip_ops.KernelProbe(["conv2_gemm"], dev)
@@ -257,27 +285,10 @@ def main():
         step()
     torch.cuda.synchronize()
     probe.reset()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
     # per-step HIP events on the step's stream (median step time)
-    evs = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps + 1)]
-    t0 = time.perf_counter()
-    evs[0].record()
-    for i in range(args.steps):
-        loss, stats, weight, gn = step()
-        evs[i + 1].record()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    t1 = time.perf_counter()
+    elapsed, step_ms, (loss, stats, weight, gn) = timed(step, args.steps)
     hip_ops.PROBE = None
-    step_ms = sorted(evs[i].elapsed_time(evs[i + 1]) for i in range(args.steps))
-    elapsed = t1 - t0
-    if world > 1:
-        t = torch.tensor([elapsed], device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    step_mode = runner.mode or "eager"
     ms = elapsed / args.steps * 1e3
     utt = cfg["B"] * world * args.steps / elapsed
     conv_ms, n_conv = probe.mean_ms("conv2_gemm")
@@ -302,6 +313,9 @@ def main():
     achieved = conv_flop / (conv_ms * 1e-3) / 1e12
     loss_v = float(loss.item())
     traffic, traffic_src, traffic_same = pmc_traffic() if (args.config == "c3" and amp) else (None, None, False)
+    rehearsal = None
+    if world == 1 and not args.no_dp_rehearsal and args.dp_rehearsal_steps > 0:
+        rehearsal = dp_rehearsal(model, opt, sched, batch, maxlens, cfg, eager, args, timed)
     if rank == 0:
         out = {
             "metric": METRIC, "value": round(utt, 3), "unit": "utterances/s", "n_gpus": world,
@@ -328,17 +342,61 @@ def main():
                                    "events around eager launches on the launch stream",
                          "launch_ms_events": round(conv_ev_ms, 4), "launches_events": n_ev,
                          "frac_events": round(conv_flop / (conv_ev_ms * 1e-3) / 1e12 / PEAK[dtype], 4)},
+            "step_mode": step_mode,
             "step_ms_median": round(med_ms, 3),
             "step_ms_p10_p90": [round(step_ms[len(step_ms) // 10], 3), round(step_ms[(9 * len(step_ms)) // 10], 3)],
             "value_median": round(cfg["B"] * world / (med_ms * 1e-3), 3),
             "loss": round(loss_v, 4),
         }
+        if rehearsal is not None:
+            out["dp_rehearsal"] = rehearsal
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(cfg)
             out["speedup_vs_cpu"] = round(utt / out["cpu_baseline"]["value"], 1)
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def dp_rehearsal(model, opt, sched, batch, maxlens, cfg, eager, args, timed):
+    """The per-rank step of an N-GPU job, timed on this one GPU: a world-1 RCCL group and
+    ArenaDataParallel(force_collectives=True), so the step issues every collective of an
+    N-GPU step (BatchNorm-buffer broadcasts, the packed stats all-reduce, the 64 MiB gradient
+    bucket all-reduces from the grad-ready hooks) and flushes the deferred weight-gradient
+    GEMMs per bucket as DP does — captured with its collectives like the N > 1 bench.  The
+    all-reduces of a world-1 group move no data over xGMI, so this prices the step structure
+    (per-bucket flushes, collective launches), not the link time."""
+    from espnet_amd.train.distributed import ArenaDataParallel
+    from espnet_amd.train.graph import CapturedTrainStep
+    own = False
+    try:
+        if not dist.is_initialized():
+            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            if "MASTER_PORT" not in os.environ:
+                import socket
+                with socket.socket() as sk:
+                    sk.bind(("127.0.0.1", 0))
+                    os.environ["MASTER_PORT"] = str(sk.getsockname()[1])
+            dist.init_process_group("nccl", rank=0, world_size=1, device_id=batch["speech"].device)
+            own = True
+        dp = ArenaDataParallel(model, force_collectives=True)
+        runner = CapturedTrainStep(model, opt, sched, grad_clip=5.0, dp=dp, warmup=2, enabled=not eager)
+        for _ in range(max(3, args.warmup // 2)):
+            runner(batch, maxlens)
+        torch.cuda.synchronize()
+        el, ms, _ = timed(lambda: runner(batch, maxlens), args.dp_rehearsal_steps)
+        runner.graphs.clear()
+        return {"what": "this step as one rank of a DP job: world-1 RCCL group, every collective of an "
+                        "N-GPU step issued (no xGMI traffic), weight-gradient GEMMs flushed per 64 MiB bucket",
+                "step_mode": runner.mode or "eager", "steps": args.dp_rehearsal_steps,
+                "ms_per_step": round(el / args.dp_rehearsal_steps * 1e3, 3),
+                "step_ms_median": round(ms[len(ms) // 2], 3),
+                "value": round(cfg["B"] * args.dp_rehearsal_steps / el, 3), "buckets": len(dp.buckets)}
+    except Exception as e:  # reported, never fatal for the N=1 line
+        return {"error": f"{type(e).__name__}: {e}"}
+    finally:
+        if own:
+            dist.destroy_process_group()
 
 
 def run_c5(args, world, rank, dev):

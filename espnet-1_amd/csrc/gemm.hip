@@ -129,11 +129,16 @@ __global__ void probe_end_kernel(unsigned long long* s) {
 // stamp runs after everything issued before it on the stream, so the differences are the
 // device durations of the phases, and a captured step re-measures itself on every replay.
 namespace {
-__global__ void phase_stamp_kernel(unsigned long long* st, float* ring, int cap, int phase, const float* extra) {
+__global__ void phase_stamp_kernel(unsigned long long* st, float* ring, int cap, int phase, const float* extra,
+                                   const int* skip) {
   const unsigned long long now = __builtin_amdgcn_s_memrealtime();
   if (phase > 0) {
     const long slot = (long)(st[1] % (unsigned long long)cap);
-    ring[slot * 4 + phase - 1] = (float)((double)(now - st[0]) * 1e-8);  // 100 MHz clock
+    float dt = (float)((double)(now - st[0]) * 1e-8);  // 100 MHz clock
+    // a skipped update (non-finite grad norm) registers no optim_step_time in the reference
+    // (trainer.py:662-682); NaN is what its reporter's nanmean then ignores
+    if (phase == 3 && skip && skip[0]) dt = __builtin_nanf("");
+    ring[slot * 4 + phase - 1] = dt;
     if (phase == 3) {
       ring[slot * 4 + 3] = extra ? extra[0] : 0.f;
       st[1] = st[1] + 1ull;
@@ -147,7 +152,18 @@ extern "C" int ea_phase_stamp(unsigned long long* state, float* ring, int cap, i
                               void* stream) {
   EA_ENTRY();
   EA_CHECK_ARG(state != nullptr && ring != nullptr && cap > 0 && phase >= 0 && phase <= 3);
-  hipLaunchKernelGGL(phase_stamp_kernel, dim3(1), dim3(1), 0, (hipStream_t)stream, state, ring, cap, phase, extra);
+  hipLaunchKernelGGL(phase_stamp_kernel, dim3(1), dim3(1), 0, (hipStream_t)stream, state, ring, cap, phase, extra,
+                     (const int*)nullptr);
+  EA_LAUNCH_CHECK();
+  return 0;
+}
+
+extern "C" int ea_phase_stamp_opt(unsigned long long* state, float* ring, int cap, int phase,
+                                  const ea_opt_state* opt, void* stream) {
+  EA_ENTRY();
+  EA_CHECK_ARG(state != nullptr && ring != nullptr && cap > 0 && phase >= 0 && phase <= 3 && opt != nullptr);
+  hipLaunchKernelGGL(phase_stamp_kernel, dim3(1), dim3(1), 0, (hipStream_t)stream, state, ring, cap, phase,
+                     &opt->next_lr, &opt->skip);
   EA_LAUNCH_CHECK();
   return 0;
 }

@@ -100,7 +100,9 @@ class CTCPrefixScorer:
         if len(state) == 5:  # a CTCPrefixScoreTH state (batch_score_partial), ctc.py:40-63
             r_new, log_psi, f_min, f_max, cand = state
             row = cand[i].tolist()
-            pos = row.index(int(new_id)) if int(new_id) in row else 0
+            # an id outside the scored set: scoring_idmap holds -1 there, so the reference
+            # indexes the LAST scored column (scorers/ctc.py:59-60)
+            pos = row.index(int(new_id)) if int(new_id) in row else -1
             return r_new[0][i, pos], log_psi[i, int(new_id)].expand(log_psi.size(1)), f_min, f_max
         sc, st = state
         return sc[i], st[i]

@@ -378,9 +378,26 @@ class TransformerDecoder(AbsDecoder):
             return logp, xf, new
         return logp, new
 
+    @staticmethod
+    def _as_cache(src):
+        """A hypothesis state's cache as a DecoderKVCache: a GraphStepKV (a captured run's
+        state, e.g. when a prefix outgrows graph_lcap or the memory changes) is viewed as its
+        run's static buffer cropped to its L positions; a stale one (its buffer was reused by
+        a later step) gives None, so the step re-builds the cache from the prefix."""
+        if isinstance(src, GraphStepKV):
+            run = src.run
+            if src.step != run.nstep:
+                return None
+            kv = run.per_n[src.n]["kv"][src.buf][:, :, :src.L]
+            return DecoderKVCache(kv, src.L, run.mem)
+        return src
+
     def score(self, ys, state, x):
         """transformer_decoder.py:186-192 (one hypothesis); state = (DecoderKVCache, row)."""
-        cache = state[0].select([state[1]]) if isinstance(state, tuple) else None
+        cache = None
+        if isinstance(state, tuple):
+            src = self._as_cache(state[0])
+            cache = src.select([state[1]]) if src is not None else None
         logp, cache = self.forward_one_step(ys.unsqueeze(0), None, x.unsqueeze(0), cache=cache)
         return logp.squeeze(0), (cache, 0)
 
@@ -428,8 +445,9 @@ class TransformerDecoder(AbsDecoder):
         if states and all(isinstance(s, tuple) for s in states):
             src = states[0][0]
             if all(s[0] is src for s in states) and src.L == ys.shape[1] - 1:
-                cache = src.select([s[1] for s in states])
-                if cache.mem.memory.shape[1:] != xs.shape[1:]:
+                src = self._as_cache(src)
+                cache = src.select([s[1] for s in states]) if src is not None else None
+                if cache is not None and cache.mem.memory.shape[1:] != xs.shape[1:]:
                     cache = None
         logp, new = self.forward_one_step(ys, None, xs, cache=cache)
         return logp, [(new, i) for i in range(n)]

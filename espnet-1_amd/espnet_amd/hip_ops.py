@@ -296,13 +296,45 @@ def make_epi(kind=EPI_STORE, *, alpha=1.0, beta=0.0, bias=None, post_scale=1.0, 
     return e
 
 
+MN_TAIL_COPIES = 0  # operands re-homed by _mn_tail_guard (tests read it)
+
+
+def _mn_tail_guard(X, MN, K, ld, s, batch, nh):
+    """ea_gemm's contract for an MN-major bf16 operand whose width MN is not a multiple of 8
+    (include/espnet_amd.h): the LDS-DMA loads move whole 16-B chunks, so the last chunk of a
+    row reads up to 7 elements past MN — every row, the last one included, must be readable to
+    MN rounded up to 8.  A view ending closer than that to the end of its storage (a
+    column-offset slice at the end of an allocation) is copied, with its strides, into a
+    buffer padded by 8 elements; the GEMM then reads the copy."""
+    global MN_TAIL_COPIES
+    if X.dtype != torch.bfloat16 or MN % 8 == 0 or K <= 0:
+        return X
+    esz = X.element_size()
+    total = X.untyped_storage().nbytes() // esz
+    off = X.storage_offset()
+    last = off + (batch - 1) * s[0] + (nh - 1) * s[1] + (K - 1) * ld  # start of the last row read
+    if last + (MN + 7) // 8 * 8 <= total:
+        return X
+    span = last + MN - off
+    buf = torch.empty(span + 8, dtype=X.dtype, device=X.device)
+    buf[:span].copy_(torch.as_strided(X, (span,), (1,), off))  # same strides from the new base
+    buf[span:].zero_()
+    MN_TAIL_COPIES += 1
+    return buf
+
+
 def gemm(A, B, C, *, M, N, K, a_kmajor, b_kmajor, lda, ldb, ldc,
          batch=1, nh=1, sA=(0, 0), sB=(0, 0), sC=(0, 0), epi: Epilogue = None, splitk=True):
-    """Raw batched GEMM (see include/espnet_amd.h: ea_gemm)."""
+    """Raw batched GEMM (see include/espnet_amd.h: ea_gemm).  An MN-major bf16 operand whose
+    last row cannot be read to its width rounded up to 8 is re-homed first (_mn_tail_guard)."""
     if A.dtype != B.dtype:
         raise HipError(f"gemm operand dtypes differ: {A.dtype} vs {B.dtype}")
     if epi is None:
         epi = make_epi()
+    if not a_kmajor:
+        A = _mn_tail_guard(A, M, K, lda, sA, batch, nh)
+    if not b_kmajor:
+        B = _mn_tail_guard(B, N, K, ldb, sB, batch, nh)
     ws = workspace(_SPLITK_WS, A.device) if splitk else None
     lib.ea_gemm(dt(A), int(a_kmajor), int(b_kmajor), M, N, K,
                 A.data_ptr(), lda, sA[0], sA[1],
@@ -356,6 +388,11 @@ class TransposedShadow:
         self.items = {}  # (element offset, R, C) -> (C, R) bf16 tensor
         self.tiles = self.probs = None
         self.ntiles = 0
+        # set once a hipGraph captured refresh(): that graph holds this tile / problem table
+        # and its count, so no weight may be registered afterwards (its W^T would never be
+        # refreshed by the graph, and a rebuilt table would free the captured one) — such a
+        # weight keeps the MN-major path instead
+        self.frozen = False
 
     def _rebuild(self):
         probs, tiles = [], []
@@ -374,7 +411,7 @@ class TransposedShadow:
         key = (off, int(w.shape[0]), int(w.shape[1]))
         wt = self.items.get(key)
         if wt is None:
-            if torch.cuda.is_current_stream_capturing():
+            if self.frozen or torch.cuda.is_current_stream_capturing():
                 return None  # registration happens in the eager warm-up steps
             wt = torch.empty(key[2], key[1], dtype=w.dtype, device=w.device)
             self.items[key] = wt
@@ -383,6 +420,8 @@ class TransposedShadow:
         return wt
 
     def refresh(self):
+        if torch.cuda.is_current_stream_capturing():
+            self.frozen = True
         if self.ntiles:
             lib.ea_transpose_bf16_grouped(self.ntiles, self.tiles.data_ptr(), self.probs.data_ptr(),
                                           self.shadow.data_ptr(), stream())

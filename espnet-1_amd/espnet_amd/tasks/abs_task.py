@@ -450,7 +450,8 @@ class AbsTask:
         dopt.init_torch_distributed()
         _set_all_random_seed(args.seed)
         model = cls.build_model(args=args)
-        device = torch.device("cuda", dopt.local_rank if dopt.local_rank is not None else torch.cuda.current_device())
+        device = torch.device("cuda", dopt.device_index() if dopt.local_rank is not None
+                              else torch.cuda.current_device())
         torch.cuda.set_device(device)
         for p in args.init_param:
             _load_pretrained(model, p, args.ignore_init_mismatch)

@@ -87,9 +87,11 @@ def _sum_into(running: Dict[str, torch.Tensor], other: Dict[str, torch.Tensor]):
 
 
 def _divide_floats(running: Dict[str, torch.Tensor], n: int):
-    """Float entries become means; integer ones (BatchNorm num_batches_tracked) stay sums."""
+    """Entries become means except the torch.int* ones (BatchNorm num_batches_tracked), which
+    stay sums — the reference's dtype-name test (average_nbest_models.py:90-98), so bool /
+    uint8 entries are averaged too."""
     for key, v in running.items():
-        if v.dtype.is_floating_point or v.dtype.is_complex:
+        if not str(v.dtype).startswith("torch.int"):
             running[key] = v / n
 
 

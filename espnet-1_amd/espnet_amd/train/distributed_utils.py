@@ -68,15 +68,25 @@ class DistributedOption:
             self.dist_master_addr, self.dist_master_port = addr, port
             self.dist_init_method = f"tcp://{addr}:{port}"
 
+    def device_index(self) -> Optional[int]:
+        """This worker's GPU.  RCCL needs one GPU per rank (local_rank); with a host transport
+        (gloo) ranks beyond the node's GPU count share them round-robin, which is how the
+        multi-worker entry point is rehearsed on a one-GPU box (bench.py does the same)."""
+        if self.local_rank is None:
+            return None
+        if self.dist_backend != "nccl":
+            return self.local_rank % max(1, torch.cuda.device_count())
+        return self.local_rank
+
     def init_torch_distributed(self):
         if not self.distributed:
             return
         os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
         kwargs = {}
         if self.ngpu > 0 and self.local_rank is not None:
-            torch.cuda.set_device(self.local_rank)
+            torch.cuda.set_device(self.device_index())
             if self.dist_backend == "nccl":
-                kwargs["device_id"] = torch.device("cuda", self.local_rank)
+                kwargs["device_id"] = torch.device("cuda", self.device_index())
         dist.init_process_group(backend=self.dist_backend, init_method=self.dist_init_method,
                                 world_size=self.dist_world_size, rank=self.dist_rank, **kwargs)
         self.control_group = dist.new_group(backend="gloo") if self.dist_backend != "gloo" else None

@@ -33,13 +33,21 @@ from ..layers.common import multisequential_draw as layerdrop_draw
 from .trainer import Trainer
 
 
+def _backend(group) -> str:
+    import torch.distributed as dist
+    try:
+        return str(dist.get_backend(group))
+    except (RuntimeError, ValueError):
+        return ""
+
+
 class _Captured:
     __slots__ = ("graph", "inputs", "outputs", "maxlens")
 
 
 class CapturedTrainStep:
     def __init__(self, model, optimizer, scheduler=None, *, grad_clip: float = 5.0, dp=None,
-                 warmup: int = 2, enabled: bool = True):
+                 warmup: int = 2, enabled: bool = True, control_group=None):
         self.model = model
         self.optimizer = optimizer
         self.scheduler = scheduler
@@ -51,6 +59,12 @@ class CapturedTrainStep:
         self._seen: Dict[tuple, int] = {}
         self._pool = None
         self._side = None
+        self.control_group = control_group  # gloo group for the capture decision (optional)
+        if dp is not None and dp.active and _backend(dp.group) == "gloo":
+            self.enabled = False  # gloo collectives (host copies) cannot be captured
+        # "graph" once steps replay, "eager" once capture was given up (on any rank); None
+        # while the warm-up steps run
+        self.mode = None if self.enabled else "eager"
 
     # ------------------------------------------------------------------ helpers
     def _eager(self, batch, maxlens):
@@ -125,20 +139,57 @@ class CapturedTrainStep:
                     out = self._eager(dbatch, maxlens)
                 main.wait_stream(self._side)
                 return out
+            err = None
             try:
-                return self._capture(key, dbatch, maxlens)
+                cap = self._capture(key, dbatch, maxlens)
             except RuntimeError as e:
-                # a stack that cannot capture this step (e.g. a collective library without
-                # graph support on some node): warn once and run every step eagerly.  Capture
-                # executes nothing, so the step is simply run now.
-                import warnings
-                warnings.warn(f"hipGraph capture of the training step failed ({e}); running eager steps")
-                torch.cuda.synchronize()
-                self.enabled = False
-                self.graphs.pop(key, None)
-                return self._eager(dbatch, maxlens)
+                cap, err = None, e
+                self._reset_after_failed_capture()
+            # the decision is collective: every rank replays its graph or every rank runs
+            # eager steps (a graph replay beside an eager step would issue the same
+            # collectives, but at a different pace, and the bench would time a mixed mode)
+            if self._agree(cap is not None):
+                self.graphs[key] = cap
+                self.mode = "graph"
+                cap.graph.replay()  # capture executes nothing: run this batch's step now
+                return cap.outputs
+            # a stack that cannot capture this step (e.g. a collective library without graph
+            # support on some node) on this rank or another: warn once and run every step
+            # eagerly.  Capture executes nothing, so the step is simply run now.
+            import warnings
+            why = f"failed here ({err})" if err is not None else "failed on another rank"
+            warnings.warn(f"hipGraph capture of the training step {why}; running eager steps")
+            torch.cuda.synchronize()
+            self.enabled = False
+            self.mode = "eager"
+            self.graphs.clear()
+            return self._eager(dbatch, maxlens)
         finally:
             common.SKIP_LAYERDROP_DRAWS = False
+
+    def _reset_after_failed_capture(self):
+        """A capture that raised mid-step leaves per-pass host state behind (the deferred
+        queues are dropped by their context; the DP grad-ready hook and bucket bookkeeping
+        are not): clear it so the eager step starts clean."""
+        from .. import hip_ops
+        hip_ops.GRAD_READY = None
+        if self.dp is not None:
+            self.dp._pending = None
+            self.dp._works = []
+
+    def _agree(self, ok: bool) -> bool:
+        """True when the capture succeeded on every rank: one MIN-style all-reduce of a failure
+        count over the control group (gloo, host memory) when there is one, else over the
+        data-parallel group.  Without an active DP group this rank decides alone."""
+        dp = self.dp
+        if dp is None or not dp.active:
+            return ok
+        import torch.distributed as dist
+        group = self.control_group
+        dev = "cpu" if group is not None else self.model._device
+        flag = torch.tensor([0 if ok else 1], dtype=torch.int32, device=dev)
+        dist.all_reduce(flag, group=group if group is not None else dp.group)
+        return int(flag.item()) == 0
 
     def _capture(self, key, dbatch, maxlens):
         cap = _Captured()
@@ -152,6 +203,4 @@ class CapturedTrainStep:
             self._pool = g.pool()
         cap.graph = g
         cap.outputs = out
-        self.graphs[key] = cap
-        g.replay()  # capture executes nothing: run this batch's step now
-        return out
+        return cap

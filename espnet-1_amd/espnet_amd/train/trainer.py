@@ -36,7 +36,7 @@ import torch
 import torch.distributed as dist
 
 from .. import hip_ops as ops
-from .._lib import OPT_STATE_NEXT_LR, lib
+from .._lib import lib
 from ..optim.adam import ArenaAdam
 
 
@@ -80,9 +80,14 @@ class PhaseTimer:
         self.state = torch.zeros(2, dtype=torch.int64, device=device)
         self.ring = torch.zeros(cap, 4, dtype=torch.float32, device=device)
         self.extra = None  # device float read at phase 3 (the applied lr)
+        self.opt = None    # ea_opt_state (device): phase 3 reads next_lr and the skip flag
         self.count = 0     # host mirror of the device step counter
 
     def stamp(self, phase: int):
+        if self.opt is not None:
+            lib.ea_phase_stamp_opt(self.state.data_ptr(), self.ring.data_ptr(), self.cap, phase,
+                                   self.opt.data_ptr(), ops.stream())
+            return
         lib.ea_phase_stamp(self.state.data_ptr(), self.ring.data_ptr(), self.cap, phase,
                            None if self.extra is None else self.extra.data_ptr(), ops.stream())
 
@@ -180,11 +185,15 @@ class Trainer:
         timer = getattr(model, "_phase_timer", None)
         if timer is None:
             timer = model._phase_timer = PhaseTimer(device)
-        # ea_opt_state.next_lr: the lr after scheduler.step(), which the reference registers
-        timer.extra = optimizer.state_dev.view(torch.float32)[OPT_STATE_NEXT_LR:OPT_STATE_NEXT_LR + 1]
+        # ea_opt_state: next_lr (the lr after scheduler.step(), which the reference registers)
+        # and the skip flag (a skipped update's optimizer time is NaN: not registered)
+        timer.opt = optimizer.state_dev
+        # applied updates are counted on the device (a non-finite grad norm skips the update
+        # there); read once at the end of the epoch for all_steps_are_invalid (trainer.py:681)
+        applied0 = optimizer.state_dev[0].clone()
         stop = torch.zeros((), dtype=torch.long)  # host flag over the gloo control group
         ctrl = getattr(distributed_option, "control_group", None)
-        all_invalid = True
+        ran_no_forward = False
         unread = 0
         start = time.perf_counter()
         TIMER = timer
@@ -196,7 +205,7 @@ class Trainer:
                     if stop.item() > 0:
                         break
                 if options.no_forward_run:
-                    all_invalid = False
+                    ran_no_forward = True
                     continue
                 # the padded maxima from the host copy of the lengths (no device read)
                 maxlens = (int(batch["speech_lengths"].max()), int(batch["text_lengths"].max())) \
@@ -219,9 +228,9 @@ class Trainer:
                 reporter.register({k: snap[i] for i, k in enumerate(keys)}, snap[-1])
                 reporter.register({"forward_time": timer.ring[slot, 0], "backward_time": timer.ring[slot, 1]})
                 if update:
-                    # a non-finite gradient skips the update on the device (ArenaAdam), not on
-                    # the host: the step still counts as valid here
-                    all_invalid = False
+                    # a non-finite gradient skips the update on the device (ArenaAdam); its
+                    # optim_step_time is NaN there, which the epoch average ignores like the
+                    # reference's missing entry
                     reporter.register({"optim_step_time": timer.ring[slot, 2], "optim0_lr0": timer.ring[slot, 3],
                                        "train_time": time.perf_counter() - start})
                     start = time.perf_counter()
@@ -240,7 +249,8 @@ class Trainer:
                     dist.all_reduce(stop, group=ctrl)
         finally:
             TIMER = None
-        return all_invalid
+        applied = int((optimizer.state_dev[0] - applied0).item())
+        return not (ran_no_forward or applied > 0)
 
     @staticmethod
     @torch.no_grad()
@@ -321,7 +331,8 @@ class Trainer:
         runner = None
         if opts.accum_grad == 1:
             runner = CapturedTrainStep(model, optimizers[0], schedulers[0] if schedulers else None,
-                                       grad_clip=opts.grad_clip, dp=dp, warmup=2)
+                                       grad_clip=opts.grad_clip, dp=dp, warmup=2,
+                                       control_group=getattr(distributed_option, "control_group", None))
         all_invalid = False
         for iepoch in range(start_epoch, opts.max_epoch + 1):
             logging.info(f"{iepoch}/{opts.max_epoch}epoch started")

@@ -54,6 +54,11 @@ typedef struct ea_epilogue {
  *  b_kmajor=1: B[k,n] at B[n*ldb + k]   (torch Linear weight N x K) else B[k*ldb + n]
  *  z in [0, batch*nh): zb = z / nh, zh = z % nh; operand offset = zb*s?b + zh*s?h.
  *  16-B aligned bases / leading dims take 16-B vector loads; others an element-wise path.
+ *  Contract of the 16-B (LDS-DMA) path for an MN-major bf16 operand whose extent MN (M for
+ *  A, N for B) is not a multiple of 8: every row, the last one included, is read in whole
+ *  16-B chunks up to MN rounded up to 8, so the caller keeps that many elements readable
+ *  past the row start (hip_ops.gemm re-homes a view that ends closer to its allocation's
+ *  end; the values read past MN never reach C).
  *  workspace (f32, ws_elems) enables split-K for EA_EPI_STORE; NULL disables it.
  * Replaces: torch.nn.Linear / torch.matmul in transformer/attention.py:54-93,262-305,
  * positionwise_feed_forward.py:30-32, conformer/convolution.py:71-77 (1x1 convs),
@@ -170,6 +175,12 @@ int ea_gemm_set_diag(unsigned long long* buf);
  * phase 3 also copies *extra (e.g. the optimizer's device lr; NULL: 0) into ring[slot*4+3]
  * and advances the counter.  state = {last stamp, step counter} (2 x u64, zeroed). */
 int ea_phase_stamp(unsigned long long* state, float* ring, int cap, int phase, const float* extra, void* stream);
+/* ea_phase_stamp with the optimizer's device state: phase 3 records opt->next_lr as the extra
+ * value and NaN as the optimizer duration when opt->skip (the update was skipped: the
+ * reference registers no optim_step_time then, trainer.py:662-682). */
+struct ea_opt_state;
+int ea_phase_stamp_opt(unsigned long long* state, float* ring, int cap, int phase, const struct ea_opt_state* opt,
+                       void* stream);
 int ea_probe_begin(unsigned long long* slots, void* stream);
 int ea_probe_end(unsigned long long* slots, void* stream);
 

@@ -229,6 +229,70 @@ def test_gemm_bf16_tiles_epilogue_splitk(forced_tile):
     torch.testing.assert_close(dw.double().cpu(), refw, atol=2e-3 * R ** 0.5, rtol=2e-3)
 
 
+@pytest.mark.parametrize("forced_tile", TILES, indirect=True, ids=lambda t: f"{t[0]}x{t[1]}{'p' * t[2]}")
+@pytest.mark.parametrize("mn_major", ["A", "B", "AB"])
+def test_gemm_mn_major_slice_at_allocation_end(forced_tile, mn_major):
+    """The bf16 decoder fault of round 3 (commit 9880edd): an MN-major operand that is a
+    column-offset slice whose last row ends exactly at the end of its allocation, with
+    MN % 8 != 0.  The LDS-DMA loads read whole 16-B chunks up to MN rounded to 8 (the ea_gemm
+    contract in include/espnet_amd.h), so hip_ops.gemm re-homes such a view into a padded
+    copy first; the product equals fp64 and values past MN never reach C (the storage after
+    the slice's columns in earlier rows holds NaN)."""
+    ops, L = _ops()
+    bm, bn = forced_tile
+    a_k = 0 if "A" in mn_major else 1
+    b_k = 0 if "B" in mn_major else 1
+    if bm <= 64 and not a_k:
+        pytest.skip("narrow tiles take K-major A only")
+    M, N, K = 173, 203, 136
+    W = 512  # row stride; the slice starts at column 256 (16-B aligned)
+    g = torch.Generator().manual_seed(41 + len(mn_major))
+
+    def operand(rows, cols, kmaj):
+        if kmaj:  # K-major: (rows, cols) contiguous enough
+            return mk((rows, (cols + 7) // 8 * 8), torch.bfloat16, g), None
+        # MN-major (K rows of MN columns): flat storage that ends at the last row's column MN
+        flat = torch.full(((rows - 1) * W + 256 + cols,), float("nan"), dtype=torch.bfloat16)
+        v = torch.as_strided(flat, (rows, cols), (W, 1), 256)
+        v.copy_(torch.randn(rows, cols, generator=g).to(torch.bfloat16))
+        flat = flat.cuda()
+        return torch.as_strided(flat, (rows, cols), (W, 1), 256), flat
+
+    A, fa = operand(K if not a_k else M, M if not a_k else K, a_k)
+    B, fb = operand(K if not b_k else N, N if not b_k else K, b_k)
+    for f in (fa, fb):
+        if f is not None:
+            assert f.untyped_storage().nbytes() >= f.numel() * 2  # the view ends at numel
+    C = torch.full((M, N + 4), 7.0, device="cuda")
+    before = ops.MN_TAIL_COPIES
+    ops.gemm(A, B, C, M=M, N=N, K=K, a_kmajor=a_k, b_kmajor=b_k, lda=A.stride(0), ldb=B.stride(0),
+             ldc=C.stride(0), splitk=False)
+    torch.cuda.synchronize()
+    # each MN-major view ends exactly at its storage's end (a storage's nbytes is the size
+    # asked for, whatever block the caching allocator rounded it into): each is re-homed
+    assert ops.MN_TAIL_COPIES - before == len(mn_major)
+    ref = ref_mm(A, B, a_k, b_k, M, N, K)
+    got = C[:, :N].double().cpu()
+    assert torch.isfinite(got).all()
+    torch.testing.assert_close(got, ref, atol=2e-3 * K ** 0.5, rtol=2e-3)
+    assert (C[:, N:] == 7.0).all()
+
+
+def test_mn_tail_guard_rehomes_exact_views():
+    """_mn_tail_guard copies an MN-major bf16 view (MN % 8 != 0) exactly when its storage ends
+    before the last row's 16-B chunk does, keeping the view's strides from the new base."""
+    ops, _ = _ops()
+    K, MN, W = 5, 13, 64
+    flat = torch.arange((K - 1) * W + 16 + MN, dtype=torch.float32).to(torch.bfloat16).cuda()
+    v = torch.as_strided(flat, (K, MN), (W, 1), 16)
+    got = ops._mn_tail_guard(v, MN, K, W, (0, 0), 1, 1)
+    assert got is not v and got.numel() >= (K - 1) * W + MN + 8
+    torch.testing.assert_close(torch.as_strided(got, (K, MN), (W, 1), 0), v, atol=0, rtol=0)
+    roomy = torch.zeros((K - 1) * W + 16 + 16, dtype=torch.bfloat16).cuda()
+    v2 = torch.as_strided(roomy, (K, MN), (W, 1), 16)
+    assert ops._mn_tail_guard(v2, MN, K, W, (0, 0), 1, 1) is v2
+    assert ops._mn_tail_guard(v, 16, K, W, (0, 0), 1, 1) is v  # MN % 8 == 0: whole chunks
+
 
 def test_gemm_grouped_vs_fp64():
     """ea_gemm_grouped: several (0,0)-layout f32-accumulating problems in one launch (edge

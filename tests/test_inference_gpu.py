@@ -107,6 +107,56 @@ def test_decoder_kv_cache_steps_match_full_forward(amp, graph, monkeypatch):
     m.train()
 
 
+def test_decoder_graph_states_fall_back_past_capacity(monkeypatch):
+    """A captured decoding run hands out GraphStepKV states; once a prefix outgrows the run's
+    key/value capacity (graph_lcap) batch_score continues on the eager incremental path from
+    those states (the run's buffer cropped to the prefix), and a stale state re-builds its
+    cache from the prefix.  Every step still equals the full decoder forward (fp32, 2e-5)."""
+    from test_model_build import build
+    from espnet_amd.asr.decoder.transformer_decoder import DecoderKVCache, GraphStepKV, TransformerDecoder
+    monkeypatch.setattr(TransformerDecoder, "decode_graph", True)
+    monkeypatch.setattr(TransformerDecoder, "graph_lcap", 4)
+    cfg, d = load("tiny_hybrid")
+    torch.manual_seed(0)
+    m = build(cfg)
+    m.load_state_dict({k: torch.from_numpy(v) for k, v in section(d, "w").items()})
+    m.prepare("cuda", amp=False)
+    inp = {k: torch.from_numpy(v) for k, v in section(d, "in").items()}
+    m.eval()
+    g = torch.Generator().manual_seed(5)
+    kinds = []
+    with torch.no_grad():
+        enc, _ = m.encode(inp["speech"][:1, :int(inp["speech_lengths"][0])], inp["speech_lengths"][:1])
+        n, V, T = 3, m.vocab_size, enc.shape[1]
+        xs = enc.expand(n, -1, -1)
+        ys = torch.full((n, 1), m.sos, dtype=torch.long)
+        states = [None] * n
+        for step in range(7):
+            logp, st = m.decoder.batch_score(ys.cuda(), states, xs)
+            kinds.append(type(st[0][0]).__name__)
+            full, _ = m.decoder(xs.contiguous(), torch.full((n,), T, dtype=torch.long, device="cuda"), ys.cuda(),
+                                torch.full((n,), ys.shape[1], dtype=torch.long, device="cuda"))
+            torch.testing.assert_close(logp, torch.log_softmax(full[:, -1].float(), -1), atol=2e-5, rtol=2e-5)
+            parents = torch.randperm(n, generator=g)
+            ys = torch.cat([ys[parents], torch.randint(2, V - 1, (n, 1), generator=g)], dim=1)
+            states = [st[int(p)] for p in parents]
+        assert kinds[:4] == ["GraphStepKV"] * 4 and kinds[4:] == ["DecoderKVCache"] * 3
+        # a stale captured state (its run has stepped on since) scores from the prefix
+        enc2 = enc.expand(1, -1, -1)
+        y1 = torch.full((1, 1), m.sos, dtype=torch.long).cuda()
+        _, s1 = m.decoder.batch_score(y1, [None], enc2)
+        y2 = torch.cat([y1, torch.full((1, 1), 5, dtype=torch.long, device="cuda")], 1)
+        _, s2 = m.decoder.batch_score(y2, s1, enc2)
+        assert isinstance(s1[0][0], GraphStepKV) and s1[0][0].step != s1[0][0].run.nstep
+        assert TransformerDecoder._as_cache(s1[0][0]) is None
+        logp, s3 = m.decoder.score(y2[0], s1[0], enc2[0])
+        full, _ = m.decoder(enc2.contiguous(), torch.full((1,), T, dtype=torch.long, device="cuda"), y2,
+                            torch.full((1,), 2, dtype=torch.long, device="cuda"))
+        torch.testing.assert_close(logp, torch.log_softmax(full[0, -1].float(), -1), atol=2e-5, rtol=2e-5)
+        assert isinstance(s3[0], DecoderKVCache)
+    m.train()
+
+
 def test_beam_search_matches_reference_goldens():
     """BeamSearch (decoder + LengthBonus, and joint CTC/attention with the CTC prefix kernel at
     ctc_weight 0.3/0.5; beams 3/4, maxlenratio 0 with end detection and 0.5) on the HIP model: every n-best hypothesis's token sequence equals the reference

@@ -30,6 +30,19 @@ def test_grouped_transpose_and_refresh():
     for v, wt in zip(views, wts):
         assert torch.equal(wt, v.t().contiguous())
     assert ts.get(views[1]) is wts[1]  # registered once
+    # a captured refresh freezes the table: a weight first seen afterwards is not registered
+    # (the graph would never refresh its copy, and rebuilding would free the captured table)
+    tiles_ptr = ts.tiles.data_ptr()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        ts.refresh()
+    late = shadow[:64 * 64].view(64, 64)
+    assert ts.frozen and ts.get(late) is None and ts.tiles.data_ptr() == tiles_ptr
+    shadow.mul_(3.0)
+    g.replay()
+    torch.cuda.synchronize()
+    for v, wt in zip(views, wts):
+        assert torch.equal(wt, v.t().contiguous())
 
 
 def _amp_grads(wt_on):
