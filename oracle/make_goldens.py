@@ -681,6 +681,18 @@ SIZED = {
         model_conf=dict(ctc_weight=1.0, lsm_weight=0.0, length_normalized_loss=False),
         speech_lengths=[500, 437], text_lengths=[20, 14], seed=0,
     ),
+    # BASELINE.json configs[4] (C5): Conformer-L + 6-layer decoder with SpecAug (conformer8),
+    # a bucketed pair at the longest length of T ~ U[200, 2000] (T' = 499) and a ragged one,
+    # L = round(T/25); the TimeWarp / mask draws and MultiSequential's layer-drop draws come
+    # from torch.manual_seed(spec_seed) set before each forward
+    "c5_b2": dict(
+        encoder="conformer", input_size=80, vocab_size=5000,
+        encoder_conf=conformer_conf(512, 8, 2048, 12), decoder="transformer",
+        decoder_conf=decoder_conf(8, 2048, 6),
+        model_conf=dict(ctc_weight=0.3, lsm_weight=0.1, length_normalized_loss=False),
+        speech_lengths=[2000, 1317], text_lengths=[80, 53], seed=0,
+        specaug="conformer8", spec_seed=77,
+    ),
     # AMP check: d_k = 64, 2+2 blocks, T' = 99 (two 64-query tiles), ragged
     "amp_hybrid": dict(
         encoder="conformer", input_size=80, vocab_size=300,
@@ -712,6 +724,15 @@ def capture_sized(name):
     torch.manual_seed(seed)
     model = build_reference_model(cfg)
     perturb_norms(model, torch.Generator().manual_seed(1000 + seed))
+    if cfg.get("specaug"):
+        from espnet2.asr.specaug.specaug import SpecAug
+        model.specaug = SpecAug(**SPECAUG_CONFS[cfg["specaug"]])
+        cfg = dict(cfg, specaug_conf=SPECAUG_CONFS[cfg["specaug"]])
+
+    def reseed():  # the host draws of the step (SpecAug, then repeat.py:27), same for both passes
+        if cfg.get("spec_seed") is not None:
+            torch.manual_seed(cfg["spec_seed"])
+
     batch = make_batch(cfg, torch.Generator().manual_seed(1))
     model.train()
     sd0 = {k: v.clone() for k, v in model.state_dict().items()}
@@ -726,6 +747,7 @@ def capture_sized(name):
         enc_out["x"], enc_out["lens"] = out[0], out[1]
 
     h = model.encoder.register_forward_hook(enc_hook)
+    reseed()
     loss, stats, weight = model(**{k: v.clone() for k, v in batch.items()})
     loss.backward()
     h.remove()
@@ -756,6 +778,7 @@ def capture_sized(name):
     # the same step under CPU autocast (bf16), from the same initial state
     model.load_state_dict(sd0)
     model.zero_grad()
+    reseed()
     with torch.autocast("cpu", dtype=torch.bfloat16):
         aloss, astats, _ = model(**{k: v.clone() for k, v in batch.items()})
     aloss.backward()

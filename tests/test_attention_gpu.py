@@ -125,6 +125,11 @@ def _inputs(B, H, T1, T2, rel, seed=0):
     (1, 2, 270, 270, False, True, [270]),
     (2, 1, 64, 64, True, False, [64, 1]),
     (1, 1, 130, 130, True, False, [130]),
+    # C5's longest bucket: T' = 499 (997-row positional band through the band rings, the
+    # T-dependent dbd layout), ragged; decoder self / source attention over 499 frames
+    (2, 2, 499, 499, True, False, [499, 331]),
+    (1, 1, 499, 499, False, True, [499]),
+    (2, 2, 81, 499, False, False, [499, 330]),
 ])
 def test_fused_attention_matches_fp32_reference(B, H, T1, T2, rel, causal, klens, v2):
     q, k, v, u, vb, pp, dO = _inputs(B, H, T1, T2, rel)
@@ -204,6 +209,7 @@ def test_fused_matches_unfused_with_dropout():
     (3, 2, 249, [249, 200, 64], 0.0),
     (1, 2, 300, [300], 0.0),
     (2, 2, 97, [97, 60], 0.1),
+    (2, 2, 499, [499, 331], 0.1),
 ])
 def test_fused_bwd2_rel_terms(B, H, T, klens, p):
     """ea_attn_fused_bwd2 with flags=1 and the forward's keep bits: dq includes the (q+v)
@@ -294,6 +300,7 @@ def test_fused_dropout_mask_matches_rehash(causal, T1, T2, klens):
     (1, 2, 300, [300], 0.1, True),
     (2, 1, 97, [97, 1], 0.0, False),
     (2, 2, 45, [45, 30], 0.1, True),
+    (2, 2, 499, [499, 331], 0.1, True),
 ])
 def test_bwdq_pipelined_matches_original(B, H, T, klens, p, mask):
     """The pipelined dQ pass (flags bit 1: LDS-DMA one chunk ahead, bpermute gather, 64-column
@@ -345,6 +352,8 @@ def test_bwdq_pipelined_matches_original(B, H, T, klens, p, mask):
     (2, 2, 45, 45, False, True, [45, 30], 0.1),
     (2, 1, 41, 300, False, False, [300, 131], 0.0),
     (1, 1, 5, 5, True, False, [5], 0.1),
+    (2, 2, 499, 499, True, False, [499, 331], 0.1),
+    (2, 1, 81, 499, False, False, [499, 330], 0.0),
 ])
 def test_fwd_pipelined_matches_original(B, H, T1, T2, rel, causal, klens, p, monkeypatch):
     """The pipelined forward (LDS-DMA one chunk ahead, bpermute BD gather, Pd^T image) is the
@@ -378,6 +387,8 @@ def test_fwd_pipelined_matches_original(B, H, T1, T2, rel, causal, klens, p, mon
     (2, 2, 45, 45, False, True, [45, 30], 0.1, True),
     (2, 1, 41, 300, False, False, [300, 131], 0.0, False),
     (1, 1, 5, 5, True, False, [5], 0.1, True),
+    (2, 2, 499, 499, True, False, [499, 331], 0.1, True),
+    (1, 1, 499, 499, False, True, [499], 0.1, False),
 ])
 def test_bwdkv_pipelined_matches_original(B, H, T1, T2, rel, causal, klens, p, mask, monkeypatch):
     """The pipelined dK/dV pass (LDS-DMA one query tile ahead, per-wave BD tiles gathered by

@@ -1,0 +1,217 @@
+"""Parity at the exact shapes the bench times (BASELINE.json configs[2] C3 and configs[4] C5).
+
+The sized goldens (test_model_sized_gpu.py) run B=2; at the bench's B=32 the same model takes
+different kernel paths: Linear GEMMs at M = 7,968 tokens on 64x128 tiles over the 3-deep ring
+with the transposed-weight shadow, 256x256 ping-pong tiles, the grouped full-K weight
+gradient with K = 7,968, and the subsampling conv2 implicit GEMMs at M = 151,392 with the
+XCD-contiguous (batch slice, K split, tile) mapping and the 7-way split-K weight gradient.
+
+* Conv2dSubsampling (subsampling.py:46-91) forward + backward at C3 (B=32, T=1000) and at the
+  longest C5 bucket (B=17, T=2000, T'=499), bf16, against a float64 restatement that rounds
+  to bf16 exactly where the HIP path stores bf16 (conv1 output x1p, the bf16 weight shadow,
+  conv2 output x2, the scaled output gradient, the ReLU-masked conv2 / conv1 input
+  gradients): what is left is the f32 accumulation order and the bf16 rounding flips it
+  causes (relative L2 <= 1e-3 per tensor; an indexing or tiling error is O(1) on the rows
+  it touches).  The same HIP results are also reported against plain float64.
+* The whole C3 model (Conformer-L 12x512 + 6-layer decoder, V=5000, L=40) at B=32, T=1000
+  with two ragged utterances, forward + backward in fp32 and in bf16 AMP, against the
+  oracle run in float64 on the host cores (oracle/asr_oracle.py, pinned by
+  test_oracle_goldens.py): fp32 every gradient relative L2 <= 2e-5; bf16 per tensor within
+  max(2x the reference's own bf16 deviation at this architecture (tests/golden/c3_b2.npz
+  ampdev), 2e-2).
+"""
+import math
+
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+from goldens import is_null_grad, regenerate_sized, section, sibling_weight
+from test_model_build import build
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda:0"
+
+
+def _rel(a, b):
+    a = torch.as_tensor(a).double()
+    b = torch.as_tensor(b).double()
+    den = float(b.norm())
+    return float((a - b).norm()) / den if den > 0 else float((a - b).norm())
+
+
+# ---------------------------------------------------------------------------- subsampling
+def _bf(x):
+    return x.to(torch.bfloat16).to(torch.float64)
+
+
+def _subsampling_f64(P, feats, gy, emulate_bf16):
+    """Conv2dSubsampling fwd + bwd in float64 (dropout 0).  emulate_bf16: round where the
+    implicit-GEMM path stores bf16.  Returns (y, {param: grad})."""
+    r = _bf if emulate_bf16 else (lambda t: t)
+    W1, b1 = P["conv.0.weight"], P["conv.0.bias"]
+    W2, b2 = P["conv.2.weight"], P["conv.2.bias"]
+    Wl, bl = P["out.0.weight"], P["out.0.bias"]
+    C = W1.shape[0]
+    xs = math.sqrt(C)
+    x = feats.unsqueeze(1)
+    x1 = r(torch.relu(F.conv2d(x, W1, b1, stride=2)))              # (B, C, T1, F1)
+    W2r = r(W2)
+    x2 = r(torch.relu(F.conv2d(x1, W2r, b2, stride=2)))            # (B, C, T2, F2)
+    B, _, T2, F2 = x2.shape
+    xr = x2.transpose(1, 2).reshape(B, T2, C * F2)                   # subsampling.py:66-69
+    Wlr = r(Wl)
+    y = (xr @ Wlr.t() + bl) * xs
+    g = {}
+    gs = gy * xs
+    dv = r(gs)
+    g["out.0.bias"] = gs.reshape(-1, C).sum(0)
+    g["out.0.weight"] = dv.reshape(-1, C).t() @ xr.reshape(-1, C * F2)
+    dxr = (dv @ Wlr).reshape(B, T2, C, F2).transpose(1, 2)           # (B, C, T2, F2)
+    dh2 = r(dxr * (x2 > 0))
+    g["conv.2.bias"] = dh2.sum((0, 2, 3))
+    g["conv.2.weight"] = torch.nn.grad.conv2d_weight(x1, W2.shape, dh2, stride=2)
+    dx1 = r(torch.nn.grad.conv2d_input(x1.shape, W2r, dh2, stride=2) * (x1 > 0))
+    g["conv.0.bias"] = dx1.sum((0, 2, 3))
+    g["conv.0.weight"] = torch.nn.grad.conv2d_weight(x, W1.shape, dx1, stride=2)
+    return y, g
+
+
+@pytest.mark.parametrize("B,T", [(32, 1000), (17, 2000)], ids=["c3_b32", "c5_b17_t2000"])
+def test_subsampling_bench_shapes_bf16_vs_float64(B, T):
+    from espnet_amd.arena import ParamArena
+    from espnet_amd.layers import subsampling as S
+    C = 512
+    torch.manual_seed(0)
+    sub = S.Conv2dSubsampling(80, C, 0.0)
+    dev = torch.device(DEV)
+    arena = ParamArena(sub, dev, [], shadow_dtype=torch.bfloat16)
+    sub.bind(arena, "", torch.bfloat16)
+    sub._anchor = torch.zeros(1, device=dev, requires_grad=True)
+    sub.train()
+    assert S._implicit_ok(torch.bfloat16, C)
+    g = torch.Generator().manual_seed(5)
+    feats = torch.randn(B, T, 80, generator=g)
+    T2 = ((T - 1) // 2 - 1) // 2
+    gy = torch.randn(B, T2, C, generator=g)
+    y = sub(feats.to(dev), 0)
+    y.backward(gy.to(dev))
+    torch.cuda.synchronize()
+    y_hip = y.detach().double().cpu()
+    g_hip = {k: p.grad.detach().double().cpu() for k, p in sub.named_parameters()}
+    P = {k: p.detach().double().cpu() for k, p in sub.named_parameters()}
+    del sub, arena, y
+    torch.set_num_threads(16)
+    with torch.no_grad():
+        y_em, g_em = _subsampling_f64(P, feats.double(), gy.double(), True)
+        y_ex, g_ex = _subsampling_f64(P, feats.double(), gy.double(), False)
+    report = {"y": (_rel(y_hip, y_em), _rel(y_hip, y_ex))}
+    for k in g_em:
+        report[k] = (_rel(g_hip[k], g_em[k]), _rel(g_hip[k], g_ex[k]))
+    print(f"B={B} T={T}: rel L2 vs (bf16-emulating f64, plain f64): "
+          + "; ".join(f"{k} {a:.2e} / {b:.2e}" for k, (a, b) in report.items()))
+    # per utterance as well: a tile-edge / batch-slice error shows up in the rows it touches
+    per_utt = max(_rel(y_hip[b], y_em[b]) for b in range(B))
+    assert per_utt <= 2e-3, per_utt
+    for k, (e_em, e_ex) in report.items():
+        assert e_em <= 1e-3, (k, e_em)
+        assert e_ex <= 2e-2, (k, e_ex)
+
+
+# ---------------------------------------------------------------------------- whole C3 model
+_EXACT = {}
+
+
+def _c3_b32_batch():
+    g = torch.Generator().manual_seed(11)
+    B, T, L, V = 32, 1000, 40, 5000
+    lens = [T] * B
+    lens[5], lens[20] = 913, 777  # ragged: the padded frames of two utterances (T' 227, 193)
+    tl = [L] * B
+    tl[5], tl[20], tl[31] = 37, 31, 12
+    speech = torch.zeros(B, T, 80)
+    text = torch.full((B, L), -1, dtype=torch.long)
+    for b in range(B):
+        speech[b, :lens[b]] = torch.randn(lens[b], 80, generator=g)
+        text[b, :tl[b]] = torch.randint(2, V - 1, (tl[b],), generator=g)
+    return dict(speech=speech, speech_lengths=torch.tensor(lens), text=text, text_lengths=torch.tensor(tl))
+
+
+def _exact_c3_b32(cfg, m_cpu, inp):
+    if "c3" not in _EXACT:
+        from oracle.asr_oracle import OracleASR
+        torch.set_num_threads(16)
+        ora = OracleASR(cfg, {k: v.detach() for k, v in m_cpu.state_dict().items()}, dtype=torch.float64)
+        loss, stats, _ = ora(**inp)
+        loss.backward()
+        _EXACT["c3"] = (loss.item(), {k: float(v) for k, v in stats.items()},
+                        {k: p.grad.detach() for k, p in ora.params.items()},
+                        ora.encoder_out.detach(), ora.encoder_out_lens)
+        del ora
+    return _EXACT["c3"]
+
+
+def _hip_step(m, inp, amp):
+    m.prepare(DEV, amp=amp)
+    m.train()
+    loss, stats, weight = m(**inp)
+    loss.backward()
+    torch.cuda.synchronize()
+    return loss, stats, weight
+
+
+def test_c3_b32_fp32_vs_float64():
+    cfg, d, m = regenerate_sized("c3_b2", build)
+    inp = _c3_b32_batch()
+    x_loss, x_stats, x_grads, x_enc, x_olens = _exact_c3_b32(cfg, m, inp)
+    loss, stats, weight = _hip_step(m, inp, amp=False)
+    np.testing.assert_allclose(loss.item(), x_loss, rtol=2e-6, atol=1e-4)
+    assert weight.item() == 32
+    for k in ("loss_ctc", "loss_att", "acc"):
+        np.testing.assert_allclose(stats[k].item(), x_stats[k], rtol=2e-6, atol=1e-4, err_msg=k)
+    enc, olens = m._last_encoder_out
+    np.testing.assert_array_equal(olens.cpu().numpy(), x_olens.numpy())
+    e_enc = _rel(enc.detach().cpu(), x_enc)
+    assert e_enc <= 2e-5, e_enc
+    worst = []
+    for k, p in m.named_parameters():
+        mine = p.grad.detach().cpu()
+        if is_null_grad(k):
+            sib = dict(m.named_parameters())[sibling_weight(k)].grad.detach().double().norm().item()
+            assert mine.double().norm().item() <= 1e-3 * sib, k
+            continue
+        e = _rel(mine, x_grads[k])
+        worst.append((e, k))
+        assert e <= 2e-5, (k, e)
+    worst.sort(reverse=True)
+    print(f"c3 B=32 fp32: encoder_out {e_enc:.2e}; gradient relative L2 vs float64, worst: {worst[:3]}")
+
+
+AMP_FLOOR = 2e-2
+
+
+def test_c3_b32_bf16_vs_float64():
+    cfg, d, m = regenerate_sized("c3_b2", build)
+    inp = _c3_b32_batch()
+    x_loss, _, x_grads, _, _ = _exact_c3_b32(cfg, m, inp)
+    loss, stats, _ = _hip_step(m, inp, amp=True)
+    loss_dev = abs(loss.item() - x_loss) / abs(x_loss)
+    ref_loss_dev = abs(float(d["amp.loss"]) - float(d["out.loss"])) / abs(float(d["out.loss"]))
+    assert loss_dev <= max(2 * ref_loss_dev, 2e-3), (loss_dev, ref_loss_dev)
+    ampdev = section(d, "ampdev")
+    params = dict(m.named_parameters())
+    worst = []
+    for k, p in params.items():
+        mine = p.grad.detach().cpu()
+        if is_null_grad(k):
+            assert mine.double().norm().item() <= 1e-2 * params[sibling_weight(k)].grad.double().norm().item(), k
+            continue
+        e = _rel(mine, x_grads[k])
+        bound = max(2.0 * float(ampdev[k]), AMP_FLOOR)
+        worst.append((e / bound, e, float(ampdev[k]), k))
+    worst.sort(reverse=True)
+    print(f"c3 B=32 bf16: loss dev {loss_dev:.2e}; worst e/bound:",
+          "; ".join(f"{k} {e:.2e} (ref B=2 {r:.2e})" for _, e, r, k in worst[:5]))
+    bad = [w for w in worst if w[0] > 1.0]
+    assert not bad, bad[:10]

@@ -147,7 +147,7 @@ def test_oracle_ddp_gloo_two_ranks(tmp_path):
     assert bufs < 1e-5, bufs
 
 
-@pytest.mark.parametrize("name", ["c2_b2", "amp_hybrid", "c3_b2"])
+@pytest.mark.parametrize("name", ["c2_b2", "amp_hybrid", "c3_b2", "c5_b2"])
 def test_oracle_sized_goldens(name):
     """The oracle at BASELINE sizes (C3 / C2 architectures, B=2, ragged) against the
     reference's fp32 capture: loss, stats, encoder output, CTC argmax, every parameter's
@@ -158,6 +158,8 @@ def test_oracle_sized_goldens(name):
     torch.set_num_threads(8)
     ora = OracleASR(cfg, {k: v.detach() for k, v in m.state_dict().items()})
     inp = {k: torch.from_numpy(v) for k, v in section(d, "in").items()}
+    if cfg.get("spec_seed") is not None:  # c5_b2: SpecAug + layer-drop draws, as captured
+        torch.manual_seed(cfg["spec_seed"])
     loss, stats, _ = ora(**inp)
     loss.backward()
     np.testing.assert_allclose(loss.item(), d["out.loss"], rtol=2e-6, atol=1e-4)
@@ -173,7 +175,10 @@ def test_oracle_sized_goldens(name):
             assert g.norm().item() <= 1e-3 * gn_all[sibling_weight(k)], k
             continue
         np.testing.assert_allclose(g.norm().item(), gn, rtol=5e-4, err_msg=k)
-        assert_grad_close(g.reshape(-1)[:256].numpy(), d["gh." + k], k)
+        # c5_b2 (T' = 499): the fp32 summation-order noise of the reference vs the oracle grows
+        # with the reduction length (measured 1.2e-3 of the tensor's max on the worst head)
+        assert_grad_close(g.reshape(-1)[:256].numpy(), d["gh." + k], k,
+                          scale_tol=2e-3 if name == "c5_b2" else 1e-3)
     for k, v in section(d, "buf_after").items():
         np.testing.assert_allclose(ora.bufs[k].numpy(), v, atol=1e-5, rtol=1e-5, err_msg=k)
 
