@@ -63,17 +63,20 @@ __global__ void ctc_prefix_init_kernel(int T, int V, int blank, const float* __r
 }
 
 // one thread per (hypothesis h, candidate c): __call__ (:303-358)
+// ol_arr: per-hypothesis output lengths, or NULL when every hypothesis has ol_uniform
 __global__ __launch_bounds__(64) void ctc_prefix_score_kernel(int T, int V, int blank, int eos, int n_hyp,
                                                               int n_cand, const float* __restrict__ logp,
                                                               const unsigned long long* __restrict__ r_prev_ptr,
-                                                              const int* __restrict__ meta, float* __restrict__ log_psi,
+                                                              const int* __restrict__ ol_arr, int ol_uniform,
+                                                              const int* __restrict__ last_arr,
+                                                              const int* __restrict__ cand_arr, float* __restrict__ log_psi,
                                                               float* __restrict__ r_new) {
   const int idx = blockIdx.x * 64 + threadIdx.x;
   if (idx >= n_hyp * n_cand) return;
   const int h = idx / n_cand;
-  const int ol = meta[h];                 // output length (prefix without <sos>)
-  const int last = meta[n_hyp + h];       // last label of the prefix
-  const int c = meta[2 * n_hyp + idx];    // candidate label
+  const int ol = ol_arr ? ol_arr[h] : ol_uniform;  // output length (prefix without <sos>)
+  const int last = last_arr[h];                     // last label of the prefix
+  const int c = cand_arr[idx];                      // candidate label
   const float* rp = (const float*)r_prev_ptr[h];
   float* r = r_new + (long)idx * T * 2;
   const bool same = ol > 0 && c == last;  // log_phi = r^b(g) for a repeated label, else r^n + r^b
@@ -155,7 +158,21 @@ extern "C" int ea_ctc_prefix_score(int T, int V, int blank, int eos, int n_hyp, 
   EA_CHECK_ARG(T >= 1 && V >= 1 && n_hyp >= 0 && n_cand >= 0);
   if (n_hyp * n_cand == 0) return 0;
   hipLaunchKernelGGL(ctc_prefix_score_kernel, dim3(ea_cdiv(n_hyp * n_cand, 64)), dim3(64), 0, (hipStream_t)stream, T,
-                     V, blank, eos, n_hyp, n_cand, logp, r_prev, meta, log_psi, r_new);
+                     V, blank, eos, n_hyp, n_cand, logp, r_prev, meta, 0, meta + n_hyp, meta + 2 * n_hyp, log_psi,
+                     r_new);
+  EA_LAUNCH_CHECK();
+  return 0;
+}
+
+extern "C" int ea_ctc_prefix_score_dev(int T, int V, int blank, int eos, int n_hyp, int n_cand, const float* logp,
+                                       const unsigned long long* r_prev, int out_len, const int* last,
+                                       const int* cand, float* log_psi, float* r_new, void* stream) {
+  EA_ENTRY();
+  EA_CHECK_ARG(T >= 1 && V >= 1 && n_hyp >= 0 && n_cand >= 0 && out_len >= 0);
+  if (n_hyp * n_cand == 0) return 0;
+  hipLaunchKernelGGL(ctc_prefix_score_kernel, dim3(ea_cdiv(n_hyp * n_cand, 64)), dim3(64), 0, (hipStream_t)stream, T,
+                     V, blank, eos, n_hyp, n_cand, logp, r_prev, (const int*)nullptr, out_len, last, cand, log_psi,
+                     r_new);
   EA_LAUNCH_CHECK();
   return 0;
 }

@@ -19,6 +19,7 @@ CTC prefix kernel (csrc/ctc_prefix.hip) on posteriors that stay in HBM.
 from __future__ import annotations
 
 import math
+import os
 from typing import Any, Dict, List, NamedTuple, Optional, Union
 
 import torch
@@ -378,4 +379,125 @@ class BatchBeamSearch(BeamSearch):
         for hyp in running_hyps:
             (ended_hyps if int(hyp.yseq[-1]) == self.eos else remained).append(hyp)
         return remained
+
+    # ------------------------------------------------------------------ device-resident steps
+    # EA_BEAM_DEVICE=0 keeps the host selection (A/B, and the reference's arithmetic on the host)
+    device_select = os.environ.get("EA_BEAM_DEVICE", "1") != "0"
+
+    def _device_plan(self, x):
+        """The joint decoding the device step covers: one decoder-like full scorer (batch_score
+        -> (n, V) log-probabilities), an optional LengthBonus, one CTCPrefixScorer as the only
+        partial scorer, pre-beam on the full weighted scores.  None otherwise."""
+        if not (self.device_select and x.is_cuda and self.do_pre_beam and self.pre_beam_score_key == "full"
+                and self.hyp_primer is None):
+            return None
+        if len(self.part_scorers) != 1:
+            return None
+        (ck, ctc), = self.part_scorers.items()
+        if not isinstance(ctc, CTCPrefixScorer):
+            return None
+        dec = [k for k, d in self.full_scorers.items() if not isinstance(d, LengthBonus)]
+        lb = [k for k, d in self.full_scorers.items() if isinstance(d, LengthBonus)]
+        if len(dec) != 1 or len(lb) > 1:
+            return None
+        nc = self.pre_beam_size + 1
+        if self.beam_size * nc > 4096 or self.n_vocab > 32768:
+            return None
+        return dec[0], (lb[0] if lb else None), ck
+
+    @torch.no_grad()
+    def forward(self, x: torch.Tensor, maxlenratio: float = 0.0, minlenratio: float = 0.0) -> List[Hypothesis]:
+        plan = self._device_plan(x)
+        if plan is None:
+            return super().forward(x, maxlenratio, minlenratio)
+        return self._forward_device(x, maxlenratio, minlenratio, *plan)
+
+    def _forward_device(self, x, maxlenratio, minlenratio, dk, lk, ck):
+        """batch_beam_search.py:170-205 + beam_search.py:346-432 with the per-step selection on
+        the device: the decoder's (n, V) log-probabilities never leave HBM; per step ONE
+        small record per new hypothesis (parent, token, scores) comes back to the host, which
+        keeps the reference's hypothesis bookkeeping (yseq, per-scorer scores, <eos> handling,
+        end detection)."""
+        if maxlenratio == 0:
+            maxlen = x.shape[0]
+        elif maxlenratio < 0:
+            maxlen = -1 * int(maxlenratio)
+        else:
+            maxlen = max(1, int(maxlenratio * x.size(0)))
+        dec, ctc = self.full_scorers[dk], self.part_scorers[ck]
+        w_dec, w_ctc = float(self.weights[dk]), float(self.weights[ck])
+        w_lb, use_lb = (float(self.weights[lk]), 1) if lk is not None else (0.0, 0)
+        K, P, V = self.beam_size, self.pre_beam_size, self.n_vocab
+        Pc = P + 1
+        dev = x.device
+        running = self.init_hyp(x)  # CTC init_state: log-posteriors + r0 on the device
+        T = ctc.logp.shape[0]
+        i32, f32 = torch.int32, torch.float32
+        cand = torch.empty(K * Pc, dtype=i32, device=dev)
+        psi = torch.empty(K * Pc, dtype=f32, device=dev)
+        r_buf = [torch.empty(K * Pc, T, 2, dtype=f32, device=dev) for _ in range(2)]
+        rec = torch.empty(8 * K, dtype=i32, device=dev)  # [rec_i (4K) | rec_f (4K) as f32 bits]
+        rec_host = torch.empty(8 * K, dtype=i32).pin_memory()
+        cur_st = dict(last=torch.full((K,), self.sos, dtype=i32, device=dev),
+                      rptr=torch.zeros(K, dtype=torch.int64, device=dev),
+                      prefix=torch.zeros(K, dtype=f32, device=dev), score=torch.zeros(K, dtype=f32, device=dev))
+        cur_st["rptr"][0] = running[0].states[ck][1].data_ptr()
+        nxt_st = {k: torch.empty_like(v) for k, v in cur_st.items()}
+        xs1 = x.unsqueeze(0)
+        ended: List[Hypothesis] = []
+        buf = 0
+        for i in range(maxlen):
+            n = len(running)
+            ys = torch.stack([h.yseq for h in running])  # host: the decoder reads the last tokens
+            logp, dstates = dec.batch_score(ys, [h.states[dk] for h in running], xs1.expand(n, *x.shape))
+            logp = logp.float()
+            if not logp.is_contiguous():
+                logp = logp.contiguous()
+            r_new = r_buf[buf]
+            lib.ea_beam_prebeam(n, V, logp.data_ptr(), V, w_dec, w_lb, use_lb, P, self.eos, cand.data_ptr(),
+                                ops.stream())
+            lib.ea_ctc_prefix_score_dev(T, V, ctc.blank, self.eos, n, Pc, ctc.logp.data_ptr(),
+                                        cur_st["rptr"].data_ptr(), i, cur_st["last"].data_ptr(), cand.data_ptr(),
+                                        psi.data_ptr(), r_new.data_ptr(), ops.stream())
+            lib.ea_beam_select(n, V, P, K, T, logp.data_ptr(), V, cand.data_ptr(), psi.data_ptr(),
+                               cur_st["prefix"].data_ptr(), cur_st["score"].data_ptr(), w_dec, w_lb, use_lb, w_ctc,
+                               r_new.data_ptr(), rec.data_ptr(), rec.data_ptr() + 16 * K, nxt_st["last"].data_ptr(),
+                               nxt_st["rptr"].data_ptr(), nxt_st["prefix"].data_ptr(), nxt_st["score"].data_ptr(),
+                               ops.stream())
+            rec_host.copy_(rec)  # the one device -> host read of the step
+            ri = rec_host[:4 * K].view(K, 4).tolist()
+            rf = rec_host[4 * K:].view(f32).view(K, 4).tolist()
+            best = []
+            for b in range(K):
+                hi, j, k, empty = ri[b]
+                if empty:
+                    raise RuntimeError("beam step left fewer candidates than the beam")
+                tot, dsc, inc, ps = rf[b]
+                hyp = running[hi]
+                sc = dict(hyp.scores)
+                sc[dk] = hyp.scores[dk] + dsc
+                sc[ck] = hyp.scores[ck] + inc
+                if lk is not None:
+                    sc[lk] = hyp.scores[lk] + 1.0
+                st = {dk: dstates[hi], ck: (ps, None)}
+                if lk is not None:
+                    st[lk] = None
+                best.append(Hypothesis(score=tot, yseq=self.append_token(hyp.yseq, j), scores=sc, states=st))
+            running = self.post_process(i, maxlen, maxlenratio, best, ended)
+            if maxlenratio == 0.0 and end_detect([h.asdict() for h in ended], i):
+                break
+            if len(running) == 0:
+                break
+            if len(running) < K:  # ended hypotheses leave the beam: keep the survivors' rows
+                alive = [b for b, h in enumerate(best) if int(h.yseq[-1]) != self.eos]
+                idx = torch.tensor(alive, dtype=torch.long).to(dev, non_blocking=True)
+                for key in cur_st:
+                    torch.index_select(nxt_st[key], 0, idx, out=cur_st[key][:len(alive)])
+            else:
+                cur_st, nxt_st = nxt_st, cur_st
+            buf ^= 1
+        nbest = sorted(ended, key=lambda h: h.score, reverse=True)
+        if len(nbest) == 0:
+            return [] if minlenratio < 0.1 else self.forward(x, maxlenratio, max(0.0, minlenratio - 0.1))
+        return nbest
 

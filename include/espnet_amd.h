@@ -593,6 +593,33 @@ int ea_ctc_prefix_score(int T, int V, int blank, int eos, int n_hyp, int n_cand,
                         const unsigned long long* r_prev, const int* meta, float* log_psi, float* r_new,
                         void* stream);
 
+/* ea_ctc_prefix_score with the metadata as separate device arrays and one output length
+ * out_len shared by every hypothesis (batch beam search: all running prefixes have one
+ * length): last[n_hyp] last labels, cand[n_hyp*n_cand] candidates. */
+int ea_ctc_prefix_score_dev(int T, int V, int blank, int eos, int n_hyp, int n_cand, const float* logp,
+                            const unsigned long long* r_prev, int out_len, const int* last, const int* cand,
+                            float* log_psi, float* r_new, void* stream);
+
+/* Device-side beam step of joint CTC/attention decoding (espnet/nets/batch_beam_search.py:
+ * 170-205 + batch_beam :81-101).  ea_beam_prebeam: per hypothesis h < n, the P best tokens of
+ * W = w_dec*logp[h] (+ w_lb when use_lb), descending (ties: lower token), then <eos>, into
+ * cand[h*(P+1) ...] (int32, device; the candidate block of ea_ctc_prefix_score's meta).
+ * V <= 32768. */
+int ea_beam_prebeam(int n, int V, const float* logp, long ld, float w_dec, float w_lb, int use_lb, int P, int eos,
+                    int* cand, void* stream);
+/* ea_beam_select: the new beam (beam hypotheses) from the n*(P+1) candidates with log_psi =
+ * psi (ea_ctc_prefix_score), per-hypothesis CTC prefix scores `prefix` and running scores
+ * `score`: total = (w_dec*logp (+ w_lb) + w_ctc*(psi - prefix)) + score, global top-k in
+ * descending order (ties: lower flattened index h*V + token; the duplicate <eos> column is
+ * skipped).  Writes per chosen hypothesis b: rec_i[4b..] = {parent, token, candidate column,
+ * 1 if no candidate was left}, rec_f[4b..] = {total, decoder log-prob, CTC increment, psi},
+ * and the next step's inputs last_next[b] = token, rptr_next[b] = &r_new[(parent*(P+1) +
+ * column)*T*2], prefix_next[b] = psi, score_next[b] = total.  n*(P+1) <= 4096. */
+int ea_beam_select(int n, int V, int P, int beam, int T, const float* logp, long ld, const int* cand,
+                   const float* psi, const float* prefix, const float* score, float w_dec, float w_lb, int use_lb,
+                   float w_ctc, const float* r_new, int* rec_i, float* rec_f, int* last_next,
+                   unsigned long long* rptr_next, float* prefix_next, float* score_next, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

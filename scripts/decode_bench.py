@@ -24,8 +24,11 @@ def main():
     ap.add_argument("--tokens", type=int, default=40)
     ap.add_argument("--utts", type=int, default=3)
     ap.add_argument("--fp32", action="store_true")
+    ap.add_argument("--single", action="store_true", help="BeamSearch (per-hypothesis selection on the host) "
+                    "instead of BatchBeamSearch, the reference's default for batch scorers")
+    ap.add_argument("--host-select", action="store_true", help="BatchBeamSearch with the host selection")
     args = ap.parse_args()
-    from espnet_amd.asr.beam_search import BeamSearch, CTCPrefixScorer, LengthBonus
+    from espnet_amd.asr.beam_search import BatchBeamSearch, BeamSearch, CTCPrefixScorer, LengthBonus
     dev = torch.device("cuda", 0)
     cfg = bench.c3_config()
     model = bench.build(cfg)
@@ -45,11 +48,14 @@ def main():
         return wrap
 
     ctc = CTCPrefixScorer(model.ctc, model.eos)
-    ctc.score_partial_multi = timed("ctc", ctc.score_partial_multi)
+    ctc.score_partial_multi = timed("ctc", ctc.score_partial_multi)  # host-selection paths only
     dec = model.decoder
     dec_batch_score = dec.batch_score
     dec.batch_score = timed("decoder", dec_batch_score)
-    bs = BeamSearch(scorers={"decoder": dec, "ctc": ctc, "length_bonus": LengthBonus(V)},
+    if args.host_select:
+        BatchBeamSearch.device_select = False
+    cls = BeamSearch if args.single else BatchBeamSearch
+    bs = cls(scorers={"decoder": dec, "ctc": ctc, "length_bonus": LengthBonus(V)},
                     weights={"decoder": 1.0 - args.ctc_weight, "ctc": args.ctc_weight, "length_bonus": 0.0},
                     beam_size=args.beam, vocab_size=V, sos=model.sos, eos=model.eos, pre_beam_score_key="full")
     g = torch.Generator().manual_seed(3)
@@ -71,7 +77,7 @@ def main():
         torch.cuda.synchronize()
         el = time.perf_counter() - t0
     n = args.utts
-    print(f"C3 joint decode: beam {args.beam}, ctc_weight {args.ctc_weight}, {args.tokens} tokens, "
+    print(f"C3 joint decode ({cls.__name__}{', host selection' if args.host_select else ''}): beam {args.beam}, ctc_weight {args.ctc_weight}, {args.tokens} tokens, "
           f"T'={enc.shape[1]}: {el / n * 1e3:.1f} ms/utt ({n / el:.2f} utt/s); encode {t_enc / n * 1e3:.1f} ms, "
           f"decoder scoring {timers['decoder'] / n * 1e3:.1f} ms, CTC prefix scoring {timers['ctc'] / n * 1e3:.1f} ms "
           f"per utt; best hyp len {len(nbest[0].yseq) - 2}", flush=True)

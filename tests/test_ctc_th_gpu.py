@@ -55,6 +55,49 @@ def test_batch_beam_search_matches_reference_batch_goldens():
                 np.testing.assert_allclose(float(h.score), float(bd[k + ".score"]), rtol=1e-4, atol=1e-3)
 
 
+@pytest.mark.parametrize("amp", [False, True])
+def test_batch_beam_device_step_matches_host_step(amp, monkeypatch):
+    """BatchBeamSearch with the selection on the device (ea_beam_prebeam -> CTC prefix kernel
+    -> ea_beam_select, one small record per new hypothesis back to the host) against the same
+    search with the reference's host arithmetic (EA_BEAM_DEVICE=0 path): identical n-best
+    token sequences, scores within 1e-4 (per-scorer sums are accumulated in float64 on the
+    device path, in float32 tensors on the host path)."""
+    from espnet_amd.asr.beam_search import BatchBeamSearch, CTCPrefixScorer, LengthBonus
+    from test_model_build import build
+    from goldens import section
+    cfg, d = load("tiny_hybrid")
+    torch.manual_seed(0)
+    m = build(cfg)
+    m.load_state_dict({k: torch.from_numpy(v) for k, v in section(d, "w").items()})
+    m.prepare(DEV, amp=amp)
+    m.eval()
+    inp = {k: torch.from_numpy(v) for k, v in section(d, "in").items()}
+    V = m.vocab_size
+    for beam, lb, cw, mlr in ((4, 0.0, 0.3, 0.0), (6, 0.5, 0.5, 0.0), (10, 1.0, 0.3, -12.0)):
+        res = {}
+        for dev_sel in (False, True):
+            monkeypatch.setattr(BatchBeamSearch, "device_select", dev_sel)
+            out = []
+            for u in range(inp["speech"].shape[0]):
+                le = int(inp["speech_lengths"][u])
+                enc, _ = m.encode(inp["speech"][u:u + 1, :le], inp["speech_lengths"][u:u + 1])
+                bs = BatchBeamSearch(scorers={"decoder": m.decoder, "ctc": CTCPrefixScorer(m.ctc, m.eos),
+                                              "length_bonus": LengthBonus(V)},
+                                     weights={"decoder": 1.0 - cw, "ctc": cw, "length_bonus": lb}, beam_size=beam,
+                                     vocab_size=V, sos=m.sos, eos=m.eos, pre_beam_score_key="full")
+                assert (bs._device_plan(enc[0]) is not None) == dev_sel
+                out.append(bs(enc[0], maxlenratio=mlr))
+            res[dev_sel] = out
+        for hu, du in zip(res[False], res[True]):
+            assert len(hu) == len(du) and len(du) > 0
+            for h, g in zip(hu, du):
+                assert h.yseq.tolist() == g.yseq.tolist(), (beam, lb, cw)
+                np.testing.assert_allclose(float(g.score), float(h.score), rtol=1e-5, atol=1e-4)
+                for k in ("decoder", "ctc"):
+                    np.testing.assert_allclose(float(g.scores[k]), float(h.scores[k]), rtol=1e-5, atol=1e-4)
+    m.train()
+
+
 def test_ctc_scorer_batch_api_matches_th():
     """CTCPrefixScorer.batch_init_state / batch_score_partial / select_state (scorers/ctc.py:
     40-126, the interface the reference's BatchBeamSearch drives) agree with CTCPrefixScoreTH
