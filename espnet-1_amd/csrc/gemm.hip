@@ -8,6 +8,7 @@
 
 namespace eag {
 int g_pipe_slots = [] { const char* e = std::getenv("EA_PIPE_SLOTS"); return e ? std::atoi(e) : 4; }();
+int g_pipe128_slots = [] { const char* e = std::getenv("EA_PIPE128_SLOTS"); return e ? std::atoi(e) : 4; }();
 }  // namespace eag
 
 namespace {
@@ -199,6 +200,13 @@ extern "C" int ea_probe_end(unsigned long long* slots, void* stream) {
 extern "C" int ea_gemm_set_pipe(int on) {
   EA_ENTRY();
   g_gemm_pipe = on;
+  return 0;
+}
+
+extern "C" int ea_gemm_set_pipe128_slots(int slots) {
+  EA_ENTRY();
+  EA_CHECK_ARG(slots == 4 || slots == 6 || slots == 8);
+  eag::g_pipe128_slots = slots;
   return 0;
 }
 

@@ -63,6 +63,7 @@ int launch_lds_dense(GemmP& p, int a_k, int b_k, dim3 grid, hipStream_t st);  //
 int launch_lds_conv(GemmP& p, dim3 grid, hipStream_t st);                     // gemm_lds_conv.hip
 // ring depth of the 256x256 ping-pong kernel: 4 slots, or 5 (EA_PIPE_SLOTS; gemm.hip)
 extern int g_pipe_slots;
+extern int g_pipe128_slots;  // ring depth of the 128x128 ping-pong tile (4, 6 or 8)
 }  // namespace eag
 
 namespace {
@@ -570,6 +571,18 @@ __global__ __launch_bounds__(NT, 2) void gemm_kernel(GemmP p) {
 template <int N>
 EA_DEV void wait_vmcnt() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+// wait until at most `newer` groups of G DMA instructions (the ones issued last) are still
+// in flight; newer in [0, MAXN] (runtime value, compile-time counts)
+template <int G, int MAXN>
+EA_DEV void wait_newer(int newer) {
+  if (MAXN >= 6 && newer >= 6) wait_vmcnt<(MAXN >= 6 ? 6 : 0) * G>();
+  else if (MAXN >= 5 && newer == 5) wait_vmcnt<(MAXN >= 5 ? 5 : 0) * G>();
+  else if (MAXN >= 4 && newer == 4) wait_vmcnt<(MAXN >= 4 ? 4 : 0) * G>();
+  else if (MAXN >= 3 && newer == 3) wait_vmcnt<(MAXN >= 3 ? 3 : 0) * G>();
+  else if (MAXN >= 2 && newer == 2) wait_vmcnt<(MAXN >= 2 ? 2 : 0) * G>();
+  else if (newer == 1) wait_vmcnt<G>();
+  else wait_vmcnt<0>();
 }
 EA_DEV void lds_barrier() {
   asm volatile("" ::: "memory");
@@ -1172,9 +1185,12 @@ struct PipeT {
   static constexpr int SMEM = RING > EPI_BYTES ? RING : EPI_BYTES;
   static constexpr int ACH = A_BYTES / (NTT * 16), BCH = B_BYTES / (NTT * 16);  // DMA per thread
   static constexpr int G = ACH + BCH;
-  static constexpr int OCC = BT == 256 ? 1 : 2;
+  // 128x128 with a deep ring (NS > 4): one block per CU whose DMA keeps NS-2 slices (up to
+  // 96 KiB) in flight — the grids where one block per CU is all there is (M = 7,968, N = 512)
+  static constexpr int OCC = BT == 256 ? 1 : (NS <= 4 ? 2 : 1);
   static_assert(BT == 256 || BT == 128, "pipe tiles");
-  static_assert(NS == 4 || NS == 5, "ring depth: 4 slots, or 5 (256x256: the whole 160 KiB LDS)");
+  static_assert((BT == 256 && (NS == 4 || NS == 5)) || (BT == 128 && NS >= 4 && NS <= 8),
+                "ring depth: 256x256 4 slots, or 5 (the whole 160 KiB LDS); 128x128 4-8 slots");
   EA_DEV static int wm(int w) { return BT == 256 ? (w >> 2) * 128 : (w >> 2) * 64 + ((w >> 1) & 1) * 32; }
   EA_DEV static int wn(int w) { return BT == 256 ? (w & 3) * 64 : (w & 1) * 64; }
 };
@@ -1353,10 +1369,7 @@ EA_DEV void pipe_tile(const GemmP& p, char* smem, const bf16* A, const bf16* B, 
   const int npre = min(NSLOT - 1, nsl);
   for (int sl = 0; sl < npre; ++sl) issue(sl);
   // own share of slice 0 landed (slices 1 .. npre-1 may stay in flight), then everyone's
-  if (NSLOT == 5 && npre >= 4) wait_vmcnt<(NSLOT == 5 ? 3 : 2) * G>();
-  else if (npre >= 3) wait_vmcnt<2 * G>();
-  else if (npre == 2) wait_vmcnt<G>();
-  else wait_vmcnt<0>();
+  wait_newer<G, NSLOT - 2>(npre - 1);
   lds_barrier();
   if (g1) lds_barrier();  // the stagger
   bf16x8 fa[MI], fb[4];
@@ -1368,11 +1381,7 @@ EA_DEV void pipe_tile(const GemmP& p, char* smem, const bf16* A, const bf16* B, 
     if (sl + NSLOT - 1 < nsl) issue(sl + NSLOT - 1);
     // own share of slice sl+1 landed: the groups issued after it (sl+2 .. sl+NSLOT-1) may stay
     // in flight
-    const int newer = min(NSLOT - 2, nsl - 2 - sl);
-    if (NSLOT == 5 && newer >= 3) wait_vmcnt<(NSLOT == 5 ? 3 : 2) * G>();
-    else if (newer >= 2) wait_vmcnt<2 * G>();
-    else if (newer == 1) wait_vmcnt<G>();
-    else wait_vmcnt<0>();
+    wait_newer<G, NSLOT - 2>(min(NSLOT - 2, nsl - 2 - sl));
     // fragments in registers before the barrier: the COMPUTE segment never waits on LDS, and
     // this wave is done reading slot sl when the barrier releases its refill
     if (!AK || !BKM) {  // asm tr-reads are invisible to the waitcnt pass

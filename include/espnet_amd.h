@@ -132,6 +132,9 @@ int ea_gemm_set_tile(int bm, int bn);
 /* Route 256x256-tile bf16 GEMMs to the pipelined kernel (gemm_pipe: 4-slot ring of 32-deep
  * K slices, counted vmcnt, one barrier per slice) when on != 0 (A/B switch). */
 int ea_gemm_set_pipe(int on);
+/* Ring depth of the 128x128 ping-pong tile: 4 slots (two blocks per CU) or 6 / 8 (one block
+ * per CU, 4 / 6 slices of 16 KiB in flight).  Process-wide; A/B switch (EA_PIPE128_SLOTS). */
+int ea_gemm_set_pipe128_slots(int slots);
 
 /* One problem of a grouped launch: C[M,N] (f32, row stride ldc) = beta*C + op(A) op(B), bf16
  * operands in the layouts of ea_gemm (a_kmajor/b_kmajor shared by the group), lda/ldb

@@ -24,12 +24,14 @@ SHAPES = [  # (name, N, K, a_kmajor, b_kmajor, epilogue, out dtype)
     ("fwd_swish N2048 K512", 2048, 512, 1, 1, "act", torch.bfloat16),
     ("qkv N1536 K512", 1536, 512, 1, 1, "store", torch.bfloat16),
 ]
-CONFIGS = [  # (label, pipe bits, forced tile (bm, bn) or None, env)
-    ("auto", 1, None),
-    ("lds64x128", 1, (64, 128)),
-    ("lds128", 1, (128, 128)),
-    ("pipe128", 3, (128, 128)),
-    ("pipe256", 1, (256, 256)),
+CONFIGS = [  # (label, pipe bits, forced tile (bm, bn) or None, 128x128 ring slots)
+    ("auto", 1, None, 4),
+    ("lds64x128", 1, (64, 128), 4),
+    ("lds128", 1, (128, 128), 4),
+    ("pipe128", 3, (128, 128), 4),
+    ("pipe128s6", 3, (128, 128), 6),
+    ("pipe128s8", 3, (128, 128), 8),
+    ("pipe256", 1, (256, 256), 4),
 ]
 
 
@@ -47,7 +49,8 @@ def run(name, N, K, ak, bk, kind, odt, iters=50):
     else:
         epi = ops.make_epi()
     out = []
-    for label, pipe, tile in CONFIGS:
+    for label, pipe, tile, slots in CONFIGS:
+        lib.ea_gemm_set_pipe128_slots(slots)
         lib.ea_gemm_set_pipe(pipe)
         lib.ea_gemm_set_tile(*(tile or (0, 0)))
         f = lambda: ops.gemm(A, B, C, M=M, N=N, K=K, a_kmajor=ak, b_kmajor=bk, lda=A.stride(0),  # noqa: E731
@@ -65,6 +68,7 @@ def run(name, N, K, ak, bk, kind, odt, iters=50):
         out.append((label, us, 2.0 * M * N * K / us * 1e-6))
     lib.ea_gemm_set_tile(0, 0)
     lib.ea_gemm_set_pipe(1)
+    lib.ea_gemm_set_pipe128_slots(4)
     # hipBLASLt reference (plain bf16 GEMM, no epilogue)
     a = A if ak else A.t()
     b = B.t() if bk else B

@@ -5,6 +5,11 @@ cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
 O=gpurun_out/r4c
 mkdir -p $O
+timeout -k 10 300 python -u -m pytest -x -q --timeout 240 --timeout-method thread -m gpu tests/test_gemm_gpu.py \
+  > $O/pytest_gemm.log 2>&1
+rc=$?; tail -3 $O/pytest_gemm.log; [ $rc -eq 0 ] || exit $rc
+timeout -k 10 300 python -u scripts/gemm_n512.py > $O/gemm_n512.txt 2>&1 || exit 1
+cat $O/gemm_n512.txt | grep -v amdgpu.ids
 timeout -k 10 300 python -u -m pytest -x -v --timeout 240 --timeout-method thread -m gpu tests/test_ctc_th_gpu.py \
   tests/test_inference_gpu.py > $O/pytest_beam.log 2>&1
 rc=$?; tail -3 $O/pytest_beam.log; [ $rc -eq 0 ] || exit $rc

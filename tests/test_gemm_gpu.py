@@ -169,21 +169,29 @@ def test_gemm_unaligned_leading_dims(dtype, a_k, b_k):
 
 # (bm, bn, pipe): pipe=1 routes the 256x256 tile to gemm_pipe (4-slot ring of 32-deep slices)
 from espnet_amd._lib import GEMM_PIPE as PIPE_DEFAULT  # noqa: E402  (restored after each test)
-TILES = [(32, 128, 0), (64, 128, 0), (128, 128, 0), (128, 128, 3), (256, 256, 0), (256, 256, 1)]
+# (bm, bn, pipe[, 128x128 ring slots])
+TILES = [(32, 128, 0), (64, 128, 0), (128, 128, 0), (128, 128, 3), (128, 128, 3, 6), (128, 128, 3, 8),
+         (256, 256, 0), (256, 256, 1)]
+
+
+def _tile_id(t):
+    return f"{t[0]}x{t[1]}{'p' * t[2]}" + (f"s{t[3]}" if len(t) > 3 else "")
 
 
 @pytest.fixture
 def forced_tile(request):
     ops, L = _ops()
-    bm, bn, pipe = request.param
+    bm, bn, pipe = request.param[:3]
     L.lib.ea_gemm_set_tile(bm, bn)
     L.lib.ea_gemm_set_pipe(pipe)
+    L.lib.ea_gemm_set_pipe128_slots(request.param[3] if len(request.param) > 3 else 4)
     yield (bm, bn)
     L.lib.ea_gemm_set_tile(0, 0)
     L.lib.ea_gemm_set_pipe(PIPE_DEFAULT)
+    L.lib.ea_gemm_set_pipe128_slots(4)
 
 
-@pytest.mark.parametrize("forced_tile", TILES, indirect=True, ids=lambda t: f"{t[0]}x{t[1]}{'p' * t[2]}")
+@pytest.mark.parametrize("forced_tile", TILES, indirect=True, ids=_tile_id)
 @pytest.mark.parametrize("a_k,b_k", [(1, 1), (1, 0), (0, 1), (0, 0)])
 @pytest.mark.parametrize("MNK", [(300, 520, 200), (513, 257, 64), (40, 300, 130), (256, 256, 128),
                                  (600, 700, 1000), (260, 300, 32)])
@@ -203,7 +211,7 @@ def test_gemm_bf16_tiles(forced_tile, a_k, b_k, MNK):
     assert (C[:, N:] == 7.0).all(), "wrote outside ldc columns"
 
 
-@pytest.mark.parametrize("forced_tile", TILES, indirect=True, ids=lambda t: f"{t[0]}x{t[1]}{'p' * t[2]}")
+@pytest.mark.parametrize("forced_tile", TILES, indirect=True, ids=_tile_id)
 def test_gemm_bf16_tiles_epilogue_splitk(forced_tile):
     """Fused ACT epilogue and split-K dW under each tile shape."""
     ops, L = _ops()
@@ -229,7 +237,7 @@ def test_gemm_bf16_tiles_epilogue_splitk(forced_tile):
     torch.testing.assert_close(dw.double().cpu(), refw, atol=2e-3 * R ** 0.5, rtol=2e-3)
 
 
-@pytest.mark.parametrize("forced_tile", TILES, indirect=True, ids=lambda t: f"{t[0]}x{t[1]}{'p' * t[2]}")
+@pytest.mark.parametrize("forced_tile", TILES, indirect=True, ids=_tile_id)
 @pytest.mark.parametrize("mn_major", ["A", "B", "AB"])
 def test_gemm_mn_major_slice_at_allocation_end(forced_tile, mn_major):
     """The bf16 decoder fault of round 3 (commit 9880edd): an MN-major operand that is a
