@@ -51,8 +51,11 @@ int g_gemm_bm64 = 1;
 int g_gemm_bm32 = [] { const char* e = std::getenv("EA_GEMM_BM32"); return e ? std::atoi(e) : 1; }();
 int g_gemm_pipe = 0;  // ea_gemm_set_pipe bits: 1 = 256x256 tiles on gemm_pipe, 2 = 128x128 tiles too
 
-int launch_lds(GemmP& p, int a_k, int b_k, int nz, hipStream_t st, bool pipe128 = false) {
+int g_gemm_k128 = [] { const char* e = std::getenv("EA_GEMM_K128"); return e ? std::atoi(e) : 0; }();
+
+int launch_lds(GemmP& p, int a_k, int b_k, int nz, hipStream_t st, bool pipe128 = false, bool k128 = false) {
   dim3 grid(p.tiles_m * p.tiles_n, 1, nz * p.splitk);
+  if (k128) return launch_k128(p, grid, st);
   if (p.g.mode != 0) {  // implicit-GEMM conv2 modes: fixed layouts, 128x128 or 256x256 tiles
     if (p.bm == 256 && g_gemm_pipe) return launch_pipe_conv(p, grid, st);
     return launch_lds_conv(p, grid, st);
@@ -91,8 +94,8 @@ void choose_tile(GemmP& p, int a_k, long nz) {
 }
 
 template <typename T>
-int launch(GemmP& p, int a_k, int b_k, int nz, hipStream_t st, bool pipe128 = false) {
-  if (sizeof(T) == 2 && p.lds) return launch_lds(p, a_k, b_k, nz, st, pipe128);
+int launch(GemmP& p, int a_k, int b_k, int nz, hipStream_t st, bool pipe128 = false, bool k128 = false) {
+  if (sizeof(T) == 2 && p.lds) return launch_lds(p, a_k, b_k, nz, st, pipe128, k128);
   if (p.bm != 128 || p.bn != 128) return EA_ERR_BAD_ARG;
   dim3 grid(p.tiles_m * p.tiles_n, 1, nz * p.splitk);
 #define EA_GEMM_CASE(AKV, BKV)                                                      \
@@ -203,6 +206,14 @@ extern "C" int ea_gemm_set_pipe(int on) {
   return 0;
 }
 
+extern "C" int ea_gemm_set_k128(int mode, int slots) {
+  EA_ENTRY();
+  EA_CHECK_ARG(mode >= 0 && mode <= 3 && (slots == 3 || slots == 4 || slots == 5));
+  g_gemm_k128 = mode;
+  eag::g_k128_slots = slots;
+  return 0;
+}
+
 extern "C" int ea_gemm_set_pipe128_slots(int slots) {
   EA_ENTRY();
   EA_CHECK_ARG(slots == 4 || slots == 6 || slots == 8);
@@ -298,6 +309,18 @@ static int gemm_impl(int dtype, int a_kmajor, int b_kmajor, int M, int N, int K,
       pipe128 = (epi128 & 2) != 0;
     }
   }
+  // gemm_k128 (ea_gemm_set_k128 / EA_GEMM_K128): both operands K-major, K a whole number of
+  // 64-deep tiles, a 64x128 / 128x128 choice whose 128x128 grid about fills the CUs (one tile
+  // per CU: the N = 512 GEMMs at M = 7,968); mode 2: any such grid of >= 128 tiles; mode 3:
+  // every eligible GEMM (tests)
+  bool k128 = false;
+  if (g_gemm_k128 && lds_path && !geo && a_kmajor && b_kmajor && K % 64 == 0 && K > 0) {
+    const long t128 = (long)ea_cdiv(M, 128) * ea_cdiv(N, 128) * batch * nh;
+    const bool fits = g_gemm_k128 == 3 ||
+                      (!g_force_bm && (p.bm == 64 || p.bm == 128) && p.bn == 128 && t128 >= 128 &&
+                       (g_gemm_k128 == 2 || t128 <= 256));
+    if (fits) { p.bm = 128; p.bn = 128; k128 = true; }
+  }
   if (p.bm <= 64 && !a_kmajor) return EA_ERR_BAD_ARG;
   p.tiles_m = ea_cdiv(M, p.bm);
   p.tiles_n = ea_cdiv(N, p.bn);
@@ -316,7 +339,7 @@ static int gemm_impl(int dtype, int a_kmajor, int b_kmajor, int M, int N, int K,
       while (splitk > 1 && (long)splitk * M * N > ws_elems) --splitk;
       splitk = max(splitk, 1);
     }
-  } else if (workspace && tiles < 200 && K >= 16 * KT && K >= 1024 && (long)p.tiles_m * p.tiles_n * nz < 128) {
+  } else if (!k128 && workspace && tiles < 200 && K >= 16 * KT && K >= 1024 && (long)p.tiles_m * p.tiles_n * nz < 128) {
     // (a grid already covering half the CUs — e.g. 32-row tiles of a decoder GEMM — runs
     // unsplit: the partial slabs and the combine pass cost more than the extra blocks gain)
     splitk = (int)((384 + tiles - 1) / tiles);
@@ -334,10 +357,11 @@ static int gemm_impl(int dtype, int a_kmajor, int b_kmajor, int M, int N, int K,
   p.kchunk = kchunk;
   static const bool trace = std::getenv("EA_GEMM_TRACE") != nullptr;  // shape census (diagnostics)
   if (trace)
-    std::fprintf(stderr, "[ea_gemm] M=%d N=%d K=%d ak=%d bk=%d nz=%d tile=%dx%d splitk=%d epi=%d geo=%d lds=%d\n", M,
-                 N, K, a_kmajor, b_kmajor, nz, p.bm, p.bn, splitk, (int)epi->kind, geo ? geo->mode : 0, (int)p.lds);
+    std::fprintf(stderr, "[ea_gemm] M=%d N=%d K=%d ak=%d bk=%d nz=%d tile=%dx%d%s splitk=%d epi=%d geo=%d lds=%d\n", M,
+                 N, K, a_kmajor, b_kmajor, nz, p.bm, p.bn, k128 ? "k" : "", splitk, (int)epi->kind, geo ? geo->mode : 0,
+                 (int)p.lds);
   hipStream_t st = (hipStream_t)stream;
-  int rc = dtype == EA_BF16 ? launch<bf16>(p, a_kmajor, b_kmajor, nz, st, pipe128)
+  int rc = dtype == EA_BF16 ? launch<bf16>(p, a_kmajor, b_kmajor, nz, st, pipe128, k128)
                             : launch<float>(p, a_kmajor, b_kmajor, nz, st);
   if (rc) return rc;
   if (splitk > 1) {

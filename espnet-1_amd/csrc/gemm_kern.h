@@ -58,12 +58,14 @@ struct GemmP {
 
 // launchers of the LDS-DMA kernels (grid = tiles x 1 x (batch * split-K slices))
 int launch_pipe(GemmP& p, int a_k, int b_k, dim3 grid, hipStream_t st);  // gemm_pipe.hip: 256 / 128 tiles
+int launch_k128(GemmP& p, dim3 grid, hipStream_t st);                     // gemm_k128.hip: 128x128 K-major
 int launch_pipe_conv(GemmP& p, dim3 grid, hipStream_t st);               // gemm_pipe_conv.hip: conv2 modes
 int launch_lds_dense(GemmP& p, int a_k, int b_k, dim3 grid, hipStream_t st);  // gemm_lds.hip
 int launch_lds_conv(GemmP& p, dim3 grid, hipStream_t st);                     // gemm_lds_conv.hip
 // ring depth of the 256x256 ping-pong kernel: 4 slots, or 5 (EA_PIPE_SLOTS; gemm.hip)
 extern int g_pipe_slots;
 extern int g_pipe128_slots;  // ring depth of the 128x128 ping-pong tile (4, 6 or 8)
+extern int g_k128_slots;     // ring depth of gemm_k128 (3, 4 or 5)
 }  // namespace eag
 
 namespace {
@@ -1090,6 +1092,146 @@ __global__ __launch_bounds__(128 * WN, 1) void gemm_bf16_lds(GemmP p) {
   }
 
   __syncthreads();  // every wave is done reading the operand ring: reuse it for the epilogue
+  const EpiK ek = make_epik(p);
+  switch (p.splitk > 1 ? EA_EPI_STORE : p.epi.kind) {
+    case EA_EPI_STORE: epi_wave<EA_EPI_STORE, MI, NJ>(p, ek, smem, z, zb, zh, m0 + wm, n0 + wn, lane, w, acc, sk); break;
+    case EA_EPI_ACT: epi_wave<EA_EPI_ACT, MI, NJ>(p, ek, smem, z, zb, zh, m0 + wm, n0 + wn, lane, w, acc, sk); break;
+    case EA_EPI_RESID: epi_wave<EA_EPI_RESID, MI, NJ>(p, ek, smem, z, zb, zh, m0 + wm, n0 + wn, lane, w, acc, sk); break;
+    default: epi_wave<EA_EPI_DACT, MI, NJ>(p, ek, smem, z, zb, zh, m0 + wm, n0 + wn, lane, w, acc, sk); break;
+  }
+  probe_end(p);
+}
+
+// ---------------------------------------------------------------- 128x128, K-major, deep ring
+// gemm_k128: the narrow-N GEMMs of the step (M = 7,968 tokens, N = 512: forward projections and
+// the input gradients over the transposed weight shadow — both operands K-major) as ONE
+// 128 x 128 tile per CU (252 blocks: the fewest operand bytes per CU for this output size,
+// 1 MiB at K = 2,048 against 1.5 MiB for two 64 x 128 tiles).  4 waves of 64 x 64; 64-deep
+// K-tiles through an S-slot LDS ring filled by LDS-DMA S-1 tiles ahead (counted vmcnt, one
+// barrier per K-tile).  The fragments of the NEXT k-step are read while the current k-step's
+// 16 MFMAs run — across the K-tile boundary too (tile t+1's first k-step is read right after
+// the barrier that publishes it) — so no MFMA waits on an LDS read it just issued.  Fragment
+// reads are inline asm with counted lgkmcnt (hipcc would put a vmcnt(0) in front of an LDS
+// read it can see while an LDS-DMA is in flight).  Same image format, DMA sources, tile
+// mapping and epilogue as gemm_bf16_lds<128, 128>; the host guarantees K % 64 == 0 per split.
+EA_DEV bf16x8 ds_read_b128_asm(const char* p) {
+  bf16x8 v;
+  const uint32_t a = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) char*)p;
+  asm volatile("ds_read_b128 %0, %1" : "=v"(v) : "v"(a) : "memory");
+  return v;
+}
+
+template <int S>
+__global__ __launch_bounds__(256, 1) void gemm_k128(GemmP p) {
+  constexpr int BM = 128, BN = 128, BK = 64, NTT = 256, NW = 4, MI = 4, NJ = 4;
+  constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2, STAGE = A_BYTES + B_BYTES;
+  constexpr int ACH = A_BYTES / (NTT * 16), BCH = B_BYTES / (NTT * 16), G = ACH + BCH;
+  constexpr int EPI_BYTES = NW * 4 * 16 * EPI_LDT * 4;
+  constexpr int SMEM = S * STAGE > EPI_BYTES ? S * STAGE : EPI_BYTES;
+  static_assert(S >= 3 && S <= 5, "ring depth");
+  __shared__ __attribute__((aligned(1024))) char smem[SMEM];
+  probe_start(p);
+
+  const TileIdx ti = tile_index(p);
+  const int m0 = ti.tm * BM, n0 = ti.tn * BN;
+  const int z = ti.z, sk = ti.sk;
+  const int zb = z / p.nh, zh = z % p.nh;
+  const bf16* A = (const bf16*)p.A + zb * p.sAb + zh * p.sAh;
+  const bf16* B = (const bf16*)p.B + zb * p.sBb + zh * p.sBh;
+  const int kbeg = sk * p.kchunk;
+  const int kend = min(p.K, kbeg + p.kchunk);
+  const int nt = max(0, (kend - kbeg) / BK);
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int wm = (w >> 1) * 64, wn = (w & 1) * 64;
+
+  // lane-linear DMA: chunk ci = (i*NW + w)*64 + lane lands at ci*16; its source is the
+  // global chunk whose swizzled slot that is (32-bit byte offsets, operands < 4 GB)
+  auto src = [&](long ld, int mn0, int MN, int ci) -> uint32_t {
+    const int row = ci >> 3, c = (ci & 7) ^ swz_k(ci >> 3);
+    return (uint32_t)(((long)min(mn0 + row, MN - 1) * ld + c * 8) * 2);
+  };
+  const char* abase = (const char*)(A + kbeg);
+  const char* bbase = (const char*)(B + kbeg);
+  uint32_t aoff[ACH], boff[BCH];
+#pragma unroll
+  for (int i = 0; i < ACH; ++i) aoff[i] = src(p.lda, m0, p.M, (i * NW + w) * 64 + lane);
+#pragma unroll
+  for (int i = 0; i < BCH; ++i) boff[i] = src(p.ldb, n0, p.N, (i * NW + w) * 64 + lane);
+
+  auto issue = [&](int t) {
+    char* base = smem + (t % S) * STAGE;
+    const char* ak = abase + (long)t * BK * 2;
+    const char* bk = bbase + (long)t * BK * 2;
+#pragma unroll
+    for (int i = 0; i < ACH; ++i)
+      __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)(ak + aoff[i]),
+                                       (__attribute__((address_space(3))) void*)(base + (i * NW + w) * 1024), 16, 0, 0);
+#pragma unroll
+    for (int i = 0; i < BCH; ++i)
+      __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)(bk + boff[i]),
+                                       (__attribute__((address_space(3))) void*)(base + A_BYTES + (i * NW + w) * 1024),
+                                       16, 0, 0);
+  };
+  // fragments of k-step ks (32 deep) of tile t: 16 rows (lane & 15), k-block 8*(lane>>4)
+  auto rd = [&](int t, int ks, bf16x8 (&fa)[MI], bf16x8 (&fb)[NJ]) {
+    const char* la = smem + (t % S) * STAGE;
+    const char* lb = la + A_BYTES;
+    const int ch = ks * 4 + (lane >> 4);
+#pragma unroll
+    for (int i = 0; i < MI; ++i) {
+      const int row = wm + i * 16 + (lane & 15);
+      fa[i] = ds_read_b128_asm(la + row * 128 + ((ch ^ swz_k(row)) << 4));
+    }
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      const int row = wn + j * 16 + (lane & 15);
+      fb[j] = ds_read_b128_asm(lb + row * 128 + ((ch ^ swz_k(row)) << 4));
+    }
+  };
+
+  f32x4 acc[MI][NJ];
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  auto mma = [&](const bf16x8 (&fa)[MI], const bf16x8 (&fb)[NJ]) {
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int i = 0; i < MI; ++i)
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+  };
+
+  bf16x8 fa0[MI], fb0[NJ], fa1[MI], fb1[NJ];
+  if (nt > 0) {
+    const int npre = min(S - 1, nt);
+    for (int t = 0; t < npre; ++t) issue(t);
+    wait_newer<G, S - 2>(npre - 1);  // own share of tile 0 landed
+    lds_barrier();                   // everyone's
+    rd(0, 0, fa0, fb0);
+    for (int t = 0; t < nt; ++t) {
+      rd(t, 1, fa1, fb1);
+      asm volatile("s_waitcnt lgkmcnt(8)" ::: "memory");  // fa0/fb0 (the older 8 reads) are in
+      __builtin_amdgcn_sched_barrier(0);
+      mma(fa0, fb0);
+      __builtin_amdgcn_sched_barrier(0);
+      if (t + 1 < nt) {
+        // own share of tile t+1 landed; tiles t+2 .. t+S-2 (issued earlier) may stay in flight
+        wait_newer<G, S - 3>(min(S - 3, nt - 2 - t));
+        lds_barrier();  // everyone's; every wave is past its tile t-1 reads: its slot is free
+        if (t + S - 1 < nt) issue(t + S - 1);
+        rd(t + 1, 0, fa0, fb0);
+        asm volatile("s_waitcnt lgkmcnt(8)" ::: "memory");  // fa1/fb1 in
+      } else {
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      mma(fa1, fb1);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+  __syncthreads();  // every wave is done reading the ring: the epilogue reuses it
   const EpiK ek = make_epik(p);
   switch (p.splitk > 1 ? EA_EPI_STORE : p.epi.kind) {
     case EA_EPI_STORE: epi_wave<EA_EPI_STORE, MI, NJ>(p, ek, smem, z, zb, zh, m0 + wm, n0 + wn, lane, w, acc, sk); break;

@@ -135,6 +135,12 @@ int ea_gemm_set_pipe(int on);
 /* Ring depth of the 128x128 ping-pong tile: 4 slots (two blocks per CU) or 6 / 8 (one block
  * per CU, 4 / 6 slices of 16 KiB in flight).  Process-wide; A/B switch (EA_PIPE128_SLOTS). */
 int ea_gemm_set_pipe128_slots(int slots);
+/* gemm_k128 (128x128 tile, K-major A and B, one block per CU, 64-deep K-tiles through a
+ * `slots`-deep LDS ring with cross-tile fragment prefetch) for bf16 GEMMs: mode 0 off, 1 =
+ * where a 64x128 / 128x128 tile was chosen and the 128x128 grid has 128-256 tiles (the
+ * N = 512 GEMMs at M = 7,968), 2 = such grids of any size >= 128 tiles, 3 = every eligible
+ * GEMM (K % 64 == 0; tests).  Process-wide (EA_GEMM_K128). */
+int ea_gemm_set_k128(int mode, int slots);
 
 /* One problem of a grouped launch: C[M,N] (f32, row stride ldc) = beta*C + op(A) op(B), bf16
  * operands in the layouts of ea_gemm (a_kmajor/b_kmajor shared by the group), lda/ldb

@@ -21,6 +21,8 @@ SHAPES = [  # (name, N, K, a_kmajor, b_kmajor, epilogue, out dtype)
     ("dx N512 K512", 512, 512, 1, 0, "store", torch.bfloat16),
     ("dx N512 K1536", 512, 1536, 1, 0, "store", torch.bfloat16),
     ("dx N512 K2048", 512, 2048, 1, 0, "store", torch.bfloat16),
+    ("dxT N512 K1536 (W^T shadow)", 512, 1536, 1, 1, "store", torch.bfloat16),
+    ("dxT N512 K2048 (W^T shadow)", 512, 2048, 1, 1, "store", torch.bfloat16),
     ("fwd_swish N2048 K512", 2048, 512, 1, 1, "act", torch.bfloat16),
     ("qkv N1536 K512", 1536, 512, 1, 1, "store", torch.bfloat16),
 ]
@@ -32,6 +34,9 @@ CONFIGS = [  # (label, pipe bits, forced tile (bm, bn) or None, 128x128 ring slo
     ("pipe128s6", 3, (128, 128), 6),
     ("pipe128s8", 3, (128, 128), 8),
     ("pipe256", 1, (256, 256), 4),
+    ("k128s3", 1, "k128:3", 4),
+    ("k128s4", 1, "k128:4", 4),
+    ("k128s5", 1, "k128:5", 4),
 ]
 
 
@@ -52,7 +57,14 @@ def run(name, N, K, ak, bk, kind, odt, iters=50):
     for label, pipe, tile, slots in CONFIGS:
         lib.ea_gemm_set_pipe128_slots(slots)
         lib.ea_gemm_set_pipe(pipe)
-        lib.ea_gemm_set_tile(*(tile or (0, 0)))
+        if isinstance(tile, str):  # gemm_k128 with a ring depth (K-major A and B only)
+            if not (ak and bk):
+                continue
+            lib.ea_gemm_set_tile(0, 0)
+            lib.ea_gemm_set_k128(3, int(tile.split(":")[1]))
+        else:
+            lib.ea_gemm_set_k128(0, 4)
+            lib.ea_gemm_set_tile(*(tile or (0, 0)))
         f = lambda: ops.gemm(A, B, C, M=M, N=N, K=K, a_kmajor=ak, b_kmajor=bk, lda=A.stride(0),  # noqa: E731
                              ldb=B.stride(0), ldc=N, epi=epi, splitk=False)
         for _ in range(5):
@@ -69,6 +81,7 @@ def run(name, N, K, ak, bk, kind, odt, iters=50):
     lib.ea_gemm_set_tile(0, 0)
     lib.ea_gemm_set_pipe(1)
     lib.ea_gemm_set_pipe128_slots(4)
+    lib.ea_gemm_set_k128(0, 4)
     # hipBLASLt reference (plain bf16 GEMM, no epilogue)
     a = A if ak else A.t()
     b = B.t() if bk else B

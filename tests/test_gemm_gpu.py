@@ -302,6 +302,62 @@ def test_mn_tail_guard_rehomes_exact_views():
     assert ops._mn_tail_guard(v, 16, K, W, (0, 0), 1, 1) is v  # MN % 8 == 0: whole chunks
 
 
+@pytest.mark.parametrize("slots", [3, 4, 5])
+@pytest.mark.parametrize("MNK", [(7968, 512, 2048), (7968, 512, 512), (300, 200, 128), (129, 520, 64),
+                                 (1000, 384, 1536)])
+def test_gemm_k128_vs_fp64(slots, MNK):
+    """gemm_k128 (128x128 tile, K-major A and B, deep LDS ring with cross-tile fragment
+    prefetch; the N = 512 GEMMs of the C3 step) against fp64: the bench shapes and edges in
+    M and N, bf16 and f32 outputs, fused RESID / ACT epilogues."""
+    ops, L = _ops()
+    M, N, K = MNK
+    g = torch.Generator().manual_seed(M + N + K + slots)
+    A = mk((M, K + 8), torch.bfloat16, g)
+    B = mk((N, K + 8), torch.bfloat16, g, 0.1)
+    L.lib.ea_gemm_set_k128(3, slots)
+    try:
+        C = torch.full((M, N + 4), 7.0, device="cuda")
+        ops.gemm(A, B, C, M=M, N=N, K=K, a_kmajor=1, b_kmajor=1, lda=A.stride(0), ldb=B.stride(0), ldc=C.stride(0))
+        ref = ref_mm(A, B, 1, 1, M, N, K)
+        torch.testing.assert_close(C[:, :N].double().cpu(), ref, atol=2e-3 * K ** 0.5, rtol=2e-3)
+        assert (C[:, N:] == 7.0).all()
+        bias = mk((N,), torch.float32, g)
+        R = torch.randn(M, N, generator=g).cuda()
+        R0 = R.clone()
+        ops.gemm(A, B, R, M=M, N=N, K=K, a_kmajor=1, b_kmajor=1, lda=A.stride(0), ldb=B.stride(0), ldc=N,
+                 epi=ops.make_epi(L.EPI_RESID, bias=bias, resid=R, rscale=0.5))
+        torch.testing.assert_close(R.double().cpu(), R0.double().cpu() + 0.5 * (ref + bias.double().cpu()),
+                                   atol=2e-3 * K ** 0.5, rtol=2e-3)
+        aux = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
+        Ca = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
+        ops.gemm(A, B, Ca, M=M, N=N, K=K, a_kmajor=1, b_kmajor=1, lda=A.stride(0), ldb=B.stride(0), ldc=N,
+                 epi=ops.make_epi(L.EPI_ACT, bias=bias, act=L.ACT_SWISH, aux=aux))
+        h = ref + bias.double().cpu()
+        torch.testing.assert_close(aux.double().cpu(), h, atol=3e-2, rtol=2e-2)
+        torch.testing.assert_close(Ca.double().cpu(), h * torch.sigmoid(h), atol=3e-2, rtol=2e-2)
+    finally:
+        L.lib.ea_gemm_set_k128(0, 4)
+
+
+def test_gemm_k128_linear_paths_match_default():
+    """ea_gemm_set_k128(1): the Linear forward / input-gradient GEMMs at the C3 token count
+    route to gemm_k128 and agree with the default tiles to bf16-accumulation-order noise."""
+    ops, L = _ops()
+    g = torch.Generator().manual_seed(8)
+    M = 7968
+    x = mk((M, 2048), torch.bfloat16, g)
+    w = mk((512, 2048), torch.bfloat16, g, 0.05)
+    y0 = torch.empty(M, 512, device="cuda")
+    y1 = torch.empty(M, 512, device="cuda")
+    ops.linear(x, w, y0)
+    L.lib.ea_gemm_set_k128(1, 4)
+    try:
+        ops.linear(x, w, y1)
+    finally:
+        L.lib.ea_gemm_set_k128(0, 4)
+    torch.testing.assert_close(y1, y0, atol=1e-3, rtol=1e-3)
+
+
 def test_gemm_grouped_vs_fp64():
     """ea_gemm_grouped: several (0,0)-layout f32-accumulating problems in one launch (edge
     tiles in M and N, K remainders, beta 0 / 1, longest-K-first order) vs fp64."""
