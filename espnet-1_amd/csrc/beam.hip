@@ -62,30 +62,72 @@ EA_DEV Best block_argmax(Best b, Best* red) {
 }
 
 // one block per hypothesis: the P best tokens of W = w_dec*logp (+ w_lb), descending, then
-// <eos>; written at cand[h*(P+1) ...].  Each thread owns tokens tid, tid+NT, ... (<= 32 of
-// them) and marks the ones already taken in a bit mask.
-constexpr int PB_NT = 1024;
+// <eos>; written at cand[h*(P+1) ...].  Two levels under the total order (value desc, token
+// asc): each wave takes the top P of its slice of the vocabulary (its lane values stay in
+// registers, P argmax rounds by shuffles), then wave 0 takes the top P of the waves' lists.
+constexpr int PB_NT = 1024, PB_NW = PB_NT / 64, PB_PER = 32;  // <= 32 tokens per lane: V <= 32768
+constexpr int PB_PMAX = 64;
+
+EA_DEV Best wave_argmax(Best b) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const float ov = __shfl_xor(b.v, o);
+    const int oi = __shfl_xor(b.i, o);
+    if (better(ov, oi, b.v, b.i)) { b.v = ov; b.i = oi; }
+  }
+  return b;
+}
+
 __global__ __launch_bounds__(PB_NT) void prebeam_kernel(int V, const float* __restrict__ logp, long ld, float w_dec,
                                                         float w_lb, int use_lb, int P, int eos, int* __restrict__ cand) {
-  __shared__ Best red[PB_NT / 64 + 1];
-  const int h = blockIdx.x;
+  __shared__ Best lst[PB_NW * PB_PMAX];
+  const int h = blockIdx.x, lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const float* row = logp + (long)h * ld;
+  const int span = (V + PB_NW - 1) / PB_NW, v0 = wv * span, v1 = min(V, v0 + span);
+  float val[PB_PER];
+#pragma unroll
+  for (int e = 0; e < PB_PER; ++e) {
+    const int v = v0 + e * 64 + lane;
+    float wvv = -INFINITY;
+    if (v < v1) {
+      wvv = __fmul_rn(w_dec, row[v]);
+      if (use_lb) wvv = __fadd_rn(wvv, w_lb);
+    }
+    val[e] = wvv;
+  }
   uint32_t taken = 0u;
-  int* out = cand + (long)h * (P + 1);
   for (int r = 0; r < P; ++r) {
     Best b{-INFINITY, 0x7fffffff};
-    int k = 0;
-    for (int v = threadIdx.x; v < V; v += PB_NT, ++k) {
-      if ((taken >> k) & 1u) continue;
-      float wv = __fmul_rn(w_dec, row[v]);
-      if (use_lb) wv = __fadd_rn(wv, w_lb);
-      if (better(wv, v, b.v, b.i)) { b.v = wv; b.i = v; }
+#pragma unroll
+    for (int e = 0; e < PB_PER; ++e) {
+      const int v = v0 + e * 64 + lane;
+      if (v < v1 && !((taken >> e) & 1u) && better(val[e], v, b.v, b.i)) { b.v = val[e]; b.i = v; }
     }
-    b = block_argmax<PB_NT>(b, red);
-    if (b.i != 0x7fffffff && b.i % PB_NT == (int)threadIdx.x) taken |= 1u << (b.i / PB_NT);
-    if (threadIdx.x == 0) out[r] = b.i;
+    b = wave_argmax(b);
+    if (b.i != 0x7fffffff && b.i >= v0 && b.i < v1 && (b.i - v0) % 64 == lane) taken |= 1u << ((b.i - v0) / 64);
+    if (lane == 0) lst[wv * PB_PMAX + r] = b;
   }
-  if (threadIdx.x == 0) out[P] = eos;
+  __syncthreads();
+  if (wv == 0) {  // (wave 0 alone: a chosen entry is retired in place)
+    const int nl = PB_NW * P;
+    int* out = cand + (long)h * (P + 1);
+    for (int r = 0; r < P; ++r) {
+      Best b{-INFINITY, 0x7fffffff};
+      int at = -1;
+      for (int q = lane; q < nl; q += 64) {
+        const Best c = lst[(q / P) * PB_PMAX + (q % P)];
+        if (c.i != 0x7fffffff && better(c.v, c.i, b.v, b.i)) {
+          b = c;
+          at = (q / P) * PB_PMAX + (q % P);
+        }
+      }
+      const Best m = wave_argmax(b);
+      if (at >= 0 && m.i == b.i) lst[at].i = 0x7fffffff;  // each token is in one list, once
+      __builtin_amdgcn_wave_barrier();
+      if (lane == 0) out[r] = m.i;
+    }
+    if (lane == 0) out[P] = eos;
+  }
 }
 
 // the new beam over the n*(P+1) candidates (duplicates of <eos> skipped).  Outputs:
@@ -152,7 +194,8 @@ __global__ __launch_bounds__(SEL_NT) void select_kernel(int n, int V, int P, int
 extern "C" int ea_beam_prebeam(int n, int V, const float* logp, long ld, float w_dec, float w_lb, int use_lb, int P,
                                int eos, int* cand, void* stream) {
   EA_ENTRY();
-  EA_CHECK_ARG(n >= 0 && V >= 1 && ld >= V && P >= 1 && P < V && V <= 32 * PB_NT && eos >= 0 && eos < V);
+  EA_CHECK_ARG(n >= 0 && V >= 1 && ld >= V && P >= 1 && P < V && P <= PB_PMAX && V <= PB_PER * PB_NT && eos >= 0 &&
+               eos < V);
   if (n == 0) return 0;
   hipLaunchKernelGGL(prebeam_kernel, dim3(n), dim3(PB_NT), 0, (hipStream_t)stream, V, logp, ld, w_dec, w_lb, use_lb, P,
                      eos, cand);

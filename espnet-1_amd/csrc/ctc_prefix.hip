@@ -123,6 +123,105 @@ __global__ __launch_bounds__(64) void ctc_prefix_score_kernel(int T, int V, int 
   log_psi[idx] = psi;
 }
 
+// The same recursion with one workgroup per hypothesis (ctc_prefix_score2): frames move through
+// LDS in chunks of CH — every thread of the block gathers the chunk's emissions of all the
+// hypothesis's candidates (logp[t][c], logp[t][blank]) and the parent's log_phi, then each
+// candidate's thread runs the serial recursion over the chunk from LDS, and the block writes
+// the candidate's forward variables back as contiguous rows.  The serial loop touches no
+// global memory (the one-thread-per-pair kernel above waited on scattered loads and stores
+// every frame); the arithmetic is the same, in the same order, so results are identical.
+template <int CH>
+__global__ __launch_bounds__(256) void ctc_prefix_score2_kernel(int T, int V, int blank, int eos, int n_cand,
+                                                                const float* __restrict__ logp,
+                                                                const unsigned long long* __restrict__ r_prev_ptr,
+                                                                const int* __restrict__ ol_arr, int ol_uniform,
+                                                                const int* __restrict__ last_arr,
+                                                                const int* __restrict__ cand_arr,
+                                                                float* __restrict__ log_psi, float* __restrict__ r_new) {
+  extern __shared__ float sm[];
+  constexpr int XS = CH + 1, RS = 2 * CH + 1;  // padded row strides (bank spread)
+  float* phi = sm;               // [CH]: lae(r^n, r^b) of the parent at frame t-1
+  float* pb = phi + CH;          // [CH]: r^b of the parent at frame t-1 (repeated label)
+  float* xb = pb + CH;           // [CH]: blank emission at frame t
+  float* xc = xb + CH;           // [n_cand][XS]: candidate emissions
+  float* ro = xc + n_cand * XS;  // [n_cand][RS]: forward variables out
+  const int h = blockIdx.x, tid = threadIdx.x;
+  const int ol = ol_arr ? ol_arr[h] : ol_uniform;
+  const int last = last_arr[h];
+  const float* rp = (const float*)r_prev_ptr[h];
+  const int* cand = cand_arr + (long)h * n_cand;
+  float* rout = r_new + (long)h * n_cand * T * 2;
+  const int start = max(ol, 1);
+  // frames before start: logzero (r[0] = (logp[c], logzero) for the empty prefix)
+  for (int q = tid; q < n_cand * 2 * min(start, T); q += 256) {
+    const int k = q / (2 * min(start, T)), e = q - k * 2 * min(start, T);
+    rout[(long)k * T * 2 + e] = (ol == 0 && e == 0) ? logp[cand[k]] : kLogZero;
+  }
+  const int k = tid;
+  const bool act = k < n_cand;
+  const int c = act ? cand[k] : 0;
+  const bool same = ol > 0 && c == last;
+  float psi = act && ol == 0 ? logp[c] : kLogZero;
+  float rn = (start - 1 < T && ol == 0 && act) ? logp[c] : kLogZero, rb = kLogZero;
+  for (int t0 = start; t0 < T; t0 += CH) {
+    const int nf = min(CH, T - t0);
+    __syncthreads();  // the previous chunk's rows are written out
+    for (int i = tid; i < nf; i += 256) {
+      const int t = t0 + i;
+      const float a = rp[2 * (t - 1)], b = rp[2 * (t - 1) + 1];
+      phi[i] = np_logaddexpf(a, b);
+      pb[i] = b;
+      xb[i] = logp[(long)t * V + blank];
+    }
+    for (int q = tid; q < n_cand * nf; q += 256) {
+      const int kk = q / nf, i = q - kk * nf;
+      xc[kk * XS + i] = logp[(long)(t0 + i) * V + cand[kk]];
+    }
+    __syncthreads();
+    if (act) {
+      const float* xk = xc + k * XS;
+      float* rk = ro + k * RS;
+      for (int i = 0; i < nf; ++i) {
+        const float ph = same ? pb[i] : phi[i];  // log_phi[t-1]
+        const float x = xk[i];
+        const float nrn = np_logaddexpf(rn, ph) + x;
+        const float nrb = np_logaddexpf(rn, rb) + xb[i];
+        psi = np_logaddexpf(psi, ph + x);
+        rn = nrn;
+        rb = nrb;
+        rk[2 * i] = rn;
+        rk[2 * i + 1] = rb;
+      }
+    }
+    __syncthreads();
+    for (int q = tid; q < n_cand * 2 * nf; q += 256) {
+      const int kk = q / (2 * nf), e = q - kk * 2 * nf;
+      rout[(long)kk * T * 2 + 2 * t0 + e] = ro[kk * RS + e];
+    }
+  }
+  if (act) {
+    if (c == eos) psi = np_logaddexpf(rp[2 * (T - 1)], rp[2 * (T - 1) + 1]);
+    if (c == blank) psi = kLogZero;
+    log_psi[(long)h * n_cand + k] = psi;
+  }
+}
+
+int launch_prefix2(int T, int V, int blank, int eos, int n_hyp, int n_cand, const float* logp,
+                   const unsigned long long* r_prev, const int* ol_arr, int ol_uniform, const int* last,
+                   const int* cand, float* log_psi, float* r_new, hipStream_t st) {
+  auto bytes = [&](int ch) { return (size_t)(3 * ch + n_cand * (ch + 1) + n_cand * (2 * ch + 1)) * 4; };
+  if (bytes(256) <= 64 * 1024)
+    hipLaunchKernelGGL(ctc_prefix_score2_kernel<256>, dim3(n_hyp), dim3(256), bytes(256), st, T, V, blank, eos, n_cand,
+                       logp, r_prev, ol_arr, ol_uniform, last, cand, log_psi, r_new);
+  else if (bytes(64) <= 64 * 1024)
+    hipLaunchKernelGGL(ctc_prefix_score2_kernel<64>, dim3(n_hyp), dim3(256), bytes(64), st, T, V, blank, eos, n_cand,
+                       logp, r_prev, ol_arr, ol_uniform, last, cand, log_psi, r_new);
+  else
+    hipLaunchKernelGGL(ctc_prefix_score_kernel, dim3(ea_cdiv(n_hyp * n_cand, 64)), dim3(64), 0, st, T, V, blank, eos,
+                       n_hyp, n_cand, logp, r_prev, ol_arr, ol_uniform, last, cand, log_psi, r_new);
+  return 0;
+}
+
 }  // namespace
 
 extern "C" int ea_ctc_prefix_init(int T, int V, const float* logits, long ld_logits, int blank, float* logp,
@@ -157,9 +256,13 @@ extern "C" int ea_ctc_prefix_score(int T, int V, int blank, int eos, int n_hyp, 
   EA_ENTRY();
   EA_CHECK_ARG(T >= 1 && V >= 1 && n_hyp >= 0 && n_cand >= 0);
   if (n_hyp * n_cand == 0) return 0;
-  hipLaunchKernelGGL(ctc_prefix_score_kernel, dim3(ea_cdiv(n_hyp * n_cand, 64)), dim3(64), 0, (hipStream_t)stream, T,
-                     V, blank, eos, n_hyp, n_cand, logp, r_prev, meta, 0, meta + n_hyp, meta + 2 * n_hyp, log_psi,
-                     r_new);
+  if (n_cand <= 256)
+    launch_prefix2(T, V, blank, eos, n_hyp, n_cand, logp, r_prev, meta, 0, meta + n_hyp, meta + 2 * n_hyp, log_psi,
+                   r_new, (hipStream_t)stream);
+  else
+    hipLaunchKernelGGL(ctc_prefix_score_kernel, dim3(ea_cdiv(n_hyp * n_cand, 64)), dim3(64), 0, (hipStream_t)stream,
+                       T, V, blank, eos, n_hyp, n_cand, logp, r_prev, meta, 0, meta + n_hyp, meta + 2 * n_hyp,
+                       log_psi, r_new);
   EA_LAUNCH_CHECK();
   return 0;
 }
@@ -170,9 +273,13 @@ extern "C" int ea_ctc_prefix_score_dev(int T, int V, int blank, int eos, int n_h
   EA_ENTRY();
   EA_CHECK_ARG(T >= 1 && V >= 1 && n_hyp >= 0 && n_cand >= 0 && out_len >= 0);
   if (n_hyp * n_cand == 0) return 0;
-  hipLaunchKernelGGL(ctc_prefix_score_kernel, dim3(ea_cdiv(n_hyp * n_cand, 64)), dim3(64), 0, (hipStream_t)stream, T,
-                     V, blank, eos, n_hyp, n_cand, logp, r_prev, (const int*)nullptr, out_len, last, cand, log_psi,
-                     r_new);
+  if (n_cand <= 256)
+    launch_prefix2(T, V, blank, eos, n_hyp, n_cand, logp, r_prev, nullptr, out_len, last, cand, log_psi, r_new,
+                   (hipStream_t)stream);
+  else
+    hipLaunchKernelGGL(ctc_prefix_score_kernel, dim3(ea_cdiv(n_hyp * n_cand, 64)), dim3(64), 0, (hipStream_t)stream,
+                       T, V, blank, eos, n_hyp, n_cand, logp, r_prev, (const int*)nullptr, out_len, last, cand,
+                       log_psi, r_new);
   EA_LAUNCH_CHECK();
   return 0;
 }

@@ -164,9 +164,11 @@ class DecodeGraphs:
         st = self.per_n.get(n) or self._setup(n)
         buf = 0 if prev is None else 1 - prev.buf
         if prev is not None:
+            # the surviving hypotheses' key/value rows of positions [0, pos) — the step writes
+            # row pos and reads no further (klen = pos + 1)
             src = self.per_n[prev.n]["kv"][prev.buf]
             idx = torch.as_tensor(rows, dtype=torch.long).to(src.device, non_blocking=True)
-            torch.index_select(src, 1, idx, out=st["kv"][buf])
+            st["kv"][buf][:, :, :pos].copy_(torch.index_select(src[:, :, :pos], 1, idx))
         st["host"][:n] = torch.as_tensor(tok, dtype=torch.long)
         st["host"][n] = pos
         st["inp"].copy_(st["host"], non_blocking=True)
