@@ -65,7 +65,8 @@ EA_DEV Best block_argmax(Best b, Best* red) {
 // <eos>; written at cand[h*(P+1) ...].  Two levels under the total order (value desc, token
 // asc): each wave takes the top P of its slice of the vocabulary (its lane values stay in
 // registers, P argmax rounds by shuffles), then wave 0 takes the top P of the waves' lists.
-constexpr int PB_NT = 1024, PB_NW = PB_NT / 64, PB_PER = 32;  // <= 32 tokens per lane: V <= 32768
+constexpr int PB_NT = 1024, PB_NW = PB_NT / 64, PB_PER = 32;  // <= 32 tokens per lane: V <= 32768 (PER
+                                                                // per instantiation: 8, 16 or 32)
 constexpr int PB_PMAX = 64;
 
 EA_DEV Best wave_argmax(Best b) {
@@ -78,15 +79,16 @@ EA_DEV Best wave_argmax(Best b) {
   return b;
 }
 
+template <int PER>
 __global__ __launch_bounds__(PB_NT) void prebeam_kernel(int V, const float* __restrict__ logp, long ld, float w_dec,
                                                         float w_lb, int use_lb, int P, int eos, int* __restrict__ cand) {
   __shared__ Best lst[PB_NW * PB_PMAX];
   const int h = blockIdx.x, lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const float* row = logp + (long)h * ld;
   const int span = (V + PB_NW - 1) / PB_NW, v0 = wv * span, v1 = min(V, v0 + span);
-  float val[PB_PER];
+  float val[PER];
 #pragma unroll
-  for (int e = 0; e < PB_PER; ++e) {
+  for (int e = 0; e < PER; ++e) {
     const int v = v0 + e * 64 + lane;
     float wvv = -INFINITY;
     if (v < v1) {
@@ -99,7 +101,7 @@ __global__ __launch_bounds__(PB_NT) void prebeam_kernel(int V, const float* __re
   for (int r = 0; r < P; ++r) {
     Best b{-INFINITY, 0x7fffffff};
 #pragma unroll
-    for (int e = 0; e < PB_PER; ++e) {
+    for (int e = 0; e < PER; ++e) {
       const int v = v0 + e * 64 + lane;
       if (v < v1 && !((taken >> e) & 1u) && better(val[e], v, b.v, b.i)) { b.v = val[e]; b.i = v; }
     }
@@ -197,8 +199,16 @@ extern "C" int ea_beam_prebeam(int n, int V, const float* logp, long ld, float w
   EA_CHECK_ARG(n >= 0 && V >= 1 && ld >= V && P >= 1 && P < V && P <= PB_PMAX && V <= PB_PER * PB_NT && eos >= 0 &&
                eos < V);
   if (n == 0) return 0;
-  hipLaunchKernelGGL(prebeam_kernel, dim3(n), dim3(PB_NT), 0, (hipStream_t)stream, V, logp, ld, w_dec, w_lb, use_lb, P,
-                     eos, cand);
+  const int per = ((V + PB_NW - 1) / PB_NW + 63) / 64;  // tokens per lane
+  if (per <= 8)
+    hipLaunchKernelGGL(prebeam_kernel<8>, dim3(n), dim3(PB_NT), 0, (hipStream_t)stream, V, logp, ld, w_dec, w_lb,
+                       use_lb, P, eos, cand);
+  else if (per <= 16)
+    hipLaunchKernelGGL(prebeam_kernel<16>, dim3(n), dim3(PB_NT), 0, (hipStream_t)stream, V, logp, ld, w_dec, w_lb,
+                       use_lb, P, eos, cand);
+  else
+    hipLaunchKernelGGL(prebeam_kernel<32>, dim3(n), dim3(PB_NT), 0, (hipStream_t)stream, V, logp, ld, w_dec, w_lb,
+                       use_lb, P, eos, cand);
   EA_LAUNCH_CHECK();
   return 0;
 }

@@ -62,6 +62,20 @@ __global__ void ctc_prefix_init_kernel(int T, int V, int blank, const float* __r
   }
 }
 
+// log(exp(x) + exp(y)) for the serial recursion of ctc_prefix_score2: npy_logaddexpf's cases
+// (x == y -> x + ln 2; NaN passes through) with the hardware exp / log (v_exp_f32 / v_log_f32,
+// ~1 ulp) instead of the libm expf / log1pf chains, and a cubic for log1p(e) at e < 1e-3 (where
+// 1 + e would round).  Deviation from float32 numpy: an ulp of the result at most per call.
+EA_DEV float fast_logaddexpf(float x, float y) {
+  if (x == y) return x + 0.693147180559945309417232121458176568f;
+  const float d = x - y;
+  if (d != d) return d;  // NaN
+  const float m = fmaxf(x, y);
+  const float e = __expf(-fabsf(d));
+  const float l = e < 1e-3f ? e * (1.f - e * (0.5f - e * 0.333333343f)) : __logf(1.f + e);
+  return m + l;
+}
+
 // one thread per (hypothesis h, candidate c): __call__ (:303-358)
 // ol_arr: per-hypothesis output lengths, or NULL when every hypothesis has ol_uniform
 __global__ __launch_bounds__(64) void ctc_prefix_score_kernel(int T, int V, int blank, int eos, int n_hyp,
@@ -129,7 +143,7 @@ __global__ __launch_bounds__(64) void ctc_prefix_score_kernel(int T, int V, int 
 // candidate's thread runs the serial recursion over the chunk from LDS, and the block writes
 // the candidate's forward variables back as contiguous rows.  The serial loop touches no
 // global memory (the one-thread-per-pair kernel above waited on scattered loads and stores
-// every frame); the arithmetic is the same, in the same order, so results are identical.
+// every frame); the recursion is the same, in the same order, with fast_logaddexpf.
 template <int CH>
 __global__ __launch_bounds__(256) void ctc_prefix_score2_kernel(int T, int V, int blank, int eos, int n_cand,
                                                                 const float* __restrict__ logp,
@@ -184,9 +198,9 @@ __global__ __launch_bounds__(256) void ctc_prefix_score2_kernel(int T, int V, in
       for (int i = 0; i < nf; ++i) {
         const float ph = same ? pb[i] : phi[i];  // log_phi[t-1]
         const float x = xk[i];
-        const float nrn = np_logaddexpf(rn, ph) + x;
-        const float nrb = np_logaddexpf(rn, rb) + xb[i];
-        psi = np_logaddexpf(psi, ph + x);
+        const float nrn = fast_logaddexpf(rn, ph) + x;
+        const float nrb = fast_logaddexpf(rn, rb) + xb[i];
+        psi = fast_logaddexpf(psi, ph + x);
         rn = nrn;
         rb = nrb;
         rk[2 * i] = rn;
