@@ -141,6 +141,11 @@ int ea_gemm_set_pipe128_slots(int slots);
  * N = 512 GEMMs at M = 7,968), 2 = such grids of any size >= 128 tiles, 3 = every eligible
  * GEMM (K % 64 == 0; tests).  Process-wide (EA_GEMM_K128). */
 int ea_gemm_set_k128(int mode, int slots);
+/* bf16 GEMMs with M <= max_m rows (K-major A and B, K % 32 == 0, unbatched: the incremental
+ * decoder's per-step Linears) on gemm_skinny — 16 x 32 output blocks whose 8 waves split K,
+ * operands loaded straight into MFMA fragments, partial tiles summed through LDS before the
+ * epilogue.  0 = off; default 16 (EA_GEMM_SKINNY).  Process-wide. */
+int ea_gemm_set_skinny(int max_m);
 
 /* One problem of a grouped launch: C[M,N] (f32, row stride ldc) = beta*C + op(A) op(B), bf16
  * operands in the layouts of ea_gemm (a_kmajor/b_kmajor shared by the group), lda/ldb

@@ -10,6 +10,7 @@ import torch
 
 sys.path.insert(0, os.path.join(os.path.dirname(__file__), "..", "..", "tests"))
 sys.path.insert(0, os.path.join(os.path.dirname(__file__), "..", ".."))
+sys.path.insert(0, os.path.join(os.path.dirname(__file__), "..", "..", "espnet-1_amd"))
 
 from goldens import is_null_grad, regenerate_sized  # noqa: E402
 from test_model_build import build  # noqa: E402

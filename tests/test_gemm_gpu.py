@@ -448,3 +448,47 @@ def test_deferred_linear_dw_queue():
             torch.testing.assert_close(d, imm, atol=1e-5 * R ** 0.5, rtol=1e-5)
     finally:
         ops.DEFER_BUDGET = budget
+
+
+@pytest.mark.parametrize("MNK", [(1, 512, 512), (10, 2048, 512), (10, 512, 2048), (16, 5000, 512), (7, 1024, 512),
+                                 (13, 30, 96), (3, 4999, 64)])
+def test_gemm_skinny_vs_fp64(MNK):
+    """gemm_skinny (M <= 16 rows: the decoder's per-step Linears; 16 x 32 blocks whose 8 waves
+    split K) against fp64 with every epilogue kind, N tails (30, 4999: element-wise epilogue)
+    and ldc wider than N; and equal to the tile kernels (ea_gemm_set_skinny(0)) within
+    accumulation-order noise."""
+    ops, L = _ops()
+    M, N, K = MNK
+    g = torch.Generator().manual_seed(M * 131 + N + K)
+    A = mk((M, K + 8), torch.bfloat16, g)
+    W = mk((N, K + 8), torch.bfloat16, g, 0.1)
+    bias = mk((N + 4,), torch.float32, g)[:N]
+    ref = ref_mm(A, W, 1, 1, M, N, K) + bias.double().cpu()
+    tol = dict(atol=2e-3 * K ** 0.5, rtol=2e-3)
+    ldc = N + 4
+    C = torch.full((M, ldc), 7.0, device="cuda")
+    ops.gemm(A, W, C, M=M, N=N, K=K, a_kmajor=1, b_kmajor=1, lda=A.stride(0), ldb=W.stride(0), ldc=ldc,
+             epi=ops.make_epi(bias=bias))
+    torch.testing.assert_close(C[:, :N].double().cpu(), ref, **tol)
+    assert (C[:, N:] == 7.0).all(), "wrote outside ldc columns"
+    L.lib.ea_gemm_set_skinny(0)
+    try:
+        C0 = torch.full((M, ldc), 7.0, device="cuda")
+        ops.gemm(A, W, C0, M=M, N=N, K=K, a_kmajor=1, b_kmajor=1, lda=A.stride(0), ldb=W.stride(0), ldc=ldc,
+                 epi=ops.make_epi(bias=bias))
+    finally:
+        L.lib.ea_gemm_set_skinny(16)
+    torch.testing.assert_close(C, C0, atol=1e-4 * K ** 0.5, rtol=1e-4)
+    # ACT (ReLU, pre-activation to aux) with bf16 outputs
+    aux = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
+    Ca = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
+    ops.gemm(A, W, Ca, M=M, N=N, K=K, a_kmajor=1, b_kmajor=1, lda=A.stride(0), ldb=W.stride(0), ldc=N,
+             epi=ops.make_epi(L.EPI_ACT, bias=bias, act=L.ACT_RELU, aux=aux))
+    torch.testing.assert_close(aux.double().cpu(), ref, atol=3e-2, rtol=2e-2)
+    torch.testing.assert_close(Ca.double().cpu(), ref.clamp_min(0), atol=3e-2, rtol=2e-2)
+    # RESID in place (f32 residual stream)
+    R = torch.randn(M, N, generator=g).cuda()
+    R0 = R.clone()
+    ops.gemm(A, W, R, M=M, N=N, K=K, a_kmajor=1, b_kmajor=1, lda=A.stride(0), ldb=W.stride(0), ldc=N,
+             epi=ops.make_epi(L.EPI_RESID, bias=bias, resid=R, rscale=1.0))
+    torch.testing.assert_close(R.double().cpu(), R0.double().cpu() + ref, **tol)
