@@ -39,13 +39,25 @@ __global__ void group_upload(GroupChunk c, GroupProbD* table, int* map) {
 
 template <bool AK, bool BKM, int NS = 4>
 __global__ __launch_bounds__(512, 1) void gemm_grouped(const GroupProbD* __restrict__ table,
-                                                       const int* __restrict__ map, int ntiles) {
+                                                       const int* __restrict__ map, int ntiles, int xchunk) {
   using PC = PipeT<256, NS>;
   __shared__ __attribute__((aligned(1024))) char smem[PC::SMEM];
   const int nt = ntiles;
   const int bid = blockIdx.x;
-  const int q8 = nt / 8, r8 = nt % 8, xcd = bid % 8;
-  const int t = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + bid / 8;
+  const int xcd = bid % 8;
+  int t;
+  if (xchunk > 0) {
+    // block bid runs on XCD bid % 8 as that XCD's (bid / 8)-th block: chunks of G consecutive
+    // tiles (neighbours sharing an A panel) go to one XCD, successive chunks round-robin over
+    // the XCDs, so every XCD walks the longest-first order at the same pace (a contiguous
+    // 1/8 range per XCD gave XCD 0 only full-K encoder tiles and XCD 7 only decoder tiles)
+    const int G = xchunk, full = nt / (8 * G) * (8 * G);
+    const int j = bid / 8;
+    t = bid < full ? ((j / G) * 8 + xcd) * G + j % G : bid;
+  } else {
+    const int q8 = nt / 8, r8 = nt % 8;
+    t = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + bid / 8;
+  }
   const GroupProbD q = table[__builtin_amdgcn_readfirstlane(map[t])];
   const int lt = t - q.tile0;
   const int tm = lt / q.tiles_n, tn = lt - tm * q.tiles_n;  // neighbours share the A panel
@@ -73,6 +85,17 @@ __global__ __launch_bounds__(512, 1) void gemm_grouped(const GroupProbD* __restr
 }
 
 }  // namespace
+
+// tile -> XCD assignment of gemm_grouped: chunks of this many consecutive tiles round-robin
+// over the XCDs (0: one contiguous range per XCD, the round-3 mapping); EA_GROUPED_XCD_CHUNK
+static int g_xcd_chunk = [] { const char* e = std::getenv("EA_GROUPED_XCD_CHUNK"); return e ? std::atoi(e) : 4; }();
+
+extern "C" int ea_gemm_grouped_set_xcd_chunk(int chunk) {
+  EA_ENTRY();
+  EA_CHECK_ARG(chunk >= 0 && chunk <= 64);
+  g_xcd_chunk = chunk;
+  return 0;
+}
 
 static long grouped_ws_bytes(int n, long ntiles) { return (long)n * (long)sizeof(GroupProbD) + 4 * ntiles + 256; }
 
@@ -126,15 +149,15 @@ extern "C" int ea_gemm_grouped(int a_kmajor, int b_kmajor, int n, const ea_group
   }
   const dim3 grid((unsigned)ntiles), block(512);
   if (eag::g_pipe_slots == 5) {
-    if (a_kmajor && b_kmajor) hipLaunchKernelGGL((gemm_grouped<true, true, 5>), grid, block, 0, st, table, map, (int)ntiles);
-    else if (a_kmajor) hipLaunchKernelGGL((gemm_grouped<true, false, 5>), grid, block, 0, st, table, map, (int)ntiles);
-    else if (b_kmajor) hipLaunchKernelGGL((gemm_grouped<false, true, 5>), grid, block, 0, st, table, map, (int)ntiles);
-    else hipLaunchKernelGGL((gemm_grouped<false, false, 5>), grid, block, 0, st, table, map, (int)ntiles);
+    if (a_kmajor && b_kmajor) hipLaunchKernelGGL((gemm_grouped<true, true, 5>), grid, block, 0, st, table, map, (int)ntiles, g_xcd_chunk);
+    else if (a_kmajor) hipLaunchKernelGGL((gemm_grouped<true, false, 5>), grid, block, 0, st, table, map, (int)ntiles, g_xcd_chunk);
+    else if (b_kmajor) hipLaunchKernelGGL((gemm_grouped<false, true, 5>), grid, block, 0, st, table, map, (int)ntiles, g_xcd_chunk);
+    else hipLaunchKernelGGL((gemm_grouped<false, false, 5>), grid, block, 0, st, table, map, (int)ntiles, g_xcd_chunk);
   } else {
-    if (a_kmajor && b_kmajor) hipLaunchKernelGGL((gemm_grouped<true, true>), grid, block, 0, st, table, map, (int)ntiles);
-    else if (a_kmajor) hipLaunchKernelGGL((gemm_grouped<true, false>), grid, block, 0, st, table, map, (int)ntiles);
-    else if (b_kmajor) hipLaunchKernelGGL((gemm_grouped<false, true>), grid, block, 0, st, table, map, (int)ntiles);
-    else hipLaunchKernelGGL((gemm_grouped<false, false>), grid, block, 0, st, table, map, (int)ntiles);
+    if (a_kmajor && b_kmajor) hipLaunchKernelGGL((gemm_grouped<true, true>), grid, block, 0, st, table, map, (int)ntiles, g_xcd_chunk);
+    else if (a_kmajor) hipLaunchKernelGGL((gemm_grouped<true, false>), grid, block, 0, st, table, map, (int)ntiles, g_xcd_chunk);
+    else if (b_kmajor) hipLaunchKernelGGL((gemm_grouped<false, true>), grid, block, 0, st, table, map, (int)ntiles, g_xcd_chunk);
+    else hipLaunchKernelGGL((gemm_grouped<false, false>), grid, block, 0, st, table, map, (int)ntiles, g_xcd_chunk);
   }
   EA_LAUNCH_CHECK();
   return 0;

@@ -170,6 +170,11 @@ int ea_gemm_grouped(int a_kmajor, int b_kmajor, int n, const ea_group_gemm* prob
                     void* stream);
 /* *bytes = workspace size ea_gemm_grouped needs for n problems with ntiles output tiles. */
 int ea_gemm_grouped_ws_bytes(int n, long ntiles, long* bytes);
+/* Tile -> XCD assignment of ea_gemm_grouped: chunks of `chunk` consecutive tiles go to one XCD
+ * and successive chunks round-robin over the 8 XCDs, so every XCD walks the longest-K-first
+ * order at the same pace (default 4, EA_GROUPED_XCD_CHUNK); 0 = one contiguous 1/8 of the
+ * tiles per XCD.  Process-wide; A/B switch. */
+int ea_gemm_grouped_set_xcd_chunk(int chunk);
 
 /* Kernel-span probe for measurement (bench.py): slots = 4 device u64
  * {span start, span end, sum of spans, count} in units of the GPU's constant 100 MHz

@@ -358,14 +358,18 @@ def test_gemm_k128_linear_paths_match_default():
     torch.testing.assert_close(y1, y0, atol=1e-3, rtol=1e-3)
 
 
-def test_gemm_grouped_vs_fp64():
+@pytest.mark.parametrize("xchunk", [4, 1, 0])
+def test_gemm_grouped_vs_fp64(xchunk):
     """ea_gemm_grouped: several (0,0)-layout f32-accumulating problems in one launch (edge
-    tiles in M and N, K remainders, beta 0 / 1, longest-K-first order) vs fp64."""
+    tiles in M and N, K remainders, beta 0 / 1, longest-K-first order) vs fp64, under each
+    tile -> XCD assignment (chunks of 4 / 1 tiles round-robin over the XCDs with the
+    remainder past the last whole round of chunks in launch order; 0 = contiguous ranges):
+    87 tiles, so every mapping has both a chunked part and a remainder."""
     ops, L = _ops()
     import ctypes
     g = torch.Generator().manual_seed(5)
     shapes = [(300, 520, 1000, 1.0), (513, 260, 64, 0.0), (40, 300, 130, 1.0), (256, 256, 7968, 1.0),
-              (1024, 512, 33, 0.0)]
+              (1024, 512, 33, 0.0), (2048, 2048, 200, 0.0)]
     probs = []
     for M, N, K, beta in sorted(shapes, key=lambda s: -s[2]):
         up = lambda n: (n + 7) // 8 * 8 + 8  # noqa: E731  (leading dims: 16-B multiples)
@@ -383,8 +387,12 @@ def test_gemm_grouped_vs_fp64():
     nb = ctypes.c_long(0)
     L.lib.ea_gemm_grouped_ws_bytes(len(probs), ntiles, ctypes.addressof(nb))
     ws = torch.empty(nb.value, dtype=torch.uint8, device="cuda")
-    L.lib.ea_gemm_grouped(0, 0, len(probs), ctypes.addressof(arr), ws.data_ptr(), ws.numel(), ops.stream())
-    torch.cuda.synchronize()
+    L.lib.ea_gemm_grouped_set_xcd_chunk(xchunk)
+    try:
+        L.lib.ea_gemm_grouped(0, 0, len(probs), ctypes.addressof(arr), ws.data_ptr(), ws.numel(), ops.stream())
+        torch.cuda.synchronize()
+    finally:
+        L.lib.ea_gemm_grouped_set_xcd_chunk(4)
     for A, B, C, C0, M, N, K, beta in probs:
         ref = beta * C0[:, :N].double().cpu() + ref_mm(A, B, 0, 0, M, N, K)
         torch.testing.assert_close(C[:, :N].double().cpu(), ref, atol=2e-3 * K ** 0.5, rtol=2e-3)
