@@ -49,6 +49,19 @@ def c3_config():
     )
 
 
+def _diag_dropout(cfg):
+    """EA_BENCH_DIAG_DROPOUT=x: every dropout rate set to x — a diagnostic A/B of what the
+    dropout costs (the bench line then names the rate in `config`; never the reported run)."""
+    x = os.environ.get("EA_BENCH_DIAG_DROPOUT")
+    if x is None:
+        return cfg
+    for k in ("encoder_conf", "decoder_conf"):
+        for kk in list(cfg[k]):
+            if "dropout_rate" in kk:
+                cfg[k][kk] = float(x)
+    return cfg
+
+
 def c2_config():
     c = c3_config()
     c.update(B=16, T=500, L=20, decoder=None, gflop_per_step=282.8)
@@ -233,7 +246,7 @@ def main():
 
     if args.config == "c5":
         return run_c5(args, world, rank, dev)
-    cfg = c3_config() if args.config == "c3" else c2_config()
+    cfg = _diag_dropout(c3_config() if args.config == "c3" else c2_config())
     amp = not args.fp32
     model = build(cfg)
     model.prepare(dev, amp=amp, seed=1234)
@@ -327,7 +340,9 @@ def main():
                 "hybrid CTC/att 0.3/0.7, lsm 0.1, V=5000, T=1000 frames x 80, L=40, dropout 0.1, "
                 "Adam+WarmupLR+clip 5" if args.config == "c3" else
                 "Conformer-S (6x256, 4 heads, ff 1024), CTC only, V=5000, T=500, L=20"),
-                "global_batch": B * world, "seq_len": T, "parallelism": f"dp{world}"},
+                "global_batch": B * world, "seq_len": T, "parallelism": f"dp{world}",
+                **({"diag_dropout": float(os.environ["EA_BENCH_DIAG_DROPOUT"])}
+                   if "EA_BENCH_DIAG_DROPOUT" in os.environ else {})},
             "model_tflops_per_s": round(cfg["gflop_per_step"] * world / (ms * 1e-3) / 1e3, 2),
             "roofline": {"bound": "mfma", "kernel": ("gemm_pipe" if GEMM_PIPE else "gemm_bf16_lds") +
                          f" bf16 conv2 implicit GEMM (subsampling forward, M={B * T2 * F2} N={C} K={9 * C})",

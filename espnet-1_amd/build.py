@@ -59,7 +59,9 @@ def build(jobs: int = 8, force: bool = False, verbose: bool = True) -> str:
         raise RuntimeError("HIP compile failed:\n" + "\n".join(errs))
     objs = [o for o, _ in results]
     if force or _stale(LIB, objs):
-        cmd = [HIPCC, "-shared", f"--offload-arch={ARCH}", "-o", LIB, *objs]
+        # hipBLASLt (plain bf16 GEMMs, csrc/blaslt.hip); in a torch process the loader binds the
+        # libhipblaslt.so.1 torch already loaded
+        cmd = [HIPCC, "-shared", f"--offload-arch={ARCH}", "-o", LIB, *objs, "-L/opt/rocm/lib", "-lhipblaslt"]
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError(f"link failed:\n{r.stdout}\n{r.stderr}")

@@ -24,8 +24,18 @@ __global__ void splitk_reduce(GemmP p) {
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n4; i += (long)gridDim.x * blockDim.x) {
     if (vec) {
       float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
-      for (int s = 0; s < p.splitk; ++s) {
-        const float4 b = *(const float4*)(base + s * MN + i * 4);
+      int s = 0;
+      // 8 slab loads in flight per thread (the combine is latency-bound: a 512 x 64 output
+      // is 32 K float4s over 12 slabs), summed in slab order as before
+      for (; s + 8 <= p.splitk; s += 8) {
+        float4 b[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) b[j] = *(const float4*)(base + (long)(s + j) * MN + i * 4);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) { a.x += b[j].x; a.y += b[j].y; a.z += b[j].z; a.w += b[j].w; }
+      }
+      for (; s < p.splitk; ++s) {
+        const float4 b = *(const float4*)(base + (long)s * MN + i * 4);
         a.x += b.x; a.y += b.y; a.z += b.z; a.w += b.w;
       }
       const int row = (int)(i * 4 / p.N), col = (int)(i * 4 % p.N);
@@ -239,6 +249,9 @@ extern "C" int ea_gemm_set_tile(int bm, int bn) {
   return 0;
 }
 
+int ea_blaslt_try(int a_kmajor, int b_kmajor, int M, int N, int K, const void* A, long lda, const void* B, long ldb,
+                  void* C, int c_dtype, long ldc, float alpha, float beta, hipStream_t st);  // blaslt.hip
+
 static int gemm_impl(int dtype, int a_kmajor, int b_kmajor, int M, int N, int K,
                      const void* A, long lda, long sAb, long sAh,
                      const void* B, long ldb, long sBb, long sBh,
@@ -291,6 +304,12 @@ static int gemm_impl(int dtype, int a_kmajor, int b_kmajor, int M, int N, int K,
     if (trace_s) std::fprintf(stderr, "[ea_gemm] M=%d N=%d K=%d skinny epi=%d\n", M, N, K, (int)epi->kind);
     return launch_skinny(p, (hipStream_t)stream);
   }
+  // plain products (no bias / scale / dropout / activation) on hipBLASLt where enabled
+  if (dtype == EA_BF16 && !geo && !w1part && batch * nh == 1 && epi->kind == EA_EPI_STORE && !epi->bias &&
+      epi->post_scale == 1.f && epi->drop_p <= 0.f &&
+      ea_blaslt_try(a_kmajor, b_kmajor, M, N, K, A, lda, B, ldb, C, c_dtype, ldc, epi->alpha, epi->beta,
+                    (hipStream_t)stream) == 0)
+    return 0;
   // operand extent per batch slice (bytes) must fit the kernel's 32-bit source offsets
   const double a_ext = 2.0 * ((a_kmajor ? (double)M : (double)K) * lda);
   const double b_ext = 2.0 * ((b_kmajor ? (double)N : (double)K) * ldb);

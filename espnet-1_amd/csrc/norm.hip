@@ -805,9 +805,14 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_vec_kernel(int rows, int C, 
                                                                const float* __restrict__ b, int act,
                                                                const float* __restrict__ dgamma,
                                                                const float* __restrict__ dbeta,
-                                                               float* __restrict__ dy) {
+                                                               float* __restrict__ dy,
+                                                               float* __restrict__ pgrad, int acc_params) {
   const float invn = 1.f / rows;
   const int c4 = C / 4;
+  // the parameter gradients (gamma | beta, adjacent) (+)= the batch sums (dgamma | dbeta
+  // adjacent in `sums`), from block 0 instead of a separate reduce launch
+  if (pgrad != nullptr && blockIdx.x == 0)
+    for (int c = threadIdx.x; c < 2 * C; c += blockDim.x) pgrad[c] = acc_params ? pgrad[c] + dgamma[c] : dgamma[c];
   const long total4 = (long)rows * c4;
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total4; i += (long)gridDim.x * blockDim.x) {
     const int c = (int)(i % c4) * 4;
@@ -1203,9 +1208,11 @@ extern "C" int ea_batchnorm_bwd(int rows, int C, const void* dz, int dz_dtype, c
   if (vec) {
     dim3 g4(ea_grid_cap(ea_cdiv(total / 4, 256)));
     if (dz_dtype == EA_BF16)
-      hipLaunchKernelGGL(bn_bwd_apply_vec_kernel<bf16>, g4, dim3(256), 0, st, rows, C, (const bf16*)dz, y, mean, rstd, gamma, beta, act, sums, sums + C, dy);
+      hipLaunchKernelGGL(bn_bwd_apply_vec_kernel<bf16>, g4, dim3(256), 0, st, rows, C, (const bf16*)dz, y, mean, rstd, gamma, beta, act, sums, sums + C, dy, dgamma, accumulate_params);
     else
-      hipLaunchKernelGGL(bn_bwd_apply_vec_kernel<float>, g4, dim3(256), 0, st, rows, C, (const float*)dz, y, mean, rstd, gamma, beta, act, sums, sums + C, dy);
+      hipLaunchKernelGGL(bn_bwd_apply_vec_kernel<float>, g4, dim3(256), 0, st, rows, C, (const float*)dz, y, mean, rstd, gamma, beta, act, sums, sums + C, dy, dgamma, accumulate_params);
+    EA_LAUNCH_CHECK();
+    return 0;
   } else if (dz_dtype == EA_BF16)
     hipLaunchKernelGGL(bn_bwd_apply_kernel<bf16>, g2, dim3(256), 0, st, total, C, rows, (const bf16*)dz, y, mean, rstd, gamma, beta, act, sums, sums + C, dy);
   else

@@ -146,6 +146,11 @@ int ea_gemm_set_k128(int mode, int slots);
  * operands loaded straight into MFMA fragments, partial tiles summed through LDS before the
  * epilogue.  0 = off; default 16 (EA_GEMM_SKINNY).  Process-wide. */
 int ea_gemm_set_skinny(int max_m);
+/* Plain bf16 GEMMs (STORE epilogue without bias, scale or dropout; alpha / beta honoured;
+ * unbatched; M >= 1024) on hipBLASLt: mode bit 1 = N <= 512, bit 2 = N > 512; 0 = off
+ * (EA_GEMM_BLASLT; default 1).  Shapes hipBLASLt has no workspace-free algorithm for stay on ea_gemm's
+ * own kernels.  Process-wide. */
+int ea_gemm_set_blaslt(int mode);
 
 /* One problem of a grouped launch: C[M,N] (f32, row stride ldc) = beta*C + op(A) op(B), bf16
  * operands in the layouts of ea_gemm (a_kmajor/b_kmajor shared by the group), lda/ldb

@@ -500,3 +500,38 @@ def test_gemm_skinny_vs_fp64(MNK):
     ops.gemm(A, W, R, M=M, N=N, K=K, a_kmajor=1, b_kmajor=1, lda=A.stride(0), ldb=W.stride(0), ldc=N,
              epi=ops.make_epi(L.EPI_RESID, bias=bias, resid=R, rscale=1.0))
     torch.testing.assert_close(R.double().cpu(), R0.double().cpu() + ref, **tol)
+
+
+@pytest.mark.parametrize("a_k,b_k", [(1, 1), (1, 0), (0, 1)])
+@pytest.mark.parametrize("MNK", [(7968, 512, 2048), (2000, 1536, 512), (1100, 200, 72)])
+@pytest.mark.parametrize("out", [torch.bfloat16, torch.float32])
+def test_gemm_blaslt_plain_vs_fp64(a_k, b_k, MNK, out):
+    """ea_gemm_set_blaslt(3): plain products (alpha / beta, no other epilogue) on hipBLASLt with
+    every operand layout the host mirror issues, bf16 and f32 outputs, ldc wider than N; the
+    same call with a bias stays on the MFMA kernels — both against fp64."""
+    ops, L = _ops()
+    M, N, K = MNK
+    g = torch.Generator().manual_seed(M + N + K + a_k * 2 + b_k)
+    up = lambda n: (n + 7) // 8 * 8 + 8  # noqa: E731
+    A = mk((M, up(K)) if a_k else (K, up(M)), torch.bfloat16, g)
+    B = mk((N, up(K)) if b_k else (K, up(N)), torch.bfloat16, g, 0.1)
+    ref = ref_mm(A, B, a_k, b_k, M, N, K)
+    tol = dict(atol=2e-3 * K ** 0.5, rtol=2e-2 if out == torch.bfloat16 else 2e-3)
+    L.lib.ea_gemm_set_blaslt(3)
+    try:
+        C = torch.full((M, N + 8), 7.0, device="cuda", dtype=out)
+        ops.gemm(A, B, C, M=M, N=N, K=K, a_kmajor=a_k, b_kmajor=b_k, lda=A.stride(0), ldb=B.stride(0),
+                 ldc=C.stride(0), epi=ops.make_epi(alpha=0.5))
+        torch.testing.assert_close(C[:, :N].double().cpu(), 0.5 * ref, **tol)
+        assert (C[:, N:] == 7.0).all(), "wrote outside ldc columns"
+        C0 = C.clone()
+        ops.gemm(A, B, C, M=M, N=N, K=K, a_kmajor=a_k, b_kmajor=b_k, lda=A.stride(0), ldb=B.stride(0),
+                 ldc=C.stride(0), epi=ops.make_epi(beta=1.0))
+        torch.testing.assert_close(C[:, :N].double().cpu(), C0[:, :N].double().cpu() + ref, **tol)
+        bias = mk((N,), torch.float32, g)
+        Cb = torch.empty(M, N, device="cuda", dtype=out)
+        ops.gemm(A, B, Cb, M=M, N=N, K=K, a_kmajor=a_k, b_kmajor=b_k, lda=A.stride(0), ldb=B.stride(0), ldc=N,
+                 epi=ops.make_epi(bias=bias))
+        torch.testing.assert_close(Cb.double().cpu(), ref + bias.double().cpu(), **tol)
+    finally:
+        L.lib.ea_gemm_set_blaslt(0)
