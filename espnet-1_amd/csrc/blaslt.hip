@@ -68,8 +68,8 @@ LtPlan build_plan(int a_kmajor, int b_kmajor, int M, int N, int K, long lda, lon
 
 }  // namespace
 
-// bit 1: plain GEMMs with N <= 512 and M >= 1024 (the L2-feed-bound family); bit 2: every other
-// plain GEMM with M >= 1024; 0 = off (EA_GEMM_BLASLT).  Default 1: C3 step 1775-1776 ->
+// bit 1: plain GEMMs with N <= 512 and M >= 4096 (the L2-feed-bound family); bit 2: every other
+// plain GEMM with M >= 4096; 0 = off (EA_GEMM_BLASLT).  Default 1: C3 step 1775-1776 ->
 // 1787-1790 utt/s (mode 3: 1784-1787), profiles/r4_blaslt_ab.txt
 int g_gemm_blaslt = [] { const char* e = std::getenv("EA_GEMM_BLASLT"); return e ? std::atoi(e) : 1; }();
 
@@ -83,7 +83,9 @@ extern "C" int ea_gemm_set_blaslt(int mode) {
 // 0: launched on hipBLASLt; 1: not eligible / no algorithm (the caller runs its own kernels)
 int ea_blaslt_try(int a_kmajor, int b_kmajor, int M, int N, int K, const void* A, long lda, const void* B, long ldb,
                   void* C, int c_dtype, long ldc, float alpha, float beta, hipStream_t st) {
-  if (!g_gemm_blaslt || M < 1024 || K < 64) return 1;
+  // M >= 4096: at the decoder's 1,312 tokens hipBLASLt is slower than the tile kernels
+  // (1312x512x512: 21.4 vs 11.6 us, 1312x512x2048: 17.4 vs 15.6 us; scripts/gemm_rows_ab.py)
+  if (!g_gemm_blaslt || M < 4096 || K < 64) return 1;
   if (!((N <= 512 && (g_gemm_blaslt & 1)) || (N > 512 && (g_gemm_blaslt & 2)))) return 1;
   const LtKey key{a_kmajor, b_kmajor, M, N, K, lda, ldb, ldc, c_dtype};
   LtPlan* p;

@@ -64,6 +64,8 @@ int g_gemm_pipe = 0;  // ea_gemm_set_pipe bits: 1 = 256x256 tiles on gemm_pipe, 
 int g_gemm_k128 = [] { const char* e = std::getenv("EA_GEMM_K128"); return e ? std::atoi(e) : 0; }();
 // few-row GEMMs (M <= g_gemm_skinny) on gemm_skinny (ea_gemm_set_skinny; 0 = off)
 int g_gemm_skinny = [] { const char* e = std::getenv("EA_GEMM_SKINNY"); return e ? std::atoi(e) : 16; }();
+// ... and the 32-row variant for M up to g_gemm_rows32 (ea_gemm_set_rows32; 0 = off)
+int g_gemm_rows32 = [] { const char* e = std::getenv("EA_GEMM_ROWS32"); return e ? std::atoi(e) : 0; }();
 
 int launch_lds(GemmP& p, int a_k, int b_k, int nz, hipStream_t st, bool pipe128 = false, bool k128 = false) {
   dim3 grid(p.tiles_m * p.tiles_n, 1, nz * p.splitk);
@@ -233,6 +235,13 @@ extern "C" int ea_gemm_set_skinny(int max_m) {
   return 0;
 }
 
+extern "C" int ea_gemm_set_rows32(int max_m) {
+  EA_ENTRY();
+  EA_CHECK_ARG(max_m >= 0);
+  g_gemm_rows32 = max_m;
+  return 0;
+}
+
 extern "C" int ea_gemm_set_pipe128_slots(int slots) {
   EA_ENTRY();
   EA_CHECK_ARG(slots == 4 || slots == 6 || slots == 8);
@@ -298,11 +307,11 @@ static int gemm_impl(int dtype, int a_kmajor, int b_kmajor, int M, int N, int K,
   p.bm = 128; p.bn = 128;
   // few rows (decoder steps): K split over the waves of a 16 x 32 block instead of a tile
   // walking all of K (gemm_skinny.hip)
-  if (dtype == EA_BF16 && M <= g_gemm_skinny && a_kmajor && b_kmajor && !geo && !w1part && batch * nh == 1 &&
-      K % 32 == 0 && K > 0 && p.vec_a && p.vec_b) {
+  if (dtype == EA_BF16 && (M <= g_gemm_skinny || M <= g_gemm_rows32) && a_kmajor && b_kmajor && !geo && !w1part &&
+      batch * nh == 1 && K % 32 == 0 && K > 0 && p.vec_a && p.vec_b) {
     static const bool trace_s = std::getenv("EA_GEMM_TRACE") != nullptr;
     if (trace_s) std::fprintf(stderr, "[ea_gemm] M=%d N=%d K=%d skinny epi=%d\n", M, N, K, (int)epi->kind);
-    return launch_skinny(p, (hipStream_t)stream);
+    return launch_skinny(p, (hipStream_t)stream, M > g_gemm_skinny);
   }
   // plain products (no bias / scale / dropout / activation) on hipBLASLt where enabled
   if (dtype == EA_BF16 && !geo && !w1part && batch * nh == 1 && epi->kind == EA_EPI_STORE && !epi->bias &&

@@ -4,7 +4,7 @@
 //
 // The tile kernels give such a GEMM ceil(N / 128) blocks that each walk the whole K serially
 // (a 2048-deep K at N = 512 is 4 blocks), so the launch is one HBM round trip per K slice.
-// Here a block owns 16 rows x 32 columns and its 8 waves split K among themselves (wave w
+// Here a block owns 16 (or 32) rows x 32 columns and its 8 waves split K among themselves (wave w
 // takes the 32-deep slices w, w + 8, ...), each wave issuing the loads of up to 8 slices before
 // its first MFMA: both operands go global -> registers in MFMA fragment order (16-B loads, no
 // LDS staging — W is read exactly once per 16-row block and A is a few KB), so a launch costs
@@ -15,11 +15,7 @@
 namespace {
 using namespace eag;
 
-constexpr int SK_W = 8;   // waves per block (K split)
-constexpr int SK_U = 8;   // 32-deep slices per wave with loads in flight together
-constexpr int SK_NJ = 2;  // 16-column MFMA tiles per block
-constexpr int SK_BN = 16 * SK_NJ;
-constexpr int SK_LD = SK_BN + 4;  // floats per LDS row of a wave's partial tile
+constexpr int SK_W = 8;  // waves per block (K split)
 
 template <int KIND>
 EA_DEV void skinny_epi(const GemmP& p, const EpiK& ek, int row, int col, const float (&v)[4]) {
@@ -33,55 +29,71 @@ EA_DEV void skinny_epi(const GemmP& p, const EpiK& ek, int row, int col, const f
   }
 }
 
+// MT 16-row x NJ 16-column MFMA tiles per block; U 32-deep slices per wave with loads in flight
+template <int MT, int NJ, int U>
 __global__ __launch_bounds__(64 * SK_W) void gemm_skinny_kernel(GemmP p) {
-  __shared__ __attribute__((aligned(16))) float red[SK_W][16][SK_LD];
+  constexpr int BR = 16 * MT, BC = 16 * NJ, LD = BC + 4;
+  __shared__ __attribute__((aligned(16))) float red[SK_W][BR][LD];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int r0 = blockIdx.y * 16, c0 = blockIdx.x * SK_BN;
+  const int r0 = blockIdx.y * BR, c0 = blockIdx.x * BC;
   const bf16* __restrict__ A = (const bf16*)p.A;
   const bf16* __restrict__ B = (const bf16*)p.B;
   const int nks = p.K / 32;
   const int kq = 8 * (lane >> 4);
-  const int arow = r0 + (lane & 15);
-  const bool aok = arow < p.M;
-  const bf16* ap = A + (long)(aok ? arow : 0) * p.lda + kq;
-  const bf16* bp[SK_NJ];
-  bool bok[SK_NJ];
+  const bf16* ap[MT];
+  bool aok[MT];
 #pragma unroll
-  for (int j = 0; j < SK_NJ; ++j) {
+  for (int i = 0; i < MT; ++i) {
+    const int row = r0 + i * 16 + (lane & 15);
+    aok[i] = row < p.M;
+    ap[i] = A + (long)(aok[i] ? row : 0) * p.lda + kq;
+  }
+  const bf16* bp[NJ];
+  bool bok[NJ];
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) {
     const int col = c0 + j * 16 + (lane & 15);
     bok[j] = col < p.N;
     bp[j] = B + (long)(bok[j] ? col : 0) * p.ldb + kq;
   }
-  f32x4 acc[SK_NJ];
+  f32x4 acc[MT][NJ];
 #pragma unroll
-  for (int j = 0; j < SK_NJ; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int i = 0; i < MT; ++i)
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   const bf16x8 zero = {};
-  for (int ks0 = w; ks0 < nks; ks0 += SK_W * SK_U) {
-    bf16x8 a[SK_U], b[SK_U][SK_NJ];
+  for (int ks0 = w; ks0 < nks; ks0 += SK_W * U) {
+    bf16x8 a[U][MT], b[U][NJ];
 #pragma unroll
-    for (int u = 0; u < SK_U; ++u) {
+    for (int u = 0; u < U; ++u) {
       const int ks = ks0 + u * SK_W;
       const bool in = ks < nks;
-      a[u] = in && aok ? *(const bf16x8*)(ap + ks * 32) : zero;
 #pragma unroll
-      for (int j = 0; j < SK_NJ; ++j) b[u][j] = in && bok[j] ? *(const bf16x8*)(bp[j] + ks * 32) : zero;
+      for (int i = 0; i < MT; ++i) a[u][i] = in && aok[i] ? *(const bf16x8*)(ap[i] + ks * 32) : zero;
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) b[u][j] = in && bok[j] ? *(const bf16x8*)(bp[j] + ks * 32) : zero;
     }
 #pragma unroll
-    for (int u = 0; u < SK_U; ++u)
+    for (int u = 0; u < U; ++u)
 #pragma unroll
-      for (int j = 0; j < SK_NJ; ++j) acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[u], b[u][j], acc[j], 0, 0, 0);
+      for (int i = 0; i < MT; ++i)
+#pragma unroll
+        for (int j = 0; j < NJ; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[u][i], b[u][j], acc[i][j], 0, 0, 0);
   }
   // partial tiles -> LDS (D layout: lane holds rows 4*(lane>>4)+r of column lane&15)
 #pragma unroll
-  for (int j = 0; j < SK_NJ; ++j)
+  for (int i = 0; i < MT; ++i)
 #pragma unroll
-    for (int r = 0; r < 4; ++r) red[w][4 * (lane >> 4) + r][j * 16 + (lane & 15)] = acc[j][r];
+    for (int j = 0; j < NJ; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) red[w][i * 16 + 4 * (lane >> 4) + r][j * 16 + (lane & 15)] = acc[i][j][r];
   __syncthreads();
-  constexpr int GROUPS = 16 * SK_BN / 4;  // 4-column output groups of the block
-  if (threadIdx.x >= GROUPS) return;
-  const int row = threadIdx.x / (SK_BN / 4), cg = (threadIdx.x % (SK_BN / 4)) * 4;
-  float v[4];
-  {
+  constexpr int GROUPS = BR * BC / 4;  // 4-column output groups of the block
+  const EpiK ek = make_epik(p);
+  for (int gi = threadIdx.x; gi < GROUPS; gi += 64 * SK_W) {
+    const int row = gi / (BC / 4), cg = (gi % (BC / 4)) * 4;
+    float v[4];
     float4 s = *(const float4*)&red[0][row][cg];
 #pragma unroll
     for (int q = 1; q < SK_W; ++q) {
@@ -89,22 +101,26 @@ __global__ __launch_bounds__(64 * SK_W) void gemm_skinny_kernel(GemmP p) {
       s.x += t.x; s.y += t.y; s.z += t.z; s.w += t.w;
     }
     v[0] = s.x; v[1] = s.y; v[2] = s.z; v[3] = s.w;
-  }
-  const EpiK ek = make_epik(p);
-  switch (p.epi.kind) {
-    case EA_EPI_STORE: skinny_epi<EA_EPI_STORE>(p, ek, r0 + row, c0 + cg, v); break;
-    case EA_EPI_ACT: skinny_epi<EA_EPI_ACT>(p, ek, r0 + row, c0 + cg, v); break;
-    case EA_EPI_RESID: skinny_epi<EA_EPI_RESID>(p, ek, r0 + row, c0 + cg, v); break;
-    default: skinny_epi<EA_EPI_DACT>(p, ek, r0 + row, c0 + cg, v); break;
+    switch (p.epi.kind) {
+      case EA_EPI_STORE: skinny_epi<EA_EPI_STORE>(p, ek, r0 + row, c0 + cg, v); break;
+      case EA_EPI_ACT: skinny_epi<EA_EPI_ACT>(p, ek, r0 + row, c0 + cg, v); break;
+      case EA_EPI_RESID: skinny_epi<EA_EPI_RESID>(p, ek, r0 + row, c0 + cg, v); break;
+      default: skinny_epi<EA_EPI_DACT>(p, ek, r0 + row, c0 + cg, v); break;
+    }
   }
 }
 
 }  // namespace
 
 namespace eag {
-int launch_skinny(GemmP& p, hipStream_t st) {
-  dim3 grid(ea_cdiv(p.N, SK_BN), ea_cdiv(p.M, 16), 1);
-  hipLaunchKernelGGL(gemm_skinny_kernel, grid, dim3(64 * SK_W), 0, st, p);
+int launch_skinny(GemmP& p, hipStream_t st, int rows32) {
+  if (rows32) {  // 32 x 32 blocks (M beyond a few 16-row blocks: the decoder's 1,312 tokens)
+    dim3 grid(ea_cdiv(p.N, 32), ea_cdiv(p.M, 32), 1);
+    hipLaunchKernelGGL((gemm_skinny_kernel<2, 2, 4>), grid, dim3(64 * SK_W), 0, st, p);
+  } else {
+    dim3 grid(ea_cdiv(p.N, 32), ea_cdiv(p.M, 16), 1);
+    hipLaunchKernelGGL((gemm_skinny_kernel<1, 2, 8>), grid, dim3(64 * SK_W), 0, st, p);
+  }
   EA_LAUNCH_CHECK();
   return 0;
 }

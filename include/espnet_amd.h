@@ -146,8 +146,12 @@ int ea_gemm_set_k128(int mode, int slots);
  * operands loaded straight into MFMA fragments, partial tiles summed through LDS before the
  * epilogue.  0 = off; default 16 (EA_GEMM_SKINNY).  Process-wide. */
 int ea_gemm_set_skinny(int max_m);
+/* The same K-split kernel with 32 x 32 output blocks for bf16 GEMMs with M <= max_m rows beyond
+ * the few-row limit (the training decoder's B*(L+1) tokens); 0 = off (EA_GEMM_ROWS32).
+ * Process-wide; A/B switch. */
+int ea_gemm_set_rows32(int max_m);
 /* Plain bf16 GEMMs (STORE epilogue without bias, scale or dropout; alpha / beta honoured;
- * unbatched; M >= 1024) on hipBLASLt: mode bit 1 = N <= 512, bit 2 = N > 512; 0 = off
+ * unbatched; M >= 4096) on hipBLASLt: mode bit 1 = N <= 512, bit 2 = N > 512; 0 = off
  * (EA_GEMM_BLASLT; default 1).  Shapes hipBLASLt has no workspace-free algorithm for stay on ea_gemm's
  * own kernels.  Process-wide. */
 int ea_gemm_set_blaslt(int mode);

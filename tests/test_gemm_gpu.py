@@ -503,7 +503,7 @@ def test_gemm_skinny_vs_fp64(MNK):
 
 
 @pytest.mark.parametrize("a_k,b_k", [(1, 1), (1, 0), (0, 1)])
-@pytest.mark.parametrize("MNK", [(7968, 512, 2048), (2000, 1536, 512), (1100, 200, 72)])
+@pytest.mark.parametrize("MNK", [(7968, 512, 2048), (4100, 1536, 512), (4096, 200, 72)])
 @pytest.mark.parametrize("out", [torch.bfloat16, torch.float32])
 def test_gemm_blaslt_plain_vs_fp64(a_k, b_k, MNK, out):
     """ea_gemm_set_blaslt(3): plain products (alpha / beta, no other epilogue) on hipBLASLt with
@@ -535,3 +535,33 @@ def test_gemm_blaslt_plain_vs_fp64(a_k, b_k, MNK, out):
         torch.testing.assert_close(Cb.double().cpu(), ref + bias.double().cpu(), **tol)
     finally:
         L.lib.ea_gemm_set_blaslt(0)
+
+
+@pytest.mark.parametrize("MNK", [(1312, 512, 512), (1312, 2048, 512), (1312, 512, 2048), (100, 1536, 96),
+                                 (37, 4999, 64)])
+def test_gemm_rows32_vs_fp64(MNK):
+    """ea_gemm_set_rows32: the K-split kernel's 32 x 32 blocks at the training decoder's token
+    count (M = 1,312) and ragged M / N tails, with the RESID and ACT epilogues, vs fp64."""
+    ops, L = _ops()
+    M, N, K = MNK
+    g = torch.Generator().manual_seed(M * 7 + N + K)
+    A = mk((M, K + 8), torch.bfloat16, g)
+    W = mk((N, K + 8), torch.bfloat16, g, 0.1)
+    bias = mk((N + 4,), torch.float32, g)[:N]
+    ref = ref_mm(A, W, 1, 1, M, N, K) + bias.double().cpu()
+    tol = dict(atol=2e-3 * K ** 0.5, rtol=2e-3)
+    L.lib.ea_gemm_set_rows32(4096)
+    try:
+        R = torch.randn(M, N, generator=g).cuda()
+        R0 = R.clone()
+        ops.gemm(A, W, R, M=M, N=N, K=K, a_kmajor=1, b_kmajor=1, lda=A.stride(0), ldb=W.stride(0), ldc=N,
+                 epi=ops.make_epi(L.EPI_RESID, bias=bias, resid=R, rscale=1.0))
+        torch.testing.assert_close(R.double().cpu(), R0.double().cpu() + ref, **tol)
+        aux = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
+        Ca = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
+        ops.gemm(A, W, Ca, M=M, N=N, K=K, a_kmajor=1, b_kmajor=1, lda=A.stride(0), ldb=W.stride(0), ldc=N,
+                 epi=ops.make_epi(L.EPI_ACT, bias=bias, act=L.ACT_RELU, aux=aux))
+        torch.testing.assert_close(aux.double().cpu(), ref, atol=3e-2, rtol=2e-2)
+        torch.testing.assert_close(Ca.double().cpu(), ref.clamp_min(0), atol=3e-2, rtol=2e-2)
+    finally:
+        L.lib.ea_gemm_set_rows32(0)
