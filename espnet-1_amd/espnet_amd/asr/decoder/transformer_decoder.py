@@ -119,14 +119,15 @@ class DecodeGraphs:
             nm = f"decoders.{l}."
             sa, xa, ff = nm + "self_attn.", nm + "src_attn.", nm + "feed_forward."
             xn1, _, _ = ln_fwd(x, b, nm + "norm1", cd)
-            q = empty(n, d, dtype=cd, device=dev)
-            ops.linear(xn1, b.w(sa + "linear_q.weight"), q, epi=ops.make_epi(bias=b.f(sa + "linear_q.bias")))
-            row = empty(n, 2 * d, dtype=cd, device=dev)
-            ops.linear(xn1, b.w(sa + "linear_k.weight", sa + "linear_v.weight", shape=(2 * d, d)), row,
-                       epi=ops.make_epi(bias=b.f(sa + "linear_k.bias", sa + "linear_v.bias", shape=(2 * d,))))
+            # q | k | v in one GEMM (adjacent in the arena); k | v of this position go to the cache
+            qkv = empty(n, 3 * d, dtype=cd, device=dev)
+            ops.linear(xn1, b.w(sa + "linear_q.weight", sa + "linear_k.weight", sa + "linear_v.weight",
+                                shape=(3 * d, d)), qkv,
+                       epi=ops.make_epi(bias=b.f(sa + "linear_q.bias", sa + "linear_k.bias", sa + "linear_v.bias",
+                                                 shape=(3 * d,))))
             kvl = kv[l]
-            kvl.index_copy_(1, pos, row.view(n, 1, 2 * d))
-            O1, _ = _mha_fwd(q, kvl, kvl[:, :, d:], B=n, H=H, T1=1, T2=self.lcap, dk=dk, ldq=d, ldk=2 * d,
+            kvl.index_copy_(1, pos, qkv[:, d:].view(n, 1, 2 * d))
+            O1, _ = _mha_fwd(qkv, kvl, kvl[:, :, d:], B=n, H=H, T1=1, T2=self.lcap, dk=dk, ldq=3 * d, ldk=2 * d,
                              ldv=2 * d, klen=klen, causal=False, scale=scale, p=0.0, seed=0, cd=cd)
             x1 = empty(n, d, device=dev)
             ops.linear(O1, b.w(sa + "linear_out.weight"), x1,
@@ -176,7 +177,7 @@ class DecodeGraphs:
             self._body(st, n, buf)  # eager warm-up (lazy workspaces), then capture
             torch.cuda.synchronize()
             g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g, pool=st["pool"]):
+            with torch.cuda.graph(g, pool=st["pool"], capture_error_mode="thread_local"):
                 st["out"][buf] = self._body(st, n, buf)
             st["pool"] = g.pool()
             st["graphs"][buf] = g

@@ -197,7 +197,9 @@ class CapturedTrainStep:
         cap.maxlens = maxlens
         g = torch.cuda.CUDAGraph()
         torch.cuda.synchronize()
-        with torch.cuda.graph(g, pool=self._pool):
+        # thread-local capture mode: other threads' HIP calls during the capture (RCCL's
+        # process-group watchdog polls its events) must not invalidate it or fail themselves
+        with torch.cuda.graph(g, pool=self._pool, capture_error_mode="thread_local"):
             out = self._eager(cap.inputs, maxlens)
         if self._pool is None:
             self._pool = g.pool()
