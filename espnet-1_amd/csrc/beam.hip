@@ -32,35 +32,6 @@ EA_DEV bool better(float av, int ai, float bv, int bi) {
   return av > bv || (av == bv && ai < bi) || (bv != bv && av == av);  // NaN loses
 }
 
-template <int NT>
-EA_DEV Best block_argmax(Best b, Best* red) {
-  // wave level
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {
-    const float ov = __shfl_xor(b.v, o);
-    const int oi = __shfl_xor(b.i, o);
-    if (better(ov, oi, b.v, b.i)) { b.v = ov; b.i = oi; }
-  }
-  constexpr int NW = NT / 64;
-  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  if (lane == 0) red[w] = b;
-  __syncthreads();
-  if (w == 0) {
-    b = lane < NW ? red[lane] : Best{-INFINITY, 0x7fffffff};
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-      const float ov = __shfl_xor(b.v, o);
-      const int oi = __shfl_xor(b.i, o);
-      if (better(ov, oi, b.v, b.i)) { b.v = ov; b.i = oi; }
-    }
-    if (lane == 0) red[NW] = b;
-  }
-  __syncthreads();
-  b = red[NW];
-  __syncthreads();
-  return b;
-}
-
 // one block per hypothesis: the P best tokens of W = w_dec*logp (+ w_lb), descending, then
 // <eos>; written at cand[h*(P+1) ...].  Two levels under the total order (value desc, token
 // asc): each wave takes the top P of its slice of the vocabulary (its lane values stay in
@@ -69,14 +40,36 @@ constexpr int PB_NT = 1024, PB_NW = PB_NT / 64, PB_PER = 32;  // <= 32 tokens pe
                                                                 // per instantiation: 8, 16 or 32)
 constexpr int PB_PMAX = 64;
 
+// Wave argmax under `better` (a total order, so the combination order is immaterial): DPP
+// within each 16-lane row (quad swaps, then row rotations by 4 and 8: every lane of a row ends
+// with the row's best), then the four rows' results by readlane.  A shuffle (ds_bpermute)
+// reduction costs an LDS round trip per step; these are VALU moves.
+template <int CTRL>
+EA_DEV void dpp_step(float& v, int& i) {
+  const float ov = __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), CTRL, 0xF, 0xF, false));
+  const int oi = __builtin_amdgcn_mov_dpp(i, CTRL, 0xF, 0xF, false);
+  if (better(ov, oi, v, i)) { v = ov; i = oi; }
+}
+template <int CTRL>
+EA_DEV void dpp_step3(float& v, int& i, int& c) {
+  const float ov = __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), CTRL, 0xF, 0xF, false));
+  const int oi = __builtin_amdgcn_mov_dpp(i, CTRL, 0xF, 0xF, false);
+  const int oc = __builtin_amdgcn_mov_dpp(c, CTRL, 0xF, 0xF, false);
+  if (better(ov, oi, v, i)) { v = ov; i = oi; c = oc; }
+}
 EA_DEV Best wave_argmax(Best b) {
+  dpp_step<0xB1>(b.v, b.i);   // quad_perm [1,0,3,2]
+  dpp_step<0x4E>(b.v, b.i);   // quad_perm [2,3,0,1]
+  dpp_step<0x124>(b.v, b.i);  // row_ror:4
+  dpp_step<0x128>(b.v, b.i);  // row_ror:8
+  Best r{__int_as_float(__builtin_amdgcn_readlane(__float_as_int(b.v), 0)), __builtin_amdgcn_readlane(b.i, 0)};
 #pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {
-    const float ov = __shfl_xor(b.v, o);
-    const int oi = __shfl_xor(b.i, o);
-    if (better(ov, oi, b.v, b.i)) { b.v = ov; b.i = oi; }
+  for (int q = 1; q < 4; ++q) {
+    const float ov = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(b.v), 16 * q));
+    const int oi = __builtin_amdgcn_readlane(b.i, 16 * q);
+    if (better(ov, oi, r.v, r.i)) { r.v = ov; r.i = oi; }
   }
-  return b;
+  return r;
 }
 
 template <int PER>
@@ -137,7 +130,31 @@ __global__ __launch_bounds__(PB_NT) void prebeam_kernel(int V, const float* __re
 //   rec_f[b*4 + {0,1,2,3}] = weighted score, decoder log-prob, CTC increment, CTC prefix psi
 //   next step: last[b] = token, rptr[b] = &r_new[(h*(P+1)+col)*T*2], prefix[b] = psi,
 //   score[b] = weighted score (all already in the new hypothesis order)
-constexpr int SEL_NT = 1024;
+// One wave: every candidate's weighted score, decoder log-prob and psi are computed once into
+// LDS, then `beam` wave argmax rounds (shuffles only, no block barriers) pick the winners; the
+// winner's record comes from LDS (no global load in the serial part).
+constexpr int SEL_NT = 64, SEL_MAX = 4096;
+struct BestC {
+  float v;
+  int i;  // the reference's flat index h*V + token (tie order)
+  int c;  // candidate slot
+};
+EA_DEV BestC wave_argmax_c(BestC b) {
+  dpp_step3<0xB1>(b.v, b.i, b.c);
+  dpp_step3<0x4E>(b.v, b.i, b.c);
+  dpp_step3<0x124>(b.v, b.i, b.c);
+  dpp_step3<0x128>(b.v, b.i, b.c);
+  BestC r{__int_as_float(__builtin_amdgcn_readlane(__float_as_int(b.v), 0)), __builtin_amdgcn_readlane(b.i, 0),
+          __builtin_amdgcn_readlane(b.c, 0)};
+#pragma unroll
+  for (int q = 1; q < 4; ++q) {
+    const float ov = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(b.v), 16 * q));
+    const int oi = __builtin_amdgcn_readlane(b.i, 16 * q);
+    const int oc = __builtin_amdgcn_readlane(b.c, 16 * q);
+    if (better(ov, oi, r.v, r.i)) { r.v = ov; r.i = oi; r.c = oc; }
+  }
+  return r;
+}
 __global__ __launch_bounds__(SEL_NT) void select_kernel(int n, int V, int P, int beam, int T, const float* __restrict__ logp,
                                                         long ld, const int* __restrict__ cand,
                                                         const float* __restrict__ psi, const float* __restrict__ prefix,
@@ -146,47 +163,50 @@ __global__ __launch_bounds__(SEL_NT) void select_kernel(int n, int V, int P, int
                                                         float* __restrict__ rec_f, int* __restrict__ last_next,
                                                         unsigned long long* __restrict__ rptr_next,
                                                         float* __restrict__ prefix_next, float* __restrict__ score_next) {
-  __shared__ Best red[SEL_NT / 64 + 1];
-  __shared__ float wsc[4096];
-  const int nc = n * (P + 1);
-  for (int c = threadIdx.x; c < nc; c += SEL_NT) {
+  __shared__ float wsc[SEL_MAX], dec_s[SEL_MAX], psi_s[SEL_MAX];
+  const int nc = n * (P + 1), lane = threadIdx.x;
+  for (int c = lane; c < nc; c += SEL_NT) {
     const int h = c / (P + 1), k = c - h * (P + 1);
     const int j = cand[c];
     bool dup = false;
     if (k == P)
       for (int q = 0; q < P; ++q) dup |= cand[h * (P + 1) + q] == j;
-    float wv = __fmul_rn(w_dec, logp[(long)h * ld + j]);
+    const float lp = logp[(long)h * ld + j];
+    const float ps = psi[c];
+    float wv = __fmul_rn(w_dec, lp);
     if (use_lb) wv = __fadd_rn(wv, w_lb);
-    const float inc = __fsub_rn(psi[c], prefix[h]);
+    const float inc = __fsub_rn(ps, prefix[h]);
     wv = __fadd_rn(__fadd_rn(wv, __fmul_rn(w_ctc, inc)), score[h]);
     wsc[c] = dup ? -INFINITY : wv;
+    dec_s[c] = lp;
+    psi_s[c] = ps;
   }
+  __builtin_amdgcn_wave_barrier();
   __syncthreads();
   for (int b = 0; b < beam; ++b) {
-    Best best{-INFINITY, 0x7fffffff};
-    for (int c = threadIdx.x; c < nc; c += SEL_NT) {
-      const int h = c / (P + 1);
-      const int flat = h * V + cand[c];  // the reference's index into the flattened scores
-      if (wsc[c] != -INFINITY && better(wsc[c], flat, best.v, best.i)) { best.v = wsc[c]; best.i = flat; }
+    BestC best{-INFINITY, 0x7fffffff, 0};
+    for (int c = lane; c < nc; c += SEL_NT) {
+      const float w = wsc[c];
+      const int flat = (c / (P + 1)) * V + cand[c];
+      if (w != -INFINITY && better(w, flat, best.v, best.i)) { best.v = w; best.i = flat; best.c = c; }
     }
-    best = block_argmax<SEL_NT>(best, red);
-    if (threadIdx.x == 0) {
-      // locate the candidate column again (first occurrence of the token in the row)
-      const int h = best.i == 0x7fffffff ? 0 : best.i / V, j = best.i == 0x7fffffff ? cand[0] : best.i - h * V;
-      int k = 0;
-      while (k < P + 1 && cand[h * (P + 1) + k] != j) ++k;
-      if (k == P + 1) k = 0;
-      const int c = h * (P + 1) + k;
-      const float dec = logp[(long)h * ld + j];
-      const float inc = __fsub_rn(psi[c], prefix[h]);
-      rec_i[b * 4 + 0] = h; rec_i[b * 4 + 1] = j; rec_i[b * 4 + 2] = k; rec_i[b * 4 + 3] = best.i == 0x7fffffff;
-      rec_f[b * 4 + 0] = best.v; rec_f[b * 4 + 1] = dec; rec_f[b * 4 + 2] = inc; rec_f[b * 4 + 3] = psi[c];
+    best = wave_argmax_c(best);
+    const bool none = best.i == 0x7fffffff;
+    const int c = none ? 0 : best.c;
+    const int h = c / (P + 1), k = c - h * (P + 1);
+    if (lane == 0) {
+      const int j = cand[c];
+      const float ps = psi_s[c];
+      const float inc = __fsub_rn(ps, prefix[h]);
+      rec_i[b * 4 + 0] = h; rec_i[b * 4 + 1] = j; rec_i[b * 4 + 2] = k; rec_i[b * 4 + 3] = none;
+      rec_f[b * 4 + 0] = best.v; rec_f[b * 4 + 1] = dec_s[c]; rec_f[b * 4 + 2] = inc; rec_f[b * 4 + 3] = ps;
       last_next[b] = j;
       rptr_next[b] = (unsigned long long)(uintptr_t)(r_new + (long)c * T * 2);
-      prefix_next[b] = psi[c];
+      prefix_next[b] = ps;
       score_next[b] = best.v;
       wsc[c] = -INFINITY;  // taken
     }
+    __builtin_amdgcn_wave_barrier();
     __syncthreads();
   }
 }
@@ -218,7 +238,7 @@ extern "C" int ea_beam_select(int n, int V, int P, int beam, int T, const float*
                               int use_lb, float w_ctc, const float* r_new, int* rec_i, float* rec_f, int* last_next,
                               unsigned long long* rptr_next, float* prefix_next, float* score_next, void* stream) {
   EA_ENTRY();
-  EA_CHECK_ARG(n >= 1 && V >= 1 && ld >= V && P >= 1 && beam >= 1 && T >= 1 && n * (P + 1) <= 4096 &&
+  EA_CHECK_ARG(n >= 1 && V >= 1 && ld >= V && P >= 1 && beam >= 1 && T >= 1 && n * (P + 1) <= SEL_MAX &&
                beam <= n * (P + 1));
   hipLaunchKernelGGL(select_kernel, dim3(1), dim3(SEL_NT), 0, (hipStream_t)stream, n, V, P, beam, T, logp, ld, cand,
                      psi, prefix, score, w_dec, w_lb, use_lb, w_ctc, r_new, rec_i, rec_f, last_next, rptr_next,

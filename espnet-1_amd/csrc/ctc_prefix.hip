@@ -62,18 +62,16 @@ __global__ void ctc_prefix_init_kernel(int T, int V, int blank, const float* __r
   }
 }
 
-// log(exp(x) + exp(y)) for the serial recursion of ctc_prefix_score2: npy_logaddexpf's cases
-// (x == y -> x + ln 2; NaN passes through) with the hardware exp / log (v_exp_f32 / v_log_f32,
-// ~1 ulp) instead of the libm expf / log1pf chains, and a cubic for log1p(e) at e < 1e-3 (where
-// 1 + e would round).  Deviation from float32 numpy: an ulp of the result at most per call.
-EA_DEV float fast_logaddexpf(float x, float y) {
-  if (x == y) return x + 0.693147180559945309417232121458176568f;
-  const float d = x - y;
-  if (d != d) return d;  // NaN
+// log(exp(x) + exp(y)) for the serial recursion of ctc_prefix_score2, branch-free on the
+// hardware base-2 exp / log (v_exp_f32 / v_log_f32, ~1 ulp): max + ln2 * log2(1 + 2^-(|x-y| log2 e)).
+// x == y gives x + ln 2 and NaN propagates through x - y, as npy_logaddexpf; for |x - y| > ~17
+// the 1 + e rounds to 1 where log1p would keep ~e (absolute error < 6e-8, an ulp of any
+// log-probability the recursion carries).  (npy_logaddexpf's branches and the libm log1p chain
+// made each frame of the serial loop ~1,000 cycles.)
+EA_DEV float lae_fast(float x, float y) {
   const float m = fmaxf(x, y);
-  const float e = __expf(-fabsf(d));
-  const float l = e < 1e-3f ? e * (1.f - e * (0.5f - e * 0.333333343f)) : __logf(1.f + e);
-  return m + l;
+  const float e = __builtin_amdgcn_exp2f(-fabsf(x - y) * 1.44269504088896341f);
+  return m + 0.693147180559945309f * __builtin_amdgcn_logf(1.f + e);
 }
 
 // one thread per (hypothesis h, candidate c): __call__ (:303-358)
@@ -143,7 +141,7 @@ __global__ __launch_bounds__(64) void ctc_prefix_score_kernel(int T, int V, int 
 // candidate's thread runs the serial recursion over the chunk from LDS, and the block writes
 // the candidate's forward variables back as contiguous rows.  The serial loop touches no
 // global memory (the one-thread-per-pair kernel above waited on scattered loads and stores
-// every frame); the recursion is the same, in the same order, with fast_logaddexpf.
+// every frame); the recursion is the same, in the same order, with lae_fast.
 template <int CH>
 __global__ __launch_bounds__(256) void ctc_prefix_score2_kernel(int T, int V, int blank, int eos, int n_cand,
                                                                 const float* __restrict__ logp,
@@ -174,6 +172,8 @@ __global__ __launch_bounds__(256) void ctc_prefix_score2_kernel(int T, int V, in
   const int k = tid;
   const bool act = k < n_cand;
   const int c = act ? cand[k] : 0;
+  __shared__ int cl[256];  // the candidates (n_cand <= 256), for the emission gather
+  if (act) cl[k] = c;
   const bool same = ol > 0 && c == last;
   float psi = act && ol == 0 ? logp[c] : kLogZero;
   float rn = (start - 1 < T && ol == 0 && act) ? logp[c] : kLogZero, rb = kLogZero;
@@ -187,20 +187,42 @@ __global__ __launch_bounds__(256) void ctc_prefix_score2_kernel(int T, int V, in
       pb[i] = b;
       xb[i] = logp[(long)t * V + blank];
     }
-    for (int q = tid; q < n_cand * nf; q += 256) {
-      const int kk = q / nf, i = q - kk * nf;
-      xc[kk * XS + i] = logp[(long)(t0 + i) * V + cand[kk]];
+    // candidate emissions: scattered 4-B reads (one row of the posteriors per frame), GU of
+    // them in flight per thread before any is stored (a load -> store loop ran them serially)
+    {
+      constexpr int GU = 16;
+      const int nq = n_cand * nf;
+      for (int q0 = 0; q0 < nq; q0 += 256 * GU) {
+        float v[GU];
+        int dst[GU];
+#pragma unroll
+        for (int u = 0; u < GU; ++u) {  // clamped, unconditional loads: all GU in flight at once
+          const int q = min(q0 + tid + 256 * u, nq - 1);
+          const int kk = q / nf, i = q - kk * nf;
+          dst[u] = kk * XS + i;
+          v[u] = logp[(long)(t0 + i) * V + cl[kk]];
+        }
+#pragma unroll
+        for (int u = 0; u < GU; ++u)
+          if (q0 + tid + 256 * u < nq) xc[dst[u]] = v[u];
+      }
     }
     __syncthreads();
     if (act) {
       const float* xk = xc + k * XS;
+      const float* pk = same ? pb : phi;  // log_phi[t-1]
       float* rk = ro + k * RS;
+      // next frame's operands loaded one iteration ahead (LDS latency off the serial chain)
+      float ph_n = pk[0], x_n = xk[0], xb_n = xb[0];
       for (int i = 0; i < nf; ++i) {
-        const float ph = same ? pb[i] : phi[i];  // log_phi[t-1]
-        const float x = xk[i];
-        const float nrn = fast_logaddexpf(rn, ph) + x;
-        const float nrb = fast_logaddexpf(rn, rb) + xb[i];
-        psi = fast_logaddexpf(psi, ph + x);
+        const float ph = ph_n, x = x_n, xbb = xb_n;
+        const int in = i + 1 < nf ? i + 1 : i;
+        ph_n = pk[in];
+        x_n = xk[in];
+        xb_n = xb[in];
+        const float nrn = lae_fast(rn, ph) + x;
+        const float nrb = lae_fast(rn, rb) + xbb;
+        psi = lae_fast(psi, ph + x);
         rn = nrn;
         rb = nrb;
         rk[2 * i] = rn;

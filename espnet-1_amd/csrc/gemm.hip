@@ -429,6 +429,33 @@ extern "C" int ea_gemm(int dtype, int a_kmajor, int b_kmajor, int M, int N, int 
                    ldc, sCb, sCh, epi, workspace, ws_elems, stream, nullptr);
 }
 
+extern "C" int ea_gemm_ln(int M, int N, int K, const float* x, long ldx, const float* gamma, const float* beta,
+                          float eps, const void* W, long ldw, void* C, int c_dtype, long ldc, const ea_epilogue* epi,
+                          void* stream) {
+  EA_ENTRY();
+  EA_CHECK_ARG(epi != nullptr && M >= 0 && N >= 0 && K > 0 && K % 32 == 0 && K <= 32 * 8 * 8);
+  EA_CHECK_ARG(x && gamma && beta && W && C && ldx >= K && ldw >= K && ldc >= N);
+  EA_CHECK_ARG(ldx % 4 == 0 && ((uintptr_t)x % 16) == 0 && ldw % 8 == 0 && ((uintptr_t)W % 16) == 0 &&
+               ((uintptr_t)gamma % 16) == 0 && ((uintptr_t)beta % 16) == 0);
+  if (epi->kind == EA_EPI_RESID) EA_CHECK_ARG(c_dtype == EA_F32);
+  if (M == 0 || N == 0) return 0;
+  GemmP p{};
+  p.M = M; p.N = N; p.K = K;
+  p.A = x; p.lda = ldx;
+  p.B = W; p.ldb = ldw;
+  p.nh = 1; p.splitk = 1; p.kchunk = K;
+  p.C = C; p.c_dtype = c_dtype; p.ldc = ldc;
+  p.epi = *epi;
+  p.salt = ea_g_rng_salt;
+  const int ce = c_dtype == EA_BF16 ? 2 : 4;
+  bool vc = (N % 4 == 0) && ldc % 4 == 0 && ((uintptr_t)C % (4 * ce)) == 0;
+  if (epi->bias) vc = vc && ((uintptr_t)epi->bias % 16) == 0;
+  if (epi->aux) vc = vc && epi->ldaux % 4 == 0 && ((uintptr_t)epi->aux % (4 * (epi->aux_dtype == EA_BF16 ? 2 : 4))) == 0;
+  if (epi->resid) vc = vc && epi->ldr % 4 == 0 && ((uintptr_t)epi->resid % 16) == 0;
+  p.vec_c = vc;
+  return launch_skinny_ln(p, gamma, beta, eps, (hipStream_t)stream);
+}
+
 extern "C" int ea_gemm_conv(const ea_conv_geo* geo, int a_kmajor, int b_kmajor, int M, int N, int K,
                             const void* A, long lda, const void* B, long ldb, void* C, int c_dtype, long ldc,
                             const ea_epilogue* epi, float* workspace, long ws_elems, void* stream) {

@@ -115,16 +115,24 @@ class DecodeGraphs:
         x = empty(n, d, device=dev)
         lib.ea_embed_fwd(n, d, 1, tok.data_ptr(), b.f("embed.0.weight").data_ptr(), pe.xscale, pe_row.data_ptr(),
                          0.0, 0, x.data_ptr(), ops.stream())
+        # each LayerNorm computed inside the Linear that consumes it (ea_gemm_ln: few-row bf16)
+        fuse_ln = cd == torch.bfloat16 and n <= 16 and d % 32 == 0 and d <= 2048
+
+        def ln_linear(xin, norm, w, out, epi):
+            if fuse_ln:
+                return ops.linear_ln(xin, b.f(norm + ".weight"), b.f(norm + ".bias"), w, out, epi=epi)
+            xn, _, _ = ln_fwd(xin, b, norm, cd)
+            return ops.linear(xn, w, out, epi=epi)
+
         for l in range(nb):
             nm = f"decoders.{l}."
             sa, xa, ff = nm + "self_attn.", nm + "src_attn.", nm + "feed_forward."
-            xn1, _, _ = ln_fwd(x, b, nm + "norm1", cd)
             # q | k | v in one GEMM (adjacent in the arena); k | v of this position go to the cache
             qkv = empty(n, 3 * d, dtype=cd, device=dev)
-            ops.linear(xn1, b.w(sa + "linear_q.weight", sa + "linear_k.weight", sa + "linear_v.weight",
-                                shape=(3 * d, d)), qkv,
-                       epi=ops.make_epi(bias=b.f(sa + "linear_q.bias", sa + "linear_k.bias", sa + "linear_v.bias",
-                                                 shape=(3 * d,))))
+            ln_linear(x, nm + "norm1", b.w(sa + "linear_q.weight", sa + "linear_k.weight", sa + "linear_v.weight",
+                                           shape=(3 * d, d)), qkv,
+                      ops.make_epi(bias=b.f(sa + "linear_q.bias", sa + "linear_k.bias", sa + "linear_v.bias",
+                                            shape=(3 * d,))))
             kvl = kv[l]
             kvl.index_copy_(1, pos, qkv[:, d:].view(n, 1, 2 * d))
             O1, _ = _mha_fwd(qkv, kvl, kvl[:, :, d:], B=n, H=H, T1=1, T2=self.lcap, dk=dk, ldq=3 * d, ldk=2 * d,
@@ -132,27 +140,24 @@ class DecodeGraphs:
             x1 = empty(n, d, device=dev)
             ops.linear(O1, b.w(sa + "linear_out.weight"), x1,
                        epi=ops.make_epi(EPI_RESID, bias=b.f(sa + "linear_out.bias"), resid=x))
-            xn2, _, _ = ln_fwd(x1, b, nm + "norm2", cd)
             q2 = empty(n, d, dtype=cd, device=dev)
-            ops.linear(xn2, b.w(xa + "linear_q.weight"), q2, epi=ops.make_epi(bias=b.f(xa + "linear_q.bias")))
+            ln_linear(x1, nm + "norm2", b.w(xa + "linear_q.weight"), q2, ops.make_epi(bias=b.f(xa + "linear_q.bias")))
             O2, _ = _mha_fwd(q2, mkv[:, 2 * d * l:], mkv[:, 2 * d * l + d:], B=n, H=H, T1=1, T2=Tm, dk=dk,
                              ldq=d, ldk=ldm, ldv=ldm, klen=hlens, causal=False, scale=scale, p=0.0, seed=0, cd=cd)
             x2 = empty(n, d, device=dev)
             ops.linear(O2, b.w(xa + "linear_out.weight"), x2,
                        epi=ops.make_epi(EPI_RESID, bias=b.f(xa + "linear_out.bias"), resid=x1))
-            xn3, _, _ = ln_fwd(x2, b, nm + "norm3", cd)
             Fh = dec.decoders[l].feed_forward.w_1.out_features
             h = empty(n, Fh, dtype=cd, device=dev)
             a = empty(n, Fh, dtype=cd, device=dev)
-            ops.linear(xn3, b.w(ff + "w_1.weight"), a,
-                       epi=ops.make_epi(EPI_ACT, bias=b.f(ff + "w_1.bias"), act=ACT_RELU, aux=h))
+            ln_linear(x2, nm + "norm3", b.w(ff + "w_1.weight"), a,
+                      ops.make_epi(EPI_ACT, bias=b.f(ff + "w_1.bias"), act=ACT_RELU, aux=h))
             x3 = empty(n, d, device=dev)
             ops.linear(a, b.w(ff + "w_2.weight"), x3,
                        epi=ops.make_epi(EPI_RESID, bias=b.f(ff + "w_2.bias"), resid=x2))
             x = x3
-        xf, _, _ = ln_fwd(x, b, "after_norm", cd)
         logits = empty(n, V, device=dev)
-        ops.linear(xf, b.w("output_layer.weight"), logits, epi=ops.make_epi(bias=b.f("output_layer.bias")))
+        ln_linear(x, "after_norm", b.w("output_layer.weight"), logits, ops.make_epi(bias=b.f("output_layer.bias")))
         logp = empty(n, V, device=dev)
         lib.ea_softmax_rows(n, V, logits.data_ptr(), V, logp.data_ptr(), 1, ops.stream())
         return logp

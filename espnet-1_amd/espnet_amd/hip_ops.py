@@ -736,6 +736,18 @@ def layernorm_fwd(x, gamma, beta, y, mean, rstd, eps=1e-12):
                          mean.data_ptr(), rstd.data_ptr(), stream())
 
 
+def linear_ln(x, gamma, beta, w, out, *, epi=None, eps=1e-12):
+    """out = epi(LayerNorm(x) . w^T) in one launch (ea_gemm_ln): x f32 (rows, K), w bf16
+    (N, K); the normalised rows are rounded to bf16 as the unfused LayerNorm stores them."""
+    rows, K, ldx = _rows(x)
+    N = w.shape[0]
+    if epi is None:
+        epi = make_epi()
+    lib.ea_gemm_ln(rows, N, K, x.data_ptr(), ldx, gamma.data_ptr(), beta.data_ptr(), ctypes.c_float(eps),
+                   w.data_ptr(), w.stride(0), out.data_ptr(), dt(out), out.stride(0), ctypes.byref(epi), stream())
+    return out
+
+
 def layernorm_bwd(dy, x, gamma, mean, rstd, dx, dgamma, dbeta, accumulate=True, drop=None):
     """drop=(y, scale, p, seed[, ycol]): also y = dropout(scale * dx) once dx is final (the next
     residual site's dropout backward, ea_layernorm_bwd_drop), instead of an ea_scale_dropout

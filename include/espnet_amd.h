@@ -150,6 +150,13 @@ int ea_gemm_set_skinny(int max_m);
  * the few-row limit (the training decoder's B*(L+1) tokens); 0 = off (EA_GEMM_ROWS32).
  * Process-wide; A/B switch. */
 int ea_gemm_set_rows32(int max_m);
+/* C = epi(LayerNorm(x) . W^T): x f32 (M x K, ldx, rows 16-B aligned), gamma / beta f32 (K),
+ * W bf16 (N x K, ldw) — the LayerNorm (eps) computed per row inside the few-row GEMM
+ * (16 x 32 blocks, 8 waves splitting K) and rounded to bf16 in the MFMA operand registers,
+ * as the unfused path stores it.  K % 32 == 0, K <= 2048.  Any epilogue of ea_gemm.
+ * Replaces a LayerNorm (layer_norm.py) + Linear pair of the incremental decoder's step. */
+int ea_gemm_ln(int M, int N, int K, const float* x, long ldx, const float* gamma, const float* beta, float eps,
+               const void* W, long ldw, void* C, int c_dtype, long ldc, const ea_epilogue* epi, void* stream);
 /* Plain bf16 GEMMs (STORE epilogue without bias, scale or dropout; alpha / beta honoured;
  * unbatched; M >= 4096) on hipBLASLt: mode bit 1 = N <= 512, bit 2 = N > 512; 0 = off
  * (EA_GEMM_BLASLT; default 1).  Shapes hipBLASLt has no workspace-free algorithm for stay on ea_gemm's

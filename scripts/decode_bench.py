@@ -1,7 +1,8 @@
 """Joint CTC/attention beam search on the C3 model (Conformer-L + 6-layer Transformer decoder,
 V=5000, random init): one 1000-frame utterance (249 encoder frames), beam 10, ctc_weight 0.3,
 a fixed 40-token output (maxlenratio -40, the C3 label length).  Prints the decode time per
-utterance and the time split between encode, decoder scoring and CTC prefix scoring.
+utterance (and with --split the time in decoder scoring / CTC prefix scoring, measured with
+synchronisations that themselves add to the total).
 
     python scripts/decode_bench.py [--beam 10] [--ctc-weight 0.3] [--tokens 40] [--utts 3]
 """
@@ -27,6 +28,9 @@ def main():
     ap.add_argument("--single", action="store_true", help="BeamSearch (per-hypothesis selection on the host) "
                     "instead of BatchBeamSearch, the reference's default for batch scorers")
     ap.add_argument("--host-select", action="store_true", help="BatchBeamSearch with the host selection")
+    ap.add_argument("--split", action="store_true", help="synchronise around the decoder / CTC scoring calls to "
+                    "report their time (the syncs themselves add to the total)")
+    ap.add_argument("--cprofile", action="store_true", help="host profile of the timed decodes (top 30)")
     args = ap.parse_args()
     from espnet_amd.asr.beam_search import BatchBeamSearch, BeamSearch, CTCPrefixScorer, LengthBonus
     dev = torch.device("cuda", 0)
@@ -38,6 +42,9 @@ def main():
     timers = {"decoder": 0.0, "ctc": 0.0}
 
     def timed(name, fn):
+        if not args.split:
+            return fn
+
         def wrap(*a, **k):
             torch.cuda.synchronize()
             t0 = time.perf_counter()
@@ -67,6 +74,11 @@ def main():
         torch.cuda.synchronize()
         timers.update(decoder=0.0, ctc=0.0)
         t_enc = 0.0
+        prof = None
+        if args.cprofile:
+            import cProfile
+            prof = cProfile.Profile()
+            prof.enable()
         t0 = time.perf_counter()
         for _ in range(args.utts):
             te = time.perf_counter()
@@ -76,11 +88,16 @@ def main():
             nbest = bs(enc[0], maxlenratio=-float(args.tokens))
         torch.cuda.synchronize()
         el = time.perf_counter() - t0
+        if prof is not None:
+            import pstats
+            prof.disable()
+            pstats.Stats(prof).sort_stats("tottime").print_stats(30)
     n = args.utts
     print(f"C3 joint decode ({cls.__name__}{', host selection' if args.host_select else ''}): beam {args.beam}, ctc_weight {args.ctc_weight}, {args.tokens} tokens, "
-          f"T'={enc.shape[1]}: {el / n * 1e3:.1f} ms/utt ({n / el:.2f} utt/s); encode {t_enc / n * 1e3:.1f} ms, "
-          f"decoder scoring {timers['decoder'] / n * 1e3:.1f} ms, CTC prefix scoring {timers['ctc'] / n * 1e3:.1f} ms "
-          f"per utt; best hyp len {len(nbest[0].yseq) - 2}", flush=True)
+          f"T'={enc.shape[1]}: {el / n * 1e3:.1f} ms/utt ({n / el:.2f} utt/s); encode {t_enc / n * 1e3:.1f} ms"
+          + (f", decoder scoring {timers['decoder'] / n * 1e3:.1f} ms, CTC prefix scoring "
+             f"{timers['ctc'] / n * 1e3:.1f} ms per utt (synchronised split)" if args.split else "")
+          + f"; best hyp len {len(nbest[0].yseq) - 2}", flush=True)
 
 
 if __name__ == "__main__":

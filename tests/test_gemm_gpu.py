@@ -565,3 +565,33 @@ def test_gemm_rows32_vs_fp64(MNK):
         torch.testing.assert_close(Ca.double().cpu(), ref.clamp_min(0), atol=3e-2, rtol=2e-2)
     finally:
         L.lib.ea_gemm_set_rows32(0)
+
+
+@pytest.mark.parametrize("MNK", [(10, 1536, 512), (10, 2048, 512), (16, 5000, 512), (3, 40, 96), (7, 512, 2048)])
+def test_gemm_ln_vs_fp64(MNK):
+    """ea_gemm_ln (LayerNorm of f32 rows computed inside the few-row GEMM, normalised rows
+    rounded to bf16 as the unfused LayerNorm stores them): against fp64 LayerNorm -> bf16 ->
+    GEMM, and equal to the unfused pair (ea_layernorm_fwd + ea_gemm) within accumulation noise."""
+    ops, L = _ops()
+    M, N, K = MNK
+    g = torch.Generator().manual_seed(M * 5 + N + K)
+    x = (torch.randn(M, K + 4, generator=g) * 3 + 1).cuda()[:, :K]
+    gam = (torch.rand(K, generator=g) + 0.5).cuda()
+    bet = torch.randn(K, generator=g).cuda() * 0.1
+    W = mk((N, K + 8), torch.bfloat16, g, 0.1)[:, :K]
+    bias = mk((N,), torch.float32, g)
+    xd = x.double().cpu()
+    xn = (xd - xd.mean(1, keepdim=True)) / torch.sqrt(xd.var(1, unbiased=False, keepdim=True) + 1e-12)
+    xn = (xn * gam.double().cpu() + bet.double().cpu()).to(torch.bfloat16).double()
+    ref = xn @ W.double().cpu().t() + bias.double().cpu()
+    C = torch.full((M, N + 4), 7.0, device="cuda")
+    ops.linear_ln(x, gam, bet, W, C[:, :N], epi=ops.make_epi(bias=bias))
+    torch.testing.assert_close(C[:, :N].double().cpu(), ref, atol=2e-3 * K ** 0.5, rtol=2e-3)
+    assert (C[:, N:] == 7.0).all()
+    if K > 1024:
+        return  # (the unfused LayerNorm kernel takes d <= 1024)
+    xn_dev = torch.empty(M, K, device="cuda", dtype=torch.bfloat16)
+    ops.layernorm_fwd(x, gam, bet, xn_dev, torch.empty(M, device="cuda"), torch.empty(M, device="cuda"))
+    C0 = torch.empty(M, N, device="cuda")
+    ops.linear(xn_dev, W, C0, epi=ops.make_epi(bias=bias))
+    torch.testing.assert_close(C[:, :N], C0, atol=2e-2, rtol=1e-2)
