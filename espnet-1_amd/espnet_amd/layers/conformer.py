@@ -25,6 +25,23 @@ from .common import (ACT_SWISH, EPI_ACT, EPI_DACT, EPI_RESID, EPI_STORE, F32, Bo
 
 # ----------------------------------------------------------------------------- holders
 
+# the attention's dropout keep bits drawn ahead on the auxiliary stream (EA_ATTN_BITS_AHEAD=1;
+# outputs are bit-identical either way).  Measured: the forward kernel 44.1 -> 37.7 us, but the
+# generator (13.3 us) slows the macaron FFN GEMMs it runs beside: step 1781-1786 -> 1777 utt/s
+# (profiles/r4_attn_bits_ab.txt), so the hash stays in the forward by default
+ATTN_BITS_AHEAD = os.environ.get("EA_ATTN_BITS_AHEAD", "0") == "1"
+_KEEP_WORDS = {}
+
+
+def attn_keep_words(B, H, T1, T2):
+    key = (B, H, T1, T2)
+    if key not in _KEEP_WORDS:
+        n = ctypes.c_long(0)
+        lib.ea_attn_keep_bits_words(B, H, T1, T2, ctypes.addressof(n))
+        _KEEP_WORDS[key] = n.value
+    return _KEEP_WORDS[key]
+
+
 # depthwise-conv dw / dbias partials deferred into the grouped reduce (EA_DWCONV_DEFER=1; measured neutral, off)
 DWCONV_DEFER = os.environ.get("EA_DWCONV_DEFER", "0") == "1"
 
@@ -183,6 +200,18 @@ class ConformerBlockFn(torch.autograd.Function):
         li = L.layer_idx
         sd = lambda s: site_seed(seed, li, s)  # noqa: E731
         x0 = x.reshape(N, d)
+        # the attention's dropout keep bits drawn on the auxiliary stream while the macaron FFN's
+        # MFMA-bound GEMMs run (ea_attn_keep_bits); the forward then reads them (fwd2b)
+        pre = None
+        if ATTN_BITS_AHEAD and pa > 0 and fused_attn_ok(cd, dk, T, T) and torch.cuda.is_available():
+            dmask_a, ldm_a = attn_dmask(B * H * T, T, pa, dev)
+            fmask_a = empty(attn_keep_words(B, H, T, T), dtype=torch.int32, device=dev)
+            with ops.aux(dmask_a, fmask_a, olens):
+                lib.ea_attn_keep_bits(B, H, T, T, olens.data_ptr(), 0, float(pa), sd(3), dmask_a.data_ptr(), ldm_a,
+                                      fmask_a.data_ptr(), ops.stream())
+                ev_a = torch.cuda.Event()
+                ev_a.record()
+            pre = (dmask_a, ldm_a, fmask_a, ev_a)
         # ---- macaron FFN  (encoder_layer.py:115-123)
         x1, s_ff1 = _ffn_fwd(L, b, x0, "feed_forward_macaron", "norm_ff_macaron", p, sd(1), sd(2))
         # ---- rel-pos MHSA (encoder_layer.py:126-149, attention.py:262-305)
@@ -200,12 +229,21 @@ class ConformerBlockFn(torch.autograd.Function):
             # one kernel: (q+u)k^T + rel_shift((q+v)p^T), mask, softmax, dropout, @v
             O = empty(N, d, dtype=cd, device=dev)
             lse = empty(B * H * T, device=dev)
-            dmask, ldm = attn_dmask(B * H * T, T, pa, dev)
-            lib.ea_attn_fused_fwd2(B, H, T, T, dk, qkv.data_ptr(), 3 * d, qkv[:, d:].data_ptr(), 3 * d,
-                                   qkv[:, 2 * d:].data_ptr(), 3 * d, b.f(A + "pos_bias_u").data_ptr(),
-                                   b.f(A + "pos_bias_v").data_ptr(), pp.data_ptr(), d, olens.data_ptr(), 0,
-                                   scale, float(pa), sd(3), O.data_ptr(), d, lse.data_ptr(), ptr(dmask), ldm,
-                                   ops.stream())
+            if pre is not None:
+                dmask, ldm, fmask_a, ev_a = pre
+                torch.cuda.current_stream().wait_event(ev_a)
+                lib.ea_attn_fused_fwd2b(B, H, T, T, dk, qkv.data_ptr(), 3 * d, qkv[:, d:].data_ptr(), 3 * d,
+                                        qkv[:, 2 * d:].data_ptr(), 3 * d, b.f(A + "pos_bias_u").data_ptr(),
+                                        b.f(A + "pos_bias_v").data_ptr(), pp.data_ptr(), d, olens.data_ptr(), 0,
+                                        scale, float(pa), sd(3), O.data_ptr(), d, lse.data_ptr(),
+                                        fmask_a.data_ptr(), ops.stream())
+            else:
+                dmask, ldm = attn_dmask(B * H * T, T, pa, dev)
+                lib.ea_attn_fused_fwd2(B, H, T, T, dk, qkv.data_ptr(), 3 * d, qkv[:, d:].data_ptr(), 3 * d,
+                                       qkv[:, 2 * d:].data_ptr(), 3 * d, b.f(A + "pos_bias_u").data_ptr(),
+                                       b.f(A + "pos_bias_v").data_ptr(), pp.data_ptr(), d, olens.data_ptr(), 0,
+                                       scale, float(pa), sd(3), O.data_ptr(), d, lse.data_ptr(), ptr(dmask), ldm,
+                                       ops.stream())
             ldT = 0
             s_core = ("fused", lse, dmask, ldm)
         else:

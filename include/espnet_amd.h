@@ -493,6 +493,20 @@ int ea_attn_fused_fwd2(int B, int H, int T1, int T2, int dk, const void* q, long
                        const void* pp, long ldp, const long long* klen, int causal, float scale, float p,
                        unsigned long long seed, void* o, long ldo, float* lse, unsigned* dmask, int ldm,
                        void* stream);
+/* The dropout keep decisions of ea_attn_fused_fwd2 (same B, H, T1, T2, klen, causal, p > 0 and
+ * seed; the same per-step salt) computed ahead of the forward, e.g. on a side stream beside
+ * MFMA-bound work: the backward's row words into dmask (as ea_attn_fused_fwd2 writes them) and
+ * the forward's own order into fmask (ea_attn_keep_bits_words() 32-bit words).  Then
+ * ea_attn_fused_fwd2b runs the forward reading fmask instead of hashing — bit-identical output,
+ * and dmask serves the backward. */
+int ea_attn_keep_bits_words(int B, int H, int T1, int T2, long* words);
+int ea_attn_keep_bits(int B, int H, int T1, int T2, const long long* klen, int causal, float p,
+                      unsigned long long seed, unsigned* dmask, int ldm, unsigned* fmask, void* stream);
+int ea_attn_fused_fwd2b(int B, int H, int T1, int T2, int dk, const void* q, long ldq, const void* k,
+                        long ldk, const void* v, long ldv, const float* bu, const float* bv,
+                        const void* pp, long ldp, const long long* klen, int causal, float scale, float p,
+                        unsigned long long seed, void* o, long ldo, float* lse, const unsigned* fmask,
+                        void* stream);
 /* Backward of ea_attn_fused_fwd(2): dq = d(q + bu) (flags bit 0, pp only: + d(q + bv), the
  * rel-pos path dBD·pp computed in-kernel), dk, dv (bf16), and optionally:
  *   dbd (pp only, or NULL): the band dbd[h][b][i][T-1-i+j] = gradient of the raw rel-pos term
