@@ -67,9 +67,15 @@ int g_gemm_skinny = [] { const char* e = std::getenv("EA_GEMM_SKINNY"); return e
 // ... and the 32-row variant for M up to g_gemm_rows32 (ea_gemm_set_rows32; 0 = off)
 int g_gemm_rows32 = [] { const char* e = std::getenv("EA_GEMM_ROWS32"); return e ? std::atoi(e) : 0; }();
 
+// 256x256 K-major tiles on gemm_quad (4 waves of 128x128; ea_gemm_set_quad / EA_GEMM_QUAD; 0 = off)
+int g_gemm_quad = [] { const char* e = std::getenv("EA_GEMM_QUAD"); return e ? std::atoi(e) : 0; }();
+
 int launch_lds(GemmP& p, int a_k, int b_k, int nz, hipStream_t st, bool pipe128 = false, bool k128 = false) {
   dim3 grid(p.tiles_m * p.tiles_n, 1, nz * p.splitk);
   if (k128) return launch_k128(p, grid, st);
+  if (g_gemm_quad && p.g.mode == 0 && p.bm == 256 && p.bn == 256 && a_k && b_k && p.K % 64 == 0 &&
+      p.kchunk % 64 == 0)
+    return launch_quad(p, grid, st);
   if (p.g.mode != 0) {  // implicit-GEMM conv2 modes: fixed layouts, 128x128 or 256x256 tiles
     if (p.bm == 256 && g_gemm_pipe) return launch_pipe_conv(p, grid, st);
     return launch_lds_conv(p, grid, st);
@@ -232,6 +238,14 @@ extern "C" int ea_gemm_set_skinny(int max_m) {
   EA_ENTRY();
   EA_CHECK_ARG(max_m >= 0 && max_m <= 64);
   g_gemm_skinny = max_m;
+  return 0;
+}
+
+extern "C" int ea_gemm_set_quad(int on, int slots) {
+  EA_ENTRY();
+  EA_CHECK_ARG(slots == 4 || slots == 5);
+  g_gemm_quad = on;
+  eag::g_quad_slots = slots;
   return 0;
 }
 
