@@ -90,16 +90,33 @@ __global__ __launch_bounds__(PB_NT) void prebeam_kernel(int V, const float* __re
     }
     val[e] = wvv;
   }
-  uint32_t taken = 0u;
-  for (int r = 0; r < P; ++r) {
-    Best b{-INFINITY, 0x7fffffff};
+  // each lane sorts its PER (value, token) pairs once (odd-even transposition network under
+  // `better`); a selection round is then one wave argmax over the lanes' heads, and the winning
+  // lane shifts its list — instead of every lane rescanning all PER values every round (with 4
+  // waves per SIMD that rescan was ~2 us per round)
+  int idx[PER];
 #pragma unroll
-    for (int e = 0; e < PER; ++e) {
-      const int v = v0 + e * 64 + lane;
-      if (v < v1 && !((taken >> e) & 1u) && better(val[e], v, b.v, b.i)) { b.v = val[e]; b.i = v; }
+  for (int e = 0; e < PER; ++e) {
+    const int v = v0 + e * 64 + lane;
+    idx[e] = v < v1 ? v : 0x7fffffff;
+    if (v >= v1) val[e] = -INFINITY;
+  }
+#pragma unroll
+  for (int pass = 0; pass < PER; ++pass)
+#pragma unroll
+    for (int e = pass & 1; e + 1 < PER; e += 2)
+      if (better(val[e + 1], idx[e + 1], val[e], idx[e])) {
+        const float tv = val[e]; val[e] = val[e + 1]; val[e + 1] = tv;
+        const int ti = idx[e]; idx[e] = idx[e + 1]; idx[e + 1] = ti;
+      }
+  for (int r = 0; r < P; ++r) {
+    Best b = wave_argmax(Best{val[0], idx[0]});
+    if (idx[0] == b.i && b.i != 0x7fffffff) {  // this lane's head was taken: shift its list
+#pragma unroll
+      for (int e = 0; e + 1 < PER; ++e) { val[e] = val[e + 1]; idx[e] = idx[e + 1]; }
+      val[PER - 1] = -INFINITY;
+      idx[PER - 1] = 0x7fffffff;
     }
-    b = wave_argmax(b);
-    if (b.i != 0x7fffffff && b.i >= v0 && b.i < v1 && (b.i - v0) % 64 == lane) taken |= 1u << ((b.i - v0) / 64);
     if (lane == 0) lst[wv * PB_PMAX + r] = b;
   }
   __syncthreads();

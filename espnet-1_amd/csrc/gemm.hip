@@ -73,9 +73,9 @@ int g_gemm_quad = [] { const char* e = std::getenv("EA_GEMM_QUAD"); return e ? s
 int launch_lds(GemmP& p, int a_k, int b_k, int nz, hipStream_t st, bool pipe128 = false, bool k128 = false) {
   dim3 grid(p.tiles_m * p.tiles_n, 1, nz * p.splitk);
   if (k128) return launch_k128(p, grid, st);
-  if (g_gemm_quad && p.g.mode == 0 && p.bm == 256 && p.bn == 256 && a_k && b_k && p.K % 64 == 0 &&
-      p.kchunk % 64 == 0)
-    return launch_quad(p, grid, st);
+  if (g_gemm_quad && p.g.mode == 0 && p.bm == 256 && p.bn == 256 && a_k && (b_k || (g_gemm_quad & 2)) &&
+      p.K % 64 == 0 && p.kchunk % 64 == 0)
+    return launch_quad(p, b_k, grid, st);
   if (p.g.mode != 0) {  // implicit-GEMM conv2 modes: fixed layouts, 128x128 or 256x256 tiles
     if (p.bm == 256 && g_gemm_pipe) return launch_pipe_conv(p, grid, st);
     return launch_lds_conv(p, grid, st);

@@ -62,7 +62,7 @@ int launch_k128(GemmP& p, dim3 grid, hipStream_t st);                     // gem
 int launch_pipe_conv(GemmP& p, dim3 grid, hipStream_t st);               // gemm_pipe_conv.hip: conv2 modes
 int launch_lds_dense(GemmP& p, int a_k, int b_k, dim3 grid, hipStream_t st);  // gemm_lds.hip
 int launch_lds_conv(GemmP& p, dim3 grid, hipStream_t st);                     // gemm_lds_conv.hip
-int launch_quad(GemmP& p, dim3 grid, hipStream_t st);    // gemm_quad.hip: 256x256, 4 waves of 128x128
+int launch_quad(GemmP& p, int b_k, dim3 grid, hipStream_t st);  // gemm_quad.hip: 256x256, 4 waves of 128x128
 extern int g_quad_slots;
 int launch_skinny(GemmP& p, hipStream_t st, int rows32);  // gemm_skinny.hip: few-row bf16, K split over waves
 int launch_skinny_ln(GemmP& p, const float* gamma, const float* beta, float eps, hipStream_t st);  // + LayerNorm

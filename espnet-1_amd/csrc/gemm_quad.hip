@@ -19,6 +19,13 @@
 namespace {
 using namespace eag;
 
+template <int N>
+EA_DEV void wait_lgkm() {  // at most N LDS reads outstanding
+  if constexpr (N == 4) asm volatile("s_waitcnt lgkmcnt(4)" ::: "memory");
+  else if constexpr (N == 8) asm volatile("s_waitcnt lgkmcnt(8)" ::: "memory");
+  else asm volatile("s_waitcnt lgkmcnt(12)" ::: "memory");
+}
+
 template <int OFF>
 EA_DEV bf16x8 ds_read_b128_off(uint32_t a) {  // LDS byte address a + OFF (immediate)
   bf16x8 v;
@@ -26,7 +33,7 @@ EA_DEV bf16x8 ds_read_b128_off(uint32_t a) {  // LDS byte address a + OFF (immed
   return v;
 }
 
-template <int S>
+template <int S, bool BKM>
 __global__ __launch_bounds__(256, 1) void gemm_quad(GemmP p) {
   constexpr int BT = 256, BK = 32, NTT = 256, NW = 4, MI = 8, NJ = 8;
   constexpr int A_BYTES = BT * BK * 2, B_BYTES = BT * BK * 2, SLOT = A_BYTES + B_BYTES;
@@ -51,22 +58,28 @@ __global__ __launch_bounds__(256, 1) void gemm_quad(GemmP p) {
 
   // lane-linear DMA: chunk ci = (i*NW + w)*64 + lane lands at ci*16 (64-B rows of 4 chunks);
   // its source is the global chunk whose swizzled slot that is
-  auto src = [&](long ld, int mn0, int MN, int ci) -> uint32_t {
-    const int row = ci >> 2, c = (ci & 3) ^ swz32(ci >> 2);
-    return (uint32_t)(((long)min(mn0 + row, MN - 1) * ld + c * 8) * 2);
+  auto src = [&](long ld, int mn0, int MN, bool kmaj, int ci) -> uint32_t {
+    if (kmaj) {
+      const int row = ci >> 2, c = (ci & 3) ^ swz32(ci >> 2);
+      return (uint32_t)(((long)min(mn0 + row, MN - 1) * ld + c * 8) * 2);
+    }
+    // MN-major: two [32 k][128] panels per slice (gemm_pipe's image, swz_mn_bf16 chunk swizzle)
+    const int pnl = ci >> 9, cj = ci & 511, k = cj >> 4, c = (cj & 15) ^ swz_mn_bf16(k);
+    return (uint32_t)(((long)k * ld + min((long)(mn0 + pnl * 128 + c * 8), (long)((MN - 1) & ~7))) * 2);
   };
   const char* abase = (const char*)(A + kbeg);
-  const char* bbase = (const char*)(B + kbeg);
+  const char* bbase = (const char*)(B + (BKM ? (long)kbeg : (long)kbeg * p.ldb));
+  const long bstep = (BKM ? BK : (long)BK * p.ldb) * 2;  // bytes per slice
   uint32_t aoff[ACH], boff[BCH];
 #pragma unroll
-  for (int i = 0; i < ACH; ++i) aoff[i] = src(p.lda, m0, p.M, (i * NW + w) * 64 + lane);
+  for (int i = 0; i < ACH; ++i) aoff[i] = src(p.lda, m0, p.M, true, (i * NW + w) * 64 + lane);
 #pragma unroll
-  for (int i = 0; i < BCH; ++i) boff[i] = src(p.ldb, n0, p.N, (i * NW + w) * 64 + lane);
+  for (int i = 0; i < BCH; ++i) boff[i] = src(p.ldb, n0, p.N, BKM, (i * NW + w) * 64 + lane);
 
   auto issue = [&](int sl) {
     char* base = smem + (sl % S) * SLOT;
     const char* ak = abase + (long)sl * BK * 2;
-    const char* bk = bbase + (long)sl * BK * 2;
+    const char* bk = bbase + (long)sl * bstep;
 #pragma unroll
     for (int i = 0; i < ACH; ++i)
       __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)(ak + aoff[i]),
@@ -83,11 +96,37 @@ __global__ __launch_bounds__(256, 1) void gemm_quad(GemmP p) {
   // immediate offset i * 1024 (a per-fragment address would hold 24 VGPRs per ring slot).
   const uint32_t lane_off = (uint32_t)((lane & 15) * 64 + (((lane >> 4) ^ swz32(lane & 15)) << 4));
   const uint32_t smem_lds = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) char*)smem;
-  auto rd = [&](uint32_t a, bf16x8 (&f)[8]) {
-    f[0] = ds_read_b128_off<0>(a); f[1] = ds_read_b128_off<1024>(a);
-    f[2] = ds_read_b128_off<2048>(a); f[3] = ds_read_b128_off<3072>(a);
-    f[4] = ds_read_b128_off<4096>(a); f[5] = ds_read_b128_off<5120>(a);
-    f[6] = ds_read_b128_off<6144>(a); f[7] = ds_read_b128_off<7168>(a);
+  // MN-major B (16 columns wn + 16 j, k-chunk lane >> 4): frag32<false>'s two 4 x 4 transposed
+  // reads; the chunk of fragment j is (2 j + (pp >> 1)) ^ swz (swz even: bit 0 untouched), so
+  // the lane term and j separate as ((j ^ (swz >> 1)) << 5) | ((pp >> 1) << 4) + within
+  const int tq = (lane & 15) >> 2, tp = lane & 3;
+  uint32_t trow[2], tsw[2];
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int row = 8 * (lane >> 4) + 4 * h + tq;
+    trow[h] = (uint32_t)(row * 256 + ((tp >> 1) << 4) + (tp & 1) * 8);
+    tsw[h] = (uint32_t)(swz_mn_bf16(row) >> 1);
+  }
+  auto rd_bmn = [&](uint32_t pnl, int j0, bf16x8 (&f)[8]) {  // fragments j0 .. j0+3
+#pragma unroll
+    for (int j = j0; j < j0 + 4; ++j) {
+      union { bf16x8 v; s16x4 h[2]; } o;
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const uint32_t a = pnl + trow[h] + ((((uint32_t)j) ^ tsw[h]) << 5);
+        asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(o.h[h]) : "v"(a) : "memory");
+      }
+      f[j] = o.v;
+    }
+  };
+  auto rd_bk = [&](uint32_t a, int j0, bf16x8 (&f)[8]) {
+    if (j0 == 0) {
+      f[0] = ds_read_b128_off<0>(a); f[1] = ds_read_b128_off<1024>(a);
+      f[2] = ds_read_b128_off<2048>(a); f[3] = ds_read_b128_off<3072>(a);
+    } else {
+      f[4] = ds_read_b128_off<4096>(a); f[5] = ds_read_b128_off<5120>(a);
+      f[6] = ds_read_b128_off<6144>(a); f[7] = ds_read_b128_off<7168>(a);
+    }
   };
 
   f32x4 acc[MI][NJ];
@@ -116,9 +155,19 @@ __global__ __launch_bounds__(256, 1) void gemm_quad(GemmP p) {
     f[4] = ds_read_b128_off<4096>(a); f[5] = ds_read_b128_off<5120>(a);
     f[6] = ds_read_b128_off<6144>(a); f[7] = ds_read_b128_off<7168>(a);
   };
-  // lane addresses of a slot's A rows wm.. and B rows wn..
+  // lane addresses of a slot's A rows wm.. and B rows wn.. (K-major) / B panel wn >> 7 (MN-major)
   auto a_addr = [&](int sl) { return smem_lds + (uint32_t)((sl % S) * SLOT + wm * 64) + lane_off; };
-  auto b_addr = [&](int sl) { return smem_lds + (uint32_t)((sl % S) * SLOT + A_BYTES + wn * 64) + lane_off; };
+  auto b_addr = [&](int sl) {
+    return BKM ? smem_lds + (uint32_t)((sl % S) * SLOT + A_BYTES + wn * 64) + lane_off
+               : smem_lds + (uint32_t)((sl % S) * SLOT + A_BYTES + (wn >> 7) * 8192);
+  };
+  auto rd_b = [&](uint32_t a, int j0, bf16x8 (&f)[8]) {
+    if constexpr (BKM) rd_bk(a, j0, f);
+    else rd_bmn(a, j0, f);
+  };
+  // reads per B half (4 fragments): 4 (K-major) or 8 (two transposed reads each); lgkmcnt order
+  // per slice s: Bh0(s+1) | MFMA rows 0-3 | A[0-3](s+1) Bh1(s+1) | MFMA rows 4-7 | A[4-7](s+1)
+  constexpr int NBH = BKM ? 4 : 8;
   bf16x8 fa[8], fb0[8], fb1[8];
   // the register data flow is the same every slice (the last slice re-reads its own slot
   // instead of a next one): conditional fragment reads made the compiler keep both versions
@@ -132,17 +181,19 @@ __global__ __launch_bounds__(256, 1) void gemm_quad(GemmP p) {
       lds_barrier();  // everyone's; every wave is past its reads of slice sl-1: its slot is free
       if (sl + S - 1 < nsl) issue(sl + S - 1);
     }
-    rd(b_addr(nx), nbuf);
-    asm volatile("s_waitcnt lgkmcnt(12)" ::: "memory");  // A[0-3](s) and B(s) in
+    const uint32_t bad = b_addr(nx), aad = a_addr(nx);
+    rd_b(bad, 0, nbuf);
+    wait_lgkm<NBH>();  // every read of slice sl is in
     __builtin_amdgcn_sched_barrier(0);
     mma_rows(0, fa, fb);
     __builtin_amdgcn_sched_barrier(0);
-    rd4lo(a_addr(nx), fa);
-    asm volatile("s_waitcnt lgkmcnt(12)" ::: "memory");  // A[4-7](s) in
+    rd4lo(aad, fa);
+    rd_b(bad, 4, nbuf);
+    wait_lgkm<4 + NBH>();  // A[4-7](s) in
     __builtin_amdgcn_sched_barrier(0);
     mma_rows(4, fa, fb);
     __builtin_amdgcn_sched_barrier(0);
-    rd4hi(a_addr(nx), fa);
+    rd4hi(aad, fa);
   };
 
   diag_stamp(p, 0);
@@ -151,7 +202,8 @@ __global__ __launch_bounds__(256, 1) void gemm_quad(GemmP p) {
     for (int sl = 0; sl < npre; ++sl) issue(sl);
     wait_newer<G, S - 2>(npre - 1);  // own share of slice 0 landed
     lds_barrier();                   // everyone's
-    rd(b_addr(0), fb0);
+    rd_b(b_addr(0), 0, fb0);
+    rd_b(b_addr(0), 4, fb0);
     rd4lo(a_addr(0), fa);
     rd4hi(a_addr(0), fa);
     for (int sl = 0; sl < nsl; sl += 2) {  // nsl even (host: K % 64 == 0)
@@ -180,9 +232,14 @@ __global__ __launch_bounds__(256, 1) void gemm_quad(GemmP p) {
 
 namespace eag {
 int g_quad_slots = 5;
-int launch_quad(GemmP& p, dim3 grid, hipStream_t st) {
-  if (g_quad_slots == 4) hipLaunchKernelGGL((gemm_quad<4>), grid, dim3(256), 0, st, p);
-  else hipLaunchKernelGGL((gemm_quad<5>), grid, dim3(256), 0, st, p);
+int launch_quad(GemmP& p, int b_k, dim3 grid, hipStream_t st) {
+  if (b_k) {
+    if (g_quad_slots == 4) hipLaunchKernelGGL((gemm_quad<4, true>), grid, dim3(256), 0, st, p);
+    else hipLaunchKernelGGL((gemm_quad<5, true>), grid, dim3(256), 0, st, p);
+  } else {
+    if (g_quad_slots == 4) hipLaunchKernelGGL((gemm_quad<4, false>), grid, dim3(256), 0, st, p);
+    else hipLaunchKernelGGL((gemm_quad<5, false>), grid, dim3(256), 0, st, p);
+  }
   EA_LAUNCH_CHECK();
   return 0;
 }

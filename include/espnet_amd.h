@@ -150,9 +150,10 @@ int ea_gemm_set_skinny(int max_m);
  * the few-row limit (the training decoder's B*(L+1) tokens); 0 = off (EA_GEMM_ROWS32).
  * Process-wide; A/B switch. */
 int ea_gemm_set_rows32(int max_m);
-/* 256x256 bf16 tiles with K-major A and B (K % 64 == 0) on gemm_quad — four waves of 128 x 128
- * (a third less LDS fragment traffic per MFMA than gemm_pipe's eight waves of 128 x 64), ring of
- * `slots` (4 or 5) 32-deep slices.  on = 0: gemm_pipe (EA_GEMM_QUAD).  Process-wide; A/B switch. */
+/* 256x256 bf16 tiles with K-major A (K % 64 == 0) on gemm_quad — four waves of 128 x 128 (a
+ * third less LDS fragment traffic per MFMA than gemm_pipe's eight waves of 128 x 64), ring of
+ * `slots` (4 or 5) 32-deep slices.  on: bit 1 = K-major B, bit 2 = MN-major B too; 0 = gemm_pipe
+ * (EA_GEMM_QUAD).  Process-wide; A/B switch. */
 int ea_gemm_set_quad(int on, int slots);
 /* C = epi(LayerNorm(x) . W^T): x f32 (M x K, ldx, rows 16-B aligned), gamma / beta f32 (K),
  * W bf16 (N x K, ldw) — the LayerNorm (eps) computed per row inside the few-row GEMM

@@ -9,13 +9,14 @@ import torch  # noqa: E402
 from espnet_amd import _lib as L  # noqa: E402
 from espnet_amd import hip_ops as ops  # noqa: E402
 
-SHAPES = [(4096, 4096, 4096, "store"), (7968, 2048, 512, "act_drop"), (7968, 1536, 512, "bias"),
-          (7968, 2048, 512, "store"), (151392, 512, 4608, "store"), (7968, 6144, 512, "bias")]
+SHAPES = [(4096, 4096, 4096, "store", 1), (7968, 2048, 512, "act_drop", 1), (7968, 1536, 512, "bias", 1),
+          (7968, 2048, 512, "store", 1), (151392, 512, 4608, "store", 1), (7968, 6144, 512, "bias", 1),
+          (7968, 2048, 512, "store", 0), (4096, 4096, 4096, "store", 0)]
 
 
-def run(M, N, K, kind, reps=20):
+def run(M, N, K, kind, bk, reps=20):
     A = torch.randn(M, K, device="cuda").bfloat16()
-    W = torch.randn(N, K, device="cuda").bfloat16()
+    W = torch.randn(N, K, device="cuda").bfloat16() if bk else torch.randn(K, N, device="cuda").bfloat16()
     b = torch.randn(N, device="cuda")
     C = torch.empty(M, N, device="cuda").bfloat16()
     if kind == "act_drop":
@@ -25,7 +26,8 @@ def run(M, N, K, kind, reps=20):
         epi = ops.make_epi(bias=b)
     else:
         epi = ops.make_epi()
-    f = lambda: ops.gemm(A, W, C, M=M, N=N, K=K, a_kmajor=1, b_kmajor=1, lda=K, ldb=K, ldc=N, epi=epi)  # noqa: E731
+    f = lambda: ops.gemm(A, W, C, M=M, N=N, K=K, a_kmajor=1, b_kmajor=bk, lda=K, ldb=K if bk else N, ldc=N,  # noqa: E731
+                         epi=epi)
     for _ in range(3):
         f()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -39,12 +41,12 @@ def run(M, N, K, kind, reps=20):
 
 
 L.lib.ea_gemm_set_tile(256, 256)
-for M, N, K, kind in SHAPES:
+for M, N, K, kind, bk in SHAPES:
     out = []
-    for name, q, s in (("pipe", 0, 5), ("quad5", 1, 5), ("quad4", 1, 4)):
+    for name, q, s in (("pipe", 0, 5), ("quad5", 3, 5), ("quad4", 3, 4)):
         L.lib.ea_gemm_set_quad(q, s)
-        us, tf = run(M, N, K, kind)
+        us, tf = run(M, N, K, kind, bk)
         out.append(f"{name} {us:7.1f} us {tf:6.0f} TF/s")
     L.lib.ea_gemm_set_quad(0, 5)
-    print(f"{M}x{N}x{K} {kind:8s}: " + " | ".join(out), flush=True)
+    print(f"{M}x{N}x{K} {kind:8s} bk={bk}: " + " | ".join(out), flush=True)
 L.lib.ea_gemm_set_tile(0, 0)

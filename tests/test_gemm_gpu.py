@@ -597,34 +597,35 @@ def test_gemm_ln_vs_fp64(MNK):
     torch.testing.assert_close(C[:, :N], C0, atol=2e-2, rtol=1e-2)
 
 
+@pytest.mark.parametrize("b_k", [1, 0])
 @pytest.mark.parametrize("slots", [4, 5])
-@pytest.mark.parametrize("MNK", [(7968, 2048, 512), (300, 520, 128), (513, 260, 2048), (256, 256, 64)])
-def test_gemm_quad_vs_fp64(slots, MNK):
-    """gemm_quad (256x256 tiles, four waves of 128 x 128, K-major A and B): against fp64 with
-    the STORE / RESID / ACT epilogues, M and N edges, bf16 and f32 outputs."""
+@pytest.mark.parametrize("MNK", [(7968, 2048, 512), (300, 520, 128), (513, 264, 2048), (256, 256, 64)])
+def test_gemm_quad_vs_fp64(slots, MNK, b_k):
+    """gemm_quad (256x256 tiles, four waves of 128 x 128, K-major A; K-major or MN-major B):
+    against fp64 with the STORE / RESID / ACT epilogues, M and N edges, bf16 and f32 outputs."""
     ops, L = _ops()
     M, N, K = MNK
     g = torch.Generator().manual_seed(M + N + K + slots)
     A = mk((M, K + 8), torch.bfloat16, g)
-    B = mk((N, K + 8), torch.bfloat16, g, 0.1)
-    L.lib.ea_gemm_set_quad(1, slots)
+    B = mk((N, K + 8) if b_k else (K, N + 8), torch.bfloat16, g, 0.1)
+    L.lib.ea_gemm_set_quad(3, slots)
     L.lib.ea_gemm_set_tile(256, 256)
     try:
-        ref = ref_mm(A, B, 1, 1, M, N, K)
+        ref = ref_mm(A, B, 1, b_k, M, N, K)
         C = torch.full((M, N + 4), 7.0, device="cuda")
-        ops.gemm(A, B, C, M=M, N=N, K=K, a_kmajor=1, b_kmajor=1, lda=A.stride(0), ldb=B.stride(0), ldc=C.stride(0))
+        ops.gemm(A, B, C, M=M, N=N, K=K, a_kmajor=1, b_kmajor=b_k, lda=A.stride(0), ldb=B.stride(0), ldc=C.stride(0))
         torch.testing.assert_close(C[:, :N].double().cpu(), ref, atol=2e-3 * K ** 0.5, rtol=2e-3)
         assert (C[:, N:] == 7.0).all()
         bias = mk((N,), torch.float32, g)
         R = torch.randn(M, N, generator=g).cuda()
         R0 = R.clone()
-        ops.gemm(A, B, R, M=M, N=N, K=K, a_kmajor=1, b_kmajor=1, lda=A.stride(0), ldb=B.stride(0), ldc=N,
+        ops.gemm(A, B, R, M=M, N=N, K=K, a_kmajor=1, b_kmajor=b_k, lda=A.stride(0), ldb=B.stride(0), ldc=N,
                  epi=ops.make_epi(L.EPI_RESID, bias=bias, resid=R, rscale=0.5))
         torch.testing.assert_close(R.double().cpu(), R0.double().cpu() + 0.5 * (ref + bias.double().cpu()),
                                    atol=2e-3 * K ** 0.5, rtol=2e-3)
         aux = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
         Ca = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
-        ops.gemm(A, B, Ca, M=M, N=N, K=K, a_kmajor=1, b_kmajor=1, lda=A.stride(0), ldb=B.stride(0), ldc=N,
+        ops.gemm(A, B, Ca, M=M, N=N, K=K, a_kmajor=1, b_kmajor=b_k, lda=A.stride(0), ldb=B.stride(0), ldc=N,
                  epi=ops.make_epi(L.EPI_ACT, bias=bias, act=L.ACT_SWISH, aux=aux))
         h = ref + bias.double().cpu()
         torch.testing.assert_close(aux.double().cpu(), h, atol=3e-2, rtol=2e-2)
