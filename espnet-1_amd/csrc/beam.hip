@@ -120,23 +120,17 @@ __global__ __launch_bounds__(PB_NT) void prebeam_kernel(int V, const float* __re
     if (lane == 0) lst[wv * PB_PMAX + r] = b;
   }
   __syncthreads();
-  if (wv == 0) {  // (wave 0 alone: a chosen entry is retired in place)
-    const int nl = PB_NW * P;
+  if (wv == 0) {  // 16-way merge of the waves' sorted lists: lane l < PB_NW holds list l's head
     int* out = cand + (long)h * (P + 1);
+    int hp = 0;
+    Best head = lane < PB_NW ? lst[lane * PB_PMAX] : Best{-INFINITY, 0x7fffffff};
     for (int r = 0; r < P; ++r) {
-      Best b{-INFINITY, 0x7fffffff};
-      int at = -1;
-      for (int q = lane; q < nl; q += 64) {
-        const Best c = lst[(q / P) * PB_PMAX + (q % P)];
-        if (c.i != 0x7fffffff && better(c.v, c.i, b.v, b.i)) {
-          b = c;
-          at = (q / P) * PB_PMAX + (q % P);
-        }
-      }
-      const Best m = wave_argmax(b);
-      if (at >= 0 && m.i == b.i) lst[at].i = 0x7fffffff;  // each token is in one list, once
-      __builtin_amdgcn_wave_barrier();
+      const Best m = wave_argmax(head);
       if (lane == 0) out[r] = m.i;
+      if (lane < PB_NW && head.i == m.i && m.i != 0x7fffffff) {  // tokens are distinct across lists
+        ++hp;
+        head = hp < P ? lst[lane * PB_PMAX + hp] : Best{-INFINITY, 0x7fffffff};
+      }
     }
     if (lane == 0) out[P] = eos;
   }
