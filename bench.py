@@ -22,6 +22,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "espnet-1_amd"))
 sys.path.insert(0, ROOT)
 
+import espnet_amd  # noqa: E402,F401  (process-group settings for the captured DP step, before any init)
 import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
