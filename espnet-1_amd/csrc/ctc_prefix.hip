@@ -82,7 +82,7 @@ __global__ __launch_bounds__(64) void ctc_prefix_score_kernel(int T, int V, int 
                                                               const int* __restrict__ ol_arr, int ol_uniform,
                                                               const int* __restrict__ last_arr,
                                                               const int* __restrict__ cand_arr, float* __restrict__ log_psi,
-                                                              float* __restrict__ r_new) {
+                                                              float* __restrict__ r_new, int wstart, int wend) {
   const int idx = blockIdx.x * 64 + threadIdx.x;
   if (idx >= n_hyp * n_cand) return;
   const int h = idx / n_cand;
@@ -92,25 +92,24 @@ __global__ __launch_bounds__(64) void ctc_prefix_score_kernel(int T, int V, int 
   const float* rp = (const float*)r_prev_ptr[h];
   float* r = r_new + (long)idx * T * 2;
   const bool same = ol > 0 && c == last;  // log_phi = r^b(g) for a repeated label, else r^n + r^b
-  const int start = max(ol, 1);
-  for (int t = 0; t < min(start, T); ++t) { r[2 * t] = kLogZero; r[2 * t + 1] = kLogZero; }
-  float psi;
-  if (ol == 0) {
-    r[0] = logp[c];
-    psi = r[0];
-  } else {
-    psi = kLogZero;  // r[ol-1, 0]
-  }
-  float rn = start - 1 < T ? r[2 * (start - 1)] : kLogZero, rb = start - 1 < T ? r[2 * (start - 1) + 1] : kLogZero;
+  // frames [start, end): max(ol, 1) .. T, or the attention window (wstart > 0)
+  const int end = wend > 0 ? min(wend, T) : T;
+  const int start = min(wstart > 0 ? wstart : max(ol, 1), max(end, 1));
+  for (int t = 0; t < T; ++t)
+    if (t < start || t >= end) { r[2 * t] = kLogZero; r[2 * t + 1] = kLogZero; }
+  if (ol == 0) r[0] = logp[c];
+  // r[start-1] (logzero but for the empty prefix's first frame)
+  float psi = ol == 0 && start == 1 ? logp[c] : kLogZero;
+  float rn = psi, rb = kLogZero;
   // frames in chunks of CH: the chunk's loads (and its log_phi values, which do not depend on
   // the recursion) are issued together, so one memory latency is exposed per chunk instead of
   // one per frame; the serial recursion then runs from registers
   constexpr int CH = 16;
-  for (int t0 = start; t0 < T; t0 += CH) {
+  for (int t0 = start; t0 < end; t0 += CH) {
     float xc[CH], xb[CH], ph[CH];
 #pragma unroll
     for (int k = 0; k < CH; ++k) {
-      const int t = min(t0 + k, T - 1);
+      const int t = min(t0 + k, end - 1);
       xc[k] = logp[(long)t * V + c];
       xb[k] = logp[(long)t * V + blank];
       const float a = rp[2 * (t - 1)], b = rp[2 * (t - 1) + 1];
@@ -119,7 +118,7 @@ __global__ __launch_bounds__(64) void ctc_prefix_score_kernel(int T, int V, int 
 #pragma unroll
     for (int k = 0; k < CH; ++k) {
       const int t = t0 + k;
-      if (t < T) {
+      if (t < end) {
         const float nrn = np_logaddexpf(rn, ph[k]) + xc[k];
         const float nrb = np_logaddexpf(rn, rb) + xb[k];
         psi = np_logaddexpf(psi, ph[k] + xc[k]);
@@ -149,7 +148,8 @@ __global__ __launch_bounds__(256) void ctc_prefix_score2_kernel(int T, int V, in
                                                                 const int* __restrict__ ol_arr, int ol_uniform,
                                                                 const int* __restrict__ last_arr,
                                                                 const int* __restrict__ cand_arr,
-                                                                float* __restrict__ log_psi, float* __restrict__ r_new) {
+                                                                float* __restrict__ log_psi, float* __restrict__ r_new,
+                                                                int wstart, int wend) {
   extern __shared__ float sm[];
   constexpr int XS = CH + 1, RS = 2 * CH + 1;  // padded row strides (bank spread)
   float* phi = sm;               // [CH]: lae(r^n, r^b) of the parent at frame t-1
@@ -163,11 +163,18 @@ __global__ __launch_bounds__(256) void ctc_prefix_score2_kernel(int T, int V, in
   const float* rp = (const float*)r_prev_ptr[h];
   const int* cand = cand_arr + (long)h * n_cand;
   float* rout = r_new + (long)h * n_cand * T * 2;
-  const int start = max(ol, 1);
+  // frames [start, end): max(ol, 1) .. T, or the attention window (wstart > 0)
+  const int end = wend > 0 ? min(wend, T) : T;
+  const int start = min(wstart > 0 ? wstart : max(ol, 1), max(end, 1));
   // frames before start: logzero (r[0] = (logp[c], logzero) for the empty prefix)
   for (int q = tid; q < n_cand * 2 * min(start, T); q += 256) {
     const int k = q / (2 * min(start, T)), e = q - k * 2 * min(start, T);
     rout[(long)k * T * 2 + e] = (ol == 0 && e == 0) ? logp[cand[k]] : kLogZero;
+  }
+  // frames from end on (a window ending before the utterance): logzero
+  for (int q = tid; q < n_cand * 2 * (T - end); q += 256) {
+    const int k = q / (2 * (T - end)), e = q - k * 2 * (T - end);
+    rout[(long)k * T * 2 + 2 * end + e] = kLogZero;
   }
   const int k = tid;
   const bool act = k < n_cand;
@@ -175,10 +182,11 @@ __global__ __launch_bounds__(256) void ctc_prefix_score2_kernel(int T, int V, in
   __shared__ int cl[256];  // the candidates (n_cand <= 256), for the emission gather
   if (act) cl[k] = c;
   const bool same = ol > 0 && c == last;
-  float psi = act && ol == 0 ? logp[c] : kLogZero;
-  float rn = (start - 1 < T && ol == 0 && act) ? logp[c] : kLogZero, rb = kLogZero;
-  for (int t0 = start; t0 < T; t0 += CH) {
-    const int nf = min(CH, T - t0);
+  // r[start-1] (logzero but for the empty prefix's first frame)
+  float psi = act && ol == 0 && start == 1 ? logp[c] : kLogZero;
+  float rn = psi, rb = kLogZero;
+  for (int t0 = start; t0 < end; t0 += CH) {
+    const int nf = min(CH, end - t0);
     __syncthreads();  // the previous chunk's rows are written out
     for (int i = tid; i < nf; i += 256) {
       const int t = t0 + i;
@@ -244,17 +252,17 @@ __global__ __launch_bounds__(256) void ctc_prefix_score2_kernel(int T, int V, in
 
 int launch_prefix2(int T, int V, int blank, int eos, int n_hyp, int n_cand, const float* logp,
                    const unsigned long long* r_prev, const int* ol_arr, int ol_uniform, const int* last,
-                   const int* cand, float* log_psi, float* r_new, hipStream_t st) {
+                   const int* cand, float* log_psi, float* r_new, hipStream_t st, int wstart = 0, int wend = 0) {
   auto bytes = [&](int ch) { return (size_t)(3 * ch + n_cand * (ch + 1) + n_cand * (2 * ch + 1)) * 4; };
   if (bytes(256) <= 64 * 1024)
     hipLaunchKernelGGL(ctc_prefix_score2_kernel<256>, dim3(n_hyp), dim3(256), bytes(256), st, T, V, blank, eos, n_cand,
-                       logp, r_prev, ol_arr, ol_uniform, last, cand, log_psi, r_new);
+                       logp, r_prev, ol_arr, ol_uniform, last, cand, log_psi, r_new, wstart, wend);
   else if (bytes(64) <= 64 * 1024)
     hipLaunchKernelGGL(ctc_prefix_score2_kernel<64>, dim3(n_hyp), dim3(256), bytes(64), st, T, V, blank, eos, n_cand,
-                       logp, r_prev, ol_arr, ol_uniform, last, cand, log_psi, r_new);
+                       logp, r_prev, ol_arr, ol_uniform, last, cand, log_psi, r_new, wstart, wend);
   else
     hipLaunchKernelGGL(ctc_prefix_score_kernel, dim3(ea_cdiv(n_hyp * n_cand, 64)), dim3(64), 0, st, T, V, blank, eos,
-                       n_hyp, n_cand, logp, r_prev, ol_arr, ol_uniform, last, cand, log_psi, r_new);
+                       n_hyp, n_cand, logp, r_prev, ol_arr, ol_uniform, last, cand, log_psi, r_new, wstart, wend);
   return 0;
 }
 
@@ -286,19 +294,60 @@ extern "C" int ea_softmax_rows(long rows, int V, const float* logits, long ld, f
   return 0;
 }
 
+static int prefix_score_meta(int T, int V, int blank, int eos, int n_hyp, int n_cand, const float* logp,
+                             const unsigned long long* r_prev, const int* meta, float* log_psi, float* r_new,
+                             int wstart, int wend, hipStream_t st) {
+  if (n_hyp * n_cand == 0) return 0;
+  if (n_cand <= 256)
+    launch_prefix2(T, V, blank, eos, n_hyp, n_cand, logp, r_prev, meta, 0, meta + n_hyp, meta + 2 * n_hyp, log_psi,
+                   r_new, st, wstart, wend);
+  else
+    hipLaunchKernelGGL(ctc_prefix_score_kernel, dim3(ea_cdiv(n_hyp * n_cand, 64)), dim3(64), 0, st, T, V, blank,
+                       eos, n_hyp, n_cand, logp, r_prev, meta, 0, meta + n_hyp, meta + 2 * n_hyp, log_psi, r_new,
+                       wstart, wend);
+  EA_LAUNCH_CHECK();
+  return 0;
+}
+
 extern "C" int ea_ctc_prefix_score(int T, int V, int blank, int eos, int n_hyp, int n_cand, const float* logp,
                                    const unsigned long long* r_prev, const int* meta, float* log_psi, float* r_new,
                                    void* stream) {
   EA_ENTRY();
   EA_CHECK_ARG(T >= 1 && V >= 1 && n_hyp >= 0 && n_cand >= 0);
-  if (n_hyp * n_cand == 0) return 0;
-  if (n_cand <= 256)
-    launch_prefix2(T, V, blank, eos, n_hyp, n_cand, logp, r_prev, meta, 0, meta + n_hyp, meta + 2 * n_hyp, log_psi,
-                   r_new, (hipStream_t)stream);
-  else
-    hipLaunchKernelGGL(ctc_prefix_score_kernel, dim3(ea_cdiv(n_hyp * n_cand, 64)), dim3(64), 0, (hipStream_t)stream,
-                       T, V, blank, eos, n_hyp, n_cand, logp, r_prev, meta, 0, meta + n_hyp, meta + 2 * n_hyp,
-                       log_psi, r_new);
+  return prefix_score_meta(T, V, blank, eos, n_hyp, n_cand, logp, r_prev, meta, log_psi, r_new, 0, 0,
+                           (hipStream_t)stream);
+}
+
+extern "C" int ea_ctc_prefix_score_win(int T, int V, int blank, int eos, int n_hyp, int n_cand, const float* logp,
+                                       const unsigned long long* r_prev, const int* meta, int start, int end,
+                                       float* log_psi, float* r_new, void* stream) {
+  EA_ENTRY();
+  EA_CHECK_ARG(T >= 1 && V >= 1 && n_hyp >= 0 && n_cand >= 0 && start >= 1 && end >= 1);
+  return prefix_score_meta(T, V, blank, eos, n_hyp, n_cand, logp, r_prev, meta, log_psi, r_new, start, end,
+                           (hipStream_t)stream);
+}
+
+// streaming: the forward variables of a hypothesis over T_old frames extended to T frames —
+// r^n logzero, r^b accumulating the blank emissions in frame order (ctc_prefix_score.py:244-269)
+__global__ void ctc_prefix_extend_kernel(int T_old, int T, int V, int blank, const float* __restrict__ logp,
+                                         const float* __restrict__ r_old, float* __restrict__ r) {
+  for (int t = 0; t < T_old; ++t) { r[2 * t] = r_old[2 * t]; r[2 * t + 1] = r_old[2 * t + 1]; }
+  const int start = max(T_old, 1);
+  if (T_old == 0) { r[0] = kLogZero; r[1] = kLogZero; }
+  float acc = r[2 * (start - 1) + 1];
+  for (int t = start; t < T; ++t) {
+    acc = acc + logp[(long)t * V + blank];
+    r[2 * t] = kLogZero;
+    r[2 * t + 1] = acc;
+  }
+}
+
+extern "C" int ea_ctc_prefix_extend(int T_old, int T, int V, int blank, const float* logp, const float* r_old,
+                                    float* r, void* stream) {
+  EA_ENTRY();
+  EA_CHECK_ARG(T_old >= 0 && T >= T_old && T >= 1 && V >= 1 && blank >= 0 && blank < V);
+  hipLaunchKernelGGL(ctc_prefix_extend_kernel, dim3(1), dim3(1), 0, (hipStream_t)stream, T_old, T, V, blank, logp,
+                     r_old, r);
   EA_LAUNCH_CHECK();
   return 0;
 }
@@ -315,7 +364,7 @@ extern "C" int ea_ctc_prefix_score_dev(int T, int V, int blank, int eos, int n_h
   else
     hipLaunchKernelGGL(ctc_prefix_score_kernel, dim3(ea_cdiv(n_hyp * n_cand, 64)), dim3(64), 0, (hipStream_t)stream,
                        T, V, blank, eos, n_hyp, n_cand, logp, r_prev, (const int*)nullptr, out_len, last, cand,
-                       log_psi, r_new);
+                       log_psi, r_new, 0, 0);
   EA_LAUNCH_CHECK();
   return 0;
 }

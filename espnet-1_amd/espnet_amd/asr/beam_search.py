@@ -121,6 +121,16 @@ class CTCPrefixScorer:
                        if state[0] is not None else None)
         return self.impl(y, batch_state, ids)
 
+    def extend_prob(self, x: torch.Tensor):
+        """ctc.py:128-139 (streaming decoding): the encoder output so far -> the vectorised
+        scorer's posteriors extended to its frames."""
+        logp = self.ctc.log_softmax(x.unsqueeze(0)).float()
+        self.impl.extend_prob(logp)
+
+    def extend_state(self, state):
+        """ctc.py:141-158: every hypothesis's state extended to the new frames."""
+        return [self.impl.extend_state(s) for s in state]
+
     def final_score(self, state):
         return 0.0
 

@@ -14,8 +14,10 @@ utterance is one thread of the CTC prefix kernel (csrc/ctc_prefix.hip, one launc
 utterance and step), walking the utterance's own frames only — the reference's padded frames
 (logzero labels, log 1 blank) contribute nothing above f32 rounding, so they are not
 visited.  A hypothesis's state is its (T_b, 2) forward variables in HBM.  Attention-windowed
-scoring (margin > 0) and streaming extension (extend_prob / extend_state) are outside the
-recipes' decoding and raise NotImplementedError.
+scoring (margin > 0 with att_w, :143-153) runs the kernel over the window's frames only
+(ea_ctc_prefix_score_win); streaming decoding's extend_prob / extend_state (:222-269) append
+frames to the posteriors and extend a hypothesis's forward variables with the blank recursion
+(ea_ctc_prefix_extend).
 """
 from __future__ import annotations
 
@@ -31,8 +33,6 @@ LOGZERO = -10000000000.0
 
 class CTCPrefixScoreTH:
     def __init__(self, x: torch.Tensor, xlens, blank: int, eos: int, margin: int = 0):
-        if margin > 0:
-            raise NotImplementedError("CTCPrefixScoreTH: attention-windowed scoring (margin > 0)")
         if x.device.type != "cuda":
             raise RuntimeError("CTCPrefixScoreTH runs on the HIP device (x must be a device tensor)")
         self.logzero = LOGZERO
@@ -46,12 +46,18 @@ class CTCPrefixScoreTH:
                 x[i, l:, :] = self.logzero
                 x[i, l:, self.blank] = 0
         self.logp = [x[b, :l].float().contiguous() for b, l in enumerate(self.xlens)]
+        self._init_r0()
+        self.scoring_num = 0
+        self.margin = int(margin)
+        if self.margin > 0:  # frame positions for the attention-weighted centre (:57-62)
+            self.frame_ids = torch.arange(self.input_length, dtype=self.dtype, device=self.device)
+
+    def _init_r0(self):
         self.r0 = []
         for lp in self.logp:  # initial state: (logzero, cumulative blank log-probability)
             r = torch.full((lp.shape[0], 2), self.logzero, dtype=torch.float32, device=self.device)
             r[:, 1] = torch.cumsum(lp[:, self.blank], 0)
             self.r0.append(r)
-        self.scoring_num = 0
 
     def __call__(self, y: List[torch.Tensor], state, scoring_ids=None, att_w=None):
         n_bh = len(y)
@@ -61,8 +67,18 @@ class CTCPrefixScoreTH:
         if state is None:
             r_prev = [self.r0[i // n_hyps] for i in range(n_bh)]
             s_prev = torch.zeros(n_bh, 1, device=self.device)
+            f_min_prev, f_max_prev = 0, 1
         else:
-            r_prev, s_prev = state[0], state[1]
+            r_prev, s_prev, f_min_prev, f_max_prev = state[0], state[1], state[2], state[3]
+        # the attention window (:143-153): frames [start, end) around the attended frames
+        win = None
+        if att_w is not None and self.margin > 0:
+            f_arg = torch.matmul(att_w, self.frame_ids)
+            f_min = max(int(f_arg.min().cpu()), f_min_prev)
+            f_max = max(int(f_arg.max().cpu()), f_max_prev)
+            win = (min(f_max_prev, max(f_min - self.margin, out_len, 1)), min(f_max + self.margin, self.input_length))
+        else:
+            f_min = f_max = 0
         if scoring_ids is not None:
             cand = scoring_ids.to(torch.int64).cpu()
             self.scoring_num = int(cand.shape[-1])
@@ -87,14 +103,19 @@ class CTCPrefixScoreTH:
             meta_d, ptrs_d = meta.to(self.device), ptrs.to(self.device)
             psi = torch.empty(n_hyps * nc, device=self.device)
             rn = torch.empty(n_hyps, nc, T, 2, device=self.device)
-            lib.ea_ctc_prefix_score(T, self.odim, self.blank, self.eos, n_hyps, nc, self.logp[b].data_ptr(),
-                                    ptrs_d.data_ptr(), meta_d.data_ptr(), psi.data_ptr(), rn.data_ptr(),
-                                    ops.stream())
+            if win is None:
+                lib.ea_ctc_prefix_score(T, self.odim, self.blank, self.eos, n_hyps, nc, self.logp[b].data_ptr(),
+                                        ptrs_d.data_ptr(), meta_d.data_ptr(), psi.data_ptr(), rn.data_ptr(),
+                                        ops.stream())
+            else:  # (an utterance shorter than the window's end: its own frames only)
+                lib.ea_ctc_prefix_score_win(T, self.odim, self.blank, self.eos, n_hyps, nc, self.logp[b].data_ptr(),
+                                            ptrs_d.data_ptr(), meta_d.data_ptr(), win[0], min(win[1], T),
+                                            psi.data_ptr(), rn.data_ptr(), ops.stream())
             idx = cand[b * n_hyps:(b + 1) * n_hyps].to(self.device)
             log_psi[b * n_hyps:(b + 1) * n_hyps].scatter_(1, idx, psi.view(n_hyps, nc))
             r_new.append(rn)
         log_psi[:, self.blank] = self.logzero
-        return log_psi - s_prev, (r_new, log_psi, 0, 0, cand[:, :nsc])
+        return log_psi - s_prev, (r_new, log_psi, f_min, f_max, cand[:, :nsc])
 
     def index_select_state(self, state, best_ids):
         """best_ids (B, W) in each utterance's (n_hyps * O) space -> the selected hypotheses'
@@ -119,7 +140,32 @@ class CTCPrefixScoreTH:
         return r_sel, s_new, f_min, f_max
 
     def extend_prob(self, x):
-        raise NotImplementedError("CTCPrefixScoreTH.extend_prob: streaming decoding is not built")
+        """Streaming decoding (:222-242): x (1, T', O) log-posteriors of the utterance so far;
+        when longer than the frames held, the new frames are appended (the frames already held
+        are kept as they are)."""
+        if x.shape[1] <= self.input_length:
+            return
+        if self.batch != 1:
+            raise ValueError("CTCPrefixScoreTH.extend_prob: streaming decoding holds one utterance")
+        new = x[0, self.input_length:].to(self.device).float()
+        self.logp = [torch.cat([self.logp[0][:self.input_length], new]).contiguous()]
+        self.input_length = int(x.shape[1])
+        self.xlens = [self.input_length]
+        self._init_r0()
+        if self.margin > 0:
+            self.frame_ids = torch.arange(self.input_length, dtype=self.dtype, device=self.device)
 
     def extend_state(self, state):
-        raise NotImplementedError("CTCPrefixScoreTH.extend_state: streaming decoding is not built")
+        """Streaming decoding (:244-269): one hypothesis's state (r (T_old, 2), prefix scores,
+        f_min, f_max) with r extended to the frames extend_prob appended: r^n logzero, r^b the
+        blank recursion continued frame by frame."""
+        if state is None:
+            return state
+        r_prev, s_prev, f_min_prev, f_max_prev = state
+        T_old, T = int(r_prev.shape[0]), self.input_length
+        if T_old >= T:
+            return state
+        r = torch.empty(T, 2, dtype=torch.float32, device=self.device)
+        lib.ea_ctc_prefix_extend(T_old, T, self.odim, self.blank, self.logp[0].data_ptr(),
+                                 r_prev.contiguous().data_ptr(), r.data_ptr(), ops.stream())
+        return (r, s_prev, f_min_prev, f_max_prev)

@@ -220,6 +220,11 @@ GRAD_READY = None  # callable(prefix): a block's parameter gradients are final (
 STREAM_WGRAD = int(os.environ.get("EA_STREAM_WGRAD", "0"))
 # the end-of-pass reduction flush on the side stream beside the grouped GEMM (EA_REDUCE_SIDE=0: serial)
 REDUCE_SIDE = os.environ.get("EA_REDUCE_SIDE", "1") != "0"
+# single process, deferred pass: the main stream joins the side stream after every block
+# (EA_LAYER_JOIN=1) or only once, at the end of the pass (0).  The per-block side work left
+# under deferral (the linear_pos product dBD^T (q+v), read by the deferred flush) needs no
+# earlier join; each join is a cross-queue dependency of the captured graph, ~10 us idle
+LAYER_JOIN = os.environ.get("EA_LAYER_JOIN", "1") != "0"
 _STREAM_COUNT = [0]
 
 
@@ -240,6 +245,8 @@ def grad_ready(bound):
             with wgrad(*deferred_tensors()):
                 flush_deferred()
         return
+    if not LAYER_JOIN and (WGRAD_Q.active or REDUCE_Q.active):
+        return  # deferred_wgrad's exit joins the side stream before anything reads its results
     join_wgrad()
 
 
@@ -378,7 +385,7 @@ def linear(x, w, out, *, epi: Epilogue = None):
 # transpose after every optimizer step (and shadow refresh), lets those GEMMs read both
 # operands K-major.  EA_WT_SHADOW=0 turns it off (A/B).
 WT_SHADOW = os.environ.get("EA_WT_SHADOW", "1") != "0"
-WT_MAX_KIN = 512
+WT_MAX_KIN = int(os.environ.get("EA_WT_MAX_KIN", "512"))
 TSHADOWS = {}  # arena shadow storage pointer -> weakref(TransposedShadow) (the arena owns it)
 
 
@@ -691,6 +698,8 @@ class deferred_wgrad:
         WGRAD_Q.active, REDUCE_Q.active = self.prev
         _STREAM_COUNT[0] = 0
         if exc[0] is None:
+            if GRAD_READY is None and not LAYER_JOIN:
+                join_wgrad()  # the queued products may read what the side stream wrote
             if GRAD_READY is None and OVERLAP_WGRAD and REDUCE_SIDE and torch.cuda.is_available():
                 # the pass's reductions (bias column sums, LayerNorm parameter sums: bandwidth-
                 # bound) on the side stream beside the grouped weight-gradient GEMM (MFMA-bound)

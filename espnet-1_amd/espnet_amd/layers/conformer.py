@@ -44,6 +44,10 @@ def attn_keep_words(B, H, T1, T2):
 
 # depthwise-conv dw / dbias partials deferred into the grouped reduce (EA_DWCONV_DEFER=1; measured neutral, off)
 DWCONV_DEFER = os.environ.get("EA_DWCONV_DEFER", "0") == "1"
+# the attention block's input-gradient GEMM issued before the linear_pos product forks onto the
+# side stream (EA_DPP_LATE=1) instead of after it: the graph keeps the captured order of a
+# node's dependents when it spreads them over queues
+DPP_LATE = os.environ.get("EA_DPP_LATE", "0") == "1"
 
 class PositionwiseFeedForward(nn.Module):
     """positionwise_feed_forward.py:12-32 (w_2(dropout(act(w_1 x))))."""
@@ -400,6 +404,11 @@ class ConformerBlockFn(torch.autograd.Function):
             ops.colsum(dqv, b.g(A + "pos_bias_v", shape=(d,)))
             lib.ea_add_2d(N, d, dqv.data_ptr(), ops.dt(dqv), d, dqkv.data_ptr(), ops.dt(dqkv), 3 * d, 1.0,
                           ops.stream())
+        qkv_w = b.w(A + "linear_q.weight", A + "linear_k.weight", A + "linear_v.weight", shape=(3 * d, d))
+        dxn2 = None
+        if DPP_LATE:  # the input gradient captured ahead of the side-stream product below
+            dxn2 = empty(N, d, dtype=cd, device=dev)
+            ops.linear_dx(dqkv, qkv_w, dxn2)
         # linear_pos: dp[h] = sum_b dBD[h][b]^T qv[b, :, h]  (K = B*T), dWpos = dp^T pos; with the
         # shifted layout the GEMM runs over every physical column and rows [shift, shift + P2) of
         # its output are dp
@@ -410,13 +419,13 @@ class ConformerBlockFn(torch.autograd.Function):
                      batch=1, nh=H, sA=(0, B * T * ldbd), sB=(0, dk), sC=(0, dk))
             ops.linear_dw(dpp_full[shift:], pos, b.g(A + "linear_pos.weight"), accumulate=True)
         del dbd
-        qkv_w = b.w(A + "linear_q.weight", A + "linear_k.weight", A + "linear_v.weight", shape=(3 * d, d))
         with ops.wgrad(dqkv, xn2):
             ops.colsum(dqkv, b.g(A + "linear_q.bias", A + "linear_k.bias", A + "linear_v.bias", shape=(3 * d,)))
             ops.linear_dw(dqkv, xn2, b.g(A + "linear_q.weight", A + "linear_k.weight", A + "linear_v.weight",
                                           shape=(3 * d, d)), accumulate=True)
-        dxn2 = empty(N, d, dtype=cd, device=dev)
-        ops.linear_dx(dqkv, qkv_w, dxn2)
+        if dxn2 is None:
+            dxn2 = empty(N, d, dtype=cd, device=dev)
+            ops.linear_dx(dqkv, qkv_w, dxn2)
         dv_ff1 = dv_buf(N, d, cd, dev)
         ln_bwd(dxn2, x1, b, "norm_mha", mu2, rs2, dx, accumulate=True,
                drop=drop_arg(dv_ff1, L.ff_scale, p, sd(2), b.g("feed_forward_macaron.w_2.bias")))

@@ -654,6 +654,20 @@ int ea_ctc_prefix_score_dev(int T, int V, int blank, int eos, int n_hyp, int n_c
                             const unsigned long long* r_prev, int out_len, const int* last, const int* cand,
                             float* log_psi, float* r_new, void* stream);
 
+/* ea_ctc_prefix_score over the attention window of CTCPrefixScoreTH (margin > 0,
+ * ctc_prefix_score.py:143-161): the recursion runs over frames [start, end) only (start >= 1,
+ * end clamped to T), r_new frames outside it are logzero (r_new[0][0] = logp[0][c] for the
+ * empty prefix) and log_psi sums the window's terms with r[start-1][0]. */
+int ea_ctc_prefix_score_win(int T, int V, int blank, int eos, int n_hyp, int n_cand, const float* logp,
+                            const unsigned long long* r_prev, const int* meta, int start, int end,
+                            float* log_psi, float* r_new, void* stream);
+
+/* CTCPrefixScoreTH.extend_state (ctc_prefix_score.py:244-269, streaming decoding): a
+ * hypothesis's forward variables r_old (T_old x 2) extended to r (T x 2): frames < T_old
+ * copied, then r^n = logzero and r^b accumulating logp[t][blank] frame by frame. */
+int ea_ctc_prefix_extend(int T_old, int T, int V, int blank, const float* logp, const float* r_old, float* r,
+                         void* stream);
+
 /* Device-side beam step of joint CTC/attention decoding (espnet/nets/batch_beam_search.py:
  * 170-205 + batch_beam :81-101).  ea_beam_prebeam: per hypothesis h < n, the P best tokens of
  * W = w_dec*logp[h] (+ w_lb when use_lb), descending (ties: lower token), then <eos>, into

@@ -615,7 +615,10 @@ class OracleCTCPrefixScore:
             r[i, 1] = r[i - 1, 1] + self.x[i, self.blank]
         return r
 
-    def __call__(self, y, cs, r_prev):
+    def __call__(self, y, cs, r_prev, window=None):
+        """window: (start, end) frames of CTCPrefixScoreTH's attention window
+        (ctc_prefix_score.py:143-161; end clamped to this utterance's frames): the recursion
+        runs over [start, end) only, every other frame's variables stay logzero."""
         ol = len(y) - 1
         r = np.full((self.T, 2, len(cs)), self.logzero, dtype=np.float32)  # unread rows: logzero
         xs = self.x[:, cs]
@@ -632,9 +635,9 @@ class OracleCTCPrefixScore:
                 log_phi[:, i] = r_sum if cs[i] != last else r_prev[:, 1]
         else:
             log_phi = r_sum
-        start = max(ol, 1)
-        log_psi = r[start - 1, 0]
-        for t in range(start, self.T):
+        start, end = (max(ol, 1), self.T) if window is None else (window[0], min(window[1], self.T))
+        log_psi = r[start - 1, 0].copy()
+        for t in range(start, end):
             r[t, 0] = np.logaddexp(r[t - 1, 0], log_phi[t - 1]) + xs[t]
             r[t, 1] = np.logaddexp(r[t - 1, 0], r[t - 1, 1]) + self.x[t, self.blank]
             log_psi = np.logaddexp(log_psi, log_phi[t - 1] + xs[t])
@@ -645,6 +648,16 @@ class OracleCTCPrefixScore:
         if len(blank_pos) > 0:
             log_psi[blank_pos] = self.logzero
         return log_psi, np.rollaxis(r, 2)
+
+    def extend_state(self, r_prev):
+        """ctc_prefix_score.py:244-269 (streaming): forward variables over the first
+        len(r_prev) frames extended to this scorer's T: r^n logzero, r^b the blank recursion."""
+        r = np.full((self.T, 2), self.logzero, dtype=np.float32)
+        start = max(len(r_prev), 1)
+        r[:start] = r_prev
+        for t in range(start, self.T):
+            r[t, 1] = r[t - 1, 1] + self.x[t, self.blank]
+        return r
 
 
 @torch.no_grad()

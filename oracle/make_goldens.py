@@ -1016,6 +1016,83 @@ def capture_ctc_th(name="ctc_th"):
     print(f"{name} -> {path}")
 
 
+def capture_ctc_th_ext(name="ctc_th_ext"):
+    """CTCPrefixScoreTH's attention-windowed scoring (margin > 0 with att_w,
+    espnet/nets/ctc_prefix_score.py:57-62, 143-153) and its streaming extension (extend_prob /
+    extend_state, :222-269, driven per hypothesis as scorers/ctc.py:128-158 does), on seeded
+    log-posteriors.  Window case: two utterances (30 and 21 frames), margin 3, attention
+    weights peaked on a centre that advances each step, three steps with index_select_state
+    between them.  Streaming case: one utterance revealed 12 -> 20 -> 30 frames, one step per
+    chunk, the selected hypotheses' states extended before each new chunk's step."""
+    from espnet.nets.ctc_prefix_score import CTCPrefixScoreTH
+    g = torch.Generator().manual_seed(11)
+    out = {}
+    # --- window
+    B, T, O, W, margin = 2, 30, 9, 3, 3
+    eos = O - 1
+    x = torch.log_softmax(torch.randn(B, T, O, generator=g) * 2.0, dim=-1)
+    xlens = torch.tensor([30, 21])
+    out["w.x"] = np32(x)
+    out["w.xlens"] = xlens.numpy().astype(np.int64)
+    impl = CTCPrefixScoreTH(x.clone(), xlens, 0, eos, margin=margin)
+    n_bh = B * W
+    y = [torch.tensor([eos]) for _ in range(n_bh)]
+    state = None
+    plan = [None, torch.tensor([[1, 2, 3, 8], [2, 4, 5, 6], [1, 3, 5, 7], [2, 3, 4, 5], [1, 6, 7, 8],
+                                [3, 4, 6, 7]]), None]
+    best_plan = [torch.tensor([[1, 9 + 2, 18 + 3], [4, 9 + 5, 18 + 7]]),
+                 torch.tensor([[2, 9 + 4, 18 + 6], [3 + 9, 18 + 7, 8]]), None]
+    frames = torch.arange(T, dtype=torch.float32)
+    for step, sids in enumerate(plan):
+        centre = 4.0 + 6.0 * step + torch.rand(n_bh, 1, generator=g) * 3.0
+        att_w = torch.softmax(-((frames.view(1, -1) - centre) ** 2) / 4.0, dim=-1)
+        sc, st = impl(y, state, sids, att_w)
+        out[f"w.s{step}.att_w"] = np32(att_w)
+        out[f"w.s{step}.scores"] = np32(sc)
+        out[f"w.s{step}.y"] = np.stack([yy.numpy() for yy in y]).astype(np.int64)
+        out[f"w.s{step}.fminmax"] = np.array([st[2], st[3]], dtype=np.int64)
+        if sids is not None:
+            out[f"w.s{step}.ids"] = sids.numpy().astype(np.int64)
+        best = best_plan[step]
+        if best is None:
+            break
+        out[f"w.s{step}.best"] = best.numpy().astype(np.int64)
+        state = impl.index_select_state(st, best)
+        hyp = (best // O + (torch.arange(B) * W).view(-1, 1)).view(-1)
+        lab = torch.fmod(best, O).view(-1)
+        y = [torch.cat([y[int(h)], lab[i:i + 1]]) for i, h in enumerate(hyp)]
+    # --- streaming
+    T, W = 30, 3
+    xs = torch.log_softmax(torch.randn(1, T, O, generator=g) * 2.0, dim=-1)
+    out["s.x"] = np32(xs)
+    chunks = [12, 20, 30]
+    impl = CTCPrefixScoreTH(xs[:, :chunks[0]].clone(), torch.tensor([chunks[0]]), 0, eos)
+    y = [torch.tensor([eos]) for _ in range(W)]
+    state = None
+    best_plan = [torch.tensor([[1, 9 + 2, 18 + 3]]), torch.tensor([[2, 9 + 4, 18 + 6]]), None]
+    for step, tc in enumerate(chunks):
+        if step > 0:
+            impl.extend_prob(xs[:, :tc].clone())
+            per = [impl.extend_state((state[0][:, :, i], state[1][i], state[2], state[3])) for i in range(W)]
+            state = (torch.stack([s[0] for s in per], dim=2), torch.stack([s[1] for s in per]), per[0][2], per[0][3])
+        sc, st = impl(y, state, None)
+        out[f"s.s{step}.scores"] = np32(sc)
+        out[f"s.s{step}.y"] = np.stack([yy.numpy() for yy in y]).astype(np.int64)
+        best = best_plan[step]
+        if best is None:
+            break
+        out[f"s.s{step}.best"] = best.numpy().astype(np.int64)
+        state = impl.index_select_state(st, best)
+        lab = torch.fmod(best, O).view(-1)
+        hyp = (best // O).view(-1)
+        y = [torch.cat([y[int(h)], lab[i:i + 1]]) for i, h in enumerate(hyp)]
+    out["cfg"] = np.array(json.dumps({"B": B, "O": O, "W": W, "eos": eos, "blank": 0, "margin": margin,
+                                      "chunks": chunks}))
+    path = os.path.join(OUT, f"{name}.npz")
+    np.savez_compressed(path, **out)
+    print(f"{name} -> {path}")
+
+
 def capture_beam_batch(name="beam_batch", cfg_name="tiny_hybrid"):
     """espnet/nets/batch_beam_search.py BatchBeamSearch (decoder batch_score, CTCPrefixScorer
     batch_score_partial over CTCPrefixScoreTH, LengthBonus) on the tiny hybrid model, the
@@ -1143,6 +1220,8 @@ if __name__ == "__main__":
         capture_beam()
     if "ctc_th" in which:
         capture_ctc_th()
+    if "ctc_th_ext" in which:
+        capture_ctc_th_ext()
     if "beam_batch" in which:
         capture_beam_batch()
     if "lm" in which:

@@ -129,3 +129,65 @@ def test_ctc_scorer_batch_api_matches_th():
     s4, _ = ref(y2, (r_sel, s_new, 0, 0), ids)
     assert torch.equal(s3, s4)
     m.train()
+
+
+def _check(sc, ref, tag):
+    mine = sc.cpu().numpy()
+    low = ref < -1e9
+    assert np.array_equal(mine < -1e9, low), tag
+    np.testing.assert_allclose(mine[~low], ref[~low], rtol=1e-5, atol=2e-4, err_msg=tag)
+
+
+def test_ctc_prefix_score_th_window_matches_reference():
+    """margin > 0 with attention weights (ctc_prefix_score.py:57-62, 143-161): the window's
+    frame range on the device kernel (ea_ctc_prefix_score_win) vs the reference's scores and
+    (f_min, f_max) over three steps (tests/golden/ctc_th_ext.npz)."""
+    from espnet_amd.asr.ctc_prefix_score import CTCPrefixScoreTH
+    cfg, d = load("ctc_th_ext")
+    O, eos, margin = cfg["O"], cfg["eos"], cfg["margin"]
+    x = torch.from_numpy(d["w.x"]).to(DEV)
+    impl = CTCPrefixScoreTH(x.clone(), torch.from_numpy(d["w.xlens"]), 0, eos, margin=margin)
+    state, step = None, 0
+    while f"w.s{step}.scores" in d:
+        y = [torch.from_numpy(r) for r in d[f"w.s{step}.y"]]
+        ids = torch.from_numpy(d[f"w.s{step}.ids"]) if f"w.s{step}.ids" in d else None
+        sc, st = impl(y, state, ids, torch.from_numpy(d[f"w.s{step}.att_w"]).to(DEV))
+        _check(sc, d[f"w.s{step}.scores"], f"window step {step}")
+        assert [st[2], st[3]] == d[f"w.s{step}.fminmax"].tolist()
+        if f"w.s{step}.best" not in d:
+            break
+        state = impl.index_select_state(st, torch.from_numpy(d[f"w.s{step}.best"]))
+        step += 1
+    assert step == 2
+
+
+def test_ctc_prefix_score_th_streaming_matches_reference():
+    """extend_prob / extend_state (ctc_prefix_score.py:222-269, per hypothesis as
+    scorers/ctc.py:128-158 drives them): one utterance revealed 12 -> 20 -> 30 frames, a step
+    per chunk, vs the reference's scores; the extended forward variables also equal a scorer
+    built on the whole utterance's initial state (a prefix of <sos> only)."""
+    from espnet_amd.asr.ctc_prefix_score import CTCPrefixScoreTH
+    cfg, d = load("ctc_th_ext")
+    O, W, eos, chunks = cfg["O"], cfg["W"], cfg["eos"], cfg["chunks"]
+    xs = torch.from_numpy(d["s.x"]).to(DEV)
+    impl = CTCPrefixScoreTH(xs[:, :chunks[0]].clone(), torch.tensor([chunks[0]]), 0, eos)
+    state, step = None, 0
+    for step, tc in enumerate(chunks):
+        if step > 0:
+            impl.extend_prob(xs[:, :tc].clone())
+            per = [impl.extend_state((state[0][i], state[1][i], state[2], state[3])) for i in range(W)]
+            assert all(p[0].shape == (tc, 2) for p in per)
+            state = ([p[0] for p in per], torch.stack([p[1] for p in per]), per[0][2], per[0][3])
+        y = [torch.from_numpy(r) for r in d[f"s.s{step}.y"]]
+        sc, st = impl(y, state, None)
+        _check(sc, d[f"s.s{step}.scores"], f"streaming step {step}")
+        if f"s.s{step}.best" not in d:
+            break
+        state = impl.index_select_state(st, torch.from_numpy(d[f"s.s{step}.best"]))
+    assert step == 2
+    # the <sos> state extended from 12 frames equals the 30-frame initial state
+    small = CTCPrefixScoreTH(xs[:, :12].clone(), torch.tensor([12]), 0, eos)
+    full = CTCPrefixScoreTH(xs.clone(), torch.tensor([30]), 0, eos)
+    small.extend_prob(xs.clone())
+    r, _, _, _ = small.extend_state((small.r0[0][:12].clone(), None, 0, 1))
+    torch.testing.assert_close(r, full.r0[0], rtol=1e-6, atol=1e-5)
