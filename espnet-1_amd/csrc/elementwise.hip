@@ -635,13 +635,22 @@ __global__ __launch_bounds__(256) void dwconv_fwd_k_kernel(int B, int T, int C, 
     const int ci = i / K, k = i - ci * K;
     wsm[k * DW_CT + ci] = c0 + ci < C ? w[(long)c0 * K + i] : 0.f;
   }
-  if (C % 4 == 0) {  // 16-B loads: 16 lanes cover one 64-channel row
-    for (int i = threadIdx.x; i < RL * (DW_CT / 4); i += 256) {
+  if (C % 4 == 0) {  // 16-B loads: 16 lanes cover one 64-channel row; all NL in flight at once
+    constexpr int NL = (RL * (DW_CT / 4) + 255) / 256;
+    float4 v[NL];
+#pragma unroll
+    for (int u = 0; u < NL; ++u) {
+      const int i = threadIdx.x + 256 * u;
       const int rr = i / (DW_CT / 4), c4 = (i % (DW_CT / 4)) * 4;
       const int t = t0 + rr - P;
-      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (t >= 0 && t < T && c0 + c4 < C) v = *(const float4*)(x + ((long)b * T + t) * C + c0 + c4);
-      *(float4*)(tile + rr * DW_CT + c4) = v;
+      v[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (i < RL * (DW_CT / 4) && t >= 0 && t < T && c0 + c4 < C)
+        v[u] = *(const float4*)(x + ((long)b * T + t) * C + c0 + c4);
+    }
+#pragma unroll
+    for (int u = 0; u < NL; ++u) {
+      const int i = threadIdx.x + 256 * u;
+      if (i < RL * (DW_CT / 4)) *(float4*)(tile + (i / (DW_CT / 4)) * DW_CT + (i % (DW_CT / 4)) * 4) = v[u];
     }
   } else {
     for (int rr = tq; rr < RL; rr += 4) {
@@ -674,10 +683,15 @@ __global__ __launch_bounds__(256) void dwconv_fwd_k_kernel(int B, int T, int C, 
 // dx[t] = sum_k w[k] dy[t-k+P];  part[blk][k*C+c] = sum_t dy[t] x[t+k-P];  part[blk][K*C+c] = sum_t dy[t]
 // CK: partials laid out as the parameters are — [c][k] (dw is (C, 1, K)) then [c] (dbias) — so
 // their sums are plain row reductions the host can defer into the pass's grouped reduce
-template <int K, int R, bool CK = false>
+// GLU: the GLU backward fused into the dx store (conformer/convolution.py:64-66: the depthwise
+// conv's input is glu(g2)): dg2 = (dx * sigmoid(b), dx * a * s * (1 - s)) for g2 = [a | b] rows of
+// 2C bf16 — the arithmetic of glu_bwd_kernel, without dx's f32 round trip through HBM
+template <int K, int R, bool CK = false, bool GLU = false>
 __global__ __launch_bounds__(256) void dwconv_bwd_k_kernel(int B, int T, int C, const float* __restrict__ x,
                                                            const float* __restrict__ w, const float* __restrict__ dy,
-                                                           float* __restrict__ dx, float* __restrict__ part) {
+                                                           float* __restrict__ dx, float* __restrict__ part,
+                                                           const bf16* __restrict__ g2 = nullptr,
+                                                           bf16* __restrict__ dg2 = nullptr) {
   constexpr int P = (K - 1) / 2, TT = 4 * R, RL = TT + K - 1, WIN = R + K - 1;
   constexpr int SM = 2 * RL * DW_CT > 4 * (K + 1) * DW_CT ? 2 * RL * DW_CT : 4 * (K + 1) * DW_CT;
   __shared__ float sm[SM];
@@ -693,16 +707,40 @@ __global__ __launch_bounds__(256) void dwconv_bwd_k_kernel(int B, int T, int C, 
     const int ci = i / K, k = i - ci * K;
     wsm[k * DW_CT + ci] = c0 + ci < C ? w[(long)c0 * K + i] : 0.f;
   }
-  if (C % 4 == 0) {
-    for (int i = threadIdx.x; i < RL * (DW_CT / 4); i += 256) {
+  // GLU: the gate rows this thread's dx store needs, loaded first (their latency hides behind
+  // the tile loads; the LDS budget, not registers, bounds this kernel's occupancy)
+  bf16 ga[GLU ? R : 1], gb[GLU ? R : 1];
+  if constexpr (GLU) {
+#pragma unroll
+    for (int j = 0; j < R; ++j) {
+      const long row = (long)b * T + min(t0 + tq * R + j, T - 1);
+      const int cl = min(c, C - 1);
+      ga[j] = g2[row * 2 * C + cl];
+      gb[j] = g2[row * 2 * C + C + cl];
+    }
+  }
+  if (C % 4 == 0) {  // 16-B loads, all NL of both tiles in flight before the LDS stores
+    constexpr int NL = (RL * (DW_CT / 4) + 255) / 256;
+    float4 va[NL], vb[NL];
+#pragma unroll
+    for (int u = 0; u < NL; ++u) {
+      const int i = threadIdx.x + 256 * u;
       const int rr = i / (DW_CT / 4), c4 = (i % (DW_CT / 4)) * 4;
       const int td = t0 + rr - (K - 1 - P), tx_ = t0 + rr - P;
-      const bool okc = c0 + c4 < C;
-      float4 a = make_float4(0.f, 0.f, 0.f, 0.f), bb = a;
-      if (okc && td >= 0 && td < T) a = *(const float4*)(dy + ((long)b * T + td) * C + c0 + c4);
-      if (okc && tx_ >= 0 && tx_ < T) bb = *(const float4*)(x + ((long)b * T + tx_) * C + c0 + c4);
-      *(float4*)(tdy + rr * DW_CT + c4) = a;
-      *(float4*)(tx + rr * DW_CT + c4) = bb;
+      const bool okc = i < RL * (DW_CT / 4) && c0 + c4 < C;
+      va[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+      vb[u] = va[u];
+      if (okc && td >= 0 && td < T) va[u] = *(const float4*)(dy + ((long)b * T + td) * C + c0 + c4);
+      if (okc && tx_ >= 0 && tx_ < T) vb[u] = *(const float4*)(x + ((long)b * T + tx_) * C + c0 + c4);
+    }
+#pragma unroll
+    for (int u = 0; u < NL; ++u) {
+      const int i = threadIdx.x + 256 * u;
+      if (i < RL * (DW_CT / 4)) {
+        const int o = (i / (DW_CT / 4)) * DW_CT + (i % (DW_CT / 4)) * 4;
+        *(float4*)(tdy + o) = va[u];
+        *(float4*)(tx + o) = vb[u];
+      }
     }
   } else {
     for (int rr = tq; rr < RL; rr += 4) {
@@ -728,10 +766,24 @@ __global__ __launch_bounds__(256) void dwconv_bwd_k_kernel(int B, int T, int C, 
 #pragma unroll
         for (int j = 0; j < R; ++j) acc[j] += wk * win[j - k + K - 1];
       }
+      if constexpr (GLU) {
 #pragma unroll
-      for (int j = 0; j < R; ++j) {
-        const int t = t0 + tq * R + j;
-        if (t < T) dx[((long)b * T + t) * C + c] = acc[j];
+        for (int j = 0; j < R; ++j) {
+          const int t = t0 + tq * R + j;
+          if (t < T) {
+            const long row = (long)b * T + t;
+            const float a = to_f(ga[j]), g = to_f(gb[j]);
+            const float s = sigmoidf_(g), d = acc[j];
+            dg2[row * 2 * C + c] = from_f<bf16>(d * s);
+            dg2[row * 2 * C + C + c] = from_f<bf16>(d * a * s * (1.f - s));
+          }
+        }
+      } else {
+#pragma unroll
+        for (int j = 0; j < R; ++j) {
+          const int t = t0 + tq * R + j;
+          if (t < T) dx[((long)b * T + t) * C + c] = acc[j];
+        }
       }
     }
     // dy[t0 + tq*R + j] = win[j + K-1-P]  (rows past T are zero)
@@ -1157,6 +1209,31 @@ extern "C" int ea_dwconv_bwd(int B, int T, int C, int K, const float* x, const f
   if (rc) return rc;
   if (dbias) return ea_colsum(B * T, C, dy, EA_F32, C, dbias, accumulate_params, workspace, ws_elems, stream);
   return 0;
+}
+
+extern "C" int ea_dwconv_glu_bwd(int B, int T, int C, int K, const float* x, const float* w, const float* dy,
+                                 const void* g2, void* dg2, float* dw, float* dbias, int accumulate_params,
+                                 float* workspace, long ws_elems, void* stream) {
+  EA_ENTRY();
+  EA_CHECK_ARG((K == 3 || K == 5 || K == 7 || K == 15 || K == 31) && g2 && dg2 && dw && dbias);
+  const int nblkr = B * ea_cdiv(T, 4 * DW_R);
+  dim3 gridr(nblkr, ea_cdiv(C, DW_CT));
+  const long rowlen = (long)C * (K + 1);
+  EA_CHECK_ARG((long)nblkr * rowlen <= ws_elems);
+  hipStream_t st = (hipStream_t)stream;
+  switch (K) {
+#define EA_DWB(KK)                                                                                          \
+  case KK:                                                                                                  \
+    hipLaunchKernelGGL((dwconv_bwd_k_kernel<KK, DW_R, false, true>), gridr, dim3(256), 0, st, B, T, C, x, w, dy, \
+                       (float*)nullptr, workspace, (const bf16*)g2, (bf16*)dg2);                                  \
+    break;
+    EA_DWB(3) EA_DWB(5) EA_DWB(7) EA_DWB(15) EA_DWB(31)
+#undef EA_DWB
+  }
+  EA_LAUNCH_CHECK();
+  int rc = ea_reduce_partials_tr(nblkr, C * K, workspace, rowlen, dw, accumulate_params, C, K, stream);
+  if (rc) return rc;
+  return ea_reduce_partials(nblkr, C, workspace + (long)C * K, rowlen, dbias, accumulate_params, stream);
 }
 
 extern "C" int ea_dwconv_bwd_partials(int B, int T, int C, int K, const float* x, const float* w, const float* dy,

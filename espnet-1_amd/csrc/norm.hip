@@ -398,7 +398,7 @@ struct LnDrop {
   bf16* y; long ldy; float scale, p; uint64_t seed; const unsigned long long* salt; float* ypart;
   bool want_ycol; float* ycol;  // host side: column sums requested; their final target (direct mode)
 };
-template <int NJ, typename TI, bool DROP = false>
+template <int NJ, typename TI, bool DROP = false, int UR = 2>
 __global__ __launch_bounds__(256) void ln_bwd_vec_kernel(int rows, int d, const TI* __restrict__ dy, long lddy,
                                                          const float* __restrict__ x, long ldx,
                                                          const float* __restrict__ g, const float* __restrict__ mean,
@@ -425,10 +425,7 @@ __global__ __launch_bounds__(256) void ln_bwd_vec_kernel(int rows, int d, const 
   // U rows per wave step (rows rb and rb + 4): every load of both rows is issued before
   // either row is computed (the grid is ~2 waves per SIMD: latency, not bandwidth, bounds a
   // one-row step).  Rows are still folded into the partials in order rb, rb + 4.
-#ifndef EA_LN_BWD_U
-#define EA_LN_BWD_U 2
-#endif
-  constexpr int U = NJ == 1 ? EA_LN_BWD_U : 1;
+  constexpr int U = NJ == 1 ? UR : 1;
   for (int rb = r0 + w; rb < r1; rb += 4 * U) {
     float xv[U][NJ][8], dv[U][NJ][8], pv[U][NJ][8], mu[U], rs[U];
 #pragma unroll
@@ -768,15 +765,17 @@ __global__ __launch_bounds__(256) void bn_bwd_partial_vec_kernel(int rows, int C
       }
     };
     int r = r0 + w;
-    for (; r + 4 < r1; r += 8) {
-      float yv[2][4], dv[2][4];
+    // four rows per wave step, every load issued before any is consumed (the grid is ~2
+    // blocks per CU: memory latency, not bandwidth, bounds a one- or two-row step)
+    for (; r + 12 < r1; r += 16) {
+      float yv[4][4], dv[4][4];
 #pragma unroll
-      for (int j = 0; j < 2; ++j) {
+      for (int j = 0; j < 4; ++j) {
         vld4(y + (long)(r + 4 * j) * C + c, yv[j]);
         vld4(dz + (long)(r + 4 * j) * C + c, dv[j]);
       }
 #pragma unroll
-      for (int j = 0; j < 2; ++j) accum(yv[j], dv[j]);
+      for (int j = 0; j < 4; ++j) accum(yv[j], dv[j]);
     }
     for (; r < r1; r += 4) {
       float yv[4], dv[4];
@@ -916,20 +915,22 @@ static int ln_bwd_impl(int rows, int d, const void* dy, int dy_dtype, long lddy,
     EA_CHECK_ARG(ws_elems >= (long)nb * per);
     LnDrop dd = kdrop ? *drop : LnDrop{};
     dd.ypart = ycs ? workspace + (long)nb * 2 * d : nullptr;
-#define EA_LNB(NJ)                                                                                        \
+#define EA_LNB(NJ, U)                                                                                     \
   if (kdrop && dy_dtype == EA_BF16)                                                                       \
-    hipLaunchKernelGGL((ln_bwd_vec_kernel<NJ, bf16, true>), dim3(nb), dim3(256), 0, st, rows, d, (const bf16*)dy, lddy, \
+    hipLaunchKernelGGL((ln_bwd_vec_kernel<NJ, bf16, true, U>), dim3(nb), dim3(256), 0, st, rows, d, (const bf16*)dy, lddy, \
                        x, ldx, gamma, mean, rstd, dx, lddx, accumulate, rpb, workspace, dd);               \
   else if (kdrop)                                                                                         \
-    hipLaunchKernelGGL((ln_bwd_vec_kernel<NJ, float, true>), dim3(nb), dim3(256), 0, st, rows, d, (const float*)dy, lddy, \
+    hipLaunchKernelGGL((ln_bwd_vec_kernel<NJ, float, true, U>), dim3(nb), dim3(256), 0, st, rows, d, (const float*)dy, lddy, \
                        x, ldx, gamma, mean, rstd, dx, lddx, accumulate, rpb, workspace, dd);               \
   else if (dy_dtype == EA_BF16)                                                                           \
-    hipLaunchKernelGGL((ln_bwd_vec_kernel<NJ, bf16>), dim3(nb), dim3(256), 0, st, rows, d, (const bf16*)dy, lddy, x, ldx, \
+    hipLaunchKernelGGL((ln_bwd_vec_kernel<NJ, bf16, false, U>), dim3(nb), dim3(256), 0, st, rows, d, (const bf16*)dy, lddy, x, ldx, \
                        gamma, mean, rstd, dx, lddx, accumulate, rpb, workspace);                           \
   else                                                                                                    \
-    hipLaunchKernelGGL((ln_bwd_vec_kernel<NJ, float>), dim3(nb), dim3(256), 0, st, rows, d, (const float*)dy, lddy, x, \
+    hipLaunchKernelGGL((ln_bwd_vec_kernel<NJ, float, false, U>), dim3(nb), dim3(256), 0, st, rows, d, (const float*)dy, lddy, x, \
                        ldx, gamma, mean, rstd, dx, lddx, accumulate, rpb, workspace);
-    if (d <= 512) { EA_LNB(1) } else { EA_LNB(2) }
+    // rows in flight per wave step (d <= 512): EA_LN_BWD_U = 2 (default) or 4 (A/B)
+    static const int ln_u = [] { const char* e = std::getenv("EA_LN_BWD_U"); return e ? std::atoi(e) : 2; }();
+    if (d > 512) { EA_LNB(2, 1) } else if (ln_u == 4) { EA_LNB(1, 4) } else { EA_LNB(1, 2) }
 #undef EA_LNB
     EA_LAUNCH_CHECK();
     if (!dgamma) { *nparts_out = nb; return 0; }
@@ -1184,7 +1185,9 @@ extern "C" int ea_batchnorm_bwd(int rows, int C, const void* dz, int dz_dtype, c
   EA_ENTRY();
   hipStream_t st = (hipStream_t)stream;
   const long total = (long)rows * C;
-  const int rpb = max(32, ea_cdiv(rows, 64));
+  // <= 256 row blocks of >= 16 rows: ~2 blocks per CU at C = 512 (64 row blocks of 125 rows
+  // left half the CUs idle: 16.8 us for 24 MB)
+  const int rpb = max(16, ea_cdiv(rows, 256));
   const int nparts = ea_cdiv(rows, rpb);
   EA_CHECK_ARG((long)nparts * 2 * C + 2 * C <= ws_elems && rows > 0);
   EA_CHECK_ARG(dbeta == dgamma + C);

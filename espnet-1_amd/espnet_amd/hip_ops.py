@@ -837,7 +837,7 @@ def batchnorm_fwd(y, gamma, beta, mean, rstd, run_mean, run_var, nbt, z, trainin
 
 def batchnorm_bwd(dz, y, mean, rstd, gamma, beta, act, dy, dgamma, dbeta):
     rows, C, _ = _rows(y)
-    w, wn = _ws(y.device, (rows // 32 + 4) * 2 * C)
+    w, wn = _ws(y.device, (min(rows // 16 + 1, 256) + 2) * 2 * C)
     lib.ea_batchnorm_bwd(rows, C, dz.data_ptr(), dt(dz), y.data_ptr(), mean.data_ptr(), rstd.data_ptr(),
                          gamma.data_ptr(), beta.data_ptr(), act, dy.data_ptr(), dgamma.data_ptr(),
                          dbeta.data_ptr(), 1, w, wn, stream())

@@ -48,6 +48,9 @@ DWCONV_DEFER = os.environ.get("EA_DWCONV_DEFER", "0") == "1"
 # side stream (EA_DPP_LATE=1) instead of after it: the graph keeps the captured order of a
 # node's dependents when it spreads them over queues
 DPP_LATE = os.environ.get("EA_DPP_LATE", "0") == "1"
+# the GLU backward fused into the depthwise conv's backward kernel (ea_dwconv_glu_bwd: the
+# same arithmetic without the f32 dglu round trip; EA_FUSE_DW_GLU=0: the two-kernel path)
+FUSE_DW_GLU = os.environ.get("EA_FUSE_DW_GLU", "1") != "0"
 
 class PositionwiseFeedForward(nn.Module):
     """positionwise_feed_forward.py:12-32 (w_2(dropout(act(w_1 x))))."""
@@ -334,24 +337,34 @@ class ConformerBlockFn(torch.autograd.Function):
         dy = empty(N, d, device=dev)
         ops.batchnorm_bwd(dz, y, bn_mean, bn_rstd, b.f(C + "norm.weight"), b.f(C + "norm.bias"),
                           ACT_SWISH, dy, b.g(C + "norm.weight"), b.g(C + "norm.bias"))
-        dglu = empty(N, d, device=dev)
-        if DWCONV_DEFER and ops.REDUCE_Q.active and K in (3, 5, 7, 15, 31):
-            # dw / dbias partials summed with the pass's other parameter-gradient reductions
-            part = empty(B * ((T + 31) // 32) * d * (K + 1), device=dev)
-            npart = ctypes.c_int(0)
-            lib.ea_dwconv_bwd_partials(B, T, d, K, glu.data_ptr(), b.f(C + "depthwise_conv.weight").data_ptr(),
-                                       dy.data_ptr(), dglu.data_ptr(), part.data_ptr(), part.numel(),
-                                       ctypes.addressof(npart), ops.stream())
-            rl = d * (K + 1)
-            ops.REDUCE_Q.add_reduce(part, npart.value, d * K, rl, b.g(C + "depthwise_conv.weight").view(-1))
-            ops.REDUCE_Q.add_reduce(part[d * K:], npart.value, d, rl, b.g(C + "depthwise_conv.bias"))
-        else:
-            w, wn = ops._ws(dev, B * ((T + 31) // 32) * d * (K + 1) + 1024)
-            lib.ea_dwconv_bwd(B, T, d, K, glu.data_ptr(), b.f(C + "depthwise_conv.weight").data_ptr(),
-                              dy.data_ptr(), dglu.data_ptr(), b.g(C + "depthwise_conv.weight").data_ptr(),
-                              b.g(C + "depthwise_conv.bias").data_ptr(), 1, w, wn, ops.stream())
         dg2 = empty(N, 2 * d, dtype=cd, device=dev)
-        lib.ea_glu_bwd(N, d, g2.data_ptr(), ops.dt(g2), dglu.data_ptr(), dg2.data_ptr(), ops.stream())
+        fuse = (FUSE_DW_GLU and K in (3, 5, 7, 15, 31) and g2.dtype == torch.bfloat16
+                and not (DWCONV_DEFER and ops.REDUCE_Q.active))
+        if fuse:
+            # the GLU backward inside the depthwise conv's input-gradient store (no f32 dglu)
+            w, wn = ops._ws(dev, B * ((T + 31) // 32) * d * (K + 1) + 1024)
+            lib.ea_dwconv_glu_bwd(B, T, d, K, glu.data_ptr(), b.f(C + "depthwise_conv.weight").data_ptr(),
+                                  dy.data_ptr(), g2.data_ptr(), dg2.data_ptr(),
+                                  b.g(C + "depthwise_conv.weight").data_ptr(),
+                                  b.g(C + "depthwise_conv.bias").data_ptr(), 1, w, wn, ops.stream())
+        else:
+            dglu = empty(N, d, device=dev)
+            if DWCONV_DEFER and ops.REDUCE_Q.active and K in (3, 5, 7, 15, 31):
+                # dw / dbias partials summed with the pass's other parameter-gradient reductions
+                part = empty(B * ((T + 31) // 32) * d * (K + 1), device=dev)
+                npart = ctypes.c_int(0)
+                lib.ea_dwconv_bwd_partials(B, T, d, K, glu.data_ptr(), b.f(C + "depthwise_conv.weight").data_ptr(),
+                                           dy.data_ptr(), dglu.data_ptr(), part.data_ptr(), part.numel(),
+                                           ctypes.addressof(npart), ops.stream())
+                rl = d * (K + 1)
+                ops.REDUCE_Q.add_reduce(part, npart.value, d * K, rl, b.g(C + "depthwise_conv.weight").view(-1))
+                ops.REDUCE_Q.add_reduce(part[d * K:], npart.value, d, rl, b.g(C + "depthwise_conv.bias"))
+            else:
+                w, wn = ops._ws(dev, B * ((T + 31) // 32) * d * (K + 1) + 1024)
+                lib.ea_dwconv_bwd(B, T, d, K, glu.data_ptr(), b.f(C + "depthwise_conv.weight").data_ptr(),
+                                  dy.data_ptr(), dglu.data_ptr(), b.g(C + "depthwise_conv.weight").data_ptr(),
+                                  b.g(C + "depthwise_conv.bias").data_ptr(), 1, w, wn, ops.stream())
+            lib.ea_glu_bwd(N, d, g2.data_ptr(), ops.dt(g2), dglu.data_ptr(), dg2.data_ptr(), ops.stream())
         with ops.wgrad(dg2, xn3):
             ops.colsum(dg2, b.g(C + "pointwise_conv1.bias"))
             ops.linear_dw(dg2, xn3, b.g(C + "pointwise_conv1.weight", shape=(2 * d, d)), accumulate=True)

@@ -310,7 +310,8 @@ int ea_batchnorm_fwd(int rows, int C, const float* y, const float* gamma, const 
                      float* running_mean, float* running_var, long long* num_batches_tracked,
                      int act, void* z, int z_dtype, float* workspace, long ws_elems, void* stream);
 
-/* Backward of z = act(BN_train(y)): dy, dgamma/dbeta (dbeta == dgamma + C). */
+/* Backward of z = act(BN_train(y)): dy, dgamma/dbeta (dbeta == dgamma + C).
+ * workspace >= (min(ceil(rows/16), 256) + 1) * 2C floats. */
 int ea_batchnorm_bwd(int rows, int C, const void* dz, int dz_dtype, const float* y, const float* mean,
                      const float* rstd, const float* gamma, const float* beta, int act, float* dy,
                      float* dgamma, float* dbeta, int accumulate_params, float* workspace,
@@ -427,6 +428,14 @@ int ea_dwconv_fwd(int B, int T, int C, int K, const float* x, const float* w, co
 int ea_dwconv_bwd(int B, int T, int C, int K, const float* x, const float* w, const float* dy,
                   float* dx, float* dw, float* dbias, int accumulate_params, float* workspace,
                   long ws_elems, void* stream);
+/* ea_dwconv_bwd (K in {3,5,7,15,31}) with the GLU backward that precedes the depthwise conv in
+ * the backward (conformer/convolution.py:64-66, x = glu(g2)) fused into the input-gradient
+ * store: g2 = [a | b] (rows x 2C bf16, the pointwise_conv1 output), dg2 (rows x 2C bf16) =
+ * (dx * sigmoid(b), dx * a * sigmoid(b) * (1 - sigmoid(b))) — the arithmetic of ea_dwconv_bwd
+ * followed by ea_glu_bwd (equal up to the f32 rounding of the tap sums); dx is never stored. */
+int ea_dwconv_glu_bwd(int B, int T, int C, int K, const float* x, const float* w, const float* dy,
+                      const void* g2, void* dg2, float* dw, float* dbias, int accumulate_params,
+                      float* workspace, long ws_elems, void* stream);
 /* ea_dwconv_bwd without the parameter reductions (K in {3,5,7,15,31}): dx, and per-block
  * partials part[p][0 : C*K] of dw in its (C, 1, K) layout and part[p][C*K : C*(K+1)] of dbias,
  * p < *nparts (row stride C*(K+1)) — plain row sums the caller may defer and group. */
