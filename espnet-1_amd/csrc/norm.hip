@@ -1146,7 +1146,9 @@ extern "C" int ea_batchnorm_fwd(int rows, int C, const float* y, const float* ga
   const long total = (long)rows * C;
   const bool vec = C % 4 == 0 && ((uintptr_t)y % 16) == 0 && ((uintptr_t)z % (z_dtype == EA_BF16 ? 8 : 16)) == 0;
   if (training) {
-    const int rpb = max(32, ea_cdiv(rows, 64));
+    // <= 256 row blocks of >= 16 rows (as the backward: 64 blocks of 125 rows left half the
+    // CUs idle)
+    const int rpb = max(16, ea_cdiv(rows, 256));
     const int nparts = ea_cdiv(rows, rpb);
     EA_CHECK_ARG((long)nparts * 2 * C <= ws_elems && rows > 0);
     if (vec)

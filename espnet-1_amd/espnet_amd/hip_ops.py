@@ -829,7 +829,7 @@ def colsum(x, out, accumulate=True, defer=True):
 def batchnorm_fwd(y, gamma, beta, mean, rstd, run_mean, run_var, nbt, z, training, act,
                   eps=1e-5, momentum=0.1):
     rows, C, _ = _rows(y)
-    w, wn = _ws(y.device, (rows // 32 + 2) * 2 * C)
+    w, wn = _ws(y.device, (min(rows // 16 + 1, 256) + 2) * 2 * C)
     lib.ea_batchnorm_fwd(rows, C, y.data_ptr(), gamma.data_ptr(), beta.data_ptr(), eps, momentum,
                          int(training), mean.data_ptr(), rstd.data_ptr(), ptr(run_mean), ptr(run_var),
                          ptr(nbt), act, z.data_ptr(), dt(z), w, wn, stream())

@@ -304,7 +304,8 @@ int ea_grouped_table_bytes(int n, long* colsum_bytes, long* reduce_bytes);
 /* BatchNorm1d (training: batch stats over ALL rows incl. padding, running stats update
  * with momentum and unbiased var, num_batches_tracked += 1; eval: given mean/rstd) fused
  * with the following activation: z = act(BN(y)).  y, z: (rows, C) channel-last.
- * Replaces conformer/convolution.py:45,75 (norm + Swish). */
+ * Replaces conformer/convolution.py:45,75 (norm + Swish).
+ * workspace >= min(ceil(rows/16), 256) * 2C floats (training). */
 int ea_batchnorm_fwd(int rows, int C, const float* y, const float* gamma, const float* beta,
                      float eps, float momentum, int training, float* mean, float* rstd,
                      float* running_mean, float* running_var, long long* num_batches_tracked,
