@@ -619,10 +619,27 @@ __global__ __launch_bounds__(256) void dwconv_bwd_kernel(int B, int T, int C, in
 // touches in registers (one LDS read per row instead of one per tap) and does the R*K taps
 // from registers; the block's taps are staged through LDS by one coalesced pass.
 constexpr int DW_R = 16;  // rows per thread (64-row tiles: the K-1 halo costs < 1.5x)
-template <int K, int R>
+
+// the conv input x = glu(g2) = a * sigmoid(b) for g2 rows [a | b] (2C bf16; glu_fwd_kernel's
+// arithmetic), 4 channels from two 8-B loads: the depthwise conv reads the pointwise conv's
+// bf16 output directly and the f32 GLU activation is never stored
+EA_DEV float4 glu4(const bf16* __restrict__ g2, long row, int C, int c) {
+  const uint2 ua = *(const uint2*)(g2 + row * 2 * C + c), ub = *(const uint2*)(g2 + row * 2 * C + C + c);
+  const float a0 = __uint_as_float(ua.x << 16), a1 = __uint_as_float(ua.x & 0xffff0000u);
+  const float a2 = __uint_as_float(ua.y << 16), a3 = __uint_as_float(ua.y & 0xffff0000u);
+  const float b0 = __uint_as_float(ub.x << 16), b1 = __uint_as_float(ub.x & 0xffff0000u);
+  const float b2 = __uint_as_float(ub.y << 16), b3 = __uint_as_float(ub.y & 0xffff0000u);
+  return make_float4(a0 * sigmoidf_(b0), a1 * sigmoidf_(b1), a2 * sigmoidf_(b2), a3 * sigmoidf_(b3));
+}
+EA_DEV float glu1(const bf16* __restrict__ g2, long row, int C, int c) {
+  return to_f(g2[row * 2 * C + c]) * sigmoidf_(to_f(g2[row * 2 * C + C + c]));
+}
+
+template <int K, int R, bool G2IN = false>
 __global__ __launch_bounds__(256) void dwconv_fwd_k_kernel(int B, int T, int C, const float* __restrict__ x,
                                                            const float* __restrict__ w,
-                                                           const float* __restrict__ bias, float* __restrict__ y) {
+                                                           const float* __restrict__ bias, float* __restrict__ y,
+                                                           const bf16* __restrict__ g2 = nullptr) {
   constexpr int P = (K - 1) / 2, TT = 4 * R, RL = TT + K - 1, WIN = R + K - 1;
   __shared__ float tile[RL * DW_CT];
   __shared__ float wsm[K * DW_CT];  // [k][c]
@@ -644,8 +661,12 @@ __global__ __launch_bounds__(256) void dwconv_fwd_k_kernel(int B, int T, int C, 
       const int rr = i / (DW_CT / 4), c4 = (i % (DW_CT / 4)) * 4;
       const int t = t0 + rr - P;
       v[u] = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (i < RL * (DW_CT / 4) && t >= 0 && t < T && c0 + c4 < C)
-        v[u] = *(const float4*)(x + ((long)b * T + t) * C + c0 + c4);
+      if (i < RL * (DW_CT / 4) && t >= 0 && t < T && c0 + c4 < C) {
+        if constexpr (G2IN)
+          v[u] = glu4(g2, (long)b * T + t, C, c0 + c4);
+        else
+          v[u] = *(const float4*)(x + ((long)b * T + t) * C + c0 + c4);
+      }
     }
 #pragma unroll
     for (int u = 0; u < NL; ++u) {
@@ -655,7 +676,14 @@ __global__ __launch_bounds__(256) void dwconv_fwd_k_kernel(int B, int T, int C, 
   } else {
     for (int rr = tq; rr < RL; rr += 4) {
       const int t = t0 + rr - P;
-      tile[rr * DW_CT + cc] = (t >= 0 && t < T && c < C) ? x[((long)b * T + t) * C + c] : 0.f;
+      float v = 0.f;
+      if (t >= 0 && t < T && c < C) {
+        if constexpr (G2IN)
+          v = glu1(g2, (long)b * T + t, C, c);
+        else
+          v = x[((long)b * T + t) * C + c];
+      }
+      tile[rr * DW_CT + cc] = v;
     }
   }
   __syncthreads();
@@ -686,7 +714,8 @@ __global__ __launch_bounds__(256) void dwconv_fwd_k_kernel(int B, int T, int C, 
 // GLU: the GLU backward fused into the dx store (conformer/convolution.py:64-66: the depthwise
 // conv's input is glu(g2)): dg2 = (dx * sigmoid(b), dx * a * s * (1 - s)) for g2 = [a | b] rows of
 // 2C bf16 — the arithmetic of glu_bwd_kernel, without dx's f32 round trip through HBM
-template <int K, int R, bool CK = false, bool GLU = false>
+// G2IN: x = glu(g2) recomputed in the tile loader (the forward did not store it)
+template <int K, int R, bool CK = false, bool GLU = false, bool G2IN = false>
 __global__ __launch_bounds__(256) void dwconv_bwd_k_kernel(int B, int T, int C, const float* __restrict__ x,
                                                            const float* __restrict__ w, const float* __restrict__ dy,
                                                            float* __restrict__ dx, float* __restrict__ part,
@@ -731,7 +760,12 @@ __global__ __launch_bounds__(256) void dwconv_bwd_k_kernel(int B, int T, int C, 
       va[u] = make_float4(0.f, 0.f, 0.f, 0.f);
       vb[u] = va[u];
       if (okc && td >= 0 && td < T) va[u] = *(const float4*)(dy + ((long)b * T + td) * C + c0 + c4);
-      if (okc && tx_ >= 0 && tx_ < T) vb[u] = *(const float4*)(x + ((long)b * T + tx_) * C + c0 + c4);
+      if (okc && tx_ >= 0 && tx_ < T) {
+        if constexpr (G2IN)
+          vb[u] = glu4(g2, (long)b * T + tx_, C, c0 + c4);
+        else
+          vb[u] = *(const float4*)(x + ((long)b * T + tx_) * C + c0 + c4);
+      }
     }
 #pragma unroll
     for (int u = 0; u < NL; ++u) {
@@ -747,7 +781,14 @@ __global__ __launch_bounds__(256) void dwconv_bwd_k_kernel(int B, int T, int C, 
       const int td = t0 + rr - (K - 1 - P), tx_ = t0 + rr - P;
       const bool okc = c < C;
       tdy[rr * DW_CT + cc] = (okc && td >= 0 && td < T) ? dy[((long)b * T + td) * C + c] : 0.f;
-      tx[rr * DW_CT + cc] = (okc && tx_ >= 0 && tx_ < T) ? x[((long)b * T + tx_) * C + c] : 0.f;
+      float xv = 0.f;
+      if (okc && tx_ >= 0 && tx_ < T) {
+        if constexpr (G2IN)
+          xv = glu1(g2, (long)b * T + tx_, C, c);
+        else
+          xv = x[((long)b * T + tx_) * C + c];
+      }
+      tx[rr * DW_CT + cc] = xv;
     }
   }
   __syncthreads();
@@ -1211,21 +1252,46 @@ extern "C" int ea_dwconv_bwd(int B, int T, int C, int K, const float* x, const f
   return 0;
 }
 
+extern "C" int ea_dwconv_fwd_glu(int B, int T, int C, int K, const void* g2, const float* w, const float* bias,
+                                 float* y, void* stream) {
+  EA_ENTRY();
+  EA_CHECK_ARG((K == 3 || K == 5 || K == 7 || K == 15 || K == 31) && g2 && y && C % 4 == 0 &&
+               ((uintptr_t)g2 % 8) == 0);
+  dim3 gridr(B * ea_cdiv(T, 4 * DW_R), ea_cdiv(C, DW_CT));
+  hipStream_t st = (hipStream_t)stream;
+  switch (K) {
+#define EA_DWF(KK)                                                                                          \
+  case KK:                                                                                                  \
+    hipLaunchKernelGGL((dwconv_fwd_k_kernel<KK, DW_R, true>), gridr, dim3(256), 0, st, B, T, C, (const float*)nullptr, \
+                       w, bias, y, (const bf16*)g2);                                                        \
+    break;
+    EA_DWF(3) EA_DWF(5) EA_DWF(7) EA_DWF(15) EA_DWF(31)
+#undef EA_DWF
+  }
+  EA_LAUNCH_CHECK();
+  return 0;
+}
+
 extern "C" int ea_dwconv_glu_bwd(int B, int T, int C, int K, const float* x, const float* w, const float* dy,
                                  const void* g2, void* dg2, float* dw, float* dbias, int accumulate_params,
                                  float* workspace, long ws_elems, void* stream) {
   EA_ENTRY();
   EA_CHECK_ARG((K == 3 || K == 5 || K == 7 || K == 15 || K == 31) && g2 && dg2 && dw && dbias);
+  EA_CHECK_ARG(x != nullptr || (C % 4 == 0 && ((uintptr_t)g2 % 8) == 0));
   const int nblkr = B * ea_cdiv(T, 4 * DW_R);
   dim3 gridr(nblkr, ea_cdiv(C, DW_CT));
   const long rowlen = (long)C * (K + 1);
   EA_CHECK_ARG((long)nblkr * rowlen <= ws_elems);
   hipStream_t st = (hipStream_t)stream;
   switch (K) {
-#define EA_DWB(KK)                                                                                          \
-  case KK:                                                                                                  \
-    hipLaunchKernelGGL((dwconv_bwd_k_kernel<KK, DW_R, false, true>), gridr, dim3(256), 0, st, B, T, C, x, w, dy, \
-                       (float*)nullptr, workspace, (const bf16*)g2, (bf16*)dg2);                                  \
+#define EA_DWB(KK)                                                                                            \
+  case KK:                                                                                                    \
+    if (x)                                                                                                    \
+      hipLaunchKernelGGL((dwconv_bwd_k_kernel<KK, DW_R, false, true>), gridr, dim3(256), 0, st, B, T, C, x, w, dy, \
+                         (float*)nullptr, workspace, (const bf16*)g2, (bf16*)dg2);                                  \
+    else                                                                                                      \
+      hipLaunchKernelGGL((dwconv_bwd_k_kernel<KK, DW_R, false, true, true>), gridr, dim3(256), 0, st, B, T, C,    \
+                         (const float*)nullptr, w, dy, (float*)nullptr, workspace, (const bf16*)g2, (bf16*)dg2);    \
     break;
     EA_DWB(3) EA_DWB(5) EA_DWB(7) EA_DWB(15) EA_DWB(31)
 #undef EA_DWB

@@ -344,8 +344,17 @@ __global__ __launch_bounds__(256) void ln_fwd_vec_kernel(int rows, int d, const 
   const int r = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (r >= rows) return;
   const float* xr = x + (long)r * ldx;
-  float v[NJ][8];
+  float v[NJ][8], gg[NJ][8], bb[NJ][8];
   float s = 0.f;
+  // gamma / beta loaded with the row (not after the two reductions: one latency fewer)
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) {
+    const int c = (lane + 64 * j) * 8;
+    if (c < d) {
+      ld8(g + c, gg[j]);
+      ld8(b + c, bb[j]);
+    }
+  }
 #pragma unroll
   for (int j = 0; j < NJ; ++j) {
     const int c = (lane + 64 * j) * 8;
@@ -374,11 +383,9 @@ __global__ __launch_bounds__(256) void ln_fwd_vec_kernel(int rows, int d, const 
   for (int j = 0; j < NJ; ++j) {
     const int c = (lane + 64 * j) * 8;
     if (c >= d) continue;
-    float gg[8], bb[8], o[8];
-    ld8(g + c, gg);
-    ld8(b + c, bb);
+    float o[8];
 #pragma unroll
-    for (int i = 0; i < 8; ++i) o[i] = (v[j][i] - mu) * rs * gg[i] + bb[i];
+    for (int i = 0; i < 8; ++i) o[i] = (v[j][i] - mu) * rs * gg[j][i] + bb[j][i];
     st8(y + (long)r * ldy + c, o);
   }
   if (lane == 0) {
@@ -663,30 +670,32 @@ __global__ __launch_bounds__(256) void bn_partial_vec_kernel(int rows, int C, co
   }
 }
 
-// parallel finalize: 64 channels x 4 part-lanes per block, fp64 combine in fixed order
+// parallel finalize: BNF_C channels x BNF_P part-lanes per block (C / 16 blocks: the <= 256
+// partial rows are summed 16 lanes wide), fp64 combine in fixed order
+constexpr int BNF_C = 16, BNF_P = 16;
 __global__ __launch_bounds__(256) void bn_finalize_par_kernel(int rows, int C, int nparts, const float* __restrict__ y,
                                                               const float* __restrict__ part, float eps, float momentum,
                                                               float* __restrict__ mean, float* __restrict__ rstd,
                                                               float* __restrict__ run_mean, float* __restrict__ run_var,
                                                               long long* __restrict__ nbt) {
-  __shared__ double red[2][4][64];
-  const int cx = threadIdx.x & 63, py = threadIdx.x >> 6;
-  const int c = blockIdx.x * 64 + cx;
+  __shared__ double red[2][BNF_P][BNF_C];
+  const int cx = threadIdx.x % BNF_C, py = threadIdx.x / BNF_C;
+  const int c = blockIdx.x * BNF_C + cx;
   if (blockIdx.x == 0 && threadIdx.x == 0 && nbt) nbt[0] += 1;
   double s = 0.0, ss = 0.0;
   if (c < C) {
     int p = py;
-    for (; p + 12 < nparts; p += 16) {
+    for (; p + 3 * BNF_P < nparts; p += 4 * BNF_P) {
       float a[4], b[4];
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        a[j] = part[(long)(p + 4 * j) * 2 * C + c];
-        b[j] = part[(long)(p + 4 * j) * 2 * C + C + c];
+        a[j] = part[(long)(p + BNF_P * j) * 2 * C + c];
+        b[j] = part[(long)(p + BNF_P * j) * 2 * C + C + c];
       }
 #pragma unroll
       for (int j = 0; j < 4; ++j) { s += a[j]; ss += b[j]; }
     }
-    for (; p < nparts; p += 4) {
+    for (; p < nparts; p += BNF_P) {
       s += part[(long)p * 2 * C + c];
       ss += part[(long)p * 2 * C + C + c];
     }
@@ -695,8 +704,10 @@ __global__ __launch_bounds__(256) void bn_finalize_par_kernel(int rows, int C, i
   red[1][py][cx] = ss;
   __syncthreads();
   if (py != 0 || c >= C) return;
-  s = (red[0][0][cx] + red[0][1][cx]) + (red[0][2][cx] + red[0][3][cx]);
-  ss = (red[1][0][cx] + red[1][1][cx]) + (red[1][2][cx] + red[1][3][cx]);
+  s = 0.0;
+  ss = 0.0;
+#pragma unroll
+  for (int l = 0; l < BNF_P; ++l) { s += red[0][l][cx]; ss += red[1][l][cx]; }
   const double n = rows;
   const double m = s / n;
   double var = ss / n - m * m;
@@ -1156,7 +1167,7 @@ extern "C" int ea_batchnorm_fwd(int rows, int C, const float* y, const float* ga
     else
       hipLaunchKernelGGL(bn_partial_kernel, dim3(ea_cdiv(C, 256), nparts), dim3(256), 0, st, rows, C, y, rpb, workspace);
     EA_LAUNCH_CHECK();
-    hipLaunchKernelGGL(bn_finalize_par_kernel, dim3(ea_cdiv(C, 64)), dim3(256), 0, st, rows, C, nparts, y, workspace,
+    hipLaunchKernelGGL(bn_finalize_par_kernel, dim3(ea_cdiv(C, BNF_C)), dim3(256), 0, st, rows, C, nparts, y, workspace,
                        eps, momentum, mean, rstd, running_mean, running_var, num_batches_tracked);
     EA_LAUNCH_CHECK();
   } else {

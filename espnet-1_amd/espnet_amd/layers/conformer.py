@@ -51,6 +51,15 @@ DPP_LATE = os.environ.get("EA_DPP_LATE", "0") == "1"
 # the GLU backward fused into the depthwise conv's backward kernel (ea_dwconv_glu_bwd: the
 # same arithmetic without the f32 dglu round trip; EA_FUSE_DW_GLU=0: the two-kernel path)
 FUSE_DW_GLU = os.environ.get("EA_FUSE_DW_GLU", "1") != "0"
+# the depthwise conv's forward and backward read glu(g2) from the bf16 pointwise-conv output
+# instead of a stored f32 GLU activation (ea_dwconv_fwd_glu / ea_dwconv_glu_bwd with x = NULL;
+# EA_GLU_IN_CONV=0: glu_fwd + the stored activation)
+GLU_IN_CONV = os.environ.get("EA_GLU_IN_CONV", "1") != "0"
+
+
+def _glu_in_conv(K, g2, d):
+    return (GLU_IN_CONV and FUSE_DW_GLU and not DWCONV_DEFER and K in (3, 5, 7, 15, 31)
+            and g2.dtype == torch.bfloat16 and d % 4 == 0 and g2.data_ptr() % 8 == 0 and torch.cuda.is_available())
 
 class PositionwiseFeedForward(nn.Module):
     """positionwise_feed_forward.py:12-32 (w_2(dropout(act(w_1 x))))."""
@@ -279,11 +288,18 @@ class ConformerBlockFn(torch.autograd.Function):
         g2 = empty(N, 2 * d, dtype=cd, device=dev)
         ops.linear(xn3, b.w(C + "pointwise_conv1.weight", shape=(2 * d, d)), g2,
                    epi=ops.make_epi(bias=b.f(C + "pointwise_conv1.bias")))
-        glu = empty(N, d, device=dev)
-        lib.ea_glu_fwd(N, d, g2.data_ptr(), ops.dt(g2), glu.data_ptr(), 0, ops.stream())
         y = empty(N, d, device=dev)
-        lib.ea_dwconv_fwd(B, T, d, K, glu.data_ptr(), b.f(C + "depthwise_conv.weight").data_ptr(),
-                          b.f(C + "depthwise_conv.bias").data_ptr(), y.data_ptr(), ops.stream())
+        if _glu_in_conv(K, g2, d):
+            # the depthwise conv reads glu(g2) straight from the pointwise conv's bf16 output; the
+            # f32 GLU activation is neither stored nor re-read (the backward recomputes it too)
+            glu = None
+            lib.ea_dwconv_fwd_glu(B, T, d, K, g2.data_ptr(), b.f(C + "depthwise_conv.weight").data_ptr(),
+                                  b.f(C + "depthwise_conv.bias").data_ptr(), y.data_ptr(), ops.stream())
+        else:
+            glu = empty(N, d, device=dev)
+            lib.ea_glu_fwd(N, d, g2.data_ptr(), ops.dt(g2), glu.data_ptr(), 0, ops.stream())
+            lib.ea_dwconv_fwd(B, T, d, K, glu.data_ptr(), b.f(C + "depthwise_conv.weight").data_ptr(),
+                              b.f(C + "depthwise_conv.bias").data_ptr(), y.data_ptr(), ops.stream())
         z = empty(N, d, dtype=cd, device=dev)
         bn_mean = empty(d, device=dev)
         bn_rstd = empty(d, device=dev)
@@ -343,11 +359,14 @@ class ConformerBlockFn(torch.autograd.Function):
         if fuse:
             # the GLU backward inside the depthwise conv's input-gradient store (no f32 dglu)
             w, wn = ops._ws(dev, B * ((T + 31) // 32) * d * (K + 1) + 1024)
-            lib.ea_dwconv_glu_bwd(B, T, d, K, glu.data_ptr(), b.f(C + "depthwise_conv.weight").data_ptr(),
+            lib.ea_dwconv_glu_bwd(B, T, d, K, ops.ptr(glu), b.f(C + "depthwise_conv.weight").data_ptr(),
                                   dy.data_ptr(), g2.data_ptr(), dg2.data_ptr(),
                                   b.g(C + "depthwise_conv.weight").data_ptr(),
                                   b.g(C + "depthwise_conv.bias").data_ptr(), 1, w, wn, ops.stream())
         else:
+            if glu is None:  # (forward without the stored activation, backward on the two-kernel path)
+                glu = empty(N, d, device=dev)
+                lib.ea_glu_fwd(N, d, g2.data_ptr(), ops.dt(g2), glu.data_ptr(), 0, ops.stream())
             dglu = empty(N, d, device=dev)
             if DWCONV_DEFER and ops.REDUCE_Q.active and K in (3, 5, 7, 15, 31):
                 # dw / dbias partials summed with the pass's other parameter-gradient reductions

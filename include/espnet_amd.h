@@ -437,6 +437,12 @@ int ea_dwconv_bwd(int B, int T, int C, int K, const float* x, const float* w, co
 int ea_dwconv_glu_bwd(int B, int T, int C, int K, const float* x, const float* w, const float* dy,
                       const void* g2, void* dg2, float* dw, float* dbias, int accumulate_params,
                       float* workspace, long ws_elems, void* stream);
+/* x == NULL in ea_dwconv_glu_bwd: the conv input is recomputed as glu(g2) (C % 4 == 0, g2 8-B
+ * aligned).  ea_dwconv_fwd_glu: ea_dwconv_fwd of x = glu(g2) = a * sigmoid(b) computed from the
+ * bf16 pointwise_conv1 output in the tile loader (ea_glu_fwd's arithmetic, f32): the GLU
+ * activation (convolution.py:66) is never stored. */
+int ea_dwconv_fwd_glu(int B, int T, int C, int K, const void* g2, const float* w, const float* bias,
+                      float* y, void* stream);
 /* ea_dwconv_bwd without the parameter reductions (K in {3,5,7,15,31}): dx, and per-block
  * partials part[p][0 : C*K] of dw in its (C, 1, K) layout and part[p][C*K : C*(K+1)] of dbias,
  * p < *nparts (row stride C*(K+1)) — plain row sums the caller may defer and group. */

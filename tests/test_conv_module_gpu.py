@@ -92,3 +92,46 @@ def test_dwconv_glu_bwd_fused(B, T, C, K):
     torch.testing.assert_close(dg2.double().cpu(), g2r.grad, atol=3e-2, rtol=1e-2)
     torch.testing.assert_close(dw.double().cpu(), wr.grad, atol=2e-2, rtol=1e-3)
     torch.testing.assert_close(db.double().cpu(), bias.grad, atol=2e-3, rtol=1e-4)
+
+
+@pytest.mark.parametrize("B,T,C,K", [(32, 249, 512, 31), (3, 37, 64, 31), (2, 70, 128, 15), (4, 20, 64, 3)])
+def test_dwconv_glu_in_conv(B, T, C, K):
+    """The depthwise conv of glu(g2) computed in the tile loaders (no stored f32 GLU activation):
+    ea_dwconv_fwd_glu vs ea_glu_fwd + ea_dwconv_fwd, and ea_dwconv_glu_bwd with x = NULL vs with
+    the stored activation — the same conv-input values (bit-identical glu), tap sums equal up to
+    last-ulp contraction differences; and the forward vs fp64."""
+    from espnet_amd._lib import lib
+    from espnet_amd import hip_ops as ops
+    g = torch.Generator().manual_seed(7 * B + T + C + K)
+    N = B * T
+    g2 = torch.randn(N, 2 * C, generator=g).to(torch.bfloat16).cuda()
+    w = (torch.randn(C, K, generator=g) * 0.2).cuda()
+    bias = torch.randn(C, generator=g).cuda()
+    dy = torch.randn(N, C, generator=g).cuda()
+    st = ops.stream()
+    glu = torch.empty(N, C, device="cuda")
+    assert lib.ea_glu_fwd(N, C, g2.data_ptr(), ops.dt(g2), glu.data_ptr(), 0, st) == 0
+    y0 = torch.empty(N, C, device="cuda")
+    assert lib.ea_dwconv_fwd(B, T, C, K, glu.data_ptr(), w.data_ptr(), bias.data_ptr(), y0.data_ptr(), st) == 0
+    y = torch.empty(N, C, device="cuda")
+    assert lib.ea_dwconv_fwd_glu(B, T, C, K, g2.data_ptr(), w.data_ptr(), bias.data_ptr(), y.data_ptr(), st) == 0
+    ws = torch.empty(B * ((T + 31) // 32) * C * (K + 1) + 1024, device="cuda")
+    outs = []
+    for x in (glu.data_ptr(), None):
+        dg2 = torch.empty(N, 2 * C, dtype=torch.bfloat16, device="cuda")
+        dw = torch.zeros(C, K, device="cuda")
+        db = torch.zeros(C, device="cuda")
+        assert lib.ea_dwconv_glu_bwd(B, T, C, K, x, w.data_ptr(), dy.data_ptr(), g2.data_ptr(), dg2.data_ptr(),
+                                     dw.data_ptr(), db.data_ptr(), 1, ws.data_ptr(), ws.numel(), st) == 0
+        outs.append((dg2, dw, db))
+    torch.cuda.synchronize()
+    torch.testing.assert_close(y, y0, atol=1e-5, rtol=1e-5)
+    (a0, w0, b0), (a1, w1, b1) = outs
+    torch.testing.assert_close(a1.float(), a0.float(), atol=1e-6, rtol=8e-3)
+    torch.testing.assert_close(w1, w0, atol=1e-5, rtol=1e-5)
+    torch.testing.assert_close(b1, b0, atol=1e-5, rtol=1e-5)
+    g2r = g2.double().cpu()
+    xr = (g2r[:, :C] * torch.sigmoid(g2r[:, C:])).view(B, T, C).transpose(1, 2)
+    yr = torch.nn.functional.conv1d(xr, w.double().cpu().view(C, 1, K), bias.double().cpu(), padding=(K - 1) // 2,
+                                    groups=C)
+    torch.testing.assert_close(y.double().cpu(), yr.transpose(1, 2).reshape(N, C), atol=1e-4, rtol=1e-4)
