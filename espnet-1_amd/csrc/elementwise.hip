@@ -635,11 +635,16 @@ EA_DEV float glu1(const bf16* __restrict__ g2, long row, int C, int c) {
   return to_f(g2[row * 2 * C + c]) * sigmoidf_(to_f(g2[row * 2 * C + C + c]));
 }
 
-template <int K, int R, bool G2IN = false>
+// STATS: also the following BatchNorm's batch-statistics partials of this block's rows
+// (conformer/convolution.py:75): part[blockIdx.x][c] = sum (y - bias[c]), part[..][C + c] =
+// sum (y - bias[c])^2 (f32, the 4 row groups combined in fixed order) — the shifted sums the
+// finalize pass turns into mean / var in fp64, without re-reading y
+template <int K, int R, bool G2IN = false, bool STATS = false>
 __global__ __launch_bounds__(256) void dwconv_fwd_k_kernel(int B, int T, int C, const float* __restrict__ x,
                                                            const float* __restrict__ w,
                                                            const float* __restrict__ bias, float* __restrict__ y,
-                                                           const bf16* __restrict__ g2 = nullptr) {
+                                                           const bf16* __restrict__ g2 = nullptr,
+                                                           float* __restrict__ part = nullptr) {
   constexpr int P = (K - 1) / 2, TT = 4 * R, RL = TT + K - 1, WIN = R + K - 1;
   __shared__ float tile[RL * DW_CT];
   __shared__ float wsm[K * DW_CT];  // [k][c]
@@ -687,12 +692,12 @@ __global__ __launch_bounds__(256) void dwconv_fwd_k_kernel(int B, int T, int C, 
     }
   }
   __syncthreads();
-  if (c >= C) return;
+  if (!STATS && c >= C) return;
   float win[WIN];
 #pragma unroll
   for (int i = 0; i < WIN; ++i) win[i] = tile[(tq * R + i) * DW_CT + cc];
   float acc[R];
-  const float b0 = bias ? bias[c] : 0.f;
+  const float b0 = bias && c < C ? bias[c] : 0.f;
 #pragma unroll
   for (int j = 0; j < R; ++j) acc[j] = b0;
 #pragma unroll
@@ -701,10 +706,28 @@ __global__ __launch_bounds__(256) void dwconv_fwd_k_kernel(int B, int T, int C, 
 #pragma unroll
     for (int j = 0; j < R; ++j) acc[j] += wk * win[j + k];
   }
+  float s1 = 0.f, s2 = 0.f;
 #pragma unroll
   for (int j = 0; j < R; ++j) {
     const int t = t0 + tq * R + j;
-    if (t < T) y[((long)b * T + t) * C + c] = acc[j];
+    if (t < T && c < C) {
+      y[((long)b * T + t) * C + c] = acc[j];
+      if constexpr (STATS) {
+        const float d = acc[j] - b0;
+        s1 += d;
+        s2 += d * d;
+      }
+    }
+  }
+  if constexpr (STATS) {
+    __shared__ float red[2][4][DW_CT];
+    red[0][tq][cc] = s1;
+    red[1][tq][cc] = s2;
+    __syncthreads();
+    if (tq == 0 && c < C) {
+      part[(long)blockIdx.x * 2 * C + c] = (red[0][0][cc] + red[0][1][cc]) + (red[0][2][cc] + red[0][3][cc]);
+      part[(long)blockIdx.x * 2 * C + C + c] = (red[1][0][cc] + red[1][1][cc]) + (red[1][2][cc] + red[1][3][cc]);
+    }
   }
 }
 
@@ -1269,6 +1292,33 @@ extern "C" int ea_dwconv_fwd_glu(int B, int T, int C, int K, const void* g2, con
 #undef EA_DWF
   }
   EA_LAUNCH_CHECK();
+  return 0;
+}
+
+extern "C" int ea_dwconv_fwd_glu_stats(int B, int T, int C, int K, const void* g2, const float* w, const float* bias,
+                                       float* y, float* part, void* stream) {
+  EA_ENTRY();
+  EA_CHECK_ARG((K == 3 || K == 5 || K == 7 || K == 15 || K == 31) && g2 && y && part && bias && C % 4 == 0 &&
+               ((uintptr_t)g2 % 8) == 0);
+  dim3 gridr(B * ea_cdiv(T, 4 * DW_R), ea_cdiv(C, DW_CT));
+  hipStream_t st = (hipStream_t)stream;
+  switch (K) {
+#define EA_DWF(KK)                                                                                            \
+  case KK:                                                                                                    \
+    hipLaunchKernelGGL((dwconv_fwd_k_kernel<KK, DW_R, true, true>), gridr, dim3(256), 0, st, B, T, C,           \
+                       (const float*)nullptr, w, bias, y, (const bf16*)g2, part);                             \
+    break;
+    EA_DWF(3) EA_DWF(5) EA_DWF(7) EA_DWF(15) EA_DWF(31)
+#undef EA_DWF
+  }
+  EA_LAUNCH_CHECK();
+  return 0;
+}
+
+extern "C" int ea_dwconv_stats_parts(int B, int T, int* nparts) {
+  EA_ENTRY();
+  EA_CHECK_ARG(nparts != nullptr && B > 0 && T > 0);
+  *nparts = B * ea_cdiv(T, 4 * DW_R);
   return 0;
 }
 

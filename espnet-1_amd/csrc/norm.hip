@@ -677,7 +677,8 @@ __global__ __launch_bounds__(256) void bn_finalize_par_kernel(int rows, int C, i
                                                               const float* __restrict__ part, float eps, float momentum,
                                                               float* __restrict__ mean, float* __restrict__ rstd,
                                                               float* __restrict__ run_mean, float* __restrict__ run_var,
-                                                              long long* __restrict__ nbt) {
+                                                              long long* __restrict__ nbt,
+                                                              const float* __restrict__ shift = nullptr) {
   __shared__ double red[2][BNF_P][BNF_C];
   const int cx = threadIdx.x % BNF_C, py = threadIdx.x / BNF_C;
   const int c = blockIdx.x * BNF_C + cx;
@@ -712,7 +713,7 @@ __global__ __launch_bounds__(256) void bn_finalize_par_kernel(int rows, int C, i
   const double m = s / n;
   double var = ss / n - m * m;
   if (var < 0) var = 0;
-  const double mu = m + (double)y[c];
+  const double mu = m + (double)(shift ? shift[c] : y[c]);  // the partials' shift: row 0 of y, or given
   mean[c] = (float)mu;
   rstd[c] = (float)(1.0 / sqrt(var + (double)eps));
   if (run_mean) {
@@ -1143,6 +1144,28 @@ extern "C" int ea_scale_dropout_colsum(long rows, int cols, const float* x, long
   EA_LAUNCH_CHECK();
   hipLaunchKernelGGL(reduce_partials_kernel, dim3(ea_cdiv(cols, RP_CW)), dim3(256), 0, st, np, cols, workspace, (long)cols,
                      colsum, accumulate);
+  EA_LAUNCH_CHECK();
+  return 0;
+}
+
+extern "C" int ea_batchnorm_fwd_parts(int rows, int C, const float* y, const float* part, int nparts,
+                                      const float* shift, const float* gamma, const float* beta, float eps,
+                                      float momentum, float* mean, float* rstd, float* running_mean,
+                                      float* running_var, long long* num_batches_tracked, int act, void* z,
+                                      int z_dtype, void* stream) {
+  EA_ENTRY();
+  EA_CHECK_ARG(rows > 0 && nparts > 0 && part && shift && C % 4 == 0 && ((uintptr_t)y % 16) == 0 &&
+               ((uintptr_t)z % (z_dtype == EA_BF16 ? 8 : 16)) == 0);
+  hipStream_t st = (hipStream_t)stream;
+  hipLaunchKernelGGL(bn_finalize_par_kernel, dim3(ea_cdiv(C, BNF_C)), dim3(256), 0, st, rows, C, nparts, y, part, eps,
+                     momentum, mean, rstd, running_mean, running_var, num_batches_tracked, shift);
+  EA_LAUNCH_CHECK();
+  const long total = (long)rows * C;
+  dim3 g4(ea_grid_cap(ea_cdiv(total / 4, 256)));
+  if (z_dtype == EA_BF16)
+    hipLaunchKernelGGL(bn_apply_act_vec_kernel<bf16>, g4, dim3(256), 0, st, rows, C, y, mean, rstd, gamma, beta, act, (bf16*)z);
+  else
+    hipLaunchKernelGGL(bn_apply_act_vec_kernel<float>, g4, dim3(256), 0, st, rows, C, y, mean, rstd, gamma, beta, act, (float*)z);
   EA_LAUNCH_CHECK();
   return 0;
 }

@@ -55,6 +55,9 @@ FUSE_DW_GLU = os.environ.get("EA_FUSE_DW_GLU", "1") != "0"
 # instead of a stored f32 GLU activation (ea_dwconv_fwd_glu / ea_dwconv_glu_bwd with x = NULL;
 # EA_GLU_IN_CONV=0: glu_fwd + the stored activation)
 GLU_IN_CONV = os.environ.get("EA_GLU_IN_CONV", "1") != "0"
+# with it, the depthwise conv forward also writes the BatchNorm's batch-statistics partials
+# (ea_dwconv_fwd_glu_stats + ea_batchnorm_fwd_parts; EA_BN_STATS_IN_CONV=1; off until measured)
+BN_STATS_IN_CONV = os.environ.get("EA_BN_STATS_IN_CONV", "0") == "1"
 
 
 def _glu_in_conv(K, g2, d):
@@ -289,12 +292,22 @@ class ConformerBlockFn(torch.autograd.Function):
         ops.linear(xn3, b.w(C + "pointwise_conv1.weight", shape=(2 * d, d)), g2,
                    epi=ops.make_epi(bias=b.f(C + "pointwise_conv1.bias")))
         y = empty(N, d, device=dev)
+        bn_part = None
         if _glu_in_conv(K, g2, d):
             # the depthwise conv reads glu(g2) straight from the pointwise conv's bf16 output; the
             # f32 GLU activation is neither stored nor re-read (the backward recomputes it too)
             glu = None
-            lib.ea_dwconv_fwd_glu(B, T, d, K, g2.data_ptr(), b.f(C + "depthwise_conv.weight").data_ptr(),
-                                  b.f(C + "depthwise_conv.bias").data_ptr(), y.data_ptr(), ops.stream())
+            if training and BN_STATS_IN_CONV:
+                # ... and writes the BatchNorm's batch-statistics partials of its tiles
+                npart = ctypes.c_int(0)
+                lib.ea_dwconv_stats_parts(B, T, ctypes.addressof(npart))
+                bn_part = (empty(npart.value * 2 * d, device=dev), npart.value)
+                lib.ea_dwconv_fwd_glu_stats(B, T, d, K, g2.data_ptr(), b.f(C + "depthwise_conv.weight").data_ptr(),
+                                            b.f(C + "depthwise_conv.bias").data_ptr(), y.data_ptr(),
+                                            bn_part[0].data_ptr(), ops.stream())
+            else:
+                lib.ea_dwconv_fwd_glu(B, T, d, K, g2.data_ptr(), b.f(C + "depthwise_conv.weight").data_ptr(),
+                                      b.f(C + "depthwise_conv.bias").data_ptr(), y.data_ptr(), ops.stream())
         else:
             glu = empty(N, d, device=dev)
             lib.ea_glu_fwd(N, d, g2.data_ptr(), ops.dt(g2), glu.data_ptr(), 0, ops.stream())
@@ -304,9 +317,17 @@ class ConformerBlockFn(torch.autograd.Function):
         bn_mean = empty(d, device=dev)
         bn_rstd = empty(d, device=dev)
         bn = L.conv_module.norm
-        ops.batchnorm_fwd(y, b.f(C + "norm.weight"), b.f(C + "norm.bias"), bn_mean, bn_rstd,
-                          bn.running_mean, bn.running_var, bn.num_batches_tracked, z,
-                          training, ACT_SWISH, eps=bn.eps, momentum=bn.momentum)
+        if bn_part is not None:
+            lib.ea_batchnorm_fwd_parts(N, d, y.data_ptr(), bn_part[0].data_ptr(), bn_part[1],
+                                       b.f(C + "depthwise_conv.bias").data_ptr(), b.f(C + "norm.weight").data_ptr(),
+                                       b.f(C + "norm.bias").data_ptr(), float(bn.eps), float(bn.momentum),
+                                       bn_mean.data_ptr(), bn_rstd.data_ptr(), ops.ptr(bn.running_mean),
+                                       ops.ptr(bn.running_var), ops.ptr(bn.num_batches_tracked), ACT_SWISH,
+                                       z.data_ptr(), ops.dt(z), ops.stream())
+        else:
+            ops.batchnorm_fwd(y, b.f(C + "norm.weight"), b.f(C + "norm.bias"), bn_mean, bn_rstd,
+                              bn.running_mean, bn.running_var, bn.num_batches_tracked, z,
+                              training, ACT_SWISH, eps=bn.eps, momentum=bn.momentum)
         x3 = empty(N, d, device=dev)
         ops.linear(z, b.w(C + "pointwise_conv2.weight", shape=(d, d)), x3,
                    epi=ops.make_epi(EPI_RESID, bias=b.f(C + "pointwise_conv2.bias"), resid=x2,

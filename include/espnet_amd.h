@@ -311,6 +311,14 @@ int ea_batchnorm_fwd(int rows, int C, const float* y, const float* gamma, const 
                      float* running_mean, float* running_var, long long* num_batches_tracked,
                      int act, void* z, int z_dtype, float* workspace, long ws_elems, void* stream);
 
+/* ea_batchnorm_fwd (training) from precomputed shifted partial sums part[nparts][2C] of y
+ * (sum (y - shift[c]), sum (y - shift[c])^2): fp64 finalize (mean, rstd, running stats,
+ * num_batches_tracked) and the BN + activation pass.  C % 4 == 0. */
+int ea_batchnorm_fwd_parts(int rows, int C, const float* y, const float* part, int nparts, const float* shift,
+                           const float* gamma, const float* beta, float eps, float momentum, float* mean,
+                           float* rstd, float* running_mean, float* running_var, long long* num_batches_tracked,
+                           int act, void* z, int z_dtype, void* stream);
+
 /* Backward of z = act(BN_train(y)): dy, dgamma/dbeta (dbeta == dgamma + C).
  * workspace >= (min(ceil(rows/16), 256) + 1) * 2C floats. */
 int ea_batchnorm_bwd(int rows, int C, const void* dz, int dz_dtype, const float* y, const float* mean,
@@ -443,6 +451,13 @@ int ea_dwconv_glu_bwd(int B, int T, int C, int K, const float* x, const float* w
  * activation (convolution.py:66) is never stored. */
 int ea_dwconv_fwd_glu(int B, int T, int C, int K, const void* g2, const float* w, const float* bias,
                       float* y, void* stream);
+/* ea_dwconv_fwd_glu that also writes the following BatchNorm's batch-statistics partials
+ * (convolution.py:75) of each (utterance, 64-frame tile) block: part[p][c] = sum (y - bias[c]),
+ * part[p][C + c] = sum (y - bias[c])^2, p < *nparts (ea_dwconv_stats_parts); ea_batchnorm_fwd_parts
+ * then finalizes them (shift = bias) and applies BN + activation without a statistics pass over y. */
+int ea_dwconv_fwd_glu_stats(int B, int T, int C, int K, const void* g2, const float* w, const float* bias,
+                            float* y, float* part, void* stream);
+int ea_dwconv_stats_parts(int B, int T, int* nparts);
 /* ea_dwconv_bwd without the parameter reductions (K in {3,5,7,15,31}): dx, and per-block
  * partials part[p][0 : C*K] of dw in its (C, 1, K) layout and part[p][C*K : C*(K+1)] of dbias,
  * p < *nparts (row stride C*(K+1)) — plain row sums the caller may defer and group. */

@@ -135,3 +135,54 @@ def test_dwconv_glu_in_conv(B, T, C, K):
     yr = torch.nn.functional.conv1d(xr, w.double().cpu().view(C, 1, K), bias.double().cpu(), padding=(K - 1) // 2,
                                     groups=C)
     torch.testing.assert_close(y.double().cpu(), yr.transpose(1, 2).reshape(N, C), atol=1e-4, rtol=1e-4)
+
+
+@pytest.mark.parametrize("B,T,C,K", [(32, 249, 512, 31), (3, 37, 64, 31), (4, 20, 64, 3)])
+def test_bn_stats_in_dwconv_fwd(B, T, C, K):
+    """ea_dwconv_fwd_glu_stats + ea_batchnorm_fwd_parts (the BatchNorm statistics from the conv's
+    own tiles, shifted by the conv bias) vs ea_dwconv_fwd_glu + ea_batchnorm_fwd, and the batch
+    mean / variance vs fp64."""
+    import ctypes
+    from espnet_amd._lib import lib
+    from espnet_amd import hip_ops as ops
+    from espnet_amd.layers.common import ACT_SWISH
+    g = torch.Generator().manual_seed(11 * B + T + C + K)
+    N = B * T
+    g2 = torch.randn(N, 2 * C, generator=g).to(torch.bfloat16).cuda()
+    w = (torch.randn(C, K, generator=g) * 0.2).cuda()
+    bias = torch.randn(C, generator=g).cuda()
+    gamma = (torch.rand(C, generator=g) + 0.5).cuda()
+    beta = (torch.randn(C, generator=g) * 0.1).cuda()
+    st = ops.stream()
+    res = []
+    for fused in (False, True):
+        y = torch.empty(N, C, device="cuda")
+        mean, rstd = torch.empty(C, device="cuda"), torch.empty(C, device="cuda")
+        rm, rv = torch.zeros(C, device="cuda"), torch.ones(C, device="cuda")
+        nbt = torch.zeros(1, dtype=torch.int64, device="cuda")
+        z = torch.empty(N, C, dtype=torch.bfloat16, device="cuda")
+        if fused:
+            npart = ctypes.c_int(0)
+            assert lib.ea_dwconv_stats_parts(B, T, ctypes.addressof(npart)) == 0
+            part = torch.empty(npart.value * 2 * C, device="cuda")
+            assert lib.ea_dwconv_fwd_glu_stats(B, T, C, K, g2.data_ptr(), w.data_ptr(), bias.data_ptr(), y.data_ptr(),
+                                               part.data_ptr(), st) == 0
+            assert lib.ea_batchnorm_fwd_parts(N, C, y.data_ptr(), part.data_ptr(), npart.value, bias.data_ptr(),
+                                              gamma.data_ptr(), beta.data_ptr(), 1e-5, 0.1, mean.data_ptr(),
+                                              rstd.data_ptr(), rm.data_ptr(), rv.data_ptr(), nbt.data_ptr(), ACT_SWISH,
+                                              z.data_ptr(), ops.dt(z), st) == 0
+        else:
+            assert lib.ea_dwconv_fwd_glu(B, T, C, K, g2.data_ptr(), w.data_ptr(), bias.data_ptr(), y.data_ptr(),
+                                         st) == 0
+            ops.batchnorm_fwd(y, gamma, beta, mean, rstd, rm, rv, nbt, z, True, ACT_SWISH, eps=1e-5, momentum=0.1)
+        res.append((y, mean, rstd, rm, rv, nbt, z))
+    torch.cuda.synchronize()
+    (y0, m0, r0, rm0, rv0, n0, z0), (y1, m1, r1, rm1, rv1, n1, z1) = res
+    assert torch.equal(y0, y1) and int(n0) == int(n1) == 1
+    for a, b_ in ((m0, m1), (r0, r1), (rm0, rm1), (rv0, rv1)):
+        torch.testing.assert_close(b_, a, atol=1e-5, rtol=1e-5)
+    torch.testing.assert_close(z1.float(), z0.float(), atol=2e-2, rtol=1e-2)
+    yd = y0.double().cpu()
+    torch.testing.assert_close(m1.double().cpu(), yd.mean(0), atol=1e-5, rtol=1e-5)
+    torch.testing.assert_close(r1.double().cpu(), 1.0 / torch.sqrt(yd.var(0, unbiased=False) + 1e-5), atol=1e-5,
+                               rtol=1e-5)
