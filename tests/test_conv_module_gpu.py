@@ -178,7 +178,9 @@ def test_bn_stats_in_dwconv_fwd(B, T, C, K):
         res.append((y, mean, rstd, rm, rv, nbt, z))
     torch.cuda.synchronize()
     (y0, m0, r0, rm0, rv0, n0, z0), (y1, m1, r1, rm1, rv1, n1, z1) = res
-    assert torch.equal(y0, y1) and int(n0) == int(n1) == 1
+    # (the two conv instantiations may contract the tap sums differently: last-ulp differences)
+    torch.testing.assert_close(y1, y0, atol=1e-5, rtol=1e-5)
+    assert int(n0) == int(n1) == 1
     for a, b_ in ((m0, m1), (r0, r1), (rm0, rm1), (rv0, rv1)):
         torch.testing.assert_close(b_, a, atol=1e-5, rtol=1e-5)
     torch.testing.assert_close(z1.float(), z0.float(), atol=2e-2, rtol=1e-2)
