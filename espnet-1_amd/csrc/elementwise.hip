@@ -1333,20 +1333,25 @@ extern "C" int ea_dwconv_glu_bwd(int B, int T, int C, int K, const float* x, con
   const long rowlen = (long)C * (K + 1);
   EA_CHECK_ARG((long)nblkr * rowlen <= ws_elems);
   hipStream_t st = (hipStream_t)stream;
+  // dw (C, 1, K) and dbias adjacent (the parameter arena's layout): ONE reduction over the
+  // (K + 1) C partial columns, the dw block written transposed and the dbias block straight
+  // (the same sums in the same order as the two reductions)
+  const bool adj = dbias == dw + (long)C * K;
   switch (K) {
-#define EA_DWB(KK)                                                                                            \
-  case KK:                                                                                                    \
-    if (x)                                                                                                    \
-      hipLaunchKernelGGL((dwconv_bwd_k_kernel<KK, DW_R, false, true>), gridr, dim3(256), 0, st, B, T, C, x, w, dy, \
-                         (float*)nullptr, workspace, (const bf16*)g2, (bf16*)dg2);                                  \
-    else                                                                                                      \
-      hipLaunchKernelGGL((dwconv_bwd_k_kernel<KK, DW_R, false, true, true>), gridr, dim3(256), 0, st, B, T, C,    \
-                         (const float*)nullptr, w, dy, (float*)nullptr, workspace, (const bf16*)g2, (bf16*)dg2);    \
+#define EA_DWB(KK)                                                                                              \
+  case KK:                                                                                                      \
+    if (x)                                                                                                      \
+      hipLaunchKernelGGL((dwconv_bwd_k_kernel<KK, DW_R, false, true>), gridr, dim3(256), 0, st, B, T, C, x, w, dy,   \
+                         (float*)nullptr, workspace, (const bf16*)g2, (bf16*)dg2);                                    \
+    else                                                                                                        \
+      hipLaunchKernelGGL((dwconv_bwd_k_kernel<KK, DW_R, false, true, true>), gridr, dim3(256), 0, st, B, T, C,      \
+                         (const float*)nullptr, w, dy, (float*)nullptr, workspace, (const bf16*)g2, (bf16*)dg2);      \
     break;
     EA_DWB(3) EA_DWB(5) EA_DWB(7) EA_DWB(15) EA_DWB(31)
 #undef EA_DWB
   }
   EA_LAUNCH_CHECK();
+  if (adj) return ea_reduce_partials_tr(nblkr, (int)rowlen, workspace, rowlen, dw, accumulate_params, C, K, stream);
   int rc = ea_reduce_partials_tr(nblkr, C * K, workspace, rowlen, dw, accumulate_params, C, K, stream);
   if (rc) return rc;
   return ea_reduce_partials(nblkr, C, workspace + (long)C * K, rowlen, dbias, accumulate_params, stream);

@@ -140,7 +140,8 @@ __global__ __launch_bounds__(256) void reduce_partials_kernel(int nparts, int n,
     double t = 0.0;
 #pragma unroll
     for (int l = 0; l < RP_PL; ++l) t += red[l][cx];
-    const long o = tr_rows > 0 ? (long)(c % tr_rows) * tr_cols + c / tr_rows : c;
+    // columns [0, tr_rows * tr_cols) written transposed, any after them straight
+    const long o = tr_rows > 0 && c < tr_rows * tr_cols ? (long)(c % tr_rows) * tr_cols + c / tr_rows : c;
     out[o] = accumulate ? out[o] + (float)t : (float)t;
   }
 }

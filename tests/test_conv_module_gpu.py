@@ -72,7 +72,15 @@ def test_dwconv_glu_bwd_fused(B, T, C, K):
     db = torch.zeros(C, device="cuda")
     assert lib.ea_dwconv_glu_bwd(B, T, C, K, glu.data_ptr(), w.data_ptr(), dy.data_ptr(), g2.data_ptr(),
                                  dg2.data_ptr(), dw.data_ptr(), db.data_ptr(), 1, ws.data_ptr(), ws.numel(), st) == 0
+    # dw / dbias adjacent (the parameter arena's layout): one reduction, the same sums
+    pa = torch.zeros(C * K + C, device="cuda")
+    dg2a = torch.empty(N, 2 * C, dtype=torch.bfloat16, device="cuda")
+    assert lib.ea_dwconv_glu_bwd(B, T, C, K, glu.data_ptr(), w.data_ptr(), dy.data_ptr(), g2.data_ptr(),
+                                 dg2a.data_ptr(), pa.data_ptr(), pa[C * K:].data_ptr(), 1, ws.data_ptr(), ws.numel(),
+                                 st) == 0
     torch.cuda.synchronize()
+    assert torch.equal(pa[:C * K].view(C, K), dw) and torch.equal(pa[C * K:], db)
+    assert torch.equal(dg2a.view(torch.int16), dg2.view(torch.int16))
     # the same arithmetic as the two-kernel path; the tap sums may round differently where the
     # compiler contracts them differently (last-ulp differences, visible only where the 31-tap sum
     # cancels to ~1e-7 of its terms): a handful of elements within one bf16 ulp or 1e-6
