@@ -197,6 +197,14 @@ class CapturedTrainStep:
         cap.maxlens = maxlens
         g = torch.cuda.CUDAGraph()
         torch.cuda.synchronize()
+        import torch.distributed as dist
+        if dist.is_available() and dist.is_initialized():
+            # the warm-up steps' collectives are complete now, but the process-group watchdog
+            # only retires them at its next poll (~100 ms); a poll during the capture queries an
+            # event last recorded on the now-capturing RCCL stream, which HIP refuses, and the
+            # watchdog aborts the process — let it retire them first
+            import time
+            time.sleep(0.5)
         # thread-local capture mode: other threads' HIP calls during the capture (RCCL's
         # process-group watchdog polls its events) must not invalidate it or fail themselves
         with torch.cuda.graph(g, pool=self._pool, capture_error_mode="thread_local"):
