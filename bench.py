@@ -233,6 +233,8 @@ def main():
     if world > 1:
         os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
         if backend == "nccl":
+            from espnet_amd.train.graph import prepare_nccl_env
+            prepare_nccl_env()
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
         else:
             dist.init_process_group(backend)
@@ -298,6 +300,7 @@ def main():
     for _ in range(max(args.warmup, 0 if eager else 3)):
         step()
     torch.cuda.synchronize()
+    sync_capture_mode(runner, world)
     probe.reset()
     # per-step HIP events on the step's stream (median step time)
     elapsed, step_ms, (loss, stats, weight, gn) = timed(step, args.steps)
@@ -374,6 +377,18 @@ def main():
         dist.destroy_process_group()
 
 
+def sync_capture_mode(runner, world):
+    """After the warm-up (outside any capture): if a capture failed on any rank, every rank
+    runs eager steps, so the timed region measures one mode.  Ranks capture on their own
+    (train/graph.py: per-rank shape keys, no collective at capture time)."""
+    if world <= 1:
+        return
+    flag = torch.tensor([runner.capture_failed_flag()], dtype=torch.int32, device=torch.cuda.current_device())
+    dist.all_reduce(flag)
+    if int(flag.item()) > 0:
+        runner.force_eager()
+
+
 def dp_rehearsal(model, opt, sched, batch, maxlens, cfg, eager, args, timed):
     """The per-rank step of an N-GPU job, timed on this one GPU: a world-1 RCCL group and
     ArenaDataParallel(force_collectives=True), so the step issues every collective of an
@@ -393,6 +408,8 @@ def dp_rehearsal(model, opt, sched, batch, maxlens, cfg, eager, args, timed):
                 with socket.socket() as sk:
                     sk.bind(("127.0.0.1", 0))
                     os.environ["MASTER_PORT"] = str(sk.getsockname()[1])
+            from espnet_amd.train.graph import prepare_nccl_env
+            prepare_nccl_env()
             dist.init_process_group("nccl", rank=0, world_size=1, device_id=batch["speech"].device)
             own = True
         dp = ArenaDataParallel(model, force_collectives=True)
@@ -455,6 +472,7 @@ def run_c5(args, world, rank, dev):
     for i in range(warmup):
         step(i)
     torch.cuda.synchronize()
+    sync_capture_mode(runner, world)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -490,7 +508,7 @@ def run_c5(args, world, rank, dev):
                        "global_batch": None, "seq_len": "200-2000", "parallelism": f"dp{world}"},
             "frames_per_s": round(n_frames / elapsed, 1),
             "padding_fraction": round(1.0 - n_frames / n_padded, 4),
-            "batches_in_corpus_per_rank": nb, "loss": round(float(loss.item()), 4),
+            "batches_in_corpus_per_rank": nb, "step_mode": runner.mode or "eager", "loss": round(float(loss.item()), 4),
         }), flush=True)
     if world > 1:
         dist.destroy_process_group()

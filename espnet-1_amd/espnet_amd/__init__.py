@@ -6,13 +6,5 @@ libespnet_amd.so (see include/espnet_amd.h).
 """
 __version__ = "0.1.0"
 
-import os as _os
-
-# The training step is captured as a hipGraph WITH its RCCL collectives.  ProcessGroupNCCL
-# recycles CUDA events between work objects by default; an event recycled into a captured
-# collective, while the process-group watchdog still polls the eager warm-up step's work that
-# owned it, makes the watchdog's query fail ("event last recorded in a capturing stream") and
-# abort the process.  Fresh events per work object keep the two apart.  Must be set before the
-# process group is created (read at construction).
-_os.environ.setdefault("TORCH_NCCL_CUDA_EVENT_CACHE", "0")
-
+# TORCH_NCCL_CUDA_EVENT_CACHE=0 is set where this package creates an RCCL process group
+# (train.graph.prepare_nccl_env), not on import.

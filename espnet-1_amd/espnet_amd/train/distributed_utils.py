@@ -82,6 +82,9 @@ class DistributedOption:
         if not self.distributed:
             return
         os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+        if self.dist_backend == "nccl":
+            from .graph import prepare_nccl_env
+            prepare_nccl_env()
         kwargs = {}
         if self.ngpu > 0 and self.local_rank is not None:
             torch.cuda.set_device(self.device_index())

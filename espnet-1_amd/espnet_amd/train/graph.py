@@ -41,14 +41,71 @@ def _backend(group) -> str:
         return ""
 
 
+def prepare_nccl_env():
+    """Call before creating an RCCL process group that will carry captured collectives.
+    ProcessGroupNCCL recycles HIP events between work objects by default; fresh events keep
+    every captured collective's event distinct from the eager warm-up work the watchdog
+    tracked (read at process-group construction, so set here, not at package import)."""
+    import os
+    os.environ.setdefault("TORCH_NCCL_CUDA_EVENT_CACHE", "0")
+
+
+def _retire_pending_works(group):
+    """Block until the process-group watchdog has retired every eager collective of `group`.
+
+    The warm-up steps' collectives are complete once the device is synchronised, but the
+    watchdog only drops their work objects at its next poll; a poll during the capture would
+    query an event last recorded on the now-capturing RCCL stream, which HIP refuses, and the
+    watchdog aborts the process.  ProcessGroupNCCL::waitForPendingWorks waits for exactly that
+    retirement (no timing assumption).  gloo groups carry no device events."""
+    import torch.distributed as dist
+    if not (dist.is_available() and dist.is_initialized()):
+        return
+    pg = group if group is not None else dist.distributed_c10d._get_default_group()
+    if _backend(pg) != "nccl":
+        return
+    pg._wait_for_pending_works()
+
+
 class _Captured:
-    __slots__ = ("graph", "inputs", "outputs", "maxlens")
+    __slots__ = ("graph", "inputs", "outputs", "maxlens", "update")
+
+
+class _PseudoGraph:
+    """Test double of a captured graph (CapturedTrainStep(pseudo_capture=True)): 'capture'
+    executes nothing and every replay runs the eager step on the static inputs, so the capture
+    bookkeeping (per-rank shape keys, warm-up counts, failure handling) runs over collectives
+    a hipGraph cannot hold (gloo ranks sharing one GPU)."""
+
+    def __init__(self, runner, cap):
+        self.runner, self.cap = runner, cap
+
+    def replay(self):
+        self.cap.outputs = self.runner._eager(self.cap.inputs, self.cap.maxlens, self.cap.update)
 
 
 class CapturedTrainStep:
+    """Captures per input shape and replays; see the module docstring.
+
+    Multi-rank jobs: every rank decides ALONE when it captures.  Ranks hold differently
+    padded shards (the reference pads each rank's batch[rank::world] to its own maxima,
+    abs_task.py:1566-1575), so their shape keys — and the steps at which they capture —
+    differ.  A capture executes no collective, and a replay issues the same collectives in
+    the same order as an eager step on the same communicator, so a rank replaying beside a
+    rank that warms up or captures pairs its collectives correctly.  Nothing here issues a
+    collective of its own.  A failed capture makes this rank run eager steps at once and sets
+    `failed`; `capture_failed_flag()` is packed into the training loop's per-step control
+    all-reduce (trainer.py's iterator_stop message), and `force_eager()` then turns every rank
+    eager at the same step."""
+
     def __init__(self, model, optimizer, scheduler=None, *, grad_clip: float = 5.0, dp=None,
-                 warmup: int = 2, enabled: bool = True, control_group=None):
+                 warmup: int = 2, enabled: bool = True, control_group=None, pseudo_capture: bool = False,
+                 accum_grad: int = 1):
         self.model = model
+        # accum_grad > 1 (trainer.py:619-653): two graphs per input shape — the micro-step
+        # (forward + backward accumulating into the gradient arena) and the micro-step that ends
+        # with clip + Adam + WarmupLR + zero_grad — chosen per call by iiter % accum_grad
+        self.accum_grad = max(1, int(accum_grad))
         self.optimizer = optimizer
         self.scheduler = scheduler
         self.grad_clip = grad_clip
@@ -59,17 +116,43 @@ class CapturedTrainStep:
         self._seen: Dict[tuple, int] = {}
         self._pool = None
         self._side = None
-        self.control_group = control_group  # gloo group for the capture decision (optional)
-        if dp is not None and dp.active and _backend(dp.group) == "gloo":
+        self.control_group = control_group  # kept for callers; the runner issues no collective
+        self.pseudo = pseudo_capture
+        self.failed = False       # a capture failed on this rank
+        self.captures = []        # (call index, key) of every capture on this rank
+        self.calls = 0
+        self._fail_keys = set()   # tests: keys whose capture raises on this rank
+        if dp is not None and dp.active and _backend(dp.group) == "gloo" and not pseudo_capture:
             self.enabled = False  # gloo collectives (host copies) cannot be captured
-        # "graph" once steps replay, "eager" once capture was given up (on any rank); None
-        # while the warm-up steps run
+        if enabled and dp is not None and dp.active and _backend(dp.group) == "nccl":
+            import os
+            import warnings
+            if os.environ.get("TORCH_NCCL_CUDA_EVENT_CACHE") != "0":
+                warnings.warn("TORCH_NCCL_CUDA_EVENT_CACHE is not '0' for this process group: call "
+                              "train.graph.prepare_nccl_env() before init_process_group")
+        # "graph" once steps replay, "eager" once capture was given up; None while the
+        # warm-up steps run
         self.mode = None if self.enabled else "eager"
 
+    # ------------------------------------------------------------------ multi-rank control
+    def capture_failed_flag(self) -> int:
+        """1 when a capture failed on this rank (sent in the per-step control all-reduce)."""
+        return 1 if self.failed else 0
+
+    def force_eager(self):
+        """Every later step eager (another rank's capture failed, or this one's): called at the
+        same step on every rank from the control all-reduce's result."""
+        if self.enabled or self.graphs:
+            torch.cuda.synchronize()
+        self.enabled = False
+        self.mode = "eager"
+        self.graphs.clear()
+
     # ------------------------------------------------------------------ helpers
-    def _eager(self, batch, maxlens):
+    def _eager(self, batch, maxlens, update=True):
         return Trainer.train_one_step(self.model, batch, self.optimizer, self.scheduler,
-                                      grad_clip=self.grad_clip, dp=self.dp, maxlens=maxlens)
+                                      grad_clip=self.grad_clip, accum_grad=self.accum_grad,
+                                      iiter=self.accum_grad if update else 1, dp=self.dp, maxlens=maxlens)
 
     def _device_batch(self, batch, maxlens):
         dev = self.model._device
@@ -108,16 +191,20 @@ class CapturedTrainStep:
             layerdrop_draw(len(m.decoder.decoders))
 
     # ------------------------------------------------------------------ step
-    def __call__(self, batch: Dict[str, torch.Tensor], maxlens: Optional[tuple] = None, lens_host=None):
+    def __call__(self, batch: Dict[str, torch.Tensor], maxlens: Optional[tuple] = None, lens_host=None,
+                 iiter: int = 1):
         """One training step on `batch`; returns (loss, stats, weight, grad_norm).
         `lens_host`: the speech lengths as host ints when the batch's live on the device
-        (SpecAug's per-utterance warp draws need them)."""
+        (SpecAug's per-utterance warp draws need them).  `iiter`: the epoch's 1-based batch
+        index; with accum_grad > 1 the parameters update when iiter % accum_grad == 0."""
         if maxlens is None:
             maxlens = self._maxlens(batch)
+        self.calls += 1
+        update = iiter % self.accum_grad == 0
         if not self.enabled:
-            return self._eager(batch, maxlens)
+            return self._eager(batch, maxlens, update)
         B, _, F = batch["speech"].shape
-        key = (B, maxlens[0], F, maxlens[1])
+        key = (B, maxlens[0], F, maxlens[1], update)
         self._host_draws(batch, maxlens, lens_host)
         common.SKIP_LAYERDROP_DRAWS = True
         try:
@@ -136,34 +223,30 @@ class CapturedTrainStep:
                 main = torch.cuda.current_stream()
                 self._side.wait_stream(main)
                 with torch.cuda.stream(self._side):
-                    out = self._eager(dbatch, maxlens)
+                    out = self._eager(dbatch, maxlens, update)
                 main.wait_stream(self._side)
                 return out
             err = None
             try:
-                cap = self._capture(key, dbatch, maxlens)
+                cap = self._capture(key, dbatch, maxlens, update)
             except RuntimeError as e:
                 cap, err = None, e
                 self._reset_after_failed_capture()
-            # the decision is collective: every rank replays its graph or every rank runs
-            # eager steps (a graph replay beside an eager step would issue the same
-            # collectives, but at a different pace, and the bench would time a mixed mode)
-            if self._agree(cap is not None):
+            if cap is not None:
                 self.graphs[key] = cap
+                self.captures.append((self.calls, key))
                 self.mode = "graph"
                 cap.graph.replay()  # capture executes nothing: run this batch's step now
                 return cap.outputs
             # a stack that cannot capture this step (e.g. a collective library without graph
-            # support on some node) on this rank or another: warn once and run every step
-            # eagerly.  Capture executes nothing, so the step is simply run now.
+            # support on some node): warn once and run every step eagerly on this rank; the
+            # control all-reduce turns the other ranks eager at the next step.  Capture
+            # executes nothing, so the step is simply run now.
             import warnings
-            why = f"failed here ({err})" if err is not None else "failed on another rank"
-            warnings.warn(f"hipGraph capture of the training step {why}; running eager steps")
-            torch.cuda.synchronize()
-            self.enabled = False
-            self.mode = "eager"
-            self.graphs.clear()
-            return self._eager(dbatch, maxlens)
+            warnings.warn(f"hipGraph capture of the training step failed ({err}); running eager steps")
+            self.failed = True
+            self.force_eager()
+            return self._eager(dbatch, maxlens, update)
         finally:
             common.SKIP_LAYERDROP_DRAWS = False
 
@@ -177,38 +260,25 @@ class CapturedTrainStep:
             self.dp._pending = None
             self.dp._works = []
 
-    def _agree(self, ok: bool) -> bool:
-        """True when the capture succeeded on every rank: one MIN-style all-reduce of a failure
-        count over the control group (gloo, host memory) when there is one, else over the
-        data-parallel group.  Without an active DP group this rank decides alone."""
-        dp = self.dp
-        if dp is None or not dp.active:
-            return ok
-        import torch.distributed as dist
-        group = self.control_group
-        dev = "cpu" if group is not None else self.model._device
-        flag = torch.tensor([0 if ok else 1], dtype=torch.int32, device=dev)
-        dist.all_reduce(flag, group=group if group is not None else dp.group)
-        return int(flag.item()) == 0
-
-    def _capture(self, key, dbatch, maxlens):
+    def _capture(self, key, dbatch, maxlens, update=True):
+        if key in self._fail_keys or key[:4] in self._fail_keys:
+            raise RuntimeError(f"injected capture failure for {key}")
         cap = _Captured()
         cap.inputs = dbatch  # static input buffers (own storage)
         cap.maxlens = maxlens
+        cap.update = update
+        if self.pseudo:
+            cap.graph = _PseudoGraph(self, cap)
+            cap.outputs = None
+            return cap
         g = torch.cuda.CUDAGraph()
         torch.cuda.synchronize()
-        import torch.distributed as dist
-        if dist.is_available() and dist.is_initialized():
-            # the warm-up steps' collectives are complete now, but the process-group watchdog
-            # only retires them at its next poll (~100 ms); a poll during the capture queries an
-            # event last recorded on the now-capturing RCCL stream, which HIP refuses, and the
-            # watchdog aborts the process — let it retire them first
-            import time
-            time.sleep(0.5)
+        # the watchdog must hold no eager work of the RCCL group whose stream joins the capture
+        _retire_pending_works(self.dp.group if self.dp is not None and self.dp.active else None)
         # thread-local capture mode: other threads' HIP calls during the capture (RCCL's
         # process-group watchdog polls its events) must not invalidate it or fail themselves
         with torch.cuda.graph(g, pool=self._pool, capture_error_mode="thread_local"):
-            out = self._eager(cap.inputs, maxlens)
+            out = self._eager(cap.inputs, maxlens, update)
         if self._pool is None:
             self._pool = g.pool()
         cap.graph = g

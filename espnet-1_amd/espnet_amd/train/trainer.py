@@ -171,6 +171,8 @@ class Trainer:
         without it every step is launched eagerly."""
         global TIMER
         accum_grad = options.accum_grad
+        if step_runner is not None and step_runner.accum_grad != accum_grad:
+            raise ValueError(f"step_runner.accum_grad={step_runner.accum_grad} != options.accum_grad={accum_grad}")
         distributed = distributed_option is not None and distributed_option.distributed
         log_interval = options.log_interval
         if log_interval is None:
@@ -191,7 +193,10 @@ class Trainer:
         # applied updates are counted on the device (a non-finite grad norm skips the update
         # there); read once at the end of the epoch for all_steps_are_invalid (trainer.py:681)
         applied0 = optimizer.state_dev[0].clone()
-        stop = torch.zeros((), dtype=torch.long)  # host flag over the gloo control group
+        # the reference's per-step iterator_stop all-reduce (trainer.py:507-518) over the gloo
+        # control group; its message also carries "a capture failed on some rank" so every rank
+        # turns eager at the same step (graph.CapturedTrainStep decides captures per rank)
+        ctl = torch.zeros(2, dtype=torch.long)
         ctrl = getattr(distributed_option, "control_group", None)
         ran_no_forward = False
         unread = 0
@@ -201,9 +206,13 @@ class Trainer:
             for iiter, (utt_id, batch) in enumerate(reporter.measure_iter_time(iterator, "iter_time"), 1):
                 assert isinstance(batch, dict), type(batch)
                 if distributed:
-                    dist.all_reduce(stop, group=ctrl)
-                    if stop.item() > 0:
+                    ctl[0] = 0
+                    ctl[1] = step_runner.capture_failed_flag() if step_runner is not None else 0
+                    dist.all_reduce(ctl, group=ctrl)
+                    if int(ctl[0]) > 0:
                         break
+                    if int(ctl[1]) > 0 and step_runner is not None and step_runner.mode != "eager":
+                        step_runner.force_eager()
                 if options.no_forward_run:
                     ran_no_forward = True
                     continue
@@ -214,8 +223,8 @@ class Trainer:
                 batch = {k: v.to(device, non_blocking=True) if isinstance(v, torch.Tensor) else v
                          for k, v in batch.items()}
                 update = iiter % accum_grad == 0
-                if step_runner is not None and accum_grad == 1:
-                    loss, stats, weight, gn = step_runner(batch, maxlens, lens_host=lens_host)
+                if step_runner is not None:
+                    loss, stats, weight, gn = step_runner(batch, maxlens, lens_host=lens_host, iiter=iiter)
                 else:
                     loss, stats, weight, gn = cls.train_one_step(model, batch, optimizer, scheduler,
                                                                  grad_clip=options.grad_clip, accum_grad=accum_grad,
@@ -245,8 +254,11 @@ class Trainer:
                     unread = 0
             else:
                 if distributed:
-                    stop.fill_(1)
-                    dist.all_reduce(stop, group=ctrl)
+                    ctl[0] = 1
+                    ctl[1] = step_runner.capture_failed_flag() if step_runner is not None else 0
+                    dist.all_reduce(ctl, group=ctrl)
+                    if int(ctl[1]) > 0 and step_runner is not None and step_runner.mode != "eager":
+                        step_runner.force_eager()
         finally:
             TIMER = None
         applied = int((optimizer.state_dev[0] - applied0).item())
@@ -328,11 +340,11 @@ class Trainer:
         if start_epoch == opts.max_epoch + 1:
             logging.warning(f"The training has already reached at max_epoch: {start_epoch}")
         dp = ArenaDataParallel(model) if distributed else None
-        runner = None
-        if opts.accum_grad == 1:
-            runner = CapturedTrainStep(model, optimizers[0], schedulers[0] if schedulers else None,
-                                       grad_clip=opts.grad_clip, dp=dp, warmup=2,
-                                       control_group=getattr(distributed_option, "control_group", None))
+        # steps whose shapes repeat are captured and replayed; with accum_grad > 1 the micro-step
+        # and the updating micro-step are two graphs per shape
+        runner = CapturedTrainStep(model, optimizers[0], schedulers[0] if schedulers else None,
+                                   grad_clip=opts.grad_clip, dp=dp, warmup=2, accum_grad=opts.accum_grad,
+                                   control_group=getattr(distributed_option, "control_group", None))
         all_invalid = False
         for iepoch in range(start_epoch, opts.max_epoch + 1):
             logging.info(f"{iepoch}/{opts.max_epoch}epoch started")

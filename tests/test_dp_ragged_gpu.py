@@ -1,0 +1,184 @@
+"""Captured data-parallel steps when the ranks hold differently padded shards.
+
+The reference pads each rank's batch[rank::world] to that rank's own maxima
+(espnet2/tasks/abs_task.py:1566-1575) and runs the per-step iterator_stop all-reduce
+(espnet2/train/trainer.py:505-518), so under bucketing the ranks' graph keys
+(B, T_max, F, L_max) differ and each rank reaches its capture at a different step.
+graph.CapturedTrainStep therefore decides captures per rank and issues no collective of its
+own; a failed capture travels in the control all-reduce's message so every rank turns eager
+at the same step.
+
+Two gloo ranks share cuda:0 (RCCL needs one GPU per rank), so the captured graph is the
+runner's test double (pseudo_capture: the capture bookkeeping, per-rank keys, warm-up counts
+and failure path of the real runner, each "replay" running the eager step): the check is the
+protocol — the same collectives in the same order and sizes on both ranks, no desync over two
+epochs of Trainer.train_one_epoch, captures at different steps on the two ranks — and
+parameters equal to eager DP.  The real capture WITH RCCL collectives is
+tests/test_dp_capture_gpu.py (world-1 group).
+"""
+import os
+import tempfile
+
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+pytestmark = pytest.mark.gpu
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+def _paths():
+    import sys
+    for p in (HERE, os.path.dirname(HERE), os.path.join(os.path.dirname(HERE), "espnet-1_amd")):
+        if p not in sys.path:
+            sys.path.insert(0, p)
+
+
+def _global_batches(n, seed=11):
+    """n bucketed global batches of 4 utterances with distinct lengths; rank r takes
+    utterances r::2 and trims the padding to its own maxima (the reference's collate)."""
+    g = torch.Generator().manual_seed(seed)
+    out = []
+    for i in range(n):
+        lens = [[121, 104, 88, 71], [118, 96, 110, 77]][i % 2]
+        tl = [[9, 6, 4, 7], [10, 5, 8, 3]][i % 2]
+        T, L = max(lens), max(tl)
+        speech = torch.randn(4, T, 80, generator=g)
+        text = torch.full((4, L), -1, dtype=torch.long)
+        for u in range(4):
+            text[u, :tl[u]] = torch.randint(2, 48, (tl[u],), generator=g)
+        out.append(dict(speech=speech, speech_lengths=torch.tensor(lens), text=text,
+                        text_lengths=torch.tensor(tl)))
+    return out
+
+
+def _shard(b, rank, world):
+    s = {k: v[rank::world] for k, v in b.items()}
+    T, L = int(s["speech_lengths"].max()), int(s["text_lengths"].max())
+    return dict(speech=s["speech"][:, :T].contiguous(), speech_lengths=s["speech_lengths"],
+                text=s["text"][:, :L].contiguous(), text_lengths=s["text_lengths"])
+
+
+def _opts():
+    from espnet_amd.train.trainer import TrainerOptions
+    return TrainerOptions(ngpu=1, resume=False, use_amp=True, train_dtype="float32", grad_noise=False,
+                          accum_grad=1, grad_clip=5.0, grad_clip_type=2.0, log_interval=None,
+                          no_forward_run=False, use_matplotlib=False, use_tensorboard=False, use_wandb=False,
+                          output_dir="/tmp", max_epoch=2, seed=0, sharded_ddp=False, patience=None,
+                          keep_nbest_models=[1], nbest_averaging_interval=0,
+                          early_stopping_criterion=("valid", "loss", "min"),
+                          best_model_criterion=[("train", "loss", "min")], val_scheduler_criterion=("valid", "loss"),
+                          unused_parameters=False, wandb_model_log_interval=-1, create_graph_in_tensorboard=False)
+
+
+def _worker(rank, world, init, q, mode):
+    _paths()
+    import torch.distributed as dist
+    from test_dp_capture_gpu import _setup
+    from espnet_amd.train.distributed import ArenaDataParallel
+    from espnet_amd.train.distributed_utils import DistributedOption
+    from espnet_amd.train.graph import CapturedTrainStep
+    from espnet_amd.train.reporter import Reporter
+    from espnet_amd.train.trainer import Trainer
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", init_method=f"file://{init}", rank=rank, world_size=world)
+    try:
+        # every collective of the run, in order: (op, group tag, numel)
+        log = []
+        real_ar, real_bc = dist.all_reduce, dist.broadcast
+
+        def tag(group):
+            return "world" if group is None else "other"
+
+        def ar(t, *a, group=None, **k):
+            log.append(("all_reduce", tag(group), t.numel()))
+            return real_ar(t, *a, group=group, **k)
+
+        def bc(t, src, *a, group=None, **k):
+            log.append(("broadcast", tag(group), t.numel()))
+            return real_bc(t, src, *a, group=group, **k)
+        dist.all_reduce, dist.broadcast = ar, bc
+        import espnet_amd.train.distributed as dmod
+        import espnet_amd.train.trainer as tmod
+        dmod.dist.all_reduce, dmod.dist.broadcast = ar, bc
+        tmod.dist.all_reduce = ar
+
+        _, m, opt, sched = _setup(amp=True, dropout=0.1)
+        dp = ArenaDataParallel(m, bucket_mb=0.25)
+        dopt = DistributedOption(distributed=True, dist_backend="gloo", dist_rank=rank, dist_world_size=world)
+        runner = None
+        if mode != "eager":
+            runner = CapturedTrainStep(m, opt, sched, grad_clip=5.0, dp=dp, warmup=1, pseudo_capture=True)
+            if mode == "fail":  # rank 1's capture of its second key raises: every rank turns eager
+                if rank == 1:
+                    b = _shard(_global_batches(2)[1], 1, world)
+                    runner._fail_keys.add((b["speech"].shape[0], int(b["speech_lengths"].max()),
+                                           b["speech"].shape[2], int(b["text_lengths"].max())))
+        glob = _global_batches(6)
+        # rank 0 always sees one key; rank 1 alternates two keys: rank 0 captures at its 2nd
+        # step, rank 1 at its 3rd and 4th
+        if rank == 0:
+            shards = [_shard(glob[0], 0, world)] * 6
+        else:
+            shards = [_shard(glob[i % 2], 1, world) for i in range(6)]
+        # rank 0 runs one step fewer in epoch 2: the iterator_stop all-reduce stops rank 1 too
+        rep = Reporter()
+        modes = []
+        for ep in (1, 2):
+            rep.set_epoch(ep)
+            items = [(["u"], b) for b in shards[: (5 if (ep == 2 and rank == 0) else 6)]]
+            with rep.observe("train") as sub:
+                Trainer.train_one_epoch(m, iter(items), [opt], [sched], reporter=sub, options=_opts(),
+                                        distributed_option=dopt, dp=dp, step_runner=runner)
+            modes.append(None if runner is None else runner.mode)
+        torch.cuda.synchronize()
+        q.put(dict(rank=rank, log=log, w=m.arena.data.cpu().clone(), modes=modes,
+                   captures=[] if runner is None else [c for c, _ in runner.captures],
+                   failed=None if runner is None else runner.failed))
+    except Exception:
+        import traceback
+        q.put(dict(rank=rank, error=traceback.format_exc()))
+        raise
+    finally:
+        dist.destroy_process_group()
+
+
+def _run(mode):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    init = tempfile.mktemp(prefix=f"ea_rag_{mode}_")
+    ps = [ctx.Process(target=_worker, args=(r, 2, init, q, mode)) for r in range(2)]
+    for p in ps:
+        p.start()
+    res = [q.get(timeout=150) for _ in range(2)]
+    for p in ps:
+        p.join(60)
+    for r in res:
+        assert "error" not in r, r["error"]
+    return sorted(res, key=lambda r: r["rank"])
+
+
+def test_ragged_shards_captured_protocol_matches_eager_dp():
+    eager = _run("eager")
+    cap = _run("capture")
+    # the same collectives, in the same order and sizes, on both ranks
+    assert cap[0]["log"] == cap[1]["log"]
+    assert eager[0]["log"] == eager[1]["log"]
+    assert cap[0]["log"] == eager[0]["log"]
+    # ranks captured at different steps (different shape keys), and both replay
+    assert cap[0]["captures"] == [2]
+    assert cap[1]["captures"] == [3, 4]
+    assert cap[0]["modes"] == ["graph", "graph"] and cap[1]["modes"] == ["graph", "graph"]
+    # parameters: identical on both ranks and to eager DP
+    assert torch.equal(cap[0]["w"], cap[1]["w"])
+    assert torch.equal(cap[0]["w"], eager[0]["w"])
+
+
+def test_ragged_shards_failed_capture_turns_every_rank_eager():
+    eager = _run("eager")
+    fail = _run("fail")
+    assert fail[0]["log"] == fail[1]["log"] == eager[0]["log"]
+    assert fail[1]["failed"] and not fail[0]["failed"]
+    assert fail[0]["modes"][-1] == "eager" and fail[1]["modes"][-1] == "eager"
+    assert torch.equal(fail[0]["w"], eager[0]["w"]) and torch.equal(fail[1]["w"], eager[0]["w"])

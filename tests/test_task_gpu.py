@@ -23,7 +23,11 @@ from goldens import load, section
 pytestmark = pytest.mark.gpu
 
 
-def test_train_one_epoch_accum_grad_matches_reference():
+@pytest.mark.parametrize("captured", [False, True])
+def test_train_one_epoch_accum_grad_matches_reference(captured):
+    """accum_grad=2 epoch against the reference's own epoch golden; captured=True runs it through
+    graph.CapturedTrainStep (warm-up 1): the micro-step graph is captured at batch 3 and the
+    updating micro-step's graph at batch 4 (two graphs per shape, trainer.py:619-653)."""
     from test_model_build import build
     from espnet_amd.optim.adam import ArenaAdam
     from espnet_amd.schedulers.warmup_lr import WarmupLR
@@ -50,10 +54,18 @@ def test_train_one_epoch_accum_grad_matches_reference():
                           early_stopping_criterion=("valid", "loss", "min"),
                           best_model_criterion=[("train", "loss", "min")], val_scheduler_criterion=("valid", "loss"),
                           unused_parameters=False, wandb_model_log_interval=-1, create_graph_in_tensorboard=False)
+    runner = None
+    if captured:
+        from espnet_amd.train.graph import CapturedTrainStep
+        runner = CapturedTrainStep(m, opt, sched, grad_clip=meta["grad_clip"], warmup=1,
+                                   accum_grad=meta["accum_grad"])
     rep = Reporter()
     rep.set_epoch(1)
     with rep.observe("train") as sub:
-        invalid = Trainer.train_one_epoch(m, iter(batches), [opt], [sched], reporter=sub, options=opts)
+        invalid = Trainer.train_one_epoch(m, iter(batches), [opt], [sched], reporter=sub, options=opts,
+                                          step_runner=runner)
+    if captured:
+        assert runner.mode == "graph" and [c for c, _ in runner.captures] == [3, 4], runner.captures
     torch.cuda.synchronize()
     assert invalid == bool(d["all_invalid"])
     st = rep.stats[1]["train"]
