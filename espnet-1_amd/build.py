@@ -37,46 +37,50 @@ def _stale(out, deps):
     return any(os.path.getmtime(d) > t for d in deps)
 
 
-def _compile(src, force):
-    obj = os.path.join(OBJ, os.path.basename(src) + ".o")
+def _compile(src, force, obj_dir=OBJ, extra=()):
+    obj = os.path.join(obj_dir, os.path.basename(src) + ".o")
     if not force and not _stale(obj, _deps(src)):
         return obj, None
-    cmd = [HIPCC, *CFLAGS, "-c", src, "-o", obj]
+    cmd = [HIPCC, *CFLAGS, *extra, "-c", src, "-o", obj]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         return obj, f"{' '.join(cmd)}\n{r.stdout}\n{r.stderr}"
     return obj, None
 
 
-def build(jobs: int = 8, force: bool = False, verbose: bool = True) -> str:
-    os.makedirs(OBJ, exist_ok=True)
-    os.makedirs(os.path.dirname(LIB), exist_ok=True)
+def build(jobs: int = 8, force: bool = False, verbose: bool = True, tag: str = "", extra=()) -> str:
+    """tag / extra: an A/B variant built with extra hipcc flags into its own object directory,
+    linked as libespnet_amd_<tag>.so (load it with EA_LIB_NAME)."""
+    obj_dir = OBJ + (f"_{tag}" if tag else "")
+    lib = LIB if not tag else LIB.replace(".so", f"_{tag}.so")
+    os.makedirs(obj_dir, exist_ok=True)
+    os.makedirs(os.path.dirname(lib), exist_ok=True)
     srcs = sorted(glob.glob(os.path.join(CSRC, "*.hip")))
     with cf.ThreadPoolExecutor(max_workers=jobs) as ex:
-        results = list(ex.map(lambda s: _compile(s, force), srcs))
+        results = list(ex.map(lambda s: _compile(s, force, obj_dir, extra), srcs))
     errs = [e for _, e in results if e]
     if errs:
         raise RuntimeError("HIP compile failed:\n" + "\n".join(errs))
     objs = [o for o, _ in results]
-    if force or _stale(LIB, objs):
-        # hipBLASLt (plain bf16 GEMMs, csrc/blaslt.hip); in a torch process the loader binds the
-        # libhipblaslt.so.1 torch already loaded
-        cmd = [HIPCC, "-shared", f"--offload-arch={ARCH}", "-o", LIB, *objs, "-L/opt/rocm/lib", "-lhipblaslt"]
+    if force or _stale(lib, objs):
+        cmd = [HIPCC, "-shared", f"--offload-arch={ARCH}", "-o", lib, *objs]
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError(f"link failed:\n{r.stdout}\n{r.stderr}")
         if verbose:
-            print(f"[espnet_amd] linked {LIB} ({len(objs)} objects)")
-    return LIB
+            print(f"[espnet_amd] linked {lib} ({len(objs)} objects)")
+    return lib
 
 
 if __name__ == "__main__":
     ap = argparse.ArgumentParser()
     ap.add_argument("-j", type=int, default=min(8, os.cpu_count() or 8))
     ap.add_argument("--force", action="store_true")
+    ap.add_argument("--tag", default="", help="A/B variant: libespnet_amd_<tag>.so")
+    ap.add_argument("--extra", default="", help="extra hipcc flags for the variant (space separated)")
     a = ap.parse_args()
     try:
-        build(a.j, a.force)
+        build(a.j, a.force, tag=a.tag, extra=a.extra.split())
     except RuntimeError as e:
         print(e, file=sys.stderr)
         sys.exit(1)

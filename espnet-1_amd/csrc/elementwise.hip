@@ -1357,23 +1357,6 @@ extern "C" int ea_dwconv_glu_bwd(int B, int T, int C, int K, const float* x, con
   return ea_reduce_partials(nblkr, C, workspace + (long)C * K, rowlen, dbias, accumulate_params, stream);
 }
 
-extern "C" int ea_dwconv_bwd_partials(int B, int T, int C, int K, const float* x, const float* w, const float* dy,
-                                      float* dx, float* part, long part_elems, int* nparts, void* stream) {
-  EA_ENTRY();
-  EA_CHECK_ARG((K == 3 || K == 5 || K == 7 || K == 15 || K == 31) && part && nparts);
-  const int nblkr = B * ea_cdiv(T, 4 * DW_R);
-  EA_CHECK_ARG((long)nblkr * C * (K + 1) <= part_elems);
-  dim3 gridr(nblkr, ea_cdiv(C, DW_CT));
-  hipStream_t st = (hipStream_t)stream;
-  switch (K) {
-#define EA_DWB(KK) case KK: hipLaunchKernelGGL((dwconv_bwd_k_kernel<KK, DW_R, true>), gridr, dim3(256), 0, st, B, T, C, x, w, dy, dx, part); break;
-    EA_DWB(3) EA_DWB(5) EA_DWB(7) EA_DWB(15) EA_DWB(31)
-#undef EA_DWB
-  }
-  EA_LAUNCH_CHECK();
-  *nparts = nblkr;
-  return 0;
-}
 
 extern "C" int ea_add_pos_bias(long N, int H, int dk, const void* q, long ldq, const float* u, const float* v,
                                void* qu, void* qv, int dtype, void* stream) {
@@ -1449,8 +1432,7 @@ extern "C" int ea_conv1_fwd2(int B, int T, int F, int C, const float* x, const f
   const int T1 = (T - 3) / 2 + 1, F1 = (F - 3) / 2 + 1;
   const PhaseGeo g = phase_geo(B, T1, F1, C);
   const long npix = (long)B * T1 * F1;
-  static const bool pix_kernel = std::getenv("EA_CONV1_FWD_PIX") != nullptr;  // A/B switch
-  if ((C == 512 || C == 1024 || C == 2048) && (long)B * T1 < (1L << 31) && !pix_kernel) {
+  if ((C == 512 || C == 1024 || C == 2048) && (long)B * T1 < (1L << 31)) {
     // one resident wave of blocks: each loads its 80 weights per lane once and walks rows
     static int resident = 0;
     if (!resident) {

@@ -6,11 +6,6 @@
 #include <cstdio>
 #include <cstdlib>
 
-namespace eag {
-int g_pipe_slots = [] { const char* e = std::getenv("EA_PIPE_SLOTS"); return e ? std::atoi(e) : 4; }();
-int g_pipe128_slots = [] { const char* e = std::getenv("EA_PIPE128_SLOTS"); return e ? std::atoi(e) : 4; }();
-}  // namespace eag
-
 namespace {
 // split-K combine: C = epi(sum_s slab[s]) (any epilogue kind), 4 columns per thread
 __global__ void splitk_reduce(GemmP p) {
@@ -61,27 +56,22 @@ int g_gemm_bm64 = 1;
 int g_gemm_bm32 = [] { const char* e = std::getenv("EA_GEMM_BM32"); return e ? std::atoi(e) : 1; }();
 int g_gemm_pipe = 0;  // ea_gemm_set_pipe bits: 1 = 256x256 tiles on gemm_pipe, 2 = 128x128 tiles too
 
-int g_gemm_k128 = [] { const char* e = std::getenv("EA_GEMM_K128"); return e ? std::atoi(e) : 0; }();
+// gemm_k128 for the N = 512 grids at K >= 1,024 (mode 1, default): 7968x512x2048 23.0 vs 26.3 us
+// on the 64x128 tile (RESID epilogue 28.5 vs 31.0), C3 step 1813-1827 vs 1795-1796 utt/s on one
+// box (gpurun_out/r5b); at K = 512 the 64x128 tile stays (15.0 vs 15.8 us)
+int g_gemm_k128 = [] { const char* e = std::getenv("EA_GEMM_K128"); return e ? std::atoi(e) : 1; }();
 // few-row GEMMs (M <= g_gemm_skinny) on gemm_skinny (ea_gemm_set_skinny; 0 = off)
 int g_gemm_skinny = [] { const char* e = std::getenv("EA_GEMM_SKINNY"); return e ? std::atoi(e) : 16; }();
-// ... and the 32-row variant for M up to g_gemm_rows32 (ea_gemm_set_rows32; 0 = off)
-int g_gemm_rows32 = [] { const char* e = std::getenv("EA_GEMM_ROWS32"); return e ? std::atoi(e) : 0; }();
 
-// 256x256 K-major tiles on gemm_quad (4 waves of 128x128; ea_gemm_set_quad / EA_GEMM_QUAD; 0 = off)
-int g_gemm_quad = [] { const char* e = std::getenv("EA_GEMM_QUAD"); return e ? std::atoi(e) : 0; }();
-
-int launch_lds(GemmP& p, int a_k, int b_k, int nz, hipStream_t st, bool pipe128 = false, bool k128 = false) {
+int launch_lds(GemmP& p, int a_k, int b_k, int nz, hipStream_t st, bool k128 = false) {
   dim3 grid(p.tiles_m * p.tiles_n, 1, nz * p.splitk);
   if (k128) return launch_k128(p, grid, st);
-  if (g_gemm_quad && p.g.mode == 0 && p.bm == 256 && p.bn == 256 && a_k && (b_k || (g_gemm_quad & 2)) &&
-      p.K % 64 == 0 && p.kchunk % 64 == 0)
-    return launch_quad(p, b_k, grid, st);
   if (p.g.mode != 0) {  // implicit-GEMM conv2 modes: fixed layouts, 128x128 or 256x256 tiles
     if (p.bm == 256 && g_gemm_pipe) return launch_pipe_conv(p, grid, st);
     return launch_lds_conv(p, grid, st);
   }
   if ((p.bm == 256 && p.bn == 256 && (g_gemm_pipe & 1)) ||
-      (p.bm == 128 && p.bn == 128 && ((g_gemm_pipe & 2) || pipe128)))
+      (p.bm == 128 && p.bn == 128 && (g_gemm_pipe & 2)))
     return launch_pipe(p, a_k, b_k, grid, st);
   return launch_lds_dense(p, a_k, b_k, grid, st);
 }
@@ -114,8 +104,8 @@ void choose_tile(GemmP& p, int a_k, long nz) {
 }
 
 template <typename T>
-int launch(GemmP& p, int a_k, int b_k, int nz, hipStream_t st, bool pipe128 = false, bool k128 = false) {
-  if (sizeof(T) == 2 && p.lds) return launch_lds(p, a_k, b_k, nz, st, pipe128, k128);
+int launch(GemmP& p, int a_k, int b_k, int nz, hipStream_t st, bool k128 = false) {
+  if (sizeof(T) == 2 && p.lds) return launch_lds(p, a_k, b_k, nz, st, k128);
   if (p.bm != 128 || p.bn != 128) return EA_ERR_BAD_ARG;
   dim3 grid(p.tiles_m * p.tiles_n, 1, nz * p.splitk);
 #define EA_GEMM_CASE(AKV, BKV)                                                      \
@@ -228,7 +218,7 @@ extern "C" int ea_gemm_set_pipe(int on) {
 
 extern "C" int ea_gemm_set_k128(int mode, int slots) {
   EA_ENTRY();
-  EA_CHECK_ARG(mode >= 0 && mode <= 3 && (slots == 3 || slots == 4 || slots == 5));
+  EA_CHECK_ARG(mode >= 0 && mode <= 3 && (slots == 3 || slots == 4));
   g_gemm_k128 = mode;
   eag::g_k128_slots = slots;
   return 0;
@@ -241,28 +231,6 @@ extern "C" int ea_gemm_set_skinny(int max_m) {
   return 0;
 }
 
-extern "C" int ea_gemm_set_quad(int on, int slots) {
-  EA_ENTRY();
-  EA_CHECK_ARG(slots == 4 || slots == 5);
-  g_gemm_quad = on;
-  eag::g_quad_slots = slots;
-  return 0;
-}
-
-extern "C" int ea_gemm_set_rows32(int max_m) {
-  EA_ENTRY();
-  EA_CHECK_ARG(max_m >= 0);
-  g_gemm_rows32 = max_m;
-  return 0;
-}
-
-extern "C" int ea_gemm_set_pipe128_slots(int slots) {
-  EA_ENTRY();
-  EA_CHECK_ARG(slots == 4 || slots == 6 || slots == 8);
-  eag::g_pipe128_slots = slots;
-  return 0;
-}
-
 extern "C" int ea_gemm_set_tile(int bm, int bn) {
   EA_ENTRY();
   EA_CHECK_ARG((bm == 0 && bn == 0) || (bm == 32 && bn == 128) || (bm == 64 && bn == 128) ||
@@ -271,9 +239,6 @@ extern "C" int ea_gemm_set_tile(int bm, int bn) {
   g_force_bn = bn;
   return 0;
 }
-
-int ea_blaslt_try(int a_kmajor, int b_kmajor, int M, int N, int K, const void* A, long lda, const void* B, long ldb,
-                  void* C, int c_dtype, long ldc, float alpha, float beta, hipStream_t st);  // blaslt.hip
 
 static int gemm_impl(int dtype, int a_kmajor, int b_kmajor, int M, int N, int K,
                      const void* A, long lda, long sAb, long sAh,
@@ -321,25 +286,18 @@ static int gemm_impl(int dtype, int a_kmajor, int b_kmajor, int M, int N, int K,
   p.bm = 128; p.bn = 128;
   // few rows (decoder steps): K split over the waves of a 16 x 32 block instead of a tile
   // walking all of K (gemm_skinny.hip)
-  if (dtype == EA_BF16 && (M <= g_gemm_skinny || M <= g_gemm_rows32) && a_kmajor && b_kmajor && !geo && !w1part &&
+  if (dtype == EA_BF16 && M <= g_gemm_skinny && a_kmajor && b_kmajor && !geo && !w1part &&
       batch * nh == 1 && K % 32 == 0 && K > 0 && p.vec_a && p.vec_b) {
     static const bool trace_s = std::getenv("EA_GEMM_TRACE") != nullptr;
     if (trace_s) std::fprintf(stderr, "[ea_gemm] M=%d N=%d K=%d skinny epi=%d\n", M, N, K, (int)epi->kind);
-    return launch_skinny(p, (hipStream_t)stream, M > g_gemm_skinny);
+    return launch_skinny(p, (hipStream_t)stream);
   }
-  // plain products (no bias / scale / dropout / activation) on hipBLASLt where enabled
-  if (dtype == EA_BF16 && !geo && !w1part && batch * nh == 1 && epi->kind == EA_EPI_STORE && !epi->bias &&
-      epi->post_scale == 1.f && epi->drop_p <= 0.f &&
-      ea_blaslt_try(a_kmajor, b_kmajor, M, N, K, A, lda, B, ldb, C, c_dtype, ldc, epi->alpha, epi->beta,
-                    (hipStream_t)stream) == 0)
-    return 0;
   // operand extent per batch slice (bytes) must fit the kernel's 32-bit source offsets
   const double a_ext = 2.0 * ((a_kmajor ? (double)M : (double)K) * lda);
   const double b_ext = 2.0 * ((b_kmajor ? (double)N : (double)K) * ldb);
   const bool lds_path = dtype == EA_BF16 && p.vec_a && p.vec_b && g_gemm_stages > 0 &&
                         a_ext < 4.0e9 && b_ext < 4.0e9;
   p.lds = lds_path;
-  bool pipe128 = false;
   if (geo && geo->mode != 0) {
     // gather modes: LDS-DMA path only, K a whole number of 64-deep tiles within taps
     if (!lds_path || K % 64 != 0 || geo->C % 64 != 0 || batch * nh != 1) return EA_ERR_BAD_ARG;
@@ -356,28 +314,17 @@ static int gemm_impl(int dtype, int a_kmajor, int b_kmajor, int M, int N, int K,
     if (p.bm != 256 || p.bn != 256) { p.bm = 128; p.bn = 128; }
   } else if (lds_path) {
     choose_tile(p, a_kmajor, (long)batch * nh);
-    // One-round 256x256 grids serialise each CU's main loop and its epilogue; 128x128
-    // tiles two per CU let one block's epilogue stores overlap the other's main loop.
-    // EA_EPI128 bits: 1 = switch such grids when the epilogue stores an activation pair
-    // (ACT / DACT), 2 = on the ping-pong kernel, 4 = whatever the epilogue.
-    static const int epi128 = [] { const char* e = std::getenv("EA_EPI128"); return e ? std::atoi(e) : 0; }();
-    if ((epi128 & 1) && !g_force_bm && p.bm == 256 && p.bn == 256 &&
-        ((epi128 & 4) || epi->kind == EA_EPI_ACT || epi->kind == EA_EPI_DACT) &&
-        (long)ea_cdiv(M, 256) * ea_cdiv(N, 256) * batch * nh <= 256) {
-      p.bm = 128; p.bn = 128;
-      pipe128 = (epi128 & 2) != 0;
-    }
   }
   // gemm_k128 (ea_gemm_set_k128 / EA_GEMM_K128): both operands K-major, K a whole number of
   // 64-deep tiles, a 64x128 / 128x128 choice whose 128x128 grid about fills the CUs (one tile
-  // per CU: the N = 512 GEMMs at M = 7,968); mode 2: any such grid of >= 128 tiles; mode 3:
-  // every eligible GEMM (tests)
+  // per CU: the N = 512 GEMMs at M = 7,968) and K >= 1,024; mode 2: any such grid of >= 128
+  // tiles, any K; mode 3: every eligible GEMM (tests)
   bool k128 = false;
   if (g_gemm_k128 && lds_path && !geo && a_kmajor && b_kmajor && K % 64 == 0 && K > 0) {
     const long t128 = (long)ea_cdiv(M, 128) * ea_cdiv(N, 128) * batch * nh;
     const bool fits = g_gemm_k128 == 3 ||
                       (!g_force_bm && (p.bm == 64 || p.bm == 128) && p.bn == 128 && t128 >= 128 &&
-                       (g_gemm_k128 == 2 || t128 <= 256));
+                       (g_gemm_k128 == 2 || (t128 <= 256 && K >= 1024)));
     if (fits) { p.bm = 128; p.bn = 128; k128 = true; }
   }
   if (p.bm <= 64 && !a_kmajor) return EA_ERR_BAD_ARG;
@@ -420,7 +367,7 @@ static int gemm_impl(int dtype, int a_kmajor, int b_kmajor, int M, int N, int K,
                  N, K, a_kmajor, b_kmajor, nz, p.bm, p.bn, k128 ? "k" : "", splitk, (int)epi->kind, geo ? geo->mode : 0,
                  (int)p.lds);
   hipStream_t st = (hipStream_t)stream;
-  int rc = dtype == EA_BF16 ? launch<bf16>(p, a_kmajor, b_kmajor, nz, st, pipe128, k128)
+  int rc = dtype == EA_BF16 ? launch<bf16>(p, a_kmajor, b_kmajor, nz, st, k128)
                             : launch<float>(p, a_kmajor, b_kmajor, nz, st);
   if (rc) return rc;
   if (splitk > 1) {

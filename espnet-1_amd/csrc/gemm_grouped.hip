@@ -148,17 +148,10 @@ extern "C" int ea_gemm_grouped(int a_kmajor, int b_kmajor, int n, const ea_group
     }
   }
   const dim3 grid((unsigned)ntiles), block(512);
-  if (eag::g_pipe_slots == 5) {
-    if (a_kmajor && b_kmajor) hipLaunchKernelGGL((gemm_grouped<true, true, 5>), grid, block, 0, st, table, map, (int)ntiles, g_xcd_chunk);
-    else if (a_kmajor) hipLaunchKernelGGL((gemm_grouped<true, false, 5>), grid, block, 0, st, table, map, (int)ntiles, g_xcd_chunk);
-    else if (b_kmajor) hipLaunchKernelGGL((gemm_grouped<false, true, 5>), grid, block, 0, st, table, map, (int)ntiles, g_xcd_chunk);
-    else hipLaunchKernelGGL((gemm_grouped<false, false, 5>), grid, block, 0, st, table, map, (int)ntiles, g_xcd_chunk);
-  } else {
-    if (a_kmajor && b_kmajor) hipLaunchKernelGGL((gemm_grouped<true, true>), grid, block, 0, st, table, map, (int)ntiles, g_xcd_chunk);
-    else if (a_kmajor) hipLaunchKernelGGL((gemm_grouped<true, false>), grid, block, 0, st, table, map, (int)ntiles, g_xcd_chunk);
-    else if (b_kmajor) hipLaunchKernelGGL((gemm_grouped<false, true>), grid, block, 0, st, table, map, (int)ntiles, g_xcd_chunk);
-    else hipLaunchKernelGGL((gemm_grouped<false, false>), grid, block, 0, st, table, map, (int)ntiles, g_xcd_chunk);
-  }
+  if (a_kmajor && b_kmajor) hipLaunchKernelGGL((gemm_grouped<true, true>), grid, block, 0, st, table, map, (int)ntiles, g_xcd_chunk);
+  else if (a_kmajor) hipLaunchKernelGGL((gemm_grouped<true, false>), grid, block, 0, st, table, map, (int)ntiles, g_xcd_chunk);
+  else if (b_kmajor) hipLaunchKernelGGL((gemm_grouped<false, true>), grid, block, 0, st, table, map, (int)ntiles, g_xcd_chunk);
+  else hipLaunchKernelGGL((gemm_grouped<false, false>), grid, block, 0, st, table, map, (int)ntiles, g_xcd_chunk);
   EA_LAUNCH_CHECK();
   return 0;
 }

@@ -62,14 +62,9 @@ int launch_k128(GemmP& p, dim3 grid, hipStream_t st);                     // gem
 int launch_pipe_conv(GemmP& p, dim3 grid, hipStream_t st);               // gemm_pipe_conv.hip: conv2 modes
 int launch_lds_dense(GemmP& p, int a_k, int b_k, dim3 grid, hipStream_t st);  // gemm_lds.hip
 int launch_lds_conv(GemmP& p, dim3 grid, hipStream_t st);                     // gemm_lds_conv.hip
-int launch_quad(GemmP& p, int b_k, dim3 grid, hipStream_t st);  // gemm_quad.hip: 256x256, 4 waves of 128x128
-extern int g_quad_slots;
-int launch_skinny(GemmP& p, hipStream_t st, int rows32);  // gemm_skinny.hip: few-row bf16, K split over waves
+int launch_skinny(GemmP& p, hipStream_t st);  // gemm_skinny.hip: few-row bf16, K split over waves
 int launch_skinny_ln(GemmP& p, const float* gamma, const float* beta, float eps, hipStream_t st);  // + LayerNorm
-// ring depth of the 256x256 ping-pong kernel: 4 slots, or 5 (EA_PIPE_SLOTS; gemm.hip)
-extern int g_pipe_slots;
-extern int g_pipe128_slots;  // ring depth of the 128x128 ping-pong tile (4, 6 or 8)
-extern int g_k128_slots;     // ring depth of gemm_k128 (3, 4 or 5)
+extern int g_k128_slots;     // ring depth of gemm_k128 (3 or 4)
 }  // namespace eag
 
 namespace {
@@ -1106,38 +1101,43 @@ __global__ __launch_bounds__(128 * WN, 1) void gemm_bf16_lds(GemmP p) {
   probe_end(p);
 }
 
-// ---------------------------------------------------------------- 128x128, K-major, deep ring
-// gemm_k128: the narrow-N GEMMs of the step (M = 7,968 tokens, N = 512: forward projections and
-// the input gradients over the transposed weight shadow — both operands K-major) as ONE
-// 128 x 128 tile per CU (252 blocks: the fewest operand bytes per CU for this output size,
-// 1 MiB at K = 2,048 against 1.5 MiB for two 64 x 128 tiles).  4 waves of 64 x 64; 64-deep
-// K-tiles through an S-slot LDS ring filled by LDS-DMA S-1 tiles ahead (counted vmcnt, one
-// barrier per K-tile).  The fragments of the NEXT k-step are read while the current k-step's
-// 16 MFMAs run — across the K-tile boundary too (tile t+1's first k-step is read right after
-// the barrier that publishes it) — so no MFMA waits on an LDS read it just issued.  Fragment
-// reads are inline asm with counted lgkmcnt (hipcc would put a vmcnt(0) in front of an LDS
-// read it can see while an LDS-DMA is in flight).  Same image format, DMA sources, tile
-// mapping and epilogue as gemm_bf16_lds<128, 128>; the host guarantees K % 64 == 0 per split.
-EA_DEV bf16x8 ds_read_b128_asm(const char* p) {
+// ---------------------------------------------------------------- 128x128, K-major, K-split wave groups
+// gemm_k128: the narrow-N GEMMs of the step (M = 7,968 tokens, N = 512: the Linear input
+// gradients over the transposed weight shadow and the forward projections — both operands
+// K-major) as ONE 128 x 128 tile per CU (252 blocks: the fewest operand bytes per CU for this
+// output size, 1 MiB at K = 2,048 against 1.5 MiB for two 64 x 128 tiles).  Eight waves in two
+// K groups: every wave owns a 64 x 64 quarter of the tile, and group g = w / 4 multiplies only
+// the g-th 32-deep half of each 64-deep K-tile, so every SIMD holds one wave of each group and
+// one wave's LDS reads and waits overlap the other's MFMAs (the one-wave-per-SIMD form of this
+// tile left every barrier and read latency exposed).  The two groups' partial sums are added
+// through LDS before the epilogue.  K-tiles stream through an S-slot LDS ring filled S-1 tiles
+// ahead by buffer_load ... lds (per-lane 32-bit source offsets fixed for the whole loop, the
+// K-tile advance in the scalar offset: no address arithmetic per load); one barrier per
+// K-tile, counted vmcnt, fragment reads as inline asm with immediate offsets (hipcc would put
+// a vmcnt(0) in front of an LDS read it can see while an LDS-DMA is in flight).  Image format,
+// tile mapping and epilogue as gemm_bf16_lds<128, 128>; the host guarantees K % 64 == 0 per
+// split and operands < 4 GB.
+template <int OFF>
+EA_DEV bf16x8 ds_read_b128_at(uint32_t addr) {
   bf16x8 v;
-  const uint32_t a = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) char*)p;
-  asm volatile("ds_read_b128 %0, %1" : "=v"(v) : "v"(a) : "memory");
+  asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(v) : "v"(addr), "i"(OFF) : "memory");
   return v;
 }
 
 template <int S>
-__global__ __launch_bounds__(256, 1) void gemm_k128(GemmP p) {
-  constexpr int BM = 128, BN = 128, BK = 64, NTT = 256, NW = 4, MI = 4, NJ = 4;
-  constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2, STAGE = A_BYTES + B_BYTES;
-  constexpr int ACH = A_BYTES / (NTT * 16), BCH = B_BYTES / (NTT * 16), G = ACH + BCH;
-  constexpr int EPI_BYTES = NW * 4 * 16 * EPI_LDT * 4;
-  constexpr int SMEM = S * STAGE > EPI_BYTES ? S * STAGE : EPI_BYTES;
-  static_assert(S >= 3 && S <= 5, "ring depth");
+__global__ __launch_bounds__(512, 1) void gemm_k128(GemmP p) {
+  constexpr int BK = 64, NTT = 512, NW = 8, MI = 4, NJ = 4;
+  constexpr int A_BYTES = 128 * BK * 2, B_BYTES = 128 * BK * 2, STAGE = A_BYTES + B_BYTES;
+  constexpr int ACH = A_BYTES / (NTT * 16), BCH = B_BYTES / (NTT * 16), G = ACH + BCH;  // 2 + 2
+  constexpr int EPI_BYTES = 4 * 4 * 16 * EPI_LDT * 4;  // group 0's four transposition images
+  constexpr int HAND = EPI_BYTES;                      // group 1's partial sums: 4 x 16 KiB
+  constexpr int SMEM = S * STAGE > HAND + 65536 ? S * STAGE : HAND + 65536;
+  static_assert(S >= 3 && S <= 4, "ring depth");
   __shared__ __attribute__((aligned(1024))) char smem[SMEM];
   probe_start(p);
 
   const TileIdx ti = tile_index(p);
-  const int m0 = ti.tm * BM, n0 = ti.tn * BN;
+  const int m0 = ti.tm * 128, n0 = ti.tn * 128;
   const int z = ti.z, sk = ti.sk;
   const int zb = z / p.nh, zh = z % p.nh;
   const bf16* A = (const bf16*)p.A + zb * p.sAb + zh * p.sAh;
@@ -1145,17 +1145,22 @@ __global__ __launch_bounds__(256, 1) void gemm_k128(GemmP p) {
   const int kbeg = sk * p.kchunk;
   const int kend = min(p.K, kbeg + p.kchunk);
   const int nt = max(0, (kend - kbeg) / BK);
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int wm = (w >> 1) * 64, wn = (w & 1) * 64;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int g = w >> 2, q = w & 3;                    // K group, quarter of the tile
+  const int wm = (q >> 1) * 64, wn = (q & 1) * 64;
 
-  // lane-linear DMA: chunk ci = (i*NW + w)*64 + lane lands at ci*16; its source is the
-  // global chunk whose swizzled slot that is (32-bit byte offsets, operands < 4 GB)
+  // buffer descriptors over this split's operand rows; per-lane source offsets (bytes) of the
+  // lane-linear DMA chunks: chunk ci = (i*NW + w)*64 + lane lands at ci*16 and reads the
+  // global chunk whose swizzled slot that is
+  const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(A + kbeg), (short)0, 0x7fffffff, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(B + kbeg), (short)0, 0x7fffffff, 0x00020000);
   auto src = [&](long ld, int mn0, int MN, int ci) -> uint32_t {
     const int row = ci >> 3, c = (ci & 7) ^ swz_k(ci >> 3);
     return (uint32_t)(((long)min(mn0 + row, MN - 1) * ld + c * 8) * 2);
   };
-  const char* abase = (const char*)(A + kbeg);
-  const char* bbase = (const char*)(B + kbeg);
   uint32_t aoff[ACH], boff[BCH];
 #pragma unroll
   for (int i = 0; i < ACH; ++i) aoff[i] = src(p.lda, m0, p.M, (i * NW + w) * 64 + lane);
@@ -1164,33 +1169,35 @@ __global__ __launch_bounds__(256, 1) void gemm_k128(GemmP p) {
 
   auto issue = [&](int t) {
     char* base = smem + (t % S) * STAGE;
-    const char* ak = abase + (long)t * BK * 2;
-    const char* bk = bbase + (long)t * BK * 2;
+    const int so = t * BK * 2;  // K-tile advance (bytes), scalar
 #pragma unroll
     for (int i = 0; i < ACH; ++i)
-      __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)(ak + aoff[i]),
-                                       (__attribute__((address_space(3))) void*)(base + (i * NW + w) * 1024), 16, 0, 0);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(ra, (__attribute__((address_space(3))) void*)(base + (i * NW + w) * 1024),
+                                               16, aoff[i], so, 0, 0);
 #pragma unroll
     for (int i = 0; i < BCH; ++i)
-      __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)(bk + boff[i]),
-                                       (__attribute__((address_space(3))) void*)(base + A_BYTES + (i * NW + w) * 1024),
-                                       16, 0, 0);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(
+          rb, (__attribute__((address_space(3))) void*)(base + A_BYTES + (i * NW + w) * 1024), 16, boff[i], so, 0, 0);
   };
-  // fragments of k-step ks (32 deep) of tile t: 16 rows (lane & 15), k-block 8*(lane>>4)
-  auto rd = [&](int t, int ks, bf16x8 (&fa)[MI], bf16x8 (&fb)[NJ]) {
-    const char* la = smem + (t % S) * STAGE;
-    const char* lb = la + A_BYTES;
-    const int ch = ks * 4 + (lane >> 4);
-#pragma unroll
-    for (int i = 0; i < MI; ++i) {
-      const int row = wm + i * 16 + (lane & 15);
-      fa[i] = ds_read_b128_asm(la + row * 128 + ((ch ^ swz_k(row)) << 4));
-    }
-#pragma unroll
-    for (int j = 0; j < NJ; ++j) {
-      const int row = wn + j * 16 + (lane & 15);
-      fb[j] = ds_read_b128_asm(lb + row * 128 + ((ch ^ swz_k(row)) << 4));
-    }
+
+  // fragment addresses: row r0 + (lane & 15) of a 16-row block starting at a multiple of 16
+  // swizzles by (lane & 15) only, so the blocks of a wave are immediate offsets of one base
+  const int ch = g * 4 + (lane >> 4);
+  const uint32_t lane_off = (uint32_t)((lane & 15) * 128 + ((ch ^ (((lane & 15) >> 1) & 7)) << 4));
+  const uint32_t smem0 = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) char*)smem;
+  const uint32_t a_off = smem0 + lane_off + wm * 128, b_off = smem0 + A_BYTES + lane_off + wn * 128;
+  bf16x8 fa[MI], fb[NJ];
+  auto rd = [&](int t) {
+    const uint32_t sb = (uint32_t)((t % S) * STAGE);
+    const uint32_t pa = a_off + sb, pb = b_off + sb;
+    fa[0] = ds_read_b128_at<0>(pa);
+    fa[1] = ds_read_b128_at<2048>(pa);
+    fa[2] = ds_read_b128_at<4096>(pa);
+    fa[3] = ds_read_b128_at<6144>(pa);
+    fb[0] = ds_read_b128_at<0>(pb);
+    fb[1] = ds_read_b128_at<2048>(pb);
+    fb[2] = ds_read_b128_at<4096>(pb);
+    fb[3] = ds_read_b128_at<6144>(pb);
   };
 
   f32x4 acc[MI][NJ];
@@ -1198,50 +1205,50 @@ __global__ __launch_bounds__(256, 1) void gemm_k128(GemmP p) {
   for (int i = 0; i < MI; ++i)
 #pragma unroll
     for (int j = 0; j < NJ; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
-  auto mma = [&](const bf16x8 (&fa)[MI], const bf16x8 (&fb)[NJ]) {
-    __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int i = 0; i < MI; ++i)
-#pragma unroll
-      for (int j = 0; j < NJ; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
-    __builtin_amdgcn_s_setprio(0);
-  };
 
-  bf16x8 fa0[MI], fb0[NJ], fa1[MI], fb1[NJ];
   if (nt > 0) {
     const int npre = min(S - 1, nt);
     for (int t = 0; t < npre; ++t) issue(t);
-    wait_newer<G, S - 2>(npre - 1);  // own share of tile 0 landed
-    lds_barrier();                   // everyone's
-    rd(0, 0, fa0, fb0);
     for (int t = 0; t < nt; ++t) {
-      rd(t, 1, fa1, fb1);
-      asm volatile("s_waitcnt lgkmcnt(8)" ::: "memory");  // fa0/fb0 (the older 8 reads) are in
+      // own share of tile t landed (tiles issued after it may stay in flight), then everyone's;
+      // every wave is past its reads of tile t-1, whose slot the refill below reuses
+      wait_newer<G, S - 2>(min(S - 2, nt - 1 - t));
+      lds_barrier();
+      if (t + S - 1 < nt) issue(t + S - 1);
+      rd(t);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_sched_barrier(0);
-      mma(fa0, fb0);
-      __builtin_amdgcn_sched_barrier(0);
-      if (t + 1 < nt) {
-        // own share of tile t+1 landed; tiles t+2 .. t+S-2 (issued earlier) may stay in flight
-        wait_newer<G, S - 3>(min(S - 3, nt - 2 - t));
-        lds_barrier();  // everyone's; every wave is past its tile t-1 reads: its slot is free
-        if (t + S - 1 < nt) issue(t + S - 1);
-        rd(t + 1, 0, fa0, fb0);
-        asm volatile("s_waitcnt lgkmcnt(8)" ::: "memory");  // fa1/fb1 in
-      } else {
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      }
-      __builtin_amdgcn_sched_barrier(0);
-      mma(fa1, fb1);
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int i = 0; i < MI; ++i)
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+      __builtin_amdgcn_s_setprio(0);
       __builtin_amdgcn_sched_barrier(0);
     }
   }
   __syncthreads();  // every wave is done reading the ring: the epilogue reuses it
-  const EpiK ek = make_epik(p);
-  switch (p.splitk > 1 ? EA_EPI_STORE : p.epi.kind) {
-    case EA_EPI_STORE: epi_wave<EA_EPI_STORE, MI, NJ>(p, ek, smem, z, zb, zh, m0 + wm, n0 + wn, lane, w, acc, sk); break;
-    case EA_EPI_ACT: epi_wave<EA_EPI_ACT, MI, NJ>(p, ek, smem, z, zb, zh, m0 + wm, n0 + wn, lane, w, acc, sk); break;
-    case EA_EPI_RESID: epi_wave<EA_EPI_RESID, MI, NJ>(p, ek, smem, z, zb, zh, m0 + wm, n0 + wn, lane, w, acc, sk); break;
-    default: epi_wave<EA_EPI_DACT, MI, NJ>(p, ek, smem, z, zb, zh, m0 + wm, n0 + wn, lane, w, acc, sk); break;
+  // group 1 hands its partial sums to group 0 (same quarter, same lane: conflict-free b128)
+  f32x4* hand = (f32x4*)(smem + HAND) + q * (MI * NJ * 64);
+  if (g == 1) {
+#pragma unroll
+    for (int i = 0; i < MI; ++i)
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) hand[(i * NJ + j) * 64 + lane] = acc[i][j];
+  }
+  __syncthreads();
+  if (g == 0) {
+#pragma unroll
+    for (int i = 0; i < MI; ++i)
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) acc[i][j] += hand[(i * NJ + j) * 64 + lane];
+    const EpiK ek = make_epik(p);
+    switch (p.splitk > 1 ? EA_EPI_STORE : p.epi.kind) {
+      case EA_EPI_STORE: epi_wave<EA_EPI_STORE, MI, NJ>(p, ek, smem, z, zb, zh, m0 + wm, n0 + wn, lane, q, acc, sk); break;
+      case EA_EPI_ACT: epi_wave<EA_EPI_ACT, MI, NJ>(p, ek, smem, z, zb, zh, m0 + wm, n0 + wn, lane, q, acc, sk); break;
+      case EA_EPI_RESID: epi_wave<EA_EPI_RESID, MI, NJ>(p, ek, smem, z, zb, zh, m0 + wm, n0 + wn, lane, q, acc, sk); break;
+      default: epi_wave<EA_EPI_DACT, MI, NJ>(p, ek, smem, z, zb, zh, m0 + wm, n0 + wn, lane, q, acc, sk); break;
+    }
   }
   probe_end(p);
 }
@@ -1331,12 +1338,9 @@ struct PipeT {
   static constexpr int SMEM = RING > EPI_BYTES ? RING : EPI_BYTES;
   static constexpr int ACH = A_BYTES / (NTT * 16), BCH = B_BYTES / (NTT * 16);  // DMA per thread
   static constexpr int G = ACH + BCH;
-  // 128x128 with a deep ring (NS > 4): one block per CU whose DMA keeps NS-2 slices (up to
-  // 96 KiB) in flight — the grids where one block per CU is all there is (M = 7,968, N = 512)
-  static constexpr int OCC = BT == 256 ? 1 : (NS <= 4 ? 2 : 1);
+  static constexpr int OCC = BT == 256 ? 1 : 2;
   static_assert(BT == 256 || BT == 128, "pipe tiles");
-  static_assert((BT == 256 && (NS == 4 || NS == 5)) || (BT == 128 && NS >= 4 && NS <= 8),
-                "ring depth: 256x256 4 slots, or 5 (the whole 160 KiB LDS); 128x128 4-8 slots");
+  static_assert(NS == 4, "ring depth: 4 slots (5- and 6/8-slot rings measured slower, round 3/4)");
   EA_DEV static int wm(int w) { return BT == 256 ? (w >> 2) * 128 : (w >> 2) * 64 + ((w >> 1) & 1) * 32; }
   EA_DEV static int wn(int w) { return BT == 256 ? (w & 3) * 64 : (w & 1) * 64; }
 };

@@ -1,6 +1,6 @@
 // Dense GEMM launches on the LDS-DMA kernel (gemm_kern.h: gemm_bf16_lds): 2-stage ring, except
 // the 64x128 tile, whose 3-deep ring (two blocks per CU instead of three) measured 0.9-1.2%
-// faster on the C3 step (scripts/gpu_lds64_ab.sh; EA_LDS64_STAGES=2|3|4).
+// faster on the C3 step (round 2, scripts/gpu_lds64_ab.sh).
 #include "gemm_kern.h"
 
 #include <cstdlib>
@@ -14,32 +14,16 @@ int launch_lds_dense(GemmP& p, int a_k, int b_k, dim3 grid, hipStream_t st) {
   else if (a_k) EA_GL(BMV, BNV, true, false, S);       \
   else if (b_k) EA_GL(BMV, BNV, false, true, S);       \
   else EA_GL(BMV, BNV, false, false, S);
-  static const int s64 = [] { const char* e = std::getenv("EA_LDS64_STAGES"); return e ? std::atoi(e) : 3; }();
   if (p.bm == 32) {  // small-M GEMMs (decoder tokens, positional rows): twice the blocks of 64x128
     if (b_k) EA_GL(32, 128, true, true, 3);
     else EA_GL(32, 128, true, false, 3);
   } else if (p.bm == 64) {
-    if (s64 == 3) {
-      if (b_k) EA_GL(64, 128, true, true, 3);
-      else EA_GL(64, 128, true, false, 3);
-    } else if (s64 == 4) {
-      if (b_k) EA_GL(64, 128, true, true, 4);
-      else EA_GL(64, 128, true, false, 4);
-    } else {
-      if (b_k) EA_GL(64, 128, true, true, 2);
-      else EA_GL(64, 128, true, false, 2);
-    }
+    if (b_k) EA_GL(64, 128, true, true, 3);
+    else EA_GL(64, 128, true, false, 3);
   } else if (p.bm == 256 && p.bn == 256) {
     EA_GL4(256, 256, 2)
   } else {
-    // EA_LDS128_STAGES=3: grids of at most one block per CU take a 3-deep ring (96 KiB, one
-    // block per CU) for deeper prefetch (A/B switch)
-    static const int s128 = [] { const char* e = std::getenv("EA_LDS128_STAGES"); return e ? std::atoi(e) : 2; }();
-    if (s128 == 3 && (long)grid.x * grid.y * grid.z <= 256) {
-      EA_GL4(128, 128, 3)
-    } else {
-      EA_GL4(128, 128, 2)
-    }
+    EA_GL4(128, 128, 2)
   }
 #undef EA_GL4
 #undef EA_GL

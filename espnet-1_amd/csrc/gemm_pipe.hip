@@ -3,26 +3,11 @@
 
 namespace eag {
 int launch_pipe(GemmP& p, int a_k, int b_k, dim3 grid, hipStream_t st) {
-  if (p.bm == 256 && g_pipe_slots == 5) {  // 5-slot ring: the whole 160 KiB LDS, 4 slices in flight
-    if (a_k && b_k) hipLaunchKernelGGL((gemm_pipe<true, true, 0, 256, 5>), grid, dim3(512), 0, st, p);
-    else if (a_k) hipLaunchKernelGGL((gemm_pipe<true, false, 0, 256, 5>), grid, dim3(512), 0, st, p);
-    else if (b_k) hipLaunchKernelGGL((gemm_pipe<false, true, 0, 256, 5>), grid, dim3(512), 0, st, p);
-    else hipLaunchKernelGGL((gemm_pipe<false, false, 0, 256, 5>), grid, dim3(512), 0, st, p);
-  } else if (p.bm == 256) {
+  if (p.bm == 256) {
     if (a_k && b_k) hipLaunchKernelGGL((gemm_pipe<true, true, 0, 256>), grid, dim3(512), 0, st, p);
     else if (a_k) hipLaunchKernelGGL((gemm_pipe<true, false, 0, 256>), grid, dim3(512), 0, st, p);
     else if (b_k) hipLaunchKernelGGL((gemm_pipe<false, true, 0, 256>), grid, dim3(512), 0, st, p);
     else hipLaunchKernelGGL((gemm_pipe<false, false, 0, 256>), grid, dim3(512), 0, st, p);
-  } else if (g_pipe128_slots == 8) {  // 128x128, one block per CU with 6 slices in flight
-    if (a_k && b_k) hipLaunchKernelGGL((gemm_pipe<true, true, 0, 128, 8>), grid, dim3(512), 0, st, p);
-    else if (a_k) hipLaunchKernelGGL((gemm_pipe<true, false, 0, 128, 8>), grid, dim3(512), 0, st, p);
-    else if (b_k) hipLaunchKernelGGL((gemm_pipe<false, true, 0, 128, 8>), grid, dim3(512), 0, st, p);
-    else hipLaunchKernelGGL((gemm_pipe<false, false, 0, 128, 8>), grid, dim3(512), 0, st, p);
-  } else if (g_pipe128_slots == 6) {
-    if (a_k && b_k) hipLaunchKernelGGL((gemm_pipe<true, true, 0, 128, 6>), grid, dim3(512), 0, st, p);
-    else if (a_k) hipLaunchKernelGGL((gemm_pipe<true, false, 0, 128, 6>), grid, dim3(512), 0, st, p);
-    else if (b_k) hipLaunchKernelGGL((gemm_pipe<false, true, 0, 128, 6>), grid, dim3(512), 0, st, p);
-    else hipLaunchKernelGGL((gemm_pipe<false, false, 0, 128, 6>), grid, dim3(512), 0, st, p);
   } else {
     if (a_k && b_k) hipLaunchKernelGGL((gemm_pipe<true, true, 0, 128>), grid, dim3(512), 0, st, p);
     else if (a_k) hipLaunchKernelGGL((gemm_pipe<true, false, 0, 128>), grid, dim3(512), 0, st, p);

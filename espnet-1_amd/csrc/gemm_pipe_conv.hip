@@ -3,11 +3,8 @@
 
 namespace eag {
 int launch_pipe_conv(GemmP& p, dim3 grid, hipStream_t st) {
-  const bool s5 = g_pipe_slots == 5;  // (the fused conv1-gradient dgrad needs its LDS images: 4 slots)
-  if (p.g.mode == EA_CONV_FWD && s5) hipLaunchKernelGGL((gemm_pipe<true, true, EA_CONV_FWD, 256, 5>), grid, dim3(512), 0, st, p);
-  else if (p.g.mode == EA_CONV_FWD) hipLaunchKernelGGL((gemm_pipe<true, true, EA_CONV_FWD>), grid, dim3(512), 0, st, p);
+  if (p.g.mode == EA_CONV_FWD) hipLaunchKernelGGL((gemm_pipe<true, true, EA_CONV_FWD>), grid, dim3(512), 0, st, p);
   else if (p.g.mode == EA_CONV_DGRAD) hipLaunchKernelGGL((gemm_pipe<true, false, EA_CONV_DGRAD>), grid, dim3(512), 0, st, p);
-  else if (s5) hipLaunchKernelGGL((gemm_pipe<false, false, EA_CONV_WGRAD, 256, 5>), grid, dim3(512), 0, st, p);
   else hipLaunchKernelGGL((gemm_pipe<false, false, EA_CONV_WGRAD>), grid, dim3(512), 0, st, p);
   EA_LAUNCH_CHECK();
   return 0;

@@ -240,14 +240,9 @@ int launch_skinny_ln(GemmP& p, const float* gamma, const float* beta, float eps,
   EA_LAUNCH_CHECK();
   return 0;
 }
-int launch_skinny(GemmP& p, hipStream_t st, int rows32) {
-  if (rows32) {  // 32 x 32 blocks (M beyond a few 16-row blocks: the decoder's 1,312 tokens)
-    dim3 grid(ea_cdiv(p.N, 32), ea_cdiv(p.M, 32), 1);
-    hipLaunchKernelGGL((gemm_skinny_kernel<2, 2, 4>), grid, dim3(64 * SK_W), 0, st, p);
-  } else {
-    dim3 grid(ea_cdiv(p.N, 32), ea_cdiv(p.M, 16), 1);
-    hipLaunchKernelGGL((gemm_skinny_kernel<1, 2, 8>), grid, dim3(64 * SK_W), 0, st, p);
-  }
+int launch_skinny(GemmP& p, hipStream_t st) {
+  dim3 grid(ea_cdiv(p.N, 32), ea_cdiv(p.M, 16), 1);
+  hipLaunchKernelGGL((gemm_skinny_kernel<1, 2, 8>), grid, dim3(64 * SK_W), 0, st, p);
   EA_LAUNCH_CHECK();
   return 0;
 }

@@ -941,9 +941,8 @@ static int ln_bwd_impl(int rows, int d, const void* dy, int dy_dtype, long lddy,
   else                                                                                                    \
     hipLaunchKernelGGL((ln_bwd_vec_kernel<NJ, float, false, U>), dim3(nb), dim3(256), 0, st, rows, d, (const float*)dy, lddy, x, \
                        ldx, gamma, mean, rstd, dx, lddx, accumulate, rpb, workspace);
-    // rows in flight per wave step (d <= 512): EA_LN_BWD_U = 2 (default) or 4 (A/B)
-    static const int ln_u = [] { const char* e = std::getenv("EA_LN_BWD_U"); return e ? std::atoi(e) : 2; }();
-    if (d > 512) { EA_LNB(2, 1) } else if (ln_u == 4) { EA_LNB(1, 4) } else { EA_LNB(1, 2) }
+    // two rows in flight per wave step for d <= 512 (four measured neutral, round 4)
+    if (d > 512) { EA_LNB(2, 1) } else { EA_LNB(1, 2) }
 #undef EA_LNB
     EA_LAUNCH_CHECK();
     if (!dgamma) { *nparts_out = nb; return 0; }

@@ -186,8 +186,6 @@ struct AttnP {
   uint32_t* dmask; int ldm;  // dropout keep bits [z*T1 + i][ldm words], bit j&31 of word j>>5:
                              // written by the forward, read by the backward (else rehashed)
   char* wsDummy;             // 1 KiB sink for the pipelined dQ pass's out-of-range dbd stores
-  const uint32_t* fmask; int nchm;  // forward-order keep bits (ea_attn_keep_bits): word
-                                    // [(z*nqb + qb)*nchm + c][thread], bit 4t + r
 };
 // ldm >= 2 * ceil(T2 / 64): a 64-key chunk is the word pair (j0 >> 5, +1)
 
@@ -1307,16 +1305,10 @@ __global__ __launch_bounds__(256, 2) void attn_fwd2_kernel(AttnP a) {
   const uint64_t npair = (uint64_t)((a.T2 + 1) >> 1);
   const uint64_t prA = ((uint64_t)z * a.T1 + ibase + odd) * npair, prB = prA + 2 * npair;
   const int pb = 48 - 16 * w;
-  // MM 3: this thread's keep bits of chunk c, one word per chunk, fetched a chunk ahead (issued
-  // before the chunk's DMA so the chunk-top vmcnt wait covers it)
-  const uint32_t* fm = MM == 3 ? a.fmask + ((long)z * nqb + qb) * a.nchm * 256 + tid : nullptr;
-  uint32_t fb_next = MM == 3 && nch > 0 ? fm[0] : 0u;
   for (int c = 0; c < nch; ++c) {
     const int j0 = c * KC;
     vmcnt_le<0>();  // this chunk's images (and the previous chunk's keep-bit stores) landed
     bar();          // all waves done with the previous chunk (and, at c = 0, the setup images)
-    const uint32_t fb = fb_next;
-    if (MM == 3 && c + 1 < nch) fb_next = fm[(c + 1) * 256];
     if (c + 1 < nch) {
       dma_kv(c + 1);
       if (REL) dma_ring(64 * c + 128, 8);
@@ -1399,13 +1391,6 @@ __global__ __launch_bounds__(256, 2) void attn_fwd2_kernel(AttnP a) {
 #pragma unroll
       for (int t = 0; t < 4; ++t) oacc[t][r] *= alpha;
     }
-    if (MM == 3) {  // keep bits generated ahead (ea_attn_keep_bits), already in dmask
-      const float sc = 1.f / (1.f - a.p);
-#pragma unroll
-      for (int t = 0; t < 4; ++t)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) pv[t][r] *= ((fb >> (4 * t + r)) & 1u) ? sc : 0.f;
-    }
     // dropout (keep bits -> dmask for the backward)
     if (MM == 1 || MM == 2) {
       const uint32_t key = ea_seed_key(seed), thr = ea_drop_thr(a.p);
@@ -1461,60 +1446,6 @@ __global__ __launch_bounds__(256, 2) void attn_fwd2_kernel(AttnP a) {
 #pragma unroll
     for (int t = 0; t < 4; ++t) orow[16 * t + lc] = (bf16)(oacc[t][r] * inv);
     if (lc == 0) a.lse[(long)z * a.T1 + i] = lrun[r] > 0.f ? mrun[r] + __logf(lrun[r]) : INFINITY;
-  }
-}
-
-// The forward's dropout keep decisions computed ahead of it (ea_attn_keep_bits), with the
-// forward's own indexing (workgroup (z, 64 queries), wave 16 queries, lane (row group g, key
-// lc)), pair hashes and lane-pair exchange, so the bits are those attn_fwd2_kernel<MM 1> would
-// draw: the backward's row words into dmask, and per thread and key chunk one word of the 16
-// (t, r) decisions into fmask for the forward (MM 3).  Launched on a side stream beside MFMA-
-// bound work, it takes the counter hash off the attention forward's VALU budget.
-__global__ __launch_bounds__(256) void attn_keepbits_kernel(AttnP a) {
-  const int nqb = (a.T1 + QB - 1) / QB;
-  const int z = blockIdx.x / nqb, qb = blockIdx.x % nqb;
-  const int b = z / a.H;
-  const int i0 = qb * QB;
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int g = lane >> 4, lc = lane & 15;
-  const int kl = a.klen ? (int)min((long long)a.T2, a.klen[b]) : a.T2;
-  const int kend = a.causal ? min(kl, i0 + QB) : kl;
-  const int nch = (kend + KC - 1) / KC;
-  const uint64_t seed = ea_salted(a.seed, a.salt);
-  const uint32_t key = ea_seed_key(seed), thr = ea_drop_thr(a.p);
-  const int ibase = i0 + 16 * w + 4 * g;
-  const int odd = lc & 1;
-  const uint64_t npair = (uint64_t)((a.T2 + 1) >> 1);
-  const uint64_t prA = ((uint64_t)z * a.T1 + ibase + odd) * npair, prB = prA + 2 * npair;
-  uint32_t* fm = a.fmask ? (uint32_t*)a.fmask + ((long)z * nqb + qb) * a.nchm * 256 + tid : nullptr;
-  for (int c = 0; c < nch; ++c) {
-    const int j0 = c * KC;
-    uint64_t bal[4][4];
-    uint32_t fb = 0u;
-#pragma unroll
-    for (int t = 0; t < 4; ++t) {
-      const uint64_t jp = (uint64_t)((j0 + 16 * t + lc) >> 1);
-      const uint32_t hA = ea_pair_hash(key, prA + jp), hB = ea_pair_hash(key, prB + jp);
-      const uint32_t pA = (uint32_t)__builtin_amdgcn_mov_dpp((int)hA, 0xB1, 0xF, 0xF, false);
-      const uint32_t pB = (uint32_t)__builtin_amdgcn_mov_dpp((int)hB, 0xB1, 0xF, 0xF, false);
-      const uint32_t hh[4] = {odd ? pA : hA, odd ? hA : pA, odd ? pB : hB, odd ? hB : pB};
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const bool kept = (odd ? hh[r] >> 16 : hh[r] & 0xffffu) >= thr;
-        fb |= (kept ? 1u : 0u) << (4 * t + r);
-        bal[t][r] = __ballot(kept);
-      }
-    }
-    if (fm) fm[c * 256] = fb;
-    if (a.dmask && lc < 2) {
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int i = ibase + r;
-        const uint64_t lo = lc ? bal[2][r] : bal[0][r], hi = lc ? bal[3][r] : bal[1][r];
-        const uint32_t word = (uint32_t)((lo >> (16 * g)) & 0xffffu) | ((uint32_t)((hi >> (16 * g)) & 0xffffu) << 16);
-        if (i < a.T1) a.dmask[((long)z * a.T1 + i) * a.ldm + (j0 >> 5) + lc] = word;
-      }
-    }
   }
 }
 
@@ -2012,47 +1943,6 @@ extern "C" int ea_attn_fused_fwd2(int B, int H, int T1, int T2, int dk, const vo
     else if (mm == 1) hipLaunchKernelGGL((attn_fwd2_kernel<false, 1>), grid, dim3(256), 0, st, a);
     else hipLaunchKernelGGL((attn_fwd2_kernel<false, 2>), grid, dim3(256), 0, st, a);
   }
-  EA_LAUNCH_CHECK();
-  return 0;
-}
-
-extern "C" int ea_attn_keep_bits_words(int B, int H, int T1, int T2, long* words) {
-  EA_CHECK_ARG(B >= 1 && H >= 1 && T1 >= 1 && T2 >= 1 && words != nullptr);
-  *words = (long)B * H * ((T1 + QB - 1) / QB) * ((T2 + KC - 1) / KC) * 256;
-  return 0;
-}
-
-extern "C" int ea_attn_keep_bits(int B, int H, int T1, int T2, const long long* klen, int causal, float p,
-                                 unsigned long long seed, unsigned* dmask, int ldm, unsigned* fmask, void* stream) {
-  EA_ENTRY();
-  EA_CHECK_ARG(B >= 1 && H >= 1 && T1 >= 1 && T2 >= 1 && p > 0.f && p < 1.f && fmask != nullptr);
-  EA_CHECK_ARG(dmask != nullptr && ldm >= 2 * ((T2 + 63) / 64));
-  AttnP a{};
-  a.B = B; a.H = H; a.T1 = T1; a.T2 = T2; a.klen = klen; a.causal = causal; a.p = p; a.seed = seed;
-  a.salt = ea_g_rng_salt;
-  a.dmask = (uint32_t*)dmask; a.ldm = ldm;
-  a.fmask = (const uint32_t*)fmask; a.nchm = (T2 + KC - 1) / KC;
-  hipLaunchKernelGGL(attn_keepbits_kernel, dim3(B * H * ((T1 + QB - 1) / QB)), dim3(256), 0, (hipStream_t)stream, a);
-  EA_LAUNCH_CHECK();
-  return 0;
-}
-
-extern "C" int ea_attn_fused_fwd2b(int B, int H, int T1, int T2, int dk, const void* q, long ldq, const void* k,
-                                   long ldk, const void* v, long ldv, const float* bu, const float* bv,
-                                   const void* pp, long ldp, const long long* klen, int causal, float scale, float p,
-                                   unsigned long long seed, void* o, long ldo, float* lse, const unsigned* fmask,
-                                   void* stream) {
-  EA_ENTRY();
-  EA_CHECK_ARG(dk == DK && B >= 1 && H >= 1 && T1 >= 1 && T2 >= 1 && p > 0.f && fmask != nullptr);
-  EA_CHECK_ARG(!pp || (T1 == T2 && bv != nullptr));
-  EA_CHECK_ARG(ldq % 8 == 0 && ldk % 8 == 0 && ldv % 8 == 0 && (!pp || ldp % 8 == 0));
-  AttnP a = make_p(B, H, T1, T2, q, ldq, k, ldk, v, ldv, bu, bv, pp, ldp, klen, causal, scale, p, seed);
-  a.o = (bf16*)o; a.ldo = ldo; a.lse = lse;
-  a.fmask = (const uint32_t*)fmask; a.nchm = (T2 + KC - 1) / KC;
-  dim3 grid(B * H * ((T1 + QB - 1) / QB));
-  const hipStream_t st = (hipStream_t)stream;
-  if (pp) hipLaunchKernelGGL((attn_fwd2_kernel<true, 3>), grid, dim3(256), 0, st, a);
-  else hipLaunchKernelGGL((attn_fwd2_kernel<false, 3>), grid, dim3(256), 0, st, a);
   EA_LAUNCH_CHECK();
   return 0;
 }

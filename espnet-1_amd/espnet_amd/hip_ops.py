@@ -211,42 +211,20 @@ def join_aux():
 
 
 GRAD_READY = None  # callable(prefix): a block's parameter gradients are final (DP overlap)
-# single process, EA_STREAM_WGRAD=N > 0: every N finished blocks, the deferred weight
-# gradients / reductions queued so far are launched on the weight-gradient side stream (one
-# grouped GEMM per flush) to overlap the backward of the blocks below.  Measured slower on the
-# C3 step (1599-1605 utt/s at N=1, 1588 at N=2, vs 1616-1618 with one flush at the end:
-# profiles/r3_stream_wgrad_ab.txt — the grouped tiles take whole CUs from the main stream's
-# chip-filling kernels), so the default (0) flushes once at the end of the pass
-STREAM_WGRAD = int(os.environ.get("EA_STREAM_WGRAD", "0"))
 # the end-of-pass reduction flush on the side stream beside the grouped GEMM (EA_REDUCE_SIDE=0: serial)
 REDUCE_SIDE = os.environ.get("EA_REDUCE_SIDE", "1") != "0"
-# single process, deferred pass: the main stream joins the side stream after every block
-# (EA_LAYER_JOIN=1) or only once, at the end of the pass (0).  The per-block side work left
-# under deferral (the linear_pos product dBD^T (q+v), read by the deferred flush) needs no
-# earlier join; each join is a cross-queue dependency of the captured graph, ~10 us idle
-LAYER_JOIN = os.environ.get("EA_LAYER_JOIN", "1") != "0"
-_STREAM_COUNT = [0]
 
 
 def grad_ready(bound):
     """A block's backward is done.  Data parallel (GRAD_READY set): the hook flushes the
     deferred weight gradients and issues the bucket all-reduces from the side stream, so the
-    main stream goes on with the backward.  Single process: the deferred queues are flushed
-    onto the side stream every STREAM_WGRAD blocks (deferred_wgrad's exit joins the side
-    stream before anything reads the gradients); with nothing deferred, the main stream
-    joins the side stream here."""
+    main stream goes on with the backward.  Single process: the main stream joins the side
+    stream here, once per block (the deferred queues flush at the end of the pass; flushing
+    them per block on the side stream, or joining only once per pass, measured slower:
+    profiles/r3_stream_wgrad_ab.txt)."""
     if GRAD_READY is not None:
         GRAD_READY(bound.prefix)
         return
-    if STREAM_WGRAD > 0 and OVERLAP_WGRAD and (WGRAD_Q.active or REDUCE_Q.active) and torch.cuda.is_available():
-        _STREAM_COUNT[0] += 1
-        if _STREAM_COUNT[0] >= STREAM_WGRAD:
-            _STREAM_COUNT[0] = 0
-            with wgrad(*deferred_tensors()):
-                flush_deferred()
-        return
-    if not LAYER_JOIN and (WGRAD_Q.active or REDUCE_Q.active):
-        return  # deferred_wgrad's exit joins the side stream before anything reads its results
     join_wgrad()
 
 
@@ -385,7 +363,7 @@ def linear(x, w, out, *, epi: Epilogue = None):
 # transpose after every optimizer step (and shadow refresh), lets those GEMMs read both
 # operands K-major.  EA_WT_SHADOW=0 turns it off (A/B).
 WT_SHADOW = os.environ.get("EA_WT_SHADOW", "1") != "0"
-WT_MAX_KIN = int(os.environ.get("EA_WT_MAX_KIN", "512"))
+WT_MAX_KIN = 512  # 2048-wide inputs too measured neutral (round 4): the FFN w_2 epilogue sets its time
 TSHADOWS = {}  # arena shadow storage pointer -> weakref(TransposedShadow) (the arena owns it)
 
 
@@ -696,10 +674,7 @@ class deferred_wgrad:
 
     def __exit__(self, *exc):
         WGRAD_Q.active, REDUCE_Q.active = self.prev
-        _STREAM_COUNT[0] = 0
         if exc[0] is None:
-            if GRAD_READY is None and not LAYER_JOIN:
-                join_wgrad()  # the queued products may read what the side stream wrote
             if GRAD_READY is None and OVERLAP_WGRAD and REDUCE_SIDE and torch.cuda.is_available():
                 # the pass's reductions (bias column sums, LayerNorm parameter sums: bandwidth-
                 # bound) on the side stream beside the grouped weight-gradient GEMM (MFMA-bound)
@@ -852,26 +827,14 @@ def scale_dropout(x, y, scale=1.0, p=0.0, seed=0):
     return y
 
 
-# off by default: on MI355X the two-pass form is faster (C3: 27.26 vs 27.43-28.07 ms/step,
-# scripts/ab_env.sh) since its column sums run on the weight-gradient side stream, off the
-# backward's critical path, while the fused kernel puts a reduction on it
-FUSE_DROP_COLSUM = os.environ.get("EA_FUSE_DROP_COLSUM", "0") != "0"
-
-
 def scale_dropout_colsum(x, y, out, scale=1.0, p=0.0, seed=0, accumulate=True):
-    """y = dropout(scale * x) and out (+)= column sums of y in one pass (ea_scale_dropout_colsum).
-    Default: the two-pass form (ea_scale_dropout, then ea_colsum on the weight-gradient side
-    stream); EA_FUSE_DROP_COLSUM=1 selects the fused kernel."""
-    if not FUSE_DROP_COLSUM:
-        scale_dropout(x, y, scale=scale, p=p, seed=seed)
-        with wgrad(y):
-            colsum(y, out, accumulate=accumulate)
-        return y
-    rows, cols, ldx = _rows(x)
-    _, _, ldy = _rows(y)
-    w, wn = _ws(x.device)
-    lib.ea_scale_dropout_colsum(rows, cols, x.data_ptr(), ldx, y.data_ptr(), dt(y), ldy, float(scale), float(p),
-                                seed & 0xFFFFFFFFFFFFFFFF, out.data_ptr(), int(accumulate), w, wn, stream())
+    """y = dropout(scale * x) and out (+)= column sums of y: the two-pass form (ea_scale_dropout,
+    then ea_colsum on the weight-gradient side stream).  The one-pass kernel
+    (ea_scale_dropout_colsum) puts the reduction on the backward's critical path and measured
+    slower on MI355X (C3: 27.43-28.07 vs 27.26 ms/step, round 1)."""
+    scale_dropout(x, y, scale=scale, p=p, seed=seed)
+    with wgrad(y):
+        colsum(y, out, accumulate=accumulate)
     return y
 
 

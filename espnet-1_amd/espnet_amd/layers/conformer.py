@@ -25,29 +25,6 @@ from .common import (ACT_SWISH, EPI_ACT, EPI_DACT, EPI_RESID, EPI_STORE, F32, Bo
 
 # ----------------------------------------------------------------------------- holders
 
-# the attention's dropout keep bits drawn ahead on the auxiliary stream (EA_ATTN_BITS_AHEAD=1;
-# outputs are bit-identical either way).  Measured: the forward kernel 44.1 -> 37.7 us, but the
-# generator (13.3 us) slows the macaron FFN GEMMs it runs beside: step 1781-1786 -> 1777 utt/s
-# (profiles/r4_attn_bits_ab.txt), so the hash stays in the forward by default
-ATTN_BITS_AHEAD = os.environ.get("EA_ATTN_BITS_AHEAD", "0") == "1"
-_KEEP_WORDS = {}
-
-
-def attn_keep_words(B, H, T1, T2):
-    key = (B, H, T1, T2)
-    if key not in _KEEP_WORDS:
-        n = ctypes.c_long(0)
-        lib.ea_attn_keep_bits_words(B, H, T1, T2, ctypes.addressof(n))
-        _KEEP_WORDS[key] = n.value
-    return _KEEP_WORDS[key]
-
-
-# depthwise-conv dw / dbias partials deferred into the grouped reduce (EA_DWCONV_DEFER=1; measured neutral, off)
-DWCONV_DEFER = os.environ.get("EA_DWCONV_DEFER", "0") == "1"
-# the attention block's input-gradient GEMM issued before the linear_pos product forks onto the
-# side stream (EA_DPP_LATE=1) instead of after it: the graph keeps the captured order of a
-# node's dependents when it spreads them over queues
-DPP_LATE = os.environ.get("EA_DPP_LATE", "0") == "1"
 # the GLU backward fused into the depthwise conv's backward kernel (ea_dwconv_glu_bwd: the
 # same arithmetic without the f32 dglu round trip; EA_FUSE_DW_GLU=0: the two-kernel path)
 FUSE_DW_GLU = os.environ.get("EA_FUSE_DW_GLU", "1") != "0"
@@ -62,7 +39,7 @@ BN_STATS_IN_CONV = os.environ.get("EA_BN_STATS_IN_CONV", "1") != "0"
 
 
 def _glu_in_conv(K, g2, d):
-    return (GLU_IN_CONV and FUSE_DW_GLU and not DWCONV_DEFER and K in (3, 5, 7, 15, 31)
+    return (GLU_IN_CONV and FUSE_DW_GLU and K in (3, 5, 7, 15, 31)
             and g2.dtype == torch.bfloat16 and d % 4 == 0 and g2.data_ptr() % 8 == 0 and torch.cuda.is_available())
 
 class PositionwiseFeedForward(nn.Module):
@@ -220,18 +197,6 @@ class ConformerBlockFn(torch.autograd.Function):
         li = L.layer_idx
         sd = lambda s: site_seed(seed, li, s)  # noqa: E731
         x0 = x.reshape(N, d)
-        # the attention's dropout keep bits drawn on the auxiliary stream while the macaron FFN's
-        # MFMA-bound GEMMs run (ea_attn_keep_bits); the forward then reads them (fwd2b)
-        pre = None
-        if ATTN_BITS_AHEAD and pa > 0 and fused_attn_ok(cd, dk, T, T) and torch.cuda.is_available():
-            dmask_a, ldm_a = attn_dmask(B * H * T, T, pa, dev)
-            fmask_a = empty(attn_keep_words(B, H, T, T), dtype=torch.int32, device=dev)
-            with ops.aux(dmask_a, fmask_a, olens):
-                lib.ea_attn_keep_bits(B, H, T, T, olens.data_ptr(), 0, float(pa), sd(3), dmask_a.data_ptr(), ldm_a,
-                                      fmask_a.data_ptr(), ops.stream())
-                ev_a = torch.cuda.Event()
-                ev_a.record()
-            pre = (dmask_a, ldm_a, fmask_a, ev_a)
         # ---- macaron FFN  (encoder_layer.py:115-123)
         x1, s_ff1 = _ffn_fwd(L, b, x0, "feed_forward_macaron", "norm_ff_macaron", p, sd(1), sd(2))
         # ---- rel-pos MHSA (encoder_layer.py:126-149, attention.py:262-305)
@@ -249,21 +214,12 @@ class ConformerBlockFn(torch.autograd.Function):
             # one kernel: (q+u)k^T + rel_shift((q+v)p^T), mask, softmax, dropout, @v
             O = empty(N, d, dtype=cd, device=dev)
             lse = empty(B * H * T, device=dev)
-            if pre is not None:
-                dmask, ldm, fmask_a, ev_a = pre
-                torch.cuda.current_stream().wait_event(ev_a)
-                lib.ea_attn_fused_fwd2b(B, H, T, T, dk, qkv.data_ptr(), 3 * d, qkv[:, d:].data_ptr(), 3 * d,
-                                        qkv[:, 2 * d:].data_ptr(), 3 * d, b.f(A + "pos_bias_u").data_ptr(),
-                                        b.f(A + "pos_bias_v").data_ptr(), pp.data_ptr(), d, olens.data_ptr(), 0,
-                                        scale, float(pa), sd(3), O.data_ptr(), d, lse.data_ptr(),
-                                        fmask_a.data_ptr(), ops.stream())
-            else:
-                dmask, ldm = attn_dmask(B * H * T, T, pa, dev)
-                lib.ea_attn_fused_fwd2(B, H, T, T, dk, qkv.data_ptr(), 3 * d, qkv[:, d:].data_ptr(), 3 * d,
-                                       qkv[:, 2 * d:].data_ptr(), 3 * d, b.f(A + "pos_bias_u").data_ptr(),
-                                       b.f(A + "pos_bias_v").data_ptr(), pp.data_ptr(), d, olens.data_ptr(), 0,
-                                       scale, float(pa), sd(3), O.data_ptr(), d, lse.data_ptr(), ptr(dmask), ldm,
-                                       ops.stream())
+            dmask, ldm = attn_dmask(B * H * T, T, pa, dev)
+            lib.ea_attn_fused_fwd2(B, H, T, T, dk, qkv.data_ptr(), 3 * d, qkv[:, d:].data_ptr(), 3 * d,
+                                   qkv[:, 2 * d:].data_ptr(), 3 * d, b.f(A + "pos_bias_u").data_ptr(),
+                                   b.f(A + "pos_bias_v").data_ptr(), pp.data_ptr(), d, olens.data_ptr(), 0,
+                                   scale, float(pa), sd(3), O.data_ptr(), d, lse.data_ptr(), ptr(dmask), ldm,
+                                   ops.stream())
             ldT = 0
             s_core = ("fused", lse, dmask, ldm)
         else:
@@ -376,8 +332,7 @@ class ConformerBlockFn(torch.autograd.Function):
         ops.batchnorm_bwd(dz, y, bn_mean, bn_rstd, b.f(C + "norm.weight"), b.f(C + "norm.bias"),
                           ACT_SWISH, dy, b.g(C + "norm.weight"), b.g(C + "norm.bias"))
         dg2 = empty(N, 2 * d, dtype=cd, device=dev)
-        fuse = (FUSE_DW_GLU and K in (3, 5, 7, 15, 31) and g2.dtype == torch.bfloat16
-                and not (DWCONV_DEFER and ops.REDUCE_Q.active))
+        fuse = FUSE_DW_GLU and K in (3, 5, 7, 15, 31) and g2.dtype == torch.bfloat16
         if fuse:
             # the GLU backward inside the depthwise conv's input-gradient store (no f32 dglu)
             w, wn = ops._ws(dev, B * ((T + 31) // 32) * d * (K + 1) + 1024)
@@ -390,21 +345,10 @@ class ConformerBlockFn(torch.autograd.Function):
                 glu = empty(N, d, device=dev)
                 lib.ea_glu_fwd(N, d, g2.data_ptr(), ops.dt(g2), glu.data_ptr(), 0, ops.stream())
             dglu = empty(N, d, device=dev)
-            if DWCONV_DEFER and ops.REDUCE_Q.active and K in (3, 5, 7, 15, 31):
-                # dw / dbias partials summed with the pass's other parameter-gradient reductions
-                part = empty(B * ((T + 31) // 32) * d * (K + 1), device=dev)
-                npart = ctypes.c_int(0)
-                lib.ea_dwconv_bwd_partials(B, T, d, K, glu.data_ptr(), b.f(C + "depthwise_conv.weight").data_ptr(),
-                                           dy.data_ptr(), dglu.data_ptr(), part.data_ptr(), part.numel(),
-                                           ctypes.addressof(npart), ops.stream())
-                rl = d * (K + 1)
-                ops.REDUCE_Q.add_reduce(part, npart.value, d * K, rl, b.g(C + "depthwise_conv.weight").view(-1))
-                ops.REDUCE_Q.add_reduce(part[d * K:], npart.value, d, rl, b.g(C + "depthwise_conv.bias"))
-            else:
-                w, wn = ops._ws(dev, B * ((T + 31) // 32) * d * (K + 1) + 1024)
-                lib.ea_dwconv_bwd(B, T, d, K, glu.data_ptr(), b.f(C + "depthwise_conv.weight").data_ptr(),
-                                  dy.data_ptr(), dglu.data_ptr(), b.g(C + "depthwise_conv.weight").data_ptr(),
-                                  b.g(C + "depthwise_conv.bias").data_ptr(), 1, w, wn, ops.stream())
+            w, wn = ops._ws(dev, B * ((T + 31) // 32) * d * (K + 1) + 1024)
+            lib.ea_dwconv_bwd(B, T, d, K, glu.data_ptr(), b.f(C + "depthwise_conv.weight").data_ptr(),
+                              dy.data_ptr(), dglu.data_ptr(), b.g(C + "depthwise_conv.weight").data_ptr(),
+                              b.g(C + "depthwise_conv.bias").data_ptr(), 1, w, wn, ops.stream())
             lib.ea_glu_bwd(N, d, g2.data_ptr(), ops.dt(g2), dglu.data_ptr(), dg2.data_ptr(), ops.stream())
         with ops.wgrad(dg2, xn3):
             ops.colsum(dg2, b.g(C + "pointwise_conv1.bias"))
@@ -459,10 +403,6 @@ class ConformerBlockFn(torch.autograd.Function):
             lib.ea_add_2d(N, d, dqv.data_ptr(), ops.dt(dqv), d, dqkv.data_ptr(), ops.dt(dqkv), 3 * d, 1.0,
                           ops.stream())
         qkv_w = b.w(A + "linear_q.weight", A + "linear_k.weight", A + "linear_v.weight", shape=(3 * d, d))
-        dxn2 = None
-        if DPP_LATE:  # the input gradient captured ahead of the side-stream product below
-            dxn2 = empty(N, d, dtype=cd, device=dev)
-            ops.linear_dx(dqkv, qkv_w, dxn2)
         # linear_pos: dp[h] = sum_b dBD[h][b]^T qv[b, :, h]  (K = B*T), dWpos = dp^T pos; with the
         # shifted layout the GEMM runs over every physical column and rows [shift, shift + P2) of
         # its output are dp
@@ -477,9 +417,8 @@ class ConformerBlockFn(torch.autograd.Function):
             ops.colsum(dqkv, b.g(A + "linear_q.bias", A + "linear_k.bias", A + "linear_v.bias", shape=(3 * d,)))
             ops.linear_dw(dqkv, xn2, b.g(A + "linear_q.weight", A + "linear_k.weight", A + "linear_v.weight",
                                           shape=(3 * d, d)), accumulate=True)
-        if dxn2 is None:
-            dxn2 = empty(N, d, dtype=cd, device=dev)
-            ops.linear_dx(dqkv, qkv_w, dxn2)
+        dxn2 = empty(N, d, dtype=cd, device=dev)
+        ops.linear_dx(dqkv, qkv_w, dxn2)
         dv_ff1 = dv_buf(N, d, cd, dev)
         ln_bwd(dxn2, x1, b, "norm_mha", mu2, rs2, dx, accumulate=True,
                drop=drop_arg(dv_ff1, L.ff_scale, p, sd(2), b.g("feed_forward_macaron.w_2.bias")))

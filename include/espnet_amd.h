@@ -132,29 +132,17 @@ int ea_gemm_set_tile(int bm, int bn);
 /* Route 256x256-tile bf16 GEMMs to the pipelined kernel (gemm_pipe: 4-slot ring of 32-deep
  * K slices, counted vmcnt, one barrier per slice) when on != 0 (A/B switch). */
 int ea_gemm_set_pipe(int on);
-/* Ring depth of the 128x128 ping-pong tile: 4 slots (two blocks per CU) or 6 / 8 (one block
- * per CU, 4 / 6 slices of 16 KiB in flight).  Process-wide; A/B switch (EA_PIPE128_SLOTS). */
-int ea_gemm_set_pipe128_slots(int slots);
-/* gemm_k128 (128x128 tile, K-major A and B, one block per CU, 64-deep K-tiles through a
- * `slots`-deep LDS ring with cross-tile fragment prefetch) for bf16 GEMMs: mode 0 off, 1 =
+/* gemm_k128 (128x128 tile, K-major A and B, one block per CU of 8 waves in two K groups, 64-deep
+ * K-tiles through a `slots`-deep (3 or 4) LDS ring) for bf16 GEMMs: mode 0 off, 1 =
  * where a 64x128 / 128x128 tile was chosen and the 128x128 grid has 128-256 tiles (the
  * N = 512 GEMMs at M = 7,968), 2 = such grids of any size >= 128 tiles, 3 = every eligible
- * GEMM (K % 64 == 0; tests).  Process-wide (EA_GEMM_K128). */
+ * GEMM (K % 64 == 0; tests); mode 1 also needs K >= 1024.  Default 1.  Process-wide (EA_GEMM_K128). */
 int ea_gemm_set_k128(int mode, int slots);
 /* bf16 GEMMs with M <= max_m rows (K-major A and B, K % 32 == 0, unbatched: the incremental
  * decoder's per-step Linears) on gemm_skinny — 16 x 32 output blocks whose 8 waves split K,
  * operands loaded straight into MFMA fragments, partial tiles summed through LDS before the
  * epilogue.  0 = off; default 16 (EA_GEMM_SKINNY).  Process-wide. */
 int ea_gemm_set_skinny(int max_m);
-/* The same K-split kernel with 32 x 32 output blocks for bf16 GEMMs with M <= max_m rows beyond
- * the few-row limit (the training decoder's B*(L+1) tokens); 0 = off (EA_GEMM_ROWS32).
- * Process-wide; A/B switch. */
-int ea_gemm_set_rows32(int max_m);
-/* 256x256 bf16 tiles with K-major A (K % 64 == 0) on gemm_quad — four waves of 128 x 128 (a
- * third less LDS fragment traffic per MFMA than gemm_pipe's eight waves of 128 x 64), ring of
- * `slots` (4 or 5) 32-deep slices.  on: bit 1 = K-major B, bit 2 = MN-major B too; 0 = gemm_pipe
- * (EA_GEMM_QUAD).  Process-wide; A/B switch. */
-int ea_gemm_set_quad(int on, int slots);
 /* C = epi(LayerNorm(x) . W^T): x f32 (M x K, ldx, rows 16-B aligned), gamma / beta f32 (K),
  * W bf16 (N x K, ldw) — the LayerNorm (eps) computed per row inside the few-row GEMM
  * (16 x 32 blocks, 8 waves splitting K) and rounded to bf16 in the MFMA operand registers,
@@ -162,11 +150,6 @@ int ea_gemm_set_quad(int on, int slots);
  * Replaces a LayerNorm (layer_norm.py) + Linear pair of the incremental decoder's step. */
 int ea_gemm_ln(int M, int N, int K, const float* x, long ldx, const float* gamma, const float* beta, float eps,
                const void* W, long ldw, void* C, int c_dtype, long ldc, const ea_epilogue* epi, void* stream);
-/* Plain bf16 GEMMs (STORE epilogue without bias, scale or dropout; alpha / beta honoured;
- * unbatched; M >= 4096) on hipBLASLt: mode bit 1 = N <= 512, bit 2 = N > 512; 0 = off
- * (EA_GEMM_BLASLT; default 1).  Shapes hipBLASLt has no workspace-free algorithm for stay on ea_gemm's
- * own kernels.  Process-wide. */
-int ea_gemm_set_blaslt(int mode);
 
 /* One problem of a grouped launch: C[M,N] (f32, row stride ldc) = beta*C + op(A) op(B), bf16
  * operands in the layouts of ea_gemm (a_kmajor/b_kmajor shared by the group), lda/ldb
@@ -458,12 +441,6 @@ int ea_dwconv_fwd_glu(int B, int T, int C, int K, const void* g2, const float* w
 int ea_dwconv_fwd_glu_stats(int B, int T, int C, int K, const void* g2, const float* w, const float* bias,
                             float* y, float* part, void* stream);
 int ea_dwconv_stats_parts(int B, int T, int* nparts);
-/* ea_dwconv_bwd without the parameter reductions (K in {3,5,7,15,31}): dx, and per-block
- * partials part[p][0 : C*K] of dw in its (C, 1, K) layout and part[p][C*K : C*(K+1)] of dbias,
- * p < *nparts (row stride C*(K+1)) — plain row sums the caller may defer and group. */
-int ea_dwconv_bwd_partials(int B, int T, int C, int K, const float* x, const float* w, const float* dy,
-                           float* dx, float* part, long part_elems, int* nparts, void* stream);
-
 /* q + pos_bias_u / q + pos_bias_v (attention.py:287-290) for the fused qkv rows. */
 int ea_add_pos_bias(long N, int H, int dk, const void* q, long ldq, const float* u, const float* v,
                     void* qu, void* qv, int dtype, void* stream);
@@ -529,20 +506,6 @@ int ea_attn_fused_fwd2(int B, int H, int T1, int T2, int dk, const void* q, long
                        const void* pp, long ldp, const long long* klen, int causal, float scale, float p,
                        unsigned long long seed, void* o, long ldo, float* lse, unsigned* dmask, int ldm,
                        void* stream);
-/* The dropout keep decisions of ea_attn_fused_fwd2 (same B, H, T1, T2, klen, causal, p > 0 and
- * seed; the same per-step salt) computed ahead of the forward, e.g. on a side stream beside
- * MFMA-bound work: the backward's row words into dmask (as ea_attn_fused_fwd2 writes them) and
- * the forward's own order into fmask (ea_attn_keep_bits_words() 32-bit words).  Then
- * ea_attn_fused_fwd2b runs the forward reading fmask instead of hashing — bit-identical output,
- * and dmask serves the backward. */
-int ea_attn_keep_bits_words(int B, int H, int T1, int T2, long* words);
-int ea_attn_keep_bits(int B, int H, int T1, int T2, const long long* klen, int causal, float p,
-                      unsigned long long seed, unsigned* dmask, int ldm, unsigned* fmask, void* stream);
-int ea_attn_fused_fwd2b(int B, int H, int T1, int T2, int dk, const void* q, long ldq, const void* k,
-                        long ldk, const void* v, long ldv, const float* bu, const float* bv,
-                        const void* pp, long ldp, const long long* klen, int causal, float scale, float p,
-                        unsigned long long seed, void* o, long ldo, float* lse, const unsigned* fmask,
-                        void* stream);
 /* Backward of ea_attn_fused_fwd(2): dq = d(q + bu) (flags bit 0, pp only: + d(q + bv), the
  * rel-pos path dBD·pp computed in-kernel), dk, dv (bf16), and optionally:
  *   dbd (pp only, or NULL): the band dbd[h][b][i][T-1-i+j] = gradient of the raw rel-pos term

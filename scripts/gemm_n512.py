@@ -31,12 +31,9 @@ CONFIGS = [  # (label, pipe bits, forced tile (bm, bn) or None, 128x128 ring slo
     ("lds64x128", 1, (64, 128), 4),
     ("lds128", 1, (128, 128), 4),
     ("pipe128", 3, (128, 128), 4),
-    ("pipe128s6", 3, (128, 128), 6),
-    ("pipe128s8", 3, (128, 128), 8),
     ("pipe256", 1, (256, 256), 4),
     ("k128s3", 1, "k128:3", 4),
     ("k128s4", 1, "k128:4", 4),
-    ("k128s5", 1, "k128:5", 4),
 ]
 
 
@@ -55,7 +52,6 @@ def run(name, N, K, ak, bk, kind, odt, iters=50):
         epi = ops.make_epi()
     out = []
     for label, pipe, tile, slots in CONFIGS:
-        lib.ea_gemm_set_pipe128_slots(slots)
         lib.ea_gemm_set_pipe(pipe)
         if isinstance(tile, str):  # gemm_k128 with a ring depth (K-major A and B only)
             if not (ak and bk):
@@ -80,7 +76,6 @@ def run(name, N, K, ak, bk, kind, odt, iters=50):
         out.append((label, us, 2.0 * M * N * K / us * 1e-6))
     lib.ea_gemm_set_tile(0, 0)
     lib.ea_gemm_set_pipe(1)
-    lib.ea_gemm_set_pipe128_slots(4)
     lib.ea_gemm_set_k128(0, 4)
     # hipBLASLt reference (plain bf16 GEMM, no epilogue)
     a = A if ak else A.t()

@@ -420,42 +420,3 @@ def test_bwdkv_pipelined_matches_original(B, H, T1, T2, rel, causal, klens, p, m
     assert torch.equal(dq1, dq2) and torch.equal(dk1, dk2) and torch.equal(dv1, dv2)
 
 
-@pytest.mark.parametrize("B,H,T1,T2,rel,causal,klens", [
-    (3, 2, 249, 249, True, False, [249, 200, 64]),
-    (1, 2, 300, 300, True, False, [300]),
-    (2, 2, 45, 45, False, True, [45, 30]),
-    (2, 1, 41, 300, False, False, [300, 131]),
-    (1, 1, 5, 5, True, False, [5]),
-    (2, 2, 499, 499, True, False, [499, 331]),
-])
-def test_keep_bits_ahead_match_forward(B, H, T1, T2, rel, causal, klens):
-    """ea_attn_keep_bits (the forward's dropout decisions computed ahead) + ea_attn_fused_fwd2b
-    (the forward reading them) against ea_attn_fused_fwd2 hashing in-kernel: O, lse and every
-    keep word the forward writes, bit for bit."""
-    from espnet_amd import hip_ops as ops
-    from espnet_amd._lib import lib
-    import ctypes
-    q, k, v, u, vb, pp, _ = _inputs(B, H, T1, T2, rel, seed=23)
-    klen = torch.tensor(klens, dtype=torch.long, device=DEV)
-    d = H * 64
-    p = 0.1
-    ldm = 2 * ((T2 + 63) // 64)
-    ptr = lambda t: 0 if t is None else t.data_ptr()  # noqa: E731
-    args = lambda: (B, H, T1, T2, 64, q.data_ptr(), d, k.data_ptr(), d, v.data_ptr(), d, ptr(u), ptr(vb), ptr(pp),  # noqa: E731
-                    d, klen.data_ptr(), int(causal), 1 / 8, p, 7)
-    O1 = torch.empty(B, T1, d, dtype=bf, device=DEV)
-    l1 = torch.empty(B * H * T1, device=DEV)
-    m1 = torch.zeros(B * H * T1 * ldm, dtype=torch.int32, device=DEV)
-    lib.ea_attn_fused_fwd2(*args(), O1.data_ptr(), d, l1.data_ptr(), m1.data_ptr(), ldm, ops.stream())
-    nw = ctypes.c_long(0)
-    lib.ea_attn_keep_bits_words(B, H, T1, T2, ctypes.addressof(nw))
-    fm = torch.empty(nw.value, dtype=torch.int32, device=DEV)
-    m2 = torch.zeros_like(m1)
-    lib.ea_attn_keep_bits(B, H, T1, T2, klen.data_ptr(), int(causal), p, 7, m2.data_ptr(), ldm, fm.data_ptr(),
-                          ops.stream())
-    O2 = torch.empty_like(O1)
-    l2 = torch.empty_like(l1)
-    lib.ea_attn_fused_fwd2b(*args(), O2.data_ptr(), d, l2.data_ptr(), fm.data_ptr(), ops.stream())
-    torch.cuda.synchronize()
-    assert torch.equal(m1, m2), "keep words differ"
-    assert torch.equal(l1, l2) and torch.equal(O1, O2)

@@ -170,12 +170,11 @@ def test_gemm_unaligned_leading_dims(dtype, a_k, b_k):
 # (bm, bn, pipe): pipe=1 routes the 256x256 tile to gemm_pipe (4-slot ring of 32-deep slices)
 from espnet_amd._lib import GEMM_PIPE as PIPE_DEFAULT  # noqa: E402  (restored after each test)
 # (bm, bn, pipe[, 128x128 ring slots])
-TILES = [(32, 128, 0), (64, 128, 0), (128, 128, 0), (128, 128, 3), (128, 128, 3, 6), (128, 128, 3, 8),
-         (256, 256, 0), (256, 256, 1)]
+TILES = [(32, 128, 0), (64, 128, 0), (128, 128, 0), (128, 128, 3), (256, 256, 0), (256, 256, 1)]
 
 
 def _tile_id(t):
-    return f"{t[0]}x{t[1]}{'p' * t[2]}" + (f"s{t[3]}" if len(t) > 3 else "")
+    return f"{t[0]}x{t[1]}{'p' * t[2]}"
 
 
 @pytest.fixture
@@ -184,11 +183,9 @@ def forced_tile(request):
     bm, bn, pipe = request.param[:3]
     L.lib.ea_gemm_set_tile(bm, bn)
     L.lib.ea_gemm_set_pipe(pipe)
-    L.lib.ea_gemm_set_pipe128_slots(request.param[3] if len(request.param) > 3 else 4)
     yield (bm, bn)
     L.lib.ea_gemm_set_tile(0, 0)
     L.lib.ea_gemm_set_pipe(PIPE_DEFAULT)
-    L.lib.ea_gemm_set_pipe128_slots(4)
 
 
 @pytest.mark.parametrize("forced_tile", TILES, indirect=True, ids=_tile_id)
@@ -302,13 +299,13 @@ def test_mn_tail_guard_rehomes_exact_views():
     assert ops._mn_tail_guard(v, 16, K, W, (0, 0), 1, 1) is v  # MN % 8 == 0: whole chunks
 
 
-@pytest.mark.parametrize("slots", [3, 4, 5])
+@pytest.mark.parametrize("slots", [3, 4])
 @pytest.mark.parametrize("MNK", [(7968, 512, 2048), (7968, 512, 512), (300, 200, 128), (129, 520, 64),
-                                 (1000, 384, 1536)])
+                                 (1000, 384, 1536), (7968, 512, 64)])
 def test_gemm_k128_vs_fp64(slots, MNK):
-    """gemm_k128 (128x128 tile, K-major A and B, deep LDS ring with cross-tile fragment
-    prefetch; the N = 512 GEMMs of the C3 step) against fp64: the bench shapes and edges in
-    M and N, bf16 and f32 outputs, fused RESID / ACT epilogues."""
+    """gemm_k128 (128x128 tile, K-major A and B, two K groups of four waves, buffer-load LDS
+    ring; the N = 512 GEMMs of the C3 step) against fp64: the bench shapes and edges in M and
+    N, a single K-tile, bf16 and f32 outputs, fused RESID / ACT epilogues."""
     ops, L = _ops()
     M, N, K = MNK
     g = torch.Generator().manual_seed(M + N + K + slots)
@@ -336,12 +333,13 @@ def test_gemm_k128_vs_fp64(slots, MNK):
         torch.testing.assert_close(aux.double().cpu(), h, atol=3e-2, rtol=2e-2)
         torch.testing.assert_close(Ca.double().cpu(), h * torch.sigmoid(h), atol=3e-2, rtol=2e-2)
     finally:
-        L.lib.ea_gemm_set_k128(0, 4)
+        L.lib.ea_gemm_set_k128(1, 4)
 
 
 def test_gemm_k128_linear_paths_match_default():
-    """ea_gemm_set_k128(1): the Linear forward / input-gradient GEMMs at the C3 token count
-    route to gemm_k128 and agree with the default tiles to bf16-accumulation-order noise."""
+    """ea_gemm_set_k128(1) (the default): the Linear forward / input-gradient GEMMs at the C3
+    token count route to gemm_k128 and agree with the 64x128 tile (mode 0) to
+    bf16-accumulation-order noise."""
     ops, L = _ops()
     g = torch.Generator().manual_seed(8)
     M = 7968
@@ -349,12 +347,12 @@ def test_gemm_k128_linear_paths_match_default():
     w = mk((512, 2048), torch.bfloat16, g, 0.05)
     y0 = torch.empty(M, 512, device="cuda")
     y1 = torch.empty(M, 512, device="cuda")
-    ops.linear(x, w, y0)
-    L.lib.ea_gemm_set_k128(1, 4)
+    L.lib.ea_gemm_set_k128(0, 4)
     try:
-        ops.linear(x, w, y1)
+        ops.linear(x, w, y0)
     finally:
-        L.lib.ea_gemm_set_k128(0, 4)
+        L.lib.ea_gemm_set_k128(1, 4)
+    ops.linear(x, w, y1)
     torch.testing.assert_close(y1, y0, atol=1e-3, rtol=1e-3)
 
 
@@ -505,10 +503,10 @@ def test_gemm_skinny_vs_fp64(MNK):
 @pytest.mark.parametrize("a_k,b_k", [(1, 1), (1, 0), (0, 1)])
 @pytest.mark.parametrize("MNK", [(7968, 512, 2048), (4100, 1536, 512), (4096, 200, 72)])
 @pytest.mark.parametrize("out", [torch.bfloat16, torch.float32])
-def test_gemm_blaslt_plain_vs_fp64(a_k, b_k, MNK, out):
-    """ea_gemm_set_blaslt(3): plain products (alpha / beta, no other epilogue) on hipBLASLt with
-    every operand layout the host mirror issues, bf16 and f32 outputs, ldc wider than N; the
-    same call with a bias stays on the MFMA kernels — both against fp64."""
+def test_gemm_plain_vs_fp64(a_k, b_k, MNK, out):
+    """Plain products (alpha / beta, no other epilogue: the Linear input gradients) with every
+    operand layout the host mirror issues, bf16 and f32 outputs, ldc wider than N, and the same
+    call with a bias — all on the library's own MFMA kernels, against fp64."""
     ops, L = _ops()
     M, N, K = MNK
     g = torch.Generator().manual_seed(M + N + K + a_k * 2 + b_k)
@@ -517,54 +515,20 @@ def test_gemm_blaslt_plain_vs_fp64(a_k, b_k, MNK, out):
     B = mk((N, up(K)) if b_k else (K, up(N)), torch.bfloat16, g, 0.1)
     ref = ref_mm(A, B, a_k, b_k, M, N, K)
     tol = dict(atol=2e-3 * K ** 0.5, rtol=2e-2 if out == torch.bfloat16 else 2e-3)
-    L.lib.ea_gemm_set_blaslt(3)
-    try:
-        C = torch.full((M, N + 8), 7.0, device="cuda", dtype=out)
-        ops.gemm(A, B, C, M=M, N=N, K=K, a_kmajor=a_k, b_kmajor=b_k, lda=A.stride(0), ldb=B.stride(0),
-                 ldc=C.stride(0), epi=ops.make_epi(alpha=0.5))
-        torch.testing.assert_close(C[:, :N].double().cpu(), 0.5 * ref, **tol)
-        assert (C[:, N:] == 7.0).all(), "wrote outside ldc columns"
-        C0 = C.clone()
-        ops.gemm(A, B, C, M=M, N=N, K=K, a_kmajor=a_k, b_kmajor=b_k, lda=A.stride(0), ldb=B.stride(0),
-                 ldc=C.stride(0), epi=ops.make_epi(beta=1.0))
-        torch.testing.assert_close(C[:, :N].double().cpu(), C0[:, :N].double().cpu() + ref, **tol)
-        bias = mk((N,), torch.float32, g)
-        Cb = torch.empty(M, N, device="cuda", dtype=out)
-        ops.gemm(A, B, Cb, M=M, N=N, K=K, a_kmajor=a_k, b_kmajor=b_k, lda=A.stride(0), ldb=B.stride(0), ldc=N,
-                 epi=ops.make_epi(bias=bias))
-        torch.testing.assert_close(Cb.double().cpu(), ref + bias.double().cpu(), **tol)
-    finally:
-        L.lib.ea_gemm_set_blaslt(0)
-
-
-@pytest.mark.parametrize("MNK", [(1312, 512, 512), (1312, 2048, 512), (1312, 512, 2048), (100, 1536, 96),
-                                 (37, 4999, 64)])
-def test_gemm_rows32_vs_fp64(MNK):
-    """ea_gemm_set_rows32: the K-split kernel's 32 x 32 blocks at the training decoder's token
-    count (M = 1,312) and ragged M / N tails, with the RESID and ACT epilogues, vs fp64."""
-    ops, L = _ops()
-    M, N, K = MNK
-    g = torch.Generator().manual_seed(M * 7 + N + K)
-    A = mk((M, K + 8), torch.bfloat16, g)
-    W = mk((N, K + 8), torch.bfloat16, g, 0.1)
-    bias = mk((N + 4,), torch.float32, g)[:N]
-    ref = ref_mm(A, W, 1, 1, M, N, K) + bias.double().cpu()
-    tol = dict(atol=2e-3 * K ** 0.5, rtol=2e-3)
-    L.lib.ea_gemm_set_rows32(4096)
-    try:
-        R = torch.randn(M, N, generator=g).cuda()
-        R0 = R.clone()
-        ops.gemm(A, W, R, M=M, N=N, K=K, a_kmajor=1, b_kmajor=1, lda=A.stride(0), ldb=W.stride(0), ldc=N,
-                 epi=ops.make_epi(L.EPI_RESID, bias=bias, resid=R, rscale=1.0))
-        torch.testing.assert_close(R.double().cpu(), R0.double().cpu() + ref, **tol)
-        aux = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
-        Ca = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
-        ops.gemm(A, W, Ca, M=M, N=N, K=K, a_kmajor=1, b_kmajor=1, lda=A.stride(0), ldb=W.stride(0), ldc=N,
-                 epi=ops.make_epi(L.EPI_ACT, bias=bias, act=L.ACT_RELU, aux=aux))
-        torch.testing.assert_close(aux.double().cpu(), ref, atol=3e-2, rtol=2e-2)
-        torch.testing.assert_close(Ca.double().cpu(), ref.clamp_min(0), atol=3e-2, rtol=2e-2)
-    finally:
-        L.lib.ea_gemm_set_rows32(0)
+    C = torch.full((M, N + 8), 7.0, device="cuda", dtype=out)
+    ops.gemm(A, B, C, M=M, N=N, K=K, a_kmajor=a_k, b_kmajor=b_k, lda=A.stride(0), ldb=B.stride(0),
+             ldc=C.stride(0), epi=ops.make_epi(alpha=0.5))
+    torch.testing.assert_close(C[:, :N].double().cpu(), 0.5 * ref, **tol)
+    assert (C[:, N:] == 7.0).all(), "wrote outside ldc columns"
+    C0 = C.clone()
+    ops.gemm(A, B, C, M=M, N=N, K=K, a_kmajor=a_k, b_kmajor=b_k, lda=A.stride(0), ldb=B.stride(0),
+             ldc=C.stride(0), epi=ops.make_epi(beta=1.0))
+    torch.testing.assert_close(C[:, :N].double().cpu(), C0[:, :N].double().cpu() + ref, **tol)
+    bias = mk((N,), torch.float32, g)
+    Cb = torch.empty(M, N, device="cuda", dtype=out)
+    ops.gemm(A, B, Cb, M=M, N=N, K=K, a_kmajor=a_k, b_kmajor=b_k, lda=A.stride(0), ldb=B.stride(0), ldc=N,
+             epi=ops.make_epi(bias=bias))
+    torch.testing.assert_close(Cb.double().cpu(), ref + bias.double().cpu(), **tol)
 
 
 @pytest.mark.parametrize("MNK", [(10, 1536, 512), (10, 2048, 512), (16, 5000, 512), (3, 40, 96), (7, 512, 2048)])
@@ -597,39 +561,3 @@ def test_gemm_ln_vs_fp64(MNK):
     torch.testing.assert_close(C[:, :N], C0, atol=2e-2, rtol=1e-2)
 
 
-@pytest.mark.parametrize("b_k", [1, 0])
-@pytest.mark.parametrize("slots", [4, 5])
-@pytest.mark.parametrize("MNK", [(7968, 2048, 512), (300, 520, 128), (513, 264, 2048), (256, 256, 64)])
-def test_gemm_quad_vs_fp64(slots, MNK, b_k):
-    """gemm_quad (256x256 tiles, four waves of 128 x 128, K-major A; K-major or MN-major B):
-    against fp64 with the STORE / RESID / ACT epilogues, M and N edges, bf16 and f32 outputs."""
-    ops, L = _ops()
-    M, N, K = MNK
-    g = torch.Generator().manual_seed(M + N + K + slots)
-    A = mk((M, K + 8), torch.bfloat16, g)
-    B = mk((N, K + 8) if b_k else (K, N + 8), torch.bfloat16, g, 0.1)
-    L.lib.ea_gemm_set_quad(3, slots)
-    L.lib.ea_gemm_set_tile(256, 256)
-    try:
-        ref = ref_mm(A, B, 1, b_k, M, N, K)
-        C = torch.full((M, N + 4), 7.0, device="cuda")
-        ops.gemm(A, B, C, M=M, N=N, K=K, a_kmajor=1, b_kmajor=b_k, lda=A.stride(0), ldb=B.stride(0), ldc=C.stride(0))
-        torch.testing.assert_close(C[:, :N].double().cpu(), ref, atol=2e-3 * K ** 0.5, rtol=2e-3)
-        assert (C[:, N:] == 7.0).all()
-        bias = mk((N,), torch.float32, g)
-        R = torch.randn(M, N, generator=g).cuda()
-        R0 = R.clone()
-        ops.gemm(A, B, R, M=M, N=N, K=K, a_kmajor=1, b_kmajor=b_k, lda=A.stride(0), ldb=B.stride(0), ldc=N,
-                 epi=ops.make_epi(L.EPI_RESID, bias=bias, resid=R, rscale=0.5))
-        torch.testing.assert_close(R.double().cpu(), R0.double().cpu() + 0.5 * (ref + bias.double().cpu()),
-                                   atol=2e-3 * K ** 0.5, rtol=2e-3)
-        aux = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
-        Ca = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
-        ops.gemm(A, B, Ca, M=M, N=N, K=K, a_kmajor=1, b_kmajor=b_k, lda=A.stride(0), ldb=B.stride(0), ldc=N,
-                 epi=ops.make_epi(L.EPI_ACT, bias=bias, act=L.ACT_SWISH, aux=aux))
-        h = ref + bias.double().cpu()
-        torch.testing.assert_close(aux.double().cpu(), h, atol=3e-2, rtol=2e-2)
-        torch.testing.assert_close(Ca.double().cpu(), h * torch.sigmoid(h), atol=3e-2, rtol=2e-2)
-    finally:
-        L.lib.ea_gemm_set_quad(0, 5)
-        L.lib.ea_gemm_set_tile(0, 0)
