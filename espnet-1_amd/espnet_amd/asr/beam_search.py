@@ -102,8 +102,10 @@ class CTCPrefixScorer:
             r_new, log_psi, f_min, f_max, cand = state
             row = cand[i].tolist()
             # an id outside the scored set: scoring_idmap holds -1 there, so the reference
-            # indexes the LAST scored column (scorers/ctc.py:59-60)
-            pos = row.index(int(new_id)) if int(new_id) in row else -1
+            # indexes the LAST scored column, r[:, :, i, -1] over the snum scored columns
+            # (scorers/ctc.py:59-60) — column len(row) - 1, not the appended <eos> column that
+            # r_new carries beyond them (ctc_prefix_score.py:92-93)
+            pos = row.index(int(new_id)) if int(new_id) in row else len(row) - 1
             return r_new[0][i, pos], log_psi[i, int(new_id)].expand(log_psi.size(1)), f_min, f_max
         sc, st = state
         return sc[i], st[i]

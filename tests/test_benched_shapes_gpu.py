@@ -152,6 +152,10 @@ def _exact_c3_b32(cfg, m_cpu, inp):
         _EXACT["c3"] = (loss.item(), {k: float(v) for k, v in stats.items()},
                         {k: p.grad.detach() for k, p in ora.params.items()},
                         ora.encoder_out.detach(), ora.encoder_out_lens)
+        lg = ora.ctc_logits.detach()
+        top2 = lg.topk(2, dim=-1).values
+        _EXACT["c3_out"] = dict(ctc_logits=lg, ctc_argmax=lg.argmax(-1), ctc_gap=(top2[..., 0] - top2[..., 1]),
+                                dec_logits=ora.decoder_out.detach())
         del ora
     return _EXACT["c3"]
 
@@ -204,6 +208,25 @@ def test_c3_b32_fp32_vs_float64():
     np.testing.assert_array_equal(olens.cpu().numpy(), x_olens.numpy())
     e_enc = _rel(enc.detach().cpu(), x_enc)
     assert e_enc <= 2e-5, e_enc
+    # CTC logits and alignment indices (ctc.py:119-127) and the decoder's logits
+    # (transformer_decoder.py:92-145) at the benchmarked shape, valid frames / positions only
+    xo = _EXACT["c3_out"]
+    olens_np = x_olens.numpy()
+    fmask = torch.arange(enc.shape[1])[None, :] < x_olens[:, None]
+    lg = m.ctc.logits(enc.detach()).cpu().double()
+    ctc_err = float((lg - xo["ctc_logits"]).abs()[fmask].max())
+    am = m.ctc.argmax(enc.detach()).cpu()
+    flips = (am != xo["ctc_argmax"]) & fmask
+    # a flip is only admissible where float64's own top-2 gap is inside the logit tolerance
+    assert not bool((flips & (xo["ctc_gap"] >= 1e-4)).any()), torch.nonzero(flips & (xo["ctc_gap"] >= 1e-4))[:10]
+    dl = m._last_decoder_out.detach().cpu().double()
+    pmask = torch.arange(dl.shape[1])[None, :] < (inp["text_lengths"] + 1)[:, None]
+    dec_err = float((dl - xo["dec_logits"]).abs()[pmask].max())
+    print(f"c3 B=32 fp32: CTC logits max |err| {ctc_err:.2e}, argmax flips {int(flips.sum())} of "
+          f"{int(fmask.sum())} frames ({int(((xo['ctc_gap'] < 1e-4) & fmask).sum())} near-ties); "
+          f"decoder logits max |err| {dec_err:.2e}; olens {olens_np[:3]}")
+    assert ctc_err <= 1e-4, ctc_err
+    assert dec_err <= 1e-4, dec_err
     worst = []
     for k, p in m.named_parameters():
         mine = p.grad.detach().cpu()
