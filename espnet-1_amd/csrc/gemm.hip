@@ -255,7 +255,7 @@ static int gemm_impl(int dtype, int a_kmajor, int b_kmajor, int M, int N, int K,
   const int esz = dtype == EA_BF16 ? 2 : 4;
   (void)esz;
   if (epi->kind == EA_EPI_RESID) EA_CHECK_ARG(c_dtype == EA_F32);
-  GemmP p;
+  GemmP p{};
   p.M = M; p.N = N; p.K = K;
   p.A = A; p.lda = lda; p.sAb = sAb; p.sAh = sAh;
   p.B = B; p.ldb = ldb; p.sBb = sBb; p.sBh = sBh;
@@ -361,6 +361,9 @@ static int gemm_impl(int dtype, int a_kmajor, int b_kmajor, int M, int N, int K,
   }
   p.splitk = splitk;
   p.kchunk = kchunk;
+  // keep bits are written only by the 8-column vector epilogue of the bf16 LDS-DMA kernels
+  if (epi->keep && epi->drop_p > 0.f && epi->kind == EA_EPI_ACT && (!p.lds || !p.vec8 || splitk > 1))
+    return EA_ERR_BAD_ARG;
   static const bool trace = std::getenv("EA_GEMM_TRACE") != nullptr;  // shape census (diagnostics)
   if (trace)
     std::fprintf(stderr, "[ea_gemm] M=%d N=%d K=%d ak=%d bk=%d nz=%d tile=%dx%d%s splitk=%d epi=%d geo=%d lds=%d\n", M,
@@ -449,3 +452,57 @@ extern "C" int ea_gemm_conv_w1b(const ea_conv_geo* geo, int M, int N, int K, con
                    nullptr, 0, stream, geo, x, T, Fin, part, pos);
 }
 
+
+// The four parity classes of the conv2 input gradient fused with conv1's weight gradient
+// (ea_gemm_conv_w1b each) as ONE launch: per-class launches each end in a partly filled round
+// of 256x256 tiles (2.3-2.4 rounds per class at C3); one grid ordered longest K first fills it.
+// Same tiles, same arithmetic and the same partial-tile layout as the four launches.
+extern "C" int ea_gemm_conv_w1b_all(const ea_conv_geo* geo, int N, const void* A, long lda, const void* B, long ldb,
+                                    const ea_epilogue* epi, const float* x, int T, int Fin, float* part,
+                                    const unsigned char* pos, void* stream) {
+  EA_ENTRY();
+  EA_CHECK_ARG(geo != nullptr && geo->mode == EA_CONV_DGRAD && x != nullptr && part != nullptr && pos != nullptr);
+  EA_CHECK_ARG(epi != nullptr && epi->kind == EA_EPI_DACT && epi->act == EA_ACT_RELU);
+  EA_CHECK_ARG(N >= 8 && N % 8 == 0 && geo->C % 64 == 0 && T >= 3 && Fin >= 3 && g_gemm_pipe != 0);
+  EA_CHECK_ARG(lda % 8 == 0 && ldb % 8 == 0 && ((uintptr_t)A % 16) == 0 && ((uintptr_t)B % 16) == 0);
+  GemmP p{};
+  p.N = N;
+  p.A = A; p.lda = lda;
+  p.B = B; p.ldb = ldb;
+  p.nh = 1; p.splitk = 1;
+  p.C = nullptr; p.c_dtype = EA_BF16; p.ldc = N;
+  p.epi = *epi;
+  p.salt = ea_g_rng_salt;
+  p.stamp = g_probe;
+  p.diag = g_diag;
+  p.g = *geo;
+  p.w1x = x; p.w1part = part; p.w1pos = pos; p.w1T = T; p.w1F = Fin;
+  p.vec_a = p.vec_b = p.vec_c = p.vec8 = p.lds = 1;
+  p.bm = p.bn = 256;
+  p.tiles_n = ea_cdiv(N, 256);
+  int items = 0, tiles = 0;
+  for (int c = 0; c < 4; ++c) {
+    const int a = c >> 1, e = c & 1;
+    const long rows = (long)geo->B * geo->nI[a] * geo->nJ[e];
+    EA_CHECK_ARG(rows < (1L << 24));
+    if (rows == 0) continue;
+    const int k = p.ncls++;
+    p.cls_item0[k] = items;
+    p.cls_M[k] = (int)rows;
+    p.cls_K[k] = (a ? 1 : 2) * (e ? 1 : 2) * geo->C;
+    p.cls_a[k] = a;
+    p.cls_e[k] = e;
+    p.cls_tile0[k] = tiles;
+    p.cls_pos[k] = geo->plane[c] / geo->C * (N / 8);
+    tiles += (int)ea_cdiv(rows, 256);
+    items += (int)ea_cdiv(rows, 256) * p.tiles_n;
+  }
+  if (p.ncls == 0) return 0;
+  p.cls_item0[p.ncls] = items;
+  p.M = p.cls_M[0]; p.K = p.cls_K[0]; p.kchunk = p.K; p.tiles_m = ea_cdiv(p.M, 256);
+  const int unit = 8 * p.tiles_n;  // the block -> item map is a bijection on whole units
+  const dim3 grid((unsigned)(ea_cdiv(items, unit) * unit));
+  static const bool trace = std::getenv("EA_GEMM_TRACE") != nullptr;
+  if (trace) std::fprintf(stderr, "[ea_gemm] conv dgrad x%d classes, %d tiles, grid %u\n", p.ncls, items, grid.x);
+  return launch_pipe_conv(p, grid, (hipStream_t)stream);
+}

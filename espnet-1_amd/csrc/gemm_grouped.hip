@@ -79,7 +79,7 @@ __global__ __launch_bounds__(512, 1) void gemm_grouped(const GroupProbD* __restr
   for (int i = 0; i < 8; ++i)
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
-  pipe_tile<AK, BKM, 0, 256, NS>(p, smem, q.A, q.B, m0, n0, 0, q.K, acc);
+  pipe_tile<AK, BKM, 0, 256, NS>(p, tile_ov(p), smem, q.A, q.B, m0, n0, 0, q.K, acc);
   const EpiK ek = make_epik(p);
   epi_wave<EA_EPI_STORE, 8, 4>(p, ek, smem, 0, 0, 0, m0 + wm, n0 + wn, lane, w, acc);
 }

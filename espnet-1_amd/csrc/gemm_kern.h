@@ -54,6 +54,11 @@ struct GemmP {
   float* w1part;                   //   per-M-tile conv1 weight / bias gradient partials
   const uint8_t* w1pos;            //   ReLU support bits (N/8 bytes per row) instead of aux, or null
   int w1T, w1F;
+  // ea_gemm_conv_w1b_all: the four parity classes of the conv2 input gradient in ONE grid,
+  // items ordered by class (longest K first), each class's tiles at cls_item0[c] ..; 0 = one class
+  int ncls;
+  int cls_item0[5], cls_M[4], cls_K[4], cls_a[4], cls_e[4], cls_tile0[4];
+  long cls_pos[4];                 //   byte offset of the class plane's first row in w1pos
 };
 
 // launchers of the LDS-DMA kernels (grid = tiles x 1 x (batch * split-K slices))
@@ -202,7 +207,10 @@ EA_DEV void epi_one(const GemmP& p, int z, int zb, int zh, int row, int col, flo
     const float r = e.resid ? e.resid[(long)row * e.ldr + col] : 0.f;
     ((float*)p.C)[cidx] = r + e.rscale * v;
   } else {  // EA_EPI_DACT
-    if (e.drop_p > 0.f) v *= drop_scale(seed, didx, e.drop_p);
+    if (e.drop_p > 0.f && e.keep)
+      v *= ((e.keep[(long)row * e.ldkeep + (col >> 3)] >> (col & 7)) & 1u) ? 1.f / (1.f - e.drop_p) : 0.f;
+    else if (e.drop_p > 0.f)
+      v *= drop_scale(seed, didx, e.drop_p);
     v *= act_bwd(e.act, load_as_f(e.aux, (long)row * e.ldaux + col, e.aux_dtype));
     store_from_f(p.C, cidx, p.c_dtype, v);
   }
@@ -333,7 +341,13 @@ EA_DEV void epi_four_pre(const GemmP& p, const EpiK& k, int z, int zb, int zh, i
     for (int c = 0; c < 4; ++c) v[c] = (has_o ? o[c] : 0.f) + e.rscale * v[c];
     st4(p.C, cidx, EA_F32, v);
   } else {
-    drop4k(k, didx, v);
+    if (k.drop && e.keep) {
+      const uint32_t kb = e.keep[(long)row * e.ldkeep + (col >> 3)] >> (col & 7);
+#pragma unroll
+      for (int c = 0; c < 4; ++c) v[c] *= ((kb >> c) & 1u) ? k.sc : 0.f;
+    } else {
+      drop4k(k, didx, v);
+    }
     act_bwd_mul_n<4>(e.act, v, o);
     st4(p.C, cidx, p.c_dtype, v);
   }
@@ -373,9 +387,31 @@ EA_DEV void drop8k(const EpiK& k, uint64_t idx, float (&v)[8]) {  // idx even
     v[2 * q + 1] *= (h >> 16) >= k.thr ? k.sc : 0.f;
   }
 }
+// drop8k that also returns the 8 decisions (bit c = element idx + c kept; all set without dropout)
+EA_DEV uint32_t drop8k_bits(const EpiK& k, uint64_t idx, float (&v)[8]) {  // idx even
+  if (!k.drop) return 0xffu;
+  uint32_t bits = 0u;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const uint32_t h = ea_pair_hash(k.key, (idx >> 1) + q);
+    const bool k0 = (h & 0xffffu) >= k.thr, k1 = (h >> 16) >= k.thr;
+    v[2 * q] *= k0 ? k.sc : 0.f;
+    v[2 * q + 1] *= k1 ? k.sc : 0.f;
+    bits |= (k0 ? 1u : 0u) << (2 * q) | (k1 ? 1u : 0u) << (2 * q + 1);
+  }
+  return bits;
+}
+// the decisions read back (ea_epilogue.keep) instead of re-hashed
+EA_DEV void drop8k_from(const EpiK& k, uint32_t bits, float (&v)[8]) {
+  if (!k.drop) return;
+#pragma unroll
+  for (int c = 0; c < 8; ++c) v[c] *= ((bits >> c) & 1u) ? k.sc : 0.f;
+}
+
 template <int KIND>
 EA_DEV void epi_eight_pre(const GemmP& p, const EpiK& k, int z, int zb, int zh, int row, int col,
-                          const float (&acc)[8], const float (&bias)[8], bool has_o, const float (&o)[8]) {
+                          const float (&acc)[8], const float (&bias)[8], bool has_o, const float (&o)[8],
+                          uint32_t kbits = 0u) {
   const ea_epilogue& e = p.epi;
   const long cidx = zb * p.sCb + zh * p.sCh + (long)row * p.ldc + col;
   const uint64_t didx = ((uint64_t)z * p.M + row) * (uint64_t)p.N + col;
@@ -394,7 +430,12 @@ EA_DEV void epi_eight_pre(const GemmP& p, const EpiK& k, int z, int zb, int zh, 
   } else if constexpr (KIND == EA_EPI_ACT) {
     if (e.aux) st8(e.aux, (long)row * e.ldaux + col, e.aux_dtype, v);
     act_fwd_n<8>(e.act, v);
-    drop8k(k, didx, v);
+    if (e.keep) {
+      const uint32_t kb = drop8k_bits(k, didx, v);
+      e.keep[(long)row * e.ldkeep + (col >> 3)] = (uint8_t)kb;
+    } else {
+      drop8k(k, didx, v);
+    }
     st8(p.C, cidx, p.c_dtype, v);
   } else if constexpr (KIND == EA_EPI_RESID) {
     drop8k(k, didx, v);
@@ -402,7 +443,8 @@ EA_DEV void epi_eight_pre(const GemmP& p, const EpiK& k, int z, int zb, int zh, 
     for (int c = 0; c < 8; ++c) v[c] = (has_o ? o[c] : 0.f) + e.rscale * v[c];
     st8(p.C, cidx, EA_F32, v);
   } else {
-    drop8k(k, didx, v);
+    if (e.keep) drop8k_from(k, kbits, v);
+    else drop8k(k, didx, v);
     act_bwd_mul_n<8>(e.act, v, o);
     st8(p.C, cidx, p.c_dtype, v);
   }
@@ -770,6 +812,13 @@ EA_DEV void epi_wave(const GemmP& p, const EpiK& k, char* smem, int z, int zb, i
 #pragma unroll
       for (int h0 = 0; h0 < NG8; h0 += HB8) {
         float o[HB8][8];
+        uint32_t kb[HB8];
+        if (KIND == EA_EPI_DACT && p.epi.keep && !slab) {  // keep bytes beside the aux loads
+          const int cb = min(col, p.N - 8) >> 3;
+#pragma unroll
+          for (int it = 0; it < HB8; ++it)
+            kb[it] = p.epi.keep[(long)min(rb + (h0 + it) * 8 + rl, p.M - 1) * p.epi.ldkeep + cb];
+        }
         if (reads) {  // unconditional, clamped, dtype branch outside the batch (see load_unit)
           const int cl = min(col, p.N - 8);
           if (sdt == EA_BF16) {
@@ -793,7 +842,8 @@ EA_DEV void epi_wave(const GemmP& p, const EpiK& k, char* smem, int z, int zb, i
             continue;
           }
           const float v[8] = {f0.x, f0.y, f0.z, f0.w, f1.x, f1.y, f1.z, f1.w};
-          epi_eight_pre<KIND>(p, k, z, zb, zh, row, col, v, bias, reads, o[it]);
+          epi_eight_pre<KIND>(p, k, z, zb, zh, row, col, v, bias, reads, o[it],
+                              KIND == EA_EPI_DACT && p.epi.keep ? kb[it] : 0u);
         }
       }
     }
@@ -842,6 +892,12 @@ EA_DEV long x1p_row(const ea_conv_geo& g, int b, int t2, int f2, int kh, int kw)
   return g.plane[a * 2 + e] + (((long)b * g.nI[a] + t2 + (kh >> 1)) * g.nJ[e] + f2 + (kw >> 1)) * g.C;
 }
 // DGRAD tap q of class (a, e): kh in {0,2} (a = 0) or {1}; kw likewise
+EA_DEV void dgrad_tap2(int a, int e, int q, int& kh, int& kw) {
+  const int nkw = e ? 1 : 2;
+  const int qh = q / nkw, qw = q - qh * nkw;
+  kh = a ? 1 : 2 * qh;
+  kw = e ? 1 : 2 * qw;
+}
 EA_DEV void dgrad_tap(const ea_conv_geo& g, int q, int& kh, int& kw) {
   const int nkw = g.e ? 1 : 2;
   const int qh = q / nkw, qw = q - qh * nkw;
@@ -1345,10 +1401,21 @@ struct PipeT {
   EA_DEV static int wn(int w) { return BT == 256 ? (w & 3) * 64 : (w & 1) * 64; }
 };
 
+// The per-tile values the merged conv2 input-gradient launch (GemmP.ncls) varies by parity
+// class: rows, the class (a, e), and the class's partial-tile / mask-bit bases.  Kept apart
+// from GemmP so that the kernel argument is never copied (its conv geometry is indexed at run
+// time, which would put a copy in scratch memory).
+struct TileOv {
+  int M, a, e;
+  float* w1part;
+  const uint8_t* w1pos;
+};
+EA_DEV TileOv tile_ov(const GemmP& p) { return TileOv{p.M, p.g.a, p.g.e, p.w1part, p.w1pos}; }
+
 // One BT x BT output tile over K range [kbeg, kend) into acc (the wave's sub-tile, PipeT);
 // A / B point at this tile's batch slice.  Returns with every wave done reading smem.
 template <bool AK, bool BKM, int MODE = 0, int BT = 256, int NS = 4>
-EA_DEV void pipe_tile(const GemmP& p, char* smem, const bf16* A, const bf16* B, int m0, int n0, int kbeg,
+EA_DEV void pipe_tile(const GemmP& p, const TileOv& ov, char* smem, const bf16* A, const bf16* B, int m0, int n0, int kbeg,
                       int kend, f32x4 (&acc)[PipeT<BT, NS>::MI][4]) {
   static_assert(MODE == 0 || (MODE == EA_CONV_FWD && AK && BKM) || (MODE == EA_CONV_DGRAD && AK && !BKM) ||
                 (MODE == EA_CONV_WGRAD && !AK && !BKM), "conv gather layouts");
@@ -1377,7 +1444,7 @@ EA_DEV void pipe_tile(const GemmP& p, char* smem, const bf16* A, const bf16* B, 
   const char* bbase = (const char*)(B + (BKM ? (long)kbeg : (long)kbeg * p.ldb));
   uint32_t aoff[ACH], boff[BCH];
 #pragma unroll
-  for (int i = 0; i < ACH; ++i) aoff[i] = src(p.lda, m0, p.M, AK, (i * NW + w) * 64 + lane);
+  for (int i = 0; i < ACH; ++i) aoff[i] = src(p.lda, m0, ov.M, AK, (i * NW + w) * 64 + lane);
 #pragma unroll
   for (int i = 0; i < BCH; ++i) boff[i] = src(p.ldb, n0, p.N, BKM, (i * NW + w) * 64 + lane);
   const long astep = (AK ? BK : (long)BK * p.lda) * 2;  // bytes per slice
@@ -1391,11 +1458,11 @@ EA_DEV void pipe_tile(const GemmP& p, char* smem, const bf16* A, const bf16* B, 
   const int CS = MODE ? p.g.C / BK : 1;        // slices per tap
   int gb[ACH], gt[ACH], gf[ACH], cur[ACH];
   if constexpr (MODE == EA_CONV_FWD || MODE == EA_CONV_DGRAD) {
-    const int n2 = MODE == EA_CONV_FWD ? p.g.T2 : p.g.nI[p.g.a];
-    const int n3 = MODE == EA_CONV_FWD ? p.g.F2 : p.g.nJ[p.g.e];
+    const int n2 = MODE == EA_CONV_FWD ? p.g.T2 : p.g.nI[ov.a];
+    const int n3 = MODE == EA_CONV_FWD ? p.g.F2 : p.g.nJ[ov.e];
 #pragma unroll
     for (int i = 0; i < ACH; ++i) {
-      const int m = min(m0 + ((((i * NW + w) * 64 + lane)) >> 2), p.M - 1);
+      const int m = min(m0 + ((((i * NW + w) * 64 + lane)) >> 2), ov.M - 1);
       const int bt = fdiv(m, n3);
       gf[i] = m - bt * n3;
       gb[i] = fdiv(bt, n2);
@@ -1413,7 +1480,7 @@ EA_DEV void pipe_tile(const GemmP& p, char* smem, const bf16* A, const bf16* B, 
         cur[i] = (int)x1p_row(p.g, gb[i], gt[i], gf[i], kh, kw) + cc;
       } else {
         int kh, kw;
-        dgrad_tap(p.g, q, kh, kw);
+        dgrad_tap2(ov.a, ov.e, q, kh, kw);
         const int t2 = gt[i] - (kh >> 1), f2 = gf[i] - (kw >> 1);  // t1 = 2*t2 + kh
         cur[i] = (t2 >= 0 && t2 < p.g.T2 && f2 >= 0 && f2 < p.g.F2)
                      ? ((gb[i] * p.g.T2 + t2) * p.g.F2 + f2) * p.g.C + cc
@@ -1472,7 +1539,7 @@ EA_DEV void pipe_tile(const GemmP& p, char* smem, const bf16* A, const bf16* B, 
                                          (__attribute__((address_space(3))) void*)(base + (i * NW + w) * 1024), 16, 0, 0);
       if constexpr (MODE == EA_CONV_DGRAD) {  // W2t [9][co][ci]: a slice = 32 co of one tap
         int kh, kw;
-        dgrad_tap(p.g, q, kh, kw);
+        dgrad_tap2(ov.a, ov.e, q, kh, kw);
         bk = (const char*)(B + ((long)(kh * 3 + kw) * p.g.C + c0) * p.g.C);
       }
     } else {
@@ -1569,7 +1636,7 @@ EA_DEV void pipe_tile(const GemmP& p, char* smem, const bf16* A, const bf16* B, 
       const bool km = isa ? AK : BKM;
       const bf16* base = isa ? A : B;
       const long ld = isa ? p.lda : p.ldb;
-      const int MN = isa ? p.M : p.N, mn0 = isa ? m0 : n0;
+      const int MN = isa ? ov.M : p.N, mn0 = isa ? m0 : n0;
       int mn, k;
       if (km) { mn = mn0 + (cc >> 2); k = k0 + (cc & 3) * 8; }
       else    { const int cj = cc & 511; k = k0 + (cj >> 4); mn = mn0 + (cc >> 9) * 128 + (cj & 15) * 8; }
@@ -1623,14 +1690,14 @@ constexpr int W1_SMEM = PipeT<256>::SMEM + 2 * W1_IMG;  // 152 KiB
 // The conv1 input patches of the tile's 256 pixels: loaded into registers before the main
 // loop (w1_load_x; the loads land while it runs) and written to the LDS image after it
 // (w1_stage_x), so their latency is off the tile's critical path.
-EA_DEV void w1_load_x(const GemmP& p, int m0, float (&xv)[5]) {
+EA_DEV void w1_load_x(const GemmP& p, const TileOv& ov, int m0, float (&xv)[5]) {
   const int tid = threadIdx.x;
   const int row = tid >> 1, t0 = (tid & 1) * 5;  // 512 threads: 256 rows x 2 halves of taps 0..9
   const int m = m0 + row;
 #pragma unroll
   for (int u = 0; u < 5; ++u) xv[u] = 0.f;
-  if (m < p.M) {
-    const int a = p.g.a, e = p.g.e, nI = p.g.nI[a], nJ = p.g.nJ[e];
+  if (m < ov.M) {
+    const int a = ov.a, e = ov.e, nI = p.g.nI[a], nJ = p.g.nJ[e];
     const int bi = fdiv(m, nJ), j = m - bi * nJ;
     const int b = fdiv(bi, nI), i = bi - b * nI;
     const float* xp = p.w1x + ((long)b * p.w1T + 2 * (2 * i + a)) * p.w1F + 2 * (2 * j + e);
@@ -1660,7 +1727,7 @@ EA_DEV void w1_stage_x(char* xs, const float (&xv)[5]) {
 }
 
 // one wave's 128 x 64 (rows wm.., channels wn..) share; acc as pipe_tile leaves it
-EA_DEV void w1_epilogue(const GemmP& p, char* smem, int m0, int n0, int wm, int wn, int lane, int w, int tm,
+EA_DEV void w1_epilogue(const GemmP& p, const TileOv& ov, char* smem, int m0, int n0, int wm, int wn, int lane, int w, int tm,
                         const f32x4 (&acc)[8][4]) {
   float* t = (float*)smem + w * 64 * EPI_LDT;  // the wave's 64 x 64 f32 image
   const char* xh = smem + PipeT<256>::SMEM;
@@ -1688,11 +1755,11 @@ EA_DEV void w1_epilogue(const GemmP& p, char* smem, int m0, int n0, int wm, int 
     // ReLU mask (support bits, else aux = conv1 output) and bf16 rounding, in place: lane = 8
     // columns of a row
     const int rb = m0 + wm + ch * 64, col = n0 + wn + lc8;
-    if (p.w1pos) {
+    if (ov.w1pos) {
       uint32_t mb[8];
 #pragma unroll
       for (int it = 0; it < 8; ++it)
-        mb[it] = p.w1pos[(long)min(rb + it * 8 + rl, p.M - 1) * (p.N >> 3) + min(col, p.N - 8) / 8];
+        mb[it] = ov.w1pos[(long)min(rb + it * 8 + rl, ov.M - 1) * (p.N >> 3) + min(col, p.N - 8) / 8];
 #pragma unroll
       for (int it = 0; it < 8; ++it) {
         float* tr = t + (it * 8 + rl) * EPI_LDT + lc8;
@@ -1709,7 +1776,7 @@ EA_DEV void w1_epilogue(const GemmP& p, char* smem, int m0, int n0, int wm, int 
         float o[4][8];
 #pragma unroll
         for (int it = 0; it < 4; ++it)
-          ld8(aux, (long)min(rb + (h0 + it) * 8 + rl, p.M - 1) * p.epi.ldaux + col, EA_BF16, o[it]);
+          ld8(aux, (long)min(rb + (h0 + it) * 8 + rl, ov.M - 1) * p.epi.ldaux + col, EA_BF16, o[it]);
 #pragma unroll
         for (int it = 0; it < 4; ++it) {
           float* tr = t + ((h0 + it) * 8 + rl) * EPI_LDT + lc8;
@@ -1752,7 +1819,7 @@ EA_DEV void w1_epilogue(const GemmP& p, char* smem, int m0, int n0, int wm, int 
   }
   __syncthreads();
   if (w < 4 && lc < 10) {
-    float* prow = p.w1part + (long)tm * 10 * p.N + (long)lc * p.N;
+    float* prow = ov.w1part + (long)tm * 10 * p.N + (long)lc * p.N;
 #pragma unroll
     for (int cb = 0; cb < 4; ++cb)
 #pragma unroll
@@ -1763,21 +1830,43 @@ EA_DEV void w1_epilogue(const GemmP& p, char* smem, int m0, int n0, int wm, int 
   }
 }
 
-template <bool AK, bool BKM, int MODE = 0, int BT = 256, int NS = 4>
-__global__ __launch_bounds__(512, (PipeT<BT, NS>::OCC)) void gemm_pipe(GemmP p) {
+// The four parity classes of the conv2 input gradient as one grid (GemmP.ncls): block -> item
+// so that the tiles_n N-tiles of one M panel run on one XCD (blocks bid and bid + 8 share an
+// XCD) and consecutive panels go round-robin over the XCDs; items are ordered class by class,
+// longest K first, so the long tiles start first and the short ones fill the tail.  Patches the
+// class's geometry into q; returns false for the padding blocks past the last item.
+EA_DEV bool dgrad_class_item(const GemmP& p, TileOv& ov, TileIdx& ti) {
+  const int bid = blockIdx.x, x = bid & 7, sq = bid >> 3, tn_n = p.tiles_n;
+  const int item = ((sq / tn_n) * 8 + x) * tn_n + sq % tn_n;
+  if (item >= p.cls_item0[p.ncls]) return false;
+  int c = 0;
+#pragma unroll
+  for (int k = 1; k < 4; ++k) c += (k < p.ncls && item >= p.cls_item0[k]) ? 1 : 0;
+  const int local = item - p.cls_item0[c];
+  ov.M = p.cls_M[c];
+  ov.a = p.cls_a[c];
+  ov.e = p.cls_e[c];
+  ov.w1part = p.w1part + (long)p.cls_tile0[c] * 10 * p.N;
+  ov.w1pos = p.w1pos + p.cls_pos[c];
+  ti.tm = local / tn_n;
+  ti.tn = local % tn_n;
+  ti.z = 0;
+  ti.sk = p.cls_K[c];  // (the class's K, read by pipe_body for ncls launches)
+  return true;
+}
+
+template <bool AK, bool BKM, int MODE, int BT, int NS>
+EA_DEV void pipe_body(const GemmP& p, const TileOv& ov, const TileIdx& ti, char* smem) {
   using PC = PipeT<BT, NS>;
   constexpr int MI = PC::MI;
-  __shared__ __attribute__((aligned(1024))) char smem[MODE == EA_CONV_DGRAD ? W1_SMEM : PC::SMEM];
-  probe_start(p);
-
-  const TileIdx ti = tile_index(p);
   const int tm = ti.tm, m0 = ti.tm * BT, n0 = ti.tn * BT;
-  const int z = ti.z, sk = ti.sk;
+  const bool cls = MODE == EA_CONV_DGRAD && p.ncls;  // merged parity classes: ti.sk holds K
+  const int z = ti.z, sk = cls ? 0 : ti.sk;
   const int zb = z / p.nh, zh = z % p.nh;
   const bf16* A = (const bf16*)p.A + zb * p.sAb + zh * p.sAh;
   const bf16* B = (const bf16*)p.B + zb * p.sBb + zh * p.sBh;
   const int kbeg = sk * p.kchunk;
-  const int kend = min(p.K, kbeg + p.kchunk);
+  const int kend = cls ? ti.sk : min(p.K, kbeg + p.kchunk);
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int wm = PC::wm(w), wn = PC::wn(w);
   f32x4 acc[MI][4];
@@ -1788,16 +1877,15 @@ __global__ __launch_bounds__(512, (PipeT<BT, NS>::OCC)) void gemm_pipe(GemmP p) 
   diag_stamp(p, 0);
   float w1x[5];
   if constexpr (MODE == EA_CONV_DGRAD) {
-    if (p.w1part) w1_load_x(p, m0, w1x);
+    if (p.w1part) w1_load_x(p, ov, m0, w1x);
   }
-  pipe_tile<AK, BKM, MODE, BT, NS>(p, smem, A, B, m0, n0, kbeg, kend, acc);
+  pipe_tile<AK, BKM, MODE, BT, NS>(p, ov, smem, A, B, m0, n0, kbeg, kend, acc);
   diag_stamp(p, 1);
   if constexpr (MODE == EA_CONV_DGRAD) {
     if (p.w1part) {
       w1_stage_x(smem + PC::SMEM, w1x);  // its own region: read across waves by w1_epilogue
       __syncthreads();
-      w1_epilogue(p, smem, m0, n0, wm, wn, lane, w, tm, acc);
-      probe_end(p);
+      w1_epilogue(p, ov, smem, m0, n0, wm, wn, lane, w, tm, acc);
       return;
     }
   }
@@ -1812,6 +1900,19 @@ __global__ __launch_bounds__(512, (PipeT<BT, NS>::OCC)) void gemm_pipe(GemmP p) 
     __syncthreads();
     diag_stamp(p, 2);
   }
+}
+
+template <bool AK, bool BKM, int MODE = 0, int BT = 256, int NS = 4>
+__global__ __launch_bounds__(512, (PipeT<BT, NS>::OCC)) void gemm_pipe(GemmP p) {
+  using PC = PipeT<BT, NS>;
+  __shared__ __attribute__((aligned(1024))) char smem[MODE == EA_CONV_DGRAD ? W1_SMEM : PC::SMEM];
+  probe_start(p);
+  TileOv ov = tile_ov(p);
+  TileIdx ti;
+  bool run = true;
+  if (MODE == EA_CONV_DGRAD && p.ncls) run = dgrad_class_item(p, ov, ti);
+  else ti = tile_index(p);
+  if (run) pipe_body<AK, BKM, MODE, BT, NS>(p, ov, ti, smem);
   probe_end(p);
 }
 

@@ -44,6 +44,8 @@ def phase_geo(B, T1, F1, T2, F2, C, mode, a=0, e=0, zero=0):
 FUSE_CONV1_WGRAD = os.environ.get("EA_FUSE_CONV1_WGRAD", "1") != "0"
 # ... with conv1's ReLU mask from support bits written by the forward (else the bf16 x1p rows)
 CONV1_POS_BITS = os.environ.get("EA_CONV1_POS_BITS", "1") != "0"
+# ... and the four parity classes in one launch (EA_MERGED_DGRAD=0: one launch per class)
+MERGED_DGRAD = os.environ.get("EA_MERGED_DGRAD", "1") != "0"
 
 
 def _implicit_ok(cd, C):
@@ -265,31 +267,39 @@ class SubsampleFn(torch.autograd.Function):
             tile0 = 0
         else:
             dx1p = empty(P1, C, dtype=cd, device=dev)
-        for a in (0, 1):
-            for e in (0, 1):
-                geo, nI, nJ, rows = phase_geo(B, T1, F1, T2, F2, C, CONV_DGRAD, a=a, e=e, zero=P2 * C)
-                Mc = rows[a * 2 + e]
-                if Mc == 0:
-                    continue
-                ntaps = (1 if a else 2) * (1 if e else 2)
-                o = geo.plane[a * 2 + e] // C
-                aux = x1p[o:o + Mc]
-                epi = ops.make_epi(EPI_DACT, act=ACT_RELU, aux=aux)
-                if fuse and pos1 is None:
-                    lib.ea_gemm_conv_w1(ctypes.byref(geo), Mc, C, ntaps * C, dx2.data_ptr(), C, w2t.data_ptr(), C,
-                                        ctypes.byref(epi), feats.data_ptr(), T, Fin,
-                                        part.data_ptr() + 4 * tile0 * 10 * C, ops.stream())
-                    tile0 += (Mc + 255) // 256
-                elif fuse:
-                    lib.ea_gemm_conv_w1b(ctypes.byref(geo), Mc, C, ntaps * C, dx2.data_ptr(), C, w2t.data_ptr(), C,
-                                         ctypes.byref(epi), feats.data_ptr(), T, Fin,
-                                         part.data_ptr() + 4 * tile0 * 10 * C, pos1.data_ptr() + o * (C // 8),
-                                         ops.stream())
-                    tile0 += (Mc + 255) // 256
-                else:
-                    lib.ea_gemm_conv(ctypes.byref(geo), 1, 0, Mc, C, ntaps * C, dx2.data_ptr(), C, w2t.data_ptr(),
-                                     C, dx1p[o:o + Mc].data_ptr(), ops.dt(dx1p), C, ctypes.byref(epi),
-                                     ws.data_ptr(), ws.numel(), ops.stream())
+        if fuse and pos1 is not None and MERGED_DGRAD:
+            # the four parity classes in one launch, longest K first (ea_gemm_conv_w1b_all)
+            geo, _, _, _ = phase_geo(B, T1, F1, T2, F2, C, CONV_DGRAD, zero=P2 * C)
+            epi = ops.make_epi(EPI_DACT, act=ACT_RELU)
+            lib.ea_gemm_conv_w1b_all(ctypes.byref(geo), C, dx2.data_ptr(), C, w2t.data_ptr(), C, ctypes.byref(epi),
+                                     feats.data_ptr(), T, Fin, part.data_ptr(), pos1.data_ptr(), ops.stream())
+            tile0 = sum((r + 255) // 256 for r in rows_all if r)
+        else:
+            for a in (0, 1):
+                for e in (0, 1):
+                    geo, nI, nJ, rows = phase_geo(B, T1, F1, T2, F2, C, CONV_DGRAD, a=a, e=e, zero=P2 * C)
+                    Mc = rows[a * 2 + e]
+                    if Mc == 0:
+                        continue
+                    ntaps = (1 if a else 2) * (1 if e else 2)
+                    o = geo.plane[a * 2 + e] // C
+                    aux = x1p[o:o + Mc]
+                    epi = ops.make_epi(EPI_DACT, act=ACT_RELU, aux=aux)
+                    if fuse and pos1 is None:
+                        lib.ea_gemm_conv_w1(ctypes.byref(geo), Mc, C, ntaps * C, dx2.data_ptr(), C, w2t.data_ptr(), C,
+                                            ctypes.byref(epi), feats.data_ptr(), T, Fin,
+                                            part.data_ptr() + 4 * tile0 * 10 * C, ops.stream())
+                        tile0 += (Mc + 255) // 256
+                    elif fuse:
+                        lib.ea_gemm_conv_w1b(ctypes.byref(geo), Mc, C, ntaps * C, dx2.data_ptr(), C, w2t.data_ptr(), C,
+                                             ctypes.byref(epi), feats.data_ptr(), T, Fin,
+                                             part.data_ptr() + 4 * tile0 * 10 * C, pos1.data_ptr() + o * (C // 8),
+                                             ops.stream())
+                        tile0 += (Mc + 255) // 256
+                    else:
+                        lib.ea_gemm_conv(ctypes.byref(geo), 1, 0, Mc, C, ntaps * C, dx2.data_ptr(), C, w2t.data_ptr(),
+                                         C, dx1p[o:o + Mc].data_ptr(), ops.dt(dx1p), C, ctypes.byref(epi),
+                                         ws.data_ptr(), ws.numel(), ops.stream())
         if fuse:
             lib.ea_conv1_wgrad_reduce(tile0, C, part.data_ptr(), b.g("conv.0.weight").data_ptr(),
                                       b.g("conv.0.bias").data_ptr(), ops.stream())

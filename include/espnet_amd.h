@@ -46,6 +46,11 @@ typedef struct ea_epilogue {
   long ldaux;
   const float* resid;       /* RESID: f32 [M, ldr]; may alias C */
   long ldr;
+  /* dropout keep bits, one byte per 8 columns (bit c = column 8j + c kept), row stride ldkeep
+   * bytes, or NULL: ACT writes the decisions it draws (bf16 LDS-DMA path, N % 8 == 0, no
+   * split-K), DACT reads them instead of re-hashing the same stream */
+  unsigned char* keep;
+  long ldkeep;
 } ea_epilogue;
 
 /* Batched GEMM on MFMA (bf16: v_mfma_f32_16x16x32_bf16, f32: v_mfma_f32_16x16x4_f32 —
@@ -119,6 +124,14 @@ int ea_gemm_conv_w1(const ea_conv_geo* geo, int M, int N, int K, const void* A, 
 int ea_gemm_conv_w1b(const ea_conv_geo* geo, int M, int N, int K, const void* A, long lda, const void* B,
                      long ldb, const ea_epilogue* epi, const float* x, int T, int Fin, float* part,
                      const unsigned char* pos, void* stream);
+/* The four parity classes (a, e) = (0,0), (0,1), (1,0), (1,1) of ea_gemm_conv_w1b in one
+ * launch (geo: EA_CONV_DGRAD with nI / nJ / plane; a, e ignored): class c has
+ * M_c = B*nI[a]*nJ[e] rows and K_c = (a ? 1 : 2)*(e ? 1 : 2)*C, its mask bits start at row
+ * plane[c]/C of pos, and its ceil(M_c/256) partial tiles follow the previous classes' in part —
+ * the same results as the four ea_gemm_conv_w1b calls in that order, bit for bit. */
+int ea_gemm_conv_w1b_all(const ea_conv_geo* geo, int N, const void* A, long lda, const void* B, long ldb,
+                         const ea_epilogue* epi, const float* x, int T, int Fin, float* part,
+                         const unsigned char* pos, void* stream);
 int ea_conv1_wgrad_reduce(int ntiles, int C, const float* part, float* dw, float* dbias, void* stream);
 
 /* Select the bf16 GEMM main loop: 2 = LDS-DMA (global_load_lds) 2-stage ring (default),

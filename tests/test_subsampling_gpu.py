@@ -108,3 +108,23 @@ def test_fused_conv1_wgrad_matches_unfused(C, B, T):
             assert _rel(g1[k], g0[k]) < 2e-4, (k, _rel(g1[k], g0[k]))
         else:
             assert torch.equal(g0[k], g1[k]), k
+
+
+@pytest.mark.parametrize("C,B,T", [(64, 3, 61), (512, 2, 131), (256, 4, 300), (512, 32, 1000)])
+def test_merged_dgrad_classes_bit_identical(C, B, T):
+    """ea_gemm_conv_w1b_all: the four parity classes of the conv2 input gradient (with the fused
+    conv1 weight gradient) in ONE launch, longest K first, equal bit for bit to the four
+    per-class launches — same tiles, same arithmetic, same partial-tile layout; the C3 shape
+    (B=32, T=1000) included."""
+    from espnet_amd.layers import subsampling as S
+    merged = S.MERGED_DGRAD
+    try:
+        S.MERGED_DGRAD = False
+        y0, g0 = _run(C, B, T, True, torch.bfloat16)
+        S.MERGED_DGRAD = True
+        y1, g1 = _run(C, B, T, True, torch.bfloat16)
+    finally:
+        S.MERGED_DGRAD = merged
+    assert torch.equal(y0, y1)
+    for k in g0:
+        assert torch.equal(g0[k], g1[k]), k
