@@ -361,9 +361,6 @@ static int gemm_impl(int dtype, int a_kmajor, int b_kmajor, int M, int N, int K,
   }
   p.splitk = splitk;
   p.kchunk = kchunk;
-  // keep bits are written only by the 8-column vector epilogue of the bf16 LDS-DMA kernels
-  if (epi->keep && epi->drop_p > 0.f && epi->kind == EA_EPI_ACT && (!p.lds || !p.vec8 || splitk > 1))
-    return EA_ERR_BAD_ARG;
   static const bool trace = std::getenv("EA_GEMM_TRACE") != nullptr;  // shape census (diagnostics)
   if (trace)
     std::fprintf(stderr, "[ea_gemm] M=%d N=%d K=%d ak=%d bk=%d nz=%d tile=%dx%d%s splitk=%d epi=%d geo=%d lds=%d\n", M,

@@ -207,10 +207,7 @@ EA_DEV void epi_one(const GemmP& p, int z, int zb, int zh, int row, int col, flo
     const float r = e.resid ? e.resid[(long)row * e.ldr + col] : 0.f;
     ((float*)p.C)[cidx] = r + e.rscale * v;
   } else {  // EA_EPI_DACT
-    if (e.drop_p > 0.f && e.keep)
-      v *= ((e.keep[(long)row * e.ldkeep + (col >> 3)] >> (col & 7)) & 1u) ? 1.f / (1.f - e.drop_p) : 0.f;
-    else if (e.drop_p > 0.f)
-      v *= drop_scale(seed, didx, e.drop_p);
+    if (e.drop_p > 0.f) v *= drop_scale(seed, didx, e.drop_p);
     v *= act_bwd(e.act, load_as_f(e.aux, (long)row * e.ldaux + col, e.aux_dtype));
     store_from_f(p.C, cidx, p.c_dtype, v);
   }
@@ -341,13 +338,7 @@ EA_DEV void epi_four_pre(const GemmP& p, const EpiK& k, int z, int zb, int zh, i
     for (int c = 0; c < 4; ++c) v[c] = (has_o ? o[c] : 0.f) + e.rscale * v[c];
     st4(p.C, cidx, EA_F32, v);
   } else {
-    if (k.drop && e.keep) {
-      const uint32_t kb = e.keep[(long)row * e.ldkeep + (col >> 3)] >> (col & 7);
-#pragma unroll
-      for (int c = 0; c < 4; ++c) v[c] *= ((kb >> c) & 1u) ? k.sc : 0.f;
-    } else {
-      drop4k(k, didx, v);
-    }
+    drop4k(k, didx, v);
     act_bwd_mul_n<4>(e.act, v, o);
     st4(p.C, cidx, p.c_dtype, v);
   }
@@ -387,31 +378,9 @@ EA_DEV void drop8k(const EpiK& k, uint64_t idx, float (&v)[8]) {  // idx even
     v[2 * q + 1] *= (h >> 16) >= k.thr ? k.sc : 0.f;
   }
 }
-// drop8k that also returns the 8 decisions (bit c = element idx + c kept; all set without dropout)
-EA_DEV uint32_t drop8k_bits(const EpiK& k, uint64_t idx, float (&v)[8]) {  // idx even
-  if (!k.drop) return 0xffu;
-  uint32_t bits = 0u;
-#pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    const uint32_t h = ea_pair_hash(k.key, (idx >> 1) + q);
-    const bool k0 = (h & 0xffffu) >= k.thr, k1 = (h >> 16) >= k.thr;
-    v[2 * q] *= k0 ? k.sc : 0.f;
-    v[2 * q + 1] *= k1 ? k.sc : 0.f;
-    bits |= (k0 ? 1u : 0u) << (2 * q) | (k1 ? 1u : 0u) << (2 * q + 1);
-  }
-  return bits;
-}
-// the decisions read back (ea_epilogue.keep) instead of re-hashed
-EA_DEV void drop8k_from(const EpiK& k, uint32_t bits, float (&v)[8]) {
-  if (!k.drop) return;
-#pragma unroll
-  for (int c = 0; c < 8; ++c) v[c] *= ((bits >> c) & 1u) ? k.sc : 0.f;
-}
-
 template <int KIND>
 EA_DEV void epi_eight_pre(const GemmP& p, const EpiK& k, int z, int zb, int zh, int row, int col,
-                          const float (&acc)[8], const float (&bias)[8], bool has_o, const float (&o)[8],
-                          uint32_t kbits = 0u) {
+                          const float (&acc)[8], const float (&bias)[8], bool has_o, const float (&o)[8]) {
   const ea_epilogue& e = p.epi;
   const long cidx = zb * p.sCb + zh * p.sCh + (long)row * p.ldc + col;
   const uint64_t didx = ((uint64_t)z * p.M + row) * (uint64_t)p.N + col;
@@ -430,12 +399,7 @@ EA_DEV void epi_eight_pre(const GemmP& p, const EpiK& k, int z, int zb, int zh, 
   } else if constexpr (KIND == EA_EPI_ACT) {
     if (e.aux) st8(e.aux, (long)row * e.ldaux + col, e.aux_dtype, v);
     act_fwd_n<8>(e.act, v);
-    if (e.keep) {
-      const uint32_t kb = drop8k_bits(k, didx, v);
-      e.keep[(long)row * e.ldkeep + (col >> 3)] = (uint8_t)kb;
-    } else {
-      drop8k(k, didx, v);
-    }
+    drop8k(k, didx, v);
     st8(p.C, cidx, p.c_dtype, v);
   } else if constexpr (KIND == EA_EPI_RESID) {
     drop8k(k, didx, v);
@@ -443,8 +407,7 @@ EA_DEV void epi_eight_pre(const GemmP& p, const EpiK& k, int z, int zb, int zh, 
     for (int c = 0; c < 8; ++c) v[c] = (has_o ? o[c] : 0.f) + e.rscale * v[c];
     st8(p.C, cidx, EA_F32, v);
   } else {
-    if (e.keep) drop8k_from(k, kbits, v);
-    else drop8k(k, didx, v);
+    drop8k(k, didx, v);
     act_bwd_mul_n<8>(e.act, v, o);
     st8(p.C, cidx, p.c_dtype, v);
   }
@@ -812,13 +775,6 @@ EA_DEV void epi_wave(const GemmP& p, const EpiK& k, char* smem, int z, int zb, i
 #pragma unroll
       for (int h0 = 0; h0 < NG8; h0 += HB8) {
         float o[HB8][8];
-        uint32_t kb[HB8];
-        if (KIND == EA_EPI_DACT && p.epi.keep && !slab) {  // keep bytes beside the aux loads
-          const int cb = min(col, p.N - 8) >> 3;
-#pragma unroll
-          for (int it = 0; it < HB8; ++it)
-            kb[it] = p.epi.keep[(long)min(rb + (h0 + it) * 8 + rl, p.M - 1) * p.epi.ldkeep + cb];
-        }
         if (reads) {  // unconditional, clamped, dtype branch outside the batch (see load_unit)
           const int cl = min(col, p.N - 8);
           if (sdt == EA_BF16) {
@@ -842,8 +798,7 @@ EA_DEV void epi_wave(const GemmP& p, const EpiK& k, char* smem, int z, int zb, i
             continue;
           }
           const float v[8] = {f0.x, f0.y, f0.z, f0.w, f1.x, f1.y, f1.z, f1.w};
-          epi_eight_pre<KIND>(p, k, z, zb, zh, row, col, v, bias, reads, o[it],
-                              KIND == EA_EPI_DACT && p.epi.keep ? kb[it] : 0u);
+          epi_eight_pre<KIND>(p, k, z, zb, zh, row, col, v, bias, reads, o[it]);
         }
       }
     }

@@ -37,7 +37,6 @@ class Epilogue(ctypes.Structure):
         ("bias", ctypes.c_void_p),
         ("aux", ctypes.c_void_p), ("aux_dtype", ctypes.c_int), ("ldaux", ctypes.c_long),
         ("resid", ctypes.c_void_p), ("ldr", ctypes.c_long),
-        ("keep", ctypes.c_void_p), ("ldkeep", ctypes.c_long),
     ]
 
 

@@ -260,7 +260,7 @@ _SPLITK_WS = 1 << 25  # 32M floats
 
 
 def make_epi(kind=EPI_STORE, *, alpha=1.0, beta=0.0, bias=None, post_scale=1.0, act=ACT_NONE,
-             aux=None, resid=None, rscale=1.0, drop_p=0.0, seed=0, keep=None):
+             aux=None, resid=None, rscale=1.0, drop_p=0.0, seed=0):
     e = Epilogue()
     e.kind = kind
     e.act = act
@@ -278,9 +278,6 @@ def make_epi(kind=EPI_STORE, *, alpha=1.0, beta=0.0, bias=None, post_scale=1.0, 
     if resid is not None:
         e.resid = resid.data_ptr()
         e.ldr = resid.stride(-2)
-    if keep is not None:  # uint8 (rows, N/8): ACT writes its dropout decisions, DACT reads them
-        e.keep = keep.data_ptr()
-        e.ldkeep = keep.stride(0)
     return e
 
 

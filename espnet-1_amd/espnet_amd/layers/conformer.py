@@ -36,9 +36,6 @@ GLU_IN_CONV = os.environ.get("EA_GLU_IN_CONV", "1") != "0"
 # (ea_dwconv_fwd_glu_stats + ea_batchnorm_fwd_parts; EA_BN_STATS_IN_CONV=0: a statistics pass
 # over y; measured 17.83-17.88 -> 17.73-17.76 ms per C3 step)
 BN_STATS_IN_CONV = os.environ.get("EA_BN_STATS_IN_CONV", "1") != "0"
-# the FFN activation dropout's decisions written as bits by the w_1 forward epilogue and read by
-# the w_2 input-gradient epilogue (EA_KEEP_BITS=0: the backward re-hashes the same stream)
-KEEP_BITS = os.environ.get("EA_KEEP_BITS", "1") != "0"
 
 
 def _glu_in_conv(K, g2, d):
@@ -153,18 +150,14 @@ def _ffn_fwd(L, b, x_in, pre, ln_name, p, seed_in, seed_out):
     xn, mu, rs = ln_fwd(x_in, b, ln_name, cd)
     h = empty(N, Fh, dtype=cd, device=x_in.device)
     a = empty(N, Fh, dtype=cd, device=x_in.device)
-    # the activation dropout's decisions kept as bits (1/16 of h's bytes) for the backward's
-    # Swish-derivative epilogue, which then reads them instead of re-hashing (bf16 path)
-    keep = (torch.empty(N, Fh // 8, dtype=torch.uint8, device=x_in.device)
-            if KEEP_BITS and p > 0 and cd == torch.bfloat16 and Fh % 8 == 0 else None)
     ops.linear(xn, b.w(pre + ".w_1.weight"), a,
                epi=ops.make_epi(EPI_ACT, bias=b.f(pre + ".w_1.bias"), act=ACT_SWISH, aux=h,
-                                drop_p=p, seed=seed_in, keep=keep))
+                                drop_p=p, seed=seed_in))
     x_out = empty(N, d, device=x_in.device)
     ops.linear(a, b.w(pre + ".w_2.weight"), x_out,
                epi=ops.make_epi(EPI_RESID, bias=b.f(pre + ".w_2.bias"), resid=x_in,
                                 rscale=L.ff_scale, drop_p=p, seed=seed_out))
-    return x_out, (xn, mu, rs, h, a, keep)
+    return x_out, (xn, mu, rs, h, a)
 
 
 def _ffn_bwd(L, b, dx, x_in, saved, pre, ln_name, p, seed_in, seed_out, dv_in=None, next_drop=None):
@@ -172,14 +165,14 @@ def _ffn_bwd(L, b, dx, x_in, saved, pre, ln_name, p, seed_in, seed_out, dv_in=No
     site's dv when already written; next_drop: the following site's (dv, scale, p, seed) for the
     LayerNorm backward to write."""
     cd = b.cd
-    xn, mu, rs, h, a, keep = saved
+    xn, mu, rs, h, a = saved
     N, d = dx.shape
     dv = site_dv(dx, dv_in, b.g(pre + ".w_2.bias"), L.ff_scale, p, seed_out, cd)
     with ops.wgrad(dv, a):
         ops.linear_dw(dv, a, b.g(pre + ".w_2.weight"), accumulate=True)
     dh = empty(*h.shape, dtype=cd, device=dx.device)
     ops.linear_dx(dv, b.w(pre + ".w_2.weight"), dh,
-                  epi=ops.make_epi(EPI_DACT, act=ACT_SWISH, aux=h, drop_p=p, seed=seed_in, keep=keep))
+                  epi=ops.make_epi(EPI_DACT, act=ACT_SWISH, aux=h, drop_p=p, seed=seed_in))
     with ops.wgrad(dh, xn):
         ops.colsum(dh, b.g(pre + ".w_1.bias"))
         ops.linear_dw(dh, xn, b.g(pre + ".w_1.weight"), accumulate=True)

@@ -46,11 +46,6 @@ typedef struct ea_epilogue {
   long ldaux;
   const float* resid;       /* RESID: f32 [M, ldr]; may alias C */
   long ldr;
-  /* dropout keep bits, one byte per 8 columns (bit c = column 8j + c kept), row stride ldkeep
-   * bytes, or NULL: ACT writes the decisions it draws (bf16 LDS-DMA path, N % 8 == 0, no
-   * split-K), DACT reads them instead of re-hashing the same stream */
-  unsigned char* keep;
-  long ldkeep;
 } ea_epilogue;
 
 /* Batched GEMM on MFMA (bf16: v_mfma_f32_16x16x32_bf16, f32: v_mfma_f32_16x16x4_f32 —

@@ -561,40 +561,3 @@ def test_gemm_ln_vs_fp64(MNK):
     torch.testing.assert_close(C[:, :N], C0, atol=2e-2, rtol=1e-2)
 
 
-
-
-@pytest.mark.parametrize("MN", [(7968, 2048), (300, 264)])
-def test_dropout_keep_bits_act_dact(MN):
-    """ea_epilogue.keep: the ACT epilogue writes its dropout decisions as bits (one byte per 8
-    columns) and the DACT epilogue that reads them produces exactly what re-hashing the same
-    stream gives — the FFN w_1 forward / w_2 input-gradient pair at the C3 shape and an edge
-    shape (partial tiles in M and N)."""
-    ops, L = _ops()
-    M, N = MN
-    K = 512
-    g = torch.Generator().manual_seed(M + N)
-    x = mk((M, K), torch.bfloat16, g)
-    w1 = mk((N, K), torch.bfloat16, g, 0.05)
-    b1 = mk((N,), torch.float32, g)
-    h = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
-    a0 = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
-    a1 = torch.empty_like(a0)
-    keep = torch.full((M, N // 8), 0x5A, device="cuda", dtype=torch.uint8)
-    ops.gemm(x, w1, a0, M=M, N=N, K=K, a_kmajor=1, b_kmajor=1, lda=K, ldb=K, ldc=N,
-             epi=ops.make_epi(L.EPI_ACT, bias=b1, act=L.ACT_SWISH, aux=h, drop_p=0.1, seed=11))
-    ops.gemm(x, w1, a1, M=M, N=N, K=K, a_kmajor=1, b_kmajor=1, lda=K, ldb=K, ldc=N,
-             epi=ops.make_epi(L.EPI_ACT, bias=b1, act=L.ACT_SWISH, aux=h, drop_p=0.1, seed=11, keep=keep))
-    assert torch.equal(a0, a1)
-    bits = torch.stack([(keep >> c) & 1 for c in range(8)], -1).reshape(M, N).bool()
-    frac = 1.0 - bits.float().mean().item()
-    assert abs(frac - 0.1) < 0.01, frac  # the drop rate
-    assert not bool((a1[~bits] != 0).any())  # dropped elements are zero
-    dy = mk((M, K), torch.bfloat16, g)
-    w2 = mk((K, N), torch.bfloat16, g, 0.05)
-    d0 = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
-    d1 = torch.empty_like(d0)
-    ops.gemm(dy, w2, d0, M=M, N=N, K=K, a_kmajor=1, b_kmajor=0, lda=K, ldb=N, ldc=N,
-             epi=ops.make_epi(L.EPI_DACT, act=L.ACT_SWISH, aux=h, drop_p=0.1, seed=11))
-    ops.gemm(dy, w2, d1, M=M, N=N, K=K, a_kmajor=1, b_kmajor=0, lda=K, ldb=N, ldc=N,
-             epi=ops.make_epi(L.EPI_DACT, act=L.ACT_SWISH, aux=h, drop_p=0.1, seed=11, keep=keep))
-    assert torch.equal(d0, d1)
