@@ -119,6 +119,12 @@ __global__ void scale_inplace_kernel(long n, float* __restrict__ x, const float*
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) x[i] *= k;
 }
 
+__global__ void axpy_dev_kernel(long n, const float* __restrict__ x, float* __restrict__ y, const float* __restrict__ s,
+                                float c) {
+  const float k = s[0] * c;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) y[i] += k * x[i];
+}
+
 // out = wa*a + wb*b (device scalars; b may be null)
 __global__ void axpby_scalar_kernel(const float* a, float wa, const float* b, float wb, float* out) {
   out[0] = wa * a[0] + (b ? wb * b[0] : 0.f);
@@ -192,6 +198,15 @@ extern "C" int ea_cast_f32_bf16(long n, const float* x, void* y, void* stream) {
 extern "C" int ea_scale_by_scalar(long n, float* x, const float* s, float c, void* stream) {
   EA_ENTRY();
   hipLaunchKernelGGL(scale_inplace_kernel, dim3(ea_grid_cap(ea_cdiv(n, 256), 4096)), dim3(256), 0, (hipStream_t)stream, n, x, s, c);
+  EA_LAUNCH_CHECK();
+  return 0;
+}
+
+extern "C" int ea_axpy_dev(long n, const float* x, float* y, const float* s, float c, void* stream) {
+  EA_ENTRY();
+  EA_CHECK_ARG(n >= 0 && (n == 0 || (x && y && s)));
+  if (n == 0) return 0;
+  hipLaunchKernelGGL(axpy_dev_kernel, dim3(ea_grid_cap(ea_cdiv(n, 256), 4096)), dim3(256), 0, (hipStream_t)stream, n, x, y, s, c);
   EA_LAUNCH_CHECK();
   return 0;
 }

@@ -21,6 +21,18 @@ def _g(t):
 
 # EA_CTC_HEAD_AUX=0: only the lattice on the auxiliary stream (A/B switch)
 CTC_HEAD_AUX = os.environ.get("EA_CTC_HEAD_AUX", "1") != "0"
+# the CTC head's backward computed in the forward, unscaled, on the auxiliary stream beside the
+# latency-bound attention-decoder forward (most CUs idle there); the backward then only scales
+# it by the upstream gradient (EA_CTC_BWD_IN_FWD=0: the whole head backward after the decoder's)
+CTC_BWD_IN_FWD = os.environ.get("EA_CTC_BWD_IN_FWD", "1") != "0"
+_ONE = {}
+
+
+def _one(dev):
+    t = _ONE.get(dev)
+    if t is None:
+        t = _ONE[dev] = torch.ones((), dtype=torch.float32, device=dev)
+    return t
 
 
 class CTCFn(torch.autograd.Function):
@@ -50,6 +62,7 @@ class CTCFn(torch.autograd.Function):
 
         if not CTC_HEAD_AUX:
             head()
+        pre = CTC_BWD_IN_FWD and ctx.needs_input_grad[0]
         with (ops.aux(hs, h, logits, hlens, ys, ylens, lse, alpha, beta, nll, loss_utt, loss) if ctc._overlap
               else contextlib.nullcontext()):
             if CTC_HEAD_AUX:
@@ -57,10 +70,36 @@ class CTCFn(torch.autograd.Function):
             lib.ea_ctc_loss_fwd(B, T, V, logits.data_ptr(), V, hlens.data_ptr(), ys.data_ptr(), ys.stride(0),
                                 ylens.data_ptr(), Lmax, lse.data_ptr(), alpha.data_ptr(), beta.data_ptr(),
                                 nll.data_ptr(), loss_utt.data_ptr(), loss.data_ptr(), ops.stream())
+            if pre:
+                # d loss_ctc / d logits for an upstream gradient of 1 (ctc.py:72-97 backward),
+                # and through ctc_lo: dh (+ the head's dropout), dW, db — all linear in the
+                # upstream gradient, which the backward multiplies in (ea_scale_by_scalar,
+                # ea_axpy_dev).  The logits / lattice buffers are released here, not kept.
+                dl = empty(N, V, dtype=cd, device=dev)
+                lib.ea_ctc_loss_bwd(B, T, V, logits.data_ptr(), V, hlens.data_ptr(), ys.data_ptr(), ys.stride(0),
+                                    ylens.data_ptr(), Lmax, lse.data_ptr(), alpha.data_ptr(), beta.data_ptr(),
+                                    nll.data_ptr(), _one(dev).data_ptr(), 1.0 / B, dl.data_ptr(), ops.dt(dl), V,
+                                    ops.stream())
+                dW = empty(V, d, device=dev)
+                db = empty(V, device=dev)
+                ops.linear_dw(dl, h, dW, accumulate=False)
+                ops.colsum(dl, db, accumulate=False, defer=False)
+                dh = empty(N, d, device=dev)
+                ops.linear_dx(dl, b.w("ctc_lo.weight"), dh)
+                if ctc.dropout_rate > 0:
+                    ops.scale_dropout(dh, dh, p=ctc.dropout_rate, seed=ctc._seed)
+                del dl
         ctx.ctc = ctc
         ctx.meta = (B, T, V, Lmax, d)
-        ctx.save = (h, logits, lse, alpha, beta, nll, hlens, ys, ylens)
-        ctx.logits = logits
+        ctx.pre = pre
+        if pre:
+            main = torch.cuda.current_stream()
+            for t in (dh, dW, db):
+                t.record_stream(main)  # read by the backward on the main stream
+            ctx.save = (dh, dW, db)
+        else:
+            ctx.save = (h, logits, lse, alpha, beta, nll, hlens, ys, ylens)
+
         return loss
 
     @staticmethod
@@ -69,6 +108,17 @@ class CTCFn(torch.autograd.Function):
         b = ctc._b
         cd = b.cd
         B, T, V, Lmax, d = ctx.meta
+        if ctx.pre:  # the head's gradients were computed in the forward for gl = 1: scale them
+            dh, dW, db = ctx.save
+            ctx.save = None
+            gl = _g(gl)
+            ops.take_aux_fork()
+            st = ops.stream()
+            lib.ea_scale_by_scalar(dh.numel(), dh.data_ptr(), gl.data_ptr(), 1.0, st)
+            lib.ea_axpy_dev(dW.numel(), dW.data_ptr(), b.g("ctc_lo.weight").data_ptr(), gl.data_ptr(), 1.0, st)
+            lib.ea_axpy_dev(V, db.data_ptr(), b.g("ctc_lo.bias").data_ptr(), gl.data_ptr(), 1.0, st)
+            ops.grad_ready(b)
+            return dh.view(B, T, d), None, None, None, None, None
         h, logits, lse, alpha, beta, nll, hlens, ys, ylens = ctx.save
         ctx.save = None
         N = B * T

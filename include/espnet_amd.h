@@ -623,6 +623,9 @@ int ea_relu_f32_inplace(long n, float* x, void* stream);
 int ea_transpose_bf16_grouped(int ntiles, const int* tiles, const void* probs, const void* src, void* stream);
 /* x *= s[0]*c (device scalar) */
 int ea_scale_by_scalar(long n, float* x, const float* s, float c, void* stream);
+/* y += s[0]*c * x (f32, s a device scalar): a gradient computed unscaled ahead of the backward,
+ * accumulated with the upstream gradient once it exists (the CTC head, layers/losses.py) */
+int ea_axpy_dev(long n, const float* x, float* y, const float* s, float c, void* stream);
 /* out[0] = wa*a[0] + wb*b[0] (b may be NULL) — loss = w*ctc + (1-w)*att, espnet_model.py:325 */
 int ea_axpby_scalar(const float* a, float wa, const float* b, float wb, float* out, void* stream);
 

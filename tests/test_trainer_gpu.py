@@ -240,3 +240,29 @@ def test_captured_specaug_steps_equal_eager(equal_lengths):
     assert torch.equal(rng_eager, torch.get_rng_state())  # the same host draws, in the same order
     for (k, p1), p2 in zip(m1.state_dict().items(), m2.state_dict().values()):
         assert torch.equal(p1, p2), k
+
+
+@pytest.mark.parametrize("amp", [False, True])
+def test_ctc_backward_in_forward_matches_after(amp):
+    """layers/losses.py CTC_BWD_IN_FWD: the CTC head's backward computed in the forward for an
+    upstream gradient of 1 and scaled by the real one in the backward equals the head backward
+    run after the decoder's (the same arithmetic up to where the scale enters: fp32 to 1e-6,
+    bf16 to its rounding of the unscaled gradient), over two training steps."""
+    from test_dp_capture_gpu import _batches, _setup
+    from espnet_amd.layers import losses as Lo
+    from espnet_amd.train.trainer import Trainer
+    out = {}
+    saved = Lo.CTC_BWD_IN_FWD
+    try:
+        for pre in (False, True):
+            Lo.CTC_BWD_IN_FWD = pre
+            d, m, opt, sched = _setup(amp=amp, dropout=0.1)
+            losses = [float(Trainer.train_one_step(m, b, opt, sched, grad_clip=5.0)[0]) for b in _batches(d, 2)]
+            torch.cuda.synchronize()
+            out[pre] = (losses, m.arena.data.cpu().clone())
+    finally:
+        Lo.CTC_BWD_IN_FWD = saved
+    np.testing.assert_allclose(out[True][0], out[False][0], rtol=1e-6 if not amp else 1e-4)
+    w0, w1 = out[False][1].double(), out[True][1].double()
+    tol = 1e-5 if not amp else 2e-3  # (two Adam steps amplify fp32 rounding: 1.6e-6 measured)
+    assert float((w1 - w0).norm() / w0.norm()) < tol
