@@ -75,8 +75,8 @@ __host__ __device__ inline uint32_t ea_mix32(uint32_t x) {
 __host__ __device__ inline uint32_t ea_seed_key(uint64_t seed) {
   return ea_mix32((uint32_t)seed ^ ea_mix32((uint32_t)(seed >> 32) ^ 0x5bd1e995U));
 }
-EA_DEV uint32_t ea_pair_hash(uint32_t key, uint64_t pair) {
-  uint32_t a = (uint32_t)pair + key + __umul24((uint32_t)(pair >> 32), 0x9e3779u);
+// the six mixing rounds on a = low word of the pair + key (+ the high word's term)
+EA_DEV uint32_t ea_pair_mix(uint32_t a) {
   a = (a + 0x7ed55d16u) + (a << 12);
   a = (a ^ 0xc761c23cu) ^ (a >> 19);
   a = (a + 0x165667b1u) + (a << 5);
@@ -84,6 +84,9 @@ EA_DEV uint32_t ea_pair_hash(uint32_t key, uint64_t pair) {
   a = (a + 0xfd7046c5u) + (a << 3);
   a = (a ^ 0xb55a4f09u) ^ (a >> 16);
   return a;
+}
+EA_DEV uint32_t ea_pair_hash(uint32_t key, uint64_t pair) {
+  return ea_pair_mix((uint32_t)pair + key + __umul24((uint32_t)(pair >> 32), 0x9e3779u));
 }
 // Per-step salt of every dropout stream (ea_set_rng_salt): launchers pass the process-wide
 // device pointer ea_g_rng_salt to their kernels, which mix *salt into the site seed.  The

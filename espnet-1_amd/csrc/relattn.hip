@@ -846,6 +846,38 @@ EA_DEV void km_dma8(char* img, int ir, const bf16* src, long ld, int r0, int rli
                                    (__attribute__((address_space(3))) void*)(img + ir * 128), 16, 0, 0);
 }
 
+// 16-lane max / sum of four values with the DPP modifier on the VALU op itself (no separate
+// v_mov_b32_dpp, no NaN canonicalisation: the operands are never NaN).  Same pairings in the
+// same order as max16 / sum16; the rows are interleaved so that every DPP read comes at least
+// two instructions after its operand's write (the leading s_nop covers the caller's write).
+#define EA_DPP4(OP, CTRL)                                                   \
+  OP " %0, %0, %0 " CTRL " row_mask:0xf bank_mask:0xf\n\t" OP " %1, %1, %1 " CTRL \
+  " row_mask:0xf bank_mask:0xf\n\t" OP " %2, %2, %2 " CTRL " row_mask:0xf bank_mask:0xf\n\t" OP \
+  " %3, %3, %3 " CTRL " row_mask:0xf bank_mask:0xf\n\t"
+EA_DEV void max16x4(float (&v)[4]) {
+  asm("s_nop 1\n\t" EA_DPP4("v_max_f32_dpp", "quad_perm:[1,0,3,2]") EA_DPP4("v_max_f32_dpp", "quad_perm:[2,3,0,1]")
+          EA_DPP4("v_max_f32_dpp", "row_half_mirror") EA_DPP4("v_max_f32_dpp", "row_mirror")
+      : "+v"(v[0]), "+v"(v[1]), "+v"(v[2]), "+v"(v[3]));
+}
+EA_DEV void sum16x4(float (&v)[4]) {
+  asm("s_nop 1\n\t" EA_DPP4("v_add_f32_dpp", "quad_perm:[1,0,3,2]") EA_DPP4("v_add_f32_dpp", "quad_perm:[2,3,0,1]")
+          EA_DPP4("v_add_f32_dpp", "row_half_mirror") EA_DPP4("v_add_f32_dpp", "row_mirror")
+      : "+v"(v[0]), "+v"(v[1]), "+v"(v[2]), "+v"(v[3]));
+}
+#undef EA_DPP4
+
+// LDS-DMA of the 8 km-image rows [ir, ir+8) at image byte `dst` (ir % 8 == 0) from the rows
+// r0 + (lane >> 3) of `src` clamped into [0, rlim), 32-bit byte offsets (the caller checked that
+// rlim rows of ldb bytes fit): one instruction per wave, lane L fills 16-B slot L & 7 of row
+// ir + (L >> 3) with logical chunk (L & 7) ^ km_swz(ir + (L >> 3)).  `chx` = the lane's
+// (L & 7) ^ ((L >> 4) & 3) (ir's own swizzle bit, (ir >> 1) & 4, is applied here).
+EA_DEV void km_dma8u(char* dst, int ir, const char* src, uint32_t ldb, int r0, int rlim, int chx, int lane) {
+  const int r = min(max(r0 + (lane >> 3), 0), rlim - 1);
+  const uint32_t off = __umul24((uint32_t)r, ldb) + ((uint32_t)(chx ^ ((ir >> 1) & 4)) << 4);
+  __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)(src + off),
+                                   (__attribute__((address_space(3))) void*)dst, 16, 0, 0);
+}
+
 // MM: dropout keep decisions — 0 none (p = 0), 1 the forward's bit mask, 2 the counter hash
 template <bool REL, int MM>
 __global__ __launch_bounds__(256, 2) void attn_bwdq2_kernel(AttnP a) {
@@ -855,7 +887,8 @@ __global__ __launch_bounds__(256, 2) void attn_bwdq2_kernel(AttnP a) {
   const int z = blockIdx.x / nqb, qb = blockIdx.x % nqb;
   const int b = z / a.H, h = z % a.H;
   const int i0 = qb * QB;
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: ring / image offsets stay scalar
   const int g = lane >> 4, lc = lane & 15;
   const int kl = a.klen ? (int)min((long long)a.T2, a.klen[b]) : a.T2;
   const uint64_t seed = a.p > 0.f ? ea_salted(a.seed, a.salt) : 0;
@@ -868,26 +901,34 @@ __global__ __launch_bounds__(256, 2) void attn_bwdq2_kernel(AttnP a) {
   const int nch = (kend + KC - 1) / KC;
   const int rlimP = 2 * a.T1 - 1;
   const int rb0 = a.T1 - 1 - (i0 + QB - 1);  // chunk 0's first positional row (ring position 0)
-  const bf16* kh_ = a.k + (long)b * a.T2 * a.ldk + h * DK;
-  const bf16* vh_ = a.v + (long)b * a.T2 * a.ldv + h * DK;
-  const bf16* ph_ = REL ? a.pp + h * DK : nullptr;
+  const char* kh_ = (const char*)(a.k + (long)b * a.T2 * a.ldk + h * DK);
+  const char* vh_ = (const char*)(a.v + (long)b * a.T2 * a.ldv + h * DK);
+  const char* ph_ = REL ? (const char*)(a.pp + h * DK) : nullptr;
+  const uint32_t ldkb = (uint32_t)a.ldk * 2, ldvb = (uint32_t)a.ldv * 2, ldpb = REL ? (uint32_t)a.ldp * 2 : 0;
+  const int chx = (lane & 7) ^ ((lane >> 4) & 3);
   // chunk c's K / V rows into buffer c & 1; ring rows [x0, x0 + 8n) (relative to rb0) by groups
+  // (32-bit source offsets: the launcher checked the head slices' byte ranges)
   auto dma_kv = [&](int c) {
     char* kb = sm + L::K + (c & 1) * KC * 128;
     char* vb = sm + L::V + (c & 1) * KC * 128;
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
-      const int gi = w + 4 * u;
-      km_dma8(kb, 8 * gi, kh_, a.ldk, 64 * c + 8 * gi, a.T2, lane);
-      km_dma8(vb, 8 * gi, vh_, a.ldv, 64 * c + 8 * gi, a.T2, lane);
+      const int ir = 8 * (w + 4 * u);
+      km_dma8u(kb + ir * 128, ir, kh_, ldkb, 64 * c + ir, a.T2, chx, lane);
+      km_dma8u(vb + ir * 128, ir, vh_, ldvb, 64 * c + ir, a.T2, chx, lane);
     }
   };
   auto dma_ring = [&](int x0, int ngrp) {  // groups gi = w, w+4, ... < ngrp
     for (int gi = w; gi < ngrp; gi += 4) {
-      const int x = x0 + 8 * gi;
-      km_dma8(sm + L::P, x % RING, ph_, a.ldp, rb0 + x, rlimP, lane);
+      const int x = x0 + 8 * gi, ir = x % RING;
+      km_dma8u(sm + L::P + ir * 128, ir, ph_, ldpb, rb0 + x, rlimP, chx, lane);
     }
   };
+  // lane offsets of the 16 x 32 fragments of a km image at a 16-row boundary (row 16t + r has
+  // r's swizzle): fragment (16t rows on, k-step ks) = image + 2048 t + loff[ks]
+  int loff[2];
+#pragma unroll
+  for (int ks = 0; ks < 2; ++ks) loff[ks] = lc * 128 + (((ks * 4 + g) ^ km_swz(lc)) << 4);
   if (nch > 0) {
     dma_kv(0);
     if (REL) dma_ring(0, 18);
@@ -1014,7 +1055,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwdq2_kernel(AttnP a) {
 #pragma unroll
       for (int t = 0; t < 4; ++t)
 #pragma unroll
-        for (int ks = 0; ks < 2; ++ks) kf[t][ks] = km_frag_asm(kimg, 16 * t, ks, lane);
+        for (int ks = 0; ks < 2; ++ks) kf[t][ks] = ld128_asm(kimg + 2048 * t + loff[ks]);
       lgkm0();
 #pragma unroll
       for (int t = 0; t < 4; ++t) {
@@ -1028,11 +1069,12 @@ __global__ __launch_bounds__(256, 2) void attn_bwdq2_kernel(AttnP a) {
       f32x4 bd[5];
       {
         bf16x8 pf[5][2];
+        const int rb = (64 * c + pb) % RING;  // wave-uniform, a multiple of 16
 #pragma unroll
         for (int t = 0; t < 5; ++t) {
-          const int rp = (64 * c + pb + 16 * t) % RING;
+          const int rp = rb + 16 * t < RING ? rb + 16 * t : rb + 16 * t - RING;
 #pragma unroll
-          for (int ks = 0; ks < 2; ++ks) pf[t][ks] = km_frag_asm(ring, rp, ks, lane);
+          for (int ks = 0; ks < 2; ++ks) pf[t][ks] = ld128_asm(ring + rp * 128 + loff[ks]);
         }
         lgkm0();
 #pragma unroll
@@ -1063,7 +1105,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwdq2_kernel(AttnP a) {
 #pragma unroll
       for (int t = 0; t < 4; ++t)
 #pragma unroll
-        for (int ks = 0; ks < 2; ++ks) vf[t][ks] = km_frag_asm(vimg, 16 * t, ks, lane);
+        for (int ks = 0; ks < 2; ++ks) vf[t][ks] = ld128_asm(vimg + 2048 * t + loff[ks]);
       lgkm0();
 #pragma unroll
       for (int t = 0; t < 4; ++t) {
@@ -1114,7 +1156,8 @@ __global__ __launch_bounds__(256, 2) void attn_bwdq2_kernel(AttnP a) {
 #pragma unroll
         for (int ks = 0; ks < 2; ++ks) {
           const bf16x8 af = band_frag_asm(win, ks, lane);
-          const int r0 = (64 * c + pb + 32 * ks) % RING, r1 = (64 * c + pb + 32 * ks + 16) % RING;
+          const int rbq = (64 * c + pb) % RING, x0 = rbq + 32 * ks, x1 = x0 + 16;  // wave-uniform
+          const int r0 = x0 < RING ? x0 : x0 - RING, r1 = x1 < RING ? x1 : x1 - RING;
           bf16x8 bf[4];
 #pragma unroll
           for (int n = 0; n < 4; ++n) bf[n] = km_tr_rows(ring, r0, r1, 16 * n, lane);
@@ -1131,8 +1174,10 @@ __global__ __launch_bounds__(256, 2) void attn_bwdq2_kernel(AttnP a) {
           lgkm0();
           const uint4 v = *(const uint4*)&vb;
           const int i = i0 + 16 * w + row, col = W0 + j0 + 8 * ch;
-          bf16* dstp = (i < a.T1 && col < a.lddbd) ? dbd_h + (long)i * a.lddbd + col
-                                                  : (bf16*)((char*)a.wsDummy + lane * 16);
+          // (32-bit row offsets: the head's dbd block is far below 4 GiB)
+          bf16* dstp = (i < a.T1 && col < a.lddbd)
+                           ? (bf16*)((char*)dbd_h + __umul24((uint32_t)i, (uint32_t)a.lddbd * 2u) + 2u * (uint32_t)col)
+                           : (bf16*)((char*)a.wsDummy + lane * 16);
           *(uint4*)dstp = v;
         }
       }
@@ -1146,7 +1191,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwdq2_kernel(AttnP a) {
         for (int u = 0; u < 3; ++u) {
           const int q = lane + 64 * u;
           if (u < 2 || q < 160) {
-            const int zr = q / 10, zc = 2 + q % 10;
+            const int zr = (int)(__umul24((uint32_t)q, 205u) >> 11), zc = 2 + q - 10 * zr;  // q / 10 (q < 192)
             st128_asm(win + zr * 192 + ((zc ^ ((zr >> 2) & 3)) << 4), zero);
           }
         }
@@ -1247,7 +1292,8 @@ __global__ __launch_bounds__(256, 2) void attn_fwd2_kernel(AttnP a) {
   const int z = blockIdx.x / nqb, qb = blockIdx.x % nqb;
   const int b = z / a.H, h = z % a.H;
   const int i0 = qb * QB;
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: ring / image offsets stay scalar
   const int g = lane >> 4, lc = lane & 15;
   const int kl = a.klen ? (int)min((long long)a.T2, a.klen[b]) : a.T2;
   const uint64_t seed = MM == 1 || MM == 2 ? ea_salted(a.seed, a.salt) : 0;
@@ -1256,29 +1302,36 @@ __global__ __launch_bounds__(256, 2) void attn_fwd2_kernel(AttnP a) {
   const int nch = (kend + KC - 1) / KC;
   const int rlimP = 2 * a.T1 - 1;
   const int rb0 = a.T1 - 1 - (i0 + QB - 1);  // chunk 0's first positional row (ring position 0)
-  const bf16* kh_ = a.k + (long)b * a.T2 * a.ldk + h * DK;
-  const bf16* vh_ = a.v + (long)b * a.T2 * a.ldv + h * DK;
-  const bf16* ph_ = REL ? a.pp + h * DK : nullptr;
+  const char* kh_ = (const char*)(a.k + (long)b * a.T2 * a.ldk + h * DK);
+  const char* vh_ = (const char*)(a.v + (long)b * a.T2 * a.ldv + h * DK);
+  const char* ph_ = REL ? (const char*)(a.pp + h * DK) : nullptr;
+  const uint32_t ldkb = (uint32_t)a.ldk * 2, ldvb = (uint32_t)a.ldv * 2, ldpb = REL ? (uint32_t)a.ldp * 2 : 0;
+  const int chx = (lane & 7) ^ ((lane >> 4) & 3);
   auto dma_kv = [&](int c) {
     char* kb = sm + L::K + (c & 1) * KC * 128;
     char* vb = sm + L::V + (c & 1) * KC * 128;
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
-      const int gi = w + 4 * u;
-      km_dma8(kb, 8 * gi, kh_, a.ldk, 64 * c + 8 * gi, a.T2, lane);
-      km_dma8(vb, 8 * gi, vh_, a.ldv, 64 * c + 8 * gi, a.T2, lane);
+      const int ir = 8 * (w + 4 * u);
+      km_dma8u(kb + ir * 128, ir, kh_, ldkb, 64 * c + ir, a.T2, chx, lane);
+      km_dma8u(vb + ir * 128, ir, vh_, ldvb, 64 * c + ir, a.T2, chx, lane);
     }
   };
-  auto dma_ring = [&](int x0, int ngrp) {
+  auto dma_ring = [&](int x0, int ngrp) {  // ring rows x0 + [0, 8 ngrp) (x0 % 8 == 0)
     for (int gi = w; gi < ngrp; gi += 4) {
-      const int x = x0 + 8 * gi;
-      km_dma8(sm + L::P, x % RF, ph_, a.ldp, rb0 + x, rlimP, lane);
+      const int x = x0 + 8 * gi, ir = x % RF;
+      km_dma8u(sm + L::P + ir * 128, ir, ph_, ldpb, rb0 + x, rlimP, chx, lane);
     }
   };
   if (nch > 0) {
     dma_kv(0);
     if (REL) dma_ring(0, 16);
   }
+  // lane offsets of the 16 x 32 A/B fragments of a km image at a 16-row boundary (the swizzle of
+  // row 16t + r is that of r): fragment (16t rows on, k-step ks) = image + 2048 t + loff[ks]
+  int loff[2];
+#pragma unroll
+  for (int ks = 0; ks < 2; ++ks) loff[ks] = lc * 128 + (((ks * 4 + g) ^ km_swz(lc)) << 4);
   // this wave's 16 query rows as A fragments (q + u, q + v), from images in the second buffers
   bf16x8 qa[2], qv[2];
   {
@@ -1304,6 +1357,12 @@ __global__ __launch_bounds__(256, 2) void attn_fwd2_kernel(AttnP a) {
   const int odd = lc & 1;
   const uint64_t npair = (uint64_t)((a.T2 + 1) >> 1);
   const uint64_t prA = ((uint64_t)z * a.T1 + ibase + odd) * npair, prB = prA + 2 * npair;
+  // every pair index of the launch below 2^32: the hash input is the pair's low word + key, so a
+  // lane's input for key pair (j0 + 16t + lc) >> 1 is aA / aB + j0 / 2 + 8t (ea_pair_hash's value)
+  // (rows run up to nqb * 64 + 2 past a head's first and key pairs up to nch * 32: a margin)
+  const bool pair32 = ((uint64_t)a.B * a.H * a.T1 + 2 * QB + 4) * npair + a.T2 + 2 * KC < (1ull << 32);
+  const uint32_t key = MM == 1 || MM == 2 ? ea_seed_key(seed) : 0u;
+  const uint32_t aA = (uint32_t)prA + key + (uint32_t)(lc >> 1), aB = (uint32_t)prB + key + (uint32_t)(lc >> 1);
   const int pb = 48 - 16 * w;
   for (int c = 0; c < nch; ++c) {
     const int j0 = c * KC;
@@ -1321,7 +1380,7 @@ __global__ __launch_bounds__(256, 2) void attn_fwd2_kernel(AttnP a) {
 #pragma unroll
       for (int t = 0; t < 4; ++t)
 #pragma unroll
-        for (int ks = 0; ks < 2; ++ks) kf[t][ks] = km_frag_asm(kimg, 16 * t, ks, lane);
+        for (int ks = 0; ks < 2; ++ks) kf[t][ks] = ld128_asm(kimg + 2048 * t + loff[ks]);
       lgkm0();
 #pragma unroll
       for (int t = 0; t < 4; ++t) {
@@ -1335,11 +1394,12 @@ __global__ __launch_bounds__(256, 2) void attn_fwd2_kernel(AttnP a) {
       f32x4 bd[5];
       {
         bf16x8 pf[5][2];
+        const int rb = (64 * c + pb) % RF;  // wave-uniform, a multiple of 16
 #pragma unroll
         for (int t = 0; t < 5; ++t) {
-          const int rp = (64 * c + pb + 16 * t) % RF;
+          const int rp = rb + 16 * t < RF ? rb + 16 * t : rb + 16 * t - RF;
 #pragma unroll
-          for (int ks = 0; ks < 2; ++ks) pf[t][ks] = km_frag_asm(sm + L::P, rp, ks, lane);
+          for (int ks = 0; ks < 2; ++ks) pf[t][ks] = ld128_asm(sm + L::P + rp * 128 + loff[ks]);
         }
         lgkm0();
 #pragma unroll
@@ -1361,45 +1421,67 @@ __global__ __launch_bounds__(256, 2) void attn_fwd2_kernel(AttnP a) {
         }
       }
     }
-    // mask, online softmax
-    float pv[4][4];
+    // mask (only a chunk that reaches past the key length, or a causal one), online softmax
+    float pv[4][4], mx[4];
+    if (!a.causal && j0 + KC <= kl) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        mx[r] = -INFINITY;
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+          pv[t][r] = s[t][r] * a.scale;
+          mx[r] = fmaxf(mx[r], pv[t][r]);
+        }
+      }
+    } else {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int i = ibase + r;
+        mx[r] = -INFINITY;
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+          const int j = j0 + 16 * t + lc;
+          const bool ok = j < kl && (!a.causal || j <= i);
+          pv[t][r] = ok ? s[t][r] * a.scale : -INFINITY;
+          mx[r] = fmaxf(mx[r], pv[t][r]);
+        }
+      }
+    }
+    max16x4(mx);
+    float sum[4], alpha[4];
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      const int i = ibase + r;
-      float mx = -INFINITY;
+      const float mnew = fmaxf(mrun[r], mx[r]);
+      alpha[r] = mnew == -INFINITY ? 1.f : __expf(mrun[r] - mnew);
+      // a masked score is -inf: exp(-inf - m) = 0 for finite m; m = -inf only if the whole row so
+      // far is masked, then every exponent is exp(-inf - 0) = 0
+      const float ms = mnew == -INFINITY ? 0.f : mnew;
 #pragma unroll
-      for (int t = 0; t < 4; ++t) {
-        const int j = j0 + 16 * t + lc;
-        const bool ok = j < kl && (!a.causal || j <= i);
-        const float x = ok ? s[t][r] * a.scale : -INFINITY;
-        pv[t][r] = x;
-        mx = fmaxf(mx, x);
-      }
-      mx = max16(mx);
-      const float mnew = fmaxf(mrun[r], mx);
-      const float alpha = mnew == -INFINITY ? 1.f : __expf(mrun[r] - mnew);
-      float sum = 0.f;
-#pragma unroll
-      for (int t = 0; t < 4; ++t) {
-        const float e = pv[t][r] == -INFINITY ? 0.f : __expf(pv[t][r] - mnew);
-        pv[t][r] = e;
-        sum += e;
-      }
-      sum = sum16(sum);
-      lrun[r] = lrun[r] * alpha + sum;
+      for (int t = 0; t < 4; ++t) pv[t][r] = __expf(pv[t][r] - ms);
+      sum[r] = ((pv[0][r] + pv[1][r]) + pv[2][r]) + pv[3][r];
       mrun[r] = mnew;
 #pragma unroll
-      for (int t = 0; t < 4; ++t) oacc[t][r] *= alpha;
+      for (int t = 0; t < 4; ++t) oacc[t][r] *= alpha[r];
     }
+    sum16x4(sum);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) lrun[r] = lrun[r] * alpha[r] + sum[r];
     // dropout (keep bits -> dmask for the backward)
     if (MM == 1 || MM == 2) {
-      const uint32_t key = ea_seed_key(seed), thr = ea_drop_thr(a.p);
+      const uint32_t thr = ea_drop_thr(a.p);
       const float sc = 1.f / (1.f - a.p);
       uint64_t bal[4][4];
 #pragma unroll
       for (int t = 0; t < 4; ++t) {
-        const uint64_t jp = (uint64_t)((j0 + 16 * t + lc) >> 1);  // shared by the lane pair
-        const uint32_t hA = ea_pair_hash(key, prA + jp), hB = ea_pair_hash(key, prB + jp);
+        uint32_t hA, hB;
+        if (pair32) {
+          hA = ea_pair_mix(aA + (uint32_t)((j0 >> 1) + 8 * t));
+          hB = ea_pair_mix(aB + (uint32_t)((j0 >> 1) + 8 * t));
+        } else {
+          const uint64_t jp = (uint64_t)((j0 + 16 * t + lc) >> 1);  // shared by the lane pair
+          hA = ea_pair_hash(key, prA + jp);
+          hB = ea_pair_hash(key, prB + jp);
+        }
         const uint32_t pA = (uint32_t)__builtin_amdgcn_mov_dpp((int)hA, 0xB1, 0xF, 0xF, false);
         const uint32_t pB = (uint32_t)__builtin_amdgcn_mov_dpp((int)hB, 0xB1, 0xF, 0xF, false);
         const uint32_t hh[4] = {odd ? pA : hA, odd ? hA : pA, odd ? pB : hB, odd ? hB : pB};
@@ -1691,7 +1773,8 @@ __global__ __launch_bounds__(256, 2) void attn_bwdkv2_kernel(AttnP a) {
   const int nkb = (a.T2 + 63) / 64;
   const int z = blockIdx.x / nkb, kb = blockIdx.x % nkb;
   const int b = z / a.H, h = z % a.H;
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: ring / image offsets stay scalar
   const int g = lane >> 4, lc = lane & 15;
   const int kl = a.klen ? (int)min((long long)a.T2, a.klen[b]) : a.T2;
   const uint64_t seed = MM == 2 ? ea_salted(a.seed, a.salt) : 0;
@@ -1717,24 +1800,34 @@ __global__ __launch_bounds__(256, 2) void attn_bwdkv2_kernel(AttnP a) {
     const int bpos = 16 * (w & 1) + lc;  // this lane's bit in keep word w>>1
     const int ntile = (a.T1 - istart + BQ - 1) / BQ;
     const int rs0 = a.T1 - 1 - (istart + BQ - 1) + j0;  // first tile's first band row
-    const bf16* quh = a.wsQu + (long)b * a.T1 * a.ldqu + h * DK;
-    const bf16* qvh = REL ? a.wsQv + (long)b * a.T1 * a.ldqvw + h * DK : nullptr;
-    const bf16* doh = a.dO + (long)b * a.T1 * a.lddo + h * DK;
-    const bf16* ph_ = REL ? a.pp + h * DK : nullptr;
+    const char* quh = (const char*)(a.wsQu + (long)b * a.T1 * a.ldqu + h * DK);
+    const char* qvh = REL ? (const char*)(a.wsQv + (long)b * a.T1 * a.ldqvw + h * DK) : nullptr;
+    const char* doh = (const char*)(a.dO + (long)b * a.T1 * a.lddo + h * DK);
+    const char* ph_ = REL ? (const char*)(a.pp + h * DK) : nullptr;
+    // 32-bit LDS-DMA source offsets (the launcher checked the head slices' byte ranges)
+    const uint32_t ldqub = (uint32_t)a.ldqu * 2, ldqvb = (uint32_t)a.ldqvw * 2, lddob = (uint32_t)a.lddo * 2;
+    const uint32_t ldpb = REL ? (uint32_t)a.ldp * 2 : 0;
+    const int chx = (lane & 7) ^ ((lane >> 4) & 3);
+    // lane offsets of the 16 x 32 fragments of a km image at a 16-row boundary
+    int loff[2];
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) loff[ks] = lc * 128 + (((ks * 4 + g) ^ km_swz(lc)) << 4);
     // tile m: images at buffer m & 1; ring rows rs0 - 32m + [0, 96) at positions
     // (row - rs0) mod 128; small arrays: D, lse (log2 scaled at use), keep words of 32 rows
     auto dma_tile = [&](int m, bool first) {
       const int i0 = istart + BQ * m;
       const int buf = m & 1;
-      km_dma8(sm + L::QU + buf * L::IMG, 8 * w, quh, a.ldqu, i0 + 8 * w, a.T1, lane);
-      if (REL) km_dma8(sm + L::QV + buf * L::IMG, 8 * w, qvh, a.ldqvw, i0 + 8 * w, a.T1, lane);
-      km_dma8(sm + L::DO + buf * L::IMG, 8 * w, doh, a.lddo, i0 + 8 * w, a.T1, lane);
+      const int ir = 8 * w;
+      km_dma8u(sm + L::QU + buf * L::IMG + ir * 128, ir, quh, ldqub, i0 + ir, a.T1, chx, lane);
+      if (REL) km_dma8u(sm + L::QV + buf * L::IMG + ir * 128, ir, qvh, ldqvb, i0 + ir, a.T1, chx, lane);
+      km_dma8u(sm + L::DO + buf * L::IMG + ir * 128, ir, doh, lddob, i0 + ir, a.T1, chx, lane);
       if (REL) {
         // first tile: all 96 rows (12 groups); later: the 32 new rows below the previous band
         const int x0 = first ? 0 : -32 * m, ng = first ? 12 : 4;
         for (int gi = w; gi < ng; gi += 4) {
           const int x = x0 + 8 * gi;  // relative to rs0; position x mod 128
-          km_dma8(sm + L::P, ((x % RINGK) + RINGK) % RINGK, ph_, a.ldp, rs0 + x, 2 * a.T1 - 1, lane);
+          const int xr = ((x % RINGK) + RINGK) % RINGK;
+          km_dma8u(sm + L::P + xr * 128, xr, ph_, ldpb, rs0 + x, 2 * a.T1 - 1, chx, lane);
         }
       }
       if (w == 0) {
@@ -1764,8 +1857,8 @@ __global__ __launch_bounds__(256, 2) void attn_bwdkv2_kernel(AttnP a) {
         for (int mi = 0; mi < 2; ++mi)
 #pragma unroll
           for (int ks = 0; ks < 2; ++ks) {
-            qf[mi][ks] = km_frag_asm(quimg, 16 * mi, ks, lane);
-            df[mi][ks] = km_frag_asm(doimg, 16 * mi, ks, lane);
+            qf[mi][ks] = ld128_asm(quimg + 2048 * mi + loff[ks]);
+            df[mi][ks] = ld128_asm(doimg + 2048 * mi + loff[ks]);
           }
         lgkm0();
 #pragma unroll
@@ -1787,12 +1880,12 @@ __global__ __launch_bounds__(256, 2) void attn_bwdkv2_kernel(AttnP a) {
 #pragma unroll
           for (int mi = 0; mi < 2; ++mi)
 #pragma unroll
-            for (int ks = 0; ks < 2; ++ks) vq[mi][ks] = km_frag_asm(qvimg, 16 * mi, ks, lane);
+            for (int ks = 0; ks < 2; ++ks) vq[mi][ks] = ld128_asm(qvimg + 2048 * mi + loff[ks]);
 #pragma unroll
           for (int u = 0; u < 3; ++u) {
             const int rp = (((16 * (w + u) - 32 * m) % RINGK) + RINGK) % RINGK;
 #pragma unroll
-            for (int ks = 0; ks < 2; ++ks) pf[u][ks] = km_frag_asm(sm + L::P, rp, ks, lane);
+            for (int ks = 0; ks < 2; ++ks) pf[u][ks] = ld128_asm(sm + L::P + rp * 128 + loff[ks]);  // rp % 16 == 0
           }
           lgkm0();
 #pragma unroll
@@ -1929,7 +2022,11 @@ extern "C" int ea_attn_fused_fwd2(int B, int H, int T1, int T2, int dk, const vo
   dim3 grid(B * H * ((T1 + QB - 1) / QB));
   const hipStream_t st = (hipStream_t)stream;
   const char* ev = getenv("EA_ATTN_FWD_V1");  // A/B: the original forward kernel
-  const bool v1 = ev && ev[0] == '1';
+  // the pipelined kernel's LDS-DMA sources are 32-bit byte offsets (__umul24(row, row bytes))
+  // from each head's base: beyond that range the original kernel runs
+  const auto fits = [](long rows, long ld) { return ld * 2 < (1L << 24) && rows * ld * 2 + 128 < (1L << 32); };
+  const bool off32 = fits(T2, ldk) && fits(T2, ldv) && (!pp || fits(2L * T1, ldp));
+  const bool v1 = (ev && ev[0] == '1') || !off32;
   const int mm = p > 0.f ? (dmask ? 1 : 2) : 0;
   if (v1) {
     if (pp) hipLaunchKernelGGL(attn_fwd_kernel<true>, grid, dim3(256), 0, st, a);
@@ -1957,6 +2054,13 @@ extern "C" int ea_attn_fused_fwd(int B, int H, int T1, int T2, int dk, const voi
 
 static int attn_bwd_launch(AttnP& a, bool rel, bool v2, hipStream_t st) {
   const int nqb = (a.T1 + QB - 1) / QB, nkb = (a.T2 + 63) / 64;
+  // the pipelined dQ pass addresses K / V / positional rows with 32-bit byte offsets from each
+  // head's base (__umul24(row, row bytes))
+  const auto fits = [](long rows, long ld) { return ld * 2 < (1L << 24) && rows * ld * 2 + 128 < (1L << 32); };
+  EA_CHECK_ARG(!v2 || (fits(a.T2, a.ldk) && fits(a.T2, a.ldv) && (!rel || fits(2L * a.T1, a.ldp)) &&
+                       (!a.dbd || fits(a.T1, a.lddbd))));
+  // the pipelined dK / dV pass likewise (else the original one runs)
+  const bool kv32 = fits(a.T1, a.ldqu) && fits(a.T1, a.lddo) && (!rel || (fits(a.T1, a.ldqvw) && fits(2L * a.T1, a.ldp)));
   const dim3 gq(a.B * a.H * nqb), gkv(a.B * a.H * nkb);
   const int mm = a.p > 0.f ? (a.dmask ? 1 : 2) : 0;
   const char* ev = getenv("EA_ATTN_BWDKV_V1");  // A/B: the original dK/dV pass
@@ -1966,7 +2070,7 @@ static int attn_bwd_launch(AttnP& a, bool rel, bool v2, hipStream_t st) {
     else if (v2 && mm == 1) hipLaunchKernelGGL((attn_bwdq2_kernel<true, 1>), gq, dim3(256), 0, st, a);
     else if (v2) hipLaunchKernelGGL((attn_bwdq2_kernel<true, 2>), gq, dim3(256), 0, st, a);
     else hipLaunchKernelGGL(attn_bwdq_kernel<true>, gq, dim3(256), 0, st, a);
-    if (kv1) hipLaunchKernelGGL(attn_bwdkv_kernel<true>, gkv, dim3(256), 0, st, a);
+    if (kv1 || !kv32) hipLaunchKernelGGL(attn_bwdkv_kernel<true>, gkv, dim3(256), 0, st, a);
     else if (mm == 0) hipLaunchKernelGGL((attn_bwdkv2_kernel<true, 0>), gkv, dim3(256), 0, st, a);
     else if (mm == 1) hipLaunchKernelGGL((attn_bwdkv2_kernel<true, 1>), gkv, dim3(256), 0, st, a);
     else hipLaunchKernelGGL((attn_bwdkv2_kernel<true, 2>), gkv, dim3(256), 0, st, a);
@@ -1975,7 +2079,7 @@ static int attn_bwd_launch(AttnP& a, bool rel, bool v2, hipStream_t st) {
     else if (v2 && mm == 1) hipLaunchKernelGGL((attn_bwdq2_kernel<false, 1>), gq, dim3(256), 0, st, a);
     else if (v2) hipLaunchKernelGGL((attn_bwdq2_kernel<false, 2>), gq, dim3(256), 0, st, a);
     else hipLaunchKernelGGL(attn_bwdq_kernel<false>, gq, dim3(256), 0, st, a);
-    if (kv1) hipLaunchKernelGGL(attn_bwdkv_kernel<false>, gkv, dim3(256), 0, st, a);
+    if (kv1 || !kv32) hipLaunchKernelGGL(attn_bwdkv_kernel<false>, gkv, dim3(256), 0, st, a);
     else if (mm == 0) hipLaunchKernelGGL((attn_bwdkv2_kernel<false, 0>), gkv, dim3(256), 0, st, a);
     else if (mm == 1) hipLaunchKernelGGL((attn_bwdkv2_kernel<false, 1>), gkv, dim3(256), 0, st, a);
     else hipLaunchKernelGGL((attn_bwdkv2_kernel<false, 2>), gkv, dim3(256), 0, st, a);
