@@ -760,6 +760,18 @@ EA_DEV bf16x8 ld128_asm(const char* p) {
   asm volatile("ds_read_b128 %0, %1" : "=v"(v) : "v"(a) : "memory");
   return v;
 }
+template <int OFF>  // LDS byte address + immediate offset
+EA_DEV bf16x8 ld128_at(uint32_t a) {
+  bf16x8 v;
+  asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(v) : "v"(a), "i"(OFF) : "memory");
+  return v;
+}
+// max of two scores that are never NaN (no canonicalisation of the operands)
+EA_DEV float fmax_nn(float a, float b) {
+  float r;
+  asm("v_max_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
 EA_DEV uint2 ld64_asm(const char* p) {
   __attribute__((ext_vector_type(2))) unsigned v;
   const uint32_t a = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) char*)p;
@@ -1377,10 +1389,11 @@ __global__ __launch_bounds__(256, 2) void attn_fwd2_kernel(AttnP a) {
     f32x4 s[4];
     {
       bf16x8 kf[4][2];
-#pragma unroll
-      for (int t = 0; t < 4; ++t)
-#pragma unroll
-        for (int ks = 0; ks < 2; ++ks) kf[t][ks] = ld128_asm(kimg + 2048 * t + loff[ks]);
+      const uint32_t ka0 = lds_addr(kimg) + loff[0], ka1 = lds_addr(kimg) + loff[1];
+      kf[0][0] = ld128_at<0>(ka0);    kf[0][1] = ld128_at<0>(ka1);
+      kf[1][0] = ld128_at<2048>(ka0); kf[1][1] = ld128_at<2048>(ka1);
+      kf[2][0] = ld128_at<4096>(ka0); kf[2][1] = ld128_at<4096>(ka1);
+      kf[3][0] = ld128_at<6144>(ka0); kf[3][1] = ld128_at<6144>(ka1);
       lgkm0();
 #pragma unroll
       for (int t = 0; t < 4; ++t) {
@@ -1395,11 +1408,12 @@ __global__ __launch_bounds__(256, 2) void attn_fwd2_kernel(AttnP a) {
       {
         bf16x8 pf[5][2];
         const int rb = (64 * c + pb) % RF;  // wave-uniform, a multiple of 16
+        const uint32_t pa0 = lds_addr(sm) + loff[0], pa1 = lds_addr(sm) + loff[1];
 #pragma unroll
         for (int t = 0; t < 5; ++t) {
           const int rp = rb + 16 * t < RF ? rb + 16 * t : rb + 16 * t - RF;
-#pragma unroll
-          for (int ks = 0; ks < 2; ++ks) pf[t][ks] = ld128_asm(sm + L::P + rp * 128 + loff[ks]);
+          pf[t][0] = ld128_at<L::P>(pa0 + rp * 128);
+          pf[t][1] = ld128_at<L::P>(pa1 + rp * 128);
         }
         lgkm0();
 #pragma unroll
@@ -1451,7 +1465,7 @@ __global__ __launch_bounds__(256, 2) void attn_fwd2_kernel(AttnP a) {
     float sum[4], alpha[4];
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      const float mnew = fmaxf(mrun[r], mx[r]);
+      const float mnew = fmax_nn(mrun[r], mx[r]);
       alpha[r] = mnew == -INFINITY ? 1.f : __expf(mrun[r] - mnew);
       // a masked score is -inf: exp(-inf - m) = 0 for finite m; m = -inf only if the whole row so
       // far is masked, then every exponent is exp(-inf - 0) = 0
@@ -1471,17 +1485,24 @@ __global__ __launch_bounds__(256, 2) void attn_fwd2_kernel(AttnP a) {
       const uint32_t thr = ea_drop_thr(a.p);
       const float sc = 1.f / (1.f - a.p);
       uint64_t bal[4][4];
+      uint32_t hAt[4], hBt[4];
+      if (pair32) {
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+          hAt[t] = ea_pair_mix(aA + (uint32_t)((j0 >> 1) + 8 * t));
+          hBt[t] = ea_pair_mix(aB + (uint32_t)((j0 >> 1) + 8 * t));
+        }
+      } else {
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+          const uint64_t jp = (uint64_t)((j0 + 16 * t + lc) >> 1);  // shared by the lane pair
+          hAt[t] = ea_pair_hash(key, prA + jp);
+          hBt[t] = ea_pair_hash(key, prB + jp);
+        }
+      }
 #pragma unroll
       for (int t = 0; t < 4; ++t) {
-        uint32_t hA, hB;
-        if (pair32) {
-          hA = ea_pair_mix(aA + (uint32_t)((j0 >> 1) + 8 * t));
-          hB = ea_pair_mix(aB + (uint32_t)((j0 >> 1) + 8 * t));
-        } else {
-          const uint64_t jp = (uint64_t)((j0 + 16 * t + lc) >> 1);  // shared by the lane pair
-          hA = ea_pair_hash(key, prA + jp);
-          hB = ea_pair_hash(key, prB + jp);
-        }
+        const uint32_t hA = hAt[t], hB = hBt[t];
         const uint32_t pA = (uint32_t)__builtin_amdgcn_mov_dpp((int)hA, 0xB1, 0xF, 0xF, false);
         const uint32_t pB = (uint32_t)__builtin_amdgcn_mov_dpp((int)hB, 0xB1, 0xF, 0xF, false);
         const uint32_t hh[4] = {odd ? pA : hA, odd ? hA : pA, odd ? pB : hB, odd ? hB : pB};
@@ -1493,11 +1514,14 @@ __global__ __launch_bounds__(256, 2) void attn_fwd2_kernel(AttnP a) {
         }
       }
       if (MM == 1 && lc < 2) {  // lane lc = u writes word u of each of its group's 4 rows
+        const bool hiw = g >= 2;   // the group's 16 ballot bits sit in the high dword
+        const uint32_t sh = 16u * (uint32_t)(g & 1);
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int i = ibase + r;
           const uint64_t lo = lc ? bal[2][r] : bal[0][r], hi = lc ? bal[3][r] : bal[1][r];
-          const uint32_t word = (uint32_t)((lo >> (16 * g)) & 0xffffu) | ((uint32_t)((hi >> (16 * g)) & 0xffffu) << 16);
+          const uint32_t x0 = hiw ? (uint32_t)(lo >> 32) : (uint32_t)lo, x1 = hiw ? (uint32_t)(hi >> 32) : (uint32_t)hi;
+          const uint32_t word = __builtin_amdgcn_ubfe(x0, sh, 16) | (__builtin_amdgcn_ubfe(x1, sh, 16) << 16);
           if (i < a.T1) a.dmask[((long)z * a.T1 + i) * a.ldm + (j0 >> 5) + lc] = word;
         }
       }
