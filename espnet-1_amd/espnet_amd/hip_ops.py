@@ -89,6 +89,7 @@ PROBE = None
 # run weight-gradient GEMMs / bias reductions on a side stream (EA_OVERLAP_WGRAD=0: serial, for profiling)
 OVERLAP_WGRAD = os.environ.get("EA_OVERLAP_WGRAD", "1") != "0"
 _SIDE = {}
+_SIDE_DIRTY = {}  # device -> the side stream forked since the main stream last joined it
 
 
 class wgrad:
@@ -96,21 +97,36 @@ class wgrad:
     backward critical path: it runs on a side HIP stream, ordered after everything the
     main stream has issued so far; `join()` makes the main stream wait for it.
     Tensors read on the side stream are record_stream()-ed so the caching allocator does
-    not recycle them under it."""
+    not recycle them under it.
 
-    def __init__(self, *tensors):
+    While the pass's weight gradients and reductions are deferred (deferred_wgrad), a block
+    of linear_dw / colsum calls only queues work, and the fork is skipped unless `launches`
+    says the block launches kernels of its own: in a captured step every fork is a graph
+    dependency whose event costs the main chain ~5 us even when nothing runs on the side
+    (a launch inside a skipped fork simply runs on the current stream, in order)."""
+
+    def __init__(self, *tensors, after=None, launches=False):
         self.tensors = tensors
+        self.after = after  # fork from this event (fork_event) instead of the stream's current point
+        self.launches = launches
 
     def __enter__(self):
         if not OVERLAP_WGRAD or not torch.cuda.is_available():  # (CPU: the gloo DP tests)
             self.ctx = None
+            return self
+        if LAZY_FORK and not self.launches and WGRAD_Q.active and REDUCE_Q.active:
+            self.ctx = None  # only deferred work inside: no fork
             return self
         main = torch.cuda.current_stream()
         dev = main.device
         side = _SIDE.get(dev)
         if side is None:
             side = _SIDE[dev] = torch.cuda.Stream(device=dev)
-        side.wait_stream(main)
+        if self.after is not None:
+            side.wait_event(self.after)
+        else:
+            side.wait_stream(main)
+        _SIDE_DIRTY[dev] = True
         for t in self.tensors:
             if t is not None:
                 t.record_stream(side)
@@ -124,14 +140,33 @@ class wgrad:
         return False
 
 
+# wgrad blocks that only queue deferred work do not fork (EA_LAZY_FORK=0: every block forks)
+LAZY_FORK = os.environ.get("EA_LAZY_FORK", "1") != "0"
+# a side-stream GEMM forked from an earlier point of the main stream, issued after the main
+# stream's next kernel (EA_FORK_AFTER=1, A/B): in the captured graph the main chain's kernel is
+# then the first successor of the fork point
+FORK_AFTER = os.environ.get("EA_FORK_AFTER", "1") != "0"
+
+
+def fork_event():
+    """An event at the main stream's current point for a later wgrad(after=...), or None."""
+    if not (FORK_AFTER and OVERLAP_WGRAD) or not torch.cuda.is_available():
+        return None
+    ev = torch.cuda.Event()
+    ev.record(torch.cuda.current_stream())
+    return ev
+
+
 def join_wgrad(device=None):
-    """Main stream waits for all weight-gradient work issued so far."""
+    """Main stream waits for all weight-gradient work issued so far (nothing to wait for —
+    and no graph dependency — when the side stream was not forked since the last join)."""
     if not _SIDE:
         return
     main = torch.cuda.current_stream()
     side = _SIDE.get(main.device)
-    if side is not None:
+    if side is not None and (_SIDE_DIRTY.get(main.device, True) or not LAZY_FORK):
         main.wait_stream(side)
+        _SIDE_DIRTY[main.device] = False
 
 
 # latency-bound work that leaves most CUs idle (the CTC lattice: 2 workgroups per utterance)
@@ -679,7 +714,7 @@ class deferred_wgrad:
                 # the pass's reductions (bias column sums, LayerNorm parameter sums: bandwidth-
                 # bound) on the side stream beside the grouped weight-gradient GEMM (MFMA-bound)
                 # on this one; disjoint outputs (bias / norm vs weight gradients)
-                with wgrad(*REDUCE_Q.tensors()):
+                with wgrad(*REDUCE_Q.tensors(), launches=True):
                     REDUCE_Q.flush()
                 WGRAD_Q.flush()
             else:

@@ -406,19 +406,27 @@ class ConformerBlockFn(torch.autograd.Function):
         # linear_pos: dp[h] = sum_b dBD[h][b]^T qv[b, :, h]  (K = B*T), dWpos = dp^T pos; with the
         # shifted layout the GEMM runs over every physical column and rows [shift, shift + P2) of
         # its output are dp
-        with ops.wgrad(dbd, qv, pos):
-            Mp = P2 + shift if shift else P2
-            dpp_full = empty(Mp, d, dtype=cd, device=dev)
-            ops.gemm(dbd, qv, dpp_full, M=Mp, N=dk, K=B * T, a_kmajor=0, b_kmajor=0, lda=ldbd, ldb=d, ldc=d,
-                     batch=1, nh=H, sA=(0, B * T * ldbd), sB=(0, dk), sC=(0, dk))
-            ops.linear_dw(dpp_full[shift:], pos, b.g(A + "linear_pos.weight"), accumulate=True)
-        del dbd
+
+        def dpp_wgrad(after=None):
+            with ops.wgrad(dbd, qv, pos, after=after, launches=True):
+                Mp = P2 + shift if shift else P2
+                dpp_full = empty(Mp, d, dtype=cd, device=dev)
+                ops.gemm(dbd, qv, dpp_full, M=Mp, N=dk, K=B * T, a_kmajor=0, b_kmajor=0, lda=ldbd, ldb=d, ldc=d,
+                         batch=1, nh=H, sA=(0, B * T * ldbd), sB=(0, dk), sC=(0, dk))
+                ops.linear_dw(dpp_full[shift:], pos, b.g(A + "linear_pos.weight"), accumulate=True)
+
+        fork = ops.fork_event()
+        if fork is None:
+            dpp_wgrad()
         with ops.wgrad(dqkv, xn2):
             ops.colsum(dqkv, b.g(A + "linear_q.bias", A + "linear_k.bias", A + "linear_v.bias", shape=(3 * d,)))
             ops.linear_dw(dqkv, xn2, b.g(A + "linear_q.weight", A + "linear_k.weight", A + "linear_v.weight",
                                           shape=(3 * d, d)), accumulate=True)
         dxn2 = empty(N, d, dtype=cd, device=dev)
         ops.linear_dx(dqkv, qkv_w, dxn2)
+        if fork is not None:  # (EA_FORK_AFTER) the side GEMM issued after the main chain's next kernel
+            dpp_wgrad(after=fork)
+        del dbd
         dv_ff1 = dv_buf(N, d, cd, dev)
         ln_bwd(dxn2, x1, b, "norm_mha", mu2, rs2, dx, accumulate=True,
                drop=drop_arg(dv_ff1, L.ff_scale, p, sd(2), b.g("feed_forward_macaron.w_2.bias")))

@@ -242,7 +242,7 @@ class SubsampleFn(torch.autograd.Function):
         dx2[P2:].zero_()
         ops.linear_dx(dv, wl, dx2[:P2].view(B * T2, F2 * C), epi=ops.make_epi(EPI_DACT, act=ACT_RELU, aux=x2r))
         ws_side = None
-        with ops.wgrad(dx2, x1p):
+        with ops.wgrad(dx2, x1p, launches=True):
             ops.colsum(dx2[:P2], b.g("conv.2.bias"))
             dw2 = empty(C, 9 * C, device=dev)
             geo, _, _, _ = phase_geo(B, T1, F1, T2, F2, C, CONV_WGRAD, zero=P1 * C)
@@ -304,7 +304,7 @@ class SubsampleFn(torch.autograd.Function):
             lib.ea_conv1_wgrad_reduce(tile0, C, part.data_ptr(), b.g("conv.0.weight").data_ptr(),
                                       b.g("conv.0.bias").data_ptr(), ops.stream())
         else:
-            with ops.wgrad(dx1p, feats):
+            with ops.wgrad(dx1p, feats, launches=True):
                 w, wn = ops._ws(dev, 1024 * 10 * C)
                 lib.ea_conv1_wgrad(B, T, Fin, C, feats.data_ptr(), dx1p.data_ptr(), ops.dt(dx1p),
                                    b.g("conv.0.weight").data_ptr(), b.g("conv.0.bias").data_ptr(), w, wn, ops.stream())
@@ -348,7 +348,7 @@ class SubsampleFn(torch.autograd.Function):
         lib.ea_col2im_conv2(B, T1, F1, C, dcol2.data_ptr(), ops.dt(dcol2), x1.data_ptr(), dx1.data_ptr(),
                             ops.dt(dx1), ops.stream())
         del dcol2
-        with ops.wgrad(dx1, col1):
+        with ops.wgrad(dx1, col1, launches=True):
             ops.colsum(dx1, b.g("conv.0.bias"))
             ops.gemm(dx1, col1, b.g("conv.0.weight", shape=(C, 9)), M=C, N=9, K=dx1.shape[0],
                      a_kmajor=0, b_kmajor=0, lda=C, ldb=16, ldc=9, epi=ops.make_epi(beta=1.0))

@@ -142,7 +142,7 @@ class ArenaDataParallel:
         if not done:
             return  # the deferred GEMMs keep accumulating until a bucket needs them
         g = self.arena.grad
-        with hip_ops.wgrad(*hip_ops.deferred_tensors()):
+        with hip_ops.wgrad(*hip_ops.deferred_tensors(), launches=True):
             hip_ops.flush_deferred()
             for i in done:
                 self._works.append(dist.all_reduce(g[self.buckets[i]], async_op=True, group=self.group))
