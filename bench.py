@@ -372,7 +372,7 @@ def main():
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(cfg)
             out["speedup_vs_cpu"] = round(utt / out["cpu_baseline"]["value"], 1)
-        print(json.dumps(out), flush=True)
+        emit(out)
     if world > 1:
         dist.destroy_process_group()
 
@@ -496,7 +496,7 @@ def run_c5(args, world, rank, dev):
         elapsed = float(mx.item())
     _, n_utt, n_frames, n_padded = (float(v) for v in tot.tolist())
     if rank == 0:
-        print(json.dumps({
+        emit({
             "metric": "utterances/sec, Conformer-L + SpecAug, bucketed T~U[200,2000] (C5)",
             "value": round(n_utt / elapsed, 3), "unit": "utterances/s", "n_gpus": world, "steps": args.steps,
             "warmup": warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3), "higher_is_better": True,
@@ -509,10 +509,28 @@ def run_c5(args, world, rank, dev):
             "frames_per_s": round(n_frames / elapsed, 1),
             "padding_fraction": round(1.0 - n_frames / n_padded, 4),
             "batches_in_corpus_per_rank": nb, "step_mode": runner.mode or "eager", "loss": round(float(loss.item()), 4),
-        }), flush=True)
+        })
     if world > 1:
         dist.destroy_process_group()
 
 
+_JSON_FD = None  # the process's original stdout: the one JSON line goes there
+
+
+def emit(obj):
+    line = (json.dumps(obj) + "\n").encode()
+    if _JSON_FD is None:
+        sys.stdout.write(line.decode())
+        sys.stdout.flush()
+    else:
+        os.write(_JSON_FD, line)
+
+
 if __name__ == "__main__":
+    # everything else written to stdout — RCCL's version banner when a communicator comes up
+    # (the DP rehearsal, N > 1), library chatter — goes to stderr, so stdout carries exactly
+    # one JSON line
+    sys.stdout.flush()
+    _JSON_FD = os.dup(1)
+    os.dup2(2, 1)
     main()
