@@ -263,6 +263,23 @@ def grad_ready(bound):
     join_wgrad()
 
 
+# the attention decoder's weight-gradient GEMMs launched per decoder layer on the side stream,
+# beside the next layer's latency-bound backward, instead of in the end-of-pass grouped GEMM
+# with the fork-after order (EA_DEC_WGRAD_LAYER=0: all in the end-of-pass grouped GEMM)
+DEC_WGRAD_LAYER = os.environ.get("EA_DEC_WGRAD_LAYER", "1") != "0"
+
+
+def flush_wgrad_side(after=None):
+    """Launch the weight gradients queued so far (one grouped GEMM) on the side stream, forked
+    from `after` (fork_event); single process only (the data-parallel hooks flush per bucket)."""
+    if not (WGRAD_Q.active and WGRAD_Q.items) or GRAD_READY is not None:
+        return
+    if not OVERLAP_WGRAD or not torch.cuda.is_available():
+        return
+    with wgrad(*WGRAD_Q.tensors(), after=after, launches=True):
+        WGRAD_Q.flush()
+
+
 def dt(t: torch.Tensor) -> int:
     try:
         return _DT[t.dtype]
