@@ -1372,7 +1372,7 @@ EA_DEV TileOv tile_ov(const GemmP& p) { return TileOv{p.M, p.g.a, p.g.e, p.w1par
 template <bool AK, bool BKM, int MODE = 0, int BT = 256, int NS = 4>
 EA_DEV void pipe_tile(const GemmP& p, const TileOv& ov, char* smem, const bf16* A, const bf16* B, int m0, int n0, int kbeg,
                       int kend, f32x4 (&acc)[PipeT<BT, NS>::MI][4]) {
-  static_assert(MODE == 0 || (MODE == EA_CONV_FWD && AK && BKM) || (MODE == EA_CONV_DGRAD && AK && !BKM) ||
+  static_assert(MODE == 0 || (MODE == EA_CONV_FWD && AK && BKM) || (MODE == EA_CONV_DGRAD && AK) ||
                 (MODE == EA_CONV_WGRAD && !AK && !BKM), "conv gather layouts");
   static_assert(MODE == 0 || BT == 256, "conv gathers run on 256-wide tiles");
   using PC = PipeT<BT, NS>;
@@ -1495,7 +1495,9 @@ EA_DEV void pipe_tile(const GemmP& p, const TileOv& ov, char* smem, const bf16* 
       if constexpr (MODE == EA_CONV_DGRAD) {  // W2t [9][co][ci]: a slice = 32 co of one tap
         int kh, kw;
         dgrad_tap2(ov.a, ov.e, q, kh, kw);
-        bk = (const char*)(B + ((long)(kh * 3 + kw) * p.g.C + c0) * p.g.C);
+        // K-major W2k [ci][tap][co] (ldb = 9C): the slice is 32 co of tap (kh, kw) in every row
+        bk = BKM ? (const char*)(B + (long)(kh * 3 + kw) * p.g.C + c0)
+                 : (const char*)(B + ((long)(kh * 3 + kw) * p.g.C + c0) * p.g.C);
       }
     } else {
 #pragma unroll

@@ -46,6 +46,8 @@ FUSE_CONV1_WGRAD = os.environ.get("EA_FUSE_CONV1_WGRAD", "1") != "0"
 CONV1_POS_BITS = os.environ.get("EA_CONV1_POS_BITS", "1") != "0"
 # ... and the four parity classes in one launch (EA_MERGED_DGRAD=0: one launch per class)
 MERGED_DGRAD = os.environ.get("EA_MERGED_DGRAD", "1") != "0"
+# ... reading conv2's weight K-major, W2k [ci][tap][co] (EA_DGRAD_KMAJOR=0: W2t [tap][co][ci])
+DGRAD_KMAJOR = os.environ.get("EA_DGRAD_KMAJOR", "1") != "0"
 
 
 def _implicit_ok(cd, C):
@@ -258,9 +260,14 @@ class SubsampleFn(torch.autograd.Function):
         # (ea_gemm_conv_w1), so dx1 is never written and conv1's weight / bias gradients are
         # the sum of per-tile partials
         ws = ops.workspace(ops._SPLITK_WS, dev)
-        w2t = empty(9, C, C, dtype=cd, device=dev)  # tap-major: every tap's (co, ci) block dense
-        ops.permute3(b.f("conv.2.weight"), w2t, 1, C * C, 9)  # (Co,Ci,9) -> (9,Co,Ci)
         fuse = FUSE_CONV1_WGRAD
+        kmaj = DGRAD_KMAJOR and fuse and pos1 is not None and MERGED_DGRAD
+        if kmaj:  # W2k: (Co, Ci*9) -> (Ci*9, Co), every output channel's K = (tap, co) row dense
+            w2t = empty(C, 9 * C, dtype=cd, device=dev)
+            ops.permute3(b.f("conv.2.weight"), w2t, 1, C, 9 * C)
+        else:
+            w2t = empty(9, C, C, dtype=cd, device=dev)  # tap-major: every tap's (co, ci) block dense
+            ops.permute3(b.f("conv.2.weight"), w2t, 1, C * C, 9)  # (Co,Ci,9) -> (9,Co,Ci)
         if fuse:
             _, _, _, rows_all = phase_geo(B, T1, F1, T2, F2, C, CONV_DGRAD)
             part = empty(sum((r + 255) // 256 for r in rows_all) * 10 * C, device=dev)
@@ -271,7 +278,8 @@ class SubsampleFn(torch.autograd.Function):
             # the four parity classes in one launch, longest K first (ea_gemm_conv_w1b_all)
             geo, _, _, _ = phase_geo(B, T1, F1, T2, F2, C, CONV_DGRAD, zero=P2 * C)
             epi = ops.make_epi(EPI_DACT, act=ACT_RELU)
-            lib.ea_gemm_conv_w1b_all(ctypes.byref(geo), C, dx2.data_ptr(), C, w2t.data_ptr(), C, ctypes.byref(epi),
+            lib.ea_gemm_conv_w1b_all(ctypes.byref(geo), C, dx2.data_ptr(), C, w2t.data_ptr(), 9 * C if kmaj else C,
+                                     ctypes.byref(epi),
                                      feats.data_ptr(), T, Fin, part.data_ptr(), pos1.data_ptr(), ops.stream())
             tile0 = sum((r + 255) // 256 for r in rows_all if r)
         else:

@@ -123,7 +123,9 @@ int ea_gemm_conv_w1b(const ea_conv_geo* geo, int M, int N, int K, const void* A,
  * launch (geo: EA_CONV_DGRAD with nI / nJ / plane; a, e ignored): class c has
  * M_c = B*nI[a]*nJ[e] rows and K_c = (a ? 1 : 2)*(e ? 1 : 2)*C, its mask bits start at row
  * plane[c]/C of pos, and its ceil(M_c/256) partial tiles follow the previous classes' in part —
- * the same results as the four ea_gemm_conv_w1b calls in that order, bit for bit. */
+ * the same results as the four ea_gemm_conv_w1b calls in that order, bit for bit.  B is conv2's
+ * weight as W2t [9][co][ci] (ldb = C) or as W2k [ci][9][co] (ldb = 9*C, K-major fragment reads;
+ * the same products in the same order, so the same results). */
 int ea_gemm_conv_w1b_all(const ea_conv_geo* geo, int N, const void* A, long lda, const void* B, long ldb,
                          const ea_epilogue* epi, const float* x, int T, int Fin, float* part,
                          const unsigned char* pos, void* stream);

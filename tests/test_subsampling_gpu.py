@@ -128,3 +128,23 @@ def test_merged_dgrad_classes_bit_identical(C, B, T):
     assert torch.equal(y0, y1)
     for k in g0:
         assert torch.equal(g0[k], g1[k]), k
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("C,B,T", [(64, 2, 67), (256, 3, 131), (512, 32, 1000)])
+def test_dgrad_kmajor_weight_bit_identical(C, B, T):
+    """The merged conv2 input gradient reading conv2's weight K-major (W2k [ci][tap][co], ldb =
+    9C: b128 fragment reads) equals the W2t [tap][co][ci] (transposed-read) launch bit for bit:
+    the same products summed in the same order."""
+    from espnet_amd.layers import subsampling as S
+    prev = S.DGRAD_KMAJOR
+    try:
+        S.DGRAD_KMAJOR = False
+        y0, g0 = _run(C, B, T, True, torch.bfloat16)
+        S.DGRAD_KMAJOR = True
+        y1, g1 = _run(C, B, T, True, torch.bfloat16)
+    finally:
+        S.DGRAD_KMAJOR = prev
+    assert torch.equal(y0, y1)
+    for k in g0:
+        assert torch.equal(g0[k], g1[k]), k
