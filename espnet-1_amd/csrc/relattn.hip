@@ -33,9 +33,14 @@ constexpr int QB = 64;     // forward: query rows per workgroup
 constexpr int KC = 64;     // forward: keys per chunk
 constexpr int NWAVE = 4;
 
-// [rows][64] bf16 image, 128-B rows, 16-B chunk c stored at c ^ swz_k(row) (conflict-free
-// ds_read_b128 over 16 consecutive rows; 2-way on the transposed reads)
-EA_DEV int km_swz(int row) { return (row >> 1) & 7; }
+// [rows][64] bf16 image, 128-B rows, 16-B chunk c stored at c ^ km_swz(row): conflict-free for
+// both access kinds the kernels make — ds_read_b128 fragments over 16 consecutive rows (lane
+// row r0 + (L & 15), chunk 4ks + (L >> 4)) and ds_read_b64_tr_b16 fragments (rows kb + 8g + 4h
+// + q, chunk pair n0/8 + {0, 1}): the rows r, r + 2, r + 8, r + 10 of one transposed read get
+// four different chunk pairs (round 4's (row >> 1) & 7 put r and r + 2 on one pair: 2-way)
+EA_DEV int km_swz(int row) { return (row & 2) | ((row >> 1) & 4); }
+// a lane's LDS-DMA slot swizzle within an 8-row group (km_dma8u): rows ir + (L >> 3), ir % 8 == 0
+EA_DEV int km_chx(int lane) { return (lane & 7) ^ ((lane >> 3) & 2); }
 EA_DEV int km_off(int row, int chunk) { return row * 128 + ((chunk ^ km_swz(row)) << 4); }
 
 // A/B fragment (16 rows from r0, k-step ks of 32): row r0 + lane&15, k = 32ks + 8(lane>>4) ..+7
@@ -841,11 +846,19 @@ EA_DEV bf16x8 km_tr_rows(const char* img, int k0, int k1, int n0, int lane) {
   }
   return out.v;
 }
+// [64 keys][16 queries] bf16 image (dS^T / Pd^T), 32-B rows of four 8-B slots (4 queries each):
+// row r at physical row r ^ (bit 3 of r ? 4 : 0), slot s at s ^ ((physical row >> 2) & 3) —
+// the 8-B stores of 16 consecutive rows and the transposed reads of rows kb + 8g + 4h + q are
+// both conflict-free (plain rows: 4-way stores, 2-way reads)
+EA_DEV int dst_off(int row, int slot) {
+  const int ph = row ^ (((row >> 3) & 1) << 2);
+  return ph * 32 + ((slot ^ ((ph >> 2) & 3)) << 3);
+}
 EA_DEV bf16x8 dst_frag_asm(const char* img, int kb, int lane) {
   const int i = lane & 15, q = i >> 2, p = i & 3, g = lane >> 4;
   union { bf16x8 v; s16x4 h[2]; } out;
 #pragma unroll
-  for (int h = 0; h < 2; ++h) out.h[h] = tr_asm(img + (kb + 8 * g + 4 * h + q) * 32 + p * 8);
+  for (int h = 0; h < 2; ++h) out.h[h] = tr_asm(img + dst_off(kb + 8 * g + 4 * h + q, p));
   return out.v;
 }
 // LDS-DMA of km-image rows [ir, ir+8) (ir % 8 == 0) from global rows src + (r0 + 0..7)*ld (64
@@ -881,8 +894,8 @@ EA_DEV void sum16x4(float (&v)[4]) {
 // LDS-DMA of the 8 km-image rows [ir, ir+8) at image byte `dst` (ir % 8 == 0) from the rows
 // r0 + (lane >> 3) of `src` clamped into [0, rlim), 32-bit byte offsets (the caller checked that
 // rlim rows of ldb bytes fit): one instruction per wave, lane L fills 16-B slot L & 7 of row
-// ir + (L >> 3) with logical chunk (L & 7) ^ km_swz(ir + (L >> 3)).  `chx` = the lane's
-// (L & 7) ^ ((L >> 4) & 3) (ir's own swizzle bit, (ir >> 1) & 4, is applied here).
+// ir + (L >> 3) with logical chunk (L & 7) ^ km_swz(ir + (L >> 3)).  `chx` = km_chx(L), the
+// swizzle's part that depends on L (ir's own swizzle bit, (ir >> 1) & 4, is applied here).
 EA_DEV void km_dma8u(char* dst, int ir, const char* src, uint32_t ldb, int r0, int rlim, int chx, int lane) {
   const int r = min(max(r0 + (lane >> 3), 0), rlim - 1);
   const uint32_t off = __umul24((uint32_t)r, ldb) + ((uint32_t)(chx ^ ((ir >> 1) & 4)) << 4);
@@ -917,7 +930,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwdq2_kernel(AttnP a) {
   const char* vh_ = (const char*)(a.v + (long)b * a.T2 * a.ldv + h * DK);
   const char* ph_ = REL ? (const char*)(a.pp + h * DK) : nullptr;
   const uint32_t ldkb = (uint32_t)a.ldk * 2, ldvb = (uint32_t)a.ldv * 2, ldpb = REL ? (uint32_t)a.ldp * 2 : 0;
-  const int chx = (lane & 7) ^ ((lane >> 4) & 3);
+  const int chx = km_chx(lane);
   // chunk c's K / V rows into buffer c & 1; ring rows [x0, x0 + 8n) (relative to rb0) by groups
   // (32-bit source offsets: the launcher checked the head slices' byte ranges)
   auto dma_kv = [&](int c) {
@@ -1143,7 +1156,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwdq2_kernel(AttnP a) {
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
       const uint2 v = make_uint2(pack_bf16x2(s[t][0], s[t][1]), pack_bf16x2(s[t][2], s[t][3]));
-      st64_asm(dst + (16 * t + lc) * 32 + g * 8, v);
+      st64_asm(dst + dst_off(16 * t + lc, g), v);
       if (REL && (with_dqv || dbd_h)) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
@@ -1318,7 +1331,7 @@ __global__ __launch_bounds__(256, 2) void attn_fwd2_kernel(AttnP a) {
   const char* vh_ = (const char*)(a.v + (long)b * a.T2 * a.ldv + h * DK);
   const char* ph_ = REL ? (const char*)(a.pp + h * DK) : nullptr;
   const uint32_t ldkb = (uint32_t)a.ldk * 2, ldvb = (uint32_t)a.ldv * 2, ldpb = REL ? (uint32_t)a.ldp * 2 : 0;
-  const int chx = (lane & 7) ^ ((lane >> 4) & 3);
+  const int chx = km_chx(lane);
   auto dma_kv = [&](int c) {
     char* kb = sm + L::K + (c & 1) * KC * 128;
     char* vb = sm + L::V + (c & 1) * KC * 128;
@@ -1529,7 +1542,7 @@ __global__ __launch_bounds__(256, 2) void attn_fwd2_kernel(AttnP a) {
     // Pd^T image: key 16t + lc, queries 4g .. 4g+3 in one 8-B store
 #pragma unroll
     for (int t = 0; t < 4; ++t)
-      st64_asm(pt + (16 * t + lc) * 32 + g * 8,
+      st64_asm(pt + dst_off(16 * t + lc, g),
                make_uint2(pack_bf16x2(pv[t][0], pv[t][1]), pack_bf16x2(pv[t][2], pv[t][3])));
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
@@ -1831,7 +1844,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwdkv2_kernel(AttnP a) {
     // 32-bit LDS-DMA source offsets (the launcher checked the head slices' byte ranges)
     const uint32_t ldqub = (uint32_t)a.ldqu * 2, ldqvb = (uint32_t)a.ldqvw * 2, lddob = (uint32_t)a.lddo * 2;
     const uint32_t ldpb = REL ? (uint32_t)a.ldp * 2 : 0;
-    const int chx = (lane & 7) ^ ((lane >> 4) & 3);
+    const int chx = km_chx(lane);
     // lane offsets of the 16 x 32 fragments of a km image at a 16-row boundary
     int loff[2];
 #pragma unroll
