@@ -34,13 +34,14 @@ constexpr int KC = 64;     // forward: keys per chunk
 constexpr int NWAVE = 4;
 
 // [rows][64] bf16 image, 128-B rows, 16-B chunk c stored at c ^ km_swz(row): conflict-free for
-// both access kinds the kernels make — ds_read_b128 fragments over 16 consecutive rows (lane
-// row r0 + (L & 15), chunk 4ks + (L >> 4)) and ds_read_b64_tr_b16 fragments (rows kb + 8g + 4h
-// + q, chunk pair n0/8 + {0, 1}): the rows r, r + 2, r + 8, r + 10 of one transposed read get
-// four different chunk pairs (round 4's (row >> 1) & 7 put r and r + 2 on one pair: 2-way)
-EA_DEV int km_swz(int row) { return (row & 2) | ((row >> 1) & 4); }
+// every access kind the kernels make — ds_read_b128 fragments over 16 consecutive rows (lane
+// row r0 + (L & 15), chunk 4ks + (L >> 4)) and the ds_read_b64_tr_b16 fragments, whose 32-lane
+// halves read chunk pair n0/8 + {0, 1} of rows {r, r+2, r+8, r+10} (km_tr_rows, km_frag_tr)
+// or {r, r+2, r+4, r+6} (km_tr2_asm): each such row set gets four different chunk pairs (found
+// by exhaustive search over 16-row swizzles; round 4's (row >> 1) & 7 was 2-way on both)
+EA_DEV int km_swz(int row) { return (row & 6) ^ (((row >> 3) & 1) * 5); }
 // a lane's LDS-DMA slot swizzle within an 8-row group (km_dma8u): rows ir + (L >> 3), ir % 8 == 0
-EA_DEV int km_chx(int lane) { return (lane & 7) ^ ((lane >> 3) & 2); }
+EA_DEV int km_chx(int lane) { return (lane & 7) ^ ((lane >> 3) & 6); }
 EA_DEV int km_off(int row, int chunk) { return row * 128 + ((chunk ^ km_swz(row)) << 4); }
 
 // A/B fragment (16 rows from r0, k-step ks of 32): row r0 + lane&15, k = 32ks + 8(lane>>4) ..+7
@@ -895,10 +896,10 @@ EA_DEV void sum16x4(float (&v)[4]) {
 // r0 + (lane >> 3) of `src` clamped into [0, rlim), 32-bit byte offsets (the caller checked that
 // rlim rows of ldb bytes fit): one instruction per wave, lane L fills 16-B slot L & 7 of row
 // ir + (L >> 3) with logical chunk (L & 7) ^ km_swz(ir + (L >> 3)).  `chx` = km_chx(L), the
-// swizzle's part that depends on L (ir's own swizzle bit, (ir >> 1) & 4, is applied here).
+// swizzle's part that depends on L (ir's own part, 5 * bit 3 of ir, is applied here).
 EA_DEV void km_dma8u(char* dst, int ir, const char* src, uint32_t ldb, int r0, int rlim, int chx, int lane) {
   const int r = min(max(r0 + (lane >> 3), 0), rlim - 1);
-  const uint32_t off = __umul24((uint32_t)r, ldb) + ((uint32_t)(chx ^ ((ir >> 1) & 4)) << 4);
+  const uint32_t off = __umul24((uint32_t)r, ldb) + ((uint32_t)(chx ^ (((ir >> 3) & 1) * 5)) << 4);
   __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)(src + off),
                                    (__attribute__((address_space(3))) void*)dst, 16, 0, 0);
 }
