@@ -167,7 +167,7 @@ def join_wgrad(device=None):
     if side is not None and (_SIDE_DIRTY.get(main.device, True) or not LAZY_FORK):
         main.wait_stream(side)
         _SIDE_DIRTY[main.device] = False
-    WGRAD_Q.side_dep = False  # whatever the side stream produced is ordered before main now
+    WGRAD_Q.side_events = []  # whatever the side stream produced is ordered before main now
 
 
 def on_side() -> bool:
@@ -556,10 +556,11 @@ class WgradQueue:
         self.items = []
         self.posts = []
         self.pending = 0  # bytes of queued dY / X kept alive
-        # an item was queued on the side stream (its operands may be side-stream products, e.g.
-        # the linear_pos GEMM's dpp) and the main stream has not joined the side stream since:
-        # a flush on another stream waits for the side stream first
-        self.side_dep = False
+        # events recorded on the side stream where items were queued there (their operands may
+        # be side-stream products, e.g. the linear_pos GEMM's dpp) since the main stream last
+        # joined it: a flush on another stream waits for them first (data parallel: no
+        # per-block joins)
+        self.side_events = []
 
     def add(self, dy, x, dw, *, M, N, K, lda, ldb, ldc, beta, post=None) -> bool:
         if not (dy.dtype == torch.bfloat16 and x.dtype == torch.bfloat16 and dw.dtype == torch.float32):
@@ -574,7 +575,9 @@ class WgradQueue:
         if any(lo < it[-1] and it[-2] < hi for it in self.items):
             self.flush()
         if on_side():
-            self.side_dep = True
+            ev = torch.cuda.Event()
+            ev.record()
+            self.side_events.append(ev)
         self.items.append((K, dy, x, dw, M, N, lda, ldb, ldc, beta, lo, hi))
         if post is not None:
             self.posts.append(post)
@@ -587,8 +590,12 @@ class WgradQueue:
         """Launch the queued GEMMs on the current stream."""
         if not self.items:
             return
-        if self.side_dep and not on_side():
-            join_wgrad()
+        if self.side_events:
+            if not on_side():
+                cur = torch.cuda.current_stream()
+                for ev in self.side_events:
+                    cur.wait_event(ev)
+            self.side_events = []
         items = sorted(self.items, key=lambda t: -t[0])
         posts = self.posts
         self.items = []
@@ -752,14 +759,7 @@ class deferred_wgrad:
                 with wgrad(*REDUCE_Q.tensors(), launches=True):
                     REDUCE_Q.flush()
                 WGRAD_Q.flush()
-            elif GRAD_READY is not None and OVERLAP_WGRAD and torch.cuda.is_available():
-                # data parallel: what the bucket hooks left, on the side stream — queued items may
-                # read side-stream products (the linear_pos GEMM's dpp), and the main stream has
-                # not joined the side stream since (allreduce_grads joins it)
-                with wgrad(*deferred_tensors(), launches=True):
-                    flush_deferred()
             else:
-                join_wgrad()
                 flush_deferred()
             if GRAD_READY is None:
                 join_wgrad()  # gradients written on the side stream during the pass are final

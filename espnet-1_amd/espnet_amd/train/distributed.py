@@ -150,8 +150,8 @@ class ArenaDataParallel:
     def allreduce_grads(self):
         """Finish the step's gradient reduction (launch what the hooks did not, wait all)."""
         hip_ops.GRAD_READY = None
-        hip_ops.join_wgrad()  # (queued items may read side-stream products: join first)
         hip_ops.flush_deferred()
+        hip_ops.join_wgrad()
         g = self.arena.grad
         if self._pending is None:
             self._pending = [set(m) for m in self._bucket_mods]
