@@ -35,6 +35,12 @@ class ArenaDataParallel:
         # force_collectives also at world_size 1 (a world-1 RCCL group exercises the same
         # code path on a one-GPU box: capture of the all-reduces, bucket hooks, packing)
         self.active = self.world_size > 1 or (force_collectives and dist.is_initialized())
+        # gloo (device tensors over the CPU transport: the multi-process tests on one GPU) gets
+        # its bucket all-reduces from the main stream after a join: issued from the side stream,
+        # the gloo run's weights drifted from the eager DP reference in about one run in six
+        # (tests/test_dp_ragged_gpu.py; none in 15 runs either with no side stream or with this
+        # ordering).  RCCL keeps them on the side stream, overlapped with the backward.
+        self.ar_main = dist.is_initialized() and dist.get_backend(group) == "gloo"
         arena = model.arena
         self.arena = arena
         n = arena.numel
@@ -142,6 +148,13 @@ class ArenaDataParallel:
         if not done:
             return  # the deferred GEMMs keep accumulating until a bucket needs them
         g = self.arena.grad
+        if self.ar_main:
+            with hip_ops.wgrad(*hip_ops.deferred_tensors(), launches=True):
+                hip_ops.flush_deferred()
+            hip_ops.join_wgrad()
+            for i in done:
+                self._works.append(dist.all_reduce(g[self.buckets[i]], async_op=True, group=self.group))
+            return
         with hip_ops.wgrad(*hip_ops.deferred_tensors(), launches=True):
             hip_ops.flush_deferred()
             for i in done:

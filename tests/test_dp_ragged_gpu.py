@@ -133,7 +133,8 @@ def _worker(rank, world, init, q, mode):
                                         distributed_option=dopt, dp=dp, step_runner=runner)
             modes.append(None if runner is None else runner.mode)
         torch.cuda.synchronize()
-        q.put(dict(rank=rank, log=log, w=m.arena.data.cpu().clone(), modes=modes,
+        spans = [(n, m.arena.offsets[n], m.arena._params[n].numel()) for n in m.arena.names]
+        q.put(dict(rank=rank, log=log, w=m.arena.data.cpu().clone(), spans=spans, modes=modes,
                    captures=[] if runner is None else [c for c, _ in runner.captures],
                    failed=None if runner is None else runner.failed))
     except Exception:
@@ -142,6 +143,16 @@ def _worker(rank, world, init, q, mode):
         raise
     finally:
         dist.destroy_process_group()
+
+
+def _wdiff(a, b):
+    """Which parameters differ between two runs' arenas (a mismatch diagnostic)."""
+    out = []
+    for n, o, k in a["spans"]:
+        x, y = a["w"][o:o + k], b["w"][o:o + k]
+        if not torch.equal(x, y):
+            out.append(f"{n}: {int((x != y).sum())}/{k} differ, max |d| {float((x - y).abs().max()):.3g}")
+    return "; ".join(out[:12]) + (f" ... ({len(out)} params)" if len(out) > 12 else "")
 
 
 def _run(mode):
@@ -171,8 +182,8 @@ def test_ragged_shards_captured_protocol_matches_eager_dp():
     assert cap[1]["captures"] == [3, 4]
     assert cap[0]["modes"] == ["graph", "graph"] and cap[1]["modes"] == ["graph", "graph"]
     # parameters: identical on both ranks and to eager DP
-    assert torch.equal(cap[0]["w"], cap[1]["w"])
-    assert torch.equal(cap[0]["w"], eager[0]["w"])
+    assert torch.equal(cap[0]["w"], cap[1]["w"]), _wdiff(cap[0], cap[1])
+    assert torch.equal(cap[0]["w"], eager[0]["w"]), _wdiff(cap[0], eager[0])
 
 
 def test_ragged_shards_failed_capture_turns_every_rank_eager():
@@ -181,4 +192,5 @@ def test_ragged_shards_failed_capture_turns_every_rank_eager():
     assert fail[0]["log"] == fail[1]["log"] == eager[0]["log"]
     assert fail[1]["failed"] and not fail[0]["failed"]
     assert fail[0]["modes"][-1] == "eager" and fail[1]["modes"][-1] == "eager"
-    assert torch.equal(fail[0]["w"], eager[0]["w"]) and torch.equal(fail[1]["w"], eager[0]["w"])
+    assert torch.equal(fail[0]["w"], eager[0]["w"]), _wdiff(fail[0], eager[0])
+    assert torch.equal(fail[1]["w"], eager[0]["w"]), _wdiff(fail[1], eager[0])
