@@ -747,7 +747,6 @@ __global__ __launch_bounds__(256) void dwconv_bwd_k_kernel(int B, int T, int C, 
   constexpr int P = (K - 1) / 2, TT = 4 * R, RL = TT + K - 1, WIN = R + K - 1;
   constexpr int SM = 2 * RL * DW_CT > 4 * (K + 1) * DW_CT ? 2 * RL * DW_CT : 4 * (K + 1) * DW_CT;
   __shared__ float sm[SM];
-  __shared__ float wsm[K * DW_CT];  // [k][c]
   float* tdy = sm;                 // dy rows t0-(K-1-P) .. t0+TT-1+P
   float* tx = sm + RL * DW_CT;     // x rows  t0-P .. t0+TT-1+(K-1-P)
   const int ntt = ea_cdiv(T, TT);
@@ -755,10 +754,11 @@ __global__ __launch_bounds__(256) void dwconv_bwd_k_kernel(int B, int T, int C, 
   const int c0 = blockIdx.y * DW_CT;
   const int cc = threadIdx.x % DW_CT, tq = threadIdx.x / DW_CT;
   const int c = c0 + cc;
-  for (int i = threadIdx.x; i < DW_CT * K; i += 256) {
-    const int ci = i / K, k = i - ci * K;
-    wsm[k * DW_CT + ci] = c0 + ci < C ? w[(long)c0 * K + i] : 0.f;
-  }
+  // the channel's K taps in registers (an LDS copy cost the block 8 KB: 47 KB fit three blocks
+  // per CU, 55 KB two)
+  float wr[K];
+#pragma unroll
+  for (int k = 0; k < K; ++k) wr[k] = c < C ? w[(long)c * K + k] : 0.f;
   // GLU: the gate rows this thread's dx store needs, loaded first (their latency hides behind
   // the tile loads; the LDS budget, not registers, bounds this kernel's occupancy)
   bf16 ga[GLU ? R : 1], gb[GLU ? R : 1];
@@ -826,7 +826,7 @@ __global__ __launch_bounds__(256) void dwconv_bwd_k_kernel(int B, int T, int C, 
       for (int j = 0; j < R; ++j) acc[j] = 0.f;
 #pragma unroll
       for (int k = 0; k < K; ++k) {
-        const float wk = wsm[k * DW_CT + cc];
+        const float wk = wr[k];
 #pragma unroll
         for (int j = 0; j < R; ++j) acc[j] += wk * win[j - k + K - 1];
       }
