@@ -16,12 +16,17 @@ of gradients this equals DDP's mean of (loss_r * w_r / sum(w) * world).
 """
 from __future__ import annotations
 
+import os
 from typing import Dict, List
 
 import torch
 import torch.distributed as dist
 
 from .. import hip_ops
+
+# EA_DP_AR_MAIN=1: every backend takes gloo's ordering (RCCL: DP rehearsal -4.4%,
+# profiles/r5_dp_ar_main_ab.txt)
+_AR_MAIN = os.environ.get("EA_DP_AR_MAIN", "0") != "0"
 
 
 class ArenaDataParallel:
@@ -40,7 +45,7 @@ class ArenaDataParallel:
         # the gloo run's weights drifted from the eager DP reference in about one run in six
         # (tests/test_dp_ragged_gpu.py; none in 15 runs either with no side stream or with this
         # ordering).  RCCL keeps them on the side stream, overlapped with the backward.
-        self.ar_main = dist.is_initialized() and dist.get_backend(group) == "gloo"
+        self.ar_main = dist.is_initialized() and (dist.get_backend(group) == "gloo" or _AR_MAIN)
         arena = model.arena
         self.arena = arena
         n = arena.numel
