@@ -164,6 +164,13 @@ class ArenaDataParallel:
             hip_ops.flush_deferred()
             for i in done:
                 self._works.append(dist.all_reduce(g[self.buckets[i]], async_op=True, group=self.group))
+        if not prefix.startswith("encoder."):
+            # after the decoder / CTC head's buckets the main stream joins the side stream before
+            # the encoder backward: without it the 2-rank DP runs drifted from eager DP in ~5% of
+            # the runs (the side stream's flush of the decoder's weight gradients running beside
+            # the encoder backward; not located further: a join after the encoder blocks' hooks
+            # alone did not remove it, after these alone did, 18 of 18 runs).  DP rehearsal -1%.
+            hip_ops.join_wgrad()
 
     def allreduce_grads(self):
         """Finish the step's gradient reduction (launch what the hooks did not, wait all)."""
