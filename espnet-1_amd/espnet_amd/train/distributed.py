@@ -46,6 +46,9 @@ class ArenaDataParallel:
         # (tests/test_dp_ragged_gpu.py; none in 15 runs either with no side stream or with this
         # ordering).  RCCL keeps them on the side stream, overlapped with the backward.
         self.ar_main = dist.is_initialized() and (dist.get_backend(group) == "gloo" or _AR_MAIN)
+        # Repeated at the end of round 5 this ordering still drifted in one run of 16, and so did
+        # a gloo process with the side stream off (profiles/r5_ragged_repeat.txt): the drift is
+        # not the side stream's, and its cause is still open.
         arena = model.arena
         self.arena = arena
         n = arena.numel
