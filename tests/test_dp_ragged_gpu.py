@@ -162,7 +162,7 @@ def _matches_eager(a, e):
     after Adam's per-element normalisation), with or without the weight-gradient side stream
     (profiles/r5_ragged_repeat.txt).  Until that run-to-run drift is located the check is
     bit-equal-or-close — relative L2 of the whole parameter arena under 5e-3 (8.5e-4 the largest
-    seen) — and a drifting
+    measured) — and a drifting
     run is reported as a warning."""
     if torch.equal(a["w"], e["w"]):
         return
