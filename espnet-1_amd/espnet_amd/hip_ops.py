@@ -86,6 +86,25 @@ class EventProbe:
 
 
 PROBE = None
+# Stream-ordering diagnostics (tests/test_dp_streams_gpu.py): EA_DEBUG_DELAY_NS holds every side /
+# auxiliary stream segment for that long before its first launch (ea_debug_spin), so a consumer
+# that misses its dependency on a side-stream producer reads stale data in every run;
+# EA_DEBUG_SERIAL=1 makes the main stream join the side / auxiliary stream at the end of every
+# segment (the overlap keeps its launch order but nothing runs concurrently).  Read at call time.
+DEBUG_DELAY_NS = int(os.environ.get("EA_DEBUG_DELAY_NS", "0"))
+DEBUG_SERIAL = os.environ.get("EA_DEBUG_SERIAL", "0") != "0"
+
+
+def _debug_enter(side):
+    if DEBUG_DELAY_NS:
+        lib.ea_debug_spin(DEBUG_DELAY_NS, side.cuda_stream)
+
+
+def _debug_exit(main, side):
+    if DEBUG_SERIAL:
+        main.wait_stream(side)
+
+
 # run weight-gradient GEMMs / bias reductions on a side stream (EA_OVERLAP_WGRAD=0: serial, for profiling)
 OVERLAP_WGRAD = os.environ.get("EA_OVERLAP_WGRAD", "1") != "0"
 _SIDE = {}
@@ -132,11 +151,14 @@ class wgrad:
                 t.record_stream(side)
         self.ctx = torch.cuda.stream(side)
         self.ctx.__enter__()
+        self.streams = (main, side)
+        _debug_enter(side)
         return self
 
     def __exit__(self, *exc):
         if self.ctx is not None:
             self.ctx.__exit__(*exc)
+            _debug_exit(*self.streams)
         return False
 
 
@@ -216,11 +238,14 @@ class aux:
                 t.record_stream(st)
         self.ctx = torch.cuda.stream(st)
         self.ctx.__enter__()
+        self.streams = (main, st)
+        _debug_enter(st)
         return self
 
     def __exit__(self, *exc):
         if self.ctx is not None:
             self.ctx.__exit__(*exc)
+            _debug_exit(*self.streams)
         return False
 
 

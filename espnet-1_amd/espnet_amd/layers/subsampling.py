@@ -18,7 +18,7 @@ import os
 import torch
 from torch import nn
 
-from .._lib import CONV_DGRAD, CONV_FWD, CONV_WGRAD, ConvGeo
+from .._lib import CONV_DGRAD, CONV_FWD, CONV_WGRAD, GEMM_PIPE, ConvGeo
 from .common import (ACT_RELU, EPI_ACT, EPI_DACT, EPI_STORE, F32, Bound, empty, lib, ops, rup)
 
 
@@ -45,7 +45,8 @@ FUSE_CONV1_WGRAD = os.environ.get("EA_FUSE_CONV1_WGRAD", "1") != "0"
 # ... with conv1's ReLU mask from support bits written by the forward (else the bf16 x1p rows)
 CONV1_POS_BITS = os.environ.get("EA_CONV1_POS_BITS", "1") != "0"
 # ... and the four parity classes in one launch (EA_MERGED_DGRAD=0: one launch per class)
-MERGED_DGRAD = os.environ.get("EA_MERGED_DGRAD", "1") != "0"
+# (the merged launch is a gemm_pipe kernel: with EA_GEMM_PIPE=0 the per-class path runs)
+MERGED_DGRAD = os.environ.get("EA_MERGED_DGRAD", "1") != "0" and GEMM_PIPE != 0
 # ... reading conv2's weight K-major, W2k [ci][tap][co] (EA_DGRAD_KMAJOR=0: W2t [tap][co][ci])
 DGRAD_KMAJOR = os.environ.get("EA_DGRAD_KMAJOR", "1") != "0"
 

@@ -31,7 +31,7 @@ _AR_MAIN = os.environ.get("EA_DP_AR_MAIN", "0") != "0"
 
 class ArenaDataParallel:
     def __init__(self, model, bucket_mb: float = 64.0, group=None, overlap: bool = True,
-                 force_collectives: bool = False):
+                 force_collectives: bool = False, check_issue: bool = None):
         self.model = model
         self.group = group
         self.world_size = dist.get_world_size(group) if dist.is_initialized() else 1
@@ -89,6 +89,14 @@ class ArenaDataParallel:
         self.overlap = overlap
         self._pending = None
         self._works = []
+        # check_issue (EA_DP_CHECK_ISSUE=1; diagnostic, eager steps only): a bucket's all-reduce
+        # is not started at its issue point; a copy of the bucket is taken there (on the issuing
+        # stream, where the collective would read it) and allreduce_grads compares it with the
+        # bucket once the backward has ended, before reducing the buckets in issue order.  A
+        # gradient written into a bucket after its all-reduce was issued raises, naming the
+        # parameters.
+        self.check_issue = (os.environ.get("EA_DP_CHECK_ISSUE", "0") != "0") if check_issue is None else check_issue
+        self._held = []
         if self.active:
             dist.broadcast(arena.data, 0, group=group)
             arena.refresh_shadow()
@@ -155,18 +163,17 @@ class ArenaDataParallel:
                     done.append(i)
         if not done:
             return  # the deferred GEMMs keep accumulating until a bucket needs them
-        g = self.arena.grad
         if self.ar_main:
             with hip_ops.wgrad(*hip_ops.deferred_tensors(), launches=True):
                 hip_ops.flush_deferred()
             hip_ops.join_wgrad()
             for i in done:
-                self._works.append(dist.all_reduce(g[self.buckets[i]], async_op=True, group=self.group))
+                self._issue(i)
             return
         with hip_ops.wgrad(*hip_ops.deferred_tensors(), launches=True):
             hip_ops.flush_deferred()
             for i in done:
-                self._works.append(dist.all_reduce(g[self.buckets[i]], async_op=True, group=self.group))
+                self._issue(i)
         if not prefix.startswith("encoder."):
             # after the decoder / CTC head's buckets the main stream joins the side stream before
             # the encoder backward: without it the 2-rank DP runs drifted from eager DP in ~5% of
@@ -175,18 +182,48 @@ class ArenaDataParallel:
             # alone did not remove it, after these alone did, 18 of 18 runs).  DP rehearsal -1%.
             hip_ops.join_wgrad()
 
+    def _issue(self, i):
+        """Start bucket i's SUM all-reduce from the current stream (async)."""
+        g = self.arena.grad[self.buckets[i]]
+        if self.check_issue:
+            self._held.append((i, g.clone()))
+            return
+        self._works.append(dist.all_reduce(g, async_op=True, group=self.group))
+
+    def _check_held(self):
+        hip_ops.join_aux()
+        held, self._held = self._held, []
+        bad = []
+        for i, snap in held:
+            b = self.buckets[i]
+            g = self.arena.grad[b]
+            if not torch.equal(g, snap):
+                for name in self.arena.names:
+                    o = self.arena.offsets[name]
+                    lo, hi = max(o, b.start), min(o + self.arena._params[name].numel(), b.stop)
+                    if lo < hi and not torch.equal(self.arena.grad[lo:hi], snap[lo - b.start:hi - b.start]):
+                        bad.append(f"bucket {i}: {name}")
+            self._works.append(dist.all_reduce(g, async_op=True, group=self.group))
+        if bad:
+            for w in self._works:
+                w.wait()
+            self._works = []
+            self._pending = None
+            raise RuntimeError("gradients written after their bucket's all-reduce was issued: " + "; ".join(bad))
+
     def allreduce_grads(self):
         """Finish the step's gradient reduction (launch what the hooks did not, wait all)."""
         hip_ops.GRAD_READY = None
         hip_ops.flush_deferred()
         hip_ops.join_wgrad()
-        g = self.arena.grad
         if self._pending is None:
             self._pending = [set(m) for m in self._bucket_mods]
         for i, mods in enumerate(self._pending):
             if mods:
                 mods.clear()
-                self._works.append(dist.all_reduce(g[self.buckets[i]], async_op=True, group=self.group))
+                self._issue(i)
+        if self._held:
+            self._check_held()
         for w in self._works:
             w.wait()
         self._works = []

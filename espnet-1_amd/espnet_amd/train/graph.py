@@ -126,10 +126,11 @@ class CapturedTrainStep:
             self.enabled = False  # gloo collectives (host copies) cannot be captured
         if enabled and dp is not None and dp.active and _backend(dp.group) == "nccl":
             import os
-            import warnings
             if os.environ.get("TORCH_NCCL_CUDA_EVENT_CACHE") != "0":
-                warnings.warn("TORCH_NCCL_CUDA_EVENT_CACHE is not '0' for this process group: call "
-                              "train.graph.prepare_nccl_env() before init_process_group")
+                # recycled RCCL events inside captured collectives intermittently abort the
+                # process: refuse instead of failing some runs later
+                raise RuntimeError("TORCH_NCCL_CUDA_EVENT_CACHE is not '0' for this process group: call "
+                                   "train.graph.prepare_nccl_env() before init_process_group")
         # "graph" once steps replay, "eager" once capture was given up; None while the
         # warm-up steps run
         self.mode = None if self.enabled else "eager"

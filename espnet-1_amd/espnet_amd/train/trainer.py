@@ -142,13 +142,20 @@ class Trainer:
                 # storage: single-process runs report loss / accum_grad
                 stats = dict(stats, loss=stats["loss"] / accum_grad)
         _stamp(1)
-        if dp is not None and dp.active:
+        # gradients are all-reduced on the micro-step that updates (accum_grad > 1: the earlier
+        # micro-steps accumulate locally).  The SUM over ranks of the accumulated gradients is
+        # then sum_r sum_k g_k,r — DDP's result (trainer.py:229-244 reduces every micro-step's
+        # accumulated .grad with a mean: mean_r(S + g_k,r) = S + mean_r g_k,r, the loss
+        # weighting making mean and SUM agree); reducing every micro-step's SUM would count
+        # the earlier micro-steps world_size times.
+        reduce_now = dp is not None and dp.active and iiter % accum_grad == 0
+        if reduce_now:
             dp.begin_backward()
         # the Linear weight gradients of the pass are queued and run as grouped GEMMs (at the
         # end of the pass, or per bucket from the DP hooks)
         with ops.deferred_wgrad():
             loss.backward()
-        if dp is not None and dp.active:
+        if reduce_now:
             dp.allreduce_grads()
         _stamp(2)
         grad_norm = None

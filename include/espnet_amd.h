@@ -216,6 +216,11 @@ int ea_phase_stamp_opt(unsigned long long* state, float* ring, int cap, int phas
                        void* stream);
 int ea_probe_begin(unsigned long long* slots, void* stream);
 int ea_probe_end(unsigned long long* slots, void* stream);
+/* Stream-ordering diagnostic: hold `stream` for ns nanoseconds (0 <= ns <= 1e8) with one
+ * sleeping single-lane workgroup.  hip_ops launches it at the head of every side / auxiliary
+ * stream segment under EA_DEBUG_DELAY_NS, so a missing cross-stream dependency shows up in
+ * every run instead of now and then (tests/test_dp_streams_gpu.py).  Not on the product path. */
+int ea_debug_spin(long ns, void* stream);
 
 /* ---------------------------------------------------------------- normalisation */
 

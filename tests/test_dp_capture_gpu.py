@@ -74,8 +74,11 @@ def _rccl_worker(init, q):
     import torch.distributed as dist
     from espnet_amd.train.distributed import ArenaDataParallel
     from espnet_amd.train.graph import CapturedTrainStep
+    from espnet_amd.train.graph import prepare_nccl_env
     from espnet_amd.train.trainer import Trainer
     torch.cuda.set_device(0)
+    prepare_nccl_env()  # fresh events for the captured collectives (read at group construction)
+    assert os.environ["TORCH_NCCL_CUDA_EVENT_CACHE"] == "0"
     dist.init_process_group("nccl", init_method=f"file://{init}", rank=0, world_size=1,
                             device_id=torch.device("cuda", 0))
     try:
@@ -140,9 +143,10 @@ def _gloo_worker(rank, world, init, q):
         dp = ArenaDataParallel(m, bucket_mb=0.25, overlap=overlap)
         full = {k: torch.from_numpy(v) for k, v in section(d, "in0").items()}
         batch = {k: v[rank::world] for k, v in full.items()}
-        # accum_grad=2, iiter=1: no optimizer step, the reduced gradients stay in the arena
-        loss, stats, weight, gn = Trainer.train_one_step(m, batch, opt, sched, grad_clip=5.0, dp=dp,
-                                                         accum_grad=2, iiter=1)
+        # no parameter update and no zero_grad: the reduced gradients stay in the arena
+        opt.step = lambda *a, **k: None
+        opt.zero_grad = lambda *a, **k: None
+        loss, stats, weight, gn = Trainer.train_one_step(m, batch, opt, sched, grad_clip=5.0, dp=dp)
         torch.cuda.synchronize()
         out[overlap] = dict(loss=float(loss), stats={k: float(v) for k, v in stats.items()},
                             weight=int(weight), grad=m.arena.grad.cpu().clone())
