@@ -43,7 +43,7 @@ def poison():
     torch.Tensor.new_empty = lambda self, *a, **k: fill(ne(self, *a, **k))
 
 
-def one_run(args, hog):
+def one_run(args, hog, runner=False):
     import test_dp_capture_gpu as C
     import test_dp_ragged_gpu as R
     from espnet_amd.train.trainer import Trainer
@@ -60,14 +60,22 @@ def one_run(args, hog):
         return orig(*a, **k)
 
     opt.compute_grad_norm = snap
-    for b in R._global_batches(6):
+    run = None
+    if runner:
+        from espnet_amd.train.graph import CapturedTrainStep
+        run = CapturedTrainStep(m, opt, sched, grad_clip=5.0, dp=dp, warmup=1, pseudo_capture=True)
+    for i, b in enumerate(R._global_batches(args.steps)):
         if hog is not None:
             src, dst, n, st = hog
             st.wait_stream(torch.cuda.current_stream())
             with torch.cuda.stream(st):
                 for _ in range(n):
                     dst.copy_(src)
-        Trainer.train_one_step(m, {k: v.to("cuda:0") for k, v in b.items()}, opt, sched, grad_clip=5.0, dp=dp)
+        b = {k: v.to("cuda:0") for k, v in b.items()}
+        if run is not None:
+            run(b, iiter=i + 1)
+        else:
+            Trainer.train_one_step(m, b, opt, sched, grad_clip=5.0, dp=dp)
     torch.cuda.synchronize()
     spans = [(n, m.arena.offsets[n], m.arena._params[n].numel()) for n in m.arena.names]
     return grads, m.arena.data.cpu().clone(), spans
@@ -92,6 +100,9 @@ def main():
     ap.add_argument("--serial", action="store_true")
     ap.add_argument("--hog", type=int, default=0)
     ap.add_argument("--dp", action="store_true")
+    ap.add_argument("--steps", type=int, default=6)
+    ap.add_argument("--modes", default="", help="comma list of serial / delay / runner / runner-delay / "
+                    "runner-serial: one run each, compared with the first (overrides --runs)")
     args = ap.parse_args()
     if args.poison:
         poison()
@@ -108,6 +119,22 @@ def main():
         n = args.hog * 2 ** 20 // 4
         hog = (torch.ones(n, device="cuda:0"), torch.empty(n, device="cuda:0"), 64, torch.cuda.Stream())
     tag = " ".join(f"{k}={v}" for k, v in vars(args).items())
+    if args.modes:
+        res = []
+        for mode in args.modes.split(","):
+            hip_ops.DEBUG_DELAY_NS = 300_000 if "delay" in mode else args.delay_ns
+            hip_ops.DEBUG_SERIAL = "serial" in mode
+            g, w, spans = one_run(args, hog, runner=mode.startswith("runner"))
+            res.append((mode, g, w))
+        m0, g0, w0 = res[0]
+        for mode, g, w in res[1:]:
+            first = next((i for i, (a, b) in enumerate(zip(g, g0)) if not torch.equal(a, b)), None)
+            if first is None:
+                print(f"[{tag}] {mode} == {m0}" + ("" if torch.equal(w, w0) else " (grads; weights differ)"), flush=True)
+            else:
+                print(f"[{tag}] {mode} != {m0}: first differing step {first}: "
+                      + "; ".join(diff(g[first], g0[first], spans)[:12]), flush=True)
+        return
     ref_g, ref_w, spans = one_run(args, hog)
     nan_steps = [i for i, g in enumerate(ref_g) if torch.isnan(g).any()]
     if nan_steps:
