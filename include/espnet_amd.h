@@ -17,6 +17,8 @@
 #ifndef ESPNET_AMD_H
 #define ESPNET_AMD_H
 
+#include <stddef.h>
+
 #ifdef __cplusplus
 extern "C" {
 #endif
@@ -221,6 +223,13 @@ int ea_probe_end(unsigned long long* slots, void* stream);
  * stream segment under EA_DEBUG_DELAY_NS, so a missing cross-stream dependency shows up in
  * every run instead of now and then (tests/test_dp_streams_gpu.py).  Not on the product path. */
 int ea_debug_spin(long ns, void* stream);
+/* Diagnostic device allocator for torch.cuda.memory.CUDAPluggableAllocator (the pluggable
+ * allocator's malloc / free signatures): each allocation is a fresh hipMalloc with a zeroed
+ * body and a 64 KiB tail guard of 0xFF bytes (NaN in f32 / bf16), so a kernel reading past
+ * the end of a buffer turns its output NaN deterministically; free synchronises the device
+ * before hipFree.  Never on the product path (scripts/dp_drift_diag.py --guard). */
+void* ea_guard_malloc(size_t size, int device, void* stream);
+void ea_guard_free(void* ptr, size_t size, int device, void* stream);
 
 /* ---------------------------------------------------------------- normalisation */
 

@@ -58,3 +58,10 @@ def test_header_symbols_exported():
     assert len(protos) >= 30
     for name in protos:
         assert hasattr(dll, name), name
+    # the entry points that do not return int (the diagnostic allocator's pair)
+    import re
+    src = re.sub(r"/\*.*?\*/", "", open(_lib.HEADER).read(), flags=re.S)
+    others = re.findall(r"\bvoid\s*\*?\s*(ea_\w+)\s*\(", src)
+    assert others
+    for name in others:
+        assert hasattr(dll, name), name
