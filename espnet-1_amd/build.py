@@ -37,11 +37,20 @@ def _stale(out, deps):
     return any(os.path.getmtime(d) > t for d in deps)
 
 
+def _file_flags(src):
+    """Per-file hipcc flags from a `// hipcc-flags: ...` line in the first lines of the source."""
+    with open(src) as f:
+        for _, line in zip(range(20), f):
+            if line.startswith("// hipcc-flags:"):
+                return line.split(":", 1)[1].split()
+    return []
+
+
 def _compile(src, force, obj_dir=OBJ, extra=()):
     obj = os.path.join(obj_dir, os.path.basename(src) + ".o")
     if not force and not _stale(obj, _deps(src)):
         return obj, None
-    cmd = [HIPCC, *CFLAGS, *extra, "-c", src, "-o", obj]
+    cmd = [HIPCC, *CFLAGS, *_file_flags(src), *extra, "-c", src, "-o", obj]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         return obj, f"{' '.join(cmd)}\n{r.stdout}\n{r.stderr}"

@@ -1,6 +1,7 @@
 // Memory-bound kernels of the ASR step: input prep (utterance MVN, subsampled lengths,
 // sos/eos), dropout/cast, weight repacking, GLU, q+pos_bias, embeddings, argmax.
 // All grid-stride, coalesced along the contiguous (channel) dimension.
+// hipcc-flags: -fno-slp-vectorize
 #include "common.h"
 
 #include <cstdlib>

@@ -29,19 +29,10 @@ def rup(n, m=8):
     return (n + m - 1) // m * m
 
 
-# EA_POISON_EMPTY=1 (diagnostic): the block Functions' fresh buffers start as NaN, so a kernel
-# that reads an element before any kernel wrote it turns its outputs NaN instead of depending
-# on what the allocator's block last held (the open DP drift)
-POISON_EMPTY = os.environ.get("EA_POISON_EMPTY", "0") != "0"
-
-
 def empty(*shape, dtype=F32, device="cuda"):
     if len(shape) == 1 and isinstance(shape[0], (tuple, list, torch.Size)):
         shape = tuple(shape[0])
-    t = torch.empty(shape, dtype=dtype, device=device)
-    if POISON_EMPTY and t.is_floating_point():
-        t.fill_(float("nan"))
-    return t
+    return torch.empty(shape, dtype=dtype, device=device)
 
 
 FUSED_ATTN = os.environ.get("EA_FUSED_ATTN", "1") != "0"

@@ -24,11 +24,6 @@ import torch.distributed as dist
 
 from .. import hip_ops
 
-# EA_DP_AR_MAIN=1: every backend takes gloo's ordering (RCCL: DP rehearsal -4.4%,
-# profiles/r5_dp_ar_main_ab.txt)
-_AR_MAIN = os.environ.get("EA_DP_AR_MAIN", "0") != "0"
-
-
 class ArenaDataParallel:
     def __init__(self, model, bucket_mb: float = 64.0, group=None, overlap: bool = True,
                  force_collectives: bool = False, check_issue: bool = None):
@@ -40,15 +35,12 @@ class ArenaDataParallel:
         # force_collectives also at world_size 1 (a world-1 RCCL group exercises the same
         # code path on a one-GPU box: capture of the all-reduces, bucket hooks, packing)
         self.active = self.world_size > 1 or (force_collectives and dist.is_initialized())
-        # gloo (device tensors over the CPU transport: the multi-process tests on one GPU) gets
-        # its bucket all-reduces from the main stream after a join: issued from the side stream,
-        # the gloo run's weights drifted from the eager DP reference in about one run in six
-        # (tests/test_dp_ragged_gpu.py; none in 15 runs either with no side stream or with this
-        # ordering).  RCCL keeps them on the side stream, overlapped with the backward.
-        self.ar_main = dist.is_initialized() and (dist.get_backend(group) == "gloo" or _AR_MAIN)
-        # Repeated at the end of round 5 this ordering still drifted in one run of 16, and so did
-        # a gloo process with the side stream off (profiles/r5_ragged_repeat.txt): the drift is
-        # not the side stream's, and its cause is still open.
+        # Every backend issues the bucket all-reduces the same way (from the weight-gradient
+        # side stream, overlapped with the rest of the backward): the gloo tests run the
+        # ordering RCCL runs in production.  (Round 5's intermittent two-process drift, which
+        # once moved gloo's all-reduces to the main stream, was a kernel's, not the ordering's:
+        # the conv1 forward sometimes computed a few wrong outputs under packed-FP32 code,
+        # DESIGN.md §5 round 6, tests/test_dp_ragged_gpu.py.)
         arena = model.arena
         self.arena = arena
         n = arena.numel
@@ -163,24 +155,10 @@ class ArenaDataParallel:
                     done.append(i)
         if not done:
             return  # the deferred GEMMs keep accumulating until a bucket needs them
-        if self.ar_main:
-            with hip_ops.wgrad(*hip_ops.deferred_tensors(), launches=True):
-                hip_ops.flush_deferred()
-            hip_ops.join_wgrad()
-            for i in done:
-                self._issue(i)
-            return
         with hip_ops.wgrad(*hip_ops.deferred_tensors(), launches=True):
             hip_ops.flush_deferred()
             for i in done:
                 self._issue(i)
-        if not prefix.startswith("encoder."):
-            # after the decoder / CTC head's buckets the main stream joins the side stream before
-            # the encoder backward: without it the 2-rank DP runs drifted from eager DP in ~5% of
-            # the runs (the side stream's flush of the decoder's weight gradients running beside
-            # the encoder backward; not located further: a join after the encoder blocks' hooks
-            # alone did not remove it, after these alone did, 18 of 18 runs).  DP rehearsal -1%.
-            hip_ops.join_wgrad()
 
     def _issue(self, i):
         """Start bucket i's SUM all-reduce from the current stream (async)."""

@@ -4,7 +4,7 @@ the same weights; every run is compared with run 0 per step: the local loss, the
 contents handed to each all-reduce (a stream-ordered copy at the issue point, --snap) and the
 reduced gradient arena.  The first step and tensor that differ name the segment.
 
-    dp_drift_diag.py [--runs R] [--steps S] [--side] [--no-overlap] [--snap] [--fresh]
+    dp_drift_diag.py [--runs R] [--steps S] [--no-overlap] [--snap] [--fresh]
 
 --fresh: every run is a new pair of processes (as every run of the test is), running the
 ragged test's own protocol (Trainer.train_one_epoch, two epochs, rank 0 one step short in the
@@ -54,8 +54,6 @@ def worker(rank, world, init, args):
     for run in range(args.runs):
         _, m, opt, sched = C._setup(amp=True, dropout=0.1)
         dp = ArenaDataParallel(m, bucket_mb=0.25)
-        if args.side:
-            dp.ar_main = False
         rec = dict(loss=[], grad=[], snap=[])
         orig = opt.compute_grad_norm
 
@@ -140,8 +138,6 @@ def fresh_worker(rank, world, init, args, out):
     dmod.dist.all_reduce = ar
     _, m, opt, sched = C._setup(amp=True, dropout=0.1)
     dp = ArenaDataParallel(m, bucket_mb=0.25)
-    if args.side:
-        dp.ar_main = False
     n = m.arena.numel
     recs = []
     orig = opt.compute_grad_norm
@@ -155,6 +151,103 @@ def fresh_worker(rank, world, init, args, out):
         return orig(*a, **k)
 
     opt.compute_grad_norm = cg
+    # the step's inputs (as the forward receives them), encoder output and local loss: stream-
+    # ordered device copies, read back at the next compute_grad_norm
+    fwd_rec, fwd_pending = [], []
+    real_fwd = m.forward
+
+    # every encoder block's output (subsampling, conformer layers), the bf16 weight shadow and
+    # the dropout salt as the forward starts
+    from espnet_amd.layers import conformer as lconf, subsampling as lsub
+    blk = []
+    for cls in (lsub.SubsampleFn, lconf.ConformerBlockFn):
+        f0 = cls.forward
+
+        def wrapped(ctx, *a, _f0=f0, _n=cls.__name__):
+            out = _f0(ctx, *a)
+            if _n == "SubsampleFn" and getattr(ctx, "implicit", False) and dup:
+                s0, s2, pre, post, _ = dup.pop()
+                x1 = ctx.save[1].view(-1)[:s0.numel()]
+                md = lambda a_, b_: (a_.float() - b_.float()).abs().max().view(1)  # noqa: E731
+                for nm_, u, v in (("01", s0, x1), ("12", x1, s2)):
+                    u16, v16 = u.view(torch.int16), v.view(torch.int16)
+                    idx = torch.nonzero(u16 != v16).view(-1)
+                    if idx.numel():
+                        dumps.append((len(fwd_rec) + len(fwd_pending), nm_, idx.cpu().numpy(), u16[idx].cpu().numpy(),
+                                      v16[idx].cpu().numpy(), v.data_ptr() if nm_ == "12" else u.data_ptr()))
+                blk.append(("sub_dupdiff", torch.cat([md(s0, x1), md(x1, s2), md(s0, s2),
+                                                      md(pre[0], post[0]), md(pre[1], post[1]), md(pre[2], post[2]),
+                                                      md(pre[0], ctx.save[0])])))
+                dup.clear()
+            if _n == "SubsampleFn" and getattr(ctx, "implicit", False):
+                for nm, t in zip(("feats", "x1p", "w2", "x2", "wl", "pos1"), ctx.save):
+                    if t is not None:
+                        blk.append((f"sub_{nm}", t.detach().clone()))
+            blk.append((_n, out.detach().clone()))
+            return out
+        cls.forward = staticmethod(wrapped)
+
+    # conv1 run twice: into x1p, then into a scratch copy right behind it on the same stream; the
+    # subsampling wrapper compares the two (different -> conv1's inputs changed while it ran, or
+    # something wrote into x1p after conv1)
+    from espnet_amd._lib import lib as _lib
+    real_c1 = _lib.ea_conv1_fwd2
+    dup = []
+
+    ctx_holder = {}
+    dumps = []
+
+    def c1(B, T, F, C, x, w, bias, y, dt, pos, st):
+        T1, F1 = (T - 3) // 2 + 1, (F - 3) // 2 + 1
+        n = B * T1 * F1 * C
+        s0 = torch.empty(n, dtype=torch.bfloat16, device="cuda:0")
+        s2 = torch.empty(n, dtype=torch.bfloat16, device="cuda:0")
+        # stream-ordered copies of the inputs just before / after (via the known views)
+        feats, wv, bv = ctx_holder["x"], ctx_holder["w"], ctx_holder["b"]
+        assert feats.data_ptr() == x and wv.data_ptr() == w and bv.data_ptr() == bias
+        pre = (feats.clone(), wv.clone(), bv.clone())
+        real_c1(B, T, F, C, x, w, bias, s0.data_ptr(), dt, 0, st)
+        real_c1(B, T, F, C, x, w, bias, y, dt, pos, st)
+        real_c1(B, T, F, C, x, w, bias, s2.data_ptr(), dt, 0, st)
+        post = (feats.clone(), wv.clone(), bv.clone())
+        dup.append((s0, s2, pre, post, y))
+
+    _lib.ea_conv1_fwd2 = c1
+    real_fi = lsub.SubsampleFn._forward_implicit
+
+    def fi(ctx, feats, mm, seed, training, *a):
+        ctx_holder.update(x=feats, w=mm._b.f("conv.0.weight"), b=mm._b.f("conv.0.bias"))
+        return real_fi(ctx, feats, mm, seed, training, *a)
+
+    lsub.SubsampleFn._forward_implicit = staticmethod(fi)
+
+    _lib.ea_conv1_fwd2 = c1
+
+    def fwd(**kw):
+        ins = {k: kw[k].detach().clone() for k in ("speech", "speech_lengths", "text", "text_lengths")}
+        ins["shadow"] = m.arena.shadow.detach().clone()
+        ins["salt"] = m._rng_salt.detach().clone()
+        blk.clear()
+        loss, stats, weight = real_fwd(**kw)
+        for i, (nm, t) in enumerate(blk):
+            ins[f"blk{i}" if not nm.startswith("sub_") else f"s{nm}"] = t
+        blk.clear()
+        eo = m._last_encoder_out[0].detach().clone()
+        fwd_pending.append((ins, eo, loss.detach().clone(), {k: v.detach().clone() for k, v in stats.items()
+                                                              if v is not None}))
+        return loss, stats, weight
+
+    m.forward = fwd
+    real_cg = opt.compute_grad_norm
+
+    def cg2(*a, **k):
+        for ins, eo, loss, st in fwd_pending:
+            fwd_rec.append(({k: v.cpu().float().numpy() for k, v in ins.items()}, eo.cpu().numpy(), float(loss),
+                            {k: float(v) for k, v in st.items()}))
+        fwd_pending.clear()
+        return real_cg(*a, **k)
+
+    opt.compute_grad_norm = cg2
     dopt = DistributedOption(distributed=True, dist_backend="gloo", dist_rank=rank, dist_world_size=world)
     glob = R._global_batches(6)
     shards = [R._shard(glob[0], 0, world)] * 6 if rank == 0 else [R._shard(glob[i % 2], 1, world) for i in range(6)]
@@ -175,7 +268,16 @@ def fresh_worker(rank, world, init, args, out):
     flat = {}
     for i, (w, lg, g) in enumerate(recs):
         flat[f"w{i}"], flat[f"l{i}"], flat[f"g{i}"] = w, lg, g
+    for i, (ins, eo, loss, st) in enumerate(fwd_rec):
+        for k, v in ins.items():
+            flat[f"in{i}_{k}"] = v
+        flat[f"eo{i}"] = eo
+        flat[f"loss{i}"] = np.array([loss] + [st[k] for k in sorted(st)])
     flat["w"] = m.arena.data.cpu().numpy()
+    for i, (st_, nm_, idx, a_, b_, ptr) in enumerate(dumps):
+        print(f"DUMP rank {rank} step {st_} pair #{nm_[0]}/#{nm_[1]} victim ptr {ptr:#x}: {idx.size} elements; "
+              f"flat idx {idx[:24].tolist()}; good {[f'{int(v) & 0xffff:04x}' for v in a_[:24]]}; "
+              f"bad {[f'{int(v) & 0xffff:04x}' for v in b_[:24]]}", flush=True)
     np.savez(f"{out}_r{rank}.npz", **flat)
     if rank == 0:
         import json
@@ -207,6 +309,13 @@ def fresh(args):
         mp.start_processes(fresh_worker, args=(2, tempfile.mktemp(prefix="ea_dpf_"), args, out), nprocs=2,
                            start_method="spawn")
         recs = {r: dict(np.load(f"{out}_r{r}.npz")) for r in (0, 1)}
+        for r in (0, 1):
+            for k in sorted(recs[r]):
+                if k.endswith("_ssub_dupdiff") and float(recs[r][k].max()) != 0.0:
+                    v = recs[r][k].tolist()
+                    print(f"run {run} rank {r} {k.split('_')[0]}: conv1 runs differ: |#0-#1| {v[0]:.3g} |#1-#2| {v[1]:.3g} "
+                          f"|#0-#2| {v[2]:.3g}; inputs pre vs post: x {v[3]:.3g} w {v[4]:.3g} b {v[5]:.3g}; "
+                          f"pre-x vs saved feats {v[6]:.3g}", flush=True)
         spans = json.load(open(f"{out}_spans.json"))
         if run == 0:
             refs = recs
@@ -224,6 +333,40 @@ def fresh(args):
             while f"g{s}" in a:
                 if not np.array_equal(a[f"w{s}"], b[f"w{s}"]):
                     msgs.append(f"rank {r} step {s}: weights at step start differ")
+                    break
+                bad_in = [k for k in a if k.startswith(f"in{s}_") and "blk" not in k and "_ssub_" not in k
+                          and not np.array_equal(a[k], b[k])]
+                bad_sub = [k.split("_ssub_")[1] for k in a if k.startswith(f"in{s}_ssub_") and "dupdiff" not in k
+                           and not np.array_equal(a[k], b[k])]
+                if bad_sub:
+                    msgs.append(f"rank {r} step {s}: subsampling tensors differ: {bad_sub}")
+                    for k in ("x1p", "x2"):
+                        kk = f"in{s}_ssub_{k}"
+                        if kk in a and not np.array_equal(a[kk], b[kk]):
+                            d = np.abs(a[kk] - b[kk])
+                            rows = sorted(set(np.nonzero(d)[0].tolist()))
+                            msgs.append(f"{k} {a[kk].shape}: {int((d > 0).sum())} el differ, rows {rows[:16]} "
+                                        f"cols [{np.nonzero(d)[1].min()},{np.nonzero(d)[1].max()}] max {d.max():.3g}")
+                if bad_in:
+                    msgs.append(f"rank {r} step {s}: forward INPUTS differ: {bad_in}")
+                    break
+                bad_blk = sorted((int(k.split("blk")[1]), k) for k in a if k.startswith(f"in{s}_blk")
+                                 and not np.array_equal(a[k], b[k]))
+                if bad_blk:
+                    k = bad_blk[0][1]
+                    d = np.abs(a[k] - b[k])
+                    nz = np.nonzero(d)
+                    msgs.append(f"rank {r} step {s}: first differing encoder block {k} ({int((d > 0).sum())}/{d.size}, "
+                                f"max {d.max():.3g}; index ranges " + ", ".join(f"[{v.min()},{v.max()}]" for v in nz) +
+                                f"; shape {a[k].shape}); differing blocks {[x[0] for x in bad_blk]}")
+                    break
+                if f"eo{s}" in a and not np.array_equal(a[f"eo{s}"], b[f"eo{s}"]):
+                    d = np.abs(a[f"eo{s}"] - b[f"eo{s}"])
+                    msgs.append(f"rank {r} step {s}: ENCODER OUTPUT differs ({int((d > 0).sum())}/{d.size}, max {d.max():.3g}"
+                                f", rows {sorted(set(np.nonzero(d)[0].tolist()))[:8]} frames {sorted(set(np.nonzero(d)[1].tolist()))[:8]})")
+                    break
+                if f"loss{s}" in a and not np.array_equal(a[f"loss{s}"], b[f"loss{s}"]):
+                    msgs.append(f"rank {r} step {s}: LOSS/stats differ {a[f'loss{s}'].tolist()} vs {b[f'loss{s}'].tolist()}")
                     break
                 if not np.array_equal(a[f"l{s}"], b[f"l{s}"], equal_nan=True):
                     msgs.append(f"rank {r} step {s}: LOCAL grads differ in " + "; ".join(_where(a[f"l{s}"], b[f"l{s}"], spans)[:12]))
@@ -245,7 +388,6 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--runs", type=int, default=24)
     ap.add_argument("--steps", type=int, default=6)
-    ap.add_argument("--side", action="store_true")
     ap.add_argument("--no-overlap", action="store_true")
     ap.add_argument("--snap", action="store_true")
     ap.add_argument("--fresh", action="store_true")

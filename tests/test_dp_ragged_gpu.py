@@ -18,7 +18,6 @@ tests/test_dp_capture_gpu.py (world-1 group).
 """
 import os
 import tempfile
-import warnings
 
 import pytest
 import torch
@@ -157,19 +156,10 @@ def _wdiff(a, b):
 
 
 def _matches_eager(a, e):
-    """Parameters equal to eager DP's.  Bit-equality is the expectation and holds in about 15
-    runs of 16; the rest drift (every parameter, both ranks alike; single elements up to ~5e-3
-    after Adam's per-element normalisation), with or without the weight-gradient side stream
-    (profiles/r5_ragged_repeat.txt).  Until that run-to-run drift is located the check is
-    bit-equal-or-close — relative L2 of the whole parameter arena under 5e-3 (8.5e-4 the largest
-    measured) — and a drifting
-    run is reported as a warning."""
-    if torch.equal(a["w"], e["w"]):
-        return
-    rel = float((a["w"] - e["w"]).norm()) / float(e["w"].norm())
-    msg = _wdiff(a, e)
-    warnings.warn(f"captured DP drifted from eager DP (relative L2 {rel:.3g}): {msg[:300]}")
-    assert rel <= 5e-3, f"relative L2 {rel:.3g}: {msg}"
+    """Parameters bit-equal to eager DP's.  (Round 5 accepted a relative-L2 drift here; its
+    cause was the conv1 forward kernel computing a few wrong outputs now and then under
+    packed-FP32 code, fixed in round 6: DESIGN.md §5, scripts/dp_drift_diag.py.)"""
+    assert torch.equal(a["w"], e["w"]), _wdiff(a, e)
 
 
 def _run(mode):

@@ -98,7 +98,6 @@ def _dp_worker(init, q):
     try:
         def mk(m):
             dp = ArenaDataParallel(m, bucket_mb=0.25, force_collectives=True, check_issue=True)
-            dp.ar_main = False  # the side-stream issue order RCCL runs in production
             assert dp.active and len(dp.buckets) > 2
             return dp
         res = {}
