@@ -1409,11 +1409,6 @@ extern "C" int ea_argmax_rows(long rows, int V, const float* x, long ld, long lo
   return 0;
 }
 
-static bool getenv_is(const char* name, const char* v) {
-  const char* e = std::getenv(name);
-  return e != nullptr && std::strcmp(e, v) == 0;
-}
-
 static PhaseGeo phase_geo(int B, int T1, int F1, int C) {
   PhaseGeo g;
   g.T1 = T1; g.F1 = F1;
@@ -1440,17 +1435,13 @@ extern "C" int ea_conv1_fwd2(int B, int T, int F, int C, const float* x, const f
       int per_cu = 0, dev = 0, ncu = 0;
       (void)hipGetDevice(&dev);
       (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
-      (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, conv1_fwd_rows_kernel<bf16, false>, 256, 0);
+      (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, conv1_fwd_rows_kernel<bf16, true>, 256, 0);
       resident = std::max(1, per_cu) * std::max(1, ncu);
     }
     dim3 grid((unsigned)std::min<long>((long)B * T1, resident));
     // streaming stores (the 0.6 GB output exceeds L2 + MALL): 210 -> 168 us at the C3 shape
-    static const bool nt = !getenv_is("EA_CONV1_FWD_NT", "0");
-    if (dtype == EA_BF16 && nt)
+    if (dtype == EA_BF16)
       hipLaunchKernelGGL((conv1_fwd_rows_kernel<bf16, true>), grid, dim3(256), 0, (hipStream_t)stream, B, T, F, g, C,
-                         x, w, bias, (bf16*)x1p, pos);
-    else if (dtype == EA_BF16)
-      hipLaunchKernelGGL((conv1_fwd_rows_kernel<bf16, false>), grid, dim3(256), 0, (hipStream_t)stream, B, T, F, g, C,
                          x, w, bias, (bf16*)x1p, pos);
     else
       hipLaunchKernelGGL((conv1_fwd_rows_kernel<float, false>), grid, dim3(256), 0, (hipStream_t)stream, B, T, F, g, C, x, w,

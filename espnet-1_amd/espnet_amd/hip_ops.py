@@ -133,7 +133,7 @@ class wgrad:
         if not OVERLAP_WGRAD or not torch.cuda.is_available():  # (CPU: the gloo DP tests)
             self.ctx = None
             return self
-        if LAZY_FORK and not self.launches and WGRAD_Q.active and REDUCE_Q.active:
+        if not self.launches and WGRAD_Q.active and REDUCE_Q.active:
             self.ctx = None  # only deferred work inside: no fork
             return self
         main = torch.cuda.current_stream()
@@ -162,20 +162,14 @@ class wgrad:
         return False
 
 
-# wgrad blocks that only queue deferred work do not fork (EA_LAZY_FORK=0: every block forks)
-LAZY_FORK = os.environ.get("EA_LAZY_FORK", "1") != "0"
-# a side-stream GEMM forked from an earlier point of the main stream, issued after the main
-# stream's next kernel (EA_FORK_AFTER=1, A/B): in the captured graph the main chain's kernel is
-# then the first successor of the fork point
-FORK_AFTER = os.environ.get("EA_FORK_AFTER", "1") != "0"
-
-
 def fork_event():
-    """An event at the main stream's current point for a later wgrad(after=...), or None.
-    Single process only: with the data-parallel hooks (GRAD_READY) the side stream also carries
-    the bucket all-reduces, and the late fork measured 4% slower there (1811 -> 1739 utt/s in
-    the DP rehearsal, profiles/r5_fork_after_dp_ab.txt)."""
-    if not (FORK_AFTER and OVERLAP_WGRAD) or GRAD_READY is not None or not torch.cuda.is_available():
+    """An event at the main stream's current point for a later wgrad(after=...), or None: a
+    side-stream GEMM forked from an earlier point of the main stream is issued after the main
+    stream's next kernel, so in the captured graph the main chain's kernel is the first successor
+    of the fork point.  Single process only: with the data-parallel hooks (GRAD_READY) the side
+    stream also carries the bucket all-reduces, and the late fork measured 4% slower there
+    (1811 -> 1739 utt/s in the DP rehearsal, profiles/r5_fork_after_dp_ab.txt)."""
+    if not OVERLAP_WGRAD or GRAD_READY is not None or not torch.cuda.is_available():
         return None
     ev = torch.cuda.Event()
     ev.record(torch.cuda.current_stream())
@@ -189,7 +183,7 @@ def join_wgrad(device=None):
         return
     main = torch.cuda.current_stream()
     side = _SIDE.get(main.device)
-    if side is not None and (_SIDE_DIRTY.get(main.device, True) or not LAZY_FORK):
+    if side is not None and _SIDE_DIRTY.get(main.device, True):
         main.wait_stream(side)
         _SIDE_DIRTY[main.device] = False
     WGRAD_Q.side_events = []  # whatever the side stream produced is ordered before main now
@@ -284,8 +278,6 @@ def join_aux():
 
 
 GRAD_READY = None  # callable(prefix): a block's parameter gradients are final (DP overlap)
-# the end-of-pass reduction flush on the side stream beside the grouped GEMM (EA_REDUCE_SIDE=0: serial)
-REDUCE_SIDE = os.environ.get("EA_REDUCE_SIDE", "1") != "0"
 
 
 def grad_ready(bound):
@@ -299,12 +291,6 @@ def grad_ready(bound):
         GRAD_READY(bound.prefix)
         return
     join_wgrad()
-
-
-# the attention decoder's weight-gradient GEMMs launched per decoder layer on the side stream,
-# beside the next layer's latency-bound backward, instead of in the end-of-pass grouped GEMM
-# with the fork-after order (EA_DEC_WGRAD_LAYER=0: all in the end-of-pass grouped GEMM)
-DEC_WGRAD_LAYER = os.environ.get("EA_DEC_WGRAD_LAYER", "1") != "0"
 
 
 def flush_wgrad_side(after=None):
@@ -780,7 +766,7 @@ class deferred_wgrad:
     def __exit__(self, *exc):
         WGRAD_Q.active, REDUCE_Q.active = self.prev
         if exc[0] is None:
-            if GRAD_READY is None and OVERLAP_WGRAD and REDUCE_SIDE and torch.cuda.is_available():
+            if GRAD_READY is None and OVERLAP_WGRAD and torch.cuda.is_available():
                 # the pass's reductions (bias column sums, LayerNorm parameter sums: bandwidth-
                 # bound) on the side stream beside the grouped weight-gradient GEMM (MFMA-bound)
                 # on this one; disjoint outputs (bias / norm vs weight gradients)

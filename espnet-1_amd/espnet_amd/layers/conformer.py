@@ -424,7 +424,7 @@ class ConformerBlockFn(torch.autograd.Function):
                                           shape=(3 * d, d)), accumulate=True)
         dxn2 = empty(N, d, dtype=cd, device=dev)
         ops.linear_dx(dqkv, qkv_w, dxn2)
-        if fork is not None:  # (EA_FORK_AFTER) the side GEMM issued after the main chain's next kernel
+        if fork is not None:  # the side GEMM issued after the main chain's next kernel (fork_event)
             dpp_wgrad(after=fork)
         del dbd
         dv_ff1 = dv_buf(N, d, cd, dev)

@@ -243,9 +243,10 @@ class DecoderFn(torch.autograd.Function):
             dv = site_dv(dx, dv_ff, b.g(ff + "w_2.bias"), 1.0, p, sd(l, 6), cd)
             with ops.wgrad(dv, a):
                 ops.linear_dw(dv, a, b.g(ff + "w_2.weight"), accumulate=True)
-            # (EA_DEC_WGRAD_LAYER) the layer above's weight gradients on the side stream, forked
-            # here and issued after this layer's first GEMM (which keeps the main chain's queue)
-            fork = ops.fork_event() if ops.DEC_WGRAD_LAYER and l < nb - 1 else None
+            # the layer above's weight gradients on the side stream (beside this layer's latency-
+            # bound backward instead of in the end-of-pass grouped GEMM), forked here and issued
+            # after this layer's first GEMM (which keeps the main chain's queue)
+            fork = ops.fork_event() if l < nb - 1 else None
             dh = empty(*h.shape, dtype=cd, device=dev)
             ops.linear_dx(dv, b.w(ff + "w_2.weight"), dh,
                           epi=ops.make_epi(EPI_DACT, act=ACT_RELU, aux=h, drop_p=p, seed=sd(l, 5)))

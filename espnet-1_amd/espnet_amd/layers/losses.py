@@ -5,7 +5,6 @@ grad_output), so nothing here synchronises with the host."""
 from __future__ import annotations
 
 import contextlib
-import os
 
 import torch
 
@@ -19,12 +18,11 @@ def _g(t):
     return t
 
 
-# EA_CTC_HEAD_AUX=0: only the lattice on the auxiliary stream (A/B switch)
-CTC_HEAD_AUX = os.environ.get("EA_CTC_HEAD_AUX", "1") != "0"
 # the CTC head's backward computed in the forward, unscaled, on the auxiliary stream beside the
 # latency-bound attention-decoder forward (most CUs idle there); the backward then only scales
-# it by the upstream gradient (EA_CTC_BWD_IN_FWD=0: the whole head backward after the decoder's)
-CTC_BWD_IN_FWD = os.environ.get("EA_CTC_BWD_IN_FWD", "1") != "0"
+# it by the upstream gradient (False: the whole head backward after the decoder's — the path of
+# a forward without input gradients; tests/test_trainer_gpu.py compares the two)
+CTC_BWD_IN_FWD = True
 _ONE = {}
 
 
@@ -60,13 +58,10 @@ class CTCFn(torch.autograd.Function):
             ops.scale_dropout(hs.reshape(N, d), h, p=ctc.dropout_rate, seed=ctc._seed)
             ops.linear(h, b.w("ctc_lo.weight"), logits, epi=ops.make_epi(bias=b.f("ctc_lo.bias")))
 
-        if not CTC_HEAD_AUX:
-            head()
         pre = CTC_BWD_IN_FWD and ctx.needs_input_grad[0]
         with (ops.aux(hs, h, logits, hlens, ys, ylens, lse, alpha, beta, nll, loss_utt, loss) if ctc._overlap
               else contextlib.nullcontext()):
-            if CTC_HEAD_AUX:
-                head()
+            head()
             lib.ea_ctc_loss_fwd(B, T, V, logits.data_ptr(), V, hlens.data_ptr(), ys.data_ptr(), ys.stride(0),
                                 ylens.data_ptr(), Lmax, lse.data_ptr(), alpha.data_ptr(), beta.data_ptr(),
                                 nll.data_ptr(), loss_utt.data_ptr(), loss.data_ptr(), ops.stream())

@@ -44,11 +44,11 @@ def phase_geo(B, T1, F1, T2, F2, C, mode, a=0, e=0, zero=0):
 FUSE_CONV1_WGRAD = os.environ.get("EA_FUSE_CONV1_WGRAD", "1") != "0"
 # ... with conv1's ReLU mask from support bits written by the forward (else the bf16 x1p rows)
 CONV1_POS_BITS = os.environ.get("EA_CONV1_POS_BITS", "1") != "0"
-# ... and the four parity classes in one launch (EA_MERGED_DGRAD=0: one launch per class)
-# (the merged launch is a gemm_pipe kernel: with EA_GEMM_PIPE=0 the per-class path runs)
-MERGED_DGRAD = os.environ.get("EA_MERGED_DGRAD", "1") != "0" and GEMM_PIPE != 0
-# ... reading conv2's weight K-major, W2k [ci][tap][co] (EA_DGRAD_KMAJOR=0: W2t [tap][co][ci])
-DGRAD_KMAJOR = os.environ.get("EA_DGRAD_KMAJOR", "1") != "0"
+# ... and the four parity classes in one launch (False: one launch per class, the path with
+# EA_GEMM_PIPE=0 since the merged launch is a gemm_pipe kernel; tests compare the two)
+MERGED_DGRAD = GEMM_PIPE != 0
+# ... reading conv2's weight K-major, W2k [ci][tap][co] (False: W2t [tap][co][ci], bit-identical)
+DGRAD_KMAJOR = True
 
 
 def _implicit_ok(cd, C):
