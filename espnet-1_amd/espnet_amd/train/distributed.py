@@ -25,8 +25,11 @@ import torch.distributed as dist
 from .. import hip_ops
 
 class ArenaDataParallel:
-    def __init__(self, model, bucket_mb: float = 64.0, group=None, overlap: bool = True,
+    def __init__(self, model, bucket_mb: float = None, group=None, overlap: bool = True,
                  force_collectives: bool = False, check_issue: bool = None):
+        # bucket size (DDP's bucket_cap_mb): EA_DP_BUCKET_MB, else 64 MiB
+        if bucket_mb is None:
+            bucket_mb = float(os.environ.get("EA_DP_BUCKET_MB", "64"))
         self.model = model
         self.group = group
         self.world_size = dist.get_world_size(group) if dist.is_initialized() else 1
